@@ -1,0 +1,59 @@
+// Python bindings of the accelerate_hpc_test_amd native extension (`accelerate_hpc_test_amd._C`).
+// Kernels live in csrc/kernels/*.hip (gfx950), the host runtime pieces in csrc/runtime/*.cpp.
+#include <torch/extension.h>
+
+// norm_act.hip
+std::vector<torch::Tensor> rmsnorm_fwd(torch::Tensor x, c10::optional<torch::Tensor> residual, torch::Tensor w, double eps);
+std::vector<torch::Tensor> rmsnorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor w, torch::Tensor rstd,
+                                       c10::optional<torch::Tensor> dres);
+torch::Tensor swiglu_fwd(torch::Tensor gu);
+torch::Tensor swiglu_bwd(torch::Tensor gu, torch::Tensor dh);
+void rope_inplace(torch::Tensor qkv, torch::Tensor cos, torch::Tensor sin, c10::optional<torch::Tensor> pos,
+                  int64_t n_rot_heads, int64_t n_heads_total, int64_t head_dim, double sign);
+// xent_optim.hip
+std::vector<torch::Tensor> xent_fwd(torch::Tensor logits, torch::Tensor labels, int64_t ignore_index);
+void xent_bwd(torch::Tensor logits, torch::Tensor labels, torch::Tensor lse, torch::Tensor scale, torch::Tensor out,
+              int64_t ignore_index);
+void adam_multi_tensor(torch::Tensor meta, torch::Tensor block_prefix, int64_t nblocks, int64_t pdtype, int64_t gdtype,
+                       int64_t sdtype, double lr, double beta1, double beta2, double eps, double wd, double bc1,
+                       double bc2_sqrt, bool adamw, c10::optional<torch::Tensor> grad_scale);
+int64_t multi_tensor_chunk();
+void sqnorm_multi_tensor(torch::Tensor meta, torch::Tensor block_prefix, int64_t nblocks, int64_t gdtype, torch::Tensor out,
+                         bool accumulate);
+void clip_multi_tensor(torch::Tensor meta, torch::Tensor block_prefix, int64_t nblocks, int64_t gdtype, torch::Tensor total_sq,
+                       double max_norm);
+// flash_attn.hip
+std::vector<torch::Tensor> flash_attn_fwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, double softmax_scale, bool causal);
+void flash_attn_bwd(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch::Tensor v, torch::Tensor o,
+                    torch::Tensor lse, torch::Tensor dq, torch::Tensor dk, torch::Tensor dv, double softmax_scale,
+                    bool causal);
+// fp8.hip
+torch::Tensor fp8_amax(torch::Tensor x, c10::optional<torch::Tensor> out);
+torch::Tensor fp8_scale_from_amax(torch::Tensor amax, double fp8_max, double margin);
+std::vector<torch::Tensor> fp8_cast(torch::Tensor x, torch::Tensor scale, bool e5m2, bool transpose);
+torch::Tensor fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor a_scale_inv, torch::Tensor b_scale_inv,
+                       bool a_e5m2, bool b_e5m2, c10::optional<torch::Tensor> bias, bool out_fp32);
+// runtime/*.cpp
+void register_runtime(pybind11::module& m);
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "MI355X (gfx950) native kernels and runtime for accelerate_hpc_test_amd";
+  m.def("rmsnorm_fwd", &rmsnorm_fwd);
+  m.def("rmsnorm_bwd", &rmsnorm_bwd);
+  m.def("swiglu_fwd", &swiglu_fwd);
+  m.def("swiglu_bwd", &swiglu_bwd);
+  m.def("rope_inplace", &rope_inplace);
+  m.def("xent_fwd", &xent_fwd);
+  m.def("xent_bwd", &xent_bwd);
+  m.def("adam_multi_tensor", &adam_multi_tensor);
+  m.def("multi_tensor_chunk", &multi_tensor_chunk);
+  m.def("sqnorm_multi_tensor", &sqnorm_multi_tensor);
+  m.def("clip_multi_tensor", &clip_multi_tensor);
+  m.def("flash_attn_fwd", &flash_attn_fwd);
+  m.def("flash_attn_bwd", &flash_attn_bwd);
+  m.def("fp8_amax", &fp8_amax);
+  m.def("fp8_scale_from_amax", &fp8_scale_from_amax);
+  m.def("fp8_cast", &fp8_cast);
+  m.def("fp8_gemm", &fp8_gemm);
+  register_runtime(m);
+}

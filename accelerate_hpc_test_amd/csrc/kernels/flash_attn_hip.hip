@@ -1,0 +1,518 @@
+#include "hip/hip_runtime.h"
+// Flash attention (forward + backward) for CDNA4 / gfx950 on v_mfma_f32_32x32x16_bf16.
+//
+// Layout: Q, K, V are read in place from a fused QKV activation [B, S, Hq + 2*Hkv, D] (any token stride), so
+// no transpose/copy precedes attention. O is [B, S, Hq, D]; LSE is fp32 [B, Hq, S] (natural log of the softmax
+// normaliser of the scaled scores, used by the backward pass and by ring-attention merges). GQA: q head h
+// reads kv head h / (Hq / Hkv). head_dim D = 128.
+//
+// Forward (query-stationary, 4 waves x 32 queries per workgroup, 64-key tiles):
+//   * "swapped" S^T = K Q^T so each lane owns ONE query column: the online-softmax max / sum and the O rescale
+//     are lane-local (one cross-half exchange per tile), no LDS round trip for P;
+//   * P^T stays in the accumulator registers and is used directly as the B operand of O^T += V^T P^T
+//     (accumulator-as-operand with the permuted k order), V^T fragments come from a padded LDS image through
+//     ds_read_b64_tr_b16 (hardware transpose); K row fragments come from an XOR-swizzled LDS image
+//     (conflict-free ds_read_b128).
+// Backward (no atomics, deterministic):
+//   * dQ kernel: query-stationary like the forward, recomputes P^T and dP^T = V dO^T, dQ^T += K^T dS^T;
+//   * dK/dV kernel: key-stationary (4 waves x 32 keys), sweeps 32-query slices: S = Q K^T and dP = dO V^T with
+//     the key on the lane, then dV^T += dO^T P and dK^T += Q^T dS with P / dS used in place as B operands;
+//     per-q-head partials are summed over the GQA group by a small reduction kernel.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include "common.h"
+
+using namespace acc;
+
+namespace {
+
+typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
+typedef __bf16 v4bf __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kD = 128;
+constexpr int kRowBytes = 256;  // row image: 128 bf16, 16-B chunk c stored at chunk c ^ (row & 15)
+constexpr int kTrBytes = 320;   // transpose image: 128 bf16 + 64 B pad (4 rows land on disjoint banks)
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }  // v_exp_f32: exp2(-inf) = 0
+
+__device__ __forceinline__ f32x16 mfma(v8bf a, v8bf b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ v8bf row_frag(const char* img, int row, int chunk) {
+  return *reinterpret_cast<const v8bf*>(img + row * kRowBytes + ((chunk ^ (row & 15)) << 4));
+}
+
+__device__ __forceinline__ void row_store(char* img, int row, int chunk, v8bf v) {
+  *reinterpret_cast<v8bf*>(img + row * kRowBytes + ((chunk ^ (row & 15)) << 4)) = v;
+}
+
+__device__ __forceinline__ void tr_store(char* img, int row, int chunk, v8bf v) {
+  *reinterpret_cast<v8bf*>(img + row * kTrBytes + (chunk << 4)) = v;
+}
+
+__device__ __forceinline__ v4bf tr_read(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+      (__attribute__((address_space(3))) v4bf*)(reinterpret_cast<uintptr_t>(p)));
+}
+
+// A-operand fragment of X^T where X is a [rows][128] tile in the transpose image: rows rb..rb+15 form the
+// MFMA k dimension in the permuted order (element j of half h <-> row rb + 8(j>>2) + 4h + (j&3)),
+// columns db*32 .. db*32+31 form the MFMA rows.
+__device__ __forceinline__ v8bf tr_frag(const char* img, int rb, int db, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const int row = rb + 4 * (g >> 1) + (i >> 2);
+  const int col = db * 32 + 16 * (g & 1) + 4 * (i & 3);
+  const char* p = img + row * kTrBytes + col * 2;
+  const v4bf lo = tr_read(p);
+  const v4bf hi = tr_read(p + 8 * kTrBytes);
+  v8bf r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+// Accumulator row index held by register i of a 32x32 C tile in lane half hf.
+__device__ __forceinline__ int acc_row(int i, int hf) { return (i & 3) + 8 * (i >> 2) + 4 * hf; }
+
+__device__ __forceinline__ v8bf pack8(const f32x16& x, int s) {
+  v8bf r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = static_cast<__bf16>(x[8 * s + j]);
+  return r;
+}
+
+struct FwdParams {
+  const bf16_t *q, *k, *v;
+  long q_ts, k_ts, v_ts, q_bs, k_bs, v_bs;
+  bf16_t* o;
+  long o_ts, o_bs;
+  float* lse;
+  int S, Hq, Hkv;
+  float scale_log2;
+};
+
+template <bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(FwdParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* k_img = smem;                      // 64 x 256 B
+  char* v_img = smem + 64 * kRowBytes;     // 64 x 320 B
+  const int nqt = p.S / 128;
+  const int qt = CAUSAL ? (nqt - 1 - (int)blockIdx.x) : (int)blockIdx.x;  // heaviest causal tiles first
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int kh = h / (p.Hq / p.Hkv);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hf = lane >> 5;
+  const int qw0 = qt * 128 + wave * 32;
+  const bf16_t* qb = p.q + b * p.q_bs + (long)h * kD;
+  const bf16_t* kb_ = p.k + b * p.k_bs + (long)kh * kD;
+  const bf16_t* vb_ = p.v + b * p.v_bs + (long)kh * kD;
+
+  v8bf qf[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) qf[s] = *reinterpret_cast<const v8bf*>(qb + (long)(qw0 + r) * p.q_ts + 16 * s + 8 * hf);
+
+  f32x16 o[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[d][i] = 0.f;
+  float m = -INFINITY, l = 0.f;
+  const int n_kt = CAUSAL ? (qt + 1) * 2 : p.S / 64;
+
+  for (int kt = 0; kt < n_kt; ++kt) {
+    const int k0 = kt * 64;
+#pragma unroll
+    for (int c = tid; c < 64 * 16; c += 256) {
+      const int row = c >> 4, ch = c & 15;
+      const v8bf kv = *reinterpret_cast<const v8bf*>(kb_ + (long)(k0 + row) * p.k_ts + ch * 8);
+      const v8bf vv = *reinterpret_cast<const v8bf*>(vb_ + (long)(k0 + row) * p.v_ts + ch * 8);
+      row_store(k_img, row, ch, kv);
+      tr_store(v_img, row, ch, vv);
+    }
+    __syncthreads();
+    if (!CAUSAL || k0 <= qw0 + 31) {
+      f32x16 sc[2];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sc[kb][i] = 0.f;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) sc[kb] = mfma(row_frag(k_img, kb * 32 + r, 2 * s + hf), qf[s], sc[kb]);
+      }
+      float mx = m;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float x = sc[kb][i] * p.scale_log2;
+          if (CAUSAL) {
+            const int key = k0 + kb * 32 + acc_row(i, hf);
+            if (key > qw0 + r) x = -INFINITY;
+          }
+          sc[kb][i] = x;
+          mx = fmaxf(mx, x);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float alpha = fast_exp2(m - mx);
+      m = mx;
+      l *= alpha;
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[d][i] *= alpha;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float pv = fast_exp2(sc[kb][i] - m);
+          sc[kb][i] = pv;
+          l += pv;
+        }
+      v8bf pb[2][2];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        pb[kb][0] = pack8(sc[kb], 0);
+        pb[kb][1] = pack8(sc[kb], 1);
+      }
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) o[d] = mfma(tr_frag(v_img, kb * 32 + 16 * s2, d, lane), pb[kb][s2], o[d]);
+    }
+    __syncthreads();
+  }
+  l += __shfl_xor(l, 32, 64);
+  const float inv = 1.f / l;
+  bf16_t* ob = p.o + b * p.o_bs + (long)h * kD + (long)(qw0 + r) * p.o_ts;
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      bf16x4 w;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) w.v[t] = f2bf(o[d][4 * g + t] * inv);
+      *reinterpret_cast<bf16x4*>(ob + d * 32 + 8 * g + 4 * hf) = w;
+    }
+  if (hf == 0) p.lse[((long)b * p.Hq + h) * p.S + qw0 + r] = (m + __builtin_amdgcn_logf(l)) * kLn2;
+}
+
+// delta[b, h, s] = sum_d dO * O (fp32).
+__global__ void attn_delta_kernel(const bf16_t* __restrict__ o, long o_ts, long o_bs, const bf16_t* __restrict__ dout,
+                                  long do_ts, long do_bs, float* __restrict__ delta, int S, int Hq, int B) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);  // one wave per (b, s, h)
+  const int lane = threadIdx.x & 63;
+  if (row >= (long)B * S * Hq) return;
+  const int h = row % Hq;
+  const long bs = row / Hq;
+  const int s = bs % S, b = bs / S;
+  const bf16_t* op = o + b * o_bs + (long)s * o_ts + (long)h * kD + lane * 2;
+  const bf16_t* dp = dout + b * do_bs + (long)s * do_ts + (long)h * kD + lane * 2;
+  float acc = bf2f(op[0]) * bf2f(dp[0]) + bf2f(op[1]) * bf2f(dp[1]);
+  acc = wave_sum(acc);
+  if (lane == 0) delta[((long)b * Hq + h) * S + s] = acc;
+}
+
+struct BwdParams {
+  const bf16_t *q, *k, *v, *dout;
+  long q_ts, k_ts, v_ts, do_ts, q_bs, k_bs, v_bs, do_bs;
+  const float *lse, *delta;
+  bf16_t* dq;
+  long dq_ts, dq_bs;
+  float *dk_part, *dv_part;  // [B, S, Hq, D] fp32
+  int S, Hq, Hkv;
+  float scale_log2, scale;
+};
+
+template <bool CAUSAL>
+__global__ __launch_bounds__(256, 1) void attn_bwd_dq_kernel(BwdParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* k_row = smem;                              // 64 x 256
+  char* k_tr = smem + 64 * kRowBytes;              // 64 x 320
+  char* v_row = k_tr + 64 * kTrBytes;              // 64 x 256
+  const int nqt = p.S / 128;
+  const int qt = CAUSAL ? (nqt - 1 - (int)blockIdx.x) : (int)blockIdx.x;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int kh = h / (p.Hq / p.Hkv);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hf = lane >> 5;
+  const int qw0 = qt * 128 + wave * 32;
+  const bf16_t* qb = p.q + b * p.q_bs + (long)h * kD;
+  const bf16_t* dob = p.dout + b * p.do_bs + (long)h * kD;
+  const bf16_t* kb_ = p.k + b * p.k_bs + (long)kh * kD;
+  const bf16_t* vb_ = p.v + b * p.v_bs + (long)kh * kD;
+
+  v8bf qf[8], df[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    qf[s] = *reinterpret_cast<const v8bf*>(qb + (long)(qw0 + r) * p.q_ts + 16 * s + 8 * hf);
+    df[s] = *reinterpret_cast<const v8bf*>(dob + (long)(qw0 + r) * p.do_ts + 16 * s + 8 * hf);
+  }
+  const long st = ((long)b * p.Hq + h) * p.S + qw0 + r;
+  const float lse2 = p.lse[st] * kLog2e;
+  const float dlt = p.delta[st];
+  f32x16 dq[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dq[d][i] = 0.f;
+  const int n_kt = CAUSAL ? (qt + 1) * 2 : p.S / 64;
+  for (int kt = 0; kt < n_kt; ++kt) {
+    const int k0 = kt * 64;
+#pragma unroll
+    for (int c = tid; c < 64 * 16; c += 256) {
+      const int row = c >> 4, ch = c & 15;
+      const v8bf kv = *reinterpret_cast<const v8bf*>(kb_ + (long)(k0 + row) * p.k_ts + ch * 8);
+      const v8bf vv = *reinterpret_cast<const v8bf*>(vb_ + (long)(k0 + row) * p.v_ts + ch * 8);
+      row_store(k_row, row, ch, kv);
+      tr_store(k_tr, row, ch, kv);
+      row_store(v_row, row, ch, vv);
+    }
+    __syncthreads();
+    if (!CAUSAL || k0 <= qw0 + 31) {
+      v8bf dsb[2][2];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        f32x16 sc, dp;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { sc[i] = 0.f; dp[i] = 0.f; }
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          sc = mfma(row_frag(k_row, kb * 32 + r, 2 * s + hf), qf[s], sc);
+          dp = mfma(row_frag(v_row, kb * 32 + r, 2 * s + hf), df[s], dp);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float pv = fast_exp2(sc[i] * p.scale_log2 - lse2);
+          if (CAUSAL && (k0 + kb * 32 + acc_row(i, hf) > qw0 + r)) pv = 0.f;
+          sc[i] = pv * (dp[i] - dlt);
+        }
+        dsb[kb][0] = pack8(sc, 0);
+        dsb[kb][1] = pack8(sc, 1);
+      }
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) dq[d] = mfma(tr_frag(k_tr, kb * 32 + 16 * s2, d, lane), dsb[kb][s2], dq[d]);
+    }
+    __syncthreads();
+  }
+  bf16_t* out = p.dq + b * p.dq_bs + (long)h * kD + (long)(qw0 + r) * p.dq_ts;
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      bf16x4 w;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) w.v[t] = f2bf(dq[d][4 * g + t] * p.scale);
+      *reinterpret_cast<bf16x4*>(out + d * 32 + 8 * g + 4 * hf) = w;
+    }
+}
+
+template <bool CAUSAL>
+__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(BwdParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* q_row = smem;                        // 32 x 256
+  char* q_tr = q_row + 32 * kRowBytes;       // 32 x 320
+  char* d_row = q_tr + 32 * kTrBytes;        // 32 x 256
+  char* d_tr = d_row + 32 * kRowBytes;       // 32 x 320
+  float* lse_s = reinterpret_cast<float*>(d_tr + 32 * kTrBytes);  // 32
+  float* dlt_s = lse_s + 32;                                       // 32
+  const int kt = blockIdx.x;  // key tile of 128 keys; tile 0 has the most work under the causal mask
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int kh = h / (p.Hq / p.Hkv);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hf = lane >> 5;
+  const int kw0 = kt * 128 + wave * 32;
+  const bf16_t* qb = p.q + b * p.q_bs + (long)h * kD;
+  const bf16_t* dob = p.dout + b * p.do_bs + (long)h * kD;
+  const bf16_t* kb_ = p.k + b * p.k_bs + (long)kh * kD;
+  const bf16_t* vb_ = p.v + b * p.v_bs + (long)kh * kD;
+  const float* lse_g = p.lse + ((long)b * p.Hq + h) * p.S;
+  const float* dlt_g = p.delta + ((long)b * p.Hq + h) * p.S;
+
+  v8bf kf[8], vf[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    kf[s] = *reinterpret_cast<const v8bf*>(kb_ + (long)(kw0 + r) * p.k_ts + 16 * s + 8 * hf);
+    vf[s] = *reinterpret_cast<const v8bf*>(vb_ + (long)(kw0 + r) * p.v_ts + 16 * s + 8 * hf);
+  }
+  f32x16 dk[4], dv[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { dk[d][i] = 0.f; dv[d][i] = 0.f; }
+
+  const int qs0 = CAUSAL ? kt * 4 : 0;
+  const int nqs = p.S / 32;
+  for (int qs = qs0; qs < nqs; ++qs) {
+    const int q0 = qs * 32;
+#pragma unroll
+    for (int c = tid; c < 32 * 16; c += 256) {
+      const int row = c >> 4, ch = c & 15;
+      const v8bf qv = *reinterpret_cast<const v8bf*>(qb + (long)(q0 + row) * p.q_ts + ch * 8);
+      const v8bf dv8 = *reinterpret_cast<const v8bf*>(dob + (long)(q0 + row) * p.do_ts + ch * 8);
+      row_store(q_row, row, ch, qv);
+      tr_store(q_tr, row, ch, qv);
+      row_store(d_row, row, ch, dv8);
+      tr_store(d_tr, row, ch, dv8);
+    }
+    if (tid < 32) lse_s[tid] = lse_g[q0 + tid] * kLog2e;
+    else if (tid < 64) dlt_s[tid - 32] = dlt_g[q0 + tid - 32];
+    __syncthreads();
+    if (!CAUSAL || q0 + 31 >= kw0) {
+      f32x16 sc, dp;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { sc[i] = 0.f; dp[i] = 0.f; }
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        sc = mfma(row_frag(q_row, r, 2 * s + hf), kf[s], sc);
+        dp = mfma(row_frag(d_row, r, 2 * s + hf), vf[s], dp);
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int qi = acc_row(i, hf);
+        float pv = fast_exp2(sc[i] * p.scale_log2 - lse_s[qi]);
+        if (CAUSAL && (kw0 + r > q0 + qi)) pv = 0.f;
+        sc[i] = pv;
+        dp[i] = pv * (dp[i] - dlt_s[qi]);
+      }
+      const v8bf pb0 = pack8(sc, 0), pb1 = pack8(sc, 1);
+      const v8bf ds0 = pack8(dp, 0), ds1 = pack8(dp, 1);
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        dv[d] = mfma(tr_frag(d_tr, 0, d, lane), pb0, dv[d]);
+        dv[d] = mfma(tr_frag(d_tr, 16, d, lane), pb1, dv[d]);
+        dk[d] = mfma(tr_frag(q_tr, 0, d, lane), ds0, dk[d]);
+        dk[d] = mfma(tr_frag(q_tr, 16, d, lane), ds1, dk[d]);
+      }
+    }
+    __syncthreads();
+  }
+  const long orow = (((long)b * p.S + kw0 + r) * p.Hq + h) * kD;
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int dd = d * 32 + 8 * g + 4 * hf;
+      *reinterpret_cast<float4*>(p.dk_part + orow + dd) =
+          make_float4(dk[d][4 * g] * p.scale, dk[d][4 * g + 1] * p.scale, dk[d][4 * g + 2] * p.scale, dk[d][4 * g + 3] * p.scale);
+      *reinterpret_cast<float4*>(p.dv_part + orow + dd) = make_float4(dv[d][4 * g], dv[d][4 * g + 1], dv[d][4 * g + 2], dv[d][4 * g + 3]);
+    }
+}
+
+// dk[b, s, kh, :] = sum over the GQA group of dk_part[b, s, h, :] (same for dv), written as bf16 (strided).
+__global__ void gqa_reduce_kernel(const float* __restrict__ dk_part, const float* __restrict__ dv_part, bf16_t* dk,
+                                  long dk_ts, long dk_bs, bf16_t* dv, long dv_ts, long dv_bs, int B, int S, int Hq,
+                                  int Hkv) {
+  const long total = (long)B * S * Hkv * (kD / 4);
+  const int grp = Hq / Hkv;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    const int c = idx % (kD / 4);
+    long rest = idx / (kD / 4);
+    const int kh = rest % Hkv;
+    rest /= Hkv;
+    const int s = rest % S;
+    const int b = rest / S;
+    float4 ak = make_float4(0.f, 0.f, 0.f, 0.f), av = ak;
+    for (int g = 0; g < grp; ++g) {
+      const long off = (((long)b * S + s) * Hq + kh * grp + g) * kD + c * 4;
+      const float4 x = *reinterpret_cast<const float4*>(dk_part + off);
+      const float4 y = *reinterpret_cast<const float4*>(dv_part + off);
+      ak.x += x.x; ak.y += x.y; ak.z += x.z; ak.w += x.w;
+      av.x += y.x; av.y += y.y; av.z += y.z; av.w += y.w;
+    }
+    bf16x4 wk, wv;
+    wk.v[0] = f2bf(ak.x); wk.v[1] = f2bf(ak.y); wk.v[2] = f2bf(ak.z); wk.v[3] = f2bf(ak.w);
+    wv.v[0] = f2bf(av.x); wv.v[1] = f2bf(av.y); wv.v[2] = f2bf(av.z); wv.v[3] = f2bf(av.w);
+    *reinterpret_cast<bf16x4*>(dk + b * dk_bs + (long)s * dk_ts + (long)kh * kD + c * 4) = wk;
+    *reinterpret_cast<bf16x4*>(dv + b * dv_bs + (long)s * dv_ts + (long)kh * kD + c * 4) = wv;
+  }
+}
+
+void check_qkv(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16, name, " must be a bf16 HIP tensor");
+  TORCH_CHECK(t.dim() == 4 && t.size(3) == kD && t.stride(3) == 1 && t.stride(2) == kD,
+              name, " must be [B, S, H, 128] with contiguous heads");
+  TORCH_CHECK((t.stride(1) % 8) == 0 && (t.stride(0) % 8) == 0, name, " strides must be multiples of 8 elements");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0, name, " must be 16-byte aligned");
+}
+
+}  // namespace
+
+// q: [B, S, Hq, D], k/v: [B, S, Hkv, D] (views into a fused QKV buffer are fine). Returns (O [B,S,Hq,D], LSE [B,Hq,S]).
+std::vector<torch::Tensor> flash_attn_fwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, double softmax_scale,
+                                          bool causal) {
+  check_qkv(q, "q");
+  check_qkv(k, "k");
+  check_qkv(v, "v");
+  const int B = q.size(0), S = q.size(1), Hq = q.size(2), Hkv = k.size(2);
+  TORCH_CHECK(k.size(1) == S && v.size(1) == S, "flash_attn: q/k/v sequence lengths must match");
+  TORCH_CHECK(S % 128 == 0, "flash_attn: sequence length must be a multiple of 128");
+  TORCH_CHECK(Hq % Hkv == 0, "flash_attn: Hq must be a multiple of Hkv");
+  auto o = torch::empty({B, S, Hq, kD}, q.options());
+  auto lse = torch::empty({B, Hq, S}, q.options().dtype(torch::kFloat32));
+  FwdParams p{reinterpret_cast<const bf16_t*>(q.data_ptr()), reinterpret_cast<const bf16_t*>(k.data_ptr()),
+              reinterpret_cast<const bf16_t*>(v.data_ptr()), q.stride(1), k.stride(1), v.stride(1), q.stride(0),
+              k.stride(0), v.stride(0), reinterpret_cast<bf16_t*>(o.data_ptr()), o.stride(1), o.stride(0),
+              lse.data_ptr<float>(), S, Hq, Hkv, (float)(softmax_scale * kLog2e)};
+  dim3 grid(S / 128, Hq, B);
+  const size_t smem = 64 * kRowBytes + 64 * kTrBytes;
+  auto stream = at::hip::getCurrentHIPStream();
+  if (causal) hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(256), smem, stream, p);
+  else hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(256), smem, stream, p);
+  return {o, lse};
+}
+
+// Writes dq / dk / dv into the given output views (e.g. slices of a fused dQKV buffer).
+void flash_attn_bwd(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch::Tensor v, torch::Tensor o,
+                    torch::Tensor lse, torch::Tensor dq, torch::Tensor dk, torch::Tensor dv, double softmax_scale,
+                    bool causal) {
+  check_qkv(q, "q");
+  check_qkv(k, "k");
+  check_qkv(v, "v");
+  check_qkv(o, "o");
+  check_qkv(dout, "dout");
+  check_qkv(dq, "dq");
+  check_qkv(dk, "dk");
+  check_qkv(dv, "dv");
+  const int B = q.size(0), S = q.size(1), Hq = q.size(2), Hkv = k.size(2);
+  TORCH_CHECK(S % 128 == 0, "flash_attn: sequence length must be a multiple of 128");
+  auto stream = at::hip::getCurrentHIPStream();
+  auto delta = torch::empty({B, Hq, S}, q.options().dtype(torch::kFloat32));
+  {
+    const long rows = (long)B * S * Hq;
+    hipLaunchKernelGGL(attn_delta_kernel, dim3((rows + 3) / 4), dim3(256), 0, stream,
+                       reinterpret_cast<const bf16_t*>(o.data_ptr()), o.stride(1), o.stride(0),
+                       reinterpret_cast<const bf16_t*>(dout.data_ptr()), dout.stride(1), dout.stride(0),
+                       delta.data_ptr<float>(), S, Hq, B);
+  }
+  auto dk_part = torch::empty({B, S, Hq, kD}, q.options().dtype(torch::kFloat32));
+  auto dv_part = torch::empty({B, S, Hq, kD}, q.options().dtype(torch::kFloat32));
+  BwdParams p{reinterpret_cast<const bf16_t*>(q.data_ptr()), reinterpret_cast<const bf16_t*>(k.data_ptr()),
+              reinterpret_cast<const bf16_t*>(v.data_ptr()), reinterpret_cast<const bf16_t*>(dout.data_ptr()),
+              q.stride(1), k.stride(1), v.stride(1), dout.stride(1), q.stride(0), k.stride(0), v.stride(0),
+              dout.stride(0), lse.data_ptr<float>(), delta.data_ptr<float>(), reinterpret_cast<bf16_t*>(dq.data_ptr()),
+              dq.stride(1), dq.stride(0), dk_part.data_ptr<float>(), dv_part.data_ptr<float>(), S, Hq, Hkv,
+              (float)(softmax_scale * kLog2e), (float)softmax_scale};
+  dim3 grid(S / 128, Hq, B);
+  const size_t smem_dq = 64 * kRowBytes * 2 + 64 * kTrBytes;
+  const size_t smem_kv = 32 * kRowBytes * 2 + 32 * kTrBytes * 2 + 64 * sizeof(float);
+  if (causal) {
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, grid, dim3(256), smem_dq, stream, p);
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<true>, grid, dim3(256), smem_kv, stream, p);
+  } else {
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<false>, grid, dim3(256), smem_dq, stream, p);
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<false>, grid, dim3(256), smem_kv, stream, p);
+  }
+  const long work = (long)B * S * Hkv * (kD / 4);
+  long g = (work + 255) / 256;
+  if (g > 2048) g = 2048;
+  hipLaunchKernelGGL(gqa_reduce_kernel, dim3(g), dim3(256), 0, stream, dk_part.data_ptr<float>(),
+                     dv_part.data_ptr<float>(), reinterpret_cast<bf16_t*>(dk.data_ptr()), dk.stride(1), dk.stride(0),
+                     reinterpret_cast<bf16_t*>(dv.data_ptr()), dv.stride(1), dv.stride(0), B, S, Hq, Hkv);
+}

@@ -1,0 +1,275 @@
+// fp8 (OCP e4m3fn / e5m2, native on gfx950) training kernels:
+//   * per-tensor amax (block max + one device-scope atomic max per workgroup),
+//   * scale-and-cast to fp8 with saturation, optionally also writing the transposed copy needed by the
+//     dgrad / wgrad GEMMs (transpose staged through LDS),
+//   * fp8 GEMM  C[M,N] = (A[M,K] . B[N,K]^T) * sa * sb (+ bias)  on v_mfma_scale_f32_32x32x64_f8f6f4 with unit
+//     block scales (the MX-scaled MFMA runs at 2x the bf16 MFMA rate; the per-tensor scales are applied in the
+//     epilogue). 128x128 tile, BK = 64, 4 waves (2x2) of 64x64, LDS double buffer with XOR-swizzled 16-B chunks,
+//     XCD-aware tile order.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include "common.h"
+
+using namespace acc;
+
+namespace {
+
+typedef int v8i __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr float kE4M3Max = 448.f;
+constexpr float kE5M2Max = 57344.f;
+
+__global__ void amax_kernel(const bf16_t* __restrict__ x, long n, unsigned int* __restrict__ out) {
+  __shared__ float scratch[16];
+  float m = 0.f;
+  const long nvec = n >> 3;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
+    const bf16x8 a = reinterpret_cast<const bf16x8*>(x)[i];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(bf2f(a.v[j])));
+  }
+  for (long i = nvec * 8 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    m = fmaxf(m, fabsf(bf2f(x[i])));
+  m = block_max(m, scratch);
+  if (threadIdx.x == 0) atomicMax(out, __float_as_uint(m));  // non-negative floats order like their bits
+}
+
+template <bool E5M2>
+__device__ __forceinline__ uint32_t cvt_pair(float a, float b) {
+  const float mx = E5M2 ? kE5M2Max : kE4M3Max;
+  a = fminf(fmaxf(a, -mx), mx);
+  b = fminf(fmaxf(b, -mx), mx);
+  if (E5M2) return (uint32_t)__builtin_amdgcn_cvt_pk_bf8_f32(a, b, 0, false) & 0xffffu;
+  return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false) & 0xffffu;
+}
+
+// y = sat(x * scale) as fp8 [M, N]; optionally yt = y^T [N, M]. 64x64 tiles, 256 threads.
+template <bool E5M2, bool TRANS>
+__global__ __launch_bounds__(256) void cast_kernel(const bf16_t* __restrict__ x, const float* __restrict__ scale,
+                                                   uint8_t* __restrict__ y, uint8_t* __restrict__ yt, int M, int N) {
+  __shared__ uint8_t tile[64][64 + 4];
+  const int tm = blockIdx.y * 64, tn = blockIdx.x * 64;
+  const float s = scale[0];
+  const int tid = threadIdx.x;
+  // each thread: 2 rows x 8 columns
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    const int rr = (tid >> 3) + pass * 32, cc = (tid & 7) * 8;
+    const int gm = tm + rr, gn = tn + cc;
+    uint8_t vals[8];
+    if (gm < M && gn + 7 < N && (N & 7) == 0) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(x + (long)gm * N + gn);
+      uint32_t w0 = cvt_pair<E5M2>(bf2f(a.v[0]) * s, bf2f(a.v[1]) * s) | (cvt_pair<E5M2>(bf2f(a.v[2]) * s, bf2f(a.v[3]) * s) << 16);
+      uint32_t w1 = cvt_pair<E5M2>(bf2f(a.v[4]) * s, bf2f(a.v[5]) * s) | (cvt_pair<E5M2>(bf2f(a.v[6]) * s, bf2f(a.v[7]) * s) << 16);
+      *reinterpret_cast<uint2*>(y + (long)gm * N + gn) = make_uint2(w0, w1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { vals[j] = (w0 >> (8 * j)) & 0xff; vals[4 + j] = (w1 >> (8 * j)) & 0xff; }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        vals[j] = 0;
+        if (gm < M && gn + j < N) {
+          const float f = bf2f(x[(long)gm * N + gn + j]) * s;
+          vals[j] = cvt_pair<E5M2>(f, 0.f) & 0xff;
+          y[(long)gm * N + gn + j] = vals[j];
+        }
+      }
+    }
+    if (TRANS) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) tile[cc + j][rr] = vals[j];
+    }
+  }
+  if (TRANS) {
+    __syncthreads();
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      const int rr = (tid >> 3) + pass * 32, cc = (tid & 7) * 8;  // rr: n index, cc: m index
+      const int gn = tn + rr, gm = tm + cc;
+      if (gn < N) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (gm + j < M) yt[(long)gn * M + gm + j] = tile[rr][cc + j];
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------ GEMM
+constexpr int BM = 128, BN = 128, BK = 64;  // BK in fp8 elements (= bytes)
+
+__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }
+
+template <int FA, int FB, bool OUT_F32>
+__global__ __launch_bounds__(256, 2) void fp8_gemm_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
+                                                          const float* __restrict__ sa, const float* __restrict__ sb,
+                                                          const bf16_t* __restrict__ bias, void* __restrict__ C, int M,
+                                                          int N, int K) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2][2][BM * BK];  // [buf][A/B][rows * 64 B]
+  const int tiles_n = N / BN;
+  const int nwg = (M / BM) * tiles_n;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int tm = (bid / tiles_n) * BM, tn = (bid % tiles_n) * BN;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hf = lane >> 5;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  // staging: 128 rows x 4 chunks of 16 B per operand = 512 chunks -> 2 per thread per operand
+  uint4 ra[2], rb[2];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int c = tid + t * 256, row = c >> 2, ch = c & 3;
+      ra[t] = *reinterpret_cast<const uint4*>(A + (long)(tm + row) * K + k0 + ch * 16);
+      rb[t] = *reinterpret_cast<const uint4*>(B + (long)(tn + row) * K + k0 + ch * 16);
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int c = tid + t * 256, row = c >> 2, ch = c & 3;
+      *reinterpret_cast<uint4*>(&smem[buf][0][row * 64 + swz(row, ch) * 16]) = ra[t];
+      *reinterpret_cast<uint4*>(&smem[buf][1][row * 64 + swz(row, ch) * 16]) = rb[t];
+    }
+  };
+  auto frag = [&](int buf, int which, int row) -> v8i {
+    const uint8_t* base = &smem[buf][which][row * 64];
+    const uint4 lo = *reinterpret_cast<const uint4*>(base + swz(row, 2 * hf) * 16);
+    const uint4 hi = *reinterpret_cast<const uint4*>(base + swz(row, 2 * hf + 1) * 16);
+    v8i v;
+    v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w; v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+    return v;
+  };
+
+  const int nk = K / BK;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload((kt + 1) * BK);  // issue next tile's loads before the MFMAs (latency hidden)
+    v8i af[2], bfr[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) af[i] = frag(cur, 0, wm + i * 32 + r);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) bfr[j] = frag(cur, 1, wn + j * 32 + r);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)  // swapped operands: acc = C^T tile (lane <-> m, registers <-> n)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(bfr[j], af[i], acc[i][j], FB, FA, 0, 0x7f7f7f7f, 0,
+                                                                    0x7f7f7f7f);
+    if (kt + 1 < nk) lstore(cur ^ 1);
+    __syncthreads();
+  }
+  const float s = sa[0] * sb[0];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int m = tm + wm + i * 32 + r;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n = tn + wn + j * 32 + 8 * g + 4 * hf;
+        float v[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          v[t] = acc[i][j][4 * g + t] * s;
+          if (bias != nullptr) v[t] += bf2f(bias[n + t]);
+        }
+        if (OUT_F32) {
+          *reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + (long)m * N + n) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+          bf16x4 w;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) w.v[t] = f2bf(v[t]);
+          *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16_t*>(C) + (long)m * N + n) = w;
+        }
+      }
+    }
+}
+
+}  // namespace
+
+torch::Tensor fp8_amax(torch::Tensor x, c10::optional<torch::Tensor> out) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous(), "fp8_amax: x must be contiguous bf16");
+  torch::Tensor o = out.has_value() ? *out : torch::empty({1}, x.options().dtype(torch::kFloat32));
+  auto stream = at::hip::getCurrentHIPStream();
+  hipMemsetAsync(o.data_ptr(), 0, sizeof(float), stream);
+  const long n = x.numel();
+  if (n == 0) return o;
+  long g = (n / 8 + 255) / 256;
+  g = std::max<long>(1, std::min<long>(g, 2048));
+  hipLaunchKernelGGL(amax_kernel, dim3(g), dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(x.data_ptr()), n,
+                     reinterpret_cast<unsigned int*>(o.data_ptr()));
+  return o;
+}
+
+torch::Tensor fp8_scale_from_amax(torch::Tensor amax, double fp8_max, double margin) {
+  // scale = fp8_max / amax / 2^margin (amax clamped away from 0), as device tensor ops (no host sync).
+  return (fp8_max / std::pow(2.0, margin)) / amax.clamp_min(1e-12);
+}
+
+std::vector<torch::Tensor> fp8_cast(torch::Tensor x, torch::Tensor scale, bool e5m2, bool transpose) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.dim() == 2, "fp8_cast: x must be 2-D contiguous bf16");
+  const int M = x.size(0), N = x.size(1);
+  auto dt = e5m2 ? at::kFloat8_e5m2 : at::kFloat8_e4m3fn;
+  auto y = torch::empty({M, N}, x.options().dtype(dt));
+  torch::Tensor yt;
+  if (transpose) yt = torch::empty({N, M}, x.options().dtype(dt));
+  if (M == 0 || N == 0) return transpose ? std::vector<torch::Tensor>{y, yt} : std::vector<torch::Tensor>{y};
+  dim3 grid((N + 63) / 64, (M + 63) / 64);
+  auto stream = at::hip::getCurrentHIPStream();
+  uint8_t* yp = reinterpret_cast<uint8_t*>(y.data_ptr());
+  uint8_t* ytp = transpose ? reinterpret_cast<uint8_t*>(yt.data_ptr()) : nullptr;
+  const bf16_t* xp = reinterpret_cast<const bf16_t*>(x.data_ptr());
+  const float* sp = scale.data_ptr<float>();
+  if (e5m2) {
+    if (transpose) hipLaunchKernelGGL((cast_kernel<true, true>), grid, dim3(256), 0, stream, xp, sp, yp, ytp, M, N);
+    else hipLaunchKernelGGL((cast_kernel<true, false>), grid, dim3(256), 0, stream, xp, sp, yp, ytp, M, N);
+  } else {
+    if (transpose) hipLaunchKernelGGL((cast_kernel<false, true>), grid, dim3(256), 0, stream, xp, sp, yp, ytp, M, N);
+    else hipLaunchKernelGGL((cast_kernel<false, false>), grid, dim3(256), 0, stream, xp, sp, yp, ytp, M, N);
+  }
+  if (transpose) return {y, yt};
+  return {y};
+}
+
+torch::Tensor fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor a_scale_inv, torch::Tensor b_scale_inv, bool a_e5m2,
+                       bool b_e5m2, c10::optional<torch::Tensor> bias, bool out_fp32) {
+  TORCH_CHECK(a.is_cuda() && b.is_cuda() && a.dim() == 2 && b.dim() == 2 && a.is_contiguous() && b.is_contiguous(),
+              "fp8_gemm: operands must be 2-D contiguous HIP tensors");
+  TORCH_CHECK(a.element_size() == 1 && b.element_size() == 1, "fp8_gemm: operands must be fp8");
+  const int M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(b.size(1) == K, "fp8_gemm: K mismatch");
+  TORCH_CHECK(M % BM == 0 && N % BN == 0 && K % BK == 0, "fp8_gemm: M, N must be multiples of 128 and K of 64");
+  auto out = torch::empty({M, N}, a.options().dtype(out_fp32 ? torch::kFloat32 : torch::kBFloat16));
+  const bf16_t* bp = nullptr;
+  if (bias.has_value()) {
+    TORCH_CHECK(bias->scalar_type() == at::kBFloat16 && bias->numel() == N, "fp8_gemm: bias must be bf16 [N]");
+    bp = reinterpret_cast<const bf16_t*>(bias->data_ptr());
+  }
+  const int nwg = (M / BM) * (N / BN);
+  auto stream = at::hip::getCurrentHIPStream();
+  const uint8_t* ap = reinterpret_cast<const uint8_t*>(a.data_ptr());
+  const uint8_t* bptr = reinterpret_cast<const uint8_t*>(b.data_ptr());
+  const float* sap = a_scale_inv.data_ptr<float>();
+  const float* sbp = b_scale_inv.data_ptr<float>();
+  void* cp = out.data_ptr();
+#define GEMM_LAUNCH(FA, FB, OF) \
+  hipLaunchKernelGGL((fp8_gemm_kernel<FA, FB, OF>), dim3(nwg), dim3(256), 0, stream, ap, bptr, sap, sbp, bp, cp, M, N, K)
+  if (!a_e5m2 && !b_e5m2) { if (out_fp32) GEMM_LAUNCH(0, 0, true); else GEMM_LAUNCH(0, 0, false); }
+  else if (!a_e5m2 && b_e5m2) { if (out_fp32) GEMM_LAUNCH(0, 1, true); else GEMM_LAUNCH(0, 1, false); }
+  else if (a_e5m2 && !b_e5m2) { if (out_fp32) GEMM_LAUNCH(1, 0, true); else GEMM_LAUNCH(1, 0, false); }
+  else { if (out_fp32) GEMM_LAUNCH(1, 1, true); else GEMM_LAUNCH(1, 1, false); }
+#undef GEMM_LAUNCH
+  return out;
+}

@@ -1,0 +1,354 @@
+// Memory-bound fused kernels for the transformer block (bf16 activations, fp32 math):
+//   * RMSNorm forward (optionally fused with the residual add) and backward (dx + dweight),
+//   * SwiGLU forward/backward on the fused [gate | up] projection output,
+//   * rotary embedding (rotate-half convention) applied in place to the Q and K heads of a fused QKV buffer.
+// All loads/stores are 16 B per lane (8 x bf16); one row per workgroup for the row-wise kernels.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include "common.h"
+
+using namespace acc;
+
+namespace {
+
+constexpr int kNormThreads = 256;
+
+template <int VPT>
+__global__ __launch_bounds__(kNormThreads) void rmsnorm_fwd_kernel(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ res, const bf16_t* __restrict__ w,
+    bf16_t* __restrict__ y, bf16_t* __restrict__ res_out, float* __restrict__ rstd_out, int H, float eps) {
+  __shared__ float scratch[16];
+  const int row = blockIdx.x;
+  const int nvec = H >> 3;
+  const bf16x8* xr = reinterpret_cast<const bf16x8*>(x + (size_t)row * H);
+  float v[VPT][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = threadIdx.x + i * kNormThreads;
+    if (c < nvec) {
+      bf16x8 a = xr[c];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = bf2f(a.v[j]);
+      if (res != nullptr) {
+        bf16x8 b = reinterpret_cast<const bf16x8*>(res + (size_t)row * H)[c];
+        bf16x8 s;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s.v[j] = f2bf(v[i][j] + bf2f(b.v[j]));
+          v[i][j] = bf2f(s.v[j]);  // normalise exactly what is stored in the residual stream
+        }
+        reinterpret_cast<bf16x8*>(res_out + (size_t)row * H)[c] = s;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[i][j] * v[i][j];
+    }
+  }
+  ss = block_sum(ss, scratch);
+  const float r = rsqrtf(ss / (float)H + eps);
+  if (threadIdx.x == 0) rstd_out[row] = r;
+  const bf16x8* wr = reinterpret_cast<const bf16x8*>(w);
+  bf16x8* yr = reinterpret_cast<bf16x8*>(y + (size_t)row * H);
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = threadIdx.x + i * kNormThreads;
+    if (c < nvec) {
+      bf16x8 ww = wr[c], o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o.v[j] = f2bf(v[i][j] * r * bf2f(ww.v[j]));
+      yr[c] = o;
+    }
+  }
+}
+
+// dx = rstd * (dy*w - xhat * mean(dy*w*xhat)) (+ dres); per-block partial dweight in fp32.
+template <int VPT>
+__global__ __launch_bounds__(kNormThreads) void rmsnorm_bwd_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+    const float* __restrict__ rstd, const bf16_t* __restrict__ dres, bf16_t* __restrict__ dx,
+    float* __restrict__ dw_part, int T, int H) {
+  __shared__ float scratch[16];
+  const int nvec = H >> 3;
+  float wv[VPT][8], dwacc[VPT][8];
+  const bf16x8* wr = reinterpret_cast<const bf16x8*>(w);
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = threadIdx.x + i * kNormThreads;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dwacc[i][j] = 0.f;
+    if (c < nvec) {
+      bf16x8 ww = wr[c];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) wv[i][j] = bf2f(ww.v[j]);
+    }
+  }
+  for (int row = blockIdx.x; row < T; row += gridDim.x) {
+    const float r = rstd[row];
+    float xh[VPT][8], g[VPT][8];
+    float dot = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int c = threadIdx.x + i * kNormThreads;
+      if (c < nvec) {
+        bf16x8 a = reinterpret_cast<const bf16x8*>(x + (size_t)row * H)[c];
+        bf16x8 d = reinterpret_cast<const bf16x8*>(dy + (size_t)row * H)[c];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xh[i][j] = bf2f(a.v[j]) * r;
+          const float dd = bf2f(d.v[j]);
+          g[i][j] = dd * wv[i][j];
+          dwacc[i][j] += dd * xh[i][j];
+          dot += g[i][j] * xh[i][j];
+        }
+      }
+    }
+    dot = block_sum(dot, scratch) / (float)H;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int c = threadIdx.x + i * kNormThreads;
+      if (c < nvec) {
+        bf16x8 o;
+        bf16x8 rr;
+        if (dres != nullptr) rr = reinterpret_cast<const bf16x8*>(dres + (size_t)row * H)[c];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float val = r * (g[i][j] - xh[i][j] * dot);
+          if (dres != nullptr) val += bf2f(rr.v[j]);
+          o.v[j] = f2bf(val);
+        }
+        reinterpret_cast<bf16x8*>(dx + (size_t)row * H)[c] = o;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = threadIdx.x + i * kNormThreads;
+    if (c < nvec) {
+      float4* dst = reinterpret_cast<float4*>(dw_part + (size_t)blockIdx.x * H + c * 8);
+      dst[0] = make_float4(dwacc[i][0], dwacc[i][1], dwacc[i][2], dwacc[i][3]);
+      dst[1] = make_float4(dwacc[i][4], dwacc[i][5], dwacc[i][6], dwacc[i][7]);
+    }
+  }
+}
+
+// Column sum of the [P, H] fp32 partials → dweight (bf16 or fp32 output).
+template <typename OutT>
+__global__ void colsum_kernel(const float* __restrict__ part, OutT* __restrict__ out, int P, int H) {
+  const int col = blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= H) return;
+  float s = 0.f;
+  for (int p = 0; p < P; ++p) s += part[(size_t)p * H + col];
+  out[col] = from_f<OutT>(s);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// SwiGLU on a fused [T, 2F] buffer: gate = gu[:, :F], up = gu[:, F:]; h = silu(gate) * up.
+// ---------------------------------------------------------------------------------------------------
+__global__ void swiglu_fwd_kernel(const bf16_t* __restrict__ gu, bf16_t* __restrict__ h, long T, int F) {
+  const long nvec_row = F >> 3;
+  const long total = T * nvec_row;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    const long row = idx / nvec_row, c = idx - row * nvec_row;
+    const bf16x8 g = reinterpret_cast<const bf16x8*>(gu + row * 2 * F)[c];
+    const bf16x8 u = reinterpret_cast<const bf16x8*>(gu + row * 2 * F + F)[c];
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float gf = bf2f(g.v[j]);
+      const float s = gf / (1.f + __expf(-gf));
+      o.v[j] = f2bf(s * bf2f(u.v[j]));
+    }
+    reinterpret_cast<bf16x8*>(h + row * F)[c] = o;
+  }
+}
+
+// dgate = dh * up * sig * (1 + g*(1-sig)), dup = dh * silu(g). Written into dgu [T, 2F].
+__global__ void swiglu_bwd_kernel(const bf16_t* __restrict__ gu, const bf16_t* __restrict__ dh,
+                                  bf16_t* __restrict__ dgu, long T, int F) {
+  const long nvec_row = F >> 3;
+  const long total = T * nvec_row;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    const long row = idx / nvec_row, c = idx - row * nvec_row;
+    const bf16x8 g = reinterpret_cast<const bf16x8*>(gu + row * 2 * F)[c];
+    const bf16x8 u = reinterpret_cast<const bf16x8*>(gu + row * 2 * F + F)[c];
+    const bf16x8 d = reinterpret_cast<const bf16x8*>(dh + row * F)[c];
+    bf16x8 og, ou;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float gf = bf2f(g.v[j]), uf = bf2f(u.v[j]), df = bf2f(d.v[j]);
+      const float sig = 1.f / (1.f + __expf(-gf));
+      const float silu = gf * sig;
+      og.v[j] = f2bf(df * uf * sig * (1.f + gf * (1.f - sig)));
+      ou.v[j] = f2bf(df * silu);
+    }
+    reinterpret_cast<bf16x8*>(dgu + row * 2 * F)[c] = og;
+    reinterpret_cast<bf16x8*>(dgu + row * 2 * F + F)[c] = ou;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// RoPE in place on qkv [T, (Hq + 2*Hkv) * D] (rotate-half pairs (i, i + D/2)); heads [0, Hq + Hkv) are
+// rotated (Q and K), V untouched. cos/sin tables are fp32 [S, D/2]; position = pos[t] (or t % S).
+// sign = +1 forward, -1 backward (inverse rotation of the incoming gradient).
+// ---------------------------------------------------------------------------------------------------
+__global__ void rope_kernel(bf16_t* __restrict__ qkv, const float* __restrict__ cosb, const float* __restrict__ sinb,
+                            const int64_t* __restrict__ pos, long T, int S, int n_rot_heads, int n_heads_total,
+                            int D, float sign) {
+  const int half = D >> 1;
+  const int nvec = half >> 2;  // 4 pairs per thread step (8 B of each half)
+  const long per_row = (long)n_rot_heads * nvec;
+  const long total = T * per_row;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    const long t = idx / per_row;
+    const int rem = (int)(idx - t * per_row);
+    const int h = rem / nvec, c = rem - h * nvec;
+    const long p = pos != nullptr ? pos[t] : (t % S);
+    bf16_t* base = qkv + (t * n_heads_total + h) * (long)D;
+    bf16x4 a = reinterpret_cast<bf16x4*>(base)[c];
+    bf16x4 b = reinterpret_cast<bf16x4*>(base + half)[c];
+    const float4 cs = reinterpret_cast<const float4*>(cosb + p * half)[c];
+    const float4 sn = reinterpret_cast<const float4*>(sinb + p * half)[c];
+    const float cc[4] = {cs.x, cs.y, cs.z, cs.w};
+    const float ss[4] = {sn.x * sign, sn.y * sign, sn.z * sign, sn.w * sign};
+    bf16x4 oa, ob;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float x1 = bf2f(a.v[j]), x2 = bf2f(b.v[j]);
+      oa.v[j] = f2bf(x1 * cc[j] - x2 * ss[j]);
+      ob.v[j] = f2bf(x2 * cc[j] + x1 * ss[j]);
+    }
+    reinterpret_cast<bf16x4*>(base)[c] = oa;
+    reinterpret_cast<bf16x4*>(base + half)[c] = ob;
+  }
+}
+
+inline int grid_for(long work, int threads) {
+  long g = (work + threads - 1) / threads;
+  if (g > 256 * 8) g = 256 * 8;  // 8 resident blocks per CU, grid-stride the rest
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+void check_bf16_cuda(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a HIP tensor");
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bf16");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+}  // namespace
+
+// ----------------------------------------------------------------------------------------- host API
+std::vector<torch::Tensor> rmsnorm_fwd(torch::Tensor x, c10::optional<torch::Tensor> residual, torch::Tensor w,
+                                       double eps) {
+  check_bf16_cuda(x, "x");
+  check_bf16_cuda(w, "weight");
+  const int H = x.size(-1);
+  TORCH_CHECK(H % 8 == 0 && H <= 8 * 256 * 8, "rmsnorm: hidden size must be a multiple of 8 and <= 16384");
+  const long T = x.numel() / H;
+  auto y = torch::empty_like(x);
+  auto rstd = torch::empty({T}, x.options().dtype(torch::kFloat32));
+  torch::Tensor res_out;
+  const bf16_t* resp = nullptr;
+  bf16_t* resop = nullptr;
+  if (residual.has_value()) {
+    check_bf16_cuda(*residual, "residual");
+    res_out = torch::empty_like(x);
+    resp = reinterpret_cast<const bf16_t*>(residual->data_ptr());
+    resop = reinterpret_cast<bf16_t*>(res_out.data_ptr());
+  }
+  if (T == 0) return {y, rstd, res_out};
+  auto stream = at::hip::getCurrentHIPStream();
+  const int vpt = (H / 8 + kNormThreads - 1) / kNormThreads;
+#define LAUNCH_FWD(V)                                                                                             \
+  hipLaunchKernelGGL(rmsnorm_fwd_kernel<V>, dim3(T), dim3(kNormThreads), 0, stream,                              \
+                     reinterpret_cast<const bf16_t*>(x.data_ptr()), resp, reinterpret_cast<const bf16_t*>(w.data_ptr()), \
+                     reinterpret_cast<bf16_t*>(y.data_ptr()), resop, rstd.data_ptr<float>(), H, (float)eps)
+  if (vpt <= 1) LAUNCH_FWD(1);
+  else if (vpt <= 2) LAUNCH_FWD(2);
+  else if (vpt <= 4) LAUNCH_FWD(4);
+  else LAUNCH_FWD(8);
+#undef LAUNCH_FWD
+  return {y, rstd, res_out};
+}
+
+std::vector<torch::Tensor> rmsnorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor w, torch::Tensor rstd,
+                                       c10::optional<torch::Tensor> dres) {
+  check_bf16_cuda(dy, "dy");
+  check_bf16_cuda(x, "x");
+  check_bf16_cuda(w, "weight");
+  const int H = x.size(-1);
+  const long T = x.numel() / H;
+  auto dx = torch::empty_like(x);
+  const int P = (int)std::min<long>(T > 0 ? T : 1, 512);
+  auto part = torch::empty({P, H}, x.options().dtype(torch::kFloat32));
+  auto dw = torch::empty({H}, w.options());
+  auto stream = at::hip::getCurrentHIPStream();
+  const bf16_t* dresp = nullptr;
+  if (dres.has_value()) {
+    check_bf16_cuda(*dres, "dres");
+    dresp = reinterpret_cast<const bf16_t*>(dres->data_ptr());
+  }
+  if (T == 0) { dw.zero_(); return {dx, dw}; }
+  const int vpt = (H / 8 + kNormThreads - 1) / kNormThreads;
+#define LAUNCH_BWD(V)                                                                                             \
+  hipLaunchKernelGGL(rmsnorm_bwd_kernel<V>, dim3(P), dim3(kNormThreads), 0, stream,                              \
+                     reinterpret_cast<const bf16_t*>(dy.data_ptr()), reinterpret_cast<const bf16_t*>(x.data_ptr()), \
+                     reinterpret_cast<const bf16_t*>(w.data_ptr()), rstd.data_ptr<float>(), dresp,               \
+                     reinterpret_cast<bf16_t*>(dx.data_ptr()), part.data_ptr<float>(), (int)T, H)
+  if (vpt <= 1) LAUNCH_BWD(1);
+  else if (vpt <= 2) LAUNCH_BWD(2);
+  else if (vpt <= 4) LAUNCH_BWD(4);
+  else LAUNCH_BWD(8);
+#undef LAUNCH_BWD
+  hipLaunchKernelGGL(colsum_kernel<bf16_t>, dim3((H + 255) / 256), dim3(256), 0, stream, part.data_ptr<float>(),
+                     reinterpret_cast<bf16_t*>(dw.data_ptr()), P, H);
+  return {dx, dw};
+}
+
+torch::Tensor swiglu_fwd(torch::Tensor gu) {
+  check_bf16_cuda(gu, "gate_up");
+  const int F = gu.size(-1) / 2;
+  TORCH_CHECK(F % 8 == 0, "swiglu: intermediate size must be a multiple of 8");
+  const long T = gu.numel() / (2 * F);
+  auto sizes = gu.sizes().vec();
+  sizes.back() = F;
+  auto h = torch::empty(sizes, gu.options());
+  const long work = T * (F / 8);
+  if (work == 0) return h;
+  hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(grid_for(work, 256)), dim3(256), 0, at::hip::getCurrentHIPStream(),
+                     reinterpret_cast<const bf16_t*>(gu.data_ptr()), reinterpret_cast<bf16_t*>(h.data_ptr()), T, F);
+  return h;
+}
+
+torch::Tensor swiglu_bwd(torch::Tensor gu, torch::Tensor dh) {
+  check_bf16_cuda(gu, "gate_up");
+  check_bf16_cuda(dh, "dh");
+  const int F = gu.size(-1) / 2;
+  const long T = gu.numel() / (2 * F);
+  auto dgu = torch::empty_like(gu);
+  const long work = T * (F / 8);
+  if (work == 0) return dgu;
+  hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(grid_for(work, 256)), dim3(256), 0, at::hip::getCurrentHIPStream(),
+                     reinterpret_cast<const bf16_t*>(gu.data_ptr()), reinterpret_cast<const bf16_t*>(dh.data_ptr()),
+                     reinterpret_cast<bf16_t*>(dgu.data_ptr()), T, F);
+  return dgu;
+}
+
+void rope_inplace(torch::Tensor qkv, torch::Tensor cos, torch::Tensor sin, c10::optional<torch::Tensor> pos,
+                  int64_t n_rot_heads, int64_t n_heads_total, int64_t head_dim, double sign) {
+  check_bf16_cuda(qkv, "qkv");
+  TORCH_CHECK(cos.scalar_type() == at::kFloat && sin.scalar_type() == at::kFloat, "rope tables must be fp32");
+  TORCH_CHECK(head_dim % 8 == 0, "rope: head_dim must be a multiple of 8");
+  const long T = qkv.numel() / (n_heads_total * head_dim);
+  const int S = cos.size(0);
+  const int64_t* posp = nullptr;
+  if (pos.has_value()) {
+    TORCH_CHECK(pos->scalar_type() == at::kLong && pos->numel() == T, "rope: positions must be int64 [T]");
+    posp = pos->data_ptr<int64_t>();
+  }
+  const long work = T * n_rot_heads * (head_dim / 8);
+  if (work == 0) return;
+  hipLaunchKernelGGL(rope_kernel, dim3(grid_for(work, 256)), dim3(256), 0, at::hip::getCurrentHIPStream(),
+                     reinterpret_cast<bf16_t*>(qkv.data_ptr()), cos.data_ptr<float>(), sin.data_ptr<float>(), posp, T,
+                     S, (int)n_rot_heads, (int)n_heads_total, (int)head_dim, (float)sign);
+}

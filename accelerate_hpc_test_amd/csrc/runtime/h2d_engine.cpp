@@ -1,0 +1,236 @@
+// Host runtime: asynchronous host->device copy engine with a pinned staging ring.
+//
+// Used by big-model inference (offloaded weights are uploaded block by block ahead of use), checkpoint loading
+// (safetensors mmap -> HBM) and FSDP CPU offload. A pageable source (e.g. an mmap'd checkpoint) cannot be
+// DMA'd directly; the engine splits it into slot-sized pieces, worker threads memcpy each piece into one of
+// `num_slots` pinned host slots (hipHostMalloc), and each filled slot is uploaded with hipMemcpyAsync on the
+// engine's own HIP stream. A per-slot HIP event gates slot reuse, so CPU copies, PCIe DMA and GPU compute all
+// overlap. Consumers order against the uploads with `wait_on_current_stream()` (hipStreamWaitEvent on the
+// caller's torch stream — no host blocking).
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <functional>
+#include <mutex>
+#include <stdexcept>
+#include <thread>
+#include <vector>
+
+#define HIP_OK(expr)                                                                         \
+  do {                                                                                      \
+    hipError_t _e = (expr);                                                                 \
+    if (_e != hipSuccess) throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(_e) + " at " #expr); \
+  } while (0)
+
+namespace {
+
+class H2DEngine {
+ public:
+  H2DEngine(int device, int64_t num_slots, int64_t slot_bytes, int64_t num_threads)
+      : device_(device), slot_bytes_(slot_bytes) {
+    HIP_OK(hipSetDevice(device_));
+    HIP_OK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, -1));
+    HIP_OK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
+    for (int64_t i = 0; i < num_slots; ++i) {
+      void* p = nullptr;
+      HIP_OK(hipHostMalloc(&p, slot_bytes_, hipHostMallocDefault));
+      hipEvent_t ev;
+      HIP_OK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+      slots_.push_back({p, ev, false});
+    }
+    for (int64_t t = 0; t < std::max<int64_t>(1, num_threads); ++t) workers_.emplace_back([this] { worker(); });
+  }
+
+  ~H2DEngine() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& w : workers_) w.join();
+    hipSetDevice(device_);
+    hipStreamSynchronize(stream_);
+    for (auto& s : slots_) {
+      hipEventDestroy(s.ev);
+      hipHostFree(s.ptr);
+    }
+    hipEventDestroy(done_);
+    hipStreamDestroy(stream_);
+  }
+
+  // Enqueue a copy of a CPU tensor (pageable or pinned, contiguous) into a contiguous device tensor.
+  void copy(torch::Tensor src, torch::Tensor dst) {
+    TORCH_CHECK(src.device().is_cpu() && dst.is_cuda(), "H2DEngine.copy: src must be CPU, dst a HIP tensor");
+    TORCH_CHECK(src.is_contiguous() && dst.is_contiguous(), "H2DEngine.copy: tensors must be contiguous");
+    TORCH_CHECK(src.nbytes() == dst.nbytes(), "H2DEngine.copy: size mismatch");
+    const char* s = static_cast<const char*>(src.data_ptr());
+    char* d = static_cast<char*>(dst.data_ptr());
+    const int64_t n = src.nbytes();
+    if (src.is_pinned()) {  // already DMA-able: one async copy, no staging
+      std::lock_guard<std::mutex> g(mu_);
+      HIP_OK(hipSetDevice(device_));
+      HIP_OK(hipMemcpyAsync(d, s, n, hipMemcpyHostToDevice, stream_));
+      keep_.push_back(src);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (int64_t off = 0; off < n; off += slot_bytes_) {
+        const int64_t len = std::min<int64_t>(slot_bytes_, n - off);
+        tasks_.push_back({s + off, d + off, len});
+        ++pending_;
+      }
+      keep_.push_back(src);
+    }
+    cv_.notify_all();
+  }
+
+  // Block the host until every enqueued piece has been staged and its DMA issued, then make the caller's
+  // current torch stream wait on the engine's stream (device-side ordering, no host wait for the DMA).
+  void wait_on_current_stream() {
+    drain_issue();
+    std::lock_guard<std::mutex> g(mu_);
+    HIP_OK(hipSetDevice(device_));
+    HIP_OK(hipEventRecord(done_, stream_));
+    HIP_OK(hipStreamWaitEvent(at::hip::getCurrentHIPStream().stream(), done_, 0));
+    keep_.clear();
+  }
+
+  void synchronize() {
+    drain_issue();
+    HIP_OK(hipSetDevice(device_));
+    HIP_OK(hipStreamSynchronize(stream_));
+    std::lock_guard<std::mutex> g(mu_);
+    keep_.clear();
+  }
+
+  int64_t slot_bytes() const { return slot_bytes_; }
+  int64_t num_slots() const { return (int64_t)slots_.size(); }
+
+ private:
+  struct Slot {
+    void* ptr;
+    hipEvent_t ev;
+    bool busy;
+  };
+  struct Task {
+    const char* src;
+    char* dst;
+    int64_t len;
+  };
+
+  void drain_issue() {
+    std::unique_lock<std::mutex> lk(mu_);
+    idle_cv_.wait(lk, [this] { return pending_ == 0; });
+  }
+
+  int acquire_slot(std::unique_lock<std::mutex>& lk) {
+    for (;;) {
+      for (size_t i = 0; i < slots_.size(); ++i) {
+        if (!slots_[i].busy) {
+          slots_[i].busy = true;
+          return (int)i;
+        }
+        // reclaim slots whose DMA has finished
+        if (hipEventQuery(slots_[i].ev) == hipSuccess && slots_[i].busy && reclaimable_[i]) {
+          reclaimable_[i] = false;
+          return (int)i;
+        }
+      }
+      lk.unlock();
+      std::this_thread::yield();
+      lk.lock();
+    }
+  }
+
+  void worker() {
+    HIP_OK(hipSetDevice(device_));
+    for (;;) {
+      Task t;
+      int slot;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [this] { return stop_ || !tasks_.empty(); });
+        if (stop_ && tasks_.empty()) return;
+        t = tasks_.front();
+        tasks_.pop_front();
+        if (reclaimable_.size() != slots_.size()) reclaimable_.assign(slots_.size(), false);
+        slot = acquire_slot(lk);
+      }
+      // a recycled slot's previous DMA must be complete before overwriting it
+      HIP_OK(hipEventSynchronize(slots_[slot].ev));
+      std::memcpy(slots_[slot].ptr, t.src, t.len);
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        HIP_OK(hipMemcpyAsync(t.dst, slots_[slot].ptr, t.len, hipMemcpyHostToDevice, stream_));
+        HIP_OK(hipEventRecord(slots_[slot].ev, stream_));
+        reclaimable_[slot] = true;
+        if (--pending_ == 0) idle_cv_.notify_all();
+      }
+    }
+  }
+
+  int device_;
+  int64_t slot_bytes_;
+  hipStream_t stream_;
+  hipEvent_t done_;
+  std::vector<Slot> slots_;
+  std::vector<bool> reclaimable_;
+  std::deque<Task> tasks_;
+  std::vector<torch::Tensor> keep_;
+  std::vector<std::thread> workers_;
+  std::mutex mu_;
+  std::condition_variable cv_, idle_cv_;
+  int64_t pending_ = 0;
+  bool stop_ = false;
+};
+
+// Rolling FNV-1a hash over the sequence of collectives a rank issued (op, group size, dtype, numel). In debug
+// mode ranks compare it every N steps, catching a desynchronised collective order before RCCL deadlocks.
+class CollectiveSeq {
+ public:
+  void record(const std::string& op, int64_t group, int64_t dtype, int64_t numel) {
+    auto mix = [this](uint64_t v) {
+      for (int i = 0; i < 8; ++i) {
+        h_ ^= (v >> (8 * i)) & 0xff;
+        h_ *= 1099511628211ull;
+      }
+    };
+    for (char c : op) mix((uint64_t)(unsigned char)c);
+    mix((uint64_t)group);
+    mix((uint64_t)dtype);
+    mix((uint64_t)numel);
+    ++count_;
+  }
+  uint64_t digest() const { return h_; }
+  int64_t count() const { return count_; }
+  void reset() { h_ = 1469598103934665603ull; count_ = 0; }
+
+ private:
+  uint64_t h_ = 1469598103934665603ull;
+  int64_t count_ = 0;
+};
+
+}  // namespace
+
+void register_runtime(pybind11::module& m) {
+  pybind11::class_<H2DEngine>(m, "H2DEngine")
+      .def(pybind11::init<int, int64_t, int64_t, int64_t>(), pybind11::arg("device"), pybind11::arg("num_slots") = 4,
+           pybind11::arg("slot_bytes") = 64 << 20, pybind11::arg("num_threads") = 4)
+      .def("copy", &H2DEngine::copy, pybind11::call_guard<pybind11::gil_scoped_release>())
+      .def("wait_on_current_stream", &H2DEngine::wait_on_current_stream, pybind11::call_guard<pybind11::gil_scoped_release>())
+      .def("synchronize", &H2DEngine::synchronize, pybind11::call_guard<pybind11::gil_scoped_release>())
+      .def_property_readonly("slot_bytes", &H2DEngine::slot_bytes)
+      .def_property_readonly("num_slots", &H2DEngine::num_slots);
+  pybind11::class_<CollectiveSeq>(m, "CollectiveSeq")
+      .def(pybind11::init<>())
+      .def("record", &CollectiveSeq::record)
+      .def("digest", &CollectiveSeq::digest)
+      .def("count", &CollectiveSeq::count)
+      .def("reset", &CollectiveSeq::reset);
+}

@@ -1,0 +1,890 @@
+"""Data-loading layer: per-rank sharding of samplers/datasets and device-prefetching loaders.
+
+Parity: `/root/reference/src/accelerate/data_loader.py:73-1451` — `SeedableRandomSampler`,
+`BatchSamplerShard` (split / no-split, `even_batches` wrap-around), `IterableDatasetShard`,
+`DataLoaderShard` (one-batch look-ahead for end-of-data detection), `DataLoaderDispatcher` (rank 0 reads
+and broadcasts), `prepare_data_loader`, `skip_first_batches`. The index sequences produced for each rank
+are identical to the reference's (tests/test_data_loader.py pins them).
+
+MI355X-native difference: on a GPU, `DataLoaderShard` moves batches with a **device prefetcher**
+(`DevicePrefetcher`): a host thread collates the next K batches into pinned memory and issues
+`hipMemcpyAsync` (non-blocking `.to`) on a dedicated copy stream, recording a HIP event per batch; the
+consumer's compute stream waits on that event instead of the host blocking, so the H2D copy of batch i+1
+overlaps compute on batch i. (The reference copies synchronously on the compute stream.)
+"""
+
+from __future__ import annotations
+
+import math
+import queue
+import threading
+from contextlib import suppress
+from typing import Callable, Optional, Union
+
+import torch
+from torch.utils.data import BatchSampler, DataLoader, IterableDataset, RandomSampler
+
+from .logging import get_logger
+from .state import DistributedType, GradientState, PartialState
+from .utils.dataclasses import RNGType
+from .utils.operations import (
+    broadcast,
+    broadcast_object_list,
+    concatenate,
+    find_batch_size,
+    get_data_structure,
+    initialize_tensors,
+    send_to_device,
+    slice_tensors,
+)
+from .utils.random import synchronize_rng_states
+
+
+logger = get_logger(__name__)
+
+# kwargs of the PyTorch DataLoader and their defaults (used to rebuild a user's DataLoader).
+_PYTORCH_DATALOADER_KWARGS = {
+    "batch_size": 1,
+    "shuffle": False,
+    "sampler": None,
+    "batch_sampler": None,
+    "num_workers": 0,
+    "collate_fn": None,
+    "pin_memory": False,
+    "drop_last": False,
+    "timeout": 0,
+    "worker_init_fn": None,
+    "multiprocessing_context": None,
+    "generator": None,
+    "prefetch_factor": None,
+    "persistent_workers": False,
+    "pin_memory_device": "",
+    "in_order": True,
+}
+
+
+class SeedableRandomSampler(RandomSampler):
+    """RandomSampler whose permutation is a function of (`initial_seed` + epoch) — identical on all ranks."""
+
+    def __init__(self, *args, **kwargs):
+        data_seed = kwargs.pop("data_seed", None)
+        super().__init__(*args, **kwargs)
+        self.initial_seed = data_seed if data_seed is not None else torch.random.initial_seed()
+        self.epoch = 0
+
+    def __iter__(self):
+        if self.generator is None:
+            self.generator = torch.Generator()
+        self.generator.manual_seed(self.epoch + self.initial_seed)
+        yield from super().__iter__()
+        self.set_epoch(self.epoch + 1)
+
+    def set_epoch(self, epoch: int):
+        self.epoch = epoch
+
+
+class BatchSamplerShard(BatchSampler):
+    """Yield only this process's batches of a wrapped `BatchSampler`.
+
+    * `split_batches=False`: process p gets batches p, p+W, p+2W, ...
+    * `split_batches=True`: every batch is cut in W equal slices; process p gets slice p.
+    With `even_batches=True` the last incomplete round is completed with indices taken cyclically from the
+    start of the data so that every process sees the same number of same-sized batches.
+    """
+
+    def __init__(
+        self,
+        batch_sampler: BatchSampler,
+        num_processes: int = 1,
+        process_index: int = 0,
+        split_batches: bool = False,
+        even_batches: bool = True,
+    ):
+        if split_batches and batch_sampler.batch_size % num_processes != 0:
+            raise ValueError(
+                f"To use `BatchSamplerShard` in `split_batches` mode, the batch size ({batch_sampler.batch_size}) "
+                f"needs to be a round multiple of the number of processes ({num_processes})."
+            )
+        self.batch_sampler = batch_sampler
+        self.num_processes = num_processes
+        self.process_index = process_index
+        self.split_batches = split_batches
+        self.even_batches = even_batches
+        self.batch_size = getattr(batch_sampler, "batch_size", None)
+        self.drop_last = getattr(batch_sampler, "drop_last", False)
+        if self.batch_size is None and self.even_batches:
+            raise ValueError(
+                "You need to use `even_batches=False` when the batch sampler has no batch size. If you "
+                "are not calling this method directly, set `accelerator.even_batches=False` instead."
+            )
+
+    @property
+    def total_length(self):
+        return len(self.batch_sampler)
+
+    def __len__(self):
+        n = len(self.batch_sampler)
+        if self.split_batches:
+            return n
+        full_rounds, leftover = divmod(n, self.num_processes)
+        if leftover == 0 or self.drop_last:
+            return full_rounds
+        if self.even_batches:
+            return full_rounds + 1
+        return full_rounds + (1 if self.process_index < leftover else 0)
+
+    def __iter__(self):
+        return self._iter_with_split() if self.split_batches else self._iter_with_no_split()
+
+    def _iter_with_split(self):
+        bs, W, p = self.batch_size, self.num_processes, self.process_index
+        width = bs // W
+        first, last = None, None
+        for batch in self.batch_sampler:
+            if first is None:
+                first = list(batch)
+            if len(batch) == bs:
+                yield batch[width * p : width * (p + 1)]
+            last = batch
+        if self.drop_last or not first or last is None or len(last) >= bs:
+            return
+        if not self.even_batches:
+            if len(last) > width * p:
+                yield last[width * p : width * (p + 1)]
+            return
+        pool = list(first)
+        while len(pool) < bs:
+            pool = pool + pool
+        completed = list(last) + pool
+        yield completed[width * p : width * (p + 1)]
+
+    def _iter_with_no_split(self):
+        bs, W, p = self.batch_size, self.num_processes, self.process_index
+        round_, pool = [], []
+        for idx, batch in enumerate(self.batch_sampler):
+            if not self.drop_last and idx < W:
+                pool.extend(batch)
+            round_.append(batch)
+            if len(round_) == W and (bs is None or len(batch) == bs):
+                yield round_[p]
+                round_ = []
+        if self.drop_last or not pool or not round_:
+            return
+        if not self.even_batches:
+            if p < len(round_):
+                yield round_[p]
+            return
+        # Even batches: full batches of the last round go out as they are; the remaining slots of the round
+        # (the partial last batch, then any missing batches) are filled cyclically from the start of the data.
+        if p < len(round_) and len(round_[p]) == bs:
+            yield round_[p]
+        while len(pool) < W * bs:
+            pool = pool + pool
+        last = round_[-1]
+        if len(last) < bs:
+            slot, carry = len(round_) - 1, list(last)
+        else:
+            slot, carry = len(round_), []
+        cursor = 0
+        while slot < W:
+            need = bs - len(carry)
+            filled = carry + pool[cursor : cursor + need]
+            cursor += need
+            if slot == p:
+                yield filled
+            carry = []
+            slot += 1
+
+
+class IterableDatasetShard(IterableDataset):
+    """Shard an iterable dataset: consume `W*batch_size` elements, give this process its contiguous slice."""
+
+    def __init__(
+        self,
+        dataset: IterableDataset,
+        batch_size: int = 1,
+        drop_last: bool = False,
+        num_processes: int = 1,
+        process_index: int = 0,
+        split_batches: bool = False,
+    ):
+        if split_batches and batch_size > 1 and batch_size % num_processes != 0:
+            raise ValueError(
+                f"To use `IterableDatasetShard` in `split_batches` mode, the batch size ({batch_size}) "
+                f"needs to be a round multiple of the number of processes ({num_processes})."
+            )
+        self.dataset = dataset
+        self.batch_size = batch_size
+        self.drop_last = drop_last
+        self.num_processes = num_processes
+        self.process_index = process_index
+        self.split_batches = split_batches
+
+    def set_epoch(self, epoch):
+        self.epoch = epoch
+        if hasattr(self.dataset, "set_epoch"):
+            self.dataset.set_epoch(epoch)
+
+    def __len__(self):
+        if self.drop_last:
+            return (len(self.dataset) // (self.batch_size * self.num_processes)) * self.batch_size
+        return math.ceil(len(self.dataset) / (self.batch_size * self.num_processes)) * self.batch_size
+
+    def __iter__(self):
+        if (
+            not hasattr(self.dataset, "set_epoch")
+            and hasattr(self.dataset, "generator")
+            and isinstance(self.dataset.generator, torch.Generator)
+        ):
+            self.dataset.generator.manual_seed(getattr(self, "epoch", 0))
+        global_bs = self.batch_size if self.split_batches else self.batch_size * self.num_processes
+        local_bs = self.batch_size // self.num_processes if self.split_batches else self.batch_size
+        lo, hi = self.process_index * local_bs, (self.process_index + 1) * local_bs
+        first, buf = None, []
+        for element in self.dataset:
+            buf.append(element)
+            if len(buf) == global_bs:
+                yield from buf[lo:hi]
+                if first is None:
+                    first = list(buf)
+                buf = []
+        if not self.drop_last and buf:
+            if first is None:
+                first = list(buf)
+            while len(buf) < global_bs:
+                buf = buf + first
+            yield from buf[lo:hi]
+
+
+class DataLoaderStateMixin:
+    """End-of-dataloader / remainder tracking shared with `GradientState`."""
+
+    def __init_subclass__(cls, **kwargs):
+        cls.end_of_dataloader = False
+        cls.remainder = -1
+
+    def reset(self):
+        self.end_of_dataloader = False
+        self.remainder = -1
+
+    def begin(self):
+        self.reset()
+        with suppress(Exception):
+            if not self._drop_last:
+                length = getattr(self.dataset, "total_dataset_length", len(self.dataset))
+                self.remainder = length % self.total_batch_size
+        self.gradient_state._add_dataloader(self)
+
+    def end(self):
+        self.gradient_state._remove_dataloader(self)
+
+
+class DevicePrefetcher:
+    """Background H2D prefetch of a batch iterator onto a dedicated HIP copy stream.
+
+    A daemon thread pulls CPU batches, pins them, launches non-blocking copies on `copy_stream` and records an
+    event; `__next__` makes the *current* stream wait on that event (no host sync) and marks each tensor as used
+    by the current stream (`record_stream`) so the caching allocator never recycles it early.
+    """
+
+    _SENTINEL = object()
+
+    def __init__(self, iterator, device: torch.device, depth: int = 2):
+        self.iterator = iterator
+        self.device = device
+        self.depth = max(1, depth)
+        self.copy_stream = torch.cuda.Stream(device=device, priority=-1)
+        self.queue: queue.Queue = queue.Queue(maxsize=self.depth)
+        self.error: Optional[BaseException] = None
+        self.thread = threading.Thread(target=self._worker, daemon=True)
+        self.thread.start()
+
+    def _pin(self, batch):
+        def _p(t):
+            return t if t.is_pinned() else t.pin_memory()
+
+        from .utils.operations import recursively_apply
+
+        return recursively_apply(_p, batch)
+
+    def _worker(self):
+        try:
+            torch.cuda.set_device(self.device)
+            for batch in self.iterator:
+                with torch.cuda.stream(self.copy_stream):
+                    try:
+                        staged = send_to_device(self._pin(batch), self.device, non_blocking=True)
+                    except RuntimeError:
+                        staged = send_to_device(batch, self.device, non_blocking=True)
+                    event = torch.cuda.Event()
+                    event.record(self.copy_stream)
+                self.queue.put((staged, event))
+        except BaseException as e:  # surfaced on the consumer thread
+            self.error = e
+        self.queue.put(self._SENTINEL)
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        item = self.queue.get()
+        if item is self._SENTINEL:
+            if self.error is not None:
+                raise self.error
+            raise StopIteration
+        batch, event = item
+        cur = torch.cuda.current_stream(self.device)
+        cur.wait_event(event)
+
+        def _rec(t):
+            if t.is_cuda:
+                t.record_stream(cur)
+            return t
+
+        from .utils.operations import recursively_apply
+
+        return recursively_apply(_rec, batch)
+
+
+class DataLoaderShard(DataLoaderStateMixin, DataLoader):
+    """A DataLoader that yields this process's batches, placed on `device`, with one-batch look-ahead so the
+    last batch is flagged (`end_of_dataloader`) before it is yielded (needed by gradient accumulation)."""
+
+    def __init__(
+        self,
+        dataset,
+        device=None,
+        rng_types=None,
+        synchronized_generator=None,
+        skip_batches=0,
+        use_stateful_dataloader=False,
+        _drop_last: bool = False,
+        _non_blocking: bool = False,
+        torch_device_mesh=None,
+        prefetch_to_device: int = 2,
+        **kwargs,
+    ):
+        super().__init__(dataset, **kwargs)
+        self.device = device
+        self.rng_types = rng_types
+        self.synchronized_generator = synchronized_generator
+        self.skip_batches = skip_batches
+        self.gradient_state = GradientState()
+        self._drop_last = _drop_last
+        self._non_blocking = _non_blocking
+        self.iteration = 0
+        self.prefetch_to_device = prefetch_to_device
+        self._batches_yielded = 0
+        self._resume_skip = 0
+
+    def _device_iter(self, base_iter):
+        dev = self.device
+        if dev is not None and torch.device(dev).type == "cuda" and self.prefetch_to_device > 0:
+            return DevicePrefetcher(base_iter, torch.device(dev), self.prefetch_to_device)
+        if dev is not None:
+            return (send_to_device(b, dev, non_blocking=self._non_blocking) for b in base_iter)
+        return base_iter
+
+    def __iter__(self):
+        if self.rng_types is not None:
+            synchronize_rng_states(self.rng_types, self.synchronized_generator)
+        self.begin()
+        self.set_epoch(self.iteration)
+        skip = self.skip_batches + self._resume_skip
+        self._resume_skip = 0
+        base = super().__iter__()
+        it = self._device_iter(base)
+        try:
+            current = next(it)
+        except StopIteration:
+            self.end()
+            return
+        index = 0
+        self._batches_yielded = 0
+        while True:
+            try:
+                nxt = next(it)
+            except StopIteration:
+                self.end_of_dataloader = True
+                if index >= skip:
+                    self._batches_yielded = index + 1
+                    yield current
+                break
+            if index >= skip:
+                self._batches_yielded = index + 1
+                yield current
+            index += 1
+            current = nxt
+        self.iteration += 1
+        self.end()
+
+    def __reduce__(self):
+        args = super().__reduce__()
+        return (DataLoaderShard, *args[1:])
+
+    def set_epoch(self, epoch: int):
+        if self.iteration != epoch:
+            self.iteration = epoch
+        if hasattr(self.batch_sampler, "sampler") and hasattr(self.batch_sampler.sampler, "set_epoch"):
+            self.batch_sampler.sampler.set_epoch(epoch)
+        elif hasattr(self.batch_sampler, "batch_sampler") and hasattr(
+            getattr(self.batch_sampler.batch_sampler, "sampler", None), "set_epoch"
+        ):
+            self.batch_sampler.batch_sampler.sampler.set_epoch(epoch)
+        elif hasattr(self.dataset, "set_epoch"):
+            self.dataset.set_epoch(epoch)
+
+    @property
+    def total_batch_size(self):
+        batch_sampler = self.sampler if isinstance(self.sampler, BatchSampler) else self.batch_sampler
+        return (
+            batch_sampler.batch_size
+            if getattr(batch_sampler, "split_batches", False)
+            else (batch_sampler.batch_size * getattr(batch_sampler, "num_processes", 1))
+        )
+
+    @property
+    def total_dataset_length(self):
+        if hasattr(self.dataset, "total_length"):
+            return self.dataset.total_length
+        return len(self.dataset)
+
+    def get_sampler(self):
+        return get_sampler(self)
+
+    def set_sampler(self, sampler):
+        sampler_is_batch_sampler = isinstance(self.sampler, BatchSampler)
+        if sampler_is_batch_sampler:
+            self.sampler.sampler = sampler
+        else:
+            self.batch_sampler.sampler = sampler
+            if hasattr(self.batch_sampler, "batch_sampler"):
+                self.batch_sampler.batch_sampler.sampler = sampler
+
+    # Native resumable state (position within the epoch); replaces torchdata's StatefulDataLoader.
+    def state_dict(self):
+        return {"iteration": self.iteration, "batches_yielded": self._batches_yielded}
+
+    def load_state_dict(self, state_dict):
+        self.iteration = state_dict.get("iteration", 0)
+        self._resume_skip = state_dict.get("batches_yielded", 0)
+
+
+class DataLoaderDispatcher(DataLoaderStateMixin, DataLoader):
+    """Rank 0 iterates the underlying loader and broadcasts each (concatenated or split) batch; every rank
+    keeps its slice. One object broadcast (structure) + one coalesced tensor broadcast per step."""
+
+    def __init__(
+        self,
+        dataset,
+        split_batches: bool = False,
+        skip_batches=0,
+        use_stateful_dataloader=False,
+        _drop_last: bool = False,
+        _non_blocking: bool = False,
+        slice_fn=None,
+        torch_device_mesh=None,
+        **kwargs,
+    ):
+        shuffle = False
+        from torch.utils.data.datapipes.iter.combinatorics import ShufflerIterDataPipe
+
+        if isinstance(dataset, ShufflerIterDataPipe):
+            shuffle = dataset._shuffle_enabled
+        super().__init__(dataset, **kwargs)
+        self.split_batches = split_batches
+        if shuffle:
+            torch.utils.data.graph_settings.apply_shuffle_settings(dataset, shuffle=shuffle)
+        self.gradient_state = GradientState()
+        self.state = PartialState()
+        self._drop_last = _drop_last
+        self._non_blocking = _non_blocking
+        self.skip_batches = skip_batches
+        self.torch_device_mesh = torch_device_mesh
+        self.slice_fn = slice_tensors if slice_fn is None else slice_fn
+        self.iteration = 0
+        self._batches_yielded = 0
+
+    def _fetch_batches(self, iterator):
+        batches, batch = None, None
+        if self.state.process_index == 0:
+            try:
+                if self.split_batches:
+                    batch = next(iterator)
+                else:
+                    batches = []
+                    for _ in range(self.state.num_processes):
+                        batches.append(next(iterator))
+                    try:
+                        batch = concatenate(batches, dim=0)
+                    except RuntimeError as e:
+                        raise RuntimeError(
+                            "You can't use batches of different size with `dispatch_batches=True` or when using an "
+                            "`IterableDataset`. Either pass `dispatch_batches=False` and have each process fetch its "
+                            "own batch or pass `split_batches=True`."
+                        ) from e
+                batch_info = [get_data_structure(batch), False]
+            except StopIteration:
+                batch_info = [None, True]
+        else:
+            batch_info = [None, self._stop_iteration]
+        broadcast_object_list(batch_info)
+        self._stop_iteration = batch_info[1]
+        if self._stop_iteration:
+            if not self.split_batches and not self._drop_last:
+                if self.state.process_index == 0 and len(batches) > 0:
+                    batch = concatenate(batches, dim=0)
+                    batch_info = [get_data_structure(batch), False]
+                else:
+                    batch_info = [None, True]
+                broadcast_object_list(batch_info)
+        return batch, batch_info
+
+    def __iter__(self):
+        self.begin()
+        self.set_epoch(self.iteration)
+        main_iterator = None
+        if self.state.process_index == 0:
+            main_iterator = super().__iter__()
+        stop_iteration = False
+        self._stop_iteration = False
+        first_batch = None
+        next_batch, next_batch_info = self._fetch_batches(main_iterator)
+        batch_index = 0
+        while not stop_iteration:
+            batch, batch_info = next_batch, next_batch_info
+            if self.state.process_index != 0:
+                batch = initialize_tensors(batch_info[0])
+            batch = send_to_device(batch, self.state.device, non_blocking=self._non_blocking)
+            batch = broadcast(batch, from_process=0)
+            if not self._drop_last and first_batch is None:
+                first_batch = self.slice_fn(
+                    batch, slice(0, self.state.num_processes), process_index=self.state.process_index, num_processes=self.state.num_processes
+                )
+            if batch is None:
+                raise ValueError(f"Batch does not contain any data ({batch}). At the end of all iterable data available before expected stop iteration.")
+            observed_batch_size = find_batch_size(batch)
+            batch_size = observed_batch_size // self.state.num_processes
+            stop_iteration = self._stop_iteration
+            if not stop_iteration:
+                next_batch, next_batch_info = self._fetch_batches(main_iterator)
+                if self._stop_iteration and next_batch_info[0] is None:
+                    stop_iteration = True
+            if not self._drop_last and stop_iteration and observed_batch_size % self.state.num_processes != 0:
+                batch = concatenate([batch, first_batch], dim=0)
+                batch_size += 1
+            data_slice = slice(self.state.process_index * batch_size, (self.state.process_index + 1) * batch_size)
+            batch = self.slice_fn(batch, data_slice, process_index=self.state.process_index, num_processes=self.state.num_processes)
+            if stop_iteration:
+                self.end_of_dataloader = True
+                self.remainder = observed_batch_size
+            if batch_index >= self.skip_batches:
+                self._batches_yielded = batch_index + 1
+                yield batch
+            batch_index += 1
+        self.iteration += 1
+        self.end()
+
+    def set_epoch(self, epoch: int):
+        if self.iteration != epoch:
+            self.iteration = epoch
+        if hasattr(self.batch_sampler, "sampler") and hasattr(self.batch_sampler.sampler, "set_epoch"):
+            self.batch_sampler.sampler.set_epoch(epoch)
+        elif hasattr(self.dataset, "set_epoch"):
+            self.dataset.set_epoch(epoch)
+
+    def __len__(self):
+        whole_length = super().__len__()
+        if self.split_batches:
+            return whole_length
+        elif self._drop_last:
+            return whole_length // self.state.num_processes
+        return math.ceil(whole_length / self.state.num_processes)
+
+    def __reduce__(self):
+        args = super().__reduce__()
+        return (DataLoaderDispatcher, *args[1:])
+
+    @property
+    def total_batch_size(self):
+        return self.dataset.batch_size if self.split_batches else (self.dataset.batch_size * self.dataset.num_processes)
+
+    @property
+    def total_dataset_length(self):
+        return len(self.dataset)
+
+    def get_sampler(self):
+        return get_sampler(self)
+
+    def set_sampler(self, sampler):
+        sampler_is_batch_sampler = isinstance(self.sampler, BatchSampler)
+        if sampler_is_batch_sampler:
+            self.sampler.sampler = sampler
+        else:
+            self.batch_sampler.sampler = sampler
+            if hasattr(self.batch_sampler, "batch_sampler"):
+                self.batch_sampler.batch_sampler.sampler = sampler
+
+    def state_dict(self):
+        return {"iteration": self.iteration, "batches_yielded": self._batches_yielded}
+
+    def load_state_dict(self, state_dict):
+        self.iteration = state_dict.get("iteration", 0)
+        self.skip_batches = state_dict.get("batches_yielded", 0)
+
+
+def get_sampler(dataloader):
+    """The sampler of a dataloader, looking through a BatchSampler used as sampler."""
+    sampler_is_batch_sampler = isinstance(dataloader.sampler, BatchSampler)
+    if sampler_is_batch_sampler:
+        sampler = getattr(dataloader.sampler, "sampler", None)
+    else:
+        sampler = getattr(dataloader.batch_sampler, "sampler", None)
+    return sampler
+
+
+def prepare_data_loader(
+    dataloader: DataLoader,
+    device: Optional[torch.device] = None,
+    num_processes: Optional[int] = None,
+    process_index: Optional[int] = None,
+    split_batches: bool = False,
+    put_on_device: bool = False,
+    rng_types: Optional[list[Union[str, RNGType]]] = None,
+    dispatch_batches: Optional[bool] = None,
+    even_batches: bool = True,
+    slice_fn_for_dispatch: Optional[Callable] = None,
+    use_seedable_sampler: bool = False,
+    data_seed: Optional[int] = None,
+    non_blocking: bool = False,
+    use_stateful_dataloader: bool = False,
+    torch_device_mesh=None,
+    prefetch_to_device: int = 2,
+) -> DataLoader:
+    """Rebuild `dataloader` so it yields only this process's share (reference `data_loader.py:996-1309`)."""
+    if dispatch_batches is None:
+        dispatch_batches = False if not put_on_device else isinstance(dataloader.dataset, IterableDataset)
+    if dispatch_batches and not put_on_device:
+        raise ValueError("Using `dispatch_batches=True` requires `put_on_device=True`.")
+    state = PartialState()
+    if num_processes is None:
+        num_processes = state.num_processes
+    if process_index is None:
+        process_index = state.process_index
+
+    # With a device mesh, ranks that share a TP/CP/SP group must see the same data: remap to data-parallel
+    # coordinates (reference `data_loader.py:1109-1145`).
+    if torch_device_mesh is not None:
+        dp_size, dp_rank = torch_device_mesh.data_parallel_size_and_rank()
+        num_processes, process_index = dp_size, dp_rank
+
+    if split_batches:
+        if dataloader.batch_size is not None:
+            batch_size_for_check = dataloader.batch_size
+        else:
+            batch_size_for_check = getattr(dataloader.batch_sampler, "batch_size", None)
+        if batch_size_for_check is not None and batch_size_for_check > 1 and batch_size_for_check % num_processes != 0:
+            raise ValueError(
+                f"To use a `DataLoader` in `split_batches` mode, the batch size ({dataloader.batch_size}) "
+                f"needs to be a round multiple of the number of processes ({num_processes})."
+            )
+
+    new_dataset = dataloader.dataset
+    new_batch_sampler = dataloader.batch_sampler if not isinstance(new_dataset, IterableDataset) else None
+    sampler_is_batch_sampler = isinstance(dataloader.sampler, BatchSampler)
+    synchronized_generator = None
+
+    sampler = get_sampler(dataloader)
+    if isinstance(sampler, RandomSampler) and use_seedable_sampler:
+        sampler = SeedableRandomSampler(
+            data_source=sampler.data_source,
+            replacement=sampler.replacement,
+            num_samples=sampler._num_samples,
+            generator=getattr(sampler, "generator", None) or torch.Generator(),
+            data_seed=data_seed,
+        )
+
+    if num_processes != 1 and not dispatch_batches:
+        if isinstance(new_dataset, IterableDataset):
+            if getattr(dataloader.dataset, "generator", None) is not None:
+                synchronized_generator = dataloader.dataset.generator
+            new_dataset = IterableDatasetShard(
+                new_dataset,
+                batch_size=dataloader.batch_size,
+                drop_last=dataloader.drop_last,
+                num_processes=num_processes,
+                process_index=process_index,
+                split_batches=split_batches,
+            )
+        else:
+            if not use_seedable_sampler and hasattr(sampler, "generator"):
+                if sampler.generator is None:
+                    sampler.generator = torch.Generator()
+                    seed = int(torch.empty((), dtype=torch.int64).random_().item())
+                    sampler.generator.manual_seed(seed)
+                synchronized_generator = sampler.generator
+            batch_sampler = dataloader.sampler if sampler_is_batch_sampler else dataloader.batch_sampler
+            new_batch_sampler = BatchSamplerShard(
+                batch_sampler,
+                num_processes=num_processes,
+                process_index=process_index,
+                split_batches=split_batches,
+                even_batches=even_batches,
+            )
+
+    ignore_kwargs = ["batch_size", "shuffle", "sampler", "batch_sampler", "drop_last"]
+    if rng_types is not None and synchronized_generator is None and "generator" in rng_types:
+        rng_types = [r for r in rng_types if r != "generator"]
+    kwargs = {
+        k: getattr(dataloader, k, _PYTORCH_DATALOADER_KWARGS[k])
+        for k in _PYTORCH_DATALOADER_KWARGS
+        if k not in ignore_kwargs and hasattr(dataloader, k)
+    }
+    if new_batch_sampler is None:
+        kwargs["drop_last"] = dataloader.drop_last
+        kwargs["batch_size"] = (
+            dataloader.batch_size // num_processes if split_batches and not dispatch_batches else dataloader.batch_size
+        )
+    if dispatch_batches:
+        kwargs.pop("generator", None)
+        dataloader = DataLoaderDispatcher(
+            new_dataset,
+            split_batches=split_batches,
+            batch_sampler=new_batch_sampler,
+            _drop_last=dataloader.drop_last,
+            _non_blocking=non_blocking,
+            slice_fn=slice_fn_for_dispatch,
+            torch_device_mesh=torch_device_mesh,
+            **kwargs,
+        )
+    elif sampler_is_batch_sampler:
+        dataloader = DataLoaderShard(
+            new_dataset,
+            device=device if put_on_device else None,
+            sampler=new_batch_sampler,
+            batch_size=dataloader.batch_size,
+            rng_types=rng_types,
+            _drop_last=dataloader.drop_last,
+            _non_blocking=non_blocking,
+            synchronized_generator=synchronized_generator,
+            prefetch_to_device=prefetch_to_device,
+            **kwargs,
+        )
+    else:
+        dataloader = DataLoaderShard(
+            new_dataset,
+            device=device if put_on_device else None,
+            batch_sampler=new_batch_sampler,
+            rng_types=rng_types,
+            synchronized_generator=synchronized_generator,
+            _drop_last=dataloader.drop_last,
+            _non_blocking=non_blocking,
+            prefetch_to_device=prefetch_to_device,
+            **kwargs,
+        )
+    if isinstance(sampler, SeedableRandomSampler) and use_seedable_sampler:
+        dataloader.set_sampler(sampler)
+    return dataloader
+
+
+class SkipBatchSampler(BatchSampler):
+    """Skip the first `skip_batches` batches of a batch sampler."""
+
+    def __init__(self, batch_sampler, skip_batches=0):
+        self.batch_sampler = batch_sampler
+        self.skip_batches = skip_batches
+
+    def __iter__(self):
+        for index, samples in enumerate(self.batch_sampler):
+            if index >= self.skip_batches:
+                yield samples
+
+    @property
+    def total_length(self):
+        return len(self.batch_sampler)
+
+    def __len__(self):
+        return len(self.batch_sampler) - self.skip_batches
+
+
+class SkipDataLoader(DataLoaderStateMixin, DataLoader):
+    """A plain DataLoader that skips its first `skip_batches` batches."""
+
+    def __init__(self, dataset, skip_batches=0, use_stateful_dataloader=False, **kwargs):
+        super().__init__(dataset, **kwargs)
+        self.skip_batches = skip_batches
+        self.gradient_state = GradientState()
+        self._drop_last = kwargs.get("drop_last", False)
+
+    def __iter__(self):
+        self.begin()
+        for index, batch in enumerate(super().__iter__()):
+            if index >= self.skip_batches:
+                yield batch
+        self.end()
+
+    def __len__(self):
+        return super().__len__() - self.skip_batches
+
+    @property
+    def total_batch_size(self):
+        return self.batch_size or 1
+
+
+def skip_first_batches(dataloader, num_batches=0):
+    """A dataloader equivalent to `dataloader` that skips its first `num_batches` batches (resume mid-epoch)."""
+    state = PartialState()
+    dataset = dataloader.dataset
+    sampler_is_batch_sampler = False
+    if isinstance(dataset, IterableDataset):
+        new_batch_sampler = None
+    else:
+        sampler_is_batch_sampler = isinstance(dataloader.sampler, BatchSampler)
+        batch_sampler = dataloader.sampler if sampler_is_batch_sampler else dataloader.batch_sampler
+        new_batch_sampler = SkipBatchSampler(batch_sampler, skip_batches=num_batches)
+
+    ignore_kwargs = ["batch_size", "shuffle", "sampler", "batch_sampler", "drop_last"]
+    kwargs = {
+        k: getattr(dataloader, k, _PYTORCH_DATALOADER_KWARGS[k])
+        for k in _PYTORCH_DATALOADER_KWARGS
+        if k not in ignore_kwargs and hasattr(dataloader, k)
+    }
+    if new_batch_sampler is None:
+        kwargs["drop_last"] = dataloader.drop_last
+        kwargs["batch_size"] = dataloader.batch_size
+
+    if isinstance(dataloader, DataLoaderDispatcher):
+        if new_batch_sampler is None:
+            kwargs["skip_batches"] = num_batches
+        kwargs.pop("generator", None)
+        dataloader = DataLoaderDispatcher(
+            dataset,
+            split_batches=dataloader.split_batches,
+            batch_sampler=new_batch_sampler,
+            _drop_last=dataloader._drop_last,
+            **kwargs,
+        )
+    elif isinstance(dataloader, DataLoaderShard):
+        if new_batch_sampler is None:
+            kwargs["skip_batches"] = num_batches
+        elif sampler_is_batch_sampler:
+            kwargs["sampler"] = new_batch_sampler
+            kwargs["batch_size"] = dataloader.batch_size
+        else:
+            kwargs["batch_sampler"] = new_batch_sampler
+        dataloader = DataLoaderShard(
+            dataset,
+            device=dataloader.device,
+            rng_types=dataloader.rng_types,
+            synchronized_generator=dataloader.synchronized_generator,
+            _drop_last=dataloader._drop_last,
+            prefetch_to_device=dataloader.prefetch_to_device,
+            **kwargs,
+        )
+    else:
+        if new_batch_sampler is None:
+            dataloader = SkipDataLoader(dataset, skip_batches=num_batches, **kwargs)
+        else:
+            dataloader = DataLoader(dataset, batch_sampler=new_batch_sampler, **kwargs)
+    _ = state
+    return dataloader

@@ -1,0 +1,223 @@
+"""fp8 training on MI355X: per-tensor scaling, OCP e4m3/e5m2 casts and MX-MFMA GEMMs (csrc/kernels/fp8.hip).
+
+Parity: the reference delegates fp8 to torchao `Float8Linear` (`/root/reference/src/accelerate/utils/ao.py:32-143`,
+`accelerator.py:2042-2068`) or TransformerEngine (`utils/transformer_engine.py`). Here `Fp8Linear` implements both
+recipes with our kernels:
+
+* dynamic scaling (torchao-style, `AORecipeKwargs`): scale = fp8_max / amax of the current tensor;
+* delayed scaling (TE-style, `TERecipeKwargs`): scale from the max of an amax history ring buffer kept on the device
+  (length `amax_history_len`), `margin` applied as 2^-margin; format "HYBRID" = e4m3 forward, e5m2 gradients.
+
+Forward  y  = (x8 · w8ᵀ) / (sx·sw)                      — fp8 GEMM, bf16 out
+Backward dx = (dy8 · w8ᵀᵀ) / (sg·sw),  dW = (dy8ᵀ · x8ᵀᵀ) / (sg·sx) — the cast kernel writes the transposed copies
+so every GEMM reads K-contiguous operands. Everything stays on the device (no host syncs).
+
+The module filter follows the reference: first and last `nn.Linear` are skipped and both dims must be divisible by 16
+(`filter_first_and_last_linear_layers`, `filter_linear_layers`).
+"""
+
+from __future__ import annotations
+
+from typing import Callable, Optional
+
+import torch
+import torch.nn as nn
+
+from ._ext import ext, use_native
+
+E4M3_MAX = 448.0
+E5M2_MAX = 57344.0
+
+
+def amax(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """abs-max of a bf16 tensor as fp32 [1] (device)."""
+    if use_native(x) and x.dtype == torch.bfloat16:
+        return ext().fp8_amax(x.contiguous(), out)
+    r = x.detach().abs().max().float().reshape(1)
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r
+
+
+def scale_from_amax(a: torch.Tensor, fp8_max: float, margin: int = 0) -> torch.Tensor:
+    return (fp8_max / (2.0**margin)) / a.clamp_min(1e-12)
+
+
+def cast(x: torch.Tensor, scale: torch.Tensor, e5m2: bool = False, transpose: bool = False):
+    """sat(x * scale) → fp8 (and its transpose when `transpose`)."""
+    if use_native(x) and x.dtype == torch.bfloat16 and x.dim() == 2:
+        outs = ext().fp8_cast(x.contiguous(), scale, e5m2, transpose)
+        return (outs[0], outs[1]) if transpose else outs[0]
+    mx = E5M2_MAX if e5m2 else E4M3_MAX
+    dt = torch.float8_e5m2 if e5m2 else torch.float8_e4m3fn
+    y = (x.float() * scale).clamp(-mx, mx).to(dt)
+    if transpose:
+        return y, y.t().contiguous()
+    return y
+
+
+def gemm(a8: torch.Tensor, b8: torch.Tensor, a_scale_inv: torch.Tensor, b_scale_inv: torch.Tensor, bias=None, out_dtype=torch.bfloat16):
+    """C = (a8 · b8ᵀ) · a_scale_inv · b_scale_inv (+ bias); a8 [M,K], b8 [N,K]."""
+    if a8.is_cuda and use_native(a8):
+        e5a = a8.dtype == torch.float8_e5m2
+        e5b = b8.dtype == torch.float8_e5m2
+        return ext().fp8_gemm(a8, b8, a_scale_inv, b_scale_inv, e5a, e5b, bias, out_dtype == torch.float32)
+    out = (a8.float() @ b8.float().t()) * a_scale_inv * b_scale_inv
+    if bias is not None:
+        out = out + bias.float()
+    return out.to(out_dtype)
+
+
+def _gemm_ok(M, N, K):
+    return M % 128 == 0 and N % 128 == 0 and K % 64 == 0
+
+
+class Fp8Recipe:
+    """Runtime scaling state of one Fp8Linear."""
+
+    def __init__(self, delayed: bool = False, history_len: int = 16, margin: int = 0, fmt: str = "HYBRID", algo: str = "max"):
+        self.delayed = delayed
+        self.history_len = history_len
+        self.margin = margin
+        self.fmt = fmt.upper()
+        self.algo = algo
+        self.hist = {}
+
+    def grad_e5m2(self):
+        return self.fmt in ("HYBRID", "E5M2")
+
+    def fwd_e5m2(self):
+        return self.fmt == "E5M2"
+
+    def scale(self, key: str, x: torch.Tensor, fp8_max: float) -> torch.Tensor:
+        cur = amax(x)
+        if not self.delayed:
+            return scale_from_amax(cur, fp8_max, self.margin)
+        h = self.hist.get(key)
+        if h is None:
+            h = cur.repeat(self.history_len).clone()
+            self.hist[key] = h
+        past = h.max().reshape(1) if self.algo == "max" else h[-1:].clone()
+        s = scale_from_amax(past, fp8_max, self.margin)
+        self.hist[key] = torch.cat([h[1:], cur])
+        return s
+
+
+class _Fp8LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, bias, recipe: Fp8Recipe):
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1])
+        M, K = x2.shape
+        N = w.shape[0]
+        fwd_max = E5M2_MAX if recipe.fwd_e5m2() else E4M3_MAX
+        sx = recipe.scale("x", x2, fwd_max)
+        sw = recipe.scale("w", w, fwd_max)
+        x8, x8t = cast(x2, sx, recipe.fwd_e5m2(), transpose=True)
+        w8, w8t = cast(w, sw, recipe.fwd_e5m2(), transpose=True)
+        y = gemm(x8, w8, 1.0 / sx, 1.0 / sw, bias, torch.bfloat16)
+        ctx.save_for_backward(x8t, w8t, sx, sw)
+        ctx.recipe = recipe
+        ctx.shape = shape
+        ctx.has_bias = bias is not None
+        return y.view(*shape[:-1], N)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x8t, w8t, sx, sw = ctx.saved_tensors
+        recipe = ctx.recipe
+        N = dy.shape[-1]
+        dy2 = dy.reshape(-1, N).contiguous().to(torch.bfloat16)
+        gmax = E5M2_MAX if recipe.grad_e5m2() else E4M3_MAX
+        sg = recipe.scale("g", dy2, gmax)
+        dy8, dy8t = cast(dy2, sg, recipe.grad_e5m2(), transpose=True)
+        dx = gemm(dy8, w8t, 1.0 / sg, 1.0 / sw, None, torch.bfloat16)
+        dw = gemm(dy8t, x8t, 1.0 / sg, 1.0 / sx, None, torch.bfloat16)
+        db = dy2.float().sum(0).to(dy.dtype) if ctx.has_bias else None
+        return dx.view(ctx.shape), dw, db, None
+
+
+class Fp8Linear(nn.Linear):
+    """`nn.Linear` whose matmuls run in fp8 (same parameters, so FSDP / state dicts are unaffected)."""
+
+    fp8_recipe: Fp8Recipe = None
+
+    def forward(self, x):
+        M = x.numel() // x.shape[-1]
+        if (
+            not self.training
+            and not getattr(self, "fp8_in_eval", True)
+        ) or not _gemm_ok(M, self.out_features, self.in_features) or x.dtype != torch.bfloat16:
+            return nn.functional.linear(x, self.weight.to(x.dtype), None if self.bias is None else self.bias.to(x.dtype))
+        w = self.weight if self.weight.dtype == torch.bfloat16 else self.weight.to(torch.bfloat16)
+        b = None if self.bias is None else self.bias.to(torch.bfloat16)
+        return _Fp8LinearFn.apply(x, w, b, self.fp8_recipe)
+
+
+def filter_linear_layers(module: nn.Module, fqn: str, layers_to_filter: list[str]) -> bool:
+    """Keep linears whose dims are divisible by 16 and whose name is not filtered (reference ao.py:55-82)."""
+    if isinstance(module, nn.Linear):
+        if module.in_features % 16 != 0 or module.out_features % 16 != 0:
+            return False
+    if fqn in layers_to_filter:
+        return False
+    return True
+
+
+def find_first_last_linear_layers(model: nn.Module):
+    first, last = None, None
+    for name, m in model.named_modules():
+        if isinstance(m, nn.Linear):
+            if first is None:
+                first = name
+            last = name
+    return first, last
+
+
+def filter_first_and_last_linear_layers(module: nn.Module, fqn: str) -> bool:
+    return True
+
+
+def convert_model_to_fp8(model: nn.Module, recipe=None, backend: str = "AO", module_filter_func: Optional[Callable] = None):
+    """Swap eligible `nn.Linear` modules for `Fp8Linear` in place."""
+    from ..utils.dataclasses import TERecipeKwargs
+
+    delayed = isinstance(recipe, TERecipeKwargs) or backend == "TE"
+    kwargs = {}
+    if delayed and recipe is not None:
+        kwargs = dict(delayed=True, history_len=max(1, min(int(recipe.amax_history_len), 1024)), margin=int(recipe.margin), fmt=recipe.fp8_format, algo=recipe.amax_compute_algo)
+    else:
+        kwargs = dict(delayed=False, fmt="HYBRID")
+    if module_filter_func is None and recipe is not None:
+        module_filter_func = getattr(recipe, "module_filter_func", None)
+    first, last = find_first_last_linear_layers(model)
+    skip = {first, last}
+    n = 0
+    for name, m in list(model.named_modules()):
+        if type(m) is not nn.Linear:
+            continue
+        if name in skip:
+            continue
+        if not filter_linear_layers(m, name, []):
+            continue
+        if module_filter_func is not None and not module_filter_func(m, name):
+            continue
+        m.__class__ = Fp8Linear
+        m.fp8_recipe = Fp8Recipe(**kwargs)
+        if delayed and recipe is not None:
+            m.fp8_in_eval = bool(recipe.use_autocast_during_eval)
+        n += 1
+    model._acc_fp8_linears = n
+    return model
+
+
+def has_fp8_layers(model: nn.Module) -> bool:
+    return any(isinstance(m, Fp8Linear) for m in model.modules())
+
+
+def fp8_linear_reference_check(a: torch.Tensor, b: torch.Tensor):
+    """Quantise a [M,K] and b [N,K] with dynamic per-tensor scaling and multiply in fp8 (test helper)."""
+    sa = scale_from_amax(amax(a), E4M3_MAX)
+    sb = scale_from_amax(amax(b), E4M3_MAX)
+    return gemm(cast(a, sa), cast(b, sb), 1.0 / sa, 1.0 / sb, None, torch.float32)

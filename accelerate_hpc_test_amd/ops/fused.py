@@ -1,0 +1,280 @@
+"""Autograd wrappers for the fused transformer-block kernels (RMSNorm, SwiGLU, RoPE, cross-entropy, flash
+attention). GPU tensors run the HIP kernels in `csrc/kernels/*.hip`; CPU tensors run a PyTorch fp32 reference of
+the same op (the reference is also the numerics oracle in tests/test_kernels_gpu.py).
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+from ._ext import ext, use_native
+
+
+# ----------------------------------------------------------------------------------------------------------
+# RMSNorm (optionally fused with the residual add)
+# ----------------------------------------------------------------------------------------------------------
+def rms_norm_reference(x, weight, eps, residual=None):
+    if residual is not None:
+        x = (x.float() + residual.float()).to(x.dtype)
+    xf = x.float()
+    y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * weight.float()
+    return y.to(x.dtype), x
+
+
+class _RMSNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, eps, residual):
+        e = ext()
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1]).contiguous()
+        r2 = residual.reshape(-1, shape[-1]).contiguous() if residual is not None else None
+        y, rstd, res_out = e.rmsnorm_fwd(x2, r2, weight.contiguous(), eps)
+        normed_input = res_out if residual is not None else x2
+        ctx.save_for_backward(normed_input, weight, rstd)
+        ctx.has_res = residual is not None
+        ctx.shape = shape
+        if residual is not None:
+            return y.view(shape), res_out.view(shape)
+        return y.view(shape), None
+
+    @staticmethod
+    def backward(ctx, dy, dres):
+        x, w, rstd = ctx.saved_tensors
+        e = ext()
+        H = ctx.shape[-1]
+        d2 = dres.reshape(-1, H).contiguous() if (dres is not None and ctx.has_res) else None
+        dx, dw = e.rmsnorm_bwd(dy.reshape(-1, H).contiguous(), x, w.contiguous(), rstd, d2)
+        dx = dx.view(ctx.shape)
+        # d(x + residual) flows to both summands.
+        return dx, dw, None, (dx if ctx.has_res else None)
+
+
+def rms_norm(x: torch.Tensor, weight: torch.Tensor, eps: float = 1e-6, residual: Optional[torch.Tensor] = None):
+    """y = RMSNorm(x [+ residual]) * weight. Returns (y, residual_out) where residual_out = x + residual (or x)."""
+    if use_native(x) and x.dtype == torch.bfloat16 and x.shape[-1] % 8 == 0:
+        y, r = _RMSNormFn.apply(x, weight, eps, residual)
+        return y, (r if residual is not None else x)
+    return rms_norm_reference(x, weight, eps, residual)
+
+
+# ----------------------------------------------------------------------------------------------------------
+# SwiGLU on a fused [..., 2F] gate|up projection
+# ----------------------------------------------------------------------------------------------------------
+def swiglu_reference(gu):
+    g, u = gu.float().chunk(2, dim=-1)
+    return (torch.nn.functional.silu(g) * u).to(gu.dtype)
+
+
+class _SwiGLUFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gu):
+        gu = gu.contiguous()
+        ctx.save_for_backward(gu)
+        return ext().swiglu_fwd(gu)
+
+    @staticmethod
+    def backward(ctx, dh):
+        (gu,) = ctx.saved_tensors
+        return ext().swiglu_bwd(gu, dh.contiguous())
+
+
+def swiglu(gu: torch.Tensor) -> torch.Tensor:
+    if use_native(gu) and gu.dtype == torch.bfloat16 and (gu.shape[-1] // 2) % 8 == 0:
+        return _SwiGLUFn.apply(gu)
+    return swiglu_reference(gu)
+
+
+# ----------------------------------------------------------------------------------------------------------
+# Rotary embeddings (rotate-half convention, as Llama) applied to the Q and K heads of a fused QKV tensor
+# ----------------------------------------------------------------------------------------------------------
+def rope_tables(seq_len: int, head_dim: int, theta: float = 500000.0, device=None, scaling: Optional[dict] = None):
+    """fp32 cos/sin tables [S, D/2]. `scaling` supports Llama-3.1 style frequency scaling."""
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64, device="cpu") / head_dim))
+    if scaling is not None and scaling.get("rope_type", scaling.get("type")) == "llama3":
+        factor = scaling["factor"]
+        low, high = scaling["low_freq_factor"], scaling["high_freq_factor"]
+        old = scaling["original_max_position_embeddings"]
+        low_wl, high_wl = old / low, old / high
+        wl = 2 * math.pi / inv
+        smooth = (old / wl - low) / (high - low)
+        scaled = torch.where(wl > low_wl, inv / factor, inv)
+        mid = (1 - smooth) * scaled / factor + smooth * scaled
+        is_mid = (wl <= low_wl) & (wl >= high_wl)
+        inv = torch.where(is_mid, mid, scaled)
+    t = torch.arange(seq_len, dtype=torch.float64)
+    f = torch.outer(t, inv)
+    return f.cos().float().to(device), f.sin().float().to(device)
+
+
+def rope_reference(qkv, cos, sin, n_rot_heads, positions=None):
+    """qkv [..., T, Htot, D] (token-major). Rotates heads [0, n_rot_heads)."""
+    T = qkv.shape[-3]
+    D = qkv.shape[-1]
+    if positions is None:
+        c, s = cos[:T], sin[:T]
+    else:
+        c, s = cos[positions.reshape(-1)], sin[positions.reshape(-1)]
+        c = c.view(*positions.shape, D // 2)
+        s = s.view(*positions.shape, D // 2)
+    c = torch.cat([c, c], dim=-1).unsqueeze(-2)
+    s = torch.cat([s, s], dim=-1).unsqueeze(-2)
+    x = qkv[..., :n_rot_heads, :].float()
+    x1, x2 = x[..., : D // 2], x[..., D // 2 :]
+    rot = torch.cat([-x2, x1], dim=-1)
+    out = x * c + rot * s
+    return torch.cat([out.to(qkv.dtype), qkv[..., n_rot_heads:, :]], dim=-2)
+
+
+class _RopeFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, n_rot_heads, positions):
+        qkv = qkv.contiguous().clone()
+        B, S, Htot, D = qkv.shape
+        pos = positions.reshape(-1).contiguous() if positions is not None else None
+        ext().rope_inplace(qkv, cos, sin, pos, n_rot_heads, Htot, D, 1.0)
+        ctx.save_for_backward(cos, sin, pos if pos is not None else torch.empty(0))
+        ctx.meta = (n_rot_heads, Htot, D, pos is not None)
+        return qkv
+
+    @staticmethod
+    def backward(ctx, g):
+        cos, sin, pos = ctx.saved_tensors
+        n_rot, Htot, D, has_pos = ctx.meta
+        g = g.contiguous().clone()
+        ext().rope_inplace(g, cos, sin, pos if has_pos else None, n_rot, Htot, D, -1.0)
+        return g, None, None, None, None
+
+
+def apply_rope(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, n_rot_heads: int, positions=None):
+    """qkv: [B, S, Htot, D]; rotates the first `n_rot_heads` heads (Q heads then K heads)."""
+    if use_native(qkv) and qkv.dtype == torch.bfloat16 and qkv.shape[-1] % 8 == 0:
+        return _RopeFn.apply(qkv, cos, sin, n_rot_heads, positions)
+    return rope_reference(qkv, cos, sin, n_rot_heads, positions)
+
+
+# ----------------------------------------------------------------------------------------------------------
+# Flash attention on a fused QKV tensor
+# ----------------------------------------------------------------------------------------------------------
+def attention_reference(q, k, v, causal=True, scale=None):
+    """q [B,S,Hq,D], k/v [B,S,Hkv,D] → O [B,S,Hq,D] in fp32 math (GQA by head repetition)."""
+    B, S, Hq, D = q.shape
+    Hkv = k.shape[2]
+    rep = Hq // Hkv
+    qf = q.float().transpose(1, 2)
+    kf = k.float().transpose(1, 2).repeat_interleave(rep, dim=1)
+    vf = v.float().transpose(1, 2).repeat_interleave(rep, dim=1)
+    o = torch.nn.functional.scaled_dot_product_attention(qf, kf, vf, is_causal=causal, scale=scale)
+    return o.transpose(1, 2).to(q.dtype)
+
+
+class _FlashAttnQKVFn(torch.autograd.Function):
+    """Attention reading Q/K/V in place from a fused [B, S, Hq+2Hkv, D] activation; the gradient is produced as
+    one fused dQKV tensor (what the QKV projection's backward consumes)."""
+
+    @staticmethod
+    def forward(ctx, qkv, n_q, n_kv, causal, scale):
+        q = qkv[:, :, :n_q]
+        k = qkv[:, :, n_q : n_q + n_kv]
+        v = qkv[:, :, n_q + n_kv :]
+        o, lse = ext().flash_attn_fwd(q, k, v, scale, causal)
+        ctx.save_for_backward(qkv, o, lse)
+        ctx.meta = (n_q, n_kv, causal, scale)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, o, lse = ctx.saved_tensors
+        n_q, n_kv, causal, scale = ctx.meta
+        dqkv = torch.empty_like(qkv)
+        ext().flash_attn_bwd(
+            do.contiguous(),
+            qkv[:, :, :n_q],
+            qkv[:, :, n_q : n_q + n_kv],
+            qkv[:, :, n_q + n_kv :],
+            o,
+            lse,
+            dqkv[:, :, :n_q],
+            dqkv[:, :, n_q : n_q + n_kv],
+            dqkv[:, :, n_q + n_kv :],
+            scale,
+            causal,
+        )
+        return dqkv, None, None, None, None
+
+
+def flash_attention_qkv(qkv: torch.Tensor, n_q: int, n_kv: int, causal: bool = True, scale: Optional[float] = None):
+    """qkv [B, S, n_q + 2 n_kv, D] → O [B, S, n_q, D]."""
+    D = qkv.shape[-1]
+    if scale is None:
+        scale = 1.0 / math.sqrt(D)
+    if use_native(qkv):
+        if qkv.dtype != torch.bfloat16 or D != 128 or qkv.shape[1] % 128 != 0:
+            raise ValueError(
+                f"HIP flash attention needs bf16, head_dim 128 and seq_len % 128 == 0 (got {qkv.dtype}, D={D}, S={qkv.shape[1]})"
+            )
+        return _FlashAttnQKVFn.apply(qkv, n_q, n_kv, causal, scale)
+    q = qkv[:, :, :n_q]
+    k = qkv[:, :, n_q : n_q + n_kv]
+    v = qkv[:, :, n_q + n_kv :]
+    return attention_reference(q, k, v, causal=causal, scale=scale)
+
+
+def flash_attn_with_lse(q, k, v, causal=True, scale=None):
+    """Forward-only attention returning (O, LSE[B,Hq,S]) — used by ring attention's merge."""
+    D = q.shape[-1]
+    if scale is None:
+        scale = 1.0 / math.sqrt(D)
+    if use_native(q):
+        return ext().flash_attn_fwd(q, k, v, scale, causal)
+    B, S, Hq, _ = q.shape
+    rep = Hq // k.shape[2]
+    qf = q.float().transpose(1, 2)
+    kf = k.float().transpose(1, 2).repeat_interleave(rep, dim=1)
+    vf = v.float().transpose(1, 2).repeat_interleave(rep, dim=1)
+    s = torch.matmul(qf, kf.transpose(-1, -2)) * scale
+    if causal:
+        mask = torch.ones(S, k.shape[1], dtype=torch.bool, device=q.device).triu(1)
+        s = s.masked_fill(mask, float("-inf"))
+    lse = torch.logsumexp(s, dim=-1)
+    o = torch.matmul(torch.softmax(s, dim=-1), vf)
+    return o.transpose(1, 2).to(q.dtype), lse
+
+
+# ----------------------------------------------------------------------------------------------------------
+# Cross entropy (mean over non-ignored targets), gradient written in place over the logits
+# ----------------------------------------------------------------------------------------------------------
+class _CrossEntropyFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, ignore_index, inplace_backward):
+        V = logits.shape[-1]
+        l2 = logits.reshape(-1, V)
+        if not l2.is_contiguous():
+            l2 = l2.contiguous()
+        lab = labels.reshape(-1).contiguous()
+        row_loss, lse = ext().xent_fwd(l2, lab, ignore_index)
+        n_valid = (lab != ignore_index).sum().clamp_min(1).float()
+        ctx.save_for_backward(l2, lab, lse, n_valid)
+        ctx.meta = (ignore_index, inplace_backward, logits.shape)
+        return row_loss.sum() / n_valid
+
+    @staticmethod
+    def backward(ctx, g):
+        l2, lab, lse, n_valid = ctx.saved_tensors
+        ignore_index, inplace, shape = ctx.meta
+        scale = (g.float() / n_valid).reshape(1).contiguous()
+        out = l2 if inplace else torch.empty_like(l2)
+        ext().xent_bwd(l2, lab, lse, scale, out, ignore_index)
+        return out.view(shape), None, None, None
+
+
+def cross_entropy(logits: torch.Tensor, labels: torch.Tensor, ignore_index: int = -100, inplace_backward: bool = True):
+    """Mean token cross-entropy. With `inplace_backward`, the logits buffer is overwritten by its gradient
+    during backward (saves one logits-sized allocation: 2 GB for Llama-3 at 8k tokens)."""
+    if use_native(logits) and logits.dtype == torch.bfloat16:
+        return _CrossEntropyFn.apply(logits, labels, ignore_index, inplace_backward)
+    return torch.nn.functional.cross_entropy(
+        logits.reshape(-1, logits.shape[-1]).float(), labels.reshape(-1), ignore_index=ignore_index
+    )

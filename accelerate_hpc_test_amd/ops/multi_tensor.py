@@ -1,0 +1,202 @@
+"""Multi-tensor HIP kernels: fused Adam/AdamW, global L2 gradient norm and device-side clipping.
+
+One kernel launch covers a whole list of tensors: the host packs (pointer, numel) metadata once, uploads it with
+one small copy, and the kernel maps each workgroup to a (tensor, 8192-element chunk). The metadata is cached per
+tensor-list identity, so steady-state steps cost one launch per parameter group.
+
+`FusedAdamStep` executes `torch.optim.AdamW` / `torch.optim.Adam` semantics on the optimizer's own param groups
+and state (`step`, `exp_avg`, `exp_avg_sq` kept in torch's format, so checkpoints are interchangeable).
+Parity target: the optimizer step the reference delegates to torch (`/root/reference/src/accelerate/optimizer.py:145-181`).
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Iterable, Optional
+
+import torch
+
+from ._ext import ext, use_native
+
+_DT = {torch.float32: 0, torch.bfloat16: 1}
+
+
+class _MetaCache:
+    def __init__(self):
+        self._cache = {}
+
+    def get(self, rows: list[tuple[int, ...]], device):
+        key = (tuple(rows), str(device))
+        hit = self._cache.get(key)
+        if hit is not None:
+            return hit
+        chunk = ext().multi_tensor_chunk()
+        meta = torch.tensor(rows, dtype=torch.int64) if rows else torch.zeros((0, 6), dtype=torch.int64)
+        nblocks = [(r[5] + chunk - 1) // chunk for r in rows]
+        prefix = [0]
+        for n in nblocks:
+            prefix.append(prefix[-1] + n)
+        entry = (
+            meta.to(device, non_blocking=False),
+            torch.tensor(prefix, dtype=torch.int64).to(device),
+            prefix[-1],
+        )
+        if len(self._cache) > 64:
+            self._cache.clear()
+        self._cache[key] = entry
+        return entry
+
+
+_CACHE = _MetaCache()
+
+
+def _merge_contiguous(rows):
+    """Merge rows whose p/g/m/v/shadow ranges are adjacent in memory (per-parameter views of one flat FSDP shard
+    become a single range → aligned vector access, fewer chunk boundaries)."""
+    if not rows:
+        return rows
+    out = [list(rows[0])]
+    for r in rows[1:]:
+        prev = out[-1]
+        n = prev[5]
+        ok = True
+        for idx, esz in ((0, r[6]), (1, r[7]), (2, r[8]), (3, r[8])):
+            if prev[idx] + n * esz != r[idx]:
+                ok = False
+                break
+        if ok and (prev[4] == 0) == (r[4] == 0) and (r[4] == 0 or prev[4] + n * 2 == r[4]) and prev[6:] == list(r[6:]):
+            prev[5] += r[5]
+        else:
+            out.append(list(r))
+    return [tuple(x[:6]) for x in out]
+
+
+class FusedAdamStep:
+    """Runs Adam/AdamW for a torch optimizer with one HIP launch per param group."""
+
+    def __init__(self, optimizer: torch.optim.Optimizer):
+        self.optimizer = optimizer
+        self.adamw = isinstance(optimizer, torch.optim.AdamW)
+
+    @torch.no_grad()
+    def step(self, grad_scale: Optional[torch.Tensor] = None):
+        opt = self.optimizer
+        e = ext()
+        for group in opt.param_groups:
+            lr = group["lr"]
+            if isinstance(lr, torch.Tensor):
+                lr = float(lr)
+            beta1, beta2 = group["betas"]
+            eps, wd = group["eps"], group["weight_decay"]
+            rows = []
+            dtypes = None
+            step_val = None
+            for p in group["params"]:
+                if p.grad is None or p.numel() == 0:
+                    continue
+                st = opt.state[p]
+                if len(st) == 0:
+                    st["step"] = torch.tensor(0.0, dtype=torch.float32)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["step"] += 1
+                s = float(st["step"]) if step_val is None else step_val
+                step_val = s
+                g = p.grad
+                m, v = st["exp_avg"], st["exp_avg_sq"]
+                for t in (p, g, m, v):
+                    if not t.is_contiguous():
+                        raise RuntimeError("FusedAdamStep requires contiguous params/grads/state")
+                dt = (_DT[p.dtype], _DT[g.dtype], _DT[m.dtype])
+                if dtypes is None:
+                    dtypes = dt
+                elif dtypes != dt:
+                    # Mixed dtypes within a group: flush what we have and start a new launch.
+                    self._launch(e, rows, dtypes, lr, beta1, beta2, eps, wd, step_val, grad_scale, p.device)
+                    rows, dtypes = [], dt
+                shadow = getattr(p, "_acc_bf16_shadow", None)
+                rows.append(
+                    (
+                        p.data_ptr(),
+                        g.data_ptr(),
+                        m.data_ptr(),
+                        v.data_ptr(),
+                        shadow.data_ptr() if shadow is not None else 0,
+                        p.numel(),
+                        p.element_size(),
+                        g.element_size(),
+                        m.element_size(),
+                    )
+                )
+            if rows:
+                self._launch(e, rows, dtypes, lr, beta1, beta2, eps, wd, step_val, grad_scale, group["params"][0].device)
+
+    def _launch(self, e, rows, dtypes, lr, beta1, beta2, eps, wd, step, grad_scale, device):
+        if not rows:
+            return
+        merged = _merge_contiguous(rows)
+        meta, prefix, nblocks = _CACHE.get(merged, device)
+        bc1 = 1.0 - beta1**step
+        bc2_sqrt = math.sqrt(1.0 - beta2**step)
+        e.adam_multi_tensor(meta, prefix, nblocks, dtypes[0], dtypes[1], dtypes[2], lr, beta1, beta2, eps, wd, bc1, bc2_sqrt, self.adamw, grad_scale)
+
+
+def _grad_rows(params, dtype):
+    rows = []
+    for p in params:
+        g = p.grad
+        if g is None or g.numel() == 0 or g.dtype != dtype:
+            continue
+        if not g.is_contiguous():
+            raise RuntimeError("multi-tensor grad norm requires contiguous grads")
+        rows.append((0, g.data_ptr(), 0, 0, 0, g.numel()))
+    return rows
+
+
+@torch.no_grad()
+def grad_sq_norm(params: Iterable[torch.nn.Parameter], out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Sum of squares of all grads (fp32 device scalar [1]); one launch per grad dtype."""
+    params = [p for p in params if p.grad is not None]
+    if not params:
+        return torch.zeros(1)
+    dev = params[0].grad.device
+    if out is None:
+        out = torch.zeros(1, dtype=torch.float32, device=dev)
+    if not use_native(params[0].grad):
+        acc = torch.zeros((), dtype=torch.float32, device=dev)
+        for p in params:
+            acc += p.grad.float().pow(2).sum()
+        out.copy_(acc.reshape(1))
+        return out
+    e = ext()
+    first = True
+    for dt in (torch.float32, torch.bfloat16):
+        rows = _grad_rows(params, dt)
+        if not rows:
+            continue
+        meta, prefix, nb = _CACHE.get(rows, dev)
+        e.sqnorm_multi_tensor(meta, prefix, nb, _DT[dt], out, not first)
+        first = False
+    if first:
+        out.zero_()
+    return out
+
+
+@torch.no_grad()
+def clip_grads_by_total_sq(params, total_sq: torch.Tensor, max_norm: float):
+    """Scale grads by min(1, max_norm / (sqrt(total_sq) + 1e-6)) entirely on device (no host sync)."""
+    params = [p for p in params if p.grad is not None]
+    if not params:
+        return
+    if not use_native(params[0].grad):
+        coef = (max_norm / (total_sq.sqrt() + 1e-6)).clamp(max=1.0)
+        for p in params:
+            p.grad.mul_(coef.to(p.grad.dtype))
+        return
+    e = ext()
+    dev = params[0].grad.device
+    for dt in (torch.float32, torch.bfloat16):
+        rows = _grad_rows(params, dt)
+        if rows:
+            meta, prefix, nb = _CACHE.get(rows, dev)
+            e.clip_multi_tensor(meta, prefix, nb, _DT[dt], total_sq, max_norm)

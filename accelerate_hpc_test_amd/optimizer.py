@@ -1,0 +1,200 @@
+"""Optimizer wrapper.
+
+Parity: `/root/reference/src/accelerate/optimizer.py:38-213`: state placement on the device, `zero_grad` and
+`step` gated by `GradientState.sync_gradients`, fp16 GradScaler stepping with overflow detection
+(`step_was_skipped`), picklability.
+
+MI355X-native addition: when the wrapped optimizer is `torch.optim.AdamW`/`Adam` and its parameters live on
+the GPU, `step()` runs our HIP multi-tensor AdamW kernel (`ops/adamw.py`: one launch per dtype group over
+chunked tensor lists, reading grad/param/m/v once and optionally writing the bf16 shadow copy that the FSDP
+engine all-gathers) instead of torch's foreach implementation. The optimizer's `state` keeps torch's layout
+(`step`, `exp_avg`, `exp_avg_sq`) so checkpoints are interchangeable. Set `ACCELERATE_FUSED_ADAMW=0` to
+disable.
+"""
+
+from __future__ import annotations
+
+import inspect
+import os
+
+import torch
+
+from .state import AcceleratorState, GradientState
+from .utils.dataclasses import DistributedType
+from .utils.operations import honor_type
+
+
+def move_to_device(state, device):
+    if isinstance(state, (list, tuple)):
+        return honor_type(state, (move_to_device(t, device) for t in state))
+    elif isinstance(state, dict):
+        return type(state)({k: move_to_device(v, device) for k, v in state.items()})
+    elif isinstance(state, torch.Tensor):
+        return state.to(device)
+    return state
+
+
+def _fused_adam_eligible(optimizer) -> bool:
+    if os.environ.get("ACCELERATE_FUSED_ADAMW", "1") == "0":
+        return False
+    if type(optimizer) not in (torch.optim.AdamW, torch.optim.Adam):
+        return False
+    for g in optimizer.param_groups:
+        if g.get("amsgrad", False) or g.get("maximize", False) or g.get("capturable", False):
+            return False
+        if g.get("differentiable", False):
+            return False
+        for p in g["params"]:
+            if not p.is_cuda:
+                return False
+    return True
+
+
+class AcceleratedOptimizer(torch.optim.Optimizer):
+    def __init__(self, optimizer, device_placement=True, scaler=None):
+        self.optimizer = optimizer
+        self.scaler = scaler
+        self.accelerator_state = AcceleratorState()
+        self.gradient_state = GradientState()
+        self.device_placement = device_placement
+        self._is_overflow = False
+        self._fused_step = None
+
+        if self.scaler is not None:
+            self._accelerate_step_called = False
+            self._optimizer_original_step_method = self.optimizer.step
+            self._optimizer_patched_step_method = patch_optimizer_step(self, self.optimizer.step)
+
+        if device_placement:
+            state_dict = self.optimizer.state_dict()
+            state_dict["state"] = move_to_device(state_dict["state"], self.accelerator_state.device)
+            self.optimizer.load_state_dict(state_dict)
+
+    # ---- fused HIP AdamW -------------------------------------------------------------------------
+    def _maybe_fused(self):
+        if self._fused_step is None:
+            if _fused_adam_eligible(self.optimizer):
+                from .ops.multi_tensor import FusedAdamStep
+
+                self._fused_step = FusedAdamStep(self.optimizer)
+            else:
+                self._fused_step = False
+        return self._fused_step
+
+    @property
+    def state(self):
+        return self.optimizer.state
+
+    @state.setter
+    def state(self, state):
+        self.optimizer.state = state
+
+    @property
+    def param_groups(self):
+        return self.optimizer.param_groups
+
+    @param_groups.setter
+    def param_groups(self, param_groups):
+        self.optimizer.param_groups = param_groups
+
+    @property
+    def defaults(self):
+        return self.optimizer.defaults
+
+    @defaults.setter
+    def defaults(self, defaults):
+        self.optimizer.defaults = defaults
+
+    def add_param_group(self, param_group):
+        self.optimizer.add_param_group(param_group)
+        self._fused_step = None
+
+    def load_state_dict(self, state_dict):
+        self.optimizer.load_state_dict(state_dict)
+        self._fused_step = None
+
+    def state_dict(self):
+        return self.optimizer.state_dict()
+
+    def zero_grad(self, set_to_none=None):
+        if self.gradient_state.sync_gradients:
+            accept_arg = "set_to_none" in inspect.signature(self.optimizer.zero_grad).parameters
+            if accept_arg:
+                if set_to_none is None:
+                    set_to_none = True
+                self.optimizer.zero_grad(set_to_none=set_to_none)
+            else:
+                if set_to_none is not None:
+                    raise ValueError("`set_to_none` for Optimizer.zero_grad` is not supported by this optimizer.")
+                self.optimizer.zero_grad()
+            hook = getattr(self.optimizer, "_accelerate_post_zero_grad", None)
+            if hook is not None:
+                hook()
+
+    def train(self):
+        if hasattr(self.optimizer, "train") and callable(self.optimizer.train):
+            self.optimizer.train()
+
+    def eval(self):
+        if hasattr(self.optimizer, "eval") and callable(self.optimizer.eval):
+            self.optimizer.eval()
+
+    def _inner_step(self, closure=None):
+        fused = self._maybe_fused()
+        if fused and closure is None:
+            fused.step()
+            self.optimizer._acc_last_step_fused = True
+        else:
+            self.optimizer.step(closure)
+            self.optimizer._acc_last_step_fused = False
+
+    def step(self, closure=None):
+        if not self.gradient_state.sync_gradients:
+            return
+        if self.scaler is not None:
+            self.optimizer.step = self._optimizer_patched_step_method
+            self.scaler.step(self.optimizer, closure)
+            self.scaler.update()
+            if not self._accelerate_step_called:
+                self._is_overflow = True
+            else:
+                self._is_overflow = False
+            self.optimizer.step = self._optimizer_original_step_method
+            self._accelerate_step_called = False
+        else:
+            self._inner_step(closure)
+        if self.scaler is not None:
+            self.optimizer._acc_last_step_fused = False
+        post = getattr(self.optimizer, "_accelerate_post_step", None)
+        if post is not None:
+            post()
+
+    def _switch_parameters(self, parameters_map):
+        for param_group in self.optimizer.param_groups:
+            param_group["params"] = [parameters_map.get(p, p) for p in param_group["params"]]
+        self._fused_step = None
+
+    @property
+    def step_was_skipped(self):
+        """Whether the last optimizer step was skipped because of fp16 overflow."""
+        return self._is_overflow
+
+    def __getstate__(self):
+        _ignored_keys = ["_accelerate_step_called", "_optimizer_original_step_method", "_optimizer_patched_step_method", "_fused_step"]
+        return {k: v for k, v in self.__dict__.items() if k not in _ignored_keys}
+
+    def __setstate__(self, state):
+        self.__dict__.update(state)
+        self._fused_step = None
+        if self.scaler is not None:
+            self._accelerate_step_called = False
+            self._optimizer_original_step_method = self.optimizer.step
+            self._optimizer_patched_step_method = patch_optimizer_step(self, self.optimizer.step)
+
+
+def patch_optimizer_step(accelerated_optimizer: AcceleratedOptimizer, method):
+    def patched_step(*args, **kwargs):
+        accelerated_optimizer._accelerate_step_called = True
+        return method(*args, **kwargs)
+
+    return patched_step

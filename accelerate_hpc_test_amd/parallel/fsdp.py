@@ -1,0 +1,825 @@
+"""Native fully-sharded data parallel engine (FSDP2-equivalent) for MI355X.
+
+Parity: the reference wraps `torch.distributed.fsdp.fully_shard` (`/root/reference/src/accelerate/accelerator.py:1656-1746`,
+`utils/fsdp_utils.py:621-737`). Here the engine is our own:
+
+* **Units.** The wrap policy (transformer classes / min params / none) selects modules; each selected module's
+  parameters (plus the leftovers, in a root unit) are flattened into ONE buffer per unit, padded to a multiple of
+  the shard world size. Rank r owns the contiguous slice r of that buffer.
+* **Precision.** Each unit keeps an fp32 master shard (what the optimizer updates), an fp32 gradient shard, and a
+  `param_dtype` (bf16) shard that is the all-gather input. The fused HIP AdamW writes the bf16 shard in the same
+  pass as the fp32 update (`_acc_bf16_shadow`), so there is no separate cast pass. The reference's fp32 "upcast"
+  loop is a no-op (`utils/fsdp_utils.py:723-736`); here master weights are explicitly fp32.
+* **Unshard.** The original `nn.Parameter` objects stay registered in their modules; their `.data` are views into
+  the unit's full bf16 buffer, whose storage is resized 0 ↔ full. Before a unit runs, RCCL `all_gather_into_tensor`
+  fills it on a dedicated HIP stream; the next unit in execution order is prefetched (depth configurable) so the
+  gather of block i+1 overlaps block i's compute. After forward (`reshard_after_forward`) the storage is freed and
+  re-gathered before the unit's backward (triggered by a gradient hook on the unit's outputs).
+* **Reduce.** Parameter grads accumulate in place into a flat bf16 gradient buffer (pre-assigned `.grad` views).
+  When every parameter of the unit has accumulated (post-accumulate-grad hooks), ONE `reduce_scatter_tensor` runs on
+  the reduce stream; its output is scaled by 1/W and accumulated into the fp32 gradient shard. HSDP adds an
+  all-reduce across the replicate group. `no_sync` (`set_requires_gradient_sync(False)`) keeps the flat grads.
+* **World size 1** degenerates to zero collectives: the bf16 shard IS the full buffer (no copies).
+
+Messages are one transformer block each (≈436 MB bf16 for Llama-3-8B), large enough for RCCL to spread over all 7
+xGMI links; streams and events order everything on the device — the host never blocks.
+"""
+
+from __future__ import annotations
+
+import json
+import math
+import os
+from collections import OrderedDict
+from contextlib import contextmanager
+from typing import Callable, Iterable, Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from ..utils.dataclasses import FullyShardedDataParallelPlugin, MixedPrecisionPolicy
+
+_ALIGN = 64  # elements; keeps every rank's shard 128-B aligned for bf16 / 256-B for fp32
+
+
+def _round_up(x, m):
+    return (x + m - 1) // m * m
+
+
+class _ParamInfo:
+    __slots__ = ("fqn", "module", "attr", "param", "orig_param", "offset", "numel", "shape", "shard_param", "local_lo", "local_hi", "param_lo")
+
+    def __init__(self, fqn, module, attr, param, offset):
+        self.fqn = fqn
+        self.module = module
+        self.attr = attr
+        self.param = param
+        self.orig_param = param
+        self.offset = offset
+        self.numel = param.numel()
+        self.shape = tuple(param.shape)
+        self.shard_param = None
+        self.local_lo = self.local_hi = self.param_lo = 0
+
+
+class FlatUnit:
+    """One sharding unit (e.g. a decoder layer)."""
+
+    def __init__(self, engine: "FSDPEngine", idx: int, module: nn.Module, infos: list[_ParamInfo]):
+        self.engine = engine
+        self.idx = idx
+        self.module = module
+        self.infos = infos
+        W = engine.world_size
+        total = sum(i.numel for i in infos)
+        self.numel = total
+        self.padded = _round_up(max(total, 1), W * _ALIGN)
+        self.shard_numel = self.padded // W
+        self.is_root = False
+        self.state = "sharded"  # or "unsharding" / "unsharded"
+        self.ag_event: Optional[torch.cuda.Event] = None
+        self.full: Optional[torch.Tensor] = None
+        self.full_grad: Optional[torch.Tensor] = None
+        self.pending_grads = 0
+        self.grad_ready = False
+        self.reduced = False
+        self.bwd_prefetched = False
+        self.in_backward = False
+
+    # --- sizes/ranges ---------------------------------------------------------------------------------
+    @property
+    def shard_lo(self):
+        return self.engine.rank * self.shard_numel
+
+    @property
+    def shard_hi(self):
+        return self.shard_lo + self.shard_numel
+
+
+class FSDPEngine:
+    def __init__(
+        self,
+        model: nn.Module,
+        plugin: FullyShardedDataParallelPlugin,
+        device: torch.device,
+        process_group=None,
+        replicate_group=None,
+        init_fn: Optional[Callable[[nn.Module], None]] = None,
+        seed: int = 0,
+        prefetch_depth: int = 1,
+    ):
+        self.model = model
+        self.plugin = plugin
+        self.device = device
+        self.group = process_group
+        self.replicate_group = replicate_group
+        if dist.is_available() and dist.is_initialized():
+            self.world_size = dist.get_world_size(process_group)
+            self.rank = dist.get_rank(process_group)
+        else:
+            self.world_size, self.rank = 1, 0
+        self.replicate_size = dist.get_world_size(replicate_group) if replicate_group is not None else 1
+        mp = plugin.mixed_precision_policy or MixedPrecisionPolicy()
+        self.param_dtype = mp.param_dtype or torch.float32
+        self.reduce_dtype = mp.reduce_dtype or self.param_dtype
+        self.output_dtype = mp.output_dtype
+        self.reshard_after_forward = bool(plugin.reshard_after_forward) and self.world_size > 1
+        self.prefetch_depth = max(0, prefetch_depth)
+        self.requires_grad_sync = True
+        self.is_cuda = device.type == "cuda"
+        self._uses_gloo = self.is_cuda is False
+        if self.is_cuda:
+            self.ag_stream = torch.cuda.Stream(device=device, priority=-1)
+            self.rs_stream = torch.cuda.Stream(device=device, priority=-1)
+        else:
+            self.ag_stream = self.rs_stream = None
+        self.units: list[FlatUnit] = []
+        self.exec_order: list[FlatUnit] = []
+        self._recording_order = True
+        self._final_cb_queued = False
+        self._pending_frees = []
+        self._build_units(init_fn, seed)
+
+    # =========================================================================================== build
+    def _wrap_fn(self):
+        fn = getattr(self.plugin, "_wrap_fn", None)
+        if fn is None and self.plugin.auto_wrap_policy not in (None, "NO_WRAP"):
+            fn = self.plugin.set_auto_wrap_policy(self.model)
+        return fn
+
+    def _build_units(self, init_fn, seed):
+        wrap = self._wrap_fn()
+        owned: set[int] = set()
+        ignored = set()
+        if self.plugin.ignored_modules is not None and not isinstance(self.plugin.ignored_modules, str):
+            for m in self.plugin.ignored_modules:
+                for p in m.parameters():
+                    ignored.add(id(p))
+        unit_modules = []
+        if wrap is not None:
+            # post-order: inner matches become units before their parents
+            def visit(m):
+                for c in m.children():
+                    visit(c)
+                if m is not self.model and wrap(m):
+                    unit_modules.append(m)
+
+            visit(self.model)
+        name_of = {id(m): n for n, m in self.model.named_modules()}
+        assigned_units = []
+        for m in unit_modules:
+            infos = self._collect(m, name_of[id(m)], owned, ignored)
+            if infos:
+                assigned_units.append((m, infos))
+        root_infos = self._collect(self.model, "", owned, ignored)
+        # Units are created in module order; the root goes first so its index is 0.
+        all_units = [(self.model, root_infos, True)] + [(m, infos, False) for m, infos in assigned_units]
+        for idx, (m, infos, is_root) in enumerate(all_units):
+            unit = FlatUnit(self, idx, m, infos)
+            unit.is_root = is_root
+            self._materialize(unit, init_fn, seed)
+            self.units.append(unit)
+        self.root = self.units[0]
+        for unit in self.units[1:]:
+            unit.module.register_forward_pre_hook(self._make_pre_forward(unit), with_kwargs=True)
+            unit.module.register_forward_hook(self._make_post_forward(unit), with_kwargs=True)
+        for unit in self.units:
+            for info in unit.infos:
+                if info.param.requires_grad:
+                    info.param.register_post_accumulate_grad_hook(self._make_grad_hook(unit))
+
+    def _replace_param(self, info: _ParamInfo, new: nn.Parameter):
+        """Swap a (meta) Parameter object for `new` in every module that registers it (tied weights included)."""
+        if not hasattr(self, "_holders"):
+            self._holders = {}
+            for m in self.model.modules():
+                for attr, p in m._parameters.items():
+                    if p is not None:
+                        self._holders.setdefault(id(p), []).append((m, attr))
+        old = info.param
+        for m, attr in self._holders.get(id(old), []):
+            m._parameters[attr] = new
+        self._holders[id(new)] = self._holders.pop(id(old), [])
+        info.orig_param = old
+        info.param = new
+
+    def _collect(self, module, prefix, owned, ignored):
+        infos, offset = [], 0
+        for name, p in module.named_parameters(recurse=True, remove_duplicate=True):
+            if id(p) in owned or id(p) in ignored:
+                continue
+            owned.add(id(p))
+            sub_name, _, attr = name.rpartition(".")
+            sub = module.get_submodule(sub_name) if sub_name else module
+            fqn = f"{prefix}.{name}" if prefix else name
+            infos.append(_ParamInfo(fqn, sub, attr, p, offset))
+            offset += p.numel()
+        return infos
+
+    @torch.no_grad()
+    def _materialize(self, unit: FlatUnit, init_fn, seed):
+        dev, W, r = self.device, self.world_size, self.rank
+        full32 = torch.zeros(unit.padded, dtype=torch.float32, device=dev)
+        on_meta = any(i.param.is_meta for i in unit.infos)
+        if on_meta:
+            # Materialise the whole unit on the GPU with a per-unit seed: every rank generates the identical unit
+            # (deterministic regardless of world size) and keeps its slice.
+            if init_fn is None:
+                raise ValueError("Meta-device parameters need an `init_fn` (e.g. model.init_weights).")
+            for info in unit.infos:
+                view = full32[info.offset : info.offset + info.numel].view(info.shape)
+                self._replace_param(info, nn.Parameter(view, requires_grad=info.param.requires_grad))
+            gen_state = torch.cuda.get_rng_state(dev) if dev.type == "cuda" else torch.get_rng_state()
+            torch.manual_seed(seed * 100003 + unit.idx)
+            if dev.type == "cuda":
+                torch.cuda.manual_seed(seed * 100003 + unit.idx)
+            mods = {id(i.module): i.module for i in unit.infos}
+            for m in mods.values():
+                init_fn(m)
+            if dev.type == "cuda":
+                torch.cuda.set_rng_state(gen_state, dev)
+            else:
+                torch.set_rng_state(gen_state)
+        else:
+            for info in unit.infos:
+                full32[info.offset : info.offset + info.numel].copy_(info.param.detach().reshape(-1).to(dev, torch.float32))
+            if self.plugin.sync_module_states and W > 1:
+                dist.broadcast(full32, src=dist.get_global_rank(self.group, 0) if self.group is not None else 0, group=self.group)
+        lo, hi = r * unit.shard_numel, (r + 1) * unit.shard_numel
+        unit.master = full32[lo:hi].clone()
+        unit.grad_shard = torch.zeros_like(unit.master)
+        unit.grad_valid = False
+        del full32
+        unit.shard_lp = unit.master.to(self.param_dtype) if self.param_dtype != torch.float32 else unit.master
+        if W == 1:
+            unit.full = unit.shard_lp  # degenerate: no collective, the shard is the full buffer
+        else:
+            unit.full = torch.empty(unit.padded, dtype=self.param_dtype, device=dev)
+        # Point every original parameter at its slice of the full buffer (views survive storage resizes).
+        for info in unit.infos:
+            info.param.data = unit.full[info.offset : info.offset + info.numel].view(info.shape)
+            # per-parameter views of the local shard, exposed to the optimizer
+            plo, phi = info.offset, info.offset + info.numel
+            a, b = max(plo, lo), min(phi, hi)
+            if b <= a:
+                a = b = max(min(plo, hi), lo)
+            info.local_lo, info.local_hi, info.param_lo = a - lo, b - lo, a - plo
+            sp = nn.Parameter(unit.master[info.local_lo : info.local_hi], requires_grad=info.param.requires_grad)
+            if self.param_dtype != torch.float32:
+                sp._acc_bf16_shadow = unit.shard_lp[info.local_lo : info.local_hi]
+            sp._acc_fsdp_fqn = info.fqn
+            sp._acc_fsdp_full_shape = info.shape
+            sp._acc_fsdp_param_lo = info.param_lo
+            info.shard_param = sp
+        if W > 1:
+            unit.state = "unsharded"
+            self._free_full(unit)
+        else:
+            unit.state = "unsharded"
+
+    # =========================================================================================== storage
+    def _free_full(self, unit: FlatUnit):
+        if self.world_size == 1 or unit.state == "sharded":
+            return
+        unit.full.untyped_storage().resize_(0)
+        unit.state = "sharded"
+        unit.ag_event = None
+
+    def _unshard(self, unit: FlatUnit):
+        """Issue the all-gather of `unit` on the AG stream (no host wait). Idempotent."""
+        if self.world_size == 1 or unit.state != "sharded":
+            return
+        nbytes = unit.padded * unit.full.element_size()
+        unit.full.untyped_storage().resize_(nbytes)
+        if self.is_cuda:
+            cur = torch.cuda.current_stream(self.device)
+            self.ag_stream.wait_stream(cur)
+            with torch.cuda.stream(self.ag_stream):
+                dist.all_gather_into_tensor(unit.full, unit.shard_lp, group=self.group)
+                ev = torch.cuda.Event()
+                ev.record(self.ag_stream)
+            unit.ag_event = ev
+        else:
+            dist.all_gather_into_tensor(unit.full, unit.shard_lp, group=self.group) if not self._gloo() else self._gloo_allgather(unit)
+            unit.ag_event = None
+        unit.state = "unsharding"
+
+    def _gloo(self):
+        return dist.get_backend(self.group) == "gloo"
+
+    def _gloo_allgather(self, unit):
+        chunks = list(unit.full.chunk(self.world_size))
+        dist.all_gather(chunks, unit.shard_lp, group=self.group)
+
+    def _wait_unsharded(self, unit: FlatUnit):
+        if unit.state == "sharded":
+            self._unshard(unit)
+        if unit.state == "unsharding":
+            if unit.ag_event is not None:
+                torch.cuda.current_stream(self.device).wait_event(unit.ag_event)
+            unit.state = "unsharded"
+
+    # =========================================================================================== hooks
+    def _in_backward(self):
+        return torch._C._current_graph_task_id() != -1
+
+    def _make_pre_forward(self, unit: FlatUnit):
+        def hook(module, args, kwargs):
+            self._wait_unsharded(unit)
+            if self._in_backward():
+                return None  # activation-checkpoint recompute: params are already gathered for backward
+            if self._recording_order:
+                if unit not in self.exec_order:
+                    self.exec_order.append(unit)
+            else:
+                self._prefetch_forward(unit)
+            return None
+
+        return hook
+
+    def _prefetch_forward(self, unit):
+        if self.world_size == 1 or self.prefetch_depth == 0:
+            return
+        try:
+            i = self.exec_order.index(unit)
+        except ValueError:
+            return
+        for nxt in self.exec_order[i + 1 : i + 1 + self.prefetch_depth]:
+            self._unshard(nxt)
+
+    def _make_post_forward(self, unit: FlatUnit):
+        def hook(module, args, kwargs, output):
+            if self._in_backward():
+                return output
+            if torch.is_grad_enabled():
+                self._register_pre_backward(unit, output)
+            if self.reshard_after_forward:
+                self._free_full(unit)
+            return output
+
+        return hook
+
+    def _register_pre_backward(self, unit, output):
+        tensors = [t for t in _flatten_tensors(output) if t.requires_grad]
+        if not tensors:
+            return
+        unit.bwd_prefetched = False
+
+        def pre_backward(grad):
+            if not unit.in_backward:
+                unit.in_backward = True
+                self._queue_final_callback()
+                self._wait_unsharded(unit)
+                self._prefetch_backward(unit)
+                self._prepare_grad_buffer(unit)
+            return grad
+
+        for t in tensors:
+            t.register_hook(pre_backward)
+
+    def _prefetch_backward(self, unit):
+        if self.world_size == 1 or self.prefetch_depth == 0:
+            return
+        try:
+            i = self.exec_order.index(unit)
+        except ValueError:
+            return
+        for j in range(i - 1, max(-1, i - 1 - self.prefetch_depth), -1):
+            self._unshard(self.exec_order[j])
+
+    def _queue_final_callback(self):
+        if not self._final_cb_queued:
+            self._final_cb_queued = True
+            torch.autograd.Variable._execution_engine.queue_callback(self._finalize_backward)
+
+    def _prepare_grad_buffer(self, unit: FlatUnit):
+        """Point every param's `.grad` at its slice of a zeroed flat grad buffer (accumulated in place)."""
+        if unit.full_grad is None:
+            if self.world_size == 1 and unit.full.dtype == self.reduce_dtype and False:
+                pass
+            unit.full_grad = torch.zeros(unit.padded, dtype=self.param_dtype, device=self.device)
+            for info in unit.infos:
+                if info.param.requires_grad:
+                    info.param.grad = unit.full_grad[info.offset : info.offset + info.numel].view(info.shape)
+        unit.pending_grads = sum(1 for i in unit.infos if i.param.requires_grad)
+        unit.reduced = False
+
+    def _make_grad_hook(self, unit: FlatUnit):
+        def hook(param):
+            if unit.full_grad is None or param.grad is None or param.grad.data_ptr() != self._grad_slot_ptr(unit, param):
+                self._absorb_foreign_grad(unit, param)
+            unit.pending_grads -= 1
+            if unit.pending_grads == 0 and self.requires_grad_sync:
+                self._reduce_unit(unit)
+
+        return hook
+
+    def _grad_slot_ptr(self, unit, param):
+        for info in unit.infos:
+            if info.param is param:
+                return unit.full_grad[info.offset : info.offset + info.numel].data_ptr()
+        return -1
+
+    def _absorb_foreign_grad(self, unit, param):
+        """A grad not living in our flat buffer (first use before a pre-backward hook, e.g. root params):
+        copy/accumulate it into the flat buffer and re-point `.grad`."""
+        if unit.full_grad is None:
+            unit.full_grad = torch.zeros(unit.padded, dtype=self.param_dtype, device=self.device)
+            unit.pending_grads = sum(1 for i in unit.infos if i.param.requires_grad)
+            for info in unit.infos:
+                if info.param.requires_grad and info.param is not param and info.param.grad is None:
+                    info.param.grad = unit.full_grad[info.offset : info.offset + info.numel].view(info.shape)
+        for info in unit.infos:
+            if info.param is param:
+                view = unit.full_grad[info.offset : info.offset + info.numel].view(info.shape)
+                if param.grad is not None and param.grad.data_ptr() != view.data_ptr():
+                    view.add_(param.grad.to(view.dtype))
+                param.grad = view
+                return
+
+    # =========================================================================================== reduction
+    @torch.no_grad()
+    def _reduce_unit(self, unit: FlatUnit):
+        if unit.reduced or unit.full_grad is None:
+            return
+        unit.reduced = True
+        W = self.world_size
+        # torch semantics: grads accumulate until the optimizer (or user) sets them to None.
+        first = (not unit.grad_valid) or all(i.shard_param.grad is None for i in unit.infos if i.shard_param.requires_grad)
+        if W == 1 and self.replicate_size == 1:
+            g = unit.full_grad[: unit.shard_numel]
+            if first:
+                unit.grad_shard.copy_(g)
+            else:
+                unit.grad_shard.add_(g)
+            unit.grad_valid = True
+            self._release_grad(unit)
+            self._expose_unit_grads(unit)
+            return
+        src = unit.full_grad if unit.full_grad.dtype == self.reduce_dtype else unit.full_grad.to(self.reduce_dtype)
+        out = torch.empty(unit.shard_numel, dtype=self.reduce_dtype, device=self.device)
+        if self.is_cuda:
+            cur = torch.cuda.current_stream(self.device)
+            self.rs_stream.wait_stream(cur)
+            with torch.cuda.stream(self.rs_stream):
+                self._rs_and_accumulate(unit, src, out, first)
+            src.record_stream(self.rs_stream)
+            out.record_stream(self.rs_stream)
+        else:
+            self._rs_and_accumulate(unit, src, out, first)
+        unit.grad_valid = True
+        self._release_grad(unit)
+        self._expose_unit_grads(unit)
+        if not unit.is_root and self.world_size > 1:
+            self._free_full(unit)  # block done with backward: drop its gathered params
+
+    def _rs_and_accumulate(self, unit, src, out, first):
+        W = self.world_size
+        if W > 1:
+            if self._uses_gloo and self._gloo():
+                self._gloo_rs(out, src)
+            else:
+                dist.reduce_scatter_tensor(out, src, group=self.group)
+        else:
+            out.copy_(src[: unit.shard_numel])
+        if self.replicate_group is not None and self.replicate_size > 1:
+            dist.all_reduce(out, group=self.replicate_group)
+        scale = 1.0 / (W * self.replicate_size)
+        if first:
+            torch.mul(out, scale, out=unit.grad_shard) if out.dtype == torch.float32 else unit.grad_shard.copy_(out).mul_(scale)
+        else:
+            unit.grad_shard.add_(out.float(), alpha=scale)
+
+    def _gloo_rs(self, out, src):
+        # gloo has no reduce_scatter: all-reduce then slice (CPU test path only).
+        tmp = src.clone()
+        dist.all_reduce(tmp, group=self.group)
+        out.copy_(tmp[self.rank * out.numel() : (self.rank + 1) * out.numel()])
+
+    def _release_grad(self, unit):
+        for info in unit.infos:
+            info.param.grad = None
+        unit.full_grad = None
+
+    def _finalize_backward(self):
+        """End of backward: flush units whose hooks did not all fire, order the compute stream after the reduce
+        stream, reshard, and expose the fp32 grad shards to the optimizer."""
+        self._final_cb_queued = False
+        if self._recording_order:
+            self._recording_order = False
+        for unit in self.units:
+            unit.in_backward = False
+            if self.requires_grad_sync and unit.full_grad is not None and not unit.reduced:
+                self._reduce_unit(unit)
+        if self.is_cuda and self.world_size * self.replicate_size > 1:
+            torch.cuda.current_stream(self.device).wait_stream(self.rs_stream)
+        for unit in self.units:
+            if self.reshard_after_forward or not unit.is_root:
+                if self.world_size > 1 and self.reshard_after_forward:
+                    self._free_full(unit)
+        if self.requires_grad_sync:
+            self._expose_grads()
+
+    def _expose_grads(self):
+        for unit in self.units:
+            self._expose_unit_grads(unit)
+
+    def _expose_unit_grads(self, unit):
+        if not unit.grad_valid:
+            return
+        for info in unit.infos:
+            sp = info.shard_param
+            if sp.requires_grad:
+                sp.grad = unit.grad_shard[info.local_lo : info.local_hi]
+
+    # =========================================================================================== public API
+    def shard_parameters(self):
+        for unit in self.units:
+            for info in unit.infos:
+                yield info.shard_param
+
+    def named_shard_parameters(self):
+        for unit in self.units:
+            for info in unit.infos:
+                yield info.fqn, info.shard_param
+
+    def param_map(self) -> dict:
+        """original nn.Parameter -> shard nn.Parameter (used to remap optimizers created before prepare)."""
+        return {info.orig_param: info.shard_param for unit in self.units for info in unit.infos}
+
+    def pre_root_forward(self):
+        """Called by the wrapper before the model's forward: gather the root unit (+ prefetch the first block)."""
+        self._wait_unsharded(self.root)
+        if not self._recording_order and self.exec_order:
+            for u in self.exec_order[: self.prefetch_depth]:
+                self._unshard(u)
+
+    def post_root_forward(self, output):
+        if self.exec_order:
+            self._recording_order = False
+        if torch.is_grad_enabled():
+            tensors = [t for t in _flatten_tensors(output) if t.requires_grad]
+
+            def hook(grad):
+                self._queue_final_callback()
+                if self.root.full_grad is None:
+                    self._prepare_grad_buffer(self.root)
+                return grad
+
+            for t in tensors:
+                t.register_hook(hook)
+        return output
+
+    def on_zero_grad(self):
+        for unit in self.units:
+            if all(info.shard_param.grad is None for info in unit.infos):
+                unit.grad_valid = False
+
+    @torch.no_grad()
+    def on_optimizer_step(self, fused_wrote_shadow: bool):
+        """Refresh the bf16 all-gather source from the fp32 master when the optimizer did not write it."""
+        if self.param_dtype == torch.float32:
+            return
+        if not fused_wrote_shadow:
+            for unit in self.units:
+                unit.shard_lp.copy_(unit.master)
+
+    def set_requires_gradient_sync(self, flag: bool):
+        self.requires_grad_sync = flag
+
+    @torch.no_grad()
+    def clip_grad_norm_(self, max_norm: float, norm_type: float = 2.0) -> torch.Tensor:
+        """Global gradient norm over all shards (HIP multi-tensor sum of squares + one all-reduce), then device-side
+        scaling. Returns the total norm (device tensor, no host sync)."""
+        from ..ops.multi_tensor import clip_grads_by_total_sq, grad_sq_norm
+
+        if norm_type != 2.0:
+            raise NotImplementedError("Only the L2 norm is supported by the FSDP engine.")
+        flat_params = []
+        for unit in self.units:
+            if unit.grad_valid:
+                holder = _GradHolder(unit.grad_shard)
+                flat_params.append(holder)
+        total = torch.zeros(1, dtype=torch.float32, device=self.device)
+        if flat_params:
+            grad_sq_norm(flat_params, out=total)
+        if self.world_size > 1:
+            dist.all_reduce(total, group=self.group)
+        clip_grads_by_total_sq(flat_params, total, max_norm)
+        return total.sqrt().reshape(())
+
+    # --- state dicts --------------------------------------------------------------------------------------
+    @torch.no_grad()
+    def full_state_dict(self, rank0_only: bool = True, cpu: bool = True, dtype=None) -> dict:
+        """Gather the fp32 master weights unit by unit (one all-gather per unit) → {fqn: full tensor}."""
+        out = OrderedDict()
+        for unit in self.units:
+            if self.world_size > 1:
+                full = torch.empty(unit.padded, dtype=torch.float32, device=self.device)
+                if self._uses_gloo and self._gloo():
+                    dist.all_gather(list(full.chunk(self.world_size)), unit.master, group=self.group)
+                else:
+                    dist.all_gather_into_tensor(full, unit.master, group=self.group)
+            else:
+                full = unit.master
+            if rank0_only and self.rank != 0:
+                continue
+            for info in unit.infos:
+                t = full[info.offset : info.offset + info.numel].view(info.shape)
+                if dtype is not None:
+                    t = t.to(dtype)
+                out[info.fqn] = t.cpu().clone() if cpu else t.clone()
+        return out
+
+    def sharded_state_dict(self) -> dict:
+        """This rank's master shards: {fqn: local 1-D slice} plus layout metadata for resharding."""
+        tensors, meta = OrderedDict(), {"world_size": self.world_size, "rank": self.rank, "params": {}}
+        for unit in self.units:
+            for info in unit.infos:
+                tensors[info.fqn] = unit.master[info.local_lo : info.local_hi].detach().cpu().clone()
+                meta["params"][info.fqn] = {"shape": list(info.shape), "param_lo": info.param_lo, "numel": info.local_hi - info.local_lo}
+        return {"tensors": tensors, "meta": meta}
+
+    @torch.no_grad()
+    def load_full_state_dict(self, sd: dict, strict: bool = True):
+        missing = []
+        for unit in self.units:
+            for info in unit.infos:
+                if info.fqn not in sd:
+                    missing.append(info.fqn)
+                    continue
+                full = sd[info.fqn].reshape(-1)
+                piece = full[info.param_lo : info.param_lo + (info.local_hi - info.local_lo)]
+                unit.master[info.local_lo : info.local_hi].copy_(piece.to(unit.master.device, torch.float32))
+            if unit.shard_lp is not unit.master:
+                unit.shard_lp.copy_(unit.master)
+        if strict and missing:
+            raise KeyError(f"Missing keys in state dict: {missing[:5]}...")
+        return missing
+
+    @torch.no_grad()
+    def load_sharded_pieces(self, pieces: list[tuple[dict, dict]]):
+        """Load from any number of saved shards (resharding): each piece is (tensors, meta) of one saved rank."""
+        for unit in self.units:
+            for info in unit.infos:
+                lo_need, hi_need = info.param_lo, info.param_lo + (info.local_hi - info.local_lo)
+                for tensors, meta in pieces:
+                    pm = meta["params"].get(info.fqn)
+                    if pm is None:
+                        continue
+                    s_lo, s_hi = pm["param_lo"], pm["param_lo"] + pm["numel"]
+                    a, b = max(lo_need, s_lo), min(hi_need, s_hi)
+                    if b > a:
+                        src = tensors[info.fqn][a - s_lo : b - s_lo]
+                        unit.master[info.local_lo + (a - lo_need) : info.local_lo + (b - lo_need)].copy_(src.to(unit.master.device))
+            if unit.shard_lp is not unit.master:
+                unit.shard_lp.copy_(unit.master)
+
+    @contextmanager
+    def summon_full_params(self):
+        for u in self.units:
+            self._wait_unsharded(u)
+        try:
+            yield
+        finally:
+            if self.reshard_after_forward:
+                for u in self.units:
+                    if not u.is_root:
+                        self._free_full(u)
+
+
+class _GradHolder:
+    """Adapter so multi-tensor grad kernels can run over flat grad shards."""
+
+    __slots__ = ("grad",)
+
+    def __init__(self, g):
+        self.grad = g
+
+
+def _flatten_tensors(obj):
+    if isinstance(obj, torch.Tensor):
+        yield obj
+    elif isinstance(obj, (list, tuple)):
+        for o in obj:
+            yield from _flatten_tensors(o)
+    elif isinstance(obj, dict):
+        for o in obj.values():
+            yield from _flatten_tensors(o)
+    elif hasattr(obj, "__dataclass_fields__"):
+        for k in obj.__dataclass_fields__:
+            yield from _flatten_tensors(getattr(obj, k))
+    elif hasattr(obj, "to_tuple"):
+        yield from _flatten_tensors(obj.to_tuple())
+
+
+class FullyShardedModule(nn.Module):
+    """Wrapper returned by `Accelerator.prepare` for FSDP models (the analogue of an FSDP2 root module).
+
+    `parameters()` / `named_parameters()` return the fp32 master shard parameters (what an optimizer should
+    see); `module` is the original model whose parameters are the gathered compute-dtype views."""
+
+    def __init__(self, module: nn.Module, engine: FSDPEngine):
+        super().__init__()
+        self.module = module
+        self._engine = [engine]  # list: keep out of nn.Module registration
+
+    @property
+    def engine(self) -> FSDPEngine:
+        return self._engine[0]
+
+    def forward(self, *args, **kwargs):
+        eng = self.engine
+        eng.pre_root_forward()
+        if eng.param_dtype != torch.float32:
+            args = tuple(_cast_floats(a, eng.param_dtype) for a in args)
+            kwargs = {k: _cast_floats(v, eng.param_dtype) for k, v in kwargs.items()}
+        out = self.module(*args, **kwargs)
+        return eng.post_root_forward(out)
+
+    def parameters(self, recurse: bool = True):
+        return self.engine.shard_parameters()
+
+    def named_parameters(self, prefix: str = "", recurse: bool = True, remove_duplicate: bool = True):
+        for n, p in self.engine.named_shard_parameters():
+            yield (prefix + "." + n if prefix else n), p
+
+    def set_requires_gradient_sync(self, flag: bool):
+        self.engine.set_requires_gradient_sync(flag)
+
+    @contextmanager
+    def no_sync(self):
+        old = self.engine.requires_grad_sync
+        self.engine.set_requires_gradient_sync(False)
+        try:
+            yield
+        finally:
+            self.engine.set_requires_gradient_sync(old)
+
+    def clip_grad_norm_(self, max_norm, norm_type=2.0):
+        return self.engine.clip_grad_norm_(max_norm, norm_type)
+
+    def state_dict(self, *args, **kwargs):
+        return self.engine.full_state_dict(rank0_only=False)
+
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        return self.engine.load_full_state_dict(state_dict, strict=strict)
+
+    def __getattr__(self, name):
+        try:
+            return super().__getattr__(name)
+        except AttributeError:
+            return getattr(self.module, name)
+
+
+def _cast_floats(x, dtype):
+    if isinstance(x, torch.Tensor) and x.is_floating_point() and x.dtype != dtype:
+        return x.to(dtype)
+    return x
+
+
+def fully_shard(
+    model: nn.Module,
+    plugin: Optional[FullyShardedDataParallelPlugin] = None,
+    device: Optional[torch.device] = None,
+    process_group=None,
+    replicate_group=None,
+    init_fn=None,
+    seed: int = 0,
+    prefetch_depth: int = 1,
+) -> FullyShardedModule:
+    """Shard `model` with the native engine and return the wrapper."""
+    if plugin is None:
+        plugin = FullyShardedDataParallelPlugin(fsdp_version=2)
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+    if plugin.auto_wrap_policy not in (None, "NO_WRAP") and not callable(getattr(plugin, "_wrap_fn", None)):
+        plugin.set_auto_wrap_policy(model)
+    if plugin.activation_checkpointing:
+        apply_activation_checkpointing(model, plugin)
+    engine = FSDPEngine(model, plugin, device, process_group, replicate_group, init_fn, seed, prefetch_depth)
+    return FullyShardedModule(model, engine)
+
+
+def apply_activation_checkpointing(model: nn.Module, plugin: FullyShardedDataParallelPlugin):
+    """Non-reentrant activation checkpointing of every wrapped block (reference `fsdp_utils.py:588-618`)."""
+    from torch.utils.checkpoint import checkpoint
+
+    wrap = plugin._wrap_fn if getattr(plugin, "_wrap_fn", None) else plugin.set_auto_wrap_policy(model)
+    if wrap is None:
+        return
+    for m in model.modules():
+        if m is not model and wrap(m) and not getattr(m, "_acc_ckpt", False):
+            orig = m.forward
+
+            def make(orig):
+                def fwd(*a, **k):
+                    if torch.is_grad_enabled():
+                        return checkpoint(orig, *a, use_reentrant=False, **k)
+                    return orig(*a, **k)
+
+                return fwd
+
+            m.forward = make(orig)
+            m._acc_ckpt = True

@@ -1,0 +1,607 @@
+"""Process / device runtime singletons: `PartialState`, `AcceleratorState`, `GradientState`.
+
+Parity: `/root/reference/src/accelerate/state.py:122-1365`. Semantics kept: shared-state (Borg) singletons,
+`_reset_state`, `wait_for_everyone`, `split_between_processes`, the `on_*_process` decorators,
+`main_process_first`, the AttributeError raised when a reset state is accessed. What differs:
+
+* Only two executable back-ends: CPU (gloo; `MULTI_CPU` when WORLD_SIZE>1) and ROCm GPUs (RCCL through
+  `torch.distributed`'s "nccl" backend, `MULTI_GPU`/`FSDP`). There is no multi-vendor backend ladder.
+* One process per GPU: `cuda:{LOCAL_RANK % device_count}`, bound before the process group is created so
+  RCCL communicators are created on the right device. When FSDP needs CPU collectives (offload, full
+  state dicts) the group is created as `cuda:nccl,cpu:gloo`.
+"""
+
+from __future__ import annotations
+
+import os
+import threading
+import warnings
+from contextlib import contextmanager
+from functools import partial
+from typing import Any, Callable
+
+import torch
+
+from .utils.dataclasses import DistributedType, GradientAccumulationPlugin, SageMakerDistributedType
+from .utils.environment import (
+    get_cpu_distributed_information,
+    get_int_from_env,
+    parse_choice_from_env,
+    parse_flag_from_env,
+    set_numa_affinity,
+    str_to_bool,
+)
+
+
+def is_initialized() -> bool:
+    """Whether an `AcceleratorState` has been created in this process."""
+    return AcceleratorState._shared_state != {}
+
+
+def do_nothing(*args, **kwargs):
+    return None
+
+
+class ThreadLocalSharedDict(threading.local):
+    """Per-thread shared dict (used when `ACCELERATE_THREAD_LOCAL_STATE=1`)."""
+
+    def __init__(self, thread_local: bool = False):
+        self._storage = {}
+
+    def __get__(self, obj, objtype=None):
+        return self._storage
+
+    def __set__(self, obj, value):
+        self._storage = value
+
+
+SharedDict = ThreadLocalSharedDict if parse_flag_from_env("ACCELERATE_THREAD_LOCAL_STATE") else dict
+
+
+class PartialState:
+    """Process-level singleton: distributed environment, device, process indices.
+
+    Creating it initialises `torch.distributed` when the launcher set `WORLD_SIZE>1` (torchrun /
+    `accelerate launch` / `debug_launcher`). All instances share one dict of attributes.
+    """
+
+    _shared_state = SharedDict()
+    _known_attrs = [
+        "_cpu",
+        "_mixed_precision",
+        "_shared_state",
+        "backend",
+        "debug",
+        "device",
+        "distributed_type",
+        "fork_launched",
+        "local_process_index",
+        "num_processes",
+        "process_index",
+    ]
+
+    def __init__(self, cpu: bool = False, **kwargs):
+        self.__dict__ = self._shared_state
+        if self.initialized:
+            return
+        self._cpu = cpu
+        self.backend = None
+        env_device = os.environ.get("ACCELERATE_TORCH_DEVICE", None)
+        self.device = torch.device(env_device) if env_device is not None else None
+        self.debug = parse_flag_from_env("ACCELERATE_DEBUG_MODE")
+        use_cpu = cpu or parse_flag_from_env("ACCELERATE_USE_CPU") or not torch.cuda.is_available()
+        self._use_cpu = use_cpu
+
+        backend, distributed_type = self._prepare_backend(use_cpu, kwargs.pop("backend", None))
+        self.backend = backend
+        self.distributed_type = distributed_type
+        timeout = kwargs.pop("timeout", None)
+        init_method = kwargs.pop("init_method", None)
+
+        world_size = get_int_from_env(["WORLD_SIZE", "PMI_SIZE", "OMPI_COMM_WORLD_SIZE"], 1)
+        if distributed_type == DistributedType.NO:
+            self.num_processes = 1
+            self.process_index = 0
+            self.local_process_index = 0
+        else:
+            if distributed_type == DistributedType.MULTI_CPU:
+                info = get_cpu_distributed_information()
+                os.environ.setdefault("RANK", str(info.rank))
+                os.environ.setdefault("WORLD_SIZE", str(info.world_size))
+                os.environ.setdefault("LOCAL_RANK", str(info.local_rank))
+                os.environ.setdefault("LOCAL_WORLD_SIZE", str(info.local_world_size))
+                os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+                os.environ.setdefault("MASTER_PORT", "29500")
+            # Bind the device BEFORE the process group so RCCL comms land on the right GPU.
+            if not use_cpu:
+                local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+                self.device = torch.device("cuda", local_rank % torch.cuda.device_count())
+                torch.cuda.set_device(self.device)
+            if not torch.distributed.is_initialized():
+                pg_kwargs = {"backend": backend}
+                if timeout is not None:
+                    pg_kwargs["timeout"] = timeout
+                if init_method is not None:
+                    pg_kwargs["init_method"] = init_method
+                if backend == "nccl" and self.device is not None:
+                    pg_kwargs["device_id"] = self.device
+                torch.distributed.init_process_group(**pg_kwargs)
+            self.num_processes = torch.distributed.get_world_size()
+            self.process_index = torch.distributed.get_rank()
+            self.local_process_index = int(os.environ.get("LOCAL_RANK", -1))
+            if self.local_process_index < 0:
+                self.local_process_index = self.process_index % max(1, get_int_from_env(["LOCAL_WORLD_SIZE"], 1))
+        if self.device is None:
+            self.device = torch.device("cpu") if use_cpu else torch.device("cuda", 0)
+            if self.device.type == "cuda":
+                torch.cuda.set_device(self.device)
+        if (
+            parse_flag_from_env("ACCELERATE_CPU_AFFINITY", False)
+            and self.device.type == "cuda"
+            and distributed_type != DistributedType.NO
+        ):
+            set_numa_affinity(self.local_process_index)
+        self.fork_launched = parse_flag_from_env("FORK_LAUNCHED", 0)
+        _ = world_size
+
+    # ------------------------------------------------------------------------------------------
+    def _prepare_backend(self, cpu: bool, backend: str | None = None) -> tuple[str | None, DistributedType]:
+        """Decide the collective backend. Reference ladder `state.py:753-812`, collapsed to gloo/RCCL."""
+        world_size = get_int_from_env(["WORLD_SIZE", "PMI_SIZE", "OMPI_COMM_WORLD_SIZE"], 1)
+        if world_size <= 1:
+            return None, DistributedType.NO
+        if cpu:
+            if backend is None or backend == "nccl":
+                backend = "gloo"
+            return backend, DistributedType.MULTI_CPU
+        if backend is None:
+            backend = "nccl"  # RCCL on ROCm
+        if backend == "nccl" and parse_flag_from_env("ACCELERATE_FSDP_CPU_COLLECTIVES", False):
+            backend = "cuda:nccl,cpu:gloo"
+        return backend, DistributedType.MULTI_GPU
+
+    def __repr__(self) -> str:
+        return (
+            f"Distributed environment: {self.distributed_type}{('  Backend: ' + self.backend) if self.backend else ''}\n"
+            f"Num processes: {self.num_processes}\n"
+            f"Process index: {self.process_index}\n"
+            f"Local process index: {self.local_process_index}\n"
+            f"Device: {self.device}\n"
+        )
+
+    @staticmethod
+    def _reset_state():
+        PartialState._shared_state.clear()
+
+    @property
+    def initialized(self) -> bool:
+        return self._shared_state != {}
+
+    @property
+    def use_distributed(self):
+        return self.distributed_type != DistributedType.NO and self.num_processes > 1
+
+    @property
+    def is_last_process(self) -> bool:
+        return self.process_index == self.num_processes - 1
+
+    @property
+    def is_main_process(self) -> bool:
+        return self.process_index == 0
+
+    @property
+    def is_local_main_process(self) -> bool:
+        return self.local_process_index == 0
+
+    def wait_for_everyone(self):
+        """Barrier across all processes (no-op single-process). On RCCL the barrier is device-bound."""
+        if (
+            self.distributed_type in (DistributedType.MULTI_GPU, DistributedType.MULTI_CPU, DistributedType.FSDP)
+            and torch.distributed.is_initialized()
+            and self.num_processes > 1
+        ):
+            if self.backend == "nccl" and self.device is not None and self.device.type == "cuda":
+                torch.distributed.barrier(device_ids=[self.device.index])
+            else:
+                torch.distributed.barrier()
+
+    def _goes_first(self, is_main: bool):
+        if not is_main:
+            self.wait_for_everyone()
+        yield
+        if is_main:
+            self.wait_for_everyone()
+
+    @contextmanager
+    def split_between_processes(self, inputs: list | tuple | dict | torch.Tensor, apply_padding: bool = False):
+        """Give each process a contiguous slice of `inputs` (reference `state.py:423-512`).
+        With `apply_padding`, the last element is repeated so every process gets the same count."""
+        if self.num_processes == 1:
+            yield inputs
+            return
+        length = len(inputs)
+        if isinstance(inputs, dict):
+            length = len(inputs[list(inputs.keys())[0]])
+            if not all(len(v) == length for v in inputs.values()):
+                raise ValueError("All values in the dictionary must have the same length")
+        num_samples_per_process, num_extras = divmod(length, self.num_processes)
+        start_index = self.process_index * num_samples_per_process + min(self.process_index, num_extras)
+        end_index = start_index + num_samples_per_process + (1 if self.process_index < num_extras else 0)
+
+        def _split_values(inputs, start_index, end_index):
+            if isinstance(inputs, (list, tuple, torch.Tensor)):
+                if start_index >= len(inputs):
+                    result = inputs[-1:]
+                else:
+                    result = inputs[start_index:end_index]
+                if apply_padding:
+                    if isinstance(result, torch.Tensor):
+                        from .utils.operations import pad_across_processes, send_to_device
+
+                        tensorized_result = send_to_device(result, self.device)
+                        result = pad_across_processes(tensorized_result, pad_index=inputs[-1])
+                    else:
+                        result += [result[-1]] * (num_samples_per_process + (1 if num_extras > 0 else 0) - len(result))
+                return result
+            elif isinstance(inputs, dict):
+                for key in inputs.keys():
+                    inputs[key] = _split_values(inputs[key], start_index, end_index)
+                return inputs
+            else:
+                try:
+                    from datasets import Dataset
+
+                    if isinstance(inputs, Dataset):
+                        if start_index >= len(inputs):
+                            start_index = len(inputs) - 1
+                        if end_index > len(inputs):
+                            end_index = len(inputs)
+                        result_idcs = list(range(start_index, end_index))
+                        if apply_padding:
+                            result_idcs += [end_index - 1] * (
+                                num_samples_per_process + (1 if num_extras > 0 else 0) - len(result_idcs)
+                            )
+                        return inputs.select(result_idcs)
+                except ImportError:
+                    pass
+                return inputs
+
+        yield _split_values(inputs, start_index, end_index)
+
+    @contextmanager
+    def main_process_first(self):
+        yield from self._goes_first(self.is_main_process)
+
+    @contextmanager
+    def local_main_process_first(self):
+        yield from self._goes_first(self.is_local_main_process)
+
+    def on_main_process(self, function: Callable[..., Any] | None = None):
+        if not self.initialized:
+            raise ValueError("The `PartialState` or `Accelerator` must be initialized before calling this function.")
+        if self.is_main_process or not self.use_distributed:
+            return function
+        return do_nothing
+
+    def on_local_main_process(self, function: Callable[..., Any] | None = None):
+        if self.is_local_main_process or not self.use_distributed:
+            return function
+        return do_nothing
+
+    def on_last_process(self, function: Callable[..., Any]):
+        if self.is_last_process or not self.use_distributed:
+            return function
+        return do_nothing
+
+    def on_process(self, function: Callable[..., Any] | None = None, process_index: int | None = None):
+        if function is None:
+            return partial(self.on_process, process_index=process_index)
+        if (self.process_index == process_index) or (not self.use_distributed):
+            return function
+        return do_nothing
+
+    def on_local_process(self, function: Callable[..., Any] | None = None, local_process_index: int | None = None):
+        if function is None:
+            return partial(self.on_local_process, local_process_index=local_process_index)
+        if (self.local_process_index == local_process_index) or (not self.use_distributed):
+            return function
+        return do_nothing
+
+    def print(self, *args, **kwargs):
+        if self.is_local_main_process:
+            print(*args, **kwargs)
+
+    @property
+    def default_device(self) -> torch.device:
+        if torch.cuda.is_available() and not self._use_cpu:
+            return torch.device("cuda")
+        return torch.device("cpu")
+
+    def set_device(self):
+        if self.device is not None:
+            return
+        if self.distributed_type == DistributedType.NO:
+            self.device = torch.device("cpu") if self._use_cpu else self.default_device
+            return
+        if self._use_cpu:
+            self.device = torch.device("cpu")
+            return
+        self.device = torch.device("cuda", self.local_process_index % torch.cuda.device_count())
+        torch.cuda.set_device(self.device)
+
+    def destroy_process_group(self, group=None):
+        if self.fork_launched and group is None:
+            return
+        if torch.distributed.is_initialized():
+            torch.distributed.destroy_process_group(group)
+
+    def __getattr__(self, name: str):
+        if name in self._known_attrs:
+            raise AttributeError(
+                f"`PartialState` object has no attribute `{name}`. "
+                "This happens if `PartialState._reset_state()` was called and "
+                "an `Accelerator` or `PartialState` was not reinitialized."
+            )
+        raise AttributeError(f"'PartialState' object has no attribute '{name}'")
+
+
+class AcceleratorState:
+    """Training-level singleton: mixed precision, plugins, and the promoted distributed type."""
+
+    _shared_state = SharedDict()
+    _known_attrs = PartialState._known_attrs + [
+        "deepspeed_plugin",
+        "use_ipex",
+        "fsdp_plugin",
+        "megatron_lm_plugin",
+        "dynamo_plugin",
+        "parallelism_config",
+        "device_mesh",
+    ]
+
+    def __init__(
+        self,
+        mixed_precision: str | None = None,
+        cpu: bool = False,
+        dynamo_plugin=None,
+        deepspeed_plugin=None,
+        fsdp_plugin=None,
+        torch_tp_plugin=None,
+        megatron_lm_plugin=None,
+        parallelism_config=None,
+        _from_accelerator: bool = False,
+        **kwargs,
+    ):
+        self.__dict__ = self._shared_state
+        if parse_flag_from_env("ACCELERATE_USE_CPU"):
+            cpu = True
+        if PartialState._shared_state == {}:
+            PartialState(cpu, **kwargs)
+        self.__dict__.update(PartialState._shared_state)
+        self._check_initialized(mixed_precision, cpu)
+        if self.initialized and getattr(self, "_mixed_precision", None) is not None:
+            return
+        self._cpu = cpu
+        mixed_precision = (
+            parse_choice_from_env("ACCELERATE_MIXED_PRECISION", "no") if mixed_precision is None else mixed_precision.lower()
+        )
+        if mixed_precision == "fp8":
+            from .utils.environment import check_fp8_capability
+
+            if not cpu and torch.cuda.is_available() and not check_fp8_capability():
+                warnings.warn("fp8 requires gfx950 (MI355X); falling back to bf16.")
+                mixed_precision = "bf16"
+        self.dynamo_plugin = dynamo_plugin
+        self._mixed_precision = mixed_precision
+        self.deepspeed_plugins = None
+        self.use_ipex = False
+        self.torch_tp_plugin = torch_tp_plugin
+        self.parallelism_config = parallelism_config
+        self.device_mesh = None
+        self.megatron_lm_plugin = None
+        if megatron_lm_plugin is not None:
+            raise NotImplementedError("Megatron-LM is not supported on MI355X.")
+        if deepspeed_plugin is not None:
+            # ZeRO stages map onto our FSDP engine.
+            if fsdp_plugin is None:
+                fsdp_plugin = deepspeed_plugin.to_fsdp_plugin()
+            self.deepspeed_plugins = None
+        if os.environ.get("ACCELERATE_USE_FSDP", "false").lower() == "true" or fsdp_plugin is not None:
+            self.fsdp_plugin = fsdp_plugin
+        else:
+            self.fsdp_plugin = None
+        if parallelism_config is not None and parallelism_config.cp_enabled and fsdp_plugin is None:
+            if not parse_flag_from_env("ACCELERATE_ALLOW_CP_STANDALONE", False):
+                raise ValueError("Context parallelism requires FSDP2 (pass an `fsdp_plugin` with fsdp_version=2).")
+        if self.fsdp_plugin is not None and self.distributed_type in (
+            DistributedType.MULTI_GPU,
+            DistributedType.MULTI_CPU,
+            DistributedType.NO,
+        ):
+            # Single-device FSDP still runs the engine (fp32 master shards + bf16 compute params); on CPU the
+            # engine uses gloo, which is how the sharding logic is tested without GPUs.
+            self.distributed_type = DistributedType.FSDP
+            if self._mixed_precision != "no" and self.fsdp_plugin.mixed_precision_policy is None:
+                self.fsdp_plugin.set_mixed_precision(self._mixed_precision)
+        PartialState._shared_state["distributed_type"] = self.distributed_type
+
+    @property
+    def initialized(self) -> bool:
+        return self._shared_state != PartialState._shared_state
+
+    def __repr__(self):
+        repr = PartialState().__repr__() + f"\nMixed precision type: {self.mixed_precision}\n"
+        return repr
+
+    def _check_initialized(self, mixed_precision=None, cpu=None):
+        if self.initialized and getattr(self, "_mixed_precision", None) is not None:
+            err = "AcceleratorState has already been initialized and cannot be changed, restart your runtime completely and pass `{flag}` to `Accelerator()`."
+            if cpu and self.device.type != "cpu":
+                raise ValueError(err.format(flag="cpu=True"))
+            if mixed_precision is not None and mixed_precision != self._mixed_precision:
+                raise ValueError(err.format(flag=f"mixed_precision='{mixed_precision}'"))
+
+    @property
+    def mixed_precision(self):
+        return self._mixed_precision
+
+    @staticmethod
+    def _reset_state(reset_partial_state: bool = False):
+        AcceleratorState._shared_state.clear()
+        if reset_partial_state:
+            PartialState._reset_state()
+
+    def destroy_process_group(self, group=None):
+        PartialState().destroy_process_group(group)
+
+    @property
+    def fork_launched(self):
+        return PartialState().fork_launched
+
+    @property
+    def use_distributed(self):
+        return PartialState().use_distributed
+
+    @property
+    def is_fsdp2(self) -> bool:
+        return self.distributed_type == DistributedType.FSDP and self.fsdp_plugin.fsdp_version == 2
+
+    @property
+    def is_last_process(self) -> bool:
+        return PartialState().is_last_process
+
+    @property
+    def is_main_process(self) -> bool:
+        return PartialState().is_main_process
+
+    @property
+    def is_local_main_process(self) -> bool:
+        return PartialState().is_local_main_process
+
+    def wait_for_everyone(self):
+        PartialState().wait_for_everyone()
+
+    @contextmanager
+    def split_between_processes(self, inputs, apply_padding: bool = False):
+        with PartialState().split_between_processes(inputs, apply_padding=apply_padding) as inputs:
+            yield inputs
+
+    @contextmanager
+    def main_process_first(self):
+        with PartialState().main_process_first():
+            yield
+
+    @contextmanager
+    def local_main_process_first(self):
+        with PartialState().local_main_process_first():
+            yield
+
+    @property
+    def deepspeed_plugin(self):
+        return None
+
+    def print(self, *args, **kwargs):
+        PartialState().print(*args, **kwargs)
+
+    def __getattr__(self, name: str):
+        if name in self._known_attrs:
+            raise AttributeError(
+                f"`AcceleratorState` object has no attribute `{name}`. "
+                "This happens if `AcceleratorState._reset_state()` was called and "
+                "an `Accelerator` or `PartialState` was not reinitialized."
+            )
+        raise AttributeError(f"'AcceleratorState' object has no attribute '{name}'")
+
+
+class GradientState:
+    """Gradient-accumulation bookkeeping shared by the Accelerator, dataloaders, optimizer, scheduler.
+
+    Parity: reference `state.py:1225-1365`.
+    """
+
+    _shared_state = SharedDict()
+
+    def __init__(self, gradient_accumulation_plugin: GradientAccumulationPlugin | None = None):
+        self.__dict__ = self._shared_state
+        if not self.initialized:
+            self.sync_gradients = True
+            self._dataloader_references_ref = [None]
+            self.plugin_kwargs = (
+                gradient_accumulation_plugin.to_kwargs() if gradient_accumulation_plugin is not None else {}
+            )
+            self._is_xla_gradients_synced = False
+        if gradient_accumulation_plugin is not None and self.plugin_kwargs != gradient_accumulation_plugin.to_kwargs():
+            self.plugin_kwargs = gradient_accumulation_plugin.to_kwargs()
+
+    @property
+    def num_steps(self) -> int:
+        return self.plugin_kwargs.get("num_steps", 1)
+
+    @property
+    def adjust_scheduler(self) -> bool:
+        return self.plugin_kwargs.get("adjust_scheduler", False)
+
+    @property
+    def sync_with_dataloader(self) -> bool:
+        return self.plugin_kwargs.get("sync_with_dataloader", True)
+
+    @property
+    def initialized(self) -> bool:
+        return GradientState._shared_state != {}
+
+    @property
+    def end_of_dataloader(self) -> bool:
+        if not self.in_dataloader:
+            return False
+        return self.active_dataloader.end_of_dataloader
+
+    @property
+    def remainder(self) -> int:
+        if not self.in_dataloader:
+            return -1
+        return self.active_dataloader.remainder
+
+    def __repr__(self):
+        return (
+            f"Sync Gradients: {self.sync_gradients}\n"
+            f"At end of current dataloader: {self.end_of_dataloader}\n"
+            f"Extra samples added: {self.remainder}\n"
+            f"Gradient accumulation plugin: {self.plugin_kwargs}\n"
+        )
+
+    def _set_sync_gradients(self, sync_gradients):
+        self.sync_gradients = sync_gradients
+
+    def _add_dataloader(self, dataloader):
+        import weakref
+
+        self.dataloader_references.append(weakref.ref(dataloader))
+
+    def _remove_dataloader(self, dataloader):
+        refs = self.dataloader_references
+        for i in range(len(refs) - 1, -1, -1):
+            r = refs[i]
+            if r is not None and r() is dataloader:
+                refs.pop(i)
+                break
+
+    @property
+    def active_dataloader(self):
+        ref = self.dataloader_references[-1]
+        return ref() if ref is not None else None
+
+    @property
+    def dataloader_references(self):
+        return self._dataloader_references_ref
+
+    @dataloader_references.setter
+    def dataloader_references(self, references):
+        self._dataloader_references_ref = references
+
+    @property
+    def in_dataloader(self) -> bool:
+        return self.active_dataloader is not None
+
+    @staticmethod
+    def _reset_state():
+        GradientState._shared_state.clear()

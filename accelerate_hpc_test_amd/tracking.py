@@ -1,0 +1,459 @@
+"""Experiment trackers.
+
+Parity: `/root/reference/src/accelerate/tracking.py:45-1317` — `GeneralTracker` API (`name`, `requires_logging_directory`,
+`store_init_configuration`, `log`, `finish`, `tracker`), `on_main_process` gating, `filter_trackers`, and adapters
+for TensorBoard, WandB, Trackio, CometML, Aim, MLflow, ClearML, DVCLive, SwanLab (each imported lazily; only the
+ones installed can be selected). `JSONLTracker` is an always-available file tracker (one JSON line per `log`),
+used by the MI355X throughput benchmark and tests.
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import time
+from functools import wraps
+from typing import Any, Optional, Union
+
+from .logging import get_logger
+from .state import PartialState
+from .utils.dataclasses import LoggerType
+from .utils.imports import (
+    is_aim_available,
+    is_clearml_available,
+    is_comet_ml_available,
+    is_dvclive_available,
+    is_mlflow_available,
+    is_swanlab_available,
+    is_tensorboard_available,
+    is_trackio_available,
+    is_wandb_available,
+)
+
+logger = get_logger(__name__)
+
+
+def on_main_process(function):
+    """Run a tracker method only on the main process (when `main_process_only` is set on the tracker)."""
+
+    @wraps(function)
+    def execute_on_main_process(self, *args, **kwargs):
+        if getattr(self, "main_process_only", False):
+            return PartialState().on_main_process(function)(self, *args, **kwargs)
+        return function(self, *args, **kwargs)
+
+    return execute_on_main_process
+
+
+def get_available_trackers():
+    return _available_trackers
+
+
+class GeneralTracker:
+    """Base class for trackers. Subclasses set `name`, `requires_logging_directory`, and implement `tracker`,
+    `store_init_configuration`, `log` (and optionally `finish`)."""
+
+    main_process_only = True
+
+    def __init__(self, _blank=False):
+        if not _blank:
+            err = ""
+            if not hasattr(self, "name"):
+                err += "`name`"
+            if not hasattr(self, "requires_logging_directory"):
+                if len(err) > 0:
+                    err += ", "
+                err += "`requires_logging_directory`"
+            if "tracker" not in dir(self):
+                if len(err) > 0:
+                    err += ", "
+                err += "`tracker`"
+            if len(err) > 0:
+                raise NotImplementedError(
+                    f"The implementation for this tracker class is missing the following required attributes. Please define them in the class definition: {err}"
+                )
+
+    def start(self):
+        pass
+
+    def store_init_configuration(self, values: dict):
+        pass
+
+    def log(self, values: dict, step: Optional[int], **kwargs):
+        pass
+
+    def finish(self):
+        pass
+
+
+class JSONLTracker(GeneralTracker):
+    """Native tracker: appends `{"step": ..., "time": ..., **values}` lines to `<logging_dir>/<run_name>/metrics.jsonl`."""
+
+    name = "jsonl"
+    requires_logging_directory = True
+
+    @on_main_process
+    def __init__(self, run_name: str, logging_dir: Union[str, os.PathLike] = ".", **kwargs):
+        super().__init__()
+        self.run_name = run_name
+        self.dir = os.path.join(str(logging_dir), run_name)
+        os.makedirs(self.dir, exist_ok=True)
+        self.path = os.path.join(self.dir, "metrics.jsonl")
+        self._f = None
+
+    @property
+    def tracker(self):
+        return self.path
+
+    @on_main_process
+    def start(self):
+        self._f = open(self.path, "a")
+
+    @on_main_process
+    def store_init_configuration(self, values: dict):
+        with open(os.path.join(self.dir, "config.json"), "w") as f:
+            json.dump({k: (v if isinstance(v, (int, float, str, bool, type(None), list, dict)) else str(v)) for k, v in values.items()}, f, indent=2)
+
+    @on_main_process
+    def log(self, values: dict, step: Optional[int] = None, **kwargs):
+        if self._f is None:
+            self.start()
+        rec = {"step": step, "time": time.time()}
+        for k, v in values.items():
+            if hasattr(v, "item"):
+                v = v.item()
+            rec[k] = v
+        self._f.write(json.dumps(rec) + "\n")
+        self._f.flush()
+
+    @on_main_process
+    def finish(self):
+        if self._f is not None:
+            self._f.close()
+            self._f = None
+
+
+class TensorBoardTracker(GeneralTracker):
+    name = "tensorboard"
+    requires_logging_directory = True
+
+    @on_main_process
+    def __init__(self, run_name: str, logging_dir: Union[str, os.PathLike], **kwargs):
+        super().__init__()
+        self.run_name = run_name
+        self.logging_dir = os.path.join(logging_dir, run_name)
+        self.init_kwargs = kwargs
+
+    @on_main_process
+    def start(self):
+        try:
+            from torch.utils import tensorboard
+        except ModuleNotFoundError:
+            import tensorboardX as tensorboard
+        self.writer = tensorboard.SummaryWriter(self.logging_dir, **self.init_kwargs)
+
+    @property
+    def tracker(self):
+        return self.writer
+
+    @on_main_process
+    def store_init_configuration(self, values: dict):
+        self.writer.add_hparams(values, metric_dict={})
+        self.writer.flush()
+        project_run_name = time.time()
+        dir_name = os.path.join(self.logging_dir, str(project_run_name))
+        os.makedirs(dir_name, exist_ok=True)
+        import yaml
+
+        with open(os.path.join(dir_name, "hparams.yml"), "w") as outfile:
+            yaml.safe_dump({k: (v if isinstance(v, (int, float, str, bool)) else str(v)) for k, v in values.items()}, outfile)
+
+    @on_main_process
+    def log(self, values: dict, step: Optional[int] = None, **kwargs):
+        for k, v in values.items():
+            if isinstance(v, (int, float)):
+                self.writer.add_scalar(k, v, global_step=step, **kwargs)
+            elif isinstance(v, str):
+                self.writer.add_text(k, v, global_step=step, **kwargs)
+            elif isinstance(v, dict):
+                self.writer.add_scalars(k, v, global_step=step, **kwargs)
+        self.writer.flush()
+
+    @on_main_process
+    def finish(self):
+        self.writer.close()
+
+
+class _LazyTracker(GeneralTracker):
+    """Adapter for a tracker library with an init/log/finish API, imported only when selected."""
+
+    module_name = ""
+    requires_logging_directory = False
+
+    @on_main_process
+    def __init__(self, run_name: str, **kwargs):
+        super().__init__()
+        self.run_name = run_name
+        self.init_kwargs = kwargs
+        self.run = None
+
+    @property
+    def tracker(self):
+        return self.run
+
+
+class WandBTracker(_LazyTracker):
+    name = "wandb"
+    main_process_only = False
+
+    @on_main_process
+    def start(self):
+        import wandb
+
+        self.run = wandb.init(project=self.run_name, **self.init_kwargs)
+
+    @on_main_process
+    def store_init_configuration(self, values: dict):
+        import wandb
+
+        wandb.config.update(values, allow_val_change=True)
+
+    @on_main_process
+    def log(self, values: dict, step: Optional[int] = None, **kwargs):
+        self.run.log(values, step=step, **kwargs)
+
+    @on_main_process
+    def finish(self):
+        self.run.finish()
+
+
+class TrackioTracker(_LazyTracker):
+    name = "trackio"
+
+    @on_main_process
+    def start(self):
+        import trackio
+
+        self.run = trackio.init(project=self.run_name, **self.init_kwargs)
+
+    @on_main_process
+    def log(self, values, step=None, **kwargs):
+        self.run.log(values, **kwargs)
+
+    @on_main_process
+    def finish(self):
+        self.run.finish()
+
+
+class CometMLTracker(_LazyTracker):
+    name = "comet_ml"
+
+    @on_main_process
+    def start(self):
+        import comet_ml
+
+        self.run = comet_ml.start(project_name=self.run_name, **self.init_kwargs)
+
+    @on_main_process
+    def store_init_configuration(self, values):
+        self.run.log_parameters(values)
+
+    @on_main_process
+    def log(self, values, step=None, **kwargs):
+        self.run.log_metrics(values, step=step, **kwargs)
+
+    @on_main_process
+    def finish(self):
+        self.run.end()
+
+
+class AimTracker(_LazyTracker):
+    name = "aim"
+    requires_logging_directory = True
+
+    @on_main_process
+    def __init__(self, run_name: str, logging_dir=".", **kwargs):
+        super().__init__(run_name, **kwargs)
+        self.aim_repo_path = logging_dir
+
+    @on_main_process
+    def start(self):
+        from aim import Run
+
+        self.run = Run(repo=self.aim_repo_path, **self.init_kwargs)
+        self.run.name = self.run_name
+
+    @on_main_process
+    def store_init_configuration(self, values):
+        self.run["hparams"] = values
+
+    @on_main_process
+    def log(self, values, step=None, **kwargs):
+        for key, value in values.items():
+            self.run.track(value, name=key, step=step, **kwargs)
+
+    @on_main_process
+    def finish(self):
+        self.run.close()
+
+
+class MLflowTracker(_LazyTracker):
+    name = "mlflow"
+    requires_logging_directory = False
+
+    @on_main_process
+    def start(self):
+        import mlflow
+
+        exp = mlflow.set_experiment(self.run_name)
+        self.run = mlflow.start_run(experiment_id=exp.experiment_id, **self.init_kwargs)
+
+    @on_main_process
+    def store_init_configuration(self, values):
+        import mlflow
+
+        mlflow.log_params({k: str(v)[:250] for k, v in values.items()})
+
+    @on_main_process
+    def log(self, values, step=None, **kwargs):
+        import mlflow
+
+        mlflow.log_metrics({k: v for k, v in values.items() if isinstance(v, (int, float))}, step=step)
+
+    @on_main_process
+    def finish(self):
+        import mlflow
+
+        mlflow.end_run()
+
+
+class ClearMLTracker(_LazyTracker):
+    name = "clearml"
+
+    @on_main_process
+    def start(self):
+        from clearml import Task
+
+        self.run = Task.init(project_name=self.run_name, **self.init_kwargs)
+
+    @on_main_process
+    def store_init_configuration(self, values):
+        self.run.connect_configuration(values)
+
+    @on_main_process
+    def log(self, values, step=None, **kwargs):
+        clearml_logger = self.run.get_logger()
+        for k, v in values.items():
+            if isinstance(v, (int, float)):
+                title, _, series = k.partition("_")
+                clearml_logger.report_scalar(title=title, series=series or title, value=v, iteration=step or 0)
+
+    @on_main_process
+    def finish(self):
+        self.run.close()
+
+
+class DVCLiveTracker(_LazyTracker):
+    name = "dvclive"
+
+    @on_main_process
+    def start(self):
+        from dvclive import Live
+
+        self.run = Live(**self.init_kwargs)
+
+    @on_main_process
+    def store_init_configuration(self, values):
+        self.run.log_params(values)
+
+    @on_main_process
+    def log(self, values, step=None, **kwargs):
+        if step is not None:
+            self.run.step = step
+        for k, v in values.items():
+            self.run.log_metric(k, v, **kwargs)
+        self.run.next_step()
+
+    @on_main_process
+    def finish(self):
+        self.run.end()
+
+
+class SwanLabTracker(_LazyTracker):
+    name = "swanlab"
+
+    @on_main_process
+    def start(self):
+        import swanlab
+
+        self.run = swanlab.init(project=self.run_name, **self.init_kwargs)
+
+    @on_main_process
+    def store_init_configuration(self, values):
+        import swanlab
+
+        swanlab.config.update(values, allow_val_change=True)
+
+    @on_main_process
+    def log(self, values, step=None, **kwargs):
+        self.run.log(values, step=step, **kwargs)
+
+    @on_main_process
+    def finish(self):
+        self.run.finish()
+
+
+LOGGER_TYPE_TO_CLASS = {
+    "aim": AimTracker,
+    "comet_ml": CometMLTracker,
+    "mlflow": MLflowTracker,
+    "tensorboard": TensorBoardTracker,
+    "wandb": WandBTracker,
+    "clearml": ClearMLTracker,
+    "dvclive": DVCLiveTracker,
+    "swanlab": SwanLabTracker,
+    "trackio": TrackioTracker,
+    "jsonl": JSONLTracker,
+}
+
+_available_trackers = ["jsonl"]
+for _name, _check in (
+    ("tensorboard", is_tensorboard_available),
+    ("wandb", is_wandb_available),
+    ("comet_ml", is_comet_ml_available),
+    ("aim", is_aim_available),
+    ("mlflow", is_mlflow_available),
+    ("clearml", is_clearml_available),
+    ("dvclive", is_dvclive_available),
+    ("swanlab", is_swanlab_available),
+    ("trackio", is_trackio_available),
+):
+    if _check():
+        _available_trackers.append(_name)
+
+
+def filter_trackers(log_with: Optional[list[Union[str, LoggerType, GeneralTracker]]] = None, logging_dir: Union[str, os.PathLike] = None):
+    """Resolve `log_with` to the list of usable trackers (`"all"` = every installed one)."""
+    loggers = []
+    if log_with is not None:
+        if not isinstance(log_with, (list, tuple)):
+            log_with = [log_with]
+        if "all" in log_with or LoggerType.ALL in log_with:
+            loggers = [o for o in log_with if issubclass(type(o), GeneralTracker)] + get_available_trackers()
+        else:
+            for log_type in log_with:
+                if log_type not in LoggerType and not issubclass(type(log_type), GeneralTracker):
+                    raise ValueError(f"Unsupported logging capability: {log_type}. Choose between {LoggerType.list()}")
+                if issubclass(type(log_type), GeneralTracker):
+                    loggers.append(log_type)
+                else:
+                    log_type = LoggerType(log_type)
+                    if log_type not in loggers:
+                        if str(log_type) in get_available_trackers():
+                            tracker_init = LOGGER_TYPE_TO_CLASS[str(log_type)]
+                            if tracker_init.requires_logging_directory and logging_dir is None:
+                                raise ValueError(f"Logging with `{log_type}` requires a `logging_dir` to be passed in.")
+                            loggers.append(log_type)
+                        else:
+                            logger.debug(f"Tried adding logger {log_type}, but package is unavailable in the system.")
+    return loggers

@@ -1,0 +1,589 @@
+"""Collective and nested-structure operations (L2 of the layer map).
+
+Parity: `/root/reference/src/accelerate/utils/operations.py:85-871` — same function names and semantics
+(`gather`, `gather_object`, `broadcast`, `broadcast_object_list`, `reduce`, `pad_across_processes`,
+`send_to_device`, `concatenate`, `slice_tensors`, `find_batch_size`, `convert_to_fp32`, debug-mode
+`verify_operation`).
+
+MI355X-specific design:
+* On GPU every tensor collective goes to RCCL (`torch.distributed` "nccl" backend) on the current HIP
+  stream. Each RCCL launch costs tens of microseconds, so nested structures of tensors are **coalesced**:
+  `reduce`/`gather`/`broadcast` of a dict/list of same-dtype tensors flatten everything into one buffer
+  and issue ONE collective (the reference issues one per leaf).
+* Shape exchange for `pad_across_processes` / `copy_tensor_to_devices` all-gathers a tiny int64 vector
+  instead of the reference's 4 MB int32 all-reduce (`operations.py:496-535`).
+"""
+
+from __future__ import annotations
+
+import pickle
+from collections.abc import Mapping
+from contextlib import contextmanager, nullcontext
+from functools import update_wrapper, wraps
+from typing import Any
+
+import torch
+
+from .dataclasses import DistributedType, TensorInformation
+
+
+def PartialState():  # noqa: N802 - lazy accessor (utils is imported by state.py; avoid the import cycle)
+    from ..state import PartialState as _PartialState
+
+    return _PartialState()
+
+
+class DistributedOperationException(Exception):
+    """Raised (in debug mode) when ranks call a collective with mismatched shapes instead of hanging RCCL."""
+
+
+def is_torch_tensor(tensor):
+    return isinstance(tensor, torch.Tensor)
+
+
+def is_tensor_information(tensor_info):
+    return isinstance(tensor_info, TensorInformation)
+
+
+def is_namedtuple(data):
+    return isinstance(data, tuple) and hasattr(data, "_asdict") and hasattr(data, "_fields")
+
+
+def honor_type(obj, generator):
+    """Rebuild `obj`'s container type from `generator` (namedtuples need positional construction)."""
+    if is_namedtuple(obj):
+        return type(obj)(*list(generator))
+    return type(obj)(generator)
+
+
+def recursively_apply(func, data, *args, test_type=is_torch_tensor, error_on_other_type=False, **kwargs):
+    """Apply `func` to every leaf of a nested list/tuple/dict structure satisfying `test_type`."""
+    if isinstance(data, (tuple, list)):
+        return honor_type(
+            data,
+            (
+                recursively_apply(func, o, *args, test_type=test_type, error_on_other_type=error_on_other_type, **kwargs)
+                for o in data
+            ),
+        )
+    elif isinstance(data, Mapping):
+        return type(data)(
+            {
+                k: recursively_apply(func, v, *args, test_type=test_type, error_on_other_type=error_on_other_type, **kwargs)
+                for k, v in data.items()
+            }
+        )
+    elif test_type(data):
+        return func(data, *args, **kwargs)
+    elif error_on_other_type:
+        raise TypeError(
+            f"Unsupported types ({type(data)}) passed to `{func.__name__}`. Only nested list/tuple/dicts of "
+            f"objects that are valid for `{test_type.__name__}` should be passed."
+        )
+    return data
+
+
+def send_to_device(tensor, device, non_blocking=False, skip_keys=None):
+    """Recursively move tensors (and objects with a `.to`) to `device`."""
+    if is_torch_tensor(tensor) or hasattr(tensor, "to"):
+        if device == "npu":
+            device = "npu:0"
+        try:
+            return tensor.to(device, non_blocking=non_blocking)
+        except TypeError:
+            return tensor.to(device)
+        except AssertionError as error:
+            raise error
+    elif isinstance(tensor, (tuple, list)):
+        return honor_type(tensor, (send_to_device(t, device, non_blocking=non_blocking, skip_keys=skip_keys) for t in tensor))
+    elif isinstance(tensor, Mapping):
+        if isinstance(skip_keys, str):
+            skip_keys = [skip_keys]
+        elif skip_keys is None:
+            skip_keys = []
+        return type(tensor)(
+            {
+                k: t if k in skip_keys else send_to_device(t, device, non_blocking=non_blocking, skip_keys=skip_keys)
+                for k, t in tensor.items()
+            }
+        )
+    return tensor
+
+
+def get_data_structure(data):
+    """Replace every tensor by its `TensorInformation` (shape + dtype)."""
+
+    def _get_data_structure(tensor):
+        return TensorInformation(shape=tensor.shape, dtype=tensor.dtype)
+
+    return recursively_apply(_get_data_structure, data)
+
+
+def get_shape(data):
+    def _get_shape(tensor):
+        return list(tensor.shape)
+
+    return recursively_apply(_get_shape, data)
+
+
+def initialize_tensors(data_structure):
+    """Allocate empty tensors matching a structure of `TensorInformation`."""
+
+    def _initialize_tensor(tensor_info):
+        return torch.empty(*tensor_info.shape, dtype=tensor_info.dtype)
+
+    return recursively_apply(_initialize_tensor, data_structure, test_type=is_tensor_information)
+
+
+def find_batch_size(data):
+    """First dimension of the first tensor found in `data`."""
+    if isinstance(data, (tuple, list, Mapping)) and (len(data) == 0):
+        raise ValueError(f"Cannot find the batch size from empty {type(data)}.")
+    if isinstance(data, (tuple, list)):
+        return find_batch_size(data[0])
+    elif isinstance(data, Mapping):
+        for k in data.keys():
+            return find_batch_size(data[k])
+    elif not isinstance(data, torch.Tensor):
+        raise TypeError(f"Can only find the batch size of tensors but got {type(data)}.")
+    return data.shape[0]
+
+
+def ignorant_find_batch_size(data):
+    try:
+        return find_batch_size(data)
+    except (ValueError, TypeError):
+        pass
+    return None
+
+
+def listify(data):
+    """Recursively convert tensors to python lists/scalars."""
+
+    def _convert_to_list(tensor):
+        tensor = tensor.detach().cpu()
+        if tensor.dtype == torch.bfloat16:
+            tensor = tensor.to(torch.float32)
+        return tensor.tolist()
+
+    return recursively_apply(_convert_to_list, data)
+
+
+# ------------------------------------------------------------------------------------------------------
+# Debug-mode cross-rank verification
+# ------------------------------------------------------------------------------------------------------
+def verify_operation(function):
+    """In debug mode (`ACCELERATE_DEBUG_MODE=1`) all-gather every rank's tensor shapes before the collective
+    and raise `DistributedOperationException` on mismatch (reference `operations.py:355-396`)."""
+
+    @wraps(function)
+    def wrapper(*args, **kwargs):
+        if PartialState().distributed_type == DistributedType.NO or not PartialState().debug:
+            return function(*args, **kwargs)
+        operation = f"{function.__module__}.{function.__name__}"
+        if "tensor" in kwargs:
+            tensor = kwargs["tensor"]
+        else:
+            tensor = args[0]
+        if PartialState().device.type != find_device(tensor).type:
+            raise DistributedOperationException(
+                f"One or more of the tensors passed to {operation} were not on the {tensor.device.type} while the "
+                f"`Accelerator` is configured for {PartialState().device.type}. Please move it to the "
+                f"{PartialState().device.type} before calling {operation}."
+            )
+        shapes = get_shape(tensor)
+        output = gather_object([shapes])
+        if output[0] is not None:
+            are_same = output.count(output[0]) == len(output)
+            if not are_same:
+                process_shape_str = "\n  - ".join([f"Process {i}: {shape}" for i, shape in enumerate(output)])
+                raise DistributedOperationException(
+                    f"Cannot apply desired operation due to shape mismatches. All shapes across devices must be valid."
+                    f"\n\nOperation: `{operation}`\nInput shapes:\n  - {process_shape_str}"
+                )
+        return function(*args, **kwargs)
+
+    return wrapper
+
+
+def chained_operation(function):
+    """Re-raise `DistributedOperationException` with the outer operation's name."""
+
+    @wraps(function)
+    def wrapper(*args, **kwargs):
+        try:
+            return function(*args, **kwargs)
+        except DistributedOperationException as e:
+            operation = f"{function.__module__}.{function.__name__}"
+            raise DistributedOperationException(
+                f"Error found while calling `{operation}`. Please see the earlier error for more details."
+            ) from e
+
+    return wrapper
+
+
+def find_device(data):
+    if isinstance(data, Mapping):
+        for obj in data.values():
+            device = find_device(obj)
+            if device is not None:
+                return device
+    elif isinstance(data, (tuple, list)):
+        for obj in data:
+            device = find_device(obj)
+            if device is not None:
+                return device
+    elif isinstance(data, torch.Tensor):
+        return data.device
+
+
+# ------------------------------------------------------------------------------------------------------
+# Coalescing helpers: one collective for a whole nested structure
+# ------------------------------------------------------------------------------------------------------
+def _leaves(data, out):
+    if isinstance(data, (tuple, list)):
+        for d in data:
+            _leaves(d, out)
+    elif isinstance(data, Mapping):
+        for v in data.values():
+            _leaves(v, out)
+    elif isinstance(data, torch.Tensor):
+        out.append(data)
+    return out
+
+
+def _rebuild(data, it):
+    if isinstance(data, (tuple, list)):
+        return honor_type(data, (_rebuild(d, it) for d in data))
+    elif isinstance(data, Mapping):
+        return type(data)({k: _rebuild(v, it) for k, v in data.items()})
+    elif isinstance(data, torch.Tensor):
+        return next(it)
+    return data
+
+
+def _coalescable(leaves):
+    if len(leaves) < 2:
+        return False
+    dev, dt = leaves[0].device, leaves[0].dtype
+    return all(t.device == dev and t.dtype == dt for t in leaves)
+
+
+# ------------------------------------------------------------------------------------------------------
+# gather
+# ------------------------------------------------------------------------------------------------------
+def _gpu_gather_one(tensor: torch.Tensor) -> torch.Tensor:
+    state = PartialState()
+    if tensor.ndim == 0:
+        tensor = tensor.clone()[None]
+    if not tensor.is_contiguous():
+        tensor = tensor.contiguous()
+    if state.backend is not None and state.backend.startswith("gloo"):
+        outs = [torch.empty_like(tensor) for _ in range(state.num_processes)]
+        torch.distributed.all_gather(outs, tensor)
+        return torch.cat(outs, dim=0)
+    out = torch.empty(state.num_processes * tensor.numel(), dtype=tensor.dtype, device=tensor.device)
+    torch.distributed.all_gather_into_tensor(out, tensor.reshape(-1))
+    return out.view(-1, *tensor.size()[1:])
+
+
+def _gpu_gather(tensor):
+    leaves = _leaves(tensor, [])
+    if not leaves:
+        return tensor
+    if _coalescable(leaves) and all(t.ndim > 0 for t in leaves):
+        # One all-gather for the whole structure: flatten, gather, then de-interleave per rank.
+        state = PartialState()
+        flat = torch.cat([t.reshape(-1) for t in leaves])
+        gathered = _gpu_gather_one(flat).view(state.num_processes, -1)
+        outs, off = [], 0
+        for t in leaves:
+            n = t.numel()
+            outs.append(gathered[:, off : off + n].reshape(state.num_processes * t.shape[0], *t.shape[1:]))
+            off += n
+        return _rebuild(tensor, iter(outs))
+    return recursively_apply(_gpu_gather_one, tensor, error_on_other_type=True)
+
+
+@verify_operation
+def gather(tensor):
+    """Concatenate `tensor` (nested) from all processes along dim 0."""
+    if PartialState().distributed_type in (DistributedType.MULTI_GPU, DistributedType.MULTI_CPU, DistributedType.FSDP) and PartialState().num_processes > 1:
+        return _gpu_gather(tensor)
+    return tensor
+
+
+def _gpu_gather_object(object: Any):
+    output_objects = [None for _ in range(PartialState().num_processes)]
+    torch.distributed.all_gather_object(output_objects, object)
+    # all_gather_object returns a list of lists; flatten them.
+    return [x for y in output_objects for x in y]
+
+
+def gather_object(object: Any):
+    """Gather picklable objects (lists are concatenated) from all processes."""
+    if PartialState().distributed_type == DistributedType.NO or PartialState().num_processes == 1:
+        return object
+    return _gpu_gather_object(object)
+
+
+# ------------------------------------------------------------------------------------------------------
+# broadcast
+# ------------------------------------------------------------------------------------------------------
+def _gpu_broadcast(data, src=0):
+    leaves = _leaves(data, [])
+    if _coalescable(leaves):
+        flat = torch.cat([t.reshape(-1) for t in leaves])
+        torch.distributed.broadcast(flat, src=src)
+        outs, off = [], 0
+        for t in leaves:
+            n = t.numel()
+            t.copy_(flat[off : off + n].view_as(t))
+            outs.append(t)
+            off += n
+        return _rebuild(data, iter(outs))
+
+    def _gpu_broadcast_one(tensor, src=0):
+        torch.distributed.broadcast(tensor, src=src)
+        return tensor
+
+    return recursively_apply(_gpu_broadcast_one, data, error_on_other_type=True, src=src)
+
+
+@verify_operation
+def broadcast(tensor, from_process: int = 0):
+    """In-place broadcast of (nested) tensors from `from_process`."""
+    if PartialState().distributed_type in (DistributedType.MULTI_GPU, DistributedType.MULTI_CPU, DistributedType.FSDP) and PartialState().num_processes > 1:
+        return _gpu_broadcast(tensor, src=from_process)
+    return tensor
+
+
+def broadcast_object_list(object_list, from_process: int = 0):
+    if PartialState().distributed_type != DistributedType.NO and PartialState().num_processes > 1:
+        torch.distributed.broadcast_object_list(object_list, src=from_process)
+    return object_list
+
+
+def slice_tensors(data, tensor_slice, process_index=None, num_processes=None):
+    def _slice_tensor(tensor, tensor_slice):
+        return tensor[tensor_slice]
+
+    return recursively_apply(_slice_tensor, data, tensor_slice)
+
+
+def concatenate(data, dim=0):
+    """Concatenate a list of (nested, identically structured) tensors."""
+    if isinstance(data[0], (tuple, list)):
+        return honor_type(data[0], (concatenate([d[i] for d in data], dim=dim) for i in range(len(data[0]))))
+    elif isinstance(data[0], Mapping):
+        return type(data[0])({k: concatenate([d[k] for d in data], dim=dim) for k in data[0].keys()})
+    elif not isinstance(data[0], torch.Tensor):
+        raise TypeError(f"Can only concatenate tensors but got {type(data[0])}")
+    return torch.cat(data, dim=dim)
+
+
+class CannotPadNestedTensorWarning(UserWarning):
+    pass
+
+
+def _all_sizes(tensor) -> torch.Tensor:
+    """All ranks' shapes as a [W, ndim] int64 tensor (one tiny all-gather)."""
+    size = torch.tensor(tensor.shape, device=tensor.device, dtype=torch.int64)[None]
+    return gather(size)
+
+
+@chained_operation
+def pad_across_processes(tensor, dim=0, pad_index=0, pad_first=False):
+    """Pad every tensor along `dim` to the largest size among processes so it can be gathered."""
+
+    def _pad_across_processes(tensor, dim=0, pad_index=0, pad_first=False):
+        if getattr(tensor, "is_nested", False):
+            import warnings
+
+            warnings.warn("Cannot pad nested tensors without more information. Leaving unprocessed.", CannotPadNestedTensorWarning)
+            return tensor
+        if dim >= len(tensor.shape) or dim < -len(tensor.shape):
+            return tensor
+        if dim < 0:
+            dim += len(tensor.shape)
+        sizes = _all_sizes(tensor).cpu()
+        max_size = int(sizes[:, dim].max())
+        if max_size == tensor.shape[dim]:
+            return tensor
+        old_size = tensor.shape
+        new_size = list(old_size)
+        new_size[dim] = max_size
+        new_tensor = tensor.new_zeros(tuple(new_size)) + pad_index
+        if pad_first:
+            indices = tuple(
+                slice(max_size - old_size[dim], max_size) if i == dim else slice(None) for i in range(len(new_size))
+            )
+        else:
+            indices = tuple(slice(0, old_size[dim]) if i == dim else slice(None) for i in range(len(new_size)))
+        new_tensor[indices] = tensor
+        return new_tensor
+
+    return recursively_apply(
+        _pad_across_processes, tensor, error_on_other_type=True, dim=dim, pad_index=pad_index, pad_first=pad_first
+    )
+
+
+def pad_input_tensors(tensor, batch_size, num_processes, dim=0):
+    """Pad the batch dimension so it divides evenly by `num_processes` (for `split_between_processes`)."""
+
+    def _pad_input_tensors(tensor, batch_size, num_processes, dim=0):
+        remainder = batch_size // num_processes
+        last_inputs = batch_size - (remainder * num_processes)
+        if batch_size // num_processes == 0:
+            to_pad = num_processes - batch_size
+        else:
+            to_pad = num_processes - (batch_size // num_processes)
+        if last_inputs > to_pad & to_pad < 1:
+            to_pad = last_inputs - to_pad
+        old_size = tensor.shape
+        new_size = list(old_size)
+        new_size[0] = batch_size + to_pad
+        new_tensor = tensor.new_zeros(tuple(new_size))
+        indices = tuple(slice(0, old_size[dim]) if i == dim else slice(None) for i in range(len(new_size)))
+        new_tensor[indices] = tensor
+        return new_tensor
+
+    return recursively_apply(
+        _pad_input_tensors, tensor, error_on_other_type=True, batch_size=batch_size, num_processes=num_processes, dim=dim
+    )
+
+
+def gather_tensor_shape(tensor):
+    """Shape of `tensor` on the process that holds it (others pass None) — used by `copy_tensor_to_devices`."""
+    state = PartialState()
+    shape = [-1] * 8
+    if tensor is not None:
+        shape[: tensor.ndim] = list(tensor.shape)
+        shape.append(tensor.ndim)
+    else:
+        shape.append(-1)
+    dev = state.device
+    t = torch.tensor(shape, dtype=torch.int64, device=dev)
+    allt = gather(t).view(state.num_processes, -1)
+    for row in allt.tolist():
+        if row[-1] >= 0:
+            return row[: row[-1]]
+    return None
+
+
+def copy_tensor_to_devices(tensor=None) -> torch.Tensor:
+    """Make the tensor held by exactly one process available on all (used by pipeline inference)."""
+    state = PartialState()
+    shape = gather_tensor_shape(tensor)
+    if tensor is None:
+        dtype_code = torch.tensor([-1], device=state.device)
+    else:
+        dtype_code = torch.tensor([_DTYPES.index(tensor.dtype)], device=state.device)
+    codes = gather(dtype_code).tolist()
+    dtype = _DTYPES[max(codes)]
+    if tensor is None:
+        tensor = torch.zeros(shape, dtype=dtype, device=state.device)
+    return reduce(tensor, reduction="sum")
+
+
+_DTYPES = [torch.float32, torch.float16, torch.bfloat16, torch.int64, torch.int32, torch.int8, torch.uint8, torch.bool, torch.float64]
+
+
+# ------------------------------------------------------------------------------------------------------
+# reduce
+# ------------------------------------------------------------------------------------------------------
+@verify_operation
+def reduce(tensor, reduction="mean", scale=1.0):
+    """All-reduce (nested) tensors with `reduction` in {"sum", "mean"}; returns new tensors.
+
+    Nested structures of same-dtype tensors are reduced with a single collective."""
+
+    state = PartialState()
+    if state.distributed_type == DistributedType.NO or state.num_processes == 1:
+        def _scale_only(t):
+            t = t.clone()
+            if scale != 1.0:
+                t *= scale
+            return t
+
+        return recursively_apply(_scale_only, tensor, error_on_other_type=True)
+
+    def _finish(t):
+        if reduction == "mean":
+            t /= state.num_processes
+        if scale != 1.0:
+            t *= scale
+        return t
+
+    leaves = _leaves(tensor, [])
+    if _coalescable(leaves):
+        flat = torch.cat([t.reshape(-1) for t in leaves])
+        torch.distributed.all_reduce(flat, torch.distributed.ReduceOp.SUM)
+        _finish(flat)
+        outs, off = [], 0
+        for t in leaves:
+            n = t.numel()
+            outs.append(flat[off : off + n].view_as(t).clone())
+            off += n
+        return _rebuild(tensor, iter(outs))
+
+    def _reduce_across_processes(t):
+        cloned = t.clone()
+        torch.distributed.all_reduce(cloned, torch.distributed.ReduceOp.SUM)
+        return _finish(cloned)
+
+    return recursively_apply(_reduce_across_processes, tensor, error_on_other_type=True)
+
+
+# ------------------------------------------------------------------------------------------------------
+# fp32 conversion of model outputs under mixed precision
+# ------------------------------------------------------------------------------------------------------
+def convert_to_fp32(tensor):
+    def _convert_to_fp32(tensor):
+        return tensor.float()
+
+    def _is_fp16_bf16_tensor(tensor):
+        return (is_torch_tensor(tensor) or hasattr(tensor, "dtype")) and tensor.dtype in (torch.float16, torch.bfloat16)
+
+    return recursively_apply(_convert_to_fp32, tensor, test_type=_is_fp16_bf16_tensor)
+
+
+class ConvertOutputsToFp32:
+    """Picklable wrapper casting a forward's fp16/bf16 outputs to fp32."""
+
+    def __init__(self, model_forward):
+        self.model_forward = model_forward
+        update_wrapper(self, model_forward)
+
+    def __call__(self, *args, **kwargs):
+        return convert_to_fp32(self.model_forward(*args, **kwargs))
+
+    def __getstate__(self):
+        raise pickle.PicklingError(
+            "Cannot pickle a prepared model with automatic mixed precision, please unwrap the model with "
+            "`Accelerator.unwrap_model(model)` before pickling it."
+        )
+
+
+def convert_outputs_to_fp32(model_forward):
+    model_forward = ConvertOutputsToFp32(model_forward)
+
+    def forward(*args, **kwargs):
+        return model_forward(*args, **kwargs)
+
+    forward.__wrapped__ = model_forward
+    return forward
+
+
+@contextmanager
+def GatheredParameters(params, modifier_rank=None, fwd_module=None, enabled=True):
+    """No-op context (the reference uses it for DeepSpeed ZeRO-3). Our FSDP engine exposes
+    `summon_full_params` for the equivalent purpose."""
+    yield
+
+
+def get_grad_scaler(distributed_type: DistributedType = None, **kwargs):
+    """fp16 GradScaler (bf16 needs none)."""
+    if torch.cuda.is_available():
+        return torch.amp.GradScaler("cuda", **kwargs)
+    return torch.amp.GradScaler("cpu", **kwargs)

@@ -1,0 +1,161 @@
+#!/usr/bin/env python
+"""Headline benchmark: Llama-3-8B FSDP2 bf16 training throughput (tokens/s, whole node) on 1/2/4/8 MI355X.
+
+Reference workload: `examples/torch_native_parallelism/fsdp2_fp8.py` — Llama-3.1-8B, seq 8192,
+micro-batch 1 per device, AdamW(lr=1e-5), FSDP2 transformer-wrap of LlamaDecoderLayer, bf16 mixed precision,
+forward / backward / optimizer.step / zero_grad each step. Same here, on this framework's stack:
+`Accelerator(fsdp_plugin=FSDP2, mixed_precision="bf16")` → native FSDP engine (RCCL all-gather / reduce-scatter per
+decoder layer on side streams), HIP kernels (flash attention, RMSNorm, RoPE, SwiGLU, cross-entropy, fused AdamW),
+hipBLASLt GEMMs. Synthetic token data (random ids) and random-init weights (no network access).
+
+Usage: python bench.py [--gpus N --steps K --warmup W]   (N>1: launched by torch.distributed.run, one rank per GPU)
+Prints ONE JSON line on rank 0.
+"""
+
+import argparse
+import json
+import os
+import time
+
+import torch
+
+BASELINE_TOKENS_PER_SEC_PER_DEVICE = 8000.0  # BASELINE.md P1 (8x H100, Llama-3.1-8B FSDP2 bf16)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--model", default="llama3-8b")
+    p.add_argument("--seq", type=int, default=8192)
+    p.add_argument("--mbs", type=int, default=1)
+    p.add_argument("--precision", default="bf16", choices=["bf16", "fp8"])
+    p.add_argument("--activation-checkpointing", action="store_true")
+    p.add_argument("--prefetch", type=int, default=1)
+    p.add_argument("--verbose", action="store_true")
+    return p.parse_args()
+
+
+class SyntheticTokens(torch.utils.data.Dataset):
+    """Random token ids of one packed sequence per item (deterministic per index)."""
+
+    def __init__(self, n, seq, vocab):
+        self.n, self.seq, self.vocab = n, seq, vocab
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, i):
+        g = torch.Generator().manual_seed(1234 + i)
+        ids = torch.randint(0, self.vocab, (self.seq,), generator=g)
+        return {"input_ids": ids, "labels": ids}
+
+
+def main():
+    args = parse()
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    from accelerate_hpc_test_amd import Accelerator, FullyShardedDataParallelPlugin
+    from accelerate_hpc_test_amd.models.llama import LLAMA_PRESETS, LlamaForCausalLM
+    from accelerate_hpc_test_amd.utils import RcclKwargs, set_seed
+
+    plugin = FullyShardedDataParallelPlugin(
+        fsdp_version=2,
+        auto_wrap_policy="transformer_based_wrap",
+        transformer_cls_names_to_wrap=["LlamaDecoderLayer"],
+        reshard_after_forward=True,
+        activation_checkpointing=args.activation_checkpointing,
+    )
+    accelerator = Accelerator(
+        mixed_precision=args.precision,
+        fsdp_plugin=plugin,
+        kwargs_handlers=[RcclKwargs(fsdp_prefetch_depth=args.prefetch)],
+    )
+    set_seed(0)
+    world = accelerator.num_processes
+    cfg = LLAMA_PRESETS[args.model]
+
+    t0 = time.time()
+    with torch.device("meta"):
+        model = LlamaForCausalLM(cfg)
+    optimizer = torch.optim.AdamW(model.parameters(), lr=1e-5)
+    total_steps = args.warmup + args.steps
+    ds = SyntheticTokens(total_steps * args.mbs * world, args.seq, cfg.vocab_size)
+    dl = torch.utils.data.DataLoader(ds, batch_size=args.mbs, num_workers=2)
+    model, optimizer, dl = accelerator.prepare(model, optimizer, dl)
+    model.train()
+    torch.cuda.synchronize()
+    if args.verbose and accelerator.is_main_process:
+        print(f"setup {time.time() - t0:.1f}s, mem {torch.cuda.memory_allocated() / 2**30:.1f} GiB", flush=True)
+
+    it = iter(dl)
+    last_loss = None
+
+    def step():
+        nonlocal last_loss
+        batch = next(it)
+        out = model(batch["input_ids"], labels=batch["labels"], return_logits=False)
+        accelerator.backward(out.loss)
+        optimizer.step()
+        optimizer.zero_grad()
+        last_loss = out.loss.detach()
+
+    for i in range(args.warmup):
+        tw = time.time()
+        step()
+        if args.verbose:
+            torch.cuda.synchronize()
+            accelerator.print(f"warmup step {i}: {time.time() - tw:.3f}s loss {last_loss.item():.4f}", flush=True)
+
+    accelerator.wait_for_everyone()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    accelerator.wait_for_everyone()
+    elapsed = time.perf_counter() - t_start
+
+    el = torch.tensor([elapsed], device=accelerator.device, dtype=torch.float64)
+    if world > 1:
+        torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
+    elapsed = el.item()
+    tokens = args.steps * args.mbs * args.seq * world
+    tps = tokens / elapsed
+    ms = elapsed / args.steps * 1000
+    flops_tok = cfg.flops_per_token(args.seq)
+    peak = torch.cuda.max_memory_allocated() / 2**30
+    if accelerator.is_main_process:
+        rec = {
+            "metric": "tokens/sec (whole node) Llama-3-8B FSDP2 bf16 at 1/2/4/8 MI355X",
+            "value": round(tps, 1),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(tps / (BASELINE_TOKENS_PER_SEC_PER_DEVICE * world), 3),
+            "dtype": args.precision,
+            "data": "synthetic (random token ids, random-init weights)",
+            "config": {
+                "model": "Llama-3-8B" if args.model.startswith("llama3") and "8b" in args.model else args.model,
+                "global_batch": args.mbs * world,
+                "seq_len": args.seq,
+                "parallelism": f"fsdp{world}",
+                "optimizer": "AdamW(lr=1e-5), fp32 master",
+                "activation_checkpointing": args.activation_checkpointing,
+            },
+            "tokens_per_sec_per_gpu": round(tps / world, 1),
+            "tflops_per_gpu": round(flops_tok * tps / world / 1e12, 1),
+            "peak_mem_gib": round(peak, 1),
+            "final_loss": round(last_loss.item(), 4) if last_loss is not None else None,
+            "baseline_tokens_per_sec": BASELINE_TOKENS_PER_SEC_PER_DEVICE * world,
+        }
+        print(json.dumps(rec), flush=True)
+    accelerator.end_training()
+
+
+if __name__ == "__main__":
+    main()

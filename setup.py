@@ -1,0 +1,58 @@
+"""Build script for accelerate_hpc_test_amd and its in-tree MI355X (gfx950) extension.
+
+    PYTORCH_ROCM_ARCH=gfx950 python setup.py build_ext --inplace
+
+produces `accelerate_hpc_test_amd/_C.*.so` next to the Python sources (the in-tree .so is what the GPU box
+loads). `__graft_entry__.build()` runs the same thing.
+"""
+
+import glob
+import os
+
+from setuptools import find_packages, setup
+
+os.environ.setdefault("PYTORCH_ROCM_ARCH", "gfx950")
+
+ext_modules = []
+cmdclass = {}
+if os.environ.get("ACCELERATE_SKIP_NATIVE_BUILD", "0") != "1":
+    from torch.utils.cpp_extension import BuildExtension, CUDAExtension
+
+    root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "accelerate_hpc_test_amd", "csrc")
+    sources = (
+        [os.path.join(root, "bindings.cpp")]
+        + sorted(glob.glob(os.path.join(root, "kernels", "*.hip")))
+        + sorted(glob.glob(os.path.join(root, "runtime", "*.cpp")))
+    )
+    sources = [os.path.relpath(s, os.path.dirname(os.path.abspath(__file__))) for s in sources]
+    ext_modules.append(
+        CUDAExtension(
+            name="accelerate_hpc_test_amd._C",
+            sources=sources,
+            include_dirs=[os.path.join(root, "kernels")],
+            extra_compile_args={
+                "cxx": ["-O3", "-std=c++17"],
+                "nvcc": ["-O3", "-std=c++17", "--offload-arch=gfx950", "-munsafe-fp-atomics"],
+            },
+        )
+    )
+    cmdclass = {"build_ext": BuildExtension.with_options(use_ninja=True)}
+
+setup(
+    name="accelerate_hpc_test_amd",
+    version="0.1.0",
+    description="MI355X-native training-loop framework with the Accelerate API (RCCL/xGMI, HIP/CDNA4 kernels)",
+    packages=find_packages(include=["accelerate_hpc_test_amd", "accelerate_hpc_test_amd.*"]),
+    python_requires=">=3.10",
+    entry_points={
+        "console_scripts": [
+            "accelerate-amd=accelerate_hpc_test_amd.commands.accelerate_cli:main",
+            "accelerate-amd-launch=accelerate_hpc_test_amd.commands.launch:main",
+            "accelerate-amd-config=accelerate_hpc_test_amd.commands.config:main",
+            "accelerate-amd-estimate-memory=accelerate_hpc_test_amd.commands.estimate:main",
+            "accelerate-amd-merge-weights=accelerate_hpc_test_amd.commands.merge:main",
+        ]
+    },
+    ext_modules=ext_modules,
+    cmdclass=cmdclass,
+)

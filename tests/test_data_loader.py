@@ -1,0 +1,148 @@
+"""Sharding math of the data layer (mirrors the reference's tests/test_data_loader.py coverage, expectations derived
+from the sharding rules: round-robin batches, even_batches wrap-around from the start of the data)."""
+
+import random
+
+import pytest
+import torch
+from torch.utils.data import BatchSampler, DataLoader, IterableDataset, SequentialSampler
+
+from accelerate_hpc_test_amd.data_loader import (
+    BatchSamplerShard,
+    DataLoaderShard,
+    IterableDatasetShard,
+    SeedableRandomSampler,
+    SkipBatchSampler,
+    SkipDataLoader,
+    skip_first_batches,
+)
+
+
+def shards(n, bs, W, drop_last=False, split=False, even=True):
+    bsamp = BatchSampler(SequentialSampler(range(n)), batch_size=bs, drop_last=drop_last)
+    return [list(BatchSamplerShard(bsamp, W, p, split_batches=split, even_batches=even)) for p in range(W)]
+
+
+def test_no_split_exact_multiple():
+    s = shards(24, 3, 2)
+    assert s[0] == [[0, 1, 2], [6, 7, 8], [12, 13, 14], [18, 19, 20]]
+    assert s[1] == [[3, 4, 5], [9, 10, 11], [15, 16, 17], [21, 22, 23]]
+
+
+def test_no_split_wraps_missing_batch():
+    s = shards(21, 3, 2)
+    assert s[0] == [[0, 1, 2], [6, 7, 8], [12, 13, 14], [18, 19, 20]]
+    assert s[1] == [[3, 4, 5], [9, 10, 11], [15, 16, 17], [0, 1, 2]]
+
+
+def test_no_split_completes_partial_batch():
+    s = shards(22, 3, 2)
+    assert s[0][-1] == [18, 19, 20]
+    assert s[1][-1] == [21, 0, 1]
+    s = shards(20, 3, 2)
+    assert s[0][-1] == [18, 19, 0]
+    assert s[1][-1] == [1, 2, 3]
+
+
+def test_no_split_drop_last_and_uneven():
+    s = shards(22, 3, 2, drop_last=True)
+    assert s[0] == [[0, 1, 2], [6, 7, 8], [12, 13, 14]]
+    assert s[1] == [[3, 4, 5], [9, 10, 11], [15, 16, 17]]
+    s = shards(22, 3, 2, even=False)
+    assert s[0][-1] == [18, 19, 20] and s[1][-1] == [21]
+
+
+@pytest.mark.parametrize("n", [20, 21, 22, 24, 2, 5])
+@pytest.mark.parametrize("W", [2, 3])
+def test_even_batches_equal_counts_and_len(n, W):
+    s = shards(n, 3, W)
+    lens = {len(x) for x in s}
+    assert len(lens) == 1
+    for p in range(W):
+        bsamp = BatchSampler(SequentialSampler(range(n)), batch_size=3, drop_last=False)
+        assert len(BatchSamplerShard(bsamp, W, p)) == len(s[p])
+        assert all(len(b) == 3 for b in s[p])
+    covered = sorted({i for x in s for b in x for i in b})
+    assert covered == list(range(n))
+
+
+def test_split_batches():
+    s = shards(24, 4, 2, split=True)
+    assert s[0][:2] == [[0, 1], [4, 5]]
+    assert s[1][:2] == [[2, 3], [6, 7]]
+    s = shards(22, 4, 2, split=True)  # last batch [20, 21] completed from the start: [20, 21, 0, 1]
+    assert s[0][-1] == [20, 21] and s[1][-1] == [0, 1]
+
+
+class RandomIterable(IterableDataset):
+    def __init__(self, p_stop=0.01, max_length=1000):
+        self.p_stop, self.max_length = p_stop, max_length
+
+    def __iter__(self):
+        count = 0
+        stop = False
+        while not stop and count < self.max_length:
+            yield count
+            count += 1
+            stop = random.random() < self.p_stop
+
+
+@pytest.mark.parametrize("split", [False, True])
+@pytest.mark.parametrize("drop_last", [False, True])
+def test_iterable_dataset_shard(split, drop_last):
+    ds = RandomIterable(max_length=103)
+    W, bs = 2, 4
+    outs = []
+    for p in range(W):
+        random.seed(42)
+        outs.append(list(IterableDatasetShard(ds, batch_size=bs, drop_last=drop_last, num_processes=W, process_index=p, split_batches=split)))
+    random.seed(42)
+    reference = list(ds)
+    assert len(outs[0]) == len(outs[1])
+    local = bs // W if split else bs
+    # interleave rank shards back to global order
+    rebuilt = []
+    for i in range(0, len(outs[0]), local):
+        for p in range(W):
+            rebuilt += outs[p][i : i + local]
+    if drop_last:
+        assert rebuilt == reference[: len(rebuilt)]
+    else:
+        assert rebuilt[: len(reference)] == reference
+        assert rebuilt[len(reference) :] == reference[: len(rebuilt) - len(reference)]
+
+
+def test_skip_batch_sampler_and_loader():
+    bsamp = BatchSampler(SequentialSampler(range(16)), batch_size=4, drop_last=False)
+    assert list(SkipBatchSampler(bsamp, 2)) == [[8, 9, 10, 11], [12, 13, 14, 15]]
+    dl = SkipDataLoader(list(range(16)), batch_size=4, skip_batches=2)
+    assert [t.tolist() for t in dl] == [[8, 9, 10, 11], [12, 13, 14, 15]]
+    dl = skip_first_batches(DataLoader(list(range(16)), batch_size=4), 3)
+    assert [t.tolist() for t in dl] == [[12, 13, 14, 15]]
+
+
+def test_dataloader_shard_end_of_dataloader_and_resume():
+    from accelerate_hpc_test_amd.state import GradientState, PartialState
+
+    PartialState(cpu=True)
+    dl = DataLoaderShard(list(range(16)), batch_size=4)
+    flags = []
+    for b in dl:
+        flags.append(dl.end_of_dataloader)
+    assert flags == [False, False, False, True]
+    it = iter(dl)
+    next(it)
+    next(it)
+    st = dl.state_dict()
+    assert st["batches_yielded"] == 2
+    dl2 = DataLoaderShard(list(range(16)), batch_size=4)
+    dl2.load_state_dict(st)
+    assert [b.tolist() for b in dl2] == [[8, 9, 10, 11], [12, 13, 14, 15]]
+    _ = GradientState()
+
+
+def test_seedable_sampler_is_reproducible():
+    s1 = SeedableRandomSampler(range(20), data_seed=7)
+    s2 = SeedableRandomSampler(range(20), data_seed=7)
+    assert list(s1) == list(s2)
+    assert list(s1) != list(SeedableRandomSampler(range(20), data_seed=7))  # epoch advanced

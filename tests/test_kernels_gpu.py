@@ -1,0 +1,200 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference of the same op (runs on the MI355X box)."""
+
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+from accelerate_hpc_test_amd.ops import _ext  # noqa: E402
+from accelerate_hpc_test_amd.ops import fused  # noqa: E402
+
+DEV = "cuda"
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+def test_extension_loaded():
+    assert _ext.available(), "native extension must be importable on the GPU box"
+
+
+@pytest.mark.parametrize("T,H", [(64, 256), (300, 4096), (17, 1024)])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_rmsnorm(T, H, with_res):
+    torch.manual_seed(0)
+    x = torch.randn(T, H, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    w = (torch.rand(H, device=DEV) + 0.5).to(torch.bfloat16).requires_grad_()
+    r = torch.randn(T, H, device=DEV, dtype=torch.bfloat16, requires_grad=True) if with_res else None
+    y, res = fused.rms_norm(x, w, 1e-5, r)
+    gy = torch.randn_like(y)
+    loss = (y.float() * gy.float()).sum() + (res.float().sum() if with_res else 0)
+    loss.backward()
+    # reference in fp32
+    x2 = x.detach().float().requires_grad_()
+    w2 = w.detach().float().requires_grad_()
+    r2 = r.detach().float().requires_grad_() if with_res else None
+    s = x2 + r2 if with_res else x2
+    s_b = s.to(torch.bfloat16).float() if with_res else s
+    y2 = s_b * torch.rsqrt(s_b.pow(2).mean(-1, keepdim=True) + 1e-5) * w2
+    loss2 = (y2 * gy.float()).sum() + (s.sum() if with_res else 0)
+    loss2.backward()
+    assert _rel(y, y2) < 1e-2
+    assert _rel(x.grad, x2.grad) < 2e-2
+    assert _rel(w.grad, w2.grad) < 2e-2
+    if with_res:
+        assert _rel(r.grad, r2.grad) < 2e-2
+
+
+def test_swiglu():
+    torch.manual_seed(0)
+    gu = torch.randn(333, 2 * 512, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    h = fused.swiglu(gu)
+    gh = torch.randn_like(h)
+    (h.float() * gh.float()).sum().backward()
+    gu2 = gu.detach().float().requires_grad_()
+    g, u = gu2.chunk(2, -1)
+    h2 = torch.nn.functional.silu(g) * u
+    (h2 * gh.float()).sum().backward()
+    assert _rel(h, h2) < 1e-2
+    assert _rel(gu.grad, gu2.grad) < 1e-2
+
+
+def test_rope_matches_reference_and_inverts():
+    torch.manual_seed(0)
+    B, S, Hq, Hkv, D = 2, 256, 4, 2, 128
+    cos, sin = fused.rope_tables(S, D, 500000.0, DEV)
+    qkv = torch.randn(B, S, Hq + 2 * Hkv, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    out = fused.apply_rope(qkv, cos, sin, Hq + Hkv)
+    ref = fused.rope_reference(qkv.detach().float(), cos, sin, Hq + Hkv)
+    assert _rel(out, ref) < 1e-2
+    g = torch.randn_like(out)
+    out.backward(g)
+    # gradient of a rotation is the inverse rotation
+    x2 = qkv.detach().float().requires_grad_()
+    fused.rope_reference(x2, cos, sin, Hq + Hkv).backward(g.float())
+    assert _rel(qkv.grad, x2.grad) < 1e-2
+
+
+@pytest.mark.parametrize("V", [512, 32000, 128256])
+def test_cross_entropy(V):
+    torch.manual_seed(0)
+    T = 257
+    logits = (torch.randn(T, V, device=DEV) * 3).to(torch.bfloat16).requires_grad_()
+    labels = torch.randint(0, V, (T,), device=DEV)
+    labels[::7] = -100
+    ref_logits = logits.detach().float().requires_grad_()
+    loss = fused.cross_entropy(logits.clone(), labels, inplace_backward=False)
+    ref = torch.nn.functional.cross_entropy(ref_logits, labels, ignore_index=-100)
+    assert abs(loss.item() - ref.item()) < 1e-3 * max(1, abs(ref.item()))
+    l2 = logits.detach().clone().requires_grad_()
+    loss2 = fused.cross_entropy(l2, labels, inplace_backward=False)
+    loss2.backward()
+    ref.backward()
+    assert _rel(l2.grad, ref_logits.grad) < 2e-2
+
+
+def _attn_ref(q, k, v, causal, scale):
+    return fused.attention_reference(q.float(), k.float(), v.float(), causal=causal, scale=scale)
+
+
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("B,S,Hq,Hkv", [(1, 256, 4, 2), (2, 512, 8, 2), (1, 384, 2, 2)])
+def test_flash_attention(causal, B, S, Hq, Hkv):
+    torch.manual_seed(0)
+    D = 128
+    qkv = torch.randn(B, S, Hq + 2 * Hkv, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    o = fused.flash_attention_qkv(qkv, Hq, Hkv, causal=causal)
+    qkv2 = qkv.detach().float().requires_grad_()
+    scale = 1 / math.sqrt(D)
+    o2 = _attn_ref(qkv2[:, :, :Hq], qkv2[:, :, Hq : Hq + Hkv], qkv2[:, :, Hq + Hkv :], causal, scale)
+    assert _rel(o, o2) < 2e-2, _rel(o, o2)
+    g = torch.randn_like(o)
+    o.backward(g)
+    o2.backward(g.float())
+    for name, sl in (("dq", slice(0, Hq)), ("dk", slice(Hq, Hq + Hkv)), ("dv", slice(Hq + Hkv, Hq + 2 * Hkv))):
+        err = _rel(qkv.grad[:, :, sl], qkv2.grad[:, :, sl])
+        assert err < 3e-2, (name, err)
+
+
+def test_flash_attention_lse():
+    torch.manual_seed(0)
+    B, S, H, D = 1, 256, 2, 128
+    q = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16)
+    k = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16)
+    v = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16)
+    o, lse = fused.flash_attn_with_lse(q, k, v, causal=True)
+    s = torch.einsum("bqhd,bkhd->bhqk", q.float(), k.float()) / math.sqrt(D)
+    s = s.masked_fill(torch.ones(S, S, device=DEV, dtype=torch.bool).triu(1), float("-inf"))
+    assert torch.allclose(lse, torch.logsumexp(s, -1), atol=2e-2, rtol=1e-3)
+
+
+def test_fused_adamw_matches_torch():
+    from accelerate_hpc_test_amd.ops.multi_tensor import FusedAdamStep
+
+    torch.manual_seed(0)
+    shapes = [(1000,), (64, 33), (8193,), (3,)]
+    p1 = [torch.randn(s, device=DEV, requires_grad=True) for s in shapes]
+    p2 = [p.detach().clone().requires_grad_() for p in p1]
+    o1 = torch.optim.AdamW(p1, lr=1e-2, weight_decay=0.1)
+    o2 = torch.optim.AdamW(p2, lr=1e-2, weight_decay=0.1)
+    fused_step = FusedAdamStep(o2)
+    for _ in range(3):
+        for a, b in zip(p1, p2):
+            g = torch.randn_like(a)
+            a.grad = g.clone()
+            b.grad = g.clone()
+        o1.step()
+        fused_step.step()
+    for a, b in zip(p1, p2):
+        assert torch.allclose(a, b, atol=1e-5, rtol=1e-4)
+
+
+def test_grad_norm_and_clip():
+    from accelerate_hpc_test_amd.ops.multi_tensor import clip_grads_by_total_sq, grad_sq_norm
+
+    torch.manual_seed(0)
+    ps = [torch.nn.Parameter(torch.zeros(s, device=DEV)) for s in [(10000,), (77, 13), (5,)]]
+    for p in ps:
+        p.grad = torch.randn_like(p)
+    ps.append(torch.nn.Parameter(torch.zeros(300, device=DEV, dtype=torch.bfloat16)))
+    ps[-1].grad = torch.randn(300, device=DEV, dtype=torch.bfloat16)
+    ref = torch.sqrt(sum(p.grad.float().pow(2).sum() for p in ps))
+    tot = grad_sq_norm(ps)
+    assert torch.allclose(tot.sqrt(), ref, rtol=1e-4)
+    clip_grads_by_total_sq(ps, tot, 1.0)
+    new = torch.sqrt(sum(p.grad.float().pow(2).sum() for p in ps))
+    assert abs(new.item() - 1.0) < 1e-2
+
+
+def test_fp8_cast_amax_gemm():
+    from accelerate_hpc_test_amd.ops import fp8
+
+    torch.manual_seed(0)
+    M, N, K = 256, 384, 512
+    a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    b = torch.randn(N, K, device=DEV, dtype=torch.bfloat16)
+    amax = fp8.amax(a)
+    assert torch.allclose(amax, a.float().abs().max().reshape(1))
+    out = fp8.fp8_linear_reference_check(a, b)
+    ref = a.float() @ b.float().t()
+    assert _rel(out, ref) < 6e-2, _rel(out, ref)
+
+
+def test_fp8_gemm_exact_small_integers():
+    """Operands that are exact in e4m3 (small integers) must give the exact product: pins the MFMA operand layout."""
+    from accelerate_hpc_test_amd.ops import fp8
+
+    torch.manual_seed(0)
+    M, N, K = 128, 128, 128
+    a = torch.randint(-3, 4, (M, K), device=DEV).to(torch.bfloat16)
+    b = torch.randint(-3, 4, (N, K), device=DEV).to(torch.bfloat16)
+    one = torch.ones(1, device=DEV)
+    out = fp8.gemm(fp8.cast(a, one), fp8.cast(b, one), one, one, out_dtype=torch.float32)
+    ref = a.float() @ b.float().t()
+    assert torch.equal(out, ref), (out - ref).abs().max()
