@@ -171,7 +171,7 @@ class DistributedDataParallel(nn.Module):
             self._launch(b)
 
     def _slot(self, b, p):
-        i = b.params.index(p)
+        i = next(j for j, q in enumerate(b.params) if q is p)
         return b.buffer[b.offsets[i] : b.offsets[i] + p.numel()].view_as(p)
 
     def _slot_ptr(self, b, p):

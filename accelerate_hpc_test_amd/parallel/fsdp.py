@@ -578,12 +578,17 @@ class FSDPEngine:
 
     @torch.no_grad()
     def on_optimizer_step(self, fused_wrote_shadow: bool):
-        """Refresh the bf16 all-gather source from the fp32 master when the optimizer did not write it."""
-        if self.param_dtype == torch.float32:
-            return
-        if not fused_wrote_shadow:
+        """Refresh the bf16 all-gather source from the fp32 master when the optimizer did not write it, and drop any
+        gathered copies (they are stale now; the next forward re-gathers)."""
+        if self.param_dtype != torch.float32 and not fused_wrote_shadow:
             for unit in self.units:
                 unit.shard_lp.copy_(unit.master)
+        if self.world_size > 1:
+            for unit in self.units:
+                if unit.state == "unsharding" and unit.ag_event is not None and self.is_cuda:
+                    torch.cuda.current_stream(self.device).wait_event(unit.ag_event)
+                unit.state = "unsharded" if unit.state == "unsharding" else unit.state
+                self._free_full(unit)
 
     def set_requires_gradient_sync(self, flag: bool):
         self.requires_grad_sync = flag

@@ -1,0 +1,40 @@
+"""Multi-rank semantics on a CPU gloo fake cluster (`debug_launcher`, world size 2) — the reference's
+tests/test_cpu.py + test_grad_sync.py strategy, applied to our native DDP/FSDP engines."""
+
+import pytest
+
+from accelerate_hpc_test_amd import debug_launcher
+from accelerate_hpc_test_amd.test_utils.scripts import test_distributed as td
+
+
+def test_collective_ops():
+    debug_launcher(td.check_ops, num_processes=2)
+
+
+def test_dataloader_sharding_and_gather_for_metrics():
+    debug_launcher(td.check_dataloader_sharding, num_processes=2)
+
+
+def test_ddp_matches_single_process():
+    debug_launcher(td.check_ddp_matches_single, num_processes=2)
+
+
+def test_ddp_gradient_accumulation():
+    debug_launcher(td.check_ddp_matches_single, args=(2,), num_processes=2)
+
+
+@pytest.mark.parametrize("reshard", [True, False])
+def test_fsdp_matches_single_process_sharded_ckpt(reshard):
+    debug_launcher(td.check_fsdp_matches_single, args=(reshard, "SHARDED_STATE_DICT"), num_processes=2)
+
+
+def test_fsdp_full_state_dict_ckpt():
+    debug_launcher(td.check_fsdp_matches_single, args=(True, "FULL_STATE_DICT"), num_processes=2)
+
+
+def test_fsdp_no_sync_accumulation():
+    debug_launcher(td.check_fsdp_no_sync_accumulation, num_processes=2)
+
+
+def test_fsdp_three_ranks():
+    debug_launcher(td.check_fsdp_matches_single, args=(True, "SHARDED_STATE_DICT"), num_processes=3)
