@@ -6,18 +6,23 @@
 // normaliser of the scaled scores, used by the backward pass and by ring-attention merges). GQA: q head h
 // reads kv head h / (Hq / Hkv). head_dim D = 128.
 //
-// Forward (query-stationary, 4 waves x 32 queries per workgroup, 64-key tiles):
-//   * "swapped" S^T = K Q^T so each lane owns ONE query column: the online-softmax max / sum and the O rescale
-//     are lane-local (one cross-half exchange per tile), no LDS round trip for P;
-//   * P^T stays in the accumulator registers and is used directly as the B operand of O^T += V^T P^T
-//     (accumulator-as-operand with the permuted k order), V^T fragments come from a padded LDS image through
-//     ds_read_b64_tr_b16 (hardware transpose); K row fragments come from an XOR-swizzled LDS image
-//     (conflict-free ds_read_b128).
+// Common structure (v2):
+//   * every K/V (or Q/dO) tile lives in ONE LDS image per operand with a 256-B row and the XOR chunk swizzle
+//     ch ^ ((row&3)<<2 | (row>>2)&3): `ds_read_b128` row fragments AND `ds_read_b64_tr_b16` transposed fragments
+//     are both bank-conflict free on it;
+//   * software pipeline: the next tile is loaded global -> registers at the top of the iteration, the current
+//     tile is consumed from LDS, then the registers are written into the other half of a double-buffered LDS
+//     region: ONE barrier per tile and the HBM/L2 latency hides under the MFMAs.
+// Forward (query-stationary, 4 waves x 32 queries, 64-key tiles):
+//   * "swapped" S^T = K Q^T so each lane owns ONE query column: online-softmax max / sum / O-rescale are
+//     lane-local (one cross-half exchange per tile);
+//   * P^T stays in the accumulator registers and is the B operand of O^T += V^T P^T (accumulator-as-operand with
+//     the permuted k order); V^T fragments come through the hardware transpose read.
 // Backward (no atomics, deterministic):
-//   * dQ kernel: query-stationary like the forward, recomputes P^T and dP^T = V dO^T, dQ^T += K^T dS^T;
-//   * dK/dV kernel: key-stationary (4 waves x 32 keys), sweeps 32-query slices: S = Q K^T and dP = dO V^T with
-//     the key on the lane, then dV^T += dO^T P and dK^T += Q^T dS with P / dS used in place as B operands;
-//     per-q-head partials are summed over the GQA group by a small reduction kernel.
+//   * dQ kernel: query-stationary like the forward; recomputes P^T, dP^T = V dO^T, dQ^T += K^T dS^T;
+//   * dK/dV kernel: key-stationary (4 waves x 32 keys, K and V held in registers), sweeps 64-query slices:
+//     S = Q K^T and dP = dO V^T with the key on the lane, then dV^T += dO^T P and dK^T += Q^T dS using P / dS in
+//     place as B operands; per-q-head partials are summed over the GQA group by a small reduction kernel.
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include "common.h"
@@ -31,27 +36,23 @@ typedef __bf16 v4bf __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kD = 128;
-constexpr int kRowBytes = 256;  // row image: 128 bf16, 16-B chunk c stored at chunk c ^ (row & 15)
-constexpr int kTrBytes = 320;   // transpose image: 128 bf16 + 64 B pad (4 rows land on disjoint banks)
+constexpr int kRow = 256;  // bytes per image row (128 bf16)
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
 
-__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }  // v_exp_f32: exp2(-inf) = 0
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }  // v_exp_f32, exp2(-inf)=0
 
 __device__ __forceinline__ f32x16 mfma(v8bf a, v8bf b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
+// Dual-use image: byte offset of 16-B chunk `ch` (0..15) of row `row`.
+__device__ __forceinline__ int img_off(int row, int ch) {
+  return row * kRow + ((ch ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4);
+}
+
 __device__ __forceinline__ v8bf row_frag(const char* img, int row, int chunk) {
-  return *reinterpret_cast<const v8bf*>(img + row * kRowBytes + ((chunk ^ (row & 15)) << 4));
-}
-
-__device__ __forceinline__ void row_store(char* img, int row, int chunk, v8bf v) {
-  *reinterpret_cast<v8bf*>(img + row * kRowBytes + ((chunk ^ (row & 15)) << 4)) = v;
-}
-
-__device__ __forceinline__ void tr_store(char* img, int row, int chunk, v8bf v) {
-  *reinterpret_cast<v8bf*>(img + row * kTrBytes + (chunk << 4)) = v;
+  return *reinterpret_cast<const v8bf*>(img + img_off(row, chunk));
 }
 
 __device__ __forceinline__ v4bf tr_read(const char* p) {
@@ -59,23 +60,22 @@ __device__ __forceinline__ v4bf tr_read(const char* p) {
       (__attribute__((address_space(3))) v4bf*)(reinterpret_cast<uintptr_t>(p)));
 }
 
-// A-operand fragment of X^T where X is a [rows][128] tile in the transpose image: rows rb..rb+15 form the
-// MFMA k dimension in the permuted order (element j of half h <-> row rb + 8(j>>2) + 4h + (j&3)),
-// columns db*32 .. db*32+31 form the MFMA rows.
+// A-operand fragment of X^T, X a [rows][128] tile in the dual image: rows rb..rb+15 form the MFMA k dimension in
+// the permuted order (element j of half h <-> row rb + 8(j>>2) + 4h + (j&3)); columns db*32..db*32+31 form the
+// MFMA rows. Lane 4q+p of each 16-lane group supplies row (r0 + q), columns c0 + 4p.
 __device__ __forceinline__ v8bf tr_frag(const char* img, int rb, int db, int lane) {
   const int g = lane >> 4, i = lane & 15;
   const int row = rb + 4 * (g >> 1) + (i >> 2);
-  const int col = db * 32 + 16 * (g & 1) + 4 * (i & 3);
-  const char* p = img + row * kTrBytes + col * 2;
-  const v4bf lo = tr_read(p);
-  const v4bf hi = tr_read(p + 8 * kTrBytes);
+  const int ch = db * 4 + 2 * (g & 1) + ((i & 3) >> 1);
+  const int sub = 8 * (i & 1);
+  const v4bf lo = tr_read(img + img_off(row, ch) + sub);
+  const v4bf hi = tr_read(img + img_off(row + 8, ch) + sub);
   v8bf r;
   r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
   r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
   return r;
 }
 
-// Accumulator row index held by register i of a 32x32 C tile in lane half hf.
 __device__ __forceinline__ int acc_row(int i, int hf) { return (i & 3) + 8 * (i >> 2) + 4 * hf; }
 
 __device__ __forceinline__ v8bf pack8(const f32x16& x, int s) {
@@ -84,6 +84,32 @@ __device__ __forceinline__ v8bf pack8(const f32x16& x, int s) {
   for (int j = 0; j < 8; ++j) r[j] = static_cast<__bf16>(x[8 * s + j]);
   return r;
 }
+
+__device__ __forceinline__ void zero(f32x16& x) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) x[i] = 0.f;
+}
+
+// Register staging of a ROWS x 128 bf16 tile by 256 threads: ROWS*16 chunks of 16 B, ROWS/16 per thread.
+template <int ROWS>
+struct Stage {
+  static constexpr int kPer = ROWS * 16 / 256;
+  v8bf r[kPer];
+  __device__ __forceinline__ void load(const bf16_t* base, long ts, int row0, int tid) {
+#pragma unroll
+    for (int t = 0; t < kPer; ++t) {
+      const int c = tid + t * 256, row = c >> 4, ch = c & 15;
+      r[t] = *reinterpret_cast<const v8bf*>(base + (long)(row0 + row) * ts + ch * 8);
+    }
+  }
+  __device__ __forceinline__ void store(char* img, int tid) const {
+#pragma unroll
+    for (int t = 0; t < kPer; ++t) {
+      const int c = tid + t * 256, row = c >> 4, ch = c & 15;
+      *reinterpret_cast<v8bf*>(img + img_off(row, ch)) = r[t];
+    }
+  }
+};
 
 struct FwdParams {
   const bf16_t *q, *k, *v;
@@ -98,11 +124,11 @@ struct FwdParams {
 template <bool CAUSAL>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(FwdParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* k_img = smem;                      // 64 x 256 B
-  char* v_img = smem + 64 * kRowBytes;     // 64 x 320 B
+  constexpr int kTile = 64 * kRow;  // 16 KB per operand image
   const int nqt = p.S / 128;
-  const int qt = CAUSAL ? (nqt - 1 - (int)blockIdx.x) : (int)blockIdx.x;  // heaviest causal tiles first
-  const int h = blockIdx.y, b = blockIdx.z;
+  // grid = (Hq, S/128, B): heads vary fastest, so the heaviest causal tiles of EVERY head are dispatched first
+  const int qt = CAUSAL ? (nqt - 1 - (int)blockIdx.y) : (int)blockIdx.y;
+  const int h = blockIdx.x, b = blockIdx.z;
   const int kh = h / (p.Hq / p.Hkv);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hf = lane >> 5;
   const int qw0 = qt * 128 + wave * 32;
@@ -116,29 +142,31 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(FwdParams p) {
 
   f32x16 o[4];
 #pragma unroll
-  for (int d = 0; d < 4; ++d)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) o[d][i] = 0.f;
+  for (int d = 0; d < 4; ++d) zero(o[d]);
   float m = -INFINITY, l = 0.f;
   const int n_kt = CAUSAL ? (qt + 1) * 2 : p.S / 64;
 
+  Stage<64> sk, sv;
+  sk.load(kb_, p.k_ts, 0, tid);
+  sv.load(vb_, p.v_ts, 0, tid);
+  sk.store(smem, tid);
+  sv.store(smem + kTile, tid);
+  __syncthreads();
+
   for (int kt = 0; kt < n_kt; ++kt) {
     const int k0 = kt * 64;
-#pragma unroll
-    for (int c = tid; c < 64 * 16; c += 256) {
-      const int row = c >> 4, ch = c & 15;
-      const v8bf kv = *reinterpret_cast<const v8bf*>(kb_ + (long)(k0 + row) * p.k_ts + ch * 8);
-      const v8bf vv = *reinterpret_cast<const v8bf*>(vb_ + (long)(k0 + row) * p.v_ts + ch * 8);
-      row_store(k_img, row, ch, kv);
-      tr_store(v_img, row, ch, vv);
+    char* k_img = smem + (kt & 1) * 2 * kTile;
+    char* v_img = k_img + kTile;
+    const bool more = kt + 1 < n_kt;
+    if (more) {
+      sk.load(kb_, p.k_ts, k0 + 64, tid);
+      sv.load(vb_, p.v_ts, k0 + 64, tid);
     }
-    __syncthreads();
     if (!CAUSAL || k0 <= qw0 + 31) {
       f32x16 sc[2];
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) sc[kb][i] = 0.f;
+        zero(sc[kb]);
 #pragma unroll
         for (int s = 0; s < 8; ++s) sc[kb] = mfma(row_frag(k_img, kb * 32 + r, 2 * s + hf), qf[s], sc[kb]);
       }
@@ -184,6 +212,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(FwdParams p) {
 #pragma unroll
           for (int s2 = 0; s2 < 2; ++s2) o[d] = mfma(tr_frag(v_img, kb * 32 + 16 * s2, d, lane), pb[kb][s2], o[d]);
     }
+    if (more) {
+      char* nk = smem + ((kt + 1) & 1) * 2 * kTile;
+      sk.store(nk, tid);
+      sv.store(nk + kTile, tid);
+    }
     __syncthreads();
   }
   l += __shfl_xor(l, 32, 64);
@@ -201,10 +234,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(FwdParams p) {
   if (hf == 0) p.lse[((long)b * p.Hq + h) * p.S + qw0 + r] = (m + __builtin_amdgcn_logf(l)) * kLn2;
 }
 
-// delta[b, h, s] = sum_d dO * O (fp32).
+// delta[b, h, s] = sum_d dO * O (fp32), one wave per (b, s, h).
 __global__ void attn_delta_kernel(const bf16_t* __restrict__ o, long o_ts, long o_bs, const bf16_t* __restrict__ dout,
                                   long do_ts, long do_bs, float* __restrict__ delta, int S, int Hq, int B) {
-  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);  // one wave per (b, s, h)
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= (long)B * S * Hq) return;
   const int h = row % Hq;
@@ -231,12 +264,10 @@ struct BwdParams {
 template <bool CAUSAL>
 __global__ __launch_bounds__(256, 1) void attn_bwd_dq_kernel(BwdParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* k_row = smem;                              // 64 x 256
-  char* k_tr = smem + 64 * kRowBytes;              // 64 x 320
-  char* v_row = k_tr + 64 * kTrBytes;              // 64 x 256
+  constexpr int kTile = 64 * kRow;
   const int nqt = p.S / 128;
-  const int qt = CAUSAL ? (nqt - 1 - (int)blockIdx.x) : (int)blockIdx.x;
-  const int h = blockIdx.y, b = blockIdx.z;
+  const int qt = CAUSAL ? (nqt - 1 - (int)blockIdx.y) : (int)blockIdx.y;  // grid (Hq, S/128, B), heavy first
+  const int h = blockIdx.x, b = blockIdx.z;
   const int kh = h / (p.Hq / p.Hkv);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hf = lane >> 5;
   const int qw0 = qt * 128 + wave * 32;
@@ -256,33 +287,36 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_kernel(BwdParams p) {
   const float dlt = p.delta[st];
   f32x16 dq[4];
 #pragma unroll
-  for (int d = 0; d < 4; ++d)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) dq[d][i] = 0.f;
+  for (int d = 0; d < 4; ++d) zero(dq[d]);
   const int n_kt = CAUSAL ? (qt + 1) * 2 : p.S / 64;
+
+  Stage<64> sk, sv;
+  sk.load(kb_, p.k_ts, 0, tid);
+  sv.load(vb_, p.v_ts, 0, tid);
+  sk.store(smem, tid);
+  sv.store(smem + kTile, tid);
+  __syncthreads();
+
   for (int kt = 0; kt < n_kt; ++kt) {
     const int k0 = kt * 64;
-#pragma unroll
-    for (int c = tid; c < 64 * 16; c += 256) {
-      const int row = c >> 4, ch = c & 15;
-      const v8bf kv = *reinterpret_cast<const v8bf*>(kb_ + (long)(k0 + row) * p.k_ts + ch * 8);
-      const v8bf vv = *reinterpret_cast<const v8bf*>(vb_ + (long)(k0 + row) * p.v_ts + ch * 8);
-      row_store(k_row, row, ch, kv);
-      tr_store(k_tr, row, ch, kv);
-      row_store(v_row, row, ch, vv);
+    char* k_img = smem + (kt & 1) * 2 * kTile;
+    char* v_img = k_img + kTile;
+    const bool more = kt + 1 < n_kt;
+    if (more) {
+      sk.load(kb_, p.k_ts, k0 + 64, tid);
+      sv.load(vb_, p.v_ts, k0 + 64, tid);
     }
-    __syncthreads();
     if (!CAUSAL || k0 <= qw0 + 31) {
       v8bf dsb[2][2];
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
         f32x16 sc, dp;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) { sc[i] = 0.f; dp[i] = 0.f; }
+        zero(sc);
+        zero(dp);
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
-          sc = mfma(row_frag(k_row, kb * 32 + r, 2 * s + hf), qf[s], sc);
-          dp = mfma(row_frag(v_row, kb * 32 + r, 2 * s + hf), df[s], dp);
+          sc = mfma(row_frag(k_img, kb * 32 + r, 2 * s + hf), qf[s], sc);
+          dp = mfma(row_frag(v_img, kb * 32 + r, 2 * s + hf), df[s], dp);
         }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
@@ -298,7 +332,12 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_kernel(BwdParams p) {
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) dq[d] = mfma(tr_frag(k_tr, kb * 32 + 16 * s2, d, lane), dsb[kb][s2], dq[d]);
+          for (int s2 = 0; s2 < 2; ++s2) dq[d] = mfma(tr_frag(k_img, kb * 32 + 16 * s2, d, lane), dsb[kb][s2], dq[d]);
+    }
+    if (more) {
+      char* nk = smem + ((kt + 1) & 1) * 2 * kTile;
+      sk.store(nk, tid);
+      sv.store(nk + kTile, tid);
     }
     __syncthreads();
   }
@@ -314,17 +353,15 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_kernel(BwdParams p) {
     }
 }
 
+// Key-stationary dK / dV: 4 waves x 32 keys, 64-query slices double buffered.
 template <bool CAUSAL>
 __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(BwdParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* q_row = smem;                        // 32 x 256
-  char* q_tr = q_row + 32 * kRowBytes;       // 32 x 320
-  char* d_row = q_tr + 32 * kTrBytes;        // 32 x 256
-  char* d_tr = d_row + 32 * kRowBytes;       // 32 x 320
-  float* lse_s = reinterpret_cast<float*>(d_tr + 32 * kTrBytes);  // 32
-  float* dlt_s = lse_s + 32;                                       // 32
-  const int kt = blockIdx.x;  // key tile of 128 keys; tile 0 has the most work under the causal mask
-  const int h = blockIdx.y, b = blockIdx.z;
+  constexpr int kSlice = 64;
+  constexpr int kImg = kSlice * kRow;            // 16 KB per operand
+  constexpr int kBuf = 2 * kImg + 2 * kSlice * 4;  // Q, dO images + lse, delta
+  const int kt = blockIdx.y;                     // key tile of 128 keys; tile 0 has the most causal work
+  const int h = blockIdx.x, b = blockIdx.z;      // grid (Hq, S/128, B): heavy tiles of every head first
   const int kh = h / (p.Hq / p.Hkv);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hf = lane >> 5;
   const int kw0 = kt * 128 + wave * 32;
@@ -343,54 +380,72 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(BwdParams p) {
   }
   f32x16 dk[4], dv[4];
 #pragma unroll
-  for (int d = 0; d < 4; ++d)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) { dk[d][i] = 0.f; dv[d][i] = 0.f; }
+  for (int d = 0; d < 4; ++d) { zero(dk[d]); zero(dv[d]); }
 
-  const int qs0 = CAUSAL ? kt * 4 : 0;
-  const int nqs = p.S / 32;
+  const int qs0 = CAUSAL ? kt * 2 : 0;  // first 64-query slice that can see this key tile
+  const int nqs = p.S / kSlice;
+  Stage<kSlice> sq, sd;
+  float st_l = 0.f, st_d = 0.f;
+  auto issue = [&](int qs) {
+    const int q0 = qs * kSlice;
+    sq.load(qb, p.q_ts, q0, tid);
+    sd.load(dob, p.do_ts, q0, tid);
+    if (tid < kSlice) st_l = lse_g[q0 + tid] * kLog2e;
+    else if (tid < 2 * kSlice) st_d = dlt_g[q0 + tid - kSlice];
+  };
+  auto commit = [&](int buf) {
+    char* base = smem + buf * kBuf;
+    sq.store(base, tid);
+    sd.store(base + kImg, tid);
+    float* ls = reinterpret_cast<float*>(base + 2 * kImg);
+    if (tid < kSlice) ls[tid] = st_l;
+    else if (tid < 2 * kSlice) ls[tid] = st_d;  // delta at ls[kSlice + i]
+  };
+  issue(qs0);
+  commit(0);
+  __syncthreads();
+
   for (int qs = qs0; qs < nqs; ++qs) {
-    const int q0 = qs * 32;
+    const int cur = (qs - qs0) & 1;
+    const char* q_img = smem + cur * kBuf;
+    const char* d_img = q_img + kImg;
+    const float* lse_s = reinterpret_cast<const float*>(q_img + 2 * kImg);
+    const float* dlt_s = lse_s + kSlice;
+    const bool more = qs + 1 < nqs;
+    if (more) issue(qs + 1);
+    const int q0 = qs * kSlice;
 #pragma unroll
-    for (int c = tid; c < 32 * 16; c += 256) {
-      const int row = c >> 4, ch = c & 15;
-      const v8bf qv = *reinterpret_cast<const v8bf*>(qb + (long)(q0 + row) * p.q_ts + ch * 8);
-      const v8bf dv8 = *reinterpret_cast<const v8bf*>(dob + (long)(q0 + row) * p.do_ts + ch * 8);
-      row_store(q_row, row, ch, qv);
-      tr_store(q_tr, row, ch, qv);
-      row_store(d_row, row, ch, dv8);
-      tr_store(d_tr, row, ch, dv8);
-    }
-    if (tid < 32) lse_s[tid] = lse_g[q0 + tid] * kLog2e;
-    else if (tid < 64) dlt_s[tid - 32] = dlt_g[q0 + tid - 32];
-    __syncthreads();
-    if (!CAUSAL || q0 + 31 >= kw0) {
-      f32x16 sc, dp;
+    for (int half = 0; half < 2; ++half) {
+      const int qh = half * 32;
+      if (!CAUSAL || q0 + qh + 31 >= kw0) {
+        f32x16 sc, dp;
+        zero(sc);
+        zero(dp);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) { sc[i] = 0.f; dp[i] = 0.f; }
+        for (int s = 0; s < 8; ++s) {
+          sc = mfma(row_frag(q_img, qh + r, 2 * s + hf), kf[s], sc);
+          dp = mfma(row_frag(d_img, qh + r, 2 * s + hf), vf[s], dp);
+        }
 #pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        sc = mfma(row_frag(q_row, r, 2 * s + hf), kf[s], sc);
-        dp = mfma(row_frag(d_row, r, 2 * s + hf), vf[s], dp);
-      }
+        for (int i = 0; i < 16; ++i) {
+          const int qi = qh + acc_row(i, hf);
+          float pv = fast_exp2(sc[i] * p.scale_log2 - lse_s[qi]);
+          if (CAUSAL && (kw0 + r > q0 + qi)) pv = 0.f;
+          sc[i] = pv;
+          dp[i] = pv * (dp[i] - dlt_s[qi]);
+        }
+        const v8bf pb0 = pack8(sc, 0), pb1 = pack8(sc, 1);
+        const v8bf ds0 = pack8(dp, 0), ds1 = pack8(dp, 1);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int qi = acc_row(i, hf);
-        float pv = fast_exp2(sc[i] * p.scale_log2 - lse_s[qi]);
-        if (CAUSAL && (kw0 + r > q0 + qi)) pv = 0.f;
-        sc[i] = pv;
-        dp[i] = pv * (dp[i] - dlt_s[qi]);
-      }
-      const v8bf pb0 = pack8(sc, 0), pb1 = pack8(sc, 1);
-      const v8bf ds0 = pack8(dp, 0), ds1 = pack8(dp, 1);
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        dv[d] = mfma(tr_frag(d_tr, 0, d, lane), pb0, dv[d]);
-        dv[d] = mfma(tr_frag(d_tr, 16, d, lane), pb1, dv[d]);
-        dk[d] = mfma(tr_frag(q_tr, 0, d, lane), ds0, dk[d]);
-        dk[d] = mfma(tr_frag(q_tr, 16, d, lane), ds1, dk[d]);
+        for (int d = 0; d < 4; ++d) {
+          dv[d] = mfma(tr_frag(d_img, qh, d, lane), pb0, dv[d]);
+          dv[d] = mfma(tr_frag(d_img, qh + 16, d, lane), pb1, dv[d]);
+          dk[d] = mfma(tr_frag(q_img, qh, d, lane), ds0, dk[d]);
+          dk[d] = mfma(tr_frag(q_img, qh + 16, d, lane), ds1, dk[d]);
+        }
       }
     }
+    if (more) commit(cur ^ 1);
     __syncthreads();
   }
   const long orow = (((long)b * p.S + kw0 + r) * p.Hq + h) * kD;
@@ -442,6 +497,16 @@ void check_qkv(const torch::Tensor& t, const char* name) {
   TORCH_CHECK((reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0, name, " must be 16-byte aligned");
 }
 
+constexpr size_t kFwdSmem = 2 * 2 * 64 * kRow;                    // 64 KB
+constexpr size_t kDqSmem = 2 * 2 * 64 * kRow;                     // 64 KB
+constexpr size_t kDkdvSmem = 2 * (2 * 64 * kRow + 2 * 64 * 4);    // 65 KB
+
+template <typename K>
+void allow_smem(K kernel, size_t bytes) {
+  // > 64 KB of dynamic LDS must be opted into explicitly (MI355X has 160 KB per CU).
+  hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
 }  // namespace
 
 // q: [B, S, Hq, D], k/v: [B, S, Hkv, D] (views into a fused QKV buffer are fine). Returns (O [B,S,Hq,D], LSE [B,Hq,S]).
@@ -460,11 +525,10 @@ std::vector<torch::Tensor> flash_attn_fwd(torch::Tensor q, torch::Tensor k, torc
               reinterpret_cast<const bf16_t*>(v.data_ptr()), q.stride(1), k.stride(1), v.stride(1), q.stride(0),
               k.stride(0), v.stride(0), reinterpret_cast<bf16_t*>(o.data_ptr()), o.stride(1), o.stride(0),
               lse.data_ptr<float>(), S, Hq, Hkv, (float)(softmax_scale * kLog2e)};
-  dim3 grid(S / 128, Hq, B);
-  const size_t smem = 64 * kRowBytes + 64 * kTrBytes;
+  dim3 grid(Hq, S / 128, B);
   auto stream = at::hip::getCurrentHIPStream();
-  if (causal) hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(256), smem, stream, p);
-  else hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(256), smem, stream, p);
+  if (causal) hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(256), kFwdSmem, stream, p);
+  else hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(256), kFwdSmem, stream, p);
   return {o, lse};
 }
 
@@ -499,15 +563,19 @@ void flash_attn_bwd(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch:
               dout.stride(0), lse.data_ptr<float>(), delta.data_ptr<float>(), reinterpret_cast<bf16_t*>(dq.data_ptr()),
               dq.stride(1), dq.stride(0), dk_part.data_ptr<float>(), dv_part.data_ptr<float>(), S, Hq, Hkv,
               (float)(softmax_scale * kLog2e), (float)softmax_scale};
-  dim3 grid(S / 128, Hq, B);
-  const size_t smem_dq = 64 * kRowBytes * 2 + 64 * kTrBytes;
-  const size_t smem_kv = 32 * kRowBytes * 2 + 32 * kTrBytes * 2 + 64 * sizeof(float);
+  dim3 grid(Hq, S / 128, B);
+  static bool attrs = false;
+  if (!attrs) {
+    allow_smem(attn_bwd_dkdv_kernel<true>, kDkdvSmem);
+    allow_smem(attn_bwd_dkdv_kernel<false>, kDkdvSmem);
+    attrs = true;
+  }
   if (causal) {
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, grid, dim3(256), smem_dq, stream, p);
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<true>, grid, dim3(256), smem_kv, stream, p);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, grid, dim3(256), kDqSmem, stream, p);
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<true>, grid, dim3(256), kDkdvSmem, stream, p);
   } else {
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<false>, grid, dim3(256), smem_dq, stream, p);
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<false>, grid, dim3(256), smem_kv, stream, p);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<false>, grid, dim3(256), kDqSmem, stream, p);
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<false>, grid, dim3(256), kDkdvSmem, stream, p);
   }
   const long work = (long)B * S * Hkv * (kD / 4);
   long g = (work + 255) / 256;

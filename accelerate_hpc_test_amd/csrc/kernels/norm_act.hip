@@ -131,14 +131,24 @@ __global__ __launch_bounds__(kNormThreads) void rmsnorm_bwd_kernel(
   }
 }
 
-// Column sum of the [P, H] fp32 partials → dweight (bf16 or fp32 output).
+// Column sum of the [P, H] fp32 partials → dweight (bf16 or fp32 output). 256 threads = 32 columns x 8 row
+// groups; each row group strides over the partial rows, then the 8 partial sums are combined through LDS.
 template <typename OutT>
-__global__ void colsum_kernel(const float* __restrict__ part, OutT* __restrict__ out, int P, int H) {
-  const int col = blockIdx.x * blockDim.x + threadIdx.x;
-  if (col >= H) return;
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part, OutT* __restrict__ out, int P, int H) {
+  __shared__ float red[8][33];
+  const int c = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int col = blockIdx.x * 32 + c;
   float s = 0.f;
-  for (int p = 0; p < P; ++p) s += part[(size_t)p * H + col];
-  out[col] = from_f<OutT>(s);
+  if (col < H)
+    for (int p = rg; p < P; p += 8) s += part[(size_t)p * H + col];
+  red[rg][c] = s;
+  __syncthreads();
+  if (rg == 0 && col < H) {
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) t += red[g][c];
+    out[col] = from_f<OutT>(t);
+  }
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -300,7 +310,7 @@ std::vector<torch::Tensor> rmsnorm_bwd(torch::Tensor dy, torch::Tensor x, torch:
   else if (vpt <= 4) LAUNCH_BWD(4);
   else LAUNCH_BWD(8);
 #undef LAUNCH_BWD
-  hipLaunchKernelGGL(colsum_kernel<bf16_t>, dim3((H + 255) / 256), dim3(256), 0, stream, part.data_ptr<float>(),
+  hipLaunchKernelGGL(colsum_kernel<bf16_t>, dim3((H + 31) / 32), dim3(256), 0, stream, part.data_ptr<float>(),
                      reinterpret_cast<bf16_t*>(dw.data_ptr()), P, H);
   return {dx, dw};
 }

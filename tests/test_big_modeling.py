@@ -1,0 +1,180 @@
+"""Big-model inference on CPU: meta init, device-map planning, checkpoint loading, cpu/disk offload, hooks
+(coverage modelled on the reference's tests/test_big_modeling.py, test_modeling_utils.py, test_hooks.py)."""
+
+import os
+import tempfile
+
+import pytest
+import torch
+import torch.nn as nn
+
+from accelerate_hpc_test_amd import (
+    cpu_offload,
+    cpu_offload_with_hook,
+    disk_offload,
+    dispatch_model,
+    infer_auto_device_map,
+    init_empty_weights,
+    init_on_device,
+    load_checkpoint_and_dispatch,
+)
+from accelerate_hpc_test_amd._big_modeling_impl import (
+    check_device_map,
+    find_tied_parameters,
+    get_balanced_memory,
+    load_checkpoint_in_model,
+    set_module_tensor_to_device,
+)
+from accelerate_hpc_test_amd.hooks import ModelHook, SequentialHook, add_hook_to_module, remove_hook_from_module
+from accelerate_hpc_test_amd.utils.modeling import compute_module_sizes
+
+
+class ModelForTest(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.linear1 = nn.Linear(3, 4)
+        self.batchnorm = nn.BatchNorm1d(4)
+        self.linear2 = nn.Linear(4, 5)
+
+    def forward(self, x):
+        return self.linear2(self.batchnorm(self.linear1(x)))
+
+
+class TiedModel(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.emb = nn.Embedding(10, 4)
+        self.body = nn.Linear(4, 4)
+        self.head = nn.Linear(4, 10, bias=False)
+        self.head.weight = self.emb.weight
+
+    def forward(self, ids):
+        return self.head(self.body(self.emb(ids)))
+
+
+def test_init_empty_weights():
+    with init_empty_weights():
+        m = nn.Linear(1000, 1000)
+    assert m.weight.device.type == "meta"
+    with init_empty_weights(include_buffers=True):
+        bn = nn.BatchNorm1d(4)
+    assert bn.running_mean.device.type == "meta"
+    with init_on_device(torch.device("cpu")):
+        m2 = nn.Linear(2, 2)
+    assert m2.weight.device.type == "cpu"
+
+
+def test_compute_module_sizes_and_tied():
+    m = ModelForTest()
+    sizes = compute_module_sizes(m)
+    assert sizes["linear1"] == (3 * 4 + 4) * 4
+    assert sizes[""] == sum(sizes[k] for k in ("linear1", "batchnorm", "linear2"))
+    assert find_tied_parameters(TiedModel()) == [["emb.weight", "head.weight"]]
+
+
+def test_infer_auto_device_map_greedy():
+    m = ModelForTest()
+    # linear1 64 B, batchnorm 72 B (incl. buffers), linear2 100 B
+    dm = infer_auto_device_map(m, max_memory={0: 200, 1: 200})
+    assert dm == {"linear1": 0, "batchnorm": 1, "linear2": 1}  # 100 B reserved for the largest layer on GPU 0
+    dm = infer_auto_device_map(m, max_memory={0: 250, 1: 400})
+    assert dm == {"": 0}  # everything fits on GPU 0 → collapsed by clean_device_map
+    dm = infer_auto_device_map(m, max_memory={0: 100, "cpu": 100}, no_split_module_classes=[])
+    assert set(dm.values()) <= {0, "cpu", "disk"}
+    check_device_map(m, dm)
+
+
+def test_tied_params_stay_together():
+    m = TiedModel()
+    dm = infer_auto_device_map(m, max_memory={0: 200, 1: 400})
+    assert dm.get("emb", dm.get("")) == dm.get("head", dm.get(""))
+
+
+def test_balanced_memory():
+    m = ModelForTest()
+    mm = get_balanced_memory(m, max_memory={0: 10_000, 1: 10_000})
+    assert mm[0] < 10_000 and mm[1] == 10_000
+
+
+def test_set_module_tensor_to_device_and_meta():
+    m = ModelForTest()
+    set_module_tensor_to_device(m, "linear1.weight", "meta")
+    assert m.linear1.weight.device.type == "meta"
+    set_module_tensor_to_device(m, "linear1.weight", "cpu", value=torch.ones(4, 3))
+    assert torch.equal(m.linear1.weight, torch.ones(4, 3))
+    with pytest.raises(ValueError):
+        set_module_tensor_to_device(m, "linear1.weight", "cpu", value=torch.ones(2, 2))
+
+
+def test_hooks_add_remove_sequential():
+    class Plus(ModelHook):
+        def __init__(self, v):
+            self.v = v
+
+        def pre_forward(self, module, *args, **kwargs):
+            return (args[0] + self.v,), kwargs
+
+    lin = nn.Linear(3, 3)
+    x = torch.randn(2, 3)
+    ref = lin(x + 3)
+    add_hook_to_module(lin, Plus(1))
+    add_hook_to_module(lin, Plus(2), append=True)
+    assert isinstance(lin._hf_hook, SequentialHook)
+    assert torch.allclose(lin(x), ref)
+    remove_hook_from_module(lin)
+    assert torch.allclose(lin(x), torch.nn.functional.linear(x, lin.weight, lin.bias))
+    assert not hasattr(lin, "_hf_hook")
+
+
+def test_cpu_and_disk_offload_match():
+    m = ModelForTest().eval()
+    x = torch.randn(2, 3)
+    expected = m(x)
+    cpu_offload(m, execution_device="cpu")
+    assert torch.allclose(m(x), expected)
+    m2 = ModelForTest().eval()
+    m2.load_state_dict({k: v for k, v in ModelForTest().state_dict().items()})
+    exp2 = m2(x)
+    with tempfile.TemporaryDirectory() as d:
+        disk_offload(m2, d, execution_device="cpu")
+        assert m2.linear1.weight.device.type == "meta"
+        assert torch.allclose(m2(x), exp2)
+
+
+def test_cpu_offload_with_hook_chain():
+    a, b = ModelForTest(), ModelForTest()
+    a, ha = cpu_offload_with_hook(a, execution_device="cpu")
+    b, hb = cpu_offload_with_hook(b, execution_device="cpu", prev_module_hook=ha)
+    x = torch.randn(2, 3)
+    b(a(x)[:, :3])
+    hb.offload()
+
+
+def test_dispatch_model_with_disk():
+    m = ModelForTest().eval()
+    x = torch.randn(2, 3)
+    expected = m(x)
+    with tempfile.TemporaryDirectory() as d:
+        dm = {"linear1": "cpu", "batchnorm": "disk", "linear2": "cpu"}
+        dispatch_model(m, dm, offload_dir=d)
+        assert m.hf_device_map == dm
+        assert torch.allclose(m(x), expected, atol=1e-6)
+
+
+def test_load_checkpoint_and_dispatch_roundtrip():
+    src = ModelForTest().eval()
+    x = torch.randn(2, 3)
+    expected = src(x)
+    with tempfile.TemporaryDirectory() as d:
+        from safetensors.torch import save_file
+
+        save_file(src.state_dict(), os.path.join(d, "model.safetensors"))
+        with init_empty_weights(include_buffers=True):
+            tgt = ModelForTest()
+        tgt = load_checkpoint_and_dispatch(tgt, d, device_map={"": "cpu"})
+        tgt.eval()
+        assert torch.allclose(tgt(x), expected, atol=1e-6)
+        # explicit load into real model
+        m3 = ModelForTest().eval()
+        load_checkpoint_in_model(m3, os.path.join(d, "model.safetensors"))
+        assert torch.allclose(m3(x), expected, atol=1e-6)

@@ -1,0 +1,38 @@
+"""Microbenchmark of the HIP flash-attention kernels (fwd / bwd) at Llama-3-8B shapes: TFLOP/s on random data."""
+import argparse, json, math, time
+import os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+from accelerate_hpc_test_amd.ops import _ext
+
+p = argparse.ArgumentParser()
+p.add_argument("--S", type=int, default=8192)
+p.add_argument("--Hq", type=int, default=32)
+p.add_argument("--Hkv", type=int, default=8)
+p.add_argument("--B", type=int, default=1)
+p.add_argument("--iters", type=int, default=10)
+a = p.parse_args()
+e = _ext.ext()
+D = 128
+qkv = torch.randn(a.B, a.S, a.Hq + 2 * a.Hkv, D, device="cuda", dtype=torch.bfloat16)
+q, k, v = qkv[:, :, :a.Hq], qkv[:, :, a.Hq:a.Hq + a.Hkv], qkv[:, :, a.Hq + a.Hkv:]
+dqkv = torch.empty_like(qkv)
+dq, dk, dv = dqkv[:, :, :a.Hq], dqkv[:, :, a.Hq:a.Hq + a.Hkv], dqkv[:, :, a.Hq + a.Hkv:]
+scale = 1 / math.sqrt(D)
+res = {}
+for causal in (True, False):
+    o, lse = e.flash_attn_fwd(q, k, v, scale, causal)
+    do = torch.randn_like(o)
+    f = 0.5 if causal else 1.0
+    fl_fwd = 4 * a.B * a.Hq * a.S * a.S * D * f
+    def tm(fn):
+        fn(); torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(a.iters): fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t) / a.iters
+    tf = tm(lambda: e.flash_attn_fwd(q, k, v, scale, causal))
+    tb = tm(lambda: e.flash_attn_bwd(do, q, k, v, o, lse, dq, dk, dv, scale, causal))
+    res["causal" if causal else "full"] = {"fwd_ms": round(tf * 1e3, 3), "fwd_tflops": round(fl_fwd / tf / 1e12, 1),
+        "bwd_ms": round(tb * 1e3, 3), "bwd_tflops": round(2.5 * fl_fwd / tb / 1e12, 1)}
+print(json.dumps({"shape": vars(a), **res}))
