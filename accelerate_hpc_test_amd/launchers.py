@@ -124,6 +124,10 @@ class _DebugWorker:
         os.environ["LOCAL_RANK"] = str(index)
         os.environ["RANK"] = str(index)
         os.environ["FORK_LAUNCHED"] = str(1)
+        # A forked child inherits the parent's OpenMP pool bookkeeping but not its threads: the first parallel
+        # region would wait forever on workers that do not exist. The fake cluster runs tiny models, so run
+        # each rank single-threaded.
+        torch.set_num_threads(1)
         rdv_file = os.environ.get("ACCELERATE_DEBUG_RDV_FILE")
         if rdv_file:
             torch.distributed.init_process_group(

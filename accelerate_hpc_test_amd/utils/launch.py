@@ -1,0 +1,362 @@
+"""Launch-time environment contract: turn parsed `launch` arguments into the env vars the runtime reads.
+
+Parity target: `/root/reference/src/accelerate/utils/launch.py:46-819` (`prepare_simple_launcher_cmd_env`,
+`prepare_multi_gpu_env`, `prepare_deepspeed_cmd_env`, `setup_fp8_env`, `PrepareForLaunch`). The env-var names are
+the reference's (ACCELERATE_*, FSDP_*, PARALLELISM_CONFIG_*) so scripts and configs carry over.
+
+MI355X-first differences:
+  * every multi-process launch is `torch.distributed.run` with one rank per GPU over RCCL (no DeepSpeed / MPI /
+    XLA launchers). A DeepSpeed request is translated into the equivalent native FSDP2 / DDP configuration
+    (ZeRO-3 → FULL_SHARD, ZeRO-2 → SHARD_GRAD_OP, ZeRO-0/1 → DDP) because the FSDP engine here *is* the ZeRO
+    implementation.
+  * GPU selection goes through `HIP_VISIBLE_DEVICES`; CPU affinity pins each rank to its GPU's NUMA node.
+  * RCCL tuning knobs of this framework travel as ACCELERATE_RCCL_* (bucket size / prefetch depth / priority).
+"""
+
+from __future__ import annotations
+
+import argparse
+import os
+import subprocess
+import sys
+from typing import Any, Optional
+
+import torch
+
+from .constants import TORCH_LAUNCH_PARAMS
+from .dataclasses import DistributedType
+from .environment import str_to_bool
+
+# ------------------------------------------------------------------------------------------------------------
+# argument → env tables.  Each row: (arg attribute, env name, formatter)
+# ------------------------------------------------------------------------------------------------------------
+
+
+def _as_str(v):
+    return str(v)
+
+
+def _as_bool(v):
+    return str(bool(v) if not isinstance(v, str) else bool(str_to_bool(v))).lower()
+
+
+def _as_upper(v):
+    return str(v).upper()
+
+
+_FSDP_ENV = [
+    ("fsdp_version", "FSDP_VERSION", _as_str),
+    ("fsdp_sharding_strategy", "FSDP_SHARDING_STRATEGY", _as_str),
+    ("fsdp_reshard_after_forward", "FSDP_RESHARD_AFTER_FORWARD", _as_str),
+    ("fsdp_offload_params", "FSDP_OFFLOAD_PARAMS", _as_bool),
+    ("fsdp_min_num_params", "FSDP_MIN_NUM_PARAMS", _as_str),
+    ("fsdp_auto_wrap_policy", "FSDP_AUTO_WRAP_POLICY", _as_str),
+    ("fsdp_transformer_layer_cls_to_wrap", "FSDP_TRANSFORMER_CLS_TO_WRAP", _as_str),
+    ("fsdp_backward_prefetch", "FSDP_BACKWARD_PREFETCH", _as_str),
+    ("fsdp_state_dict_type", "FSDP_STATE_DICT_TYPE", _as_str),
+    ("fsdp_forward_prefetch", "FSDP_FORWARD_PREFETCH", _as_bool),
+    ("fsdp_use_orig_params", "FSDP_USE_ORIG_PARAMS", _as_bool),
+    ("fsdp_cpu_ram_efficient_loading", "FSDP_CPU_RAM_EFFICIENT_LOADING", _as_bool),
+    ("fsdp_sync_module_states", "FSDP_SYNC_MODULE_STATES", _as_bool),
+    ("fsdp_activation_checkpointing", "FSDP_ACTIVATION_CHECKPOINTING", _as_bool),
+]
+
+_PARALLELISM_ENV = [
+    ("parallelism_config_dp_replicate_size", "PARALLELISM_CONFIG_DP_REPLICATE_SIZE", _as_str),
+    ("parallelism_config_dp_shard_size", "PARALLELISM_CONFIG_DP_SHARD_SIZE", _as_str),
+    ("parallelism_config_tp_size", "PARALLELISM_CONFIG_TP_SIZE", _as_str),
+    ("parallelism_config_cp_size", "PARALLELISM_CONFIG_CP_SIZE", _as_str),
+    ("parallelism_config_cp_backend", "PARALLELISM_CONFIG_CP_BACKEND", _as_str),
+    ("parallelism_config_cp_comm_strategy", "PARALLELISM_CONFIG_CP_COMM_STRATEGY", _as_str),
+    ("parallelism_config_sp_size", "PARALLELISM_CONFIG_SP_SIZE", _as_str),
+    ("parallelism_config_sp_backend", "PARALLELISM_CONFIG_SP_BACKEND", _as_str),
+    ("parallelism_config_sp_seq_length", "PARALLELISM_CONFIG_SP_SEQ_LENGTH", _as_str),
+    ("parallelism_config_sp_seq_length_is_variable", "PARALLELISM_CONFIG_SP_SEQ_LENGTH_IS_VARIABLE", _as_bool),
+    ("parallelism_config_sp_attn_implementation", "PARALLELISM_CONFIG_SP_ATTN_IMPLEMENTATION", _as_str),
+]
+
+_FP8_ENV = [
+    ("fp8_backend", "ACCELERATE_FP8_BACKEND", _as_upper),
+    ("fp8_format", "ACCELERATE_FP8_FORMAT", _as_upper),
+    ("fp8_margin", "ACCELERATE_FP8_MARGIN", _as_str),
+    ("fp8_interval", "ACCELERATE_FP8_INTERVAL", _as_str),
+    ("fp8_amax_history_len", "ACCELERATE_FP8_AMAX_HISTORY_LEN", _as_str),
+    ("fp8_amax_compute_algo", "ACCELERATE_FP8_AMAX_COMPUTE_ALGO", _as_str),
+    ("fp8_override_linear_precision", "ACCELERATE_FP8_OVERRIDE_LINEAR_PRECISION", _as_str),
+    ("fp8_use_autocast_during_eval", "ACCELERATE_FP8_USE_AUTOCAST_DURING_EVAL", _as_bool),
+    ("fp8_opt_level", "ACCELERATE_FP8_OPT_LEVEL", _as_str),
+    ("fp8_pad_inner_dim", "ACCELERATE_FP8_PAD_INNER_DIM", _as_bool),
+    ("fp8_enable_fsdp_float8_all_gather", "ACCELERATE_FP8_ENABLE_FSDP_FLOAT8_ALL_GATHER", _as_bool),
+]
+
+_DYNAMO_ENV = [
+    ("dynamo_backend", "ACCELERATE_DYNAMO_BACKEND", _as_upper),
+    ("dynamo_mode", "ACCELERATE_DYNAMO_MODE", _as_str),
+    ("dynamo_use_fullgraph", "ACCELERATE_DYNAMO_USE_FULLGRAPH", _as_bool),
+    ("dynamo_use_dynamic", "ACCELERATE_DYNAMO_USE_DYNAMIC", _as_bool),
+    ("dynamo_use_regional_compilation", "ACCELERATE_DYNAMO_USE_REGIONAL_COMPILATION", _as_bool),
+]
+
+_RCCL_ENV = [
+    ("rccl_ddp_bucket_mb", "ACCELERATE_RCCL_DDP_BUCKET_MB", _as_str),
+    ("rccl_fsdp_prefetch", "ACCELERATE_RCCL_FSDP_PREFETCH", _as_str),
+    ("rccl_stream_priority", "ACCELERATE_RCCL_STREAM_PRIORITY", _as_str),
+]
+
+
+def _apply_table(args, env: dict, table) -> dict:
+    for attr, name, fmt in table:
+        v = getattr(args, attr, None)
+        if v is not None:
+            env[name] = fmt(v)
+    return env
+
+
+def _filter_args(args: argparse.Namespace, parser: argparse.ArgumentParser, default_args: Optional[list] = None):
+    """Keep only the attributes of `args` that `parser` understands (its defaults filled from `default_args`)."""
+    known = vars(parser.parse_args(default_args or []))
+    merged = {k: getattr(args, k) for k in known if hasattr(args, k)}
+    return argparse.Namespace(**{**known, **merged})
+
+
+def _convert_nargs_to_dict(nargs: list) -> dict:
+    """`["--lr", "3e-4", "--flag", "--name", "x"]` → `{"lr": 3e-4, "flag": True, "name": "x"}`."""
+
+    def infer(s: str):
+        for conv in (int, float):
+            try:
+                return conv(s)
+            except ValueError:
+                pass
+        if s.lower() in ("true", "false"):
+            return s.lower() == "true"
+        return s
+
+    out, key = {}, None
+    for tok in nargs:
+        if tok.startswith("--"):
+            if "=" in tok:
+                k, v = tok[2:].split("=", 1)
+                out[k] = infer(v)
+                key = None
+            else:
+                key = tok[2:]
+                out[key] = True
+        elif key is not None:
+            out[key] = infer(tok)
+            key = None
+        else:
+            raise ValueError(f"positional value `{tok}` without a preceding `--key`")
+    return out
+
+
+def env_var_path_add(env_var_name: str, path_to_add: str) -> str:
+    parts = [p for p in os.environ.get(env_var_name, "").split(":") if p]
+    parts.append(str(path_to_add))
+    return ":".join(parts)
+
+
+def setup_fp8_env(args: argparse.Namespace, current_env: dict) -> dict:
+    if str(getattr(args, "mixed_precision", "") or "").lower() == "fp8":
+        current_env["ACCELERATE_MIXED_PRECISION"] = "fp8"
+    return _apply_table(args, current_env, _FP8_ENV)
+
+
+def _common_env(args: argparse.Namespace) -> dict:
+    """Env shared by the single- and multi-process launchers."""
+    env = os.environ.copy()
+    env["ACCELERATE_USE_CPU"] = str(bool(getattr(args, "cpu", False)))
+    gpu_ids = getattr(args, "gpu_ids", None)
+    if gpu_ids not in (None, "all"):
+        env["HIP_VISIBLE_DEVICES"] = str(gpu_ids)
+    mp = str(getattr(args, "mixed_precision", None) or "no").lower()
+    if mp not in ("no", "fp16", "bf16", "fp8"):
+        raise ValueError(f"Unknown mixed_precision mode: {mp}. Choose between no/fp16/bf16/fp8.")
+    env["ACCELERATE_MIXED_PRECISION"] = mp
+    if getattr(args, "debug", False):
+        env["ACCELERATE_DEBUG_MODE"] = "true"
+    if getattr(args, "enable_cpu_affinity", False):
+        env["ACCELERATE_CPU_AFFINITY"] = "1"
+    if getattr(args, "downcast_bf16", False):
+        env["ACCELERATE_DOWNCAST_BF16"] = "true"
+    if getattr(args, "gradient_accumulation_steps", None) is not None:
+        env["ACCELERATE_GRADIENT_ACCUMULATION_STEPS"] = str(args.gradient_accumulation_steps)
+    if getattr(args, "gradient_clipping", None) is not None:
+        env["ACCELERATE_GRADIENT_CLIPPING"] = str(args.gradient_clipping)
+    threads = getattr(args, "num_cpu_threads_per_process", None)
+    if threads:
+        env["OMP_NUM_THREADS"] = str(threads)
+    # the host driver only supports dmabuf IPC (RCCL / cross-process tensor sharing)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    _apply_table(args, env, _DYNAMO_ENV)
+    _apply_table(args, env, _RCCL_ENV)
+    setup_fp8_env(args, env)
+    _apply_deepspeed_translation(args, env)
+    if getattr(args, "use_fsdp", False):
+        env["ACCELERATE_USE_FSDP"] = "true"
+        _apply_table(args, env, _FSDP_ENV)
+    if getattr(args, "use_parallelism_config", False):
+        env["ACCELERATE_USE_PARALLELISM_CONFIG"] = "true"
+        _apply_table(args, env, _PARALLELISM_ENV)
+    if getattr(args, "use_megatron_lm", False):
+        raise NotImplementedError(
+            "Megatron-LM is not available on this stack; use `--use_parallelism_config` with tp/cp/dp sizes "
+            "(native TP/CP/FSDP2 over RCCL) instead."
+        )
+    return env
+
+
+def _apply_deepspeed_translation(args, env: dict):
+    """Map a DeepSpeed ZeRO request onto the native engines (see module docstring)."""
+    if not getattr(args, "use_deepspeed", False):
+        return
+    stage = int(getattr(args, "zero_stage", None) or 2)
+    env["ACCELERATE_USE_DEEPSPEED"] = "true"
+    env["ACCELERATE_DEEPSPEED_ZERO_STAGE"] = str(stage)
+    if stage >= 2:
+        env["ACCELERATE_USE_FSDP"] = "true"
+        env["FSDP_VERSION"] = "2"
+        env["FSDP_SHARDING_STRATEGY"] = "FULL_SHARD" if stage == 3 else "SHARD_GRAD_OP"
+        env["FSDP_RESHARD_AFTER_FORWARD"] = "true" if stage == 3 else "false"
+        if str(getattr(args, "offload_param_device", "none")) == "cpu" or str(getattr(args, "offload_optimizer_device", "none")) == "cpu":
+            env["FSDP_OFFLOAD_PARAMS"] = "true"
+        if getattr(args, "zero3_save_16bit_model", False):
+            env["FSDP_STATE_DICT_TYPE"] = "FULL_STATE_DICT"
+    for attr in ("gradient_accumulation_steps", "gradient_clipping"):
+        if getattr(args, attr, None) is not None:
+            env[f"ACCELERATE_{attr.upper()}"] = str(getattr(args, attr))
+
+
+def prepare_simple_launcher_cmd_env(args: argparse.Namespace) -> tuple[list, dict]:
+    """Single process: `python [-m] script args...` with the env contract applied."""
+    cmd = []
+    if getattr(args, "no_python", False) and getattr(args, "module", False):
+        raise ValueError("--module and --no_python cannot be used together")
+    if not getattr(args, "no_python", False):
+        cmd.append(sys.executable)
+        if getattr(args, "module", False):
+            cmd.append("-m")
+    cmd.append(args.training_script)
+    cmd.extend(args.training_script_args)
+    env = _common_env(args)
+    env.setdefault("LOCAL_RANK", "0")
+    env.setdefault("RANK", "0")
+    env.setdefault("WORLD_SIZE", "1")
+    return cmd, env
+
+
+def prepare_multi_gpu_env(args: argparse.Namespace) -> dict:
+    """Env for a `torch.distributed.run` launch (one rank per MI355X). Also normalises the torchrun attributes
+    (`nnodes`, `node_rank`, `nproc_per_node`, `master_addr`, `master_port`, `rdzv_endpoint`) on `args`."""
+    num_machines = int(getattr(args, "num_machines", 1) or 1)
+    num_processes = int(getattr(args, "num_processes", 1) or 1)
+    args.nnodes = str(num_machines)
+    args.node_rank = int(getattr(args, "machine_rank", 0) or 0)
+    # `--num_processes` is the job total (reference semantics); torchrun wants per-node
+    args.nproc_per_node = str(num_processes // num_machines) if num_machines > 1 else str(num_processes)
+    main_ip = getattr(args, "main_process_ip", None)
+    main_port = getattr(args, "main_process_port", None)
+    rdzv = getattr(args, "rdzv_backend", None) or "static"
+    args.rdzv_backend = rdzv
+    if num_machines > 1:
+        args.master_addr = main_ip
+        args.master_port = str(main_port or 29500)
+        if rdzv != "static":
+            args.rdzv_endpoint = f"{main_ip}:{main_port or 29500}"
+    else:
+        args.master_addr = main_ip or "127.0.0.1"
+        args.master_port = str(main_port) if main_port else None
+        if args.master_port is None:
+            from .other import get_free_port
+
+            args.master_port = str(get_free_port())
+    if getattr(args, "module", False) and getattr(args, "no_python", False):
+        raise ValueError("--module and --no_python cannot be used together")
+    env = _common_env(args)
+    env["MASTER_ADDR"] = str(args.master_addr)
+    env["MASTER_PORT"] = str(args.master_port)
+    return env
+
+
+def prepare_deepspeed_cmd_env(args: argparse.Namespace) -> tuple[list, dict]:
+    """DeepSpeed launch requests run through torchrun with the ZeRO→FSDP2 translation applied."""
+    args.use_deepspeed = True
+    env = prepare_multi_gpu_env(args)
+    return build_torchrun_cmd(args), env
+
+
+def build_torchrun_cmd(args: argparse.Namespace) -> list:
+    """Explicit `python -m torch.distributed.run ...` argv equivalent to the launch (for logs / dry runs)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", f"--nnodes={args.nnodes}", f"--nproc-per-node={args.nproc_per_node}"]
+    if int(args.nnodes) > 1 or getattr(args, "rdzv_backend", "static") != "static":
+        cmd += [f"--node-rank={args.node_rank}", f"--rdzv-backend={args.rdzv_backend}"]
+        if getattr(args, "rdzv_endpoint", None):
+            cmd.append(f"--rdzv-endpoint={args.rdzv_endpoint}")
+    cmd += [f"--master-addr={args.master_addr}", f"--master-port={args.master_port}"]
+    for flag in ("max_restarts", "monitor_interval"):
+        if getattr(args, flag, None) is not None:
+            cmd.append(f"--{flag.replace('_', '-')}={getattr(args, flag)}")
+    if getattr(args, "no_python", False):
+        cmd.append("--no-python")
+    if getattr(args, "module", False):
+        cmd.append("--module")
+    cmd.append(args.training_script)
+    cmd.extend(args.training_script_args)
+    return cmd
+
+
+def torchrun_namespace(args: argparse.Namespace) -> argparse.Namespace:
+    """Namespace accepted by `torch.distributed.run.run` (in-process elastic launch)."""
+    from torch.distributed import run as distrib_run
+
+    parser = distrib_run.get_args_parser()
+    ns = parser.parse_args([args.training_script] + list(args.training_script_args))
+    for name in TORCH_LAUNCH_PARAMS:
+        if hasattr(args, name) and getattr(args, name) is not None and hasattr(ns, name):
+            setattr(ns, name, getattr(args, name))
+    ns.nnodes = str(args.nnodes)
+    ns.nproc_per_node = str(args.nproc_per_node)
+    ns.node_rank = int(args.node_rank)
+    ns.master_addr = args.master_addr
+    ns.master_port = int(args.master_port)
+    ns.rdzv_backend = args.rdzv_backend
+    if getattr(args, "rdzv_endpoint", None):
+        ns.rdzv_endpoint = args.rdzv_endpoint
+    ns.training_script = args.training_script
+    ns.training_script_args = list(args.training_script_args)
+    ns.module = bool(getattr(args, "module", False))
+    ns.no_python = bool(getattr(args, "no_python", False))
+    return ns
+
+
+class PrepareForLaunch:
+    """Picklable wrapper that sets the per-rank env then calls `launcher(*args)` (used by notebook / debug
+    launchers spawning processes)."""
+
+    def __init__(self, launcher, distributed_type="NO", debug: bool = False):
+        self.launcher = launcher
+        self.distributed_type = DistributedType(distributed_type)
+        self.debug = debug
+
+    def __call__(self, index: int, *args):
+        if self.debug:
+            world_size = int(os.environ.get("WORLD_SIZE", "1"))
+            os.environ.update(
+                LOCAL_RANK=str(index),
+                RANK=str(index),
+                WORLD_SIZE=str(world_size),
+                ACCELERATE_DEBUG_MODE="true",
+            )
+        elif self.distributed_type in (DistributedType.MULTI_GPU, DistributedType.FSDP, DistributedType.MULTI_CPU):
+            node_rank = int(os.environ.get("NODE_RANK", "0"))
+            nproc = int(os.environ.get("NPROC_PER_NODE", os.environ.get("LOCAL_WORLD_SIZE", "1")))
+            os.environ["LOCAL_RANK"] = str(index)
+            os.environ["RANK"] = str(node_rank * nproc + index)
+        os.environ["FORK_LAUNCHED"] = str(1)
+        self.launcher(*args)
+
+
+def run_child(cmd: list, env: dict) -> int:
+    """Run `cmd` as a child process (never exec: the launcher must not replace itself after GPU init)."""
+    proc = subprocess.Popen(cmd, env=env)
+    return proc.wait()
