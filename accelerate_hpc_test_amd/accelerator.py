@@ -649,7 +649,12 @@ class Accelerator:
 
     def _remap_optimizer_params(self, optimizer):
         """An optimizer created on the original parameters is pointed at the FSDP shard parameters (replaces the
-        reference's `data_ptr` patching, accelerator.py:1690-1744)."""
+        reference's `data_ptr` patching, accelerator.py:1690-1744). TP re-sharding maps are applied first."""
+        for m in self._models:
+            tmap = getattr(extract_model_from_parallel(m), "_tp_param_map", None) or getattr(m, "_tp_param_map", None)
+            if tmap:
+                for group in optimizer.param_groups:
+                    group["params"] = [tmap.get(p, p) for p in group["params"]]
         for eng in self._fsdp_engines:
             pmap = eng.param_map()
             for group in optimizer.param_groups:
@@ -681,9 +686,12 @@ class Accelerator:
                 model.forward = convert_outputs_to_fp32(new_forward)
         if device_placement and not self.verify_device_map(model):
             model = model.to(self.device)
+        if self.parallelism_config is not None and self.parallelism_config.tp_enabled:
+            model = self._prepare_tp(model)
         if not evaluation_mode:
             if self.distributed_type in (DistributedType.MULTI_GPU, DistributedType.MULTI_CPU):
-                if any(p.requires_grad for p in model.parameters()) and self.num_processes > 1:
+                dp_size = self.parallelism_config.data_parallel_size if self.parallelism_config is not None else self.num_processes
+                if any(p.requires_grad for p in model.parameters()) and self.num_processes > 1 and dp_size > 1:
                     kwargs = self.ddp_handler.to_kwargs() if self.ddp_handler is not None else {}
                     from .parallel.ddp import DistributedDataParallel
 
@@ -716,6 +724,18 @@ class Accelerator:
                 model = torch.compile(model, **kw)
             self._models[-1] = model
         return model
+
+    def _prepare_tp(self, model):
+        """Shard the model over the `tp` mesh dim with its TP plan (parity: reference accelerator.py:1579-1639,
+        which defers to transformers' `tp_plan`; here parallel/tensor_parallel.py does the sharding)."""
+        if getattr(model, "_tp_group", None) is not None:
+            return model
+        from .parallel.tensor_parallel import parallelize_module
+
+        handler = self.parallelism_config.tp_handler
+        return parallelize_module(
+            model, self.torch_device_mesh.group("tp"), sequence_parallel=bool(getattr(handler, "sequence_parallel", False))
+        )
 
     def _prepare_fsdp(self, model):
         from .parallel.fsdp import FullyShardedModule, fully_shard
@@ -1173,11 +1193,20 @@ class Accelerator:
 
         if isinstance(model, FullyShardedModule):
             sd = model.engine.full_state_dict(rank0_only=False)
-            return sd
+            return self._gather_tp(sd, model.engine.model)
         if unwrap:
             model = self.unwrap_model(model)
         state_dict = model.state_dict()
-        return OrderedDict((k, v.detach().cpu() if isinstance(v, torch.Tensor) else v) for k, v in state_dict.items())
+        sd = OrderedDict((k, v.detach().cpu() if isinstance(v, torch.Tensor) else v) for k, v in state_dict.items())
+        return self._gather_tp(sd, model)
+
+    @staticmethod
+    def _gather_tp(sd, model):
+        if getattr(model, "_tp_group", None) is None:
+            return sd
+        from .parallel.tensor_parallel import gather_tp_state_dict
+
+        return OrderedDict(gather_tp_state_dict(sd, model))
 
     def register_for_checkpointing(self, *objects):
         invalid_objects = []

@@ -31,7 +31,10 @@ def main(argv=None):
     if not hasattr(args, "func"):
         parser.print_help()
         raise SystemExit(1)
-    return args.func(args)
+    rc = args.func(args)
+    if isinstance(rc, int) and not isinstance(rc, bool) and rc != 0:
+        raise SystemExit(rc)
+    return rc
 
 
 if __name__ == "__main__":

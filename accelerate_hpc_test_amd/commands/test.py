@@ -28,6 +28,8 @@ def test_command(args):
     rc = run_child(cmd, os.environ.copy())
     if rc == 0:
         print("Test is a success! You are ready for your distributed training!")
+    else:
+        print(f"Test failed (exit code {rc}).")
     return rc
 
 

@@ -101,9 +101,18 @@ class LlamaAttention(nn.Module):
         # Optional ring / Ulysses attention installed by parallel/context_parallel.py.
         self.attention_impl = None
 
+    def shard_heads(self, tp_size: int):
+        """Called by parallel/tensor_parallel.py after the qkv/o projections were sharded over `tp_size` ranks."""
+        if self.n_q % tp_size or self.n_kv % tp_size:
+            raise ValueError(f"tp={tp_size} must divide both head counts ({self.n_q} q, {self.n_kv} kv)")
+        self.n_q //= tp_size
+        self.n_kv //= tp_size
+
     def forward(self, x, cos, sin, position_ids=None):
-        B, S, _ = x.shape
-        qkv = self.qkv_proj(x).view(B, S, self.n_q + 2 * self.n_kv, self.head_dim)
+        B, S = x.shape[0], x.shape[1]
+        qkv = self.qkv_proj(x)
+        S = qkv.shape[1]  # sequence-parallel TP gathers the sequence inside qkv_proj
+        qkv = qkv.view(B, S, self.n_q + 2 * self.n_kv, self.head_dim)
         qkv = apply_rope(qkv, cos, sin, self.n_q + self.n_kv, position_ids)
         if self.attention_impl is not None:
             o = self.attention_impl(qkv, self.n_q, self.n_kv)
@@ -203,6 +212,33 @@ class LlamaForCausalLM(nn.Module):
             shifted[:, :-1] = labels[:, 1:]
             loss = cross_entropy(logits, shifted, ignore_index=-100, inplace_backward=not return_logits)
         return CausalLMOutput(loss=loss, logits=logits if return_logits else None)
+
+    # ----- tensor parallelism ---------------------------------------------------------------------------
+    def tp_plan(self, sequence_parallel: bool = False) -> dict:
+        """Megatron layout for parallel/tensor_parallel.py: fused qkv / gate|up sharded per segment (whole heads,
+        matching gate and up rows), o/down row-parallel, lm_head column-parallel with gathered logits."""
+        c = self.config
+        qkv = [c.num_attention_heads * c.head_dim, c.num_key_value_heads * c.head_dim, c.num_key_value_heads * c.head_dim]
+        from ..parallel.tensor_parallel import ColwiseParallel, RowwiseParallel
+
+        plan = {
+            "layers.*.self_attn.qkv_proj": ColwiseParallel(segments=qkv),
+            "layers.*.self_attn.o_proj": RowwiseParallel(),
+            "layers.*.mlp.gate_up_proj": ColwiseParallel(segments=[c.intermediate_size, c.intermediate_size]),
+            "layers.*.mlp.down_proj": RowwiseParallel(),
+        }
+        if not c.tie_word_embeddings:
+            plan["lm_head"] = ColwiseParallel(gather_output=True)
+        if sequence_parallel:
+            plan.update({
+                "embed_tokens": "seq_split",
+                "layers.*.input_layernorm": "sequence_parallel",
+                "layers.*.post_attention_layernorm": "sequence_parallel",
+                "norm": "sequence_parallel",
+            })
+            if c.tie_word_embeddings:
+                raise ValueError("sequence-parallel TP needs an untied lm_head")
+        return plan
 
     # ----- HF interop -----------------------------------------------------------------------------------
     @classmethod

@@ -198,6 +198,9 @@ class FSDPEngine:
                     if p is not None:
                         self._holders.setdefault(id(p), []).append((m, attr))
         old = info.param
+        for tag in ("_tp_spec", "_ep_spec"):  # sharding metadata of TP / EP parameters survives materialisation
+            if hasattr(old, tag):
+                setattr(new, tag, getattr(old, tag))
         for m, attr in self._holders.get(id(old), []):
             m._parameters[attr] = new
         self._holders[id(new)] = self._holders.pop(id(old), [])

@@ -288,8 +288,9 @@ class ParallelismConfig:
                 f"ParallelismConfig total_size ({self.total_size}) does not match num_processes "
                 f"({accelerator.num_processes}). Please adjust dp_replicate_size/ dp_shard_size/tp_size/cp_size/sp_size."
             )
-        if self.total_size > 1 and not (accelerator.is_fsdp2 or accelerator.multi_device):
-            raise ValueError("ParallelismConfig is only compatible with DistributedType.FSDP (version 2) or MULTI_GPU.")
+        # MULTI_CPU is accepted too: the gloo fake cluster exercises the same mesh logic on CPU.
+        if self.total_size > 1 and not (accelerator.is_fsdp2 or accelerator.multi_device or accelerator.distributed_type == "MULTI_CPU"):
+            raise ValueError("ParallelismConfig is only compatible with DistributedType.FSDP (version 2), MULTI_GPU or MULTI_CPU.")
         for parallelism, size in self._sizes.items():
             if size == 1 and getattr(self, f"{parallelism}_handler", None) is not None:
                 _warnings.add(f"ParallelismConfig.{parallelism}_handler is set, but {parallelism}_size is set to 1. This handler will be ignored.")

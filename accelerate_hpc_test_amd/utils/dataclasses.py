@@ -798,7 +798,11 @@ class DeepSpeedSequenceParallelConfig:
 
 @dataclass
 class TorchTensorParallelConfig:
+    """TP options (parity: reference dataclasses.py:2263-2282). `sequence_parallel` keeps the residual stream
+    sequence-sharded between TP regions (all-gather / reduce-scatter instead of all-reduce)."""
+
     enable_async_tp: bool = False
+    sequence_parallel: bool = False
 
 
 @dataclass

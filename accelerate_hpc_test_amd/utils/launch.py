@@ -188,6 +188,11 @@ def _common_env(args: argparse.Namespace) -> dict:
         env["OMP_NUM_THREADS"] = str(threads)
     # the host driver only supports dmabuf IPC (RCCL / cross-process tensor sharing)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    # the framework is used in-tree (its HIP extension is built in place): make it importable by the workers
+    pkg_parent = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    paths = [p for p in env.get("PYTHONPATH", "").split(os.pathsep) if p]
+    if pkg_parent not in paths:
+        env["PYTHONPATH"] = os.pathsep.join([pkg_parent] + paths)
     _apply_table(args, env, _DYNAMO_ENV)
     _apply_table(args, env, _RCCL_ENV)
     setup_fp8_env(args, env)

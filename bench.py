@@ -34,6 +34,9 @@ def parse():
     p.add_argument("--activation-checkpointing", action="store_true")
     p.add_argument("--prefetch", type=int, default=1)
     p.add_argument("--verbose", action="store_true")
+    p.add_argument("--gemm-tuning", default="auto", choices=["auto", "off", "tune"],
+                   help="auto: load the committed hipBLASLt per-shape table (ops/tuned); tune: search and write it")
+    p.add_argument("--gemm-table", default=None, help="table path for --gemm-tuning auto/tune")
     return p.parse_args()
 
 
@@ -73,6 +76,14 @@ def main():
     )
     set_seed(0)
     world = accelerator.num_processes
+    from accelerate_hpc_test_amd.ops import gemm_tuning
+
+    gemm_table = None
+    if args.gemm_tuning == "tune":
+        gemm_table = args.gemm_table or os.path.join("gpurun_out", "tunableop_gfx950.csv")
+        gemm_tuning.start_gemm_tuning(gemm_table)
+    elif args.gemm_tuning == "auto":
+        gemm_table = (args.gemm_table or gemm_tuning.DEFAULT_TABLE) if gemm_tuning.load_tuned_gemms(args.gemm_table) else None
     cfg = LLAMA_PRESETS[args.model]
 
     t0 = time.time()
@@ -106,6 +117,8 @@ def main():
         if args.verbose:
             torch.cuda.synchronize()
             accelerator.print(f"warmup step {i}: {time.time() - tw:.3f}s loss {last_loss.item():.4f}", flush=True)
+    if args.gemm_tuning == "tune":
+        gemm_tuning.finish_gemm_tuning()  # search done during warmup; the timed steps use the tuned table
 
     accelerator.wait_for_everyone()
     torch.cuda.synchronize()
@@ -152,6 +165,7 @@ def main():
             "peak_mem_gib": round(peak, 1),
             "final_loss": round(last_loss.item(), 4) if last_loss is not None else None,
             "baseline_tokens_per_sec": BASELINE_TOKENS_PER_SEC_PER_DEVICE * world,
+            "gemm_table": os.path.basename(gemm_table) if gemm_table else None,
         }
         print(json.dumps(rec), flush=True)
     accelerator.end_training()

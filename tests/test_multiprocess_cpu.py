@@ -36,5 +36,14 @@ def test_fsdp_no_sync_accumulation():
     debug_launcher(td.check_fsdp_no_sync_accumulation, num_processes=2)
 
 
+@pytest.mark.parametrize("sequence_parallel", [False, True])
+def test_tensor_parallel_matches_single_process(sequence_parallel):
+    debug_launcher(td.check_tp_matches_single, args=(sequence_parallel,), num_processes=2)
+
+
+def test_tensor_parallel_x_fsdp_2d():
+    debug_launcher(td.check_tp_matches_single, args=(False, 2), num_processes=4)
+
+
 def test_fsdp_three_ranks():
     debug_launcher(td.check_fsdp_matches_single, args=(True, "SHARDED_STATE_DICT"), num_processes=3)
