@@ -645,7 +645,20 @@ class Accelerator:
         for item in result:
             if any(item in container for container in (self._dataloaders, self._models, self._optimizers, self._schedulers)):
                 item._is_accelerate_prepared = True
+        if self.parallelism_config is not None and self.parallelism_config.sp_enabled:
+            # reference accelerator.py:2393-2409: sequence-parallel data-loader adapter after the model is prepared
+            result = tuple(self.deepspeed_ulysses_dl_adapter(x, None) if isinstance(x, (DataLoaderShard, DataLoaderDispatcher)) else x for x in result)
         return result if len(result) > 1 else result[0]
+
+    def deepspeed_ulysses_dl_adapter(self, dl, model=None):
+        """Cut batches along the sequence for Ulysses SP (parity name with reference accelerator.py:2458-2476)."""
+        if self.parallelism_config is None or not self.parallelism_config.sp_enabled:
+            return dl
+        from .parallel.ulysses import UlyssesSPDataLoaderAdapter
+
+        mesh = self.torch_device_mesh
+        return UlyssesSPDataLoaderAdapter(dl, sp_rank=mesh.local_rank("sp"), sp_group=mesh.group("sp"),
+                                          sp_world_size=mesh.size("sp"), device=self.device)
 
     def _remap_optimizer_params(self, optimizer):
         """An optimizer created on the original parameters is pointed at the FSDP shard parameters (replaces the
@@ -688,6 +701,14 @@ class Accelerator:
             model = model.to(self.device)
         if self.parallelism_config is not None and self.parallelism_config.tp_enabled:
             model = self._prepare_tp(model)
+        if self.parallelism_config is not None and self.parallelism_config.sp_enabled:
+            from .parallel.ulysses import install_ulysses
+
+            if self.distributed_type != DistributedType.FSDP:
+                raise ValueError("Ulysses sequence parallelism needs the FSDP2 engine (params are sharded over dp_shard x sp).")
+            if install_ulysses(model, self.torch_device_mesh.group("sp")) == 0:
+                raise ValueError("Ulysses SP: the model exposes no `attention_impl` hook; wrap the step in "
+                                 "`parallel.ulysses.ulysses_sdpa_context` for SDPA-based models.")
         if not evaluation_mode:
             if self.distributed_type in (DistributedType.MULTI_GPU, DistributedType.MULTI_CPU):
                 dp_size = self.parallelism_config.data_parallel_size if self.parallelism_config is not None else self.num_processes

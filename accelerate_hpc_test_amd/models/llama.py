@@ -194,9 +194,18 @@ class LlamaForCausalLM(nn.Module):
             self._rope_cache[key] = rope_tables(n, self.config.head_dim, self.config.rope_theta, device, self.config.rope_scaling)
         return self._rope_cache[key]
 
-    def forward(self, input_ids, labels=None, position_ids=None, attention_mask=None, return_logits: bool = True):
+    def forward(self, input_ids, labels=None, position_ids=None, attention_mask=None, return_logits: bool = True,
+                shift_labels=None):
+        """`labels` are shifted inside (HF convention). Under context/sequence parallelism pass `shift_labels`
+        (already shifted on the full sequence, then sharded) instead."""
         B, S = input_ids.shape
-        cos, sin = self._rope(S if position_ids is None else int(self.config.max_position_embeddings), input_ids.device)
+        if position_ids is None and getattr(self, "_cp_position_ids", None) is not None:
+            position_ids = self._cp_position_ids  # global positions of this rank's context-parallel shard
+        rope_len = S
+        if position_ids is not None:
+            rope_len = max(int(self.config.max_position_embeddings), getattr(self, "_cp_seq_len", None) or 0,
+                           S * getattr(self, "_seq_parallel_factor", 1))
+        cos, sin = self._rope(rope_len, input_ids.device)
         h = self.embed_tokens(input_ids)
         dt = self.layers[0].self_attn.qkv_proj.weight.dtype if len(self.layers) else h.dtype
         if h.dtype != dt:
@@ -207,10 +216,11 @@ class LlamaForCausalLM(nn.Module):
         h, _ = self.norm(h, residual)
         logits = self.lm_head(h)
         loss = None
-        if labels is not None:
-            shifted = torch.full_like(labels, -100)
-            shifted[:, :-1] = labels[:, 1:]
-            loss = cross_entropy(logits, shifted, ignore_index=-100, inplace_backward=not return_logits)
+        if shift_labels is None and labels is not None:
+            shift_labels = torch.full_like(labels, -100)
+            shift_labels[:, :-1] = labels[:, 1:]
+        if shift_labels is not None:
+            loss = cross_entropy(logits, shift_labels, ignore_index=-100, inplace_backward=not return_logits)
         return CausalLMOutput(loss=loss, logits=logits if return_logits else None)
 
     # ----- tensor parallelism ---------------------------------------------------------------------------

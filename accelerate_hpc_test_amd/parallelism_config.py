@@ -58,8 +58,10 @@ class RankMesh:
     def _all_named_dims(self):
         named = {d: (d,) for d in _DIM_ORDER}
         named["dp"] = ("dp_replicate", "dp_shard")
-        named["dp_shard_cp"] = ("dp_shard", "cp")
-        named["dp_cp"] = ("dp_replicate", "dp_shard", "cp")
+        # Ranks that differ in cp or sp hold identical (replicated) parameters and see disjoint tokens of the same
+        # batch, so FSDP shards over them and the loss is averaged over them — sp is folded in like cp.
+        named["dp_shard_cp"] = ("dp_shard", "cp", "sp")
+        named["dp_cp"] = ("dp_replicate", "dp_shard", "cp", "sp")
         return named
 
     def _make_groups(self, dims):
@@ -171,6 +173,8 @@ class ParallelismConfig:
             dims.append("dp_shard")
         if self.cp_enabled:
             dims.append("cp")
+        if self.sp_enabled:
+            dims.append("sp")
         return dims
 
     @property
@@ -184,6 +188,8 @@ class ParallelismConfig:
             dims.append("dp_shard")
         if self.cp_enabled:
             dims.append("cp")
+        if self.sp_enabled:
+            dims.append("sp")
         return dims
 
     @property

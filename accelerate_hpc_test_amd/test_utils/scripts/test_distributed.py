@@ -240,6 +240,143 @@ def check_tp_matches_single(sequence_parallel: bool = False, dp_shard: int = 1, 
         assert torch.allclose(full[n].float(), q.float(), atol=2e-5), (n, (full[n] - q).abs().max())
 
 
+def check_ring_attention(strategy: str = "allgather"):
+    """Zig-zag ring attention (fwd + bwd) on a cp group == full causal attention on one process."""
+    import torch.distributed as dist
+
+    from accelerate_hpc_test_amd.ops.fused import attention_reference
+    from accelerate_hpc_test_amd.parallel.context_parallel import ring_attention, zigzag_shard
+
+    PartialState(cpu=True)
+    W, r = dist.get_world_size(), dist.get_rank()
+    g = torch.Generator().manual_seed(0)
+    B, S, Hq, Hkv, D = 2, 8 * W, 4, 2, 16
+    q = torch.randn(B, S, Hq, D, generator=g)
+    k = torch.randn(B, S, Hkv, D, generator=g)
+    v = torch.randn(B, S, Hkv, D, generator=g)
+    w = torch.randn(B, S, Hq, D, generator=g)
+    # reference
+    qr, kr, vr = (t.clone().requires_grad_() for t in (q, k, v))
+    (attention_reference(qr, kr, vr, causal=True) * w).sum().backward()
+    # ring
+    ql, kl, vl = (zigzag_shard(t, 1, W, r).requires_grad_() for t in (q, k, v))
+    o = ring_attention(ql, kl, vl, None, strategy=strategy)
+    ref_o = zigzag_shard(attention_reference(q, k, v, causal=True), 1, W, r)
+    assert torch.allclose(o, ref_o, atol=1e-5), (o - ref_o).abs().max()
+    (o * zigzag_shard(w, 1, W, r)).sum().backward()
+    for name, got, ref in (("dq", ql.grad, qr.grad), ("dk", kl.grad, kr.grad), ("dv", vl.grad, vr.grad)):
+        exp = zigzag_shard(ref, 1, W, r)
+        assert torch.allclose(got, exp, atol=1e-4), (name, (got - exp).abs().max())
+
+
+def check_cp_llama_matches_single(strategy: str = "allgather", steps: int = 2):
+    """Llama trained under `maybe_context_parallel` (cp = world, FSDP over dp_shard×cp) == one process."""
+    from accelerate_hpc_test_amd import ParallelismConfig
+    from accelerate_hpc_test_amd.models.llama import LlamaForCausalLM
+    from accelerate_hpc_test_amd.utils.dataclasses import TorchContextParallelConfig
+
+    W = int(os.environ["WORLD_SIZE"])
+    pc = ParallelismConfig(cp_size=W, cp_handler=TorchContextParallelConfig(cp_comm_strategy=strategy))
+    plugin = FullyShardedDataParallelPlugin(fsdp_version=2, auto_wrap_policy="transformer_based_wrap",
+                                            transformer_cls_names_to_wrap=["LlamaDecoderLayer"])
+    acc = Accelerator(cpu=True, parallelism_config=pc, fsdp_plugin=plugin)
+    set_seed(0)
+    base = LlamaForCausalLM(_tiny_llama_cfg())
+    base.init_weights()
+    model = copy.deepcopy(base)
+    opt = torch.optim.SGD(model.parameters(), lr=0.5, momentum=0.9)
+    base_opt = torch.optim.SGD(base.parameters(), lr=0.5, momentum=0.9)
+    model, opt = acc.prepare(model, opt)
+    g = torch.Generator().manual_seed(7)
+    B, S = 2, 8 * W
+    for _ in range(steps):
+        ids = torch.randint(0, 128, (B, S), generator=g)
+        shift = torch.randint(0, 128, (B, S), generator=g)  # every position valid: equal token counts per rank
+        ref = base(ids, shift_labels=shift)
+        ref.loss.backward()
+        base_opt.step()
+        base_opt.zero_grad()
+        ids_l, shift_l = ids.clone(), shift.clone()
+        with acc.maybe_context_parallel(buffers=[ids_l, shift_l], buffer_seq_dims=[1, 1], no_restore_buffers={ids_l, shift_l}):
+            assert ids_l.shape[1] == S // W
+            out = model(ids_l, shift_labels=shift_l)
+            acc.backward(out.loss)
+        opt.step()
+        opt.zero_grad()
+        lg = acc.reduce(out.loss.detach().reshape(1), reduction="mean")
+        assert torch.allclose(lg, ref.loss.detach().reshape(1), atol=2e-5), (lg, ref.loss)
+    full = acc.get_state_dict(model)
+    for n, q in base.state_dict().items():
+        assert torch.allclose(full[n].float(), q.float(), atol=5e-5), (n, (full[n] - q).abs().max())
+
+
+def check_ulysses_attention():
+    """All-to-all (Ulysses) attention on contiguous sequence slices == full causal attention (fwd + bwd)."""
+    import torch.distributed as dist
+
+    from accelerate_hpc_test_amd.ops.fused import attention_reference
+    from accelerate_hpc_test_amd.parallel.ulysses import ulysses_attention
+
+    PartialState(cpu=True)
+    W, r = dist.get_world_size(), dist.get_rank()
+    g = torch.Generator().manual_seed(0)
+    B, S, Hq, Hkv, D = 2, 4 * W, 4, 2, 8
+    q, k, v, w = (torch.randn(B, S, h, D, generator=g) for h in (Hq, Hkv, Hkv, Hq))
+    qr, kr, vr = (t.clone().requires_grad_() for t in (q, k, v))
+    ref = attention_reference(qr, kr, vr, causal=True)
+    (ref * w).sum().backward()
+    L = S // W
+    sl = slice(r * L, (r + 1) * L)
+    ql, kl, vl = (t[:, sl].clone().requires_grad_() for t in (q, k, v))
+    o = ulysses_attention(ql, kl, vl, None)
+    assert torch.allclose(o, ref[:, sl].detach(), atol=1e-5), (o - ref[:, sl]).abs().max()
+    (o * w[:, sl]).sum().backward()
+    for name, got, exp in (("dq", ql.grad, qr.grad), ("dk", kl.grad, kr.grad), ("dv", vl.grad, vr.grad)):
+        assert torch.allclose(got, exp[:, sl], atol=1e-4), (name, (got - exp[:, sl]).abs().max())
+
+
+def check_ulysses_llama_matches_single(steps: int = 2):
+    """Llama with Ulysses SP (sp = world) fed through the prepared data loader == one process on full batches."""
+    from accelerate_hpc_test_amd import ParallelismConfig
+    from accelerate_hpc_test_amd.models.llama import LlamaForCausalLM
+
+    W = int(os.environ["WORLD_SIZE"])
+    pc = ParallelismConfig(sp_size=W)
+    plugin = FullyShardedDataParallelPlugin(fsdp_version=2, auto_wrap_policy="transformer_based_wrap",
+                                            transformer_cls_names_to_wrap=["LlamaDecoderLayer"])
+    acc = Accelerator(cpu=True, parallelism_config=pc, fsdp_plugin=plugin)
+    set_seed(0)
+    base = LlamaForCausalLM(_tiny_llama_cfg())
+    base.init_weights()
+    model = copy.deepcopy(base)
+    opt = torch.optim.SGD(model.parameters(), lr=0.5, momentum=0.9)
+    base_opt = torch.optim.SGD(base.parameters(), lr=0.5, momentum=0.9)
+    g = torch.Generator().manual_seed(11)
+    B, S = 2, 8 * W
+    data = [{"input_ids": torch.randint(0, 128, (S,), generator=g), "shift_labels": torch.randint(0, 128, (S,), generator=g)}
+            for _ in range(steps * B)]
+    dl = torch.utils.data.DataLoader(data, batch_size=B)
+    model, opt, dl = acc.prepare(model, opt, dl)
+    for i, batch in enumerate(dl):
+        assert batch["input_ids"].shape == (B, S // W) and "position_ids" in batch
+        out = model(batch["input_ids"], shift_labels=batch["shift_labels"], position_ids=batch["position_ids"])
+        acc.backward(out.loss)
+        opt.step()
+        opt.zero_grad()
+        full = data[i * B : (i + 1) * B]
+        ids = torch.stack([d["input_ids"] for d in full])
+        sl = torch.stack([d["shift_labels"] for d in full])
+        ref = base(ids, shift_labels=sl)
+        ref.loss.backward()
+        base_opt.step()
+        base_opt.zero_grad()
+        lg = acc.reduce(out.loss.detach().reshape(1), reduction="mean")
+        assert torch.allclose(lg, ref.loss.detach().reshape(1), atol=2e-5), (lg, ref.loss)
+    sd = acc.get_state_dict(model)
+    for n, q in base.state_dict().items():
+        assert torch.allclose(sd[n].float(), q.float(), atol=5e-5), (n, (sd[n] - q).abs().max())
+
+
 def main():
     check_ops()
     check_dataloader_sharding()

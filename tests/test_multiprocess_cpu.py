@@ -45,5 +45,29 @@ def test_tensor_parallel_x_fsdp_2d():
     debug_launcher(td.check_tp_matches_single, args=(False, 2), num_processes=4)
 
 
+@pytest.mark.parametrize("strategy", ["allgather", "alltoall"])
+def test_ring_attention_matches_full(strategy):
+    debug_launcher(td.check_ring_attention, args=(strategy,), num_processes=2)
+
+
+def test_ring_attention_four_ranks():
+    debug_launcher(td.check_ring_attention, args=("alltoall",), num_processes=4)
+
+
+@pytest.mark.parametrize("strategy", ["allgather", "alltoall"])
+def test_context_parallel_llama(strategy):
+    debug_launcher(td.check_cp_llama_matches_single, args=(strategy,), num_processes=2)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_ulysses_attention_matches_full(world):
+    # world 4 with 2 kv heads exercises kv-head replication
+    debug_launcher(td.check_ulysses_attention, num_processes=world)
+
+
+def test_ulysses_llama_matches_single_process():
+    debug_launcher(td.check_ulysses_llama_matches_single, num_processes=2)
+
+
 def test_fsdp_three_ranks():
     debug_launcher(td.check_fsdp_matches_single, args=(True, "SHARDED_STATE_DICT"), num_processes=3)
