@@ -1,0 +1,70 @@
+"""LocalSGD: train `local_sgd_steps` steps without gradient sync, then average the *parameters* across ranks.
+
+Parity target: `/root/reference/src/accelerate/local_sgd.py:19-106` (context manager wrapping `no_sync`, `step()`
+counting, parameter mean on every K-th step and on exit). The reference averages parameter by parameter
+(`accelerator.reduce(param, "mean")` per tensor → one collective per parameter); here all parameters of one dtype
+are packed into a single flat buffer and averaged with ONE RCCL all-reduce (a 16 GB model = one large xGMI
+all-reduce instead of ~300 small latency-bound ones), then unpacked.
+"""
+
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from .accelerator import Accelerator
+from .utils.dataclasses import DistributedType
+
+
+class LocalSGD:
+    def __enter__(self):
+        if self.enabled:
+            self.model_sync_obj = self.model.no_sync()
+            self.model_sync_obj.__enter__()
+        return self
+
+    def __exit__(self, type, value, tb):
+        if self.enabled:
+            # average parameters once more so every rank leaves the block with the same model
+            self._sync_and_avg_model_params()
+            self.model_sync_obj.__exit__(type, value, tb)
+
+    def __init__(self, accelerator: Accelerator, model: torch.nn.Module, local_sgd_steps: int, enabled: bool = True):
+        if accelerator.distributed_type not in (DistributedType.NO, DistributedType.MULTI_CPU, DistributedType.MULTI_GPU):
+            raise NotImplementedError("LocalSGD is supported only for CPU and GPU data parallelism (no FSDP / DeepSpeed).")
+        self.enabled = enabled and accelerator.distributed_type != DistributedType.NO
+        self.num_steps = 0
+        if self.enabled:
+            self.accelerator = accelerator
+            self.model = model
+            self.local_sgd_steps = local_sgd_steps
+
+    def step(self):
+        """Call after every optimizer step; averages parameters every `local_sgd_steps` calls."""
+        self.num_steps += 1
+        if not self.enabled:
+            return
+        if self.num_steps % self.local_sgd_steps == 0:
+            self._sync_and_avg_model_params()
+
+    @torch.no_grad()
+    def _sync_and_avg_model_params(self):
+        self.accelerator.wait_for_everyone()
+        model = self.accelerator.unwrap_model(self.model)
+        group = getattr(self.model, "process_group", None)
+        world = dist.get_world_size(group)
+        by_dtype: dict = {}
+        for p in model.parameters():
+            by_dtype.setdefault((p.dtype, p.device), []).append(p)
+        for (dtype, device), params in by_dtype.items():
+            flat = torch.cat([p.detach().reshape(-1) for p in params])
+            if dist.get_backend(group) == "gloo" or not dtype.is_floating_point:
+                dist.all_reduce(flat, group=group)
+                flat.div_(world)
+            else:
+                dist.all_reduce(flat, op=dist.ReduceOp.AVG, group=group)
+            off = 0
+            for p in params:
+                n = p.numel()
+                p.copy_(flat[off : off + n].view_as(p))
+                off += n

@@ -377,6 +377,74 @@ def check_ulysses_llama_matches_single(steps: int = 2):
         assert torch.allclose(sd[n].float(), q.float(), atol=5e-5), (n, (sd[n] - q).abs().max())
 
 
+def check_local_sgd(k: int = 2, steps: int = 4):
+    """LocalSGD == every rank trains alone for k steps, then parameters are averaged (simulated locally)."""
+    from accelerate_hpc_test_amd.local_sgd import LocalSGD
+
+    acc = Accelerator(cpu=True)
+    W, r = acc.num_processes, acc.process_index
+    set_seed(0)
+    base = TinyMLP()
+    sims = [copy.deepcopy(base) for _ in range(W)]
+    sim_opts = [torch.optim.SGD(m.parameters(), lr=0.1) for m in sims]
+    model = copy.deepcopy(base)
+    opt = torch.optim.SGD(model.parameters(), lr=0.1)
+    model, opt = acc.prepare(model, opt)
+    bs = 4
+    batches = _global_batches(steps, bs, W)
+    with LocalSGD(acc, model, local_sgd_steps=k) as local_sgd:
+        for step, (x, y) in enumerate(batches):
+            acc.backward(F.mse_loss(model(x[r * bs : (r + 1) * bs]), y[r * bs : (r + 1) * bs]))
+            opt.step()
+            opt.zero_grad()
+            local_sgd.step()
+            for j, (m, o) in enumerate(zip(sims, sim_opts)):
+                F.mse_loss(m(x[j * bs : (j + 1) * bs]), y[j * bs : (j + 1) * bs]).backward()
+                o.step()
+                o.zero_grad()
+            if (step + 1) % k == 0:
+                with torch.no_grad():
+                    for ps in zip(*[m.parameters() for m in sims]):
+                        avg = sum(p.detach() for p in ps) / W
+                        for p in ps:
+                            p.copy_(avg)
+    inner = acc.unwrap_model(model)
+    for (n, p), q in zip(inner.named_parameters(), sims[0].parameters()):
+        assert torch.allclose(p, q, atol=1e-6), (n, (p - q).abs().max())
+
+
+def check_pipeline_inference(gather_output: bool = True, split="auto"):
+    """prepare_pippy: the staged model's logits (micro-batched) == the full model's logits on one process."""
+    import torch.distributed as dist
+
+    from accelerate_hpc_test_amd.inference import prepare_pippy
+    from accelerate_hpc_test_amd.models.llama import LlamaConfig, LlamaForCausalLM
+
+    state = PartialState(cpu=True)
+    W, r = state.num_processes, state.process_index
+    cfg = LlamaConfig(vocab_size=128, hidden_size=64, intermediate_size=96, num_hidden_layers=2 * W,
+                      num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=64)
+    set_seed(0)
+    model = LlamaForCausalLM(cfg)
+    model.init_weights()
+    ids = torch.randint(0, 128, (4, 16), generator=torch.Generator().manual_seed(1))
+    with torch.no_grad():
+        ref = model(ids).logits
+    splits = split if split == "auto" else [f"layers.{2 * i}" for i in range(1, W)]
+    model = prepare_pippy(model, split_points=splits, gather_output=gather_output, num_chunks=2)
+    assert len(model.hf_split_points) == W - 1
+    # this rank only materialised its own stage
+    n_real = sum(p.numel() for p in model.parameters() if p.device.type != "meta")
+    n_all = sum(p.numel() for p in model.parameters())
+    assert n_real < n_all
+    out = model(ids)
+    if gather_output or r == W - 1:
+        assert torch.allclose(out.logits, ref, atol=1e-5), (out.logits - ref).abs().max()
+    else:
+        assert out is None
+    dist.barrier()
+
+
 def main():
     check_ops()
     check_dataloader_sharding()

@@ -69,5 +69,18 @@ def test_ulysses_llama_matches_single_process():
     debug_launcher(td.check_ulysses_llama_matches_single, num_processes=2)
 
 
+@pytest.mark.parametrize("gather_output,split", [(True, "auto"), (False, "explicit")])
+def test_pipeline_inference(gather_output, split):
+    debug_launcher(td.check_pipeline_inference, args=(gather_output, split), num_processes=2)
+
+
+def test_pipeline_inference_three_stages():
+    debug_launcher(td.check_pipeline_inference, args=(True, "auto"), num_processes=3)
+
+
+def test_local_sgd():
+    debug_launcher(td.check_local_sgd, num_processes=2)
+
+
 def test_fsdp_three_ranks():
     debug_launcher(td.check_fsdp_matches_single, args=(True, "SHARDED_STATE_DICT"), num_processes=3)
