@@ -664,10 +664,12 @@ class Accelerator:
         """An optimizer created on the original parameters is pointed at the FSDP shard parameters (replaces the
         reference's `data_ptr` patching, accelerator.py:1690-1744). TP re-sharding maps are applied first."""
         for m in self._models:
-            tmap = getattr(extract_model_from_parallel(m), "_tp_param_map", None) or getattr(m, "_tp_param_map", None)
-            if tmap:
-                for group in optimizer.param_groups:
-                    group["params"] = [tmap.get(p, p) for p in group["params"]]
+            inner = extract_model_from_parallel(m)
+            for attr in ("_tp_param_map", "_ep_param_map"):
+                tmap = getattr(inner, attr, None) or getattr(m, attr, None)
+                if tmap:
+                    for group in optimizer.param_groups:
+                        group["params"] = [tmap.get(p, p) for p in group["params"]]
         for eng in self._fsdp_engines:
             pmap = eng.param_map()
             for group in optimizer.param_groups:
@@ -774,6 +776,17 @@ class Accelerator:
                 replicate_group = mesh.group("dp_replicate")
         init_fn = getattr(model, "init_weights", None)
         init_fn = (lambda m, _f=init_fn: _f(m)) if init_fn is not None else (lambda m: [getattr(c, "reset_parameters", lambda: None)() for c in m.modules()])
+        if self.parallelism_config is not None and self.parallelism_config.ep_enabled:
+            # Expert parallelism: experts are sharded over the FSDP group by the model itself and stay outside the
+            # flat FSDP units (models/moe.py). Old→new parameter map lets a pre-built optimizer follow.
+            if not hasattr(model, "enable_expert_parallel"):
+                raise ValueError("ep_size > 1 needs a model with `enable_expert_parallel(group)` (e.g. MixtralForCausalLM).")
+            old_by_name = dict(model.named_parameters())
+            ep_modules = model.enable_expert_parallel(group, device=self.device)
+            new_by_name = dict(model.named_parameters())
+            model._ep_param_map = {old_by_name[n]: new_by_name[n] for n in old_by_name if new_by_name.get(n) is not old_by_name[n]}
+            existing = list(plugin.ignored_modules or []) if not isinstance(plugin.ignored_modules, str) else []
+            plugin.ignored_modules = existing + list(ep_modules)
         wrapped = fully_shard(
             model,
             plugin=plugin,

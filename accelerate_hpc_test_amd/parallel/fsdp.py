@@ -181,6 +181,13 @@ class FSDPEngine:
             self._materialize(unit, init_fn, seed)
             self.units.append(unit)
         self.root = self.units[0]
+        # parameters the engine does not own (ignored modules, expert-parallel experts): kept as plain device
+        # tensors; they still take part in the global grad-norm (see clip_grad_norm_)
+        self.extra_names = [n for n, p in self.model.named_parameters() if id(p) in ignored]
+        self.extra_params = [p for p in self.model.parameters() if id(p) in ignored]
+        for p in self.extra_params:
+            if p.device.type != "meta" and p.device != self.device:
+                p.data = p.data.to(self.device)
         for unit in self.units[1:]:
             unit.module.register_forward_pre_hook(self._make_pre_forward(unit), with_kwargs=True)
             unit.module.register_forward_hook(self._make_post_forward(unit), with_kwargs=True)
@@ -541,11 +548,14 @@ class FSDPEngine:
         for unit in self.units:
             for info in unit.infos:
                 yield info.shard_param
+        for _, p in self._extras():
+            yield p
 
     def named_shard_parameters(self):
         for unit in self.units:
             for info in unit.infos:
                 yield info.fqn, info.shard_param
+        yield from self._extras()
 
     def param_map(self) -> dict:
         """original nn.Parameter -> shard nn.Parameter (used to remap optimizers created before prepare)."""
@@ -612,9 +622,15 @@ class FSDPEngine:
         total = torch.zeros(1, dtype=torch.float32, device=self.device)
         if flat_params:
             grad_sq_norm(flat_params, out=total)
+        # non-engine params: expert-parallel shards are disjoint across the group (summed by the all-reduce);
+        # replicated ones are pre-divided by W so the all-reduce counts them once
+        extra = [p for p in getattr(self, "extra_params", []) if p.grad is not None]
+        for p in extra:
+            sq = p.grad.detach().float().pow(2).sum()
+            total += sq if getattr(p, "_ep_spec", None) is not None else sq / self.world_size
         if self.world_size > 1:
             dist.all_reduce(total, group=self.group)
-        clip_grads_by_total_sq(flat_params, total, max_norm)
+        clip_grads_by_total_sq(flat_params + extra, total, max_norm)
         return total.sqrt().reshape(())
 
     # --- state dicts --------------------------------------------------------------------------------------
@@ -638,16 +654,51 @@ class FSDPEngine:
                 if dtype is not None:
                     t = t.to(dtype)
                 out[info.fqn] = t.cpu().clone() if cpu else t.clone()
+        for name, p in self._extras():
+            t = self._gather_ep(p) if getattr(p, "_ep_spec", None) is not None else p.detach().float()
+            if rank0_only and self.rank != 0:
+                continue
+            t = t.to(dtype) if dtype is not None else t
+            out[name] = t.cpu().clone() if cpu else t.clone()
         return out
 
     def sharded_state_dict(self) -> dict:
         """This rank's master shards: {fqn: local 1-D slice} plus layout metadata for resharding."""
-        tensors, meta = OrderedDict(), {"world_size": self.world_size, "rank": self.rank, "params": {}}
+        tensors, meta = OrderedDict(), {"world_size": self.world_size, "rank": self.rank, "params": {}, "extra": {}}
         for unit in self.units:
             for info in unit.infos:
                 tensors[info.fqn] = unit.master[info.local_lo : info.local_hi].detach().cpu().clone()
                 meta["params"][info.fqn] = {"shape": list(info.shape), "param_lo": info.param_lo, "numel": info.local_hi - info.local_lo}
+        for name, p in self._extras():
+            tensors[name] = p.detach().float().cpu().clone()
+            meta["extra"][name] = {"ep": getattr(p, "_ep_spec", None) is not None, "rank": self.rank}
         return {"tensors": tensors, "meta": meta}
+
+    # --- non-engine (ignored / expert-parallel) parameters -------------------------------------------------
+    def _extras(self):
+        for name in getattr(self, "extra_names", []):
+            yield name, self.model.get_parameter(name)
+
+    def _gather_ep(self, p):
+        group, W = p._ep_spec
+        t = p.detach().float().contiguous()
+        out = torch.empty((W * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        if dist.get_backend(group) == "gloo":
+            dist.all_gather(list(out.chunk(W)), t, group=group)
+        else:
+            dist.all_gather_into_tensor(out, t, group=group)
+        return out
+
+    @torch.no_grad()
+    def _load_extra(self, name, full):
+        p = self.model.get_parameter(name)
+        spec = getattr(p, "_ep_spec", None)
+        if spec is not None:
+            group, W = spec
+            n = full.shape[0] // W
+            r = dist.get_rank(group)
+            full = full[r * n : (r + 1) * n]
+        p.copy_(full.to(p.device, p.dtype))
 
     @torch.no_grad()
     def load_full_state_dict(self, sd: dict, strict: bool = True):
@@ -662,6 +713,11 @@ class FSDPEngine:
                 unit.master[info.local_lo : info.local_hi].copy_(piece.to(unit.master.device, torch.float32))
             if unit.shard_lp is not unit.master:
                 unit.shard_lp.copy_(unit.master)
+        for name, _ in self._extras():
+            if name in sd:
+                self._load_extra(name, sd[name])
+            else:
+                missing.append(name)
         if strict and missing:
             raise KeyError(f"Missing keys in state dict: {missing[:5]}...")
         return missing
@@ -683,6 +739,16 @@ class FSDPEngine:
                         unit.master[info.local_lo + (a - lo_need) : info.local_lo + (b - lo_need)].copy_(src.to(unit.master.device))
             if unit.shard_lp is not unit.master:
                 unit.shard_lp.copy_(unit.master)
+        for name, p in self._extras():
+            found = [(m.get("extra", {}).get(name), t) for t, m in pieces if name in m.get("extra", {})]
+            if not found:
+                continue
+            if found[0][0]["ep"]:
+                # rebuild the full expert stack from every saved rank (any EP degree), then take our slice
+                full = torch.cat([t[name] for info, t in sorted(found, key=lambda x: x[0]["rank"])], 0)
+            else:
+                full = found[0][1][name]
+            self._load_extra(name, full)
 
     @contextmanager
     def summon_full_params(self):

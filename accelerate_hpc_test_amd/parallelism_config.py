@@ -122,7 +122,15 @@ class ParallelismConfig:
     tp_handler: Optional[TorchTensorParallelConfig] = None
     cp_handler: Optional[TorchContextParallelConfig] = None
     sp_handler: Optional[DeepSpeedSequenceParallelConfig] = None
+    # Expert parallelism (MI355X extension; the reference reaches EP only through Megatron-LM). Experts are
+    # sharded over the FSDP group (dp_shard × cp × sp), so ep_size is a sub-division, not an extra mesh dim:
+    # it must be 1 or equal to that group's size.
+    ep_size: Optional[int] = None
     device_mesh: Optional[RankMesh] = field(default=None, init=False)
+
+    @property
+    def ep_enabled(self):
+        return (self.ep_size or 1) > 1
 
     def __repr__(self):
         return (
@@ -265,6 +273,11 @@ class ParallelismConfig:
             self.sp_size = int(os.environ.get(env_prefix + "SP_SIZE", "1"))
         if self.sp_backend is None:
             self.sp_backend = os.environ.get(env_prefix + "SP_BACKEND", "deepspeed")
+        if self.ep_size is None:
+            self.ep_size = int(os.environ.get(env_prefix + "EP_SIZE", "1"))
+        shard_group = self.dp_shard_size * self.cp_size * self.sp_size
+        if self.ep_size > 1 and self.ep_size != shard_group:
+            raise ValueError(f"ep_size ({self.ep_size}) must equal the FSDP shard group size dp_shard*cp*sp ({shard_group}).")
         if self.tp_size > 1 and self.tp_handler is None:
             self.tp_handler = TorchTensorParallelConfig()
         if self.cp_size > 1 and self.cp_handler is None:

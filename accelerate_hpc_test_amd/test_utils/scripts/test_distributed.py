@@ -445,6 +445,60 @@ def check_pipeline_inference(gather_output: bool = True, split="auto"):
     dist.barrier()
 
 
+def check_expert_parallel_mixtral(steps: int = 2):
+    """Mixtral with experts sharded over the FSDP group (ep = world) == one process on the global batch, incl. the
+    clipped grad norm and a sharded checkpoint round trip."""
+    from accelerate_hpc_test_amd import ParallelismConfig
+    from accelerate_hpc_test_amd.models.mixtral import MixtralConfig, MixtralForCausalLM
+
+    W = int(os.environ["WORLD_SIZE"])
+    r = int(os.environ["RANK"])
+    pc = ParallelismConfig(dp_shard_size=W, ep_size=W)
+    plugin = FullyShardedDataParallelPlugin(fsdp_version=2, auto_wrap_policy="transformer_based_wrap",
+                                            transformer_cls_names_to_wrap=["MixtralDecoderLayer"], state_dict_type="SHARDED_STATE_DICT")
+    acc = Accelerator(cpu=True, parallelism_config=pc, fsdp_plugin=plugin)
+    cfg = MixtralConfig(vocab_size=128, hidden_size=32, intermediate_size=48, num_hidden_layers=2, num_attention_heads=4,
+                        num_key_value_heads=2, head_dim=8, num_local_experts=2 * W, num_experts_per_tok=2, max_position_embeddings=64)
+    set_seed(0)
+    base = MixtralForCausalLM(cfg)
+    base.init_weights()
+    model = copy.deepcopy(base)
+    opt = torch.optim.SGD(model.parameters(), lr=0.2, momentum=0.9)
+    base_opt = torch.optim.SGD(base.parameters(), lr=0.2, momentum=0.9)
+    model, opt = acc.prepare(model, opt)
+    g = torch.Generator().manual_seed(5)
+    bs, S = 2, 8
+    for _ in range(steps):
+        ids = torch.randint(0, 128, (bs * W, S), generator=g)
+        local = ids[r * bs : (r + 1) * bs]
+        out = model(local, labels=local)
+        acc.backward(out.loss)
+        n1 = acc.clip_grad_norm_(model.parameters(), 0.5)
+        opt.step()
+        opt.zero_grad()
+        ref = base(ids, labels=ids)
+        ref.loss.backward()
+        n2 = torch.nn.utils.clip_grad_norm_(base.parameters(), 0.5)
+        base_opt.step()
+        base_opt.zero_grad()
+        assert torch.allclose(n1.reshape(()), n2, rtol=1e-4), (n1, n2)
+    full = acc.get_state_dict(model)
+    for n, q in base.state_dict().items():
+        assert full[n].shape == q.shape, (n, full[n].shape, q.shape)
+        assert torch.allclose(full[n].float(), q.float(), atol=5e-5), (n, (full[n] - q).abs().max())
+    # sharded checkpoint round trip (expert shards are saved per rank and restored)
+    d = tempfile.mkdtemp() if r == 0 else None
+    d = gather_object([d])[0]
+    acc.save_state(d)
+    with torch.no_grad():
+        for p in model.parameters():  # shard params + expert shards
+            p.add_(1.0)
+    acc.load_state(d)
+    full2 = acc.get_state_dict(model)
+    for n in full:
+        assert torch.allclose(full[n], full2[n]), n
+
+
 def main():
     check_ops()
     check_dataloader_sharding()

@@ -78,6 +78,10 @@ def test_pipeline_inference_three_stages():
     debug_launcher(td.check_pipeline_inference, args=(True, "auto"), num_processes=3)
 
 
+def test_expert_parallel_mixtral():
+    debug_launcher(td.check_expert_parallel_mixtral, num_processes=2)
+
+
 def test_local_sgd():
     debug_launcher(td.check_local_sgd, num_processes=2)
 
