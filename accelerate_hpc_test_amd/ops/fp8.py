@@ -138,6 +138,23 @@ class _Fp8LinearFn(torch.autograd.Function):
         return dx.view(ctx.shape), dw, db, None
 
 
+_FP8_ON = [True]
+
+
+class fp8_enabled:  # noqa: N801 - context manager used like a function
+    """`with fp8_enabled(False): ...` runs Fp8Linear layers as plain bf16 linears (TE `fp8_autocast(enabled=)`)."""
+
+    def __init__(self, enabled: bool = True):
+        self.enabled = enabled
+
+    def __enter__(self):
+        self.prev = _FP8_ON[0]
+        _FP8_ON[0] = self.enabled
+
+    def __exit__(self, *exc):
+        _FP8_ON[0] = self.prev
+
+
 class Fp8Linear(nn.Linear):
     """`nn.Linear` whose matmuls run in fp8 (same parameters, so FSDP / state dicts are unaffected)."""
 
@@ -148,7 +165,7 @@ class Fp8Linear(nn.Linear):
         if (
             not self.training
             and not getattr(self, "fp8_in_eval", True)
-        ) or not _gemm_ok(M, self.out_features, self.in_features) or x.dtype != torch.bfloat16:
+        ) or not _FP8_ON[0] or not _gemm_ok(M, self.out_features, self.in_features) or x.dtype != torch.bfloat16:
             return nn.functional.linear(x, self.weight.to(x.dtype), None if self.bias is None else self.bias.to(x.dtype))
         w = self.weight if self.weight.dtype == torch.bfloat16 else self.weight.to(torch.bfloat16)
         b = None if self.bias is None else self.bias.to(torch.bfloat16)

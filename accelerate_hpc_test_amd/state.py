@@ -402,10 +402,14 @@ class AcceleratorState:
         if megatron_lm_plugin is not None:
             raise NotImplementedError("Megatron-LM is not supported on MI355X.")
         if deepspeed_plugin is not None:
-            # ZeRO stages map onto our FSDP engine.
+            # ZeRO stages map onto our FSDP engine. Several named plugins may be given (reference
+            # state.py:1178-1207); the first one is active until `select_deepspeed_plugin` switches.
+            plugins = deepspeed_plugin if isinstance(deepspeed_plugin, dict) else {"default": deepspeed_plugin}
+            for i, p in enumerate(plugins.values()):
+                p.selected = i == 0
+            self.deepspeed_plugins = plugins
             if fsdp_plugin is None:
-                fsdp_plugin = deepspeed_plugin.to_fsdp_plugin()
-            self.deepspeed_plugins = None
+                fsdp_plugin = next(iter(plugins.values())).to_fsdp_plugin()
         if os.environ.get("ACCELERATE_USE_FSDP", "false").lower() == "true" or fsdp_plugin is not None:
             self.fsdp_plugin = fsdp_plugin
         else:
@@ -498,7 +502,21 @@ class AcceleratorState:
 
     @property
     def deepspeed_plugin(self):
-        return None
+        """The active DeepSpeed plugin (its ZeRO semantics run on the FSDP engine), or None."""
+        plugins = self.__dict__.get("deepspeed_plugins") or self._shared_state.get("deepspeed_plugins")
+        if not plugins:
+            return None
+        return next((p for p in plugins.values() if getattr(p, "selected", False)), None)
+
+    def get_deepspeed_plugin(self, name: str):
+        return self.deepspeed_plugins[name]
+
+    def select_deepspeed_plugin(self, name: str = None):
+        if name not in (self.deepspeed_plugins or {}):
+            raise ValueError(f"{name} is not a valid DeepSpeed plugin; choose from {list(self.deepspeed_plugins or {})}")
+        for key, p in self.deepspeed_plugins.items():
+            p.selected = key == name
+        self.fsdp_plugin = self.deepspeed_plugins[name].to_fsdp_plugin()
 
     def print(self, *args, **kwargs):
         PartialState().print(*args, **kwargs)
@@ -548,6 +566,15 @@ class GradientState:
     @property
     def initialized(self) -> bool:
         return GradientState._shared_state != {}
+
+    @property
+    def is_xla_gradients_synced(self) -> bool:
+        """XLA-only flag in the reference; there is no XLA here, so gradients are always synced by our engines."""
+        return True
+
+    @is_xla_gradients_synced.setter
+    def is_xla_gradients_synced(self, value):
+        pass
 
     @property
     def end_of_dataloader(self) -> bool:

@@ -171,6 +171,18 @@ from .other import (
     wait_for_everyone,
 )
 from .random import set_seed, synchronize_rng_state, synchronize_rng_states
+from .versions import compare_versions, is_torch_version
+from .compat_api import *  # noqa: F401,F403 - remainder of the reference's utils surface (see compat_api.py)
+from .compat_api import (  # noqa: F401 - explicit for linters / IDEs
+    SAFE_WEIGHTS_PATTERN_NAME,
+    TORCH_DISTRIBUTED_OPERATION_TYPES,
+    WEIGHTS_PATTERN_NAME,
+    DummyOptim,
+    DummyScheduler,
+    check_cuda_fp8_capability,
+    fsdp2_prepare_model,
+    gather_across_data_parallel_groups,
+)
 
 
 def __getattr__(name):
@@ -203,10 +215,15 @@ def __getattr__(name):
         from ..commands.config.default import write_basic_config
 
         return write_basic_config
-    if name in ("PrepareForLaunch", "prepare_multi_gpu_env", "prepare_simple_launcher_cmd_env", "get_launch_prefix"):
+    if name in ("PrepareForLaunch", "prepare_multi_gpu_env", "prepare_simple_launcher_cmd_env", "get_launch_prefix",
+                "prepare_deepspeed_cmd_env", "_filter_args", "setup_fp8_env", "_convert_nargs_to_dict", "env_var_path_add"):
         from . import launch
 
         return getattr(launch, name)
+    if name == "ParallelismConfig":
+        from ..parallelism_config import ParallelismConfig
+
+        return ParallelismConfig
     if name == "tqdm":
         from .tqdm import tqdm
 
