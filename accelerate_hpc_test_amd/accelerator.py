@@ -564,34 +564,41 @@ class Accelerator:
 
     @contextlib.contextmanager
     def join_uneven_inputs(self, joinables, even_batches=None):
-        """Uneven inputs: with our DataLoaderShard, `even_batches=True` already equalises the number of batches.
-        This context temporarily overrides `even_batches` on prepared loaders, as the reference does."""
+        """Train on uneven per-rank inputs (reference accelerator.py:1298-1379): optionally override `even_batches`
+        on the prepared loaders and enter each DDP joinable's `join()` — ranks that finish early shadow the
+        others' gradient all-reduces with zeros until everyone is done (parallel/ddp.py)."""
         if self.distributed_type in (DistributedType.MULTI_GPU, DistributedType.MULTI_CPU):
-            iterable_dl_seen = False
-            dl_even_batches_values = []
-            if even_batches is not None:
-                self.even_batches = even_batches
-                for dl_idx, dl in enumerate(self._dataloaders):
-                    if isinstance(dl, DataLoaderDispatcher):
-                        iterable_dl_seen = True
-                        continue
-                    bs = getattr(dl, "batch_sampler", None)
-                    if bs is not None and hasattr(bs, "even_batches"):
-                        dl_even_batches_values.append((dl_idx, bs.even_batches))
-                        bs.even_batches = even_batches
-                if iterable_dl_seen:
-                    warnings.warn("Overriding even_batches is only supported for map-style datasets, yet some dataloaders given were iterable")
-            else:
-                even_batches = self.even_batches
-            try:
-                yield
-            finally:
-                for dl_idx, even_batches_value in dl_even_batches_values:
-                    self._dataloaders[dl_idx].batch_sampler.even_batches = even_batches_value
+            with contextlib.ExitStack() as stack:
+                for j in joinables:
+                    if hasattr(j, "join") and hasattr(j, "buckets"):
+                        stack.enter_context(j.join())
+                with self._override_even_batches(even_batches):
+                    yield
         else:
             if self.distributed_type != DistributedType.NO:
                 warnings.warn("Joining uneven inputs is only supported for multi-GPU training, as a result `join_uneven_inputs` will have no effect.")
             yield
+
+    @contextlib.contextmanager
+    def _override_even_batches(self, even_batches):
+        saved = []
+        if even_batches is not None:
+            iterable_seen = False
+            for dl in self._dataloaders:
+                if isinstance(dl, DataLoaderDispatcher):
+                    iterable_seen = True
+                    continue
+                bs = getattr(dl, "batch_sampler", None)
+                if bs is not None and hasattr(bs, "even_batches"):
+                    saved.append((bs, bs.even_batches))
+                    bs.even_batches = even_batches
+            if iterable_seen:
+                warnings.warn("Overriding even_batches is only supported for map-style datasets, yet some dataloaders given were iterable")
+        try:
+            yield
+        finally:
+            for bs, value in saved:
+                bs.even_batches = value
 
     # ============================================================================== prepare
     def _prepare_one(self, obj, first_pass=False, device_placement=None):
@@ -734,6 +741,7 @@ class Accelerator:
                         find_unused_parameters=kwargs.get("find_unused_parameters", False),
                         comm_hook=comm_hook,
                         comm_wrapper=comm_wrapper,
+                        comm_state_option=self.ddp_handler.comm_state_option if self.ddp_handler is not None else None,
                     )
                     self._models[-1] = model
             elif self.distributed_type == DistributedType.FSDP:

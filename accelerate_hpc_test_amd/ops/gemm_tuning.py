@@ -49,5 +49,5 @@ def start_gemm_tuning(out_path: str, max_duration_ms: int = 30, max_iterations: 
 def finish_gemm_tuning() -> None:
     import torch.cuda.tunable as tunable
 
-    tunable.write_file()
+    # results are persisted by TunableOp itself (as they are found and at exit); stop searching new shapes
     tunable.tuning_enable(False)

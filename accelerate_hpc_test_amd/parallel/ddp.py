@@ -62,10 +62,14 @@ class DistributedDataParallel(nn.Module):
         comm_hook: DDPCommunicationHookType = DDPCommunicationHookType.NO,
         comm_wrapper: DDPCommunicationHookType = DDPCommunicationHookType.NO,
         bucket_bytes: Optional[int] = None,
+        comm_state_option: Optional[dict] = None,
         **unused,
     ):
         super().__init__()
         self.module = module
+        self.comm_state_option = dict(comm_state_option or {})
+        self._psgd: dict = {}
+        self._join = None
         self.process_group = process_group
         self.world_size = dist.get_world_size(process_group)
         self.rank = dist.get_rank(process_group)
@@ -145,7 +149,15 @@ class DistributedDataParallel(nn.Module):
         # After `zero_grad(set_to_none=True)` the grads are None: re-point them at the (zeroed) buckets.
         if any(p.grad is None for b in self.buckets for p in b.params):
             self._assign_grad_views(zero=True)
-        if self.broadcast_buffers and self.world_size > 1:
+        join = getattr(self, "_join", None)
+        if join is not None:
+            syncing = int(self.require_backward_grad_sync and torch.is_grad_enabled())
+            join["active"], _ = self._join_counter(1, syncing)
+            join["steps"] += 1
+            if join["active"] < self.world_size and join["throw"]:
+                raise RuntimeError("DDP join: another rank ran out of inputs (throw_on_early_termination=True)")
+        uneven = join is not None and join["active"] < self.world_size
+        if self.broadcast_buffers and self.world_size > 1 and not uneven:
             bufs = [b for b in self.module.buffers()]
             if bufs:
                 with torch.no_grad():
@@ -167,7 +179,9 @@ class DistributedDataParallel(nn.Module):
             self._cb_queued = True
             torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
         b.pending -= 1
-        if b.pending == 0 and self.require_backward_grad_sync:
+        join = getattr(self, "_join", None)
+        deferred = join is not None and join["active"] < self.world_size  # joined ranks shadow in bucket order
+        if b.pending == 0 and self.require_backward_grad_sync and not deferred:
             self._launch(b)
 
     def _slot(self, b, p):
@@ -190,8 +204,16 @@ class DistributedDataParallel(nn.Module):
             self._allreduce(b)
 
     def _allreduce(self, b):
+        self._allreduce_buffer(b.buffer, key=self.buckets.index(b))
+        join = getattr(self, "_join", None)
+        if join is not None and not join["divide_initial"] and join["active"] < self.world_size:
+            b.buffer.mul_(self.world_size / join["active"])  # average over the ranks still training
+
+    def _allreduce_buffer(self, buf, key: int = 0):
         W = self.world_size
-        buf = b.buffer
+        if self.comm_hook in (DDPCommunicationHookType.POWER_SGD, DDPCommunicationHookType.BATCHED_POWER_SGD) and buf.dtype.is_floating_point:
+            self._powersgd(buf, key)
+            return
         if self.comm_hook in (DDPCommunicationHookType.BF16, DDPCommunicationHookType.FP16) and buf.dtype == torch.float32:
             dt = torch.bfloat16 if self.comm_hook == DDPCommunicationHookType.BF16 else torch.float16
             tmp = buf.to(dt).div_(W)
@@ -203,6 +225,55 @@ class DistributedDataParallel(nn.Module):
             buf.div_(W)
         else:
             dist.all_reduce(buf, op=dist.ReduceOp.AVG, group=self.process_group)
+
+    @torch.no_grad()
+    def _powersgd(self, buf, key: int):
+        """PowerSGD (Vogels et al. 2019), as torch's `powerSGD_hook` used by the reference via
+        `DDPCommunicationHookType.POWER_SGD` (dataclasses.py:134-151,197-237): the bucket is viewed as an [n, m]
+        matrix M (+ error feedback); P = M·Q is all-reduced and orthonormalised, Q = Mᵀ·P all-reduced, and
+        P·Qᵀ/W replaces the bucket. Two small all-reduces instead of one bucket-sized one. Vanilla all-reduce for
+        the first `start_powerSGD_iter` iterations and for buckets whose compression rate is too low."""
+        opt = self.comm_state_option
+        r = int(opt.get("matrix_approximation_rank", 1))
+        start_iter = int(opt.get("start_powerSGD_iter", 1000))
+        min_rate = float(opt.get("min_compression_rate", 2.0))
+        W = self.world_size
+        st = self._psgd.setdefault(key, {"iter": 0})
+        st["iter"] += 1
+        n_el = buf.numel()
+        m = max(1, int(n_el ** 0.5))
+        n = -(-n_el // m)
+        compressible = (n * m) / max(1, r * (n + m)) >= min_rate
+        if st["iter"] <= start_iter or not compressible:
+            if self.is_gloo:
+                dist.all_reduce(buf, group=self.process_group)
+                buf.div_(W)
+            else:
+                dist.all_reduce(buf, op=dist.ReduceOp.AVG, group=self.process_group)
+            return
+        M = torch.zeros(n * m, dtype=torch.float32, device=buf.device)
+        M[:n_el] = buf.float()
+        M = M.view(n, m)
+        if opt.get("use_error_feedback", True):
+            err = st.get("err")
+            if err is None:
+                err = st["err"] = torch.zeros_like(M)
+            M += err
+        Q = st.get("Q")
+        if Q is None or not opt.get("warm_start", True):
+            g = torch.Generator(device="cpu").manual_seed(int(opt.get("random_seed", 0)) + key)
+            Q = torch.randn(m, r, generator=g).to(buf.device)
+        P = M @ Q
+        dist.all_reduce(P, group=self.process_group)
+        P, _ = torch.linalg.qr(P)
+        Q = M.t() @ P
+        dist.all_reduce(Q, group=self.process_group)
+        Q.div_(W)
+        approx = P @ Q.t()
+        if opt.get("use_error_feedback", True):
+            st["err"] = M - approx  # note: M is this rank's (grad + error), approx is the global average
+        st["Q"] = Q
+        buf.copy_(approx.view(-1)[:n_el].to(buf.dtype))
 
     def _finalize(self):
         self._cb_queued = False
@@ -227,12 +298,72 @@ class DistributedDataParallel(nn.Module):
         self.comm_hook = DDPCommunicationHookType(hook)
         if wrapper not in (None, DDPCommunicationHookType.NO):
             self.comm_hook = DDPCommunicationHookType(wrapper)
+        if isinstance(state, dict):
+            self.comm_state_option.update(state)
 
     @contextmanager
     def join(self, divide_by_initial_world_size: bool = True, enable: bool = True, throw_on_early_termination: bool = False):
-        """Uneven-input support. Our DataLoaderShard already equalises batch counts (`even_batches=True`), so the
-        context only validates usage; with `even_batches=False` callers must stop at the shortest rank."""
-        yield
+        """Uneven inputs (torch `Join` semantics, reference accelerator.py:1298-1379).
+
+        Inside the context every forward all-reduces a tiny [active, syncing] counter. A rank whose data ran out
+        leaves the loop and, in `__exit__`, *shadows* the other ranks: for each of their iterations it joins the
+        counter all-reduce and, if they sync, all-reduces zero-filled buckets in bucket order (active ranks launch
+        their buckets in that same order at the end of backward while joined ranks exist). Gradients are divided
+        by the initial world size (joined ranks contribute zeros) or, with `divide_by_initial_world_size=False`,
+        by the number of ranks still active. `throw_on_early_termination` raises on active ranks instead."""
+        if not enable or self.world_size == 1:
+            yield
+            return
+        self._join = {"divide_initial": divide_by_initial_world_size, "throw": throw_on_early_termination,
+                      "active": self.world_size, "steps": 0}
+        try:
+            yield
+        finally:
+            try:
+                self._shadow_until_all_joined()
+                self._sync_from_last_joiner()
+            finally:
+                self._join = None
+
+    @torch.no_grad()
+    def _sync_from_last_joiner(self):
+        """Ranks that joined early stopped stepping their optimizer: re-broadcast parameters and buffers from the
+        rank that trained the longest (torch Join's `is_last_joiner` sync)."""
+        t = torch.tensor([self._join["steps"] * self.world_size + (self.world_size - 1 - self.rank)], dtype=torch.int64,
+                         device=self.device if not self.is_gloo else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.process_group)
+        src = self.world_size - 1 - int(t.item()) % self.world_size
+        tensors = [p.data for p in self.module.parameters()] + list(self.module.buffers())
+        by_dtype = {}
+        for x in tensors:
+            by_dtype.setdefault(x.dtype, []).append(x)
+        for ts in by_dtype.values():
+            flat = torch.cat([x.reshape(-1) for x in ts])
+            dist.broadcast(flat, src=dist.get_global_rank(self.process_group, src) if self.process_group else src, group=self.process_group)
+            off = 0
+            for x in ts:
+                x.copy_(flat[off : off + x.numel()].view_as(x))
+                off += x.numel()
+
+    def _join_counter(self, active: int, syncing: int) -> tuple[int, int]:
+        t = torch.tensor([active, syncing], dtype=torch.int64, device=self.device if not self.is_gloo else "cpu")
+        dist.all_reduce(t, group=self.process_group)
+        a, s = t.tolist()
+        return a, s
+
+    @torch.no_grad()
+    def _shadow_until_all_joined(self):
+        while True:
+            active, syncing = self._join_counter(0, 0)
+            if active == 0:
+                return
+            if self._join["throw"]:
+                raise RuntimeError("DDP join: this rank ran out of inputs while others are still training")
+            if syncing:
+                for i, b in enumerate(self.buckets):  # same collectives, same order, same op as the active ranks
+                    self._allreduce_buffer(torch.zeros_like(b.buffer), key=i)
+                if self.is_cuda:
+                    torch.cuda.current_stream(self.device).synchronize()
 
     def state_dict(self, *args, **kwargs):
         return self.module.state_dict(*args, **kwargs)

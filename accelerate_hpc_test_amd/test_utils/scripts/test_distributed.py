@@ -499,6 +499,63 @@ def check_expert_parallel_mixtral(steps: int = 2):
         assert torch.allclose(full[n], full2[n]), n
 
 
+def check_join_uneven_inputs():
+    """Rank r gets 2 + r batches; with `join_uneven_inputs` the short rank shadows the long rank's all-reduces.
+    Oracle: grads of each step = sum over active ranks / W (divide_by_initial_world_size)."""
+    acc = Accelerator(cpu=True)
+    W, r = acc.num_processes, acc.process_index
+    set_seed(0)
+    base = TinyMLP()
+    model = copy.deepcopy(base)
+    opt = torch.optim.SGD(model.parameters(), lr=0.1)
+    base_opt = torch.optim.SGD(base.parameters(), lr=0.1)
+    model, opt = acc.prepare(model, opt)
+    bs = 4
+    n_steps = [2 + j for j in range(W)]
+    data = {j: _global_batches(n_steps[j], bs, 1, seed=10 + j) for j in range(W)}
+    with acc.join_uneven_inputs([model]):
+        for x, y in data[r]:
+            acc.backward(F.mse_loss(model(x), y))
+            opt.step()
+            opt.zero_grad()
+    # oracle
+    for step in range(max(n_steps)):
+        active = [j for j in range(W) if step < n_steps[j]]
+        for j in active:
+            x, y = data[j][step]
+            (F.mse_loss(base(x), y) / W).backward()
+        base_opt.step()
+        base_opt.zero_grad()
+    inner = acc.unwrap_model(model)
+    for (n, p), q in zip(inner.named_parameters(), base.parameters()):
+        assert torch.allclose(p, q, atol=1e-5), (n, (p - q).abs().max())
+
+
+def check_ddp_powersgd():
+    """PowerSGD hook: with start_powerSGD_iter=0 training still converges and ranks stay in sync."""
+    from accelerate_hpc_test_amd.utils import DDPCommunicationHookType, DistributedDataParallelKwargs
+
+    kw = DistributedDataParallelKwargs(comm_hook=DDPCommunicationHookType.POWER_SGD,
+                                       comm_state_option={"start_powerSGD_iter": 0, "matrix_approximation_rank": 2, "min_compression_rate": 0.0})
+    acc = Accelerator(cpu=True, kwargs_handlers=[kw])
+    W, r = acc.num_processes, acc.process_index
+    set_seed(0)
+    model = TinyMLP()
+    opt = torch.optim.SGD(model.parameters(), lr=0.05)
+    model, opt = acc.prepare(model, opt)
+    losses = []
+    for x, y in _global_batches(30, 8, W, seed=3):
+        loss = F.mse_loss(model(x[r * 8 : (r + 1) * 8]), y[r * 8 : (r + 1) * 8])
+        acc.backward(loss)
+        opt.step()
+        opt.zero_grad()
+        losses.append(acc.reduce(loss.detach().reshape(1), "mean").item())
+    assert sum(losses[-5:]) < sum(losses[:5]), losses
+    flat = torch.cat([p.detach().reshape(-1) for p in acc.unwrap_model(model).parameters()])
+    g = gather(flat.unsqueeze(0))
+    assert torch.allclose(g[0], g[-1], atol=1e-6)
+
+
 def main():
     check_ops()
     check_dataloader_sharding()

@@ -82,6 +82,15 @@ def test_expert_parallel_mixtral():
     debug_launcher(td.check_expert_parallel_mixtral, num_processes=2)
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_ddp_join_uneven_inputs(world):
+    debug_launcher(td.check_join_uneven_inputs, num_processes=world)
+
+
+def test_ddp_powersgd_hook():
+    debug_launcher(td.check_ddp_powersgd, num_processes=2)
+
+
 def test_local_sgd():
     debug_launcher(td.check_local_sgd, num_processes=2)
 

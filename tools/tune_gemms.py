@@ -60,12 +60,10 @@ def main():
         y = lin(x)
         y.backward(torch.randn_like(y))
         torch.cuda.synchronize()
-        tunable.write_file()
         print(f"tuned linear out={out_f} in={in_f}: {time.time() - t0:.1f}s ({len(tunable.get_results())} results)", flush=True)
         del lin, x, y
         torch.cuda.empty_cache()
-    tunable.write_file()
-    print("done", flush=True)
+    print("done", flush=True)  # TunableOp persists each result to the file as it is tuned (and at exit)
 
 
 if __name__ == "__main__":
