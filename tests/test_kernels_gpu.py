@@ -186,15 +186,45 @@ def test_fp8_cast_amax_gemm():
     assert _rel(out, ref) < 6e-2, _rel(out, ref)
 
 
-def test_fp8_gemm_exact_small_integers():
-    """Operands that are exact in e4m3 (small integers) must give the exact product: pins the MFMA operand layout."""
+@pytest.mark.parametrize("M,N,K", [(128, 128, 128), (256, 256, 128), (512, 768, 1024), (768, 256, 384)])
+def test_fp8_gemm_exact_small_integers(M, N, K):
+    """Operands that are exact in e4m3 (small integers) must give the exact product: pins the MFMA operand layout
+    and the LDS swizzle of both GEMM kernels (128² v1, and the 256² glds v2 for multiples of 256/256/128)."""
     from accelerate_hpc_test_amd.ops import fp8
 
     torch.manual_seed(0)
-    M, N, K = 128, 128, 128
     a = torch.randint(-3, 4, (M, K), device=DEV).to(torch.bfloat16)
     b = torch.randint(-3, 4, (N, K), device=DEV).to(torch.bfloat16)
     one = torch.ones(1, device=DEV)
     out = fp8.gemm(fp8.cast(a, one), fp8.cast(b, one), one, one, out_dtype=torch.float32)
     ref = a.float() @ b.float().t()
     assert torch.equal(out, ref), (out - ref).abs().max()
+
+
+def test_fp8_gemm_v2_matches_v1_random():
+    """Random operands, mixed e4m3/e5m2 formats, scales and bias: the 256² glds kernel == the 128² kernel."""
+    import subprocess
+    import sys
+
+    code = (
+        "import torch, os\n"
+        "from accelerate_hpc_test_amd.ops import fp8\n"
+        "torch.manual_seed(1)\n"
+        "a=torch.randn(512,1024,device='cuda',dtype=torch.bfloat16); b=torch.randn(768,1024,device='cuda',dtype=torch.bfloat16)\n"
+        "sa=torch.tensor([2.0],device='cuda'); sb=torch.tensor([0.5],device='cuda'); bias=torch.randn(768,device='cuda',dtype=torch.bfloat16)\n"
+        "a8=fp8.cast(a,sa); b8=fp8.cast(b,sb,e5m2=True)\n"
+        "o=fp8.gemm(a8,b8,1/sa,1/sb,bias,torch.float32)\n"
+        "torch.save(o.cpu(), os.environ['OUT'])\n"
+    )
+    import os
+    import tempfile
+
+    outs = []
+    for v1 in (False, True):
+        f = tempfile.mktemp(suffix=".pt")
+        env = dict(os.environ, OUT=f)
+        if v1:
+            env["ACCELERATE_FP8_GEMM_V1"] = "1"
+        subprocess.run([sys.executable, "-c", code], check=True, env=env, timeout=300)
+        outs.append(torch.load(f, weights_only=True))
+    assert torch.allclose(outs[0], outs[1], rtol=1e-5, atol=1e-3), (outs[0] - outs[1]).abs().max()
