@@ -63,8 +63,28 @@ def main():
         print(f"tuned linear out={out_f} in={in_f}: {time.time() - t0:.1f}s ({len(tunable.get_results())} results)", flush=True)
         del lin, x, y
         torch.cuda.empty_cache()
-    print("done", flush=True)  # TunableOp persists each result to the file as it is tuned (and at exit)
+    # NOTE: TunableOp persists only the results found in THIS process (also at exit, from C++); fold the seed table
+    # back in afterwards, from another process: `python tools/tune_gemms.py --merge OUT SEED`.
+    print("done", flush=True)
+
+
+def merge_tables(out_path, *others):
+    lines = []
+    for p in (out_path,) + others:
+        if os.path.isfile(p):
+            lines += open(p).read().splitlines()
+    seen, out = set(), []
+    for ln in lines:
+        key = ",".join(ln.split(",")[:2])
+        if ln.strip() and key not in seen:
+            seen.add(key)
+            out.append(ln)
+    open(out_path, "w").write("\n".join(out) + "\n")
+    print(f"merged -> {out_path}: {sum(1 for l in out if not l.startswith('Validator'))} GEMM entries")
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 2 and sys.argv[1] == "--merge":
+        merge_tables(*sys.argv[2:])
+    else:
+        main()
