@@ -200,96 +200,131 @@ __global__ __launch_bounds__(256, 2) void fp8_gemm_kernel(const uint8_t* __restr
 }
 
 // ------------------------------------------------------------------------------------------------ GEMM v2
-// 256x256 output tile, BK = 128 fp8 bytes per K-step, 8 waves (2 along M x 4 along N, 128x64 per wave),
-// MX-scaled 32x32x64 MFMA (2x the bf16 MFMA rate). Operands are staged HBM/L2 -> LDS with
-// global_load_lds_dwordx4 (no VGPR round trip, no ds_write): one wave-instruction fills 1 KiB = 8 rows x 128 B of
-// the LDS image. The image is XOR-swizzled per 16-B chunk, chunk' = chunk ^ ((row >> 1) & 7), which makes every
-// ds_read_b128 lane group of a 32x32x64 fragment read hit 16 distinct 16-B slots of the 256-B bank row
-// (conflict-free); because a DMA writes lane-linearly, the swizzle is applied to each lane's *global source*
-// address instead. Two LDS stages (2 x 64 KiB): the next K-step's DMA is in flight while the current one runs
-// its 16 MFMAs per wave; one vmcnt(0) + barrier per K-step.
+// 256x256 output tile, BK = 128 fp8 bytes per K-step, MX-scaled 32x32x64 MFMA (2x the bf16 MFMA rate).
+// Wave grid WM x WN (default 2 x 2 = 4 waves, one per SIMD, 128x128 outputs per wave: 256 accumulator registers
+// in AGPRs, which only the full 512-entry register file of a one-wave-per-SIMD workgroup holds without spills).
+// Operands are staged HBM/L2 -> LDS with global_load_lds_dwordx4 (no VGPR round trip, no ds_write): one
+// wave-instruction fills 1 KiB = 8 rows x 128 B of the LDS image. The image is XOR-swizzled per 16-B chunk,
+// chunk' = chunk ^ ((row >> 1) & 7), which makes every ds_read_b128 lane group of a 32x32x64 fragment read hit
+// 16 distinct 16-B slots of the 256-B bank row (conflict-free); because a DMA writes lane-linearly, the swizzle
+// is applied to each lane's *global source* address instead. Two LDS stages (2 x 64 KiB): the next K-step's
+// DMA is in flight while the current one runs its MFMAs; one vmcnt(0) + barrier per K-step.
 constexpr int V2_BM = 256, V2_BN = 256, V2_BK = 128;
 constexpr int V2_STAGE = (V2_BM + V2_BN) * V2_BK;  // bytes per stage (A image then B image)
 
 __device__ __forceinline__ int v2_swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
-template <int FA, int FB, bool OUT_F32>
-__global__ __launch_bounds__(512, 1) void fp8_gemm_v2_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
-                                                             const float* __restrict__ sa, const float* __restrict__ sb,
-                                                             const bf16_t* __restrict__ bias, void* __restrict__ C, int M,
-                                                             int N, int K) {
-  extern __shared__ __attribute__((aligned(1024))) uint8_t smem[];  // [2 stages][A 256x128 | B 256x128]
+template <int FA, int FB, bool OUT_F32, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN, 1) void fp8_gemm_v2_kernel(const uint8_t* __restrict__ A,
+                                                                       const uint8_t* __restrict__ B,
+                                                                       const float* __restrict__ sa,
+                                                                       const float* __restrict__ sb,
+                                                                       const bf16_t* __restrict__ bias,
+                                                                       void* __restrict__ C, int M, int N, int K) {
+  constexpr int NW = WM * WN;
+  constexpr int TI = V2_BM / WM / 32, TJ = V2_BN / WN / 32;  // 32x32 MFMA tiles per wave along M / N
+  constexpr int DPW = 32 / NW;                                 // 1-KiB DMA blocks per wave per operand
+  // One static LDS object PER STAGE, each used with a compile-time identity (the K loop is unrolled by two):
+  // the AMDGPU LDS lowering gives distinct objects distinct alias scopes, so hipcc can see that the DMA filling
+  // one stage never feeds the ds_reads of the other and does not drain it (vmcnt(0)) before every K-step — which
+  // it does for a single array indexed by a run-time stage number (checked in the .s).
+  __shared__ __attribute__((aligned(1024))) uint8_t stage0[V2_STAGE];  // A 256x128 | B 256x128
+  __shared__ __attribute__((aligned(1024))) uint8_t stage1[V2_STAGE];
   const int tiles_n = N / V2_BN;
   const int nwg = (M / V2_BM) * tiles_n;
   const int bid = xcd_remap(blockIdx.x, nwg);
   const int tm = (bid / tiles_n) * V2_BM, tn = (bid % tiles_n) * V2_BN;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hf = lane >> 5;
-  const int wm = (wave >> 2) * 128, wn = (wave & 3) * 64;
+  const int wm = (wave / WN) * (V2_BM / WM), wn = (wave % WN) * (V2_BN / WN);
 
-  f32x16 acc[4][2];
+  f32x16 acc[TI][TJ];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < TI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < TJ; ++j)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-  // DMA assignment: each operand image is 256 rows = 32 blocks of 8 rows (1 KiB); 8 waves x 4 instructions.
+  // DMA assignment: each operand image is 256 rows = 32 blocks of 8 rows (1 KiB), DPW blocks per wave.
   // Lane l of an instruction covering rows [8b, 8b+8) writes LDS byte 16*l of that block, i.e. row 8b + l/8,
   // physical chunk l%8, which must hold logical chunk (l%8) ^ ((row>>1)&7).
+  // Sources = wave-uniform tile base (SGPRs) + a 32-bit per-lane offset, identical for A and B (same K).
   const int lrow = lane >> 3, lpch = lane & 7;
-  auto stage = [&](int k0, int buf) {
-    uint8_t* base = smem + buf * V2_STAGE;
+  int voff[DPW];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int blk = wave * 4 + t;  // 0..31
-      const int row = blk * 8 + lrow;
-      const int lch = v2_swz(row, lpch);
-      __builtin_amdgcn_global_load_lds(A + (long)(tm + row) * K + k0 + lch * 16, base + blk * 1024, 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(B + (long)(tn + row) * K + k0 + lch * 16, base + V2_BM * V2_BK + blk * 1024, 16, 0, 0);
+  for (int t = 0; t < DPW; ++t) {
+    const int row = (wave * DPW + t) * 8 + lrow;
+    voff[t] = row * K + v2_swz(row, lpch) * 16;
+  }
+  const uint8_t* const a_tile = A + (long)tm * K;
+  const uint8_t* const b_tile = B + (long)tn * K;
+  auto stage = [&](int k0, uint8_t* base) {
+    const uint8_t* a0 = a_tile + k0;
+    const uint8_t* b0 = b_tile + k0;
+#pragma unroll
+    for (int t = 0; t < DPW; ++t) {
+      const int blk = wave * DPW + t;  // 0..31
+      __builtin_amdgcn_global_load_lds(a0 + voff[t], base + blk * 1024, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(b0 + voff[t], base + V2_BM * V2_BK + blk * 1024, 16, 0, 0);
     }
   };
-  auto frag = [&](const uint8_t* img, int row, int ks) -> v8i {
-    const uint8_t* rp = img + row * V2_BK;
-    const int c0 = ks * 4 + 2 * hf;  // 32 k-bytes per lane half: chunks c0, c0+1
-    const uint4 lo = *reinterpret_cast<const uint4*>(rp + v2_swz(row, c0) * 16);
-    const uint4 hi = *reinterpret_cast<const uint4*>(rp + v2_swz(row, c0 + 1) * 16);
+  // Fragment rows are wm + 32 i + r (A) / wn + 32 j + r (B): the swizzle term (row >> 1) & 7 is (r >> 1) & 7 for
+  // all of them, so each (ks, half) chunk has ONE per-lane offset and the fragment index is an immediate.
+  const int sw = (r >> 1) & 7;
+  int loff[2][2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int p = 0; p < 2; ++p) loff[ks][p] = ((ks * 4 + 2 * hf + p) ^ sw) * 16;
+  const int arow = (wm + r) * V2_BK, brow = V2_BM * V2_BK + (wn + r) * V2_BK;
+  auto frag = [&](const uint8_t* img, int rowoff, int idx, int ks) -> v8i {
+    const uint8_t* rp = img + rowoff + idx * 32 * V2_BK;
+    const uint4 lo = *reinterpret_cast<const uint4*>(rp + loff[ks][0]);
+    const uint4 hi = *reinterpret_cast<const uint4*>(rp + loff[ks][1]);
     v8i v;
     v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w; v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
     return v;
   };
 
-  const int nk = K / V2_BK;
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) stage((kt + 1) * V2_BK, cur ^ 1);  // DMA of the next K-step overlaps this one's MFMAs
-    const uint8_t* imgA = smem + cur * V2_STAGE;
-    const uint8_t* imgB = imgA + V2_BM * V2_BK;
+  auto compute = [&](const uint8_t* img) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      v8i af[4], bfr[2];
+      v8i af[TI], bfr[TJ];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bfr[j] = frag(imgB, wn + j * 32 + r, ks);
+      for (int j = 0; j < TJ; ++j) bfr[j] = frag(img, brow, j, ks);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = frag(imgA, wm + i * 32 + r, ks);
+      for (int i = 0; i < TI; ++i) af[i] = frag(img, arow, i, ks);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)  // swapped operands: acc holds the C^T tile (lane <-> m, registers <-> n)
+        for (int j = 0; j < TJ; ++j)  // swapped operands: acc holds the C^T tile (lane <-> m, registers <-> n)
           acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(bfr[j], af[i], acc[i][j], FB, FA, 0, 0x7f7f7f7f, 0,
                                                                       0x7f7f7f7f);
     }
+  };
+  auto retire = [&]() {  // this stage's DMA landed for every wave; every wave finished reading the other stage
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+  };
+
+  const int nk = K / V2_BK;
+  stage(0, stage0);
+  retire();
+  int kt = 0;
+  for (; kt + 2 <= nk; kt += 2) {
+    stage((kt + 1) * V2_BK, stage1);  // DMA of K-step kt+1 overlaps the MFMAs of kt
+    compute(stage0);
+    retire();
+    if (kt + 2 < nk) stage((kt + 2) * V2_BK, stage0);
+    compute(stage1);
+    retire();
   }
+  if (kt < nk) compute(stage0);  // odd number of K-steps: the last one was staged into stage0
   const float s = sa[0] * sb[0];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < TI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < TJ; ++j) {
       const int m = tm + wm + i * 32 + r;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -310,11 +345,6 @@ __global__ __launch_bounds__(512, 1) void fp8_gemm_v2_kernel(const uint8_t* __re
         }
       }
     }
-}
-
-template <typename KernelT>
-void v2_allow_smem(KernelT kernel) {
-  hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize, 2 * V2_STAGE);
 }
 
 }  // namespace
@@ -385,17 +415,9 @@ torch::Tensor fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor a_scale_i
   void* cp = out.data_ptr();
   static const bool force_v1 = std::getenv("ACCELERATE_FP8_GEMM_V1") != nullptr;
   if (!force_v1 && M % V2_BM == 0 && N % V2_BN == 0 && K % V2_BK == 0) {
-    static bool attrs = false;
-    if (!attrs) {
-      v2_allow_smem(fp8_gemm_v2_kernel<0, 0, false>); v2_allow_smem(fp8_gemm_v2_kernel<0, 0, true>);
-      v2_allow_smem(fp8_gemm_v2_kernel<0, 1, false>); v2_allow_smem(fp8_gemm_v2_kernel<0, 1, true>);
-      v2_allow_smem(fp8_gemm_v2_kernel<1, 0, false>); v2_allow_smem(fp8_gemm_v2_kernel<1, 0, true>);
-      v2_allow_smem(fp8_gemm_v2_kernel<1, 1, false>); v2_allow_smem(fp8_gemm_v2_kernel<1, 1, true>);
-      attrs = true;
-    }
     const int nwg2 = (M / V2_BM) * (N / V2_BN);
 #define GEMM2_LAUNCH(FA, FB, OF) \
-  hipLaunchKernelGGL((fp8_gemm_v2_kernel<FA, FB, OF>), dim3(nwg2), dim3(512), 2 * V2_STAGE, stream, ap, bptr, sap, sbp, bp, cp, M, N, K)
+  hipLaunchKernelGGL((fp8_gemm_v2_kernel<FA, FB, OF, 2, 2>), dim3(nwg2), dim3(256), 0, stream, ap, bptr, sap, sbp, bp, cp, M, N, K)
     if (!a_e5m2 && !b_e5m2) { if (out_fp32) GEMM2_LAUNCH(0, 0, true); else GEMM2_LAUNCH(0, 0, false); }
     else if (!a_e5m2 && b_e5m2) { if (out_fp32) GEMM2_LAUNCH(0, 1, true); else GEMM2_LAUNCH(0, 1, false); }
     else if (a_e5m2 && !b_e5m2) { if (out_fp32) GEMM2_LAUNCH(1, 0, true); else GEMM2_LAUNCH(1, 0, false); }
