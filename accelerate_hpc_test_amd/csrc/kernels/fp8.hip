@@ -213,13 +213,16 @@ constexpr int V2_STAGE = (V2_BM + V2_BN) * V2_BK;  // bytes per stage (A image t
 
 __device__ __forceinline__ int v2_swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
-template <int FA, int FB, bool OUT_F32, int WM, int WN>
-__global__ __launch_bounds__(64 * WM * WN, 1) void fp8_gemm_v2_kernel(const uint8_t* __restrict__ A,
+constexpr int V2_WM = 2, V2_WN = 2;  // wave grid (a template-dependent __launch_bounds__ leaves the host stub undefined)
+
+template <int FA, int FB, bool OUT_F32>
+__global__ __launch_bounds__(64 * V2_WM * V2_WN, 1) void fp8_gemm_v2_kernel(const uint8_t* __restrict__ A,
                                                                        const uint8_t* __restrict__ B,
                                                                        const float* __restrict__ sa,
                                                                        const float* __restrict__ sb,
                                                                        const bf16_t* __restrict__ bias,
                                                                        void* __restrict__ C, int M, int N, int K) {
+  constexpr int WM = V2_WM, WN = V2_WN;
   constexpr int NW = WM * WN;
   constexpr int TI = V2_BM / WM / 32, TJ = V2_BN / WN / 32;  // 32x32 MFMA tiles per wave along M / N
   constexpr int DPW = 32 / NW;                                 // 1-KiB DMA blocks per wave per operand
@@ -416,7 +419,7 @@ torch::Tensor fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor a_scale_i
   if (!force_v1 && M % V2_BM == 0 && N % V2_BN == 0 && K % V2_BK == 0) {
     const int nwg2 = (M / V2_BM) * (N / V2_BN);
 #define GEMM2_LAUNCH(FA, FB, OF) \
-  hipLaunchKernelGGL((fp8_gemm_v2_kernel<FA, FB, OF, 2, 2>), dim3(nwg2), dim3(256), 0, stream, ap, bptr, sap, sbp, bp, cp, M, N, K)
+  hipLaunchKernelGGL((fp8_gemm_v2_kernel<FA, FB, OF>), dim3(nwg2), dim3(64 * V2_WM * V2_WN), 0, stream, ap, bptr, sap, sbp, bp, cp, M, N, K)
     if (!a_e5m2 && !b_e5m2) { if (out_fp32) GEMM2_LAUNCH(0, 0, true); else GEMM2_LAUNCH(0, 0, false); }
     else if (!a_e5m2 && b_e5m2) { if (out_fp32) GEMM2_LAUNCH(0, 1, true); else GEMM2_LAUNCH(0, 1, false); }
     else if (a_e5m2 && !b_e5m2) { if (out_fp32) GEMM2_LAUNCH(1, 0, true); else GEMM2_LAUNCH(1, 0, false); }

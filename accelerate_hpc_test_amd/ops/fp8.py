@@ -225,6 +225,12 @@ def convert_model_to_fp8(model: nn.Module, recipe=None, backend: str = "AO", mod
         if delayed and recipe is not None:
             m.fp8_in_eval = bool(recipe.use_autocast_during_eval)
         n += 1
+    # grouped MoE experts (models/moe.py) run their expert GEMMs in fp8 when they carry a recipe
+    for name, m in model.named_modules():
+        if not isinstance(m, nn.Linear) and hasattr(m, "fp8_recipe") and hasattr(m, "w_gate_up"):
+            if module_filter_func is None or module_filter_func(m, name):
+                m.fp8_recipe = Fp8Recipe(**kwargs)
+                n += 1
     model._acc_fp8_linears = n
     return model
 

@@ -59,13 +59,16 @@ def main():
     args = parse()
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     from accelerate_hpc_test_amd import Accelerator, FullyShardedDataParallelPlugin
-    from accelerate_hpc_test_amd.models.llama import LLAMA_PRESETS, LlamaForCausalLM
+    from accelerate_hpc_test_amd.models import LLAMA_PRESETS, MIXTRAL_PRESETS, LlamaForCausalLM, MixtralForCausalLM
+
+    is_moe = args.model in MIXTRAL_PRESETS
+    model_cls = MixtralForCausalLM if is_moe else LlamaForCausalLM
     from accelerate_hpc_test_amd.utils import RcclKwargs, set_seed
 
     plugin = FullyShardedDataParallelPlugin(
         fsdp_version=2,
         auto_wrap_policy="transformer_based_wrap",
-        transformer_cls_names_to_wrap=["LlamaDecoderLayer"],
+        transformer_cls_names_to_wrap=list(model_cls._no_split_modules),
         reshard_after_forward=True,
         activation_checkpointing=args.activation_checkpointing,
     )
@@ -84,11 +87,11 @@ def main():
         gemm_tuning.start_gemm_tuning(gemm_table)
     elif args.gemm_tuning == "auto":
         gemm_table = (args.gemm_table or gemm_tuning.DEFAULT_TABLE) if gemm_tuning.load_tuned_gemms(args.gemm_table) else None
-    cfg = LLAMA_PRESETS[args.model]
+    cfg = (MIXTRAL_PRESETS if is_moe else LLAMA_PRESETS)[args.model]
 
     t0 = time.time()
     with torch.device("meta"):
-        model = LlamaForCausalLM(cfg)
+        model = model_cls(cfg)
     optimizer = torch.optim.AdamW(model.parameters(), lr=1e-5)
     total_steps = args.warmup + args.steps
     ds = SyntheticTokens(total_steps * args.mbs * world, args.seq, cfg.vocab_size)
@@ -140,7 +143,7 @@ def main():
     peak = torch.cuda.max_memory_allocated() / 2**30
     if accelerator.is_main_process:
         rec = {
-            "metric": "tokens/sec (whole node) Llama-3-8B FSDP2 bf16 at 1/2/4/8 MI355X",
+            "metric": "tokens/sec (whole node) Llama-3-8B FSDP2 bf16 at 1/2/4/8 MI355X" if not is_moe else f"tokens/sec (whole node) {args.model} FSDP2 {args.precision}",
             "value": round(tps, 1),
             "unit": "tokens/s",
             "n_gpus": world,
@@ -149,11 +152,12 @@ def main():
             "ms_per_step": round(ms, 2),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": round(tps / (BASELINE_TOKENS_PER_SEC_PER_DEVICE * world), 3),
+            "vs_baseline": round(tps / (BASELINE_TOKENS_PER_SEC_PER_DEVICE * world), 3) if not is_moe else None,
             "dtype": args.precision,
             "data": "synthetic (random token ids, random-init weights)",
             "config": {
                 "model": "Llama-3-8B" if args.model.startswith("llama3") and "8b" in args.model else args.model,
+                "moe": {"experts": cfg.num_local_experts, "top_k": cfg.num_experts_per_tok} if is_moe else None,
                 "global_batch": args.mbs * world,
                 "seq_len": args.seq,
                 "parallelism": f"fsdp{world}",
@@ -164,7 +168,7 @@ def main():
             "tflops_per_gpu": round(flops_tok * tps / world / 1e12, 1),
             "peak_mem_gib": round(peak, 1),
             "final_loss": round(last_loss.item(), 4) if last_loss is not None else None,
-            "baseline_tokens_per_sec": BASELINE_TOKENS_PER_SEC_PER_DEVICE * world,
+            "baseline_tokens_per_sec": BASELINE_TOKENS_PER_SEC_PER_DEVICE * world if not is_moe else None,
             "gemm_table": os.path.basename(gemm_table) if gemm_table else None,
         }
         print(json.dumps(rec), flush=True)
