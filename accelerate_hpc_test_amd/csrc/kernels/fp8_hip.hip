@@ -214,16 +214,13 @@ constexpr int V2_STAGE = (V2_BM + V2_BN) * V2_BK;  // bytes per stage (A image t
 
 __device__ __forceinline__ int v2_swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
-constexpr int V2_WM = 2, V2_WN = 2;  // wave grid (a template-dependent __launch_bounds__ leaves the host stub undefined)
-
-template <int FA, int FB, bool OUT_F32>
-__global__ __launch_bounds__(64 * V2_WM * V2_WN, 1) void fp8_gemm_v2_kernel(const uint8_t* __restrict__ A,
-                                                                       const uint8_t* __restrict__ B,
-                                                                       const float* __restrict__ sa,
-                                                                       const float* __restrict__ sb,
-                                                                       const bf16_t* __restrict__ bias,
-                                                                       void* __restrict__ C, int M, int N, int K) {
-  constexpr int WM = V2_WM, WN = V2_WN;
+// Body shared by the two wave layouts; each __global__ wrapper below fixes its own launch bounds (a
+// template-dependent __launch_bounds__ on the kernel itself leaves the host stub undefined).
+template <int FA, int FB, bool OUT_F32, int WM, int WN>
+__device__ __forceinline__ void fp8_gemm_v2_body(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
+                                                 const float* __restrict__ sa, const float* __restrict__ sb,
+                                                 const bf16_t* __restrict__ bias, void* __restrict__ C, int M, int N,
+                                                 int K) {
   constexpr int NW = WM * WN;
   constexpr int TI = V2_BM / WM / 32, TJ = V2_BN / WN / 32;  // 32x32 MFMA tiles per wave along M / N
   constexpr int DPW = 32 / NW;                                 // 1-KiB DMA blocks per wave per operand
@@ -292,6 +289,9 @@ __global__ __launch_bounds__(64 * V2_WM * V2_WN, 1) void fp8_gemm_v2_kernel(cons
   auto compute = [&](const uint8_t* img) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
+      // 8-wave layout (256 VGPRs per wave): keep each k-sub's fragment reads next to its MFMAs, hoisting the next
+      // k-sub's reads would spill
+      if (NW > 4) __builtin_amdgcn_sched_barrier(0);
       v8i af[TI], bfr[TJ];
 #pragma unroll
       for (int j = 0; j < TJ; ++j) bfr[j] = frag(img, brow, j, ks);
@@ -348,6 +348,23 @@ __global__ __launch_bounds__(64 * V2_WM * V2_WN, 1) void fp8_gemm_v2_kernel(cons
         }
       }
     }
+}
+
+// 4 waves (one per SIMD, 128x128 per wave, 512-entry register file) and 8 waves (two per SIMD, 128x64 per wave).
+template <int FA, int FB, bool OUT_F32>
+__global__ __launch_bounds__(256, 1) void fp8_gemm_v2_w4_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
+                                                                const float* __restrict__ sa, const float* __restrict__ sb,
+                                                                const bf16_t* __restrict__ bias, void* __restrict__ C, int M,
+                                                                int N, int K) {
+  fp8_gemm_v2_body<FA, FB, OUT_F32, 2, 2>(A, B, sa, sb, bias, C, M, N, K);
+}
+
+template <int FA, int FB, bool OUT_F32>
+__global__ __launch_bounds__(512, 1) void fp8_gemm_v2_w8_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
+                                                                const float* __restrict__ sa, const float* __restrict__ sb,
+                                                                const bf16_t* __restrict__ bias, void* __restrict__ C, int M,
+                                                                int N, int K) {
+  fp8_gemm_v2_body<FA, FB, OUT_F32, 2, 4>(A, B, sa, sb, bias, C, M, N, K);
 }
 
 }  // namespace
@@ -419,8 +436,19 @@ torch::Tensor fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor a_scale_i
   static const bool force_v1 = std::getenv("ACCELERATE_FP8_GEMM_V1") != nullptr;
   if (!force_v1 && M % V2_BM == 0 && N % V2_BN == 0 && K % V2_BK == 0) {
     const int nwg2 = (M / V2_BM) * (N / V2_BN);
-#define GEMM2_LAUNCH(FA, FB, OF) \
-  hipLaunchKernelGGL((fp8_gemm_v2_kernel<FA, FB, OF>), dim3(nwg2), dim3(64 * V2_WM * V2_WN), 0, stream, ap, bptr, sap, sbp, bp, cp, M, N, K)
+    static const bool w8 = [] {
+      const char* e = std::getenv("ACCELERATE_FP8_GEMM_WAVES");
+      return e != nullptr && std::atoi(e) == 8;
+    }();
+#define GEMM2_LAUNCH(FA, FB, OF)                                                                                      \
+  do {                                                                                                                \
+    if (w8)                                                                                                           \
+      hipLaunchKernelGGL((fp8_gemm_v2_w8_kernel<FA, FB, OF>), dim3(nwg2), dim3(512), 0, stream, ap, bptr, sap, sbp, bp, \
+                         cp, M, N, K);                                                                                \
+    else                                                                                                              \
+      hipLaunchKernelGGL((fp8_gemm_v2_w4_kernel<FA, FB, OF>), dim3(nwg2), dim3(256), 0, stream, ap, bptr, sap, sbp, bp, \
+                         cp, M, N, K);                                                                                \
+  } while (0)
     if (!a_e5m2 && !b_e5m2) { if (out_fp32) GEMM2_LAUNCH(0, 0, true); else GEMM2_LAUNCH(0, 0, false); }
     else if (!a_e5m2 && b_e5m2) { if (out_fp32) GEMM2_LAUNCH(0, 1, true); else GEMM2_LAUNCH(0, 1, false); }
     else if (a_e5m2 && !b_e5m2) { if (out_fp32) GEMM2_LAUNCH(1, 0, true); else GEMM2_LAUNCH(1, 0, false); }
