@@ -22,6 +22,7 @@
 //   * dK/dV kernel: key-stationary (4 waves x 32 keys, K and V held in registers), sweeps 64-query slices:
 //     S = Q K^T and dP = dO V^T with the key on the lane, then dV^T += dO^T P and dK^T += Q^T dS using P / dS in
 //     place as B operands; per-q-head partials are summed over the GQA group by a small reduction kernel.
+#include <hip/hip_runtime.h>
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include "common.h"

@@ -6,6 +6,7 @@
 //     block scales (the MX-scaled MFMA runs at 2x the bf16 MFMA rate; the per-tensor scales are applied in the
 //     epilogue). 128x128 tile, BK = 64, 4 waves (2x2) of 64x64, LDS double buffer with XOR-swizzled 16-B chunks,
 //     XCD-aware tile order.
+#include <hip/hip_runtime.h>
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include "common.h"

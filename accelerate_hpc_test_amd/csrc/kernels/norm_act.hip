@@ -3,6 +3,7 @@
 //   * SwiGLU forward/backward on the fused [gate | up] projection output,
 //   * rotary embedding (rotate-half convention) applied in place to the Q and K heads of a fused QKV buffer.
 // All loads/stores are 16 B per lane (8 x bf16); one row per workgroup for the row-wise kernels.
+#include <hip/hip_runtime.h>
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include "common.h"

@@ -4,6 +4,7 @@
 //   * multi-tensor fused Adam/AdamW (one launch per parameter group over a chunked tensor list; optional bf16
 //     shadow write of the updated parameter for the FSDP all-gather),
 //   * multi-tensor L2 norm (two-pass, deterministic) and device-side clip scaling (no host sync).
+#include <hip/hip_runtime.h>
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include "common.h"

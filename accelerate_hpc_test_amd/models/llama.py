@@ -88,7 +88,9 @@ class RMSNorm(nn.Module):
         self.eps = eps
 
     def forward(self, x, residual=None):
-        return rms_norm(x, self.weight, self.eps, residual)
+        # fp32 weights under autocast (DDP mixed precision): the fused kernel runs in the activation dtype.
+        w = self.weight if self.weight.dtype == x.dtype else self.weight.to(x.dtype)
+        return rms_norm(x, w, self.eps, residual)
 
 
 class LlamaAttention(nn.Module):
@@ -208,6 +210,8 @@ class LlamaForCausalLM(nn.Module):
         cos, sin = self._rope(rope_len, input_ids.device)
         h = self.embed_tokens(input_ids)
         dt = self.layers[0].self_attn.qkv_proj.weight.dtype if len(self.layers) else h.dtype
+        if h.device.type in ("cuda", "cpu") and torch.is_autocast_enabled(h.device.type):
+            dt = torch.get_autocast_dtype(h.device.type)  # fp32 master params, bf16 activations (autocast)
         if h.dtype != dt:
             h = h.to(dt)
         residual = None

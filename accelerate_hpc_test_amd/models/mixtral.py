@@ -143,6 +143,8 @@ class MixtralForCausalLM(nn.Module):
         cos, sin = self._rope(rope_len, input_ids.device)
         h = self.embed_tokens(input_ids)
         dt = self.layers[0].self_attn.qkv_proj.weight.dtype if len(self.layers) else h.dtype
+        if h.device.type in ("cuda", "cpu") and torch.is_autocast_enabled(h.device.type):
+            dt = torch.get_autocast_dtype(h.device.type)
         if h.dtype != dt:
             h = h.to(dt)
         residual = None

@@ -49,45 +49,53 @@ def _swiglu_bwd(h, da):
     return torch.cat([dg, du], -1).to(h.dtype)
 
 
-def _mm(a, b_t, recipe=None):
-    """a [M,K] @ b_tᵀ where b_t is [N,K]. fp8 when a recipe is attached (per-expert dynamic scaling)."""
-    if recipe is not None and a.is_cuda and a.shape[0] > 0:
-        from ..ops.fp8 import _gemm_ok
-
-        if _gemm_ok(a.shape[0], b_t.shape[0], a.shape[1]):
-            return _fp8_mm_nograd(a, b_t, recipe)
-    return a @ b_t.t()
+def _pad_rows(t, rows):
+    if t.shape[0] == rows:
+        return t.contiguous()
+    out = t.new_zeros(rows, t.shape[1])
+    out[: t.shape[0]] = t
+    return out
 
 
-def _fp8_mm_nograd(a, b_t, recipe):
-    from ..ops.fp8 import E4M3_MAX, cast, gemm
+def _fp8_ok(x, recipe, dims):
+    from ..ops.fp8 import _gemm_ok
 
-    sa = recipe.scale("x", a, E4M3_MAX)
-    sb = recipe.scale("w", b_t, E4M3_MAX)
-    a8, _ = cast(a.contiguous(), sa, False, transpose=False)
-    b8, _ = cast(b_t.contiguous(), sb, False, transpose=False)
-    return gemm(a8, b8, 1.0 / sa, 1.0 / sb, None, torch.bfloat16)
+    return recipe is not None and x.is_cuda and use_native(x) and x.dtype == torch.bfloat16 and all(
+        _gemm_ok(128, d, 64) for d in dims
+    )
 
 
 class _GroupedExpertsFn(torch.autograd.Function):
-    """y_e = down_e(swiglu(gate_up_e(x_e))) for contiguous token segments x_e (sizes `counts`)."""
+    """y_e = down_e(swiglu(gate_up_e(x_e))) for contiguous token segments x_e (sizes `counts`).
+
+    bf16: hipBLASLt GEMMs on the raw segments. fp8 (a recipe is attached): each segment is zero-padded to a multiple
+    of 128 rows so all six GEMMs per expert (2 fwd, 2 dgrad, 2 wgrad) run on the MX-fp8 MFMA kernel; zero rows add
+    nothing to the wgrad sums and the padded output rows are dropped. Forward operands are e4m3, gradients e5m2
+    (HYBRID), per-expert per-tensor scales, and the transposed fp8 copies the backward needs come out of the same
+    cast kernel as the forward copies.
+    """
 
     @staticmethod
     def forward(ctx, x, w_gu, w_down, counts, recipe):
         y = torch.empty(x.shape[0], w_down.shape[1], dtype=x.dtype, device=x.device)
-        hs = []
+        fp8 = _fp8_ok(x, recipe, (w_gu.shape[1], w_gu.shape[2], w_down.shape[2]))
+        saved = []
         off = 0
         for e, c in enumerate(counts):
             if c == 0:
-                hs.append(None)
+                saved.append(None)
                 continue
             xe = x[off : off + c]
-            h = _mm(xe, w_gu[e], recipe)
-            y[off : off + c] = _mm(_swiglu_fwd(h), w_down[e], recipe)
-            hs.append(h)
+            if fp8:
+                y[off : off + c], st = _fp8_expert_fwd(xe, w_gu[e], w_down[e], recipe, e)
+                saved.append(st)
+            else:
+                h = xe @ w_gu[e].t()
+                y[off : off + c] = _swiglu_fwd(h) @ w_down[e].t()
+                saved.append(h)
             off += c
         ctx.save_for_backward(x, w_gu, w_down)
-        ctx.hs, ctx.counts, ctx.recipe = hs, counts, recipe
+        ctx.saved, ctx.counts, ctx.recipe, ctx.fp8 = saved, counts, recipe, fp8
         return y
 
     @staticmethod
@@ -101,17 +109,58 @@ class _GroupedExpertsFn(torch.autograd.Function):
         for e, c in enumerate(ctx.counts):
             if c == 0:
                 continue
-            h = ctx.hs[e]
             xe, dye = x[off : off + c], dy[off : off + c]
-            a = _swiglu_fwd(h)
-            torch.mm(dye.t(), a, out=dw_down[e]) if dw_down.dtype == dye.dtype else dw_down[e].copy_(dye.t() @ a)
-            da = dye @ w_down[e]
-            dh = _swiglu_bwd(h, da)
-            torch.mm(dh.t(), xe, out=dw_gu[e]) if dw_gu.dtype == dh.dtype else dw_gu[e].copy_(dh.t() @ xe)
-            dx[off : off + c] = dh @ w_gu[e]
+            if ctx.fp8:
+                dx[off : off + c] = _fp8_expert_bwd(dye, ctx.saved[e], ctx.recipe, e, dw_gu[e], dw_down[e])
+            else:
+                h = ctx.saved[e]
+                a = _swiglu_fwd(h)
+                torch.mm(dye.t(), a, out=dw_down[e]) if dw_down.dtype == dye.dtype else dw_down[e].copy_(dye.t() @ a)
+                dh = _swiglu_bwd(h, dye @ w_down[e])
+                torch.mm(dh.t(), xe, out=dw_gu[e]) if dw_gu.dtype == dh.dtype else dw_gu[e].copy_(dh.t() @ xe)
+                dx[off : off + c] = dh @ w_gu[e]
             off += c
-        ctx.hs = None
+        ctx.saved = None
         return dx, dw_gu, dw_down, None, None
+
+
+def _fp8_expert_fwd(xe, w_gu, w_down, recipe, e):
+    from ..ops.fp8 import E4M3_MAX, cast, gemm
+
+    c = xe.shape[0]
+    cp = (c + 127) // 128 * 128
+    xp = _pad_rows(xe, cp)
+    sx = recipe.scale(f"x{e}", xp, E4M3_MAX)
+    sgu = recipe.scale(f"wgu{e}", w_gu, E4M3_MAX)
+    x8, x8t = cast(xp, sx, False, transpose=True)
+    gu8, gu8t = cast(w_gu.contiguous(), sgu, False, transpose=True)
+    h = gemm(x8, gu8, 1.0 / sx, 1.0 / sgu, None, torch.bfloat16)  # [cp, 2I]; padded rows stay 0
+    a = _swiglu_fwd(h)
+    sa = recipe.scale(f"a{e}", a, E4M3_MAX)
+    sd = recipe.scale(f"wd{e}", w_down, E4M3_MAX)
+    a8, a8t = cast(a, sa, False, transpose=True)
+    d8, d8t = cast(w_down.contiguous(), sd, False, transpose=True)
+    yp = gemm(a8, d8, 1.0 / sa, 1.0 / sd, None, torch.bfloat16)
+    return yp[:c], (h, x8t, gu8t, a8t, d8t, sx, sgu, sa, sd)
+
+
+def _fp8_expert_bwd(dye, st, recipe, e, dw_gu_e, dw_down_e):
+    from ..ops.fp8 import E4M3_MAX, E5M2_MAX, cast, gemm
+
+    h, x8t, gu8t, a8t, d8t, sx, sgu, sa, sd = st
+    c, cp = dye.shape[0], h.shape[0]
+    e5 = recipe.grad_e5m2()
+    gmax = E5M2_MAX if e5 else E4M3_MAX
+    dyp = _pad_rows(dye.to(torch.bfloat16), cp)
+    sg = recipe.scale(f"gy{e}", dyp, gmax)
+    dy8, dy8t = cast(dyp, sg, e5, transpose=True)
+    dw_down_e.copy_(gemm(dy8t, a8t, 1.0 / sg, 1.0 / sa, None, torch.float32 if dw_down_e.dtype == torch.float32 else torch.bfloat16))
+    da = gemm(dy8, d8t, 1.0 / sg, 1.0 / sd, None, torch.bfloat16)  # [cp, I]
+    dh = _swiglu_bwd(h, da)  # [cp, 2I]
+    sh = recipe.scale(f"gh{e}", dh, gmax)
+    dh8, dh8t = cast(dh, sh, e5, transpose=True)
+    dw_gu_e.copy_(gemm(dh8t, x8t, 1.0 / sh, 1.0 / sx, None, torch.float32 if dw_gu_e.dtype == torch.float32 else torch.bfloat16))
+    return gemm(dh8, gu8t, 1.0 / sh, 1.0 / sgu, None, torch.bfloat16)[:c]
 
 
 class MoEExperts(nn.Module):

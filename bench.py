@@ -31,6 +31,10 @@ def parse():
     p.add_argument("--seq", type=int, default=8192)
     p.add_argument("--mbs", type=int, default=1)
     p.add_argument("--precision", default="bf16", choices=["bf16", "fp8"])
+    p.add_argument("--parallel", default="fsdp", choices=["fsdp", "ddp"],
+                   help="fsdp: FSDP2 full shard (headline); ddp: replicated fp32 params + bf16 autocast, RCCL all-reduce "
+                        "(BASELINE config 'Llama-3 8B DDP bf16')")
+    p.add_argument("--ddp-comm-hook", default="no", choices=["no", "bf16", "fp16"])
     p.add_argument("--activation-checkpointing", action="store_true")
     p.add_argument("--prefetch", type=int, default=1)
     p.add_argument("--verbose", action="store_true")
@@ -55,6 +59,13 @@ class SyntheticTokens(torch.utils.data.Dataset):
         return {"input_ids": ids, "labels": ids}
 
 
+def _metric_name(args, is_moe):
+    if not is_moe and args.parallel == "fsdp":
+        return "tokens/sec (whole node) Llama-3-8B FSDP2 bf16 at 1/2/4/8 MI355X"
+    name = "Llama-3-8B" if not is_moe else args.model
+    return f"tokens/sec (whole node) {name} {'FSDP2' if args.parallel == 'fsdp' else 'DDP'} {args.precision}"
+
+
 def main():
     args = parse()
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
@@ -72,11 +83,13 @@ def main():
         reshard_after_forward=True,
         activation_checkpointing=args.activation_checkpointing,
     )
-    accelerator = Accelerator(
-        mixed_precision=args.precision,
-        fsdp_plugin=plugin,
-        kwargs_handlers=[RcclKwargs(fsdp_prefetch_depth=args.prefetch)],
-    )
+    handlers = [RcclKwargs(fsdp_prefetch_depth=args.prefetch)]
+    if args.parallel == "ddp":
+        from accelerate_hpc_test_amd.utils import DDPCommunicationHookType, DistributedDataParallelKwargs
+
+        plugin = None
+        handlers.append(DistributedDataParallelKwargs(comm_hook=DDPCommunicationHookType(args.ddp_comm_hook)))
+    accelerator = Accelerator(mixed_precision=args.precision, fsdp_plugin=plugin, kwargs_handlers=handlers)
     set_seed(0)
     world = accelerator.num_processes
     from accelerate_hpc_test_amd.ops import gemm_tuning
@@ -92,6 +105,9 @@ def main():
     t0 = time.time()
     with torch.device("meta"):
         model = model_cls(cfg)
+    if args.parallel == "ddp":  # every rank holds the whole fp32 model (8B: 32 GB params + 32 GB grads + 64 GB Adam)
+        model.to_empty(device=accelerator.device)
+        model.init_weights()
     optimizer = torch.optim.AdamW(model.parameters(), lr=1e-5)
     total_steps = args.warmup + args.steps
     ds = SyntheticTokens(total_steps * args.mbs * world, args.seq, cfg.vocab_size)
@@ -141,9 +157,10 @@ def main():
     ms = elapsed / args.steps * 1000
     flops_tok = cfg.flops_per_token(args.seq)
     peak = torch.cuda.max_memory_allocated() / 2**30
+    headline = not is_moe and args.parallel == "fsdp"
     if accelerator.is_main_process:
         rec = {
-            "metric": "tokens/sec (whole node) Llama-3-8B FSDP2 bf16 at 1/2/4/8 MI355X" if not is_moe else f"tokens/sec (whole node) {args.model} FSDP2 {args.precision}",
+            "metric": _metric_name(args, is_moe),
             "value": round(tps, 1),
             "unit": "tokens/s",
             "n_gpus": world,
@@ -152,7 +169,7 @@ def main():
             "ms_per_step": round(ms, 2),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": round(tps / (BASELINE_TOKENS_PER_SEC_PER_DEVICE * world), 3) if not is_moe else None,
+            "vs_baseline": round(tps / (BASELINE_TOKENS_PER_SEC_PER_DEVICE * world), 3) if headline else None,
             "dtype": args.precision,
             "data": "synthetic (random token ids, random-init weights)",
             "config": {
@@ -160,7 +177,7 @@ def main():
                 "moe": {"experts": cfg.num_local_experts, "top_k": cfg.num_experts_per_tok} if is_moe else None,
                 "global_batch": args.mbs * world,
                 "seq_len": args.seq,
-                "parallelism": f"fsdp{world}",
+                "parallelism": f"{args.parallel}{world}",
                 "optimizer": "AdamW(lr=1e-5), fp32 master",
                 "activation_checkpointing": args.activation_checkpointing,
             },
@@ -168,7 +185,7 @@ def main():
             "tflops_per_gpu": round(flops_tok * tps / world / 1e12, 1),
             "peak_mem_gib": round(peak, 1),
             "final_loss": round(last_loss.item(), 4) if last_loss is not None else None,
-            "baseline_tokens_per_sec": BASELINE_TOKENS_PER_SEC_PER_DEVICE * world if not is_moe else None,
+            "baseline_tokens_per_sec": BASELINE_TOKENS_PER_SEC_PER_DEVICE * world if headline else None,
             "gemm_table": os.path.basename(gemm_table) if gemm_table else None,
         }
         print(json.dumps(rec), flush=True)

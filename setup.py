@@ -21,7 +21,7 @@ if os.environ.get("ACCELERATE_SKIP_NATIVE_BUILD", "0") != "1":
     root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "accelerate_hpc_test_amd", "csrc")
     sources = (
         [os.path.join(root, "bindings.cpp")]
-        + sorted(glob.glob(os.path.join(root, "kernels", "*.hip")))
+        + sorted(g for g in glob.glob(os.path.join(root, "kernels", "*.hip")) if not g.endswith("_hip.hip"))
         + sorted(glob.glob(os.path.join(root, "runtime", "*.cpp")))
     )
     sources = [os.path.relpath(s, os.path.dirname(os.path.abspath(__file__))) for s in sources]

@@ -228,3 +228,31 @@ def test_fp8_gemm_v2_matches_v1_random():
         subprocess.run([sys.executable, "-c", code], check=True, env=env, timeout=300)
         outs.append(torch.load(f, weights_only=True))
     assert torch.allclose(outs[0], outs[1], rtol=1e-5, atol=1e-3), (outs[0] - outs[1]).abs().max()
+
+
+def test_moe_grouped_experts_fp8_matches_bf16():
+    """fp8 grouped experts (padded segments, 6 MX-fp8 GEMMs per expert) track the bf16 grouped path: output and
+    all three gradients within fp8 quantisation error; a zero-token expert keeps a zero gradient."""
+    from accelerate_hpc_test_amd.models.moe import MoEExperts
+    from accelerate_hpc_test_amd.ops.fp8 import Fp8Recipe
+
+    torch.manual_seed(0)
+    E, H, I = 4, 256, 384
+    counts = [200, 0, 77, 300]
+    ex = MoEExperts(E, H, I).to(DEV, torch.bfloat16)
+    with torch.no_grad():
+        ex.w_gate_up.normal_(0, 0.05)
+        ex.w_down.normal_(0, 0.05)
+    x = torch.randn(sum(counts), H, device=DEV, dtype=torch.bfloat16)
+    dy = torch.randn(sum(counts), H, device=DEV, dtype=torch.bfloat16)
+    res = []
+    for recipe in (None, Fp8Recipe()):
+        ex.fp8_recipe = recipe
+        ex.zero_grad()
+        xi = x.clone().requires_grad_(True)
+        y = ex(xi, counts)
+        y.backward(dy)
+        res.append((y.float(), xi.grad.float(), ex.w_gate_up.grad.float(), ex.w_down.grad.float()))
+    for ref, out in zip(res[0], res[1]):
+        assert _rel(out, ref) < 8e-2, _rel(out, ref)
+    assert res[1][2][1].abs().max() == 0 and res[1][3][1].abs().max() == 0

@@ -113,3 +113,26 @@ def test_mixtral_hf_key_mapping():
     assert torch.equal(ex.w_gate_up[1, :I], sd[p + "block_sparse_moe.experts.1.w1.weight"])
     assert torch.equal(ex.w_gate_up[1, I:], sd[p + "block_sparse_moe.experts.1.w3.weight"])
     assert torch.equal(ex.w_down[0], sd[p + "block_sparse_moe.experts.0.w2.weight"])
+
+
+def test_llama_fp32_params_under_bf16_autocast():
+    """DDP-style mixed precision (fp32 params, Accelerator autocast): bf16 activations, fp32 grads, loss tracks the
+    fp32 model."""
+    from accelerate_hpc_test_amd import Accelerator
+    from accelerate_hpc_test_amd.models.llama import LLAMA_PRESETS, LlamaForCausalLM
+
+    torch.manual_seed(0)
+    model = LlamaForCausalLM(LLAMA_PRESETS["llama-tiny"])
+    model.init_weights()
+    ids = torch.randint(0, LLAMA_PRESETS["llama-tiny"].vocab_size, (2, 32))
+    ref = model(ids, labels=ids).loss.item()
+    acc = Accelerator(cpu=True, mixed_precision="bf16")
+    pm = acc.prepare(model)
+    seen = []
+    h = pm.layers[0].self_attn.qkv_proj.register_forward_hook(lambda m, i, o: seen.append((i[0].dtype, o.dtype)))
+    loss = pm(ids, labels=ids).loss
+    h.remove()
+    acc.backward(loss)
+    assert seen[0] == (torch.bfloat16, torch.bfloat16)
+    assert all(p.grad is not None and p.grad.dtype == torch.float32 for p in model.parameters())
+    assert abs(loss.item() - ref) < 0.05 * abs(ref)
