@@ -16,6 +16,8 @@ Parity: the reference wraps `torch.distributed.fsdp.fully_shard` (`/root/referen
   gather of block i+1 overlaps block i's compute. After forward (`reshard_after_forward`) the storage is freed and
   re-gathered before the unit's backward (triggered by a gradient hook on the unit's outputs).
 * **Reduce.** Parameter grads accumulate in place into a flat bf16 gradient buffer (pre-assigned `.grad` views).
+  For plain `nn.Linear` weights the weight-gradient GEMM itself targets the buffer (gradient-accumulation fusion:
+  `mm(dyᵀ, x, out=slot)` on first touch, `addmm_` after), so no separate grad tensor, add or zero fill exists.
   When every parameter of the unit has accumulated (post-accumulate-grad hooks), ONE `reduce_scatter_tensor` runs on
   the reduce stream; its output is scaled by 1/W and accumulated into the fp32 gradient shard. HSDP adds an
   all-reduce across the replicate group. `no_sync` (`set_requires_gradient_sync(False)`) keeps the flat grads.
@@ -48,7 +50,8 @@ def _round_up(x, m):
 
 
 class _ParamInfo:
-    __slots__ = ("fqn", "module", "attr", "param", "orig_param", "offset", "numel", "shape", "shard_param", "local_lo", "local_hi", "param_lo")
+    __slots__ = ("fqn", "module", "attr", "param", "orig_param", "offset", "numel", "shape", "shard_param", "local_lo", "local_hi",
+                 "param_lo", "fused", "fused_written")
 
     def __init__(self, fqn, module, attr, param, offset):
         self.fqn = fqn
@@ -61,6 +64,8 @@ class _ParamInfo:
         self.shape = tuple(param.shape)
         self.shard_param = None
         self.local_lo = self.local_hi = self.param_lo = 0
+        self.fused = False  # weight-gradient GEMM writes straight into the flat grad buffer (see _WgradSlot)
+        self.fused_written = False
 
 
 class FlatUnit:
@@ -195,6 +200,25 @@ class FSDPEngine:
             for info in unit.infos:
                 if info.param.requires_grad:
                     info.param.register_post_accumulate_grad_hook(self._make_grad_hook(unit))
+        if os.environ.get("ACCELERATE_FSDP_FUSED_WGRAD", "1") != "0":
+            self._install_fused_wgrad()
+
+    def _install_fused_wgrad(self):
+        """Route the weight gradient of every plain `nn.Linear` whose weight this engine owns (and that no other module
+        shares) through `_FusedWgradLinearFn`."""
+        refs = {}
+        for m in self.model.modules():
+            for p in m._parameters.values():
+                if p is not None:
+                    refs[id(p)] = refs.get(id(p), 0) + 1
+        for unit in self.units:
+            for info in unit.infos:
+                m = info.module
+                if (type(m) is nn.Linear and info.attr == "weight" and info.param.requires_grad
+                        and refs.get(id(info.param), 0) == 1 and getattr(info.param, "_tp_spec", None) is None):
+                    info.fused = True
+                    info.param._acc_wgrad_slot = _WgradSlot(self, unit, info)
+                    m.__class__ = _FusedWgradLinear
 
     def _replace_param(self, info: _ParamInfo, new: nn.Parameter):
         """Swap a (meta) Parameter object for `new` in every module that registers it (tied weights included)."""
@@ -406,17 +430,55 @@ class FSDPEngine:
     def _prepare_grad_buffer(self, unit: FlatUnit):
         """Point every param's `.grad` at its slice of a zeroed flat grad buffer (accumulated in place)."""
         if unit.full_grad is None:
-            if self.world_size == 1 and unit.full.dtype == self.reduce_dtype and False:
-                pass
-            unit.full_grad = torch.zeros(unit.padded, dtype=self.param_dtype, device=self.device)
+            unit.full_grad = self._new_grad_buffer(unit)
             for info in unit.infos:
-                if info.param.requires_grad:
+                if info.param.requires_grad and not info.fused:
                     info.param.grad = unit.full_grad[info.offset : info.offset + info.numel].view(info.shape)
         unit.pending_grads = sum(1 for i in unit.infos if i.param.requires_grad)
         unit.reduced = False
 
+    def _new_grad_buffer(self, unit: FlatUnit):
+        """Flat grad buffer; only the slots that are accumulated into (non-fused params, padding) are zeroed — a
+        fused slot is overwritten by its first weight-gradient GEMM."""
+        if not any(i.fused for i in unit.infos):
+            return torch.zeros(unit.padded, dtype=self.param_dtype, device=self.device)
+        buf = torch.empty(unit.padded, dtype=self.param_dtype, device=self.device)
+        pos = 0
+        for info in sorted(unit.infos, key=lambda i: i.offset):
+            if info.fused:
+                if info.offset > pos:
+                    buf[pos : info.offset].zero_()
+                pos = info.offset + info.numel
+                info.fused_written = False
+        if pos < unit.padded:
+            buf[pos:].zero_()
+        return buf
+
+    def _fused_wgrad(self, slot: "_WgradSlot", dy2: torch.Tensor, x2: torch.Tensor):
+        """dW = dy2ᵀ · x2 written into the unit's flat grad buffer; counts as the parameter's grad-ready event."""
+        unit, info = slot.unit, slot.info
+        if unit.full_grad is None:
+            self._prepare_grad_buffer(unit)
+        view = unit.full_grad[info.offset : info.offset + info.numel].view(info.shape)
+        if dy2.dtype != view.dtype or x2.dtype != view.dtype:
+            g = (dy2.t() @ x2).to(view.dtype)
+            view.add_(g) if info.fused_written else view.copy_(g)
+        elif info.fused_written:
+            view.addmm_(dy2.t(), x2)
+        else:
+            torch.mm(dy2.t(), x2, out=view)
+        info.fused_written = True
+        slot.uses -= 1
+        if slot.uses <= 0:
+            slot.uses = 0
+            unit.pending_grads -= 1
+            if unit.pending_grads == 0 and self.requires_grad_sync:
+                self._reduce_unit(unit)
+
     def _make_grad_hook(self, unit: FlatUnit):
         def hook(param):
+            if param.grad is None and getattr(param, "_acc_wgrad_slot", None) is not None:
+                return  # fused weight: its Linear backward already wrote the slot and counted it
             if unit.full_grad is None or param.grad is None or param.grad.data_ptr() != self._grad_slot_ptr(unit, param):
                 self._absorb_foreign_grad(unit, param)
             unit.pending_grads -= 1
@@ -435,14 +497,20 @@ class FSDPEngine:
         """A grad not living in our flat buffer (first use before a pre-backward hook, e.g. root params):
         copy/accumulate it into the flat buffer and re-point `.grad`."""
         if unit.full_grad is None:
-            unit.full_grad = torch.zeros(unit.padded, dtype=self.param_dtype, device=self.device)
+            unit.full_grad = self._new_grad_buffer(unit)
             unit.pending_grads = sum(1 for i in unit.infos if i.param.requires_grad)
             for info in unit.infos:
-                if info.param.requires_grad and info.param is not param and info.param.grad is None:
+                if info.param.requires_grad and not info.fused and info.param is not param and info.param.grad is None:
                     info.param.grad = unit.full_grad[info.offset : info.offset + info.numel].view(info.shape)
         for info in unit.infos:
             if info.param is param:
                 view = unit.full_grad[info.offset : info.offset + info.numel].view(info.shape)
+                if info.fused:  # fused weight that took the plain autograd path (autocast / dtype mismatch)
+                    if param.grad is not None:
+                        view.add_(param.grad.to(view.dtype)) if info.fused_written else view.copy_(param.grad)
+                        info.fused_written = True
+                    param.grad = None
+                    return
                 if param.grad is not None and param.grad.data_ptr() != view.data_ptr():
                     view.add_(param.grad.to(view.dtype))
                 param.grad = view
@@ -520,6 +588,9 @@ class FSDPEngine:
             self._recording_order = False
         for unit in self.units:
             unit.in_backward = False
+            for info in unit.infos:
+                if info.fused:
+                    info.param._acc_wgrad_slot.uses = 0  # forwards whose outputs never reached this backward
             if self.requires_grad_sync and unit.full_grad is not None and not unit.reduced:
                 self._reduce_unit(unit)
         if self.is_cuda and self.world_size * self.replicate_size > 1:
@@ -845,6 +916,47 @@ class FullyShardedModule(nn.Module):
             return super().__getattr__(name)
         except AttributeError:
             return getattr(self.module, name)
+
+
+class _WgradSlot:
+    """Where a fused Linear's weight gradient goes. `uses` counts forward applications whose backward is pending so a
+    weight applied twice reports grad-ready once (recomputation inside backward is not counted)."""
+
+    __slots__ = ("engine", "unit", "info", "uses")
+
+    def __init__(self, engine, unit, info):
+        self.engine, self.unit, self.info, self.uses = engine, unit, info, 0
+
+
+class _FusedWgradLinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, slot):
+        ctx.save_for_backward(x, weight)
+        ctx.slot = slot
+        ctx.has_bias = bias is not None
+        return nn.functional.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        dx = (dy2 @ w).view(*dy.shape[:-1], w.shape[1]) if ctx.needs_input_grad[0] else None
+        db = dy2.sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        ctx.slot.engine._fused_wgrad(ctx.slot, dy2, x.reshape(-1, x.shape[-1]))
+        return dx, None, db, None
+
+
+class _FusedWgradLinear(nn.Linear):
+    """`nn.Linear` owned by an FSDP unit: same parameters and forward; its weight gradient is fused into the flat
+    grad buffer (Megatron's gradient-accumulation fusion)."""
+
+    def forward(self, x):
+        slot = getattr(self.weight, "_acc_wgrad_slot", None)
+        if slot is None or not torch.is_grad_enabled() or torch.is_autocast_enabled(x.device.type) or x.dtype != self.weight.dtype:
+            return nn.functional.linear(x, self.weight, self.bias)
+        if torch._C._current_graph_task_id() == -1:
+            slot.uses += 1
+        return _FusedWgradLinearFn.apply(x, self.weight, self.bias, slot)
 
 
 def _cast_floats(x, dtype):

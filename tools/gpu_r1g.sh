@@ -9,6 +9,7 @@ run() {  # name timeout cmd...
   echo "$name rc=$rc"; tail -2 "gpurun_out/$name.log" | cut -c1-600
   [ $rc -eq 0 ] || exit $rc
 }
+run bench_8b_fusedwgrad 600 python bench.py --steps 5 --warmup 2
 run test_moe_fp8 300 python -m pytest tests/test_kernels_gpu.py -x -q -k "moe or fp8"
 run bench_mixtral_fp8 600 python bench.py --model mixtral-8x7b-4l --steps 3 --warmup 2 --precision fp8
 run bench_8b_ddp 600 python bench.py --parallel ddp --steps 5 --warmup 2
