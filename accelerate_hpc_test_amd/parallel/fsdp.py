@@ -454,20 +454,44 @@ class FSDPEngine:
             buf[pos:].zero_()
         return buf
 
+    def _direct_grads(self):
+        """World size 1 (no replicas): fused weight grads go straight to the fp32 grad shard (the GEMM writes fp32)."""
+        return self.world_size == 1 and self.replicate_size == 1 and os.environ.get("ACCELERATE_FSDP_WGRAD_FP32", "1") != "0"
+
+    def _fused_dest(self, unit, info):
+        """(destination view, accumulate?) for a fused weight gradient."""
+        if self._direct_grads():
+            # torch semantics: accumulate unless the grad was set to None (zero_grad). The grad is exposed at once, so a
+            # second use in this pass or the next no_sync micro-batch accumulates.
+            sp = info.shard_param
+            flat = unit.grad_shard[info.local_lo : info.local_hi]
+            acc = sp.grad is not None
+            sp.grad = flat
+            return flat.view(info.shape), acc
+        if unit.full_grad is None:
+            self._prepare_grad_buffer(unit)
+        dest = unit.full_grad[info.offset : info.offset + info.numel].view(info.shape)
+        acc = info.fused_written
+        info.fused_written = True
+        return dest, acc
+
     def _fused_wgrad(self, slot: "_WgradSlot", dy2: torch.Tensor, x2: torch.Tensor):
-        """dW = dy2ᵀ · x2 written into the unit's flat grad buffer; counts as the parameter's grad-ready event."""
+        """dW = dy2ᵀ · x2 written into the unit's flat grad buffer (or fp32 grad shard at world size 1); counts as the
+        parameter's grad-ready event."""
         unit, info = slot.unit, slot.info
         if unit.full_grad is None:
             self._prepare_grad_buffer(unit)
-        view = unit.full_grad[info.offset : info.offset + info.numel].view(info.shape)
-        if dy2.dtype != view.dtype or x2.dtype != view.dtype:
-            g = (dy2.t() @ x2).to(view.dtype)
-            view.add_(g) if info.fused_written else view.copy_(g)
-        elif info.fused_written:
-            view.addmm_(dy2.t(), x2)
+        dest, acc = self._fused_dest(unit, info)
+        a, b = dy2.t(), x2
+        if a.dtype != b.dtype:
+            b = b.to(a.dtype)
+        if dest.dtype == a.dtype:
+            dest.addmm_(a, b) if acc else torch.mm(a, b, out=dest)
+        elif dest.is_cuda and dest.dtype == torch.float32:
+            torch.addmm(dest, a, b, out_dtype=torch.float32, out=dest) if acc else torch.mm(a, b, out_dtype=torch.float32, out=dest)
         else:
-            torch.mm(dy2.t(), x2, out=view)
-        info.fused_written = True
+            g = (a @ b).to(dest.dtype)
+            dest.add_(g) if acc else dest.copy_(g)
         slot.uses -= 1
         if slot.uses <= 0:
             slot.uses = 0
@@ -507,8 +531,8 @@ class FSDPEngine:
                 view = unit.full_grad[info.offset : info.offset + info.numel].view(info.shape)
                 if info.fused:  # fused weight that took the plain autograd path (autocast / dtype mismatch)
                     if param.grad is not None:
-                        view.add_(param.grad.to(view.dtype)) if info.fused_written else view.copy_(param.grad)
-                        info.fused_written = True
+                        dest, acc = self._fused_dest(unit, info)
+                        dest.add_(param.grad.to(dest.dtype)) if acc else dest.copy_(param.grad)
                     param.grad = None
                     return
                 if param.grad is not None and param.grad.data_ptr() != view.data_ptr():
@@ -526,11 +550,19 @@ class FSDPEngine:
         # torch semantics: grads accumulate until the optimizer (or user) sets them to None.
         first = (not unit.grad_valid) or all(i.shard_param.grad is None for i in unit.infos if i.shard_param.requires_grad)
         if W == 1 and self.replicate_size == 1:
-            g = unit.full_grad[: unit.shard_numel]
-            if first:
-                unit.grad_shard.copy_(g)
+            if any(i.fused for i in unit.infos) and self._direct_grads():
+                for info in unit.infos:  # fused weights are already in the fp32 shard
+                    if info.fused or not info.param.requires_grad:
+                        continue
+                    g = unit.full_grad[info.offset : info.offset + info.numel]
+                    d = unit.grad_shard[info.local_lo : info.local_hi]
+                    d.copy_(g) if info.shard_param.grad is None else d.add_(g)
             else:
-                unit.grad_shard.add_(g)
+                g = unit.full_grad[: unit.shard_numel]
+                if first:
+                    unit.grad_shard.copy_(g)
+                else:
+                    unit.grad_shard.add_(g)
             unit.grad_valid = True
             self._release_grad(unit)
             self._expose_unit_grads(unit)

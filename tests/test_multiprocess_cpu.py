@@ -32,8 +32,14 @@ def test_fsdp_full_state_dict_ckpt():
     debug_launcher(td.check_fsdp_matches_single, args=(True, "FULL_STATE_DICT"), num_processes=2)
 
 
-def test_fsdp_no_sync_accumulation():
-    debug_launcher(td.check_fsdp_no_sync_accumulation, num_processes=2)
+@pytest.mark.parametrize("world", [1, 2])
+def test_fsdp_no_sync_accumulation(world):
+    debug_launcher(td.check_fsdp_no_sync_accumulation, num_processes=world)
+
+
+def test_fsdp_single_rank_matches_torch():
+    """World size 1: fused weight grads go straight to the fp32 grad shard (no flat-buffer copy)."""
+    debug_launcher(td.check_fsdp_matches_single, args=(True, "SHARDED_STATE_DICT"), num_processes=1)
 
 
 @pytest.mark.parametrize("sequence_parallel", [False, True])
