@@ -49,6 +49,9 @@ def _swiglu_bwd(h, da):
     return torch.cat([dg, du], -1).to(h.dtype)
 
 
+_FP8_ROW_PAD = 256  # the 256x256-tile fp8 GEMM (csrc/kernels/fp8.hip v2) needs M, N % 256 and K % 128
+
+
 def _pad_rows(t, rows):
     if t.shape[0] == rows:
         return t.contiguous()
@@ -69,7 +72,7 @@ class _GroupedExpertsFn(torch.autograd.Function):
     """y_e = down_e(swiglu(gate_up_e(x_e))) for contiguous token segments x_e (sizes `counts`).
 
     bf16: hipBLASLt GEMMs on the raw segments. fp8 (a recipe is attached): each segment is zero-padded to a multiple
-    of 128 rows so all six GEMMs per expert (2 fwd, 2 dgrad, 2 wgrad) run on the MX-fp8 MFMA kernel; zero rows add
+    of 256 rows so all six GEMMs per expert (2 fwd, 2 dgrad, 2 wgrad) run on the 256² MX-fp8 MFMA kernel; zero rows add
     nothing to the wgrad sums and the padded output rows are dropped. Forward operands are e4m3, gradients e5m2
     (HYBRID), per-expert per-tensor scales, and the transposed fp8 copies the backward needs come out of the same
     cast kernel as the forward copies.
@@ -128,7 +131,7 @@ def _fp8_expert_fwd(xe, w_gu, w_down, recipe, e):
     from ..ops.fp8 import E4M3_MAX, cast, gemm
 
     c = xe.shape[0]
-    cp = (c + 127) // 128 * 128
+    cp = (c + _FP8_ROW_PAD - 1) // _FP8_ROW_PAD * _FP8_ROW_PAD
     xp = _pad_rows(xe, cp)
     sx = recipe.scale(f"x{e}", xp, E4M3_MAX)
     sgu = recipe.scale(f"wgu{e}", w_gu, E4M3_MAX)

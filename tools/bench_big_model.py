@@ -63,11 +63,11 @@ def main():
             else:
                 t.normal_(0.0, 0.02, generator=g)
             host_bytes += t.numel() * 2
-            set_module_tensor_to_device(model, name, "cpu", value=t)
+            set_module_tensor_to_device(model, name, "cpu", value=t, dtype=torch.bfloat16)
         else:
             t = torch.empty(param.shape, dtype=torch.bfloat16, device=f"cuda:{dev}")
             t.fill_(1.0) if is_norm else t.normal_(0.0, 0.02)
-            set_module_tensor_to_device(model, name, f"cuda:{dev}", value=t)
+            set_module_tensor_to_device(model, name, f"cuda:{dev}", value=t, dtype=torch.bfloat16)
     torch.cuda.synchronize()
     t_mat = time.time() - t0
     t0 = time.time()
