@@ -1,0 +1,43 @@
+#!/bin/bash
+# Named GPU steps for `gpurun`: each runs under its own time limit, logs to gpurun_out/<step>.log, and the first
+# failing step ends the call (no retries, nothing more on the GPU after a fault or a timeout).
+#
+#   gpurun --timeout 1200 -- bash tools/gpu_steps.sh tests smoke bench8b prof8b
+#
+# Extra bench flags for the bench*/prof* steps: BENCH_ARGS="--prefetch 2" bash tools/gpu_steps.sh bench8b
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+export TMPDIR=/tmp
+run() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "== $name (limit ${t}s)"
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?
+  echo "$name rc=$rc"; tail -3 "gpurun_out/$name.log" | cut -c1-900
+  [ $rc -eq 0 ] || exit $rc
+}
+prof() {  # name timeout bench-args...
+  local name=$1 t=$2; shift 2
+  rm -rf "gpurun_out/$name"
+  run "$name" "$t" rocprofv3 --kernel-trace --stats --output-format csv -d "gpurun_out/$name" -o run -- python3 "$@"
+  python3 tools/prof_summary.py "gpurun_out/$name" > "gpurun_out/$name.md" && head -40 "gpurun_out/$name.md"
+}
+for step in "$@"; do
+  case $step in
+    tests) run tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench8b) run bench8b 600 python bench.py --steps 5 --warmup 2 $BENCH_ARGS ;;
+    bench8b_fp8) run bench8b_fp8 600 python bench.py --steps 5 --warmup 2 --precision fp8 $BENCH_ARGS ;;
+    bench8b_ddp) run bench8b_ddp 600 python bench.py --parallel ddp --steps 5 --warmup 2 $BENCH_ARGS ;;
+    mixtral_bf16) run mixtral_bf16 600 python bench.py --model mixtral-8x7b-4l --steps 3 --warmup 2 $BENCH_ARGS ;;
+    mixtral_fp8) run mixtral_fp8 600 python bench.py --model mixtral-8x7b-4l --steps 3 --warmup 2 --precision fp8 $BENCH_ARGS ;;
+    prof8b) prof prof8b 600 bench.py --steps 3 --warmup 2 $BENCH_ARGS ;;
+    prof8b_fp8) prof prof8b_fp8 600 bench.py --steps 3 --warmup 2 --precision fp8 $BENCH_ARGS ;;
+    prof_mixtral_fp8) prof prof_mixtral_fp8 600 bench.py --model mixtral-8x7b-4l --steps 2 --warmup 1 --precision fp8 ;;
+    attn) run attn 300 python tools/bench_attn.py ;;
+    gemm) run gemm 300 python tools/bench_gemm.py ;;
+    big70b) run big70b 900 python tools/bench_big_model.py --model llama3-70b --tokens 2048 --iters 3 ;;
+    big70b_offload) run big70b_offload 900 python tools/bench_big_model.py --model llama3-70b --gpu-mem 100GiB --tokens 2048 --iters 3 ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
