@@ -99,6 +99,8 @@ from .utils.other import (
     save,
 )
 
+from .utils.fault_tolerance import FaultInjector, StepWatchdog, check_collective_sequence  # noqa: E402
+
 logger = get_logger(__name__)
 
 _split_batches = object()  # sentinel, as in the reference
@@ -286,6 +288,10 @@ class Accelerator:
             self.rng_types = ["generator"]
         self.flag_tensor = None
         self._cp_context = None
+        # failure detection / fault drills (utils/fault_tolerance.py)
+        self._backward_calls = 0
+        self._watchdog = StepWatchdog.from_env(self.rccl_handler.watchdog_timeout, rank=self.process_index)
+        self._fault_injector = FaultInjector.from_env(self.process_index)
         check_os_kernel()
 
     # ============================================================================== properties
@@ -875,6 +881,10 @@ class Accelerator:
     # ============================================================================== training step helpers
     def backward(self, loss, **kwargs):
         learning_rate = kwargs.pop("learning_rate", None)
+        step = self._backward_calls
+        self._backward_calls += 1
+        if self._fault_injector is not None:
+            loss = self._fault_injector.before_backward(step, loss)
         loss = loss / self.gradient_accumulation_steps
         if self.scaler is not None:
             self.scaler.scale(loss).backward(**kwargs)
@@ -882,6 +892,15 @@ class Accelerator:
             self.lomo_backward(loss, learning_rate)
         else:
             loss.backward(**kwargs)
+        self.heartbeat("backward")
+        interval = self.rccl_handler.collective_check_interval
+        if self.state.debug and self.use_distributed and interval and self._backward_calls % interval == 0:
+            check_collective_sequence()
+
+    def heartbeat(self, tag: str = "step"):
+        """Tell the step watchdog (RcclKwargs.watchdog_timeout / ACCELERATE_WATCHDOG_TIMEOUT) this rank progressed."""
+        if self._watchdog is not None:
+            self._watchdog.beat(tag)
 
     def set_trigger(self):
         self.flag_tensor = torch.tensor(1, device=self.device)
@@ -1017,6 +1036,9 @@ class Accelerator:
                 tracker.log(values, step=step, **log_kwargs.get(tracker.name, {}))
 
     def end_training(self):
+        if getattr(self, "_watchdog", None) is not None:
+            self._watchdog.stop()
+            self._watchdog = None
         for tracker in self.trackers:
             if self.is_main_process or not getattr(tracker, "main_process_only", True):
                 tracker.finish()

@@ -19,9 +19,10 @@
 //     the permuted k order); V^T fragments come through the hardware transpose read.
 // Backward (no atomics, deterministic):
 //   * dQ kernel: query-stationary like the forward; recomputes P^T, dP^T = V dO^T, dQ^T += K^T dS^T;
-//   * dK/dV kernel: key-stationary (4 waves x 32 keys, K and V held in registers), sweeps 64-query slices:
-//     S = Q K^T and dP = dO V^T with the key on the lane, then dV^T += dO^T P and dK^T += Q^T dS using P / dS in
-//     place as B operands; per-q-head partials are summed over the GQA group by a small reduction kernel.
+//   * dK/dV kernel: key-stationary per (kv head, 128-key tile), 8 waves (two per SIMD), K and V in LDS; it sweeps
+//     every query head of the GQA group x 64-query slices: S = Q K^T and dP = dO V^T with the key on the lane, then
+//     dV^T += dO^T P and dK^T += Q^T dS using P / dS in place as B operands. dK / dV accumulate over the whole group
+//     in registers, so no per-q-head partials or reduction pass exist.
 #include <hip/hip_runtime.h>
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
@@ -90,22 +91,22 @@ __device__ __forceinline__ void zero(f32x16& x) {
   for (int i = 0; i < 16; ++i) x[i] = 0.f;
 }
 
-// Register staging of a ROWS x 128 bf16 tile by 256 threads: ROWS*16 chunks of 16 B, ROWS/16 per thread.
-template <int ROWS>
+// Register staging of a ROWS x 128 bf16 tile by NT threads: ROWS*16 chunks of 16 B, ROWS*16/NT per thread.
+template <int ROWS, int NT = 256>
 struct Stage {
-  static constexpr int kPer = ROWS * 16 / 256;
+  static constexpr int kPer = ROWS * 16 / NT;
   v8bf r[kPer];
   __device__ __forceinline__ void load(const bf16_t* base, long ts, int row0, int tid) {
 #pragma unroll
     for (int t = 0; t < kPer; ++t) {
-      const int c = tid + t * 256, row = c >> 4, ch = c & 15;
+      const int c = tid + t * NT, row = c >> 4, ch = c & 15;
       r[t] = *reinterpret_cast<const v8bf*>(base + (long)(row0 + row) * ts + ch * 8);
     }
   }
   __device__ __forceinline__ void store(char* img, int tid) const {
 #pragma unroll
     for (int t = 0; t < kPer; ++t) {
-      const int c = tid + t * 256, row = c >> 4, ch = c & 15;
+      const int c = tid + t * NT, row = c >> 4, ch = c & 15;
       *reinterpret_cast<v8bf*>(img + img_off(row, ch)) = r[t];
     }
   }
@@ -254,15 +255,14 @@ struct BwdParams {
   const bf16_t *q, *k, *v, *dout;
   long q_ts, k_ts, v_ts, do_ts, q_bs, k_bs, v_bs, do_bs;
   const float *lse, *delta;
-  bf16_t* dq;
-  long dq_ts, dq_bs;
-  float *dk_part, *dv_part;  // [B, S, Hq, D] fp32
+  bf16_t *dq, *dk, *dv;
+  long dq_ts, dq_bs, dk_ts, dk_bs, dv_ts, dv_bs;
   int S, Hq, Hkv;
-  float scale_log2, scale;
+  float scale_log2, scale, inv_scale;
 };
 
 template <bool CAUSAL>
-__global__ __launch_bounds__(256, 1) void attn_bwd_dq_kernel(BwdParams p) {
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(BwdParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int kTile = 64 * kRow;
   const int nqt = p.S / 128;
@@ -318,10 +318,13 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_kernel(BwdParams p) {
           sc = mfma(row_frag(k_img, kb * 32 + r, 2 * s + hf), qf[s], sc);
           dp = mfma(row_frag(v_img, kb * 32 + r, 2 * s + hf), df[s], dp);
         }
+        // causal: query qw0 + r sees keys k0 + 32kb + 4hf + acc_row(i, 0) up to itself (diagonal tiles only)
+        const int lim = qw0 + r - (k0 + kb * 32 + 4 * hf);
+        const bool diag = CAUSAL && k0 + kb * 32 + 31 > qw0;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           float pv = fast_exp2(sc[i] * p.scale_log2 - lse2);
-          if (CAUSAL && (k0 + kb * 32 + acc_row(i, hf) > qw0 + r)) pv = 0.f;
+          if (diag && acc_row(i, 0) > lim) pv = 0.f;
           sc[i] = pv * (dp[i] - dlt);
         }
         dsb[kb][0] = pack8(sc, 0);
@@ -353,140 +356,145 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_kernel(BwdParams p) {
     }
 }
 
-// Key-stationary dK / dV: 4 waves x 32 keys, 64-query slices double buffered.
+// Key-stationary dK / dV for one (batch, kv head, 128-key tile), summed over the kv head's whole GQA group of query
+// heads in registers: no per-q-head fp32 partials and no reduction pass. 8 waves, two per SIMD, so one wave's
+// softmax VALU overlaps its SIMD partner's MFMAs: wave w owns keys 32*(w&3) of the tile and the query half 32*(w>>2)
+// of every 64-query slice. K and V stay in LDS for the whole sweep (dual images, row reads for S = Q K^T and
+// dP = dO V^T); Q / dO slices (+ lse, delta) are double buffered with the async-stage split (global loads issued
+// before the MFMAs, LDS writes after them). The two query halves' partial dK / dV meet in LDS at the end.
 template <bool CAUSAL>
-__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(BwdParams p) {
+__global__ __launch_bounds__(512) void attn_bwd_dkdv_kernel(BwdParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int kSlice = 64;
-  constexpr int kImg = kSlice * kRow;            // 16 KB per operand
+  constexpr int kImg = kSlice * kRow;              // 16 KB: one 64-row Q or dO image
+  constexpr int kKV = 128 * kRow;                  // 32 KB: the key tile's K (or V) image
   constexpr int kBuf = 2 * kImg + 2 * kSlice * 4;  // Q, dO images + lse, delta
-  const int kt = blockIdx.y;                     // key tile of 128 keys; tile 0 has the most causal work
-  const int h = blockIdx.x, b = blockIdx.z;      // grid (Hq, S/128, B): heavy tiles of every head first
-  const int kh = h / (p.Hq / p.Hkv);
+  // grid.x = Hkv * nkt with the kv head fastest: key tile 0 (the most causal work) of every head is dispatched first,
+  // and all tiles of one head share blockIdx.x % 8 (one XCD under round-robin dispatch), whose L2 then serves that
+  // head's Q / dO stream to all of them.
+  const int kh = blockIdx.x % p.Hkv, kt = blockIdx.x / p.Hkv, b = blockIdx.y;
+  const int grp = p.Hq / p.Hkv;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hf = lane >> 5;
-  const int kw0 = kt * 128 + wave * 32;
-  const bf16_t* qb = p.q + b * p.q_bs + (long)h * kD;
-  const bf16_t* dob = p.dout + b * p.do_bs + (long)h * kD;
-  const bf16_t* kb_ = p.k + b * p.k_bs + (long)kh * kD;
-  const bf16_t* vb_ = p.v + b * p.v_bs + (long)kh * kD;
-  const float* lse_g = p.lse + ((long)b * p.Hq + h) * p.S;
-  const float* dlt_g = p.delta + ((long)b * p.Hq + h) * p.S;
-
-  v8bf kf[8], vf[8];
-#pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    kf[s] = *reinterpret_cast<const v8bf*>(kb_ + (long)(kw0 + r) * p.k_ts + 16 * s + 8 * hf);
-    vf[s] = *reinterpret_cast<const v8bf*>(vb_ + (long)(kw0 + r) * p.v_ts + 16 * s + 8 * hf);
+  const int kr = (wave & 3) * 32, qh = (wave >> 2) * 32;
+  const int kw0 = kt * 128 + kr;
+  char* k_img = smem;
+  char* v_img = smem + kKV;
+  char* bufs = smem + 2 * kKV;
+  {
+    Stage<128, 512> sk, sv;
+    sk.load(p.k + b * p.k_bs + (long)kh * kD, p.k_ts, kt * 128, tid);
+    sv.load(p.v + b * p.v_bs + (long)kh * kD, p.v_ts, kt * 128, tid);
+    sk.store(k_img, tid);
+    sv.store(v_img, tid);
   }
   f32x16 dk[4], dv[4];
 #pragma unroll
   for (int d = 0; d < 4; ++d) { zero(dk[d]); zero(dv[d]); }
 
   const int qs0 = CAUSAL ? kt * 2 : 0;  // first 64-query slice that can see this key tile
-  const int nqs = p.S / kSlice;
-  Stage<kSlice> sq, sd;
-  float st_l = 0.f, st_d = 0.f;
-  auto issue = [&](int qs) {
-    const int q0 = qs * kSlice;
-    sq.load(qb, p.q_ts, q0, tid);
-    sd.load(dob, p.do_ts, q0, tid);
-    if (tid < kSlice) st_l = lse_g[q0 + tid] * kLog2e;
-    else if (tid < 2 * kSlice) st_d = dlt_g[q0 + tid - kSlice];
+  const int per = p.S / kSlice - qs0;   // slices per query head
+  const int n_it = grp * per;
+  Stage<kSlice, 512> sq, sd;
+  float st = 0.f;
+  auto issue = [&](int it) {
+    const int h = kh * grp + it / per, q0 = (qs0 + it % per) * kSlice;
+    sq.load(p.q + b * p.q_bs + (long)h * kD, p.q_ts, q0, tid);
+    sd.load(p.dout + b * p.do_bs + (long)h * kD, p.do_ts, q0, tid);
+    const long row = ((long)b * p.Hq + h) * p.S + q0;
+    // row constants, pre-negated: they seed the S and dP accumulators (S' = Q K^T - LSE/scale, dP' = dO V^T - delta)
+    if (tid < kSlice) st = -p.lse[row + tid] * p.inv_scale;
+    else if (tid < 2 * kSlice) st = -p.delta[row + tid - kSlice];
   };
   auto commit = [&](int buf) {
-    char* base = smem + buf * kBuf;
+    char* base = bufs + buf * kBuf;
     sq.store(base, tid);
     sd.store(base + kImg, tid);
-    float* ls = reinterpret_cast<float*>(base + 2 * kImg);
-    if (tid < kSlice) ls[tid] = st_l;
-    else if (tid < 2 * kSlice) ls[tid] = st_d;  // delta at ls[kSlice + i]
+    if (tid < 2 * kSlice) reinterpret_cast<float*>(base + 2 * kImg)[tid] = st;  // lse [0, 64), delta [64, 128)
   };
-  issue(qs0);
+  issue(0);
   commit(0);
   __syncthreads();
+  // The second-dispatched half loses VALU arbitration to its SIMD partner on every segment; one static priority
+  // bump before the loop (no per-segment flips) evens the two halves out.
+  if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
 
-  for (int qs = qs0; qs < nqs; ++qs) {
-    const int cur = (qs - qs0) & 1;
-    const char* q_img = smem + cur * kBuf;
+  for (int it = 0; it < n_it; ++it) {
+    const int cur = it & 1;
+    const char* q_img = bufs + cur * kBuf;
     const char* d_img = q_img + kImg;
     const float* lse_s = reinterpret_cast<const float*>(q_img + 2 * kImg);
     const float* dlt_s = lse_s + kSlice;
-    const bool more = qs + 1 < nqs;
-    if (more) issue(qs + 1);
-    const int q0 = qs * kSlice;
+    const bool more = it + 1 < n_it;
+    if (more) issue(it + 1);
+    const int q0 = (qs0 + it % per) * kSlice;
+    if (!CAUSAL || q0 + qh + 31 >= kw0) {
+      f32x16 sc, dp;
 #pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      const int qh = half * 32;
-      if (!CAUSAL || q0 + qh + 31 >= kw0) {
-        f32x16 sc, dp;
-        zero(sc);
-        zero(dp);
+      for (int g = 0; g < 4; ++g) {  // rows qh + 8g + 4hf .. +3 of the slice: one 16-B LDS read per constant
+        const float4 l4 = *reinterpret_cast<const float4*>(lse_s + qh + 8 * g + 4 * hf);
+        const float4 d4 = *reinterpret_cast<const float4*>(dlt_s + qh + 8 * g + 4 * hf);
+        sc[4 * g] = l4.x; sc[4 * g + 1] = l4.y; sc[4 * g + 2] = l4.z; sc[4 * g + 3] = l4.w;
+        dp[4 * g] = d4.x; dp[4 * g + 1] = d4.y; dp[4 * g + 2] = d4.z; dp[4 * g + 3] = d4.w;
+      }
 #pragma unroll
-        for (int s = 0; s < 8; ++s) {
-          sc = mfma(row_frag(q_img, qh + r, 2 * s + hf), kf[s], sc);
-          dp = mfma(row_frag(d_img, qh + r, 2 * s + hf), vf[s], dp);
-        }
+      for (int s = 0; s < 8; ++s) {
+        sc = mfma(row_frag(q_img, qh + r, 2 * s + hf), row_frag(k_img, kr + r, 2 * s + hf), sc);
+        dp = mfma(row_frag(d_img, qh + r, 2 * s + hf), row_frag(v_img, kr + r, 2 * s + hf), dp);
+      }
+      // causal: key kw0 + r is masked for query rows q0 + qh + 4hf + acc_row(i, 0) below it (diagonal tiles only)
+      const int lim = kw0 + r - (q0 + qh + 4 * hf);
+      const bool diag = CAUSAL && q0 + qh < kw0 + 31;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int qi = qh + acc_row(i, hf);
-          float pv = fast_exp2(sc[i] * p.scale_log2 - lse_s[qi]);
-          if (CAUSAL && (kw0 + r > q0 + qi)) pv = 0.f;
-          sc[i] = pv;
-          dp[i] = pv * (dp[i] - dlt_s[qi]);
-        }
-        const v8bf pb0 = pack8(sc, 0), pb1 = pack8(sc, 1);
-        const v8bf ds0 = pack8(dp, 0), ds1 = pack8(dp, 1);
+      for (int i = 0; i < 16; ++i) {
+        float pv = fast_exp2(sc[i] * p.scale_log2);
+        if (diag && acc_row(i, 0) < lim) pv = 0.f;
+        sc[i] = pv;
+        dp[i] = pv * dp[i];
+      }
+      const v8bf pb0 = pack8(sc, 0), pb1 = pack8(sc, 1);
+      const v8bf ds0 = pack8(dp, 0), ds1 = pack8(dp, 1);
 #pragma unroll
-        for (int d = 0; d < 4; ++d) {
-          dv[d] = mfma(tr_frag(d_img, qh, d, lane), pb0, dv[d]);
-          dv[d] = mfma(tr_frag(d_img, qh + 16, d, lane), pb1, dv[d]);
-          dk[d] = mfma(tr_frag(q_img, qh, d, lane), ds0, dk[d]);
-          dk[d] = mfma(tr_frag(q_img, qh + 16, d, lane), ds1, dk[d]);
-        }
+      for (int d = 0; d < 4; ++d) {
+        dv[d] = mfma(tr_frag(d_img, qh, d, lane), pb0, dv[d]);
+        dv[d] = mfma(tr_frag(d_img, qh + 16, d, lane), pb1, dv[d]);
+        dk[d] = mfma(tr_frag(q_img, qh, d, lane), ds0, dk[d]);
+        dk[d] = mfma(tr_frag(q_img, qh + 16, d, lane), ds1, dk[d]);
       }
     }
     if (more) commit(cur ^ 1);
     __syncthreads();
   }
-  const long orow = (((long)b * p.S + kw0 + r) * p.Hq + h) * kD;
-#pragma unroll
-  for (int d = 0; d < 4; ++d)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int dd = d * 32 + 8 * g + 4 * hf;
-      *reinterpret_cast<float4*>(p.dk_part + orow + dd) =
-          make_float4(dk[d][4 * g] * p.scale, dk[d][4 * g + 1] * p.scale, dk[d][4 * g + 2] * p.scale, dk[d][4 * g + 3] * p.scale);
-      *reinterpret_cast<float4*>(p.dv_part + orow + dd) = make_float4(dv[d][4 * g], dv[d][4 * g + 1], dv[d][4 * g + 2], dv[d][4 * g + 3]);
-    }
-}
+  __builtin_amdgcn_s_setprio(0);
 
-// dk[b, s, kh, :] = sum over the GQA group of dk_part[b, s, h, :] (same for dv), written as bf16 (strided).
-__global__ void gqa_reduce_kernel(const float* __restrict__ dk_part, const float* __restrict__ dv_part, bf16_t* dk,
-                                  long dk_ts, long dk_bs, bf16_t* dv, long dv_ts, long dv_bs, int B, int S, int Hq,
-                                  int Hkv) {
-  const long total = (long)B * S * Hkv * (kD / 4);
-  const int grp = Hq / Hkv;
-  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
-    const int c = idx % (kD / 4);
-    long rest = idx / (kD / 4);
-    const int kh = rest % Hkv;
-    rest /= Hkv;
-    const int s = rest % S;
-    const int b = rest / S;
-    float4 ak = make_float4(0.f, 0.f, 0.f, 0.f), av = ak;
-    for (int g = 0; g < grp; ++g) {
-      const long off = (((long)b * S + s) * Hq + kh * grp + g) * kD + c * 4;
-      const float4 x = *reinterpret_cast<const float4*>(dk_part + off);
-      const float4 y = *reinterpret_cast<const float4*>(dv_part + off);
-      ak.x += x.x; ak.y += x.y; ak.z += x.z; ak.w += x.w;
-      av.x += y.x; av.y += y.y; av.z += y.z; av.w += y.w;
+  // Waves 4-7 hand their query-half partials to waves 0-3 through LDS (64 KB per pass: dK, then dV); the sum is
+  // scaled and written as bf16 into the strided [B, S, Hkv, D] output.
+  float* red = reinterpret_cast<float*>(smem);
+  auto finish = [&](f32x16(&acc)[4], bf16_t* dst, long ts, long bs, float scale) {
+    if (wave >= 4) {
+      float* w = red + (wave - 4) * 4096;
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[(d * 16 + i) * 64 + lane] = acc[d][i];
     }
-    bf16x4 wk, wv;
-    wk.v[0] = f2bf(ak.x); wk.v[1] = f2bf(ak.y); wk.v[2] = f2bf(ak.z); wk.v[3] = f2bf(ak.w);
-    wv.v[0] = f2bf(av.x); wv.v[1] = f2bf(av.y); wv.v[2] = f2bf(av.z); wv.v[3] = f2bf(av.w);
-    *reinterpret_cast<bf16x4*>(dk + b * dk_bs + (long)s * dk_ts + (long)kh * kD + c * 4) = wk;
-    *reinterpret_cast<bf16x4*>(dv + b * dv_bs + (long)s * dv_ts + (long)kh * kD + c * 4) = wv;
-  }
+    __syncthreads();
+    if (wave < 4) {
+      const float* w = red + wave * 4096;
+      bf16_t* out = dst + b * bs + (long)(kw0 + r) * ts + (long)kh * kD;
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          bf16x4 o;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) o.v[t] = f2bf((acc[d][4 * g + t] + w[(d * 16 + 4 * g + t) * 64 + lane]) * scale);
+          *reinterpret_cast<bf16x4*>(out + d * 32 + 8 * g + 4 * hf) = o;
+        }
+    }
+    __syncthreads();
+  };
+  finish(dk, p.dk, p.dk_ts, p.dk_bs, p.scale);
+  finish(dv, p.dv, p.dv_ts, p.dv_bs, 1.f);
 }
 
 void check_qkv(const torch::Tensor& t, const char* name) {
@@ -499,7 +507,7 @@ void check_qkv(const torch::Tensor& t, const char* name) {
 
 constexpr size_t kFwdSmem = 2 * 2 * 64 * kRow;                    // 64 KB
 constexpr size_t kDqSmem = 2 * 2 * 64 * kRow;                     // 64 KB
-constexpr size_t kDkdvSmem = 2 * (2 * 64 * kRow + 2 * 64 * 4);    // 65 KB
+constexpr size_t kDkdvSmem = 2 * 128 * kRow + 2 * (2 * 64 * kRow + 2 * 64 * 4);  // 129 KB
 
 template <typename K>
 void allow_smem(K kernel, size_t bytes) {
@@ -555,32 +563,27 @@ void flash_attn_bwd(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch:
                        reinterpret_cast<const bf16_t*>(dout.data_ptr()), dout.stride(1), dout.stride(0),
                        delta.data_ptr<float>(), S, Hq, B);
   }
-  auto dk_part = torch::empty({B, S, Hq, kD}, q.options().dtype(torch::kFloat32));
-  auto dv_part = torch::empty({B, S, Hq, kD}, q.options().dtype(torch::kFloat32));
+  TORCH_CHECK(k.size(1) == S && v.size(1) == S, "flash_attn: q/k/v sequence lengths must match");
+  TORCH_CHECK(Hq % Hkv == 0 && dk.size(2) == Hkv && dv.size(2) == Hkv && dq.size(2) == Hq, "flash_attn: head counts");
   BwdParams p{reinterpret_cast<const bf16_t*>(q.data_ptr()), reinterpret_cast<const bf16_t*>(k.data_ptr()),
               reinterpret_cast<const bf16_t*>(v.data_ptr()), reinterpret_cast<const bf16_t*>(dout.data_ptr()),
               q.stride(1), k.stride(1), v.stride(1), dout.stride(1), q.stride(0), k.stride(0), v.stride(0),
               dout.stride(0), lse.data_ptr<float>(), delta.data_ptr<float>(), reinterpret_cast<bf16_t*>(dq.data_ptr()),
-              dq.stride(1), dq.stride(0), dk_part.data_ptr<float>(), dv_part.data_ptr<float>(), S, Hq, Hkv,
-              (float)(softmax_scale * kLog2e), (float)softmax_scale};
-  dim3 grid(Hq, S / 128, B);
+              reinterpret_cast<bf16_t*>(dk.data_ptr()), reinterpret_cast<bf16_t*>(dv.data_ptr()), dq.stride(1),
+              dq.stride(0), dk.stride(1), dk.stride(0), dv.stride(1), dv.stride(0), S, Hq, Hkv,
+              (float)(softmax_scale * kLog2e), (float)softmax_scale, (float)(1.0 / softmax_scale)};
   static bool attrs = false;
   if (!attrs) {
     allow_smem(attn_bwd_dkdv_kernel<true>, kDkdvSmem);
     allow_smem(attn_bwd_dkdv_kernel<false>, kDkdvSmem);
     attrs = true;
   }
+  const dim3 dq_grid(Hq, S / 128, B), kv_grid(Hkv * (S / 128), B);
   if (causal) {
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, grid, dim3(256), kDqSmem, stream, p);
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<true>, grid, dim3(256), kDkdvSmem, stream, p);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, dq_grid, dim3(256), kDqSmem, stream, p);
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<true>, kv_grid, dim3(512), kDkdvSmem, stream, p);
   } else {
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<false>, grid, dim3(256), kDqSmem, stream, p);
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<false>, grid, dim3(256), kDkdvSmem, stream, p);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<false>, dq_grid, dim3(256), kDqSmem, stream, p);
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<false>, kv_grid, dim3(512), kDkdvSmem, stream, p);
   }
-  const long work = (long)B * S * Hkv * (kD / 4);
-  long g = (work + 255) / 256;
-  if (g > 2048) g = 2048;
-  hipLaunchKernelGGL(gqa_reduce_kernel, dim3(g), dim3(256), 0, stream, dk_part.data_ptr<float>(),
-                     dv_part.data_ptr<float>(), reinterpret_cast<bf16_t*>(dk.data_ptr()), dk.stride(1), dk.stride(0),
-                     reinterpret_cast<bf16_t*>(dv.data_ptr()), dv.stride(1), dv.stride(0), B, S, Hq, Hkv);
 }

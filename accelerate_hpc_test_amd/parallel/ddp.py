@@ -29,6 +29,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..utils.dataclasses import DDPCommunicationHookType
+from ..utils.fault_tolerance import record_collective
 
 
 class _Bucket:
@@ -211,6 +212,7 @@ class DistributedDataParallel(nn.Module):
 
     def _allreduce_buffer(self, buf, key: int = 0):
         W = self.world_size
+        record_collective("ddp_all_reduce", buf, self.process_group)
         if self.comm_hook in (DDPCommunicationHookType.POWER_SGD, DDPCommunicationHookType.BATCHED_POWER_SGD) and buf.dtype.is_floating_point:
             self._powersgd(buf, key)
             return

@@ -41,6 +41,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..utils.dataclasses import FullyShardedDataParallelPlugin, MixedPrecisionPolicy
+from ..utils.fault_tolerance import record_collective
 
 _ALIGN = 64  # elements; keeps every rank's shard 128-B aligned for bf16 / 256-B for fp32
 
@@ -329,6 +330,7 @@ class FSDPEngine:
         if self.is_cuda:
             cur = torch.cuda.current_stream(self.device)
             self.ag_stream.wait_stream(cur)
+            record_collective("fsdp_all_gather", unit.shard_lp, self.group)
             with torch.cuda.stream(self.ag_stream):
                 dist.all_gather_into_tensor(unit.full, unit.shard_lp, group=self.group)
                 ev = torch.cuda.Event()
@@ -587,6 +589,7 @@ class FSDPEngine:
     def _rs_and_accumulate(self, unit, src, out, first):
         W = self.world_size
         if W > 1:
+            record_collective("fsdp_reduce_scatter", src, self.group)
             if self._uses_gloo and self._gloo():
                 self._gloo_rs(out, src)
             else:

@@ -294,11 +294,17 @@ class RcclKwargs(KwargsHandler):
     - `ddp_bucket_mb`: DDP gradient bucket size (default 128 MB → 16 MB per peer at 8 GPUs).
     - `fsdp_prefetch_depth`: how many FSDP units are all-gathered ahead of compute.
     - `comm_stream_priority`: HIP stream priority of the collective streams (-1 = high).
+    - `watchdog_timeout`: seconds without a training-step heartbeat after which the rank dumps its stacks and exits
+      (utils/fault_tolerance.py); `ACCELERATE_WATCHDOG_TIMEOUT`; None = off.
+    - `collective_check_interval`: in debug mode, compare every rank's collective-sequence digest each N backward
+      passes (`ACCELERATE_COLLECTIVE_CHECK_INTERVAL`, default 50).
     """
 
     ddp_bucket_mb: int = None
     fsdp_prefetch_depth: int = None
     comm_stream_priority: int = None
+    watchdog_timeout: float = None
+    collective_check_interval: int = None
 
     def __post_init__(self):
         if self.ddp_bucket_mb is None:
@@ -307,6 +313,10 @@ class RcclKwargs(KwargsHandler):
             self.fsdp_prefetch_depth = int(os.environ.get("ACCELERATE_RCCL_FSDP_PREFETCH", 1))
         if self.comm_stream_priority is None:
             self.comm_stream_priority = int(os.environ.get("ACCELERATE_RCCL_STREAM_PRIORITY", -1))
+        if self.watchdog_timeout is None and os.environ.get("ACCELERATE_WATCHDOG_TIMEOUT"):
+            self.watchdog_timeout = float(os.environ["ACCELERATE_WATCHDOG_TIMEOUT"])
+        if self.collective_check_interval is None:
+            self.collective_check_interval = int(os.environ.get("ACCELERATE_COLLECTIVE_CHECK_INTERVAL", 50))
 
 
 # ---------------------------------------------------------------------------------------------------

@@ -25,6 +25,7 @@ from typing import Any
 import torch
 
 from .dataclasses import DistributedType, TensorInformation
+from .fault_tolerance import record_collective
 
 
 def PartialState():  # noqa: N802 - lazy accessor (utils is imported by state.py; avoid the import cycle)
@@ -280,9 +281,11 @@ def _gpu_gather_one(tensor: torch.Tensor) -> torch.Tensor:
         tensor = tensor.contiguous()
     if state.backend is not None and state.backend.startswith("gloo"):
         outs = [torch.empty_like(tensor) for _ in range(state.num_processes)]
+        record_collective("all_gather", tensor)
         torch.distributed.all_gather(outs, tensor)
         return torch.cat(outs, dim=0)
     out = torch.empty(state.num_processes * tensor.numel(), dtype=tensor.dtype, device=tensor.device)
+    record_collective("all_gather", tensor)
     torch.distributed.all_gather_into_tensor(out, tensor.reshape(-1))
     return out.view(-1, *tensor.size()[1:])
 
@@ -334,6 +337,7 @@ def _gpu_broadcast(data, src=0):
     leaves = _leaves(data, [])
     if _coalescable(leaves):
         flat = torch.cat([t.reshape(-1) for t in leaves])
+        record_collective("broadcast", flat)
         torch.distributed.broadcast(flat, src=src)
         outs, off = [], 0
         for t in leaves:
@@ -344,6 +348,7 @@ def _gpu_broadcast(data, src=0):
         return _rebuild(data, iter(outs))
 
     def _gpu_broadcast_one(tensor, src=0):
+        record_collective("broadcast", tensor)
         torch.distributed.broadcast(tensor, src=src)
         return tensor
 
@@ -518,6 +523,7 @@ def reduce(tensor, reduction="mean", scale=1.0):
     leaves = _leaves(tensor, [])
     if _coalescable(leaves):
         flat = torch.cat([t.reshape(-1) for t in leaves])
+        record_collective("all_reduce", flat)
         torch.distributed.all_reduce(flat, torch.distributed.ReduceOp.SUM)
         _finish(flat)
         outs, off = [], 0
@@ -529,6 +535,7 @@ def reduce(tensor, reduction="mean", scale=1.0):
 
     def _reduce_across_processes(t):
         cloned = t.clone()
+        record_collective("all_reduce", cloned)
         torch.distributed.all_reduce(cloned, torch.distributed.ReduceOp.SUM)
         return _finish(cloned)
 

@@ -104,7 +104,7 @@ def _attn_ref(q, k, v, causal, scale):
 
 
 @pytest.mark.parametrize("causal", [True, False])
-@pytest.mark.parametrize("B,S,Hq,Hkv", [(1, 256, 4, 2), (2, 512, 8, 2), (1, 384, 2, 2)])
+@pytest.mark.parametrize("B,S,Hq,Hkv", [(1, 256, 4, 2), (2, 512, 8, 2), (1, 384, 2, 2), (1, 1024, 8, 2), (1, 2048, 32, 8)])
 def test_flash_attention(causal, B, S, Hq, Hkv):
     torch.manual_seed(0)
     D = 128

@@ -47,7 +47,6 @@ def main():
         placement[str(dev)] = placement.get(str(dev), 0) + 1
     # materialise on the target devices (GPU: N(0, .02) generated in place; CPU: pinned host memory)
     t0 = time.time()
-    g = torch.Generator(device="cpu").manual_seed(0)
     host_bytes = 0
     for name, param in list(model.named_parameters()):
         dev = None
@@ -57,12 +56,16 @@ def main():
                 break
         is_norm = name.endswith("layernorm.weight") or name == "norm.weight"
         if dev in ("cpu", "disk"):
+            # random values drawn on the GPU and copied into pinned host memory (a CPU normal_ over ~100 GB takes
+            # many minutes)
             t = torch.empty(param.shape, dtype=torch.bfloat16, pin_memory=True)
-            if is_norm:
-                t.fill_(1.0)
-            else:
-                t.normal_(0.0, 0.02, generator=g)
+            src = torch.empty(param.shape, dtype=torch.bfloat16, device="cuda:0")
+            src.fill_(1.0) if is_norm else src.normal_(0.0, 0.02)
+            t.copy_(src)
+            del src
             host_bytes += t.numel() * 2
+            if host_bytes // (8 << 30) != (host_bytes - t.numel() * 2) // (8 << 30):
+                print(f"materialised {host_bytes / 2**30:.0f} GiB of host-offloaded weights", flush=True)
             set_module_tensor_to_device(model, name, "cpu", value=t, dtype=torch.bfloat16)
         else:
             t = torch.empty(param.shape, dtype=torch.bfloat16, device=f"cuda:{dev}")
@@ -77,10 +80,12 @@ def main():
     with torch.no_grad():
         model(ids, return_logits=False)  # warmup (also pins/uploads once)
         torch.cuda.synchronize()
+        print("warmup forward done", flush=True)
         t0 = time.perf_counter()
-        for _ in range(args.iters):
+        for i in range(args.iters):
             model(ids, return_logits=False)
-        torch.cuda.synchronize()
+            torch.cuda.synchronize()
+            print(f"forward {i} done", flush=True)
         dt = (time.perf_counter() - t0) / args.iters
     rec = {
         "metric": "prefill tokens/s, Llama big-model dispatch (device_map=auto)",
