@@ -544,6 +544,8 @@ class Accelerator:
             return
         old = model.require_backward_grad_sync
         model.require_backward_grad_sync = True
+        if hasattr(model, "trigger_sync"):
+            model.trigger_sync()
         try:
             yield
         finally:

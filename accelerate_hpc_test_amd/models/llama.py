@@ -55,8 +55,10 @@ class LlamaConfig:
         """Training FLOPs per token: 6·N (matmuls, fwd+bwd) + causal attention 6·L·S·Hq·D (≈ half of 12·L·S·Hq·D).
         Unlike the reference's helper (examples/torch_native_parallelism/utils.py:94-115) the attention term keeps
         the head dimension."""
-        n_matmul = self.num_params - self.vocab_size * self.hidden_size * (0 if self.tie_word_embeddings else 1) - self.hidden_size
-        n_matmul += self.vocab_size * self.hidden_size  # lm_head GEMM
+        H, L = self.hidden_size, self.num_hidden_layers
+        # decoder matmul weights (norm weights excluded) + the lm_head GEMM; the embedding lookup is not a matmul
+        n_matmul = self.num_params - self.vocab_size * H * (1 if self.tie_word_embeddings else 2) - H - 2 * H * L
+        n_matmul += self.vocab_size * H
         attn = 6 * self.num_hidden_layers * seq_len * self.num_attention_heads * self.head_dim
         return 6 * n_matmul + attn
 

@@ -30,6 +30,7 @@ import torch.nn as nn
 
 from ..utils.dataclasses import DDPCommunicationHookType
 from ..utils.fault_tolerance import record_collective
+from ..utils.tracing import trace_range
 
 
 class _Bucket:
@@ -76,6 +77,9 @@ class DistributedDataParallel(nn.Module):
         self.rank = dist.get_rank(process_group)
         self.broadcast_buffers = broadcast_buffers
         self.require_backward_grad_sync = True
+        # torch DDP semantics: whether a backward all-reduces is decided by the FORWARD that built its graph (under
+        # `no_sync()` or not), unless `trigger_sync()` (Accelerator.trigger_sync_in_backward) forces it.
+        self._sync_pending = True
         self.find_unused_parameters = find_unused_parameters
         self.device = next((p.device for p in module.parameters()), torch.device("cpu"))
         self.is_cuda = self.device.type == "cuda"
@@ -166,7 +170,13 @@ class DistributedDataParallel(nn.Module):
         for b in self.buckets:
             b.pending = len(b.params)
             b.launched = False
+        if torch.is_grad_enabled():
+            self._sync_pending = self.require_backward_grad_sync
         return self.module(*inputs, **kwargs)
+
+    def trigger_sync(self):
+        """Make the next backward all-reduce even though its forward ran under `no_sync()`."""
+        self._sync_pending = True
 
     # ------------------------------------------------------------------------------------------ reduce
     def _grad_hook(self, p):
@@ -182,7 +192,7 @@ class DistributedDataParallel(nn.Module):
         b.pending -= 1
         join = getattr(self, "_join", None)
         deferred = join is not None and join["active"] < self.world_size  # joined ranks shadow in bucket order
-        if b.pending == 0 and self.require_backward_grad_sync and not deferred:
+        if b.pending == 0 and self._sync_pending and not deferred:
             self._launch(b)
 
     def _slot(self, b, p):
@@ -199,7 +209,7 @@ class DistributedDataParallel(nn.Module):
         b.launched = True
         if self.is_cuda:
             self.comm_stream.wait_stream(torch.cuda.current_stream(self.device))
-            with torch.cuda.stream(self.comm_stream):
+            with torch.cuda.stream(self.comm_stream), trace_range("ddp.bucket_all_reduce"):
                 self._allreduce(b)
         else:
             self._allreduce(b)
@@ -279,7 +289,7 @@ class DistributedDataParallel(nn.Module):
 
     def _finalize(self):
         self._cb_queued = False
-        if self.require_backward_grad_sync:
+        if self._sync_pending:
             for b in self.buckets:
                 if not b.launched:
                     self._launch(b)

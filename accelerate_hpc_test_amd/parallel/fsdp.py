@@ -42,6 +42,7 @@ import torch.nn as nn
 
 from ..utils.dataclasses import FullyShardedDataParallelPlugin, MixedPrecisionPolicy
 from ..utils.fault_tolerance import record_collective
+from ..utils.tracing import trace_range
 
 _ALIGN = 64  # elements; keeps every rank's shard 128-B aligned for bf16 / 256-B for fp32
 
@@ -331,7 +332,7 @@ class FSDPEngine:
             cur = torch.cuda.current_stream(self.device)
             self.ag_stream.wait_stream(cur)
             record_collective("fsdp_all_gather", unit.shard_lp, self.group)
-            with torch.cuda.stream(self.ag_stream):
+            with torch.cuda.stream(self.ag_stream), trace_range(f"fsdp.all_gather[{unit.idx}]"):
                 dist.all_gather_into_tensor(unit.full, unit.shard_lp, group=self.group)
                 ev = torch.cuda.Event()
                 ev.record(self.ag_stream)
@@ -574,7 +575,7 @@ class FSDPEngine:
         if self.is_cuda:
             cur = torch.cuda.current_stream(self.device)
             self.rs_stream.wait_stream(cur)
-            with torch.cuda.stream(self.rs_stream):
+            with torch.cuda.stream(self.rs_stream), trace_range(f"fsdp.reduce_scatter[{unit.idx}]"):
                 self._rs_and_accumulate(unit, src, out, first)
             src.record_stream(self.rs_stream)
             out.record_stream(self.rs_stream)

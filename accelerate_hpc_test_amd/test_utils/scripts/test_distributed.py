@@ -556,6 +556,94 @@ def check_ddp_powersgd():
     assert torch.allclose(g[0], g[-1], atol=1e-6)
 
 
+def _grads_equal(a, b, **kw):
+    return all(torch.allclose(p.grad, q.grad, **kw) for p, q in zip(a.parameters(), b.parameters()) if p.requires_grad)
+
+
+def check_grad_sync(mode: str = "no_sync", sync_each_batch: bool = False):
+    """The reference's `test_sync.py` oracle on our DDP reducer: after each backward, the data-parallel model's local
+    grads equal a single-process model's grads on the gathered global batch exactly when a sync was due.
+
+    modes: `no_sync` (odd iterations sync), `accumulate` (GradientAccumulationPlugin(num_steps=2, sync_each_batch)),
+    `trigger` (three no_sync forwards, backwards with the last one under `trigger_sync_in_backward`)."""
+    from accelerate_hpc_test_amd.utils import GradientAccumulationPlugin
+
+    plugin = GradientAccumulationPlugin(num_steps=2, sync_each_batch=sync_each_batch) if mode == "accumulate" else None
+    acc = Accelerator(cpu=True, gradient_accumulation_plugin=plugin)
+    W, r = acc.num_processes, acc.process_index
+    set_seed(42)
+    base = TinyMLP()
+    model = acc.prepare(copy.deepcopy(base))
+    bs = 4
+    batches = _global_batches(4, bs, W, seed=1)
+    ga = acc.gradient_accumulation_steps
+
+    def base_step(x, y):
+        (F.mse_loss(base(x), y) / ga).backward()
+
+    def local(x, y):
+        return x[r * bs : (r + 1) * bs], y[r * bs : (r + 1) * bs]
+
+    if mode == "trigger":
+        losses = []
+        for x, y in batches[:3]:
+            base_step(x, y)
+            with acc.no_sync(model):
+                xl, yl = local(x, y)
+                losses.append(F.mse_loss(model(xl), yl))
+        for i, loss in enumerate(losses):
+            if i < len(losses) - 1:
+                acc.backward(loss)
+                assert not _grads_equal(base, acc.unwrap_model(model), atol=1e-6), f"synced early at backward {i}"
+            else:
+                with acc.trigger_sync_in_backward(model):
+                    acc.backward(loss)
+                assert _grads_equal(base, acc.unwrap_model(model), atol=1e-6), "not synced after triggered backward"
+        return
+    for it, (x, y) in enumerate(batches):
+        base_step(x, y)
+        xl, yl = local(x, y)
+        if mode == "no_sync":
+            synced = it % 2 == 1
+            ctx = acc.no_sync(model) if not synced else __import__("contextlib").nullcontext()
+            with ctx:
+                acc.backward(F.mse_loss(model(xl), yl))
+        else:
+            synced = (it + 1) % 2 == 0 or sync_each_batch
+            with acc.accumulate(model):
+                acc.backward(F.mse_loss(model(xl), yl))
+        same = _grads_equal(base, acc.unwrap_model(model), atol=1e-6)
+        if mode == "accumulate" and sync_each_batch:
+            # every batch synced, but the reference grads accumulate over 2 steps exactly like ours
+            assert same, f"iteration {it}: grads not in sync"
+        else:
+            assert same == synced, f"iteration {it}: in sync={same}, expected {synced}"
+        if mode == "no_sync" and synced or mode == "accumulate" and (it + 1) % 2 == 0:
+            base.zero_grad()
+            acc.unwrap_model(model).zero_grad()
+            for p in acc.unwrap_model(model).parameters():
+                p.grad = None
+
+
+def check_collective_sequence(mismatch: bool = False):
+    """Debug-mode collective-order check: identical sequences pass; an extra collective on one rank is named."""
+    from accelerate_hpc_test_amd.utils.fault_tolerance import CollectiveLog, check_collective_sequence as check
+
+    state = PartialState(cpu=True)
+    CollectiveLog.get().reset()
+    reduce(torch.ones(3), reduction="sum")
+    gather(torch.ones(2))
+    if mismatch and state.process_index == 1:
+        CollectiveLog.get().record("all_reduce", state.num_processes, torch.float32, 7)  # a collective rank 0 never issued
+    try:
+        check()
+        raised = False
+    except DistributedOperationException as e:
+        raised = True
+        assert "rank 1" in str(e)
+    assert raised == mismatch
+
+
 def main():
     check_ops()
     check_dataloader_sharding()

@@ -162,7 +162,6 @@ class StepWatchdog:
             idle = time.monotonic() - self._last
             if idle < self.timeout:
                 continue
-            self.fired = True
             log = CollectiveLog.get()
             sys.stderr.write(
                 f"[accelerate watchdog] rank {self.rank}: no training progress for {idle:.1f}s (timeout {self.timeout:.1f}s); "
@@ -171,6 +170,7 @@ class StepWatchdog:
             sys.stderr.flush()
             faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
             sys.stderr.flush()
+            self.fired = True
             if self.action == "exit":
                 os._exit(self.exit_code)
             self._last = time.monotonic()  # warn mode: report again after another full timeout

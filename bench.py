@@ -60,7 +60,7 @@ class SyntheticTokens(torch.utils.data.Dataset):
 
 
 def _metric_name(args, is_moe):
-    if not is_moe and args.parallel == "fsdp":
+    if not is_moe and args.parallel == "fsdp" and args.precision == "bf16":
         return "tokens/sec (whole node) Llama-3-8B FSDP2 bf16 at 1/2/4/8 MI355X"
     name = "Llama-3-8B" if not is_moe else args.model
     return f"tokens/sec (whole node) {name} {'FSDP2' if args.parallel == 'fsdp' else 'DDP'} {args.precision}"
