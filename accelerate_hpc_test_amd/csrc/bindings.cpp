@@ -29,10 +29,10 @@ void flash_attn_bwd(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch:
                     bool causal);
 // fp8.hip
 torch::Tensor fp8_amax(torch::Tensor x, c10::optional<torch::Tensor> out);
-torch::Tensor fp8_scale_from_amax(torch::Tensor amax, double fp8_max, double margin);
-std::vector<torch::Tensor> fp8_cast(torch::Tensor x, torch::Tensor scale, bool e5m2, bool transpose);
+std::vector<torch::Tensor> fp8_cast(torch::Tensor x, torch::Tensor t, double qmax, bool from_amax, bool e5m2, bool transpose);
 torch::Tensor fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor a_scale_inv, torch::Tensor b_scale_inv,
-                       bool a_e5m2, bool b_e5m2, c10::optional<torch::Tensor> bias, bool out_fp32);
+                       double smul, bool a_e5m2, bool b_e5m2, c10::optional<torch::Tensor> bias, bool out_fp32,
+                       c10::optional<torch::Tensor> out, bool accumulate);
 // runtime/*.cpp
 void register_runtime(pybind11::module& m);
 
@@ -52,8 +52,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("flash_attn_fwd", &flash_attn_fwd);
   m.def("flash_attn_bwd", &flash_attn_bwd);
   m.def("fp8_amax", &fp8_amax);
-  m.def("fp8_scale_from_amax", &fp8_scale_from_amax);
   m.def("fp8_cast", &fp8_cast);
-  m.def("fp8_gemm", &fp8_gemm);
+  m.def("fp8_gemm", &fp8_gemm, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("a_scale_inv"), pybind11::arg("b_scale_inv"),
+        pybind11::arg("smul"), pybind11::arg("a_e5m2"), pybind11::arg("b_e5m2"), pybind11::arg("bias"), pybind11::arg("out_fp32"),
+        pybind11::arg("out") = pybind11::none(), pybind11::arg("accumulate") = false);
   register_runtime(m);
 }

@@ -46,56 +46,87 @@ __device__ __forceinline__ uint32_t cvt_pair(float a, float b) {
   return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false) & 0xffffu;
 }
 
-// y = sat(x * scale) as fp8 [M, N]; optionally yt = y^T [N, M]. 64x64 tiles, 256 threads.
+// Scale of a cast: FROM_AMAX ? qmax / max(amax, tiny) : t[0] * qmax (t = a plain scale tensor). Reading the
+// scale straight from the amax buffer on the device keeps the scale arithmetic out of separate tiny launches.
+__device__ __forceinline__ float cast_scale(const float* t, float qmax, bool from_amax) {
+  return from_amax ? qmax / fmaxf(t[0], 1e-12f) : t[0] * qmax;
+}
+
+// 4x4 byte transpose of four dwords (w[i] = bytes of row i): returns in c[j] the four bytes of column j.
+__device__ __forceinline__ void transpose4x4(const uint32_t w[4], uint32_t c[4]) {
+  const uint32_t lo01 = __builtin_amdgcn_perm(w[1], w[0], 0x05010400u), hi01 = __builtin_amdgcn_perm(w[1], w[0], 0x07030602u);
+  const uint32_t lo23 = __builtin_amdgcn_perm(w[3], w[2], 0x05010400u), hi23 = __builtin_amdgcn_perm(w[3], w[2], 0x07030602u);
+  c[0] = __builtin_amdgcn_perm(lo23, lo01, 0x05040100u);
+  c[1] = __builtin_amdgcn_perm(lo23, lo01, 0x07060302u);
+  c[2] = __builtin_amdgcn_perm(hi23, hi01, 0x05040100u);
+  c[3] = __builtin_amdgcn_perm(hi23, hi01, 0x07060302u);
+}
+
+template <bool E5M2>
+__device__ __forceinline__ uint32_t cvt4(const bf16_t* v, float s) {
+  return cvt_pair<E5M2>(bf2f(v[0]) * s, bf2f(v[1]) * s) | (cvt_pair<E5M2>(bf2f(v[2]) * s, bf2f(v[3]) * s) << 16);
+}
+
+// y = sat(x * scale) as fp8 [M, N]; optionally yt = y^T [N, M]. One 128x128 tile per 256-thread workgroup:
+// each thread converts 4 x 16 elements (two 16-B loads -> one 16-B store per row piece) into a padded LDS byte
+// tile; the transposed copy is read back as 4-byte words, transposed 4x4 in registers (v_perm_b32) and written as
+// 16-B rows of yt, 8 lanes per 128-B line. Partial edge tiles take a per-element path.
+constexpr int kCT = 128, kCTP = kCT + 4;  // tile edge, padded LDS row pitch (bytes)
 template <bool E5M2, bool TRANS>
-__global__ __launch_bounds__(256) void cast_kernel(const bf16_t* __restrict__ x, const float* __restrict__ scale,
-                                                   uint8_t* __restrict__ y, uint8_t* __restrict__ yt, int M, int N) {
-  __shared__ uint8_t tile[64][64 + 4];
-  const int tm = blockIdx.y * 64, tn = blockIdx.x * 64;
-  const float s = scale[0];
+__global__ __launch_bounds__(256) void cast_kernel(const bf16_t* __restrict__ x, const float* __restrict__ st, float qmax,
+                                                   int from_amax, uint8_t* __restrict__ y, uint8_t* __restrict__ yt, int M,
+                                                   int N) {
+  __shared__ __attribute__((aligned(16))) uint8_t tile[kCT * kCTP];
+  const int tm = blockIdx.y * kCT, tn = blockIdx.x * kCT;
+  const float s = cast_scale(st, qmax, from_amax != 0);
   const int tid = threadIdx.x;
-  // each thread: 2 rows x 8 columns
-#pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {
-    const int rr = (tid >> 3) + pass * 32, cc = (tid & 7) * 8;
-    const int gm = tm + rr, gn = tn + cc;
-    uint8_t vals[8];
-    if (gm < M && gn + 7 < N && (N & 7) == 0) {
-      const bf16x8 a = *reinterpret_cast<const bf16x8*>(x + (long)gm * N + gn);
-      uint32_t w0 = cvt_pair<E5M2>(bf2f(a.v[0]) * s, bf2f(a.v[1]) * s) | (cvt_pair<E5M2>(bf2f(a.v[2]) * s, bf2f(a.v[3]) * s) << 16);
-      uint32_t w1 = cvt_pair<E5M2>(bf2f(a.v[4]) * s, bf2f(a.v[5]) * s) | (cvt_pair<E5M2>(bf2f(a.v[6]) * s, bf2f(a.v[7]) * s) << 16);
-      *reinterpret_cast<uint2*>(y + (long)gm * N + gn) = make_uint2(w0, w1);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) { vals[j] = (w0 >> (8 * j)) & 0xff; vals[4 + j] = (w1 >> (8 * j)) & 0xff; }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        vals[j] = 0;
-        if (gm < M && gn + j < N) {
-          const float f = bf2f(x[(long)gm * N + gn + j]) * s;
-          vals[j] = cvt_pair<E5M2>(f, 0.f) & 0xff;
-          y[(long)gm * N + gn + j] = vals[j];
-        }
+  const bool full = tm + kCT <= M && tn + kCT <= N && (N % 16) == 0 && (M % 16) == 0;
+  if (!full) {  // edge tile
+    for (int e = tid; e < kCT * kCT; e += 256) {
+      const int r = e / kCT, c = e % kCT, gm = tm + r, gn = tn + c;
+      if (gm < M && gn < N) {
+        const uint8_t v = cvt_pair<E5M2>(bf2f(x[(long)gm * N + gn]) * s, 0.f) & 0xff;
+        y[(long)gm * N + gn] = v;
+        if (TRANS) yt[(long)gn * M + gm] = v;
       }
     }
+    return;
+  }
+  // phase 1: rows r = tid/8 + 32p, 16 columns c = (tid%8)*16
+#pragma unroll
+  for (int pass = 0; pass < 4; ++pass) {
+    const int r = (tid >> 3) + pass * 32, c = (tid & 7) * 16;
+    const bf16_t* src = x + (long)(tm + r) * N + tn + c;
+    const bf16x8 a = *reinterpret_cast<const bf16x8*>(src);
+    const bf16x8 b = *reinterpret_cast<const bf16x8*>(src + 8);
+    uint4 w;
+    w.x = cvt4<E5M2>(a.v, s);
+    w.y = cvt4<E5M2>(a.v + 4, s);
+    w.z = cvt4<E5M2>(b.v, s);
+    w.w = cvt4<E5M2>(b.v + 4, s);
+    *reinterpret_cast<uint4*>(y + (long)(tm + r) * N + tn + c) = w;
     if (TRANS) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) tile[cc + j][rr] = vals[j];
+      uint32_t* t = reinterpret_cast<uint32_t*>(tile + r * kCTP + c);
+      t[0] = w.x; t[1] = w.y; t[2] = w.z; t[3] = w.w;
     }
   }
-  if (TRANS) {
-    __syncthreads();
+  if (!TRANS) return;
+  __syncthreads();
+  // phase 2: output rows n = n4 .. n4+3 (tile columns), 16 output bytes m16 .. m16+15 each
+  const int m16 = (tid & 7) * 16, n4 = (tid >> 3) * 4;
+  uint32_t col[4][4];  // col[j][q]: bytes m16+4q .. +3 of output row n4+j
 #pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
-      const int rr = (tid >> 3) + pass * 32, cc = (tid & 7) * 8;  // rr: n index, cc: m index
-      const int gn = tn + rr, gm = tm + cc;
-      if (gn < N) {
+  for (int q = 0; q < 4; ++q) {
+    uint32_t w[4], c[4];
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (gm + j < M) yt[(long)gn * M + gm + j] = tile[rr][cc + j];
-      }
-    }
+    for (int i = 0; i < 4; ++i) w[i] = *reinterpret_cast<const uint32_t*>(tile + (m16 + 4 * q + i) * kCTP + n4);
+    transpose4x4(w, c);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) col[j][q] = c[j];
   }
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    *reinterpret_cast<uint4*>(yt + (long)(tn + n4 + j) * M + tm + m16) = make_uint4(col[j][0], col[j][1], col[j][2], col[j][3]);
 }
 
 // ------------------------------------------------------------------------------------------------ GEMM
@@ -105,9 +136,9 @@ __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >>
 
 template <int FA, int FB, bool OUT_F32>
 __global__ __launch_bounds__(256, 2) void fp8_gemm_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
-                                                          const float* __restrict__ sa, const float* __restrict__ sb,
+                                                          const float* __restrict__ sa, const float* __restrict__ sb, float smul,
                                                           const bf16_t* __restrict__ bias, void* __restrict__ C, int M,
-                                                          int N, int K) {
+                                                          int N, int K, int accum) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[2][2][BM * BK];  // [buf][A/B][rows * 64 B]
   const int tiles_n = N / BN;
   const int nwg = (M / BM) * tiles_n;
@@ -172,7 +203,7 @@ __global__ __launch_bounds__(256, 2) void fp8_gemm_kernel(const uint8_t* __restr
     if (kt + 1 < nk) lstore(cur ^ 1);
     __syncthreads();
   }
-  const float s = sa[0] * sb[0];
+  const float s = sa[0] * sb[0] * smul;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -188,12 +219,23 @@ __global__ __launch_bounds__(256, 2) void fp8_gemm_kernel(const uint8_t* __restr
           if (bias != nullptr) v[t] += bf2f(bias[n + t]);
         }
         if (OUT_F32) {
-          *reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + (long)m * N + n) = make_float4(v[0], v[1], v[2], v[3]);
+          float4* cp4 = reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + (long)m * N + n);
+          if (accum) {
+            const float4 o = *cp4;
+            v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+          }
+          *cp4 = make_float4(v[0], v[1], v[2], v[3]);
         } else {
+          bf16x4* cp4 = reinterpret_cast<bf16x4*>(reinterpret_cast<bf16_t*>(C) + (long)m * N + n);
+          if (accum) {
+            const bf16x4 o = *cp4;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) v[t] += bf2f(o.v[t]);
+          }
           bf16x4 w;
 #pragma unroll
           for (int t = 0; t < 4; ++t) w.v[t] = f2bf(v[t]);
-          *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16_t*>(C) + (long)m * N + n) = w;
+          *cp4 = w;
         }
       }
     }
@@ -218,9 +260,9 @@ __device__ __forceinline__ int v2_swz(int row, int chunk) { return chunk ^ ((row
 // template-dependent __launch_bounds__ on the kernel itself leaves the host stub undefined).
 template <int FA, int FB, bool OUT_F32, int WM, int WN>
 __device__ __forceinline__ void fp8_gemm_v2_body(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
-                                                 const float* __restrict__ sa, const float* __restrict__ sb,
+                                                 const float* __restrict__ sa, const float* __restrict__ sb, float smul,
                                                  const bf16_t* __restrict__ bias, void* __restrict__ C, int M, int N,
-                                                 int K) {
+                                                 int K, int accum) {
   constexpr int NW = WM * WN;
   constexpr int TI = V2_BM / WM / 32, TJ = V2_BN / WN / 32;  // 32x32 MFMA tiles per wave along M / N
   constexpr int DPW = 32 / NW;                                 // 1-KiB DMA blocks per wave per operand
@@ -323,7 +365,7 @@ __device__ __forceinline__ void fp8_gemm_v2_body(const uint8_t* __restrict__ A, 
     retire();
   }
   if (kt < nk) compute(stage0);  // odd number of K-steps: the last one was staged into stage0
-  const float s = sa[0] * sb[0];
+  const float s = sa[0] * sb[0] * smul;
 #pragma unroll
   for (int i = 0; i < TI; ++i)
 #pragma unroll
@@ -339,12 +381,23 @@ __device__ __forceinline__ void fp8_gemm_v2_body(const uint8_t* __restrict__ A, 
           if (bias != nullptr) v[t] += bf2f(bias[n + t]);
         }
         if (OUT_F32) {
-          *reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + (long)m * N + n) = make_float4(v[0], v[1], v[2], v[3]);
+          float4* cp4 = reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + (long)m * N + n);
+          if (accum) {
+            const float4 o = *cp4;
+            v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+          }
+          *cp4 = make_float4(v[0], v[1], v[2], v[3]);
         } else {
+          bf16x4* cp4 = reinterpret_cast<bf16x4*>(reinterpret_cast<bf16_t*>(C) + (long)m * N + n);
+          if (accum) {
+            const bf16x4 o = *cp4;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) v[t] += bf2f(o.v[t]);
+          }
           bf16x4 w;
 #pragma unroll
           for (int t = 0; t < 4; ++t) w.v[t] = f2bf(v[t]);
-          *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16_t*>(C) + (long)m * N + n) = w;
+          *cp4 = w;
         }
       }
     }
@@ -353,18 +406,18 @@ __device__ __forceinline__ void fp8_gemm_v2_body(const uint8_t* __restrict__ A, 
 // 4 waves (one per SIMD, 128x128 per wave, 512-entry register file) and 8 waves (two per SIMD, 128x64 per wave).
 template <int FA, int FB, bool OUT_F32>
 __global__ __launch_bounds__(256, 1) void fp8_gemm_v2_w4_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
-                                                                const float* __restrict__ sa, const float* __restrict__ sb,
+                                                                const float* __restrict__ sa, const float* __restrict__ sb, float smul,
                                                                 const bf16_t* __restrict__ bias, void* __restrict__ C, int M,
-                                                                int N, int K) {
-  fp8_gemm_v2_body<FA, FB, OUT_F32, 2, 2>(A, B, sa, sb, bias, C, M, N, K);
+                                                                int N, int K, int accum) {
+  fp8_gemm_v2_body<FA, FB, OUT_F32, 2, 2>(A, B, sa, sb, smul, bias, C, M, N, K, accum);
 }
 
 template <int FA, int FB, bool OUT_F32>
 __global__ __launch_bounds__(512, 1) void fp8_gemm_v2_w8_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
-                                                                const float* __restrict__ sa, const float* __restrict__ sb,
+                                                                const float* __restrict__ sa, const float* __restrict__ sb, float smul,
                                                                 const bf16_t* __restrict__ bias, void* __restrict__ C, int M,
-                                                                int N, int K) {
-  fp8_gemm_v2_body<FA, FB, OUT_F32, 2, 4>(A, B, sa, sb, bias, C, M, N, K);
+                                                                int N, int K, int accum) {
+  fp8_gemm_v2_body<FA, FB, OUT_F32, 2, 4>(A, B, sa, sb, smul, bias, C, M, N, K, accum);
 }
 
 }  // namespace
@@ -383,45 +436,58 @@ torch::Tensor fp8_amax(torch::Tensor x, c10::optional<torch::Tensor> out) {
   return o;
 }
 
-torch::Tensor fp8_scale_from_amax(torch::Tensor amax, double fp8_max, double margin) {
-  // scale = fp8_max / amax / 2^margin (amax clamped away from 0), as device tensor ops (no host sync).
-  return (fp8_max / std::pow(2.0, margin)) / amax.clamp_min(1e-12);
-}
-
-std::vector<torch::Tensor> fp8_cast(torch::Tensor x, torch::Tensor scale, bool e5m2, bool transpose) {
+// scale = from_amax ? qmax / max(t, 1e-12) : t * qmax, read on the device (t: fp32 [1]).
+std::vector<torch::Tensor> fp8_cast(torch::Tensor x, torch::Tensor t, double qmax, bool from_amax, bool e5m2, bool transpose) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.dim() == 2, "fp8_cast: x must be 2-D contiguous bf16");
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.numel() >= 1, "fp8_cast: scale/amax must be a fp32 device tensor");
   const int M = x.size(0), N = x.size(1);
   auto dt = e5m2 ? at::kFloat8_e5m2 : at::kFloat8_e4m3fn;
   auto y = torch::empty({M, N}, x.options().dtype(dt));
   torch::Tensor yt;
   if (transpose) yt = torch::empty({N, M}, x.options().dtype(dt));
   if (M == 0 || N == 0) return transpose ? std::vector<torch::Tensor>{y, yt} : std::vector<torch::Tensor>{y};
-  dim3 grid((N + 63) / 64, (M + 63) / 64);
+  dim3 grid((N + kCT - 1) / kCT, (M + kCT - 1) / kCT);
   auto stream = at::hip::getCurrentHIPStream();
   uint8_t* yp = reinterpret_cast<uint8_t*>(y.data_ptr());
   uint8_t* ytp = transpose ? reinterpret_cast<uint8_t*>(yt.data_ptr()) : nullptr;
   const bf16_t* xp = reinterpret_cast<const bf16_t*>(x.data_ptr());
-  const float* sp = scale.data_ptr<float>();
+  const float* tp = t.data_ptr<float>();
+  const float q = (float)qmax;
+  const int fa = from_amax ? 1 : 0;
   if (e5m2) {
-    if (transpose) hipLaunchKernelGGL((cast_kernel<true, true>), grid, dim3(256), 0, stream, xp, sp, yp, ytp, M, N);
-    else hipLaunchKernelGGL((cast_kernel<true, false>), grid, dim3(256), 0, stream, xp, sp, yp, ytp, M, N);
+    if (transpose) hipLaunchKernelGGL((cast_kernel<true, true>), grid, dim3(256), 0, stream, xp, tp, q, fa, yp, ytp, M, N);
+    else hipLaunchKernelGGL((cast_kernel<true, false>), grid, dim3(256), 0, stream, xp, tp, q, fa, yp, ytp, M, N);
   } else {
-    if (transpose) hipLaunchKernelGGL((cast_kernel<false, true>), grid, dim3(256), 0, stream, xp, sp, yp, ytp, M, N);
-    else hipLaunchKernelGGL((cast_kernel<false, false>), grid, dim3(256), 0, stream, xp, sp, yp, ytp, M, N);
+    if (transpose) hipLaunchKernelGGL((cast_kernel<false, true>), grid, dim3(256), 0, stream, xp, tp, q, fa, yp, ytp, M, N);
+    else hipLaunchKernelGGL((cast_kernel<false, false>), grid, dim3(256), 0, stream, xp, tp, q, fa, yp, ytp, M, N);
   }
   if (transpose) return {y, yt};
   return {y};
 }
 
-torch::Tensor fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor a_scale_inv, torch::Tensor b_scale_inv, bool a_e5m2,
-                       bool b_e5m2, c10::optional<torch::Tensor> bias, bool out_fp32) {
+// C = (a . b^T) * sa[0] * sb[0] * smul (+ bias): sa / sb are inverse scales, or amax buffers with smul = 1/(qa*qb).
+// `out` (optional): write into this contiguous [M, N] tensor (fp32 when out_fp32, else bf16) instead of a new one, adding
+// to its contents when `accumulate` (the FSDP flat-grad / fp32 grad-shard destination of a weight gradient).
+torch::Tensor fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor a_scale_inv, torch::Tensor b_scale_inv, double smul,
+                       bool a_e5m2, bool b_e5m2, c10::optional<torch::Tensor> bias, bool out_fp32,
+                       c10::optional<torch::Tensor> out_opt, bool accumulate) {
   TORCH_CHECK(a.is_cuda() && b.is_cuda() && a.dim() == 2 && b.dim() == 2 && a.is_contiguous() && b.is_contiguous(),
               "fp8_gemm: operands must be 2-D contiguous HIP tensors");
   TORCH_CHECK(a.element_size() == 1 && b.element_size() == 1, "fp8_gemm: operands must be fp8");
   const int M = a.size(0), K = a.size(1), N = b.size(0);
   TORCH_CHECK(b.size(1) == K, "fp8_gemm: K mismatch");
   TORCH_CHECK(M % BM == 0 && N % BN == 0 && K % BK == 0, "fp8_gemm: M, N must be multiples of 128 and K of 64");
-  auto out = torch::empty({M, N}, a.options().dtype(out_fp32 ? torch::kFloat32 : torch::kBFloat16));
+  torch::Tensor out;
+  if (out_opt.has_value()) {
+    out = *out_opt;
+    TORCH_CHECK(out.is_cuda() && out.is_contiguous() && out.size(0) == M && out.size(1) == N &&
+                    out.scalar_type() == (out_fp32 ? torch::kFloat32 : torch::kBFloat16),
+                "fp8_gemm: out must be a contiguous [M, N] tensor of the output dtype");
+  } else {
+    TORCH_CHECK(!accumulate, "fp8_gemm: accumulate needs an out tensor");
+    out = torch::empty({M, N}, a.options().dtype(out_fp32 ? torch::kFloat32 : torch::kBFloat16));
+  }
+  const int accum = accumulate ? 1 : 0;
   const bf16_t* bp = nullptr;
   if (bias.has_value()) {
     TORCH_CHECK(bias->scalar_type() == at::kBFloat16 && bias->numel() == N, "fp8_gemm: bias must be bf16 [N]");
@@ -443,11 +509,11 @@ torch::Tensor fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor a_scale_i
 #define GEMM2_LAUNCH(FA, FB, OF)                                                                                      \
   do {                                                                                                                \
     if (w8)                                                                                                           \
-      hipLaunchKernelGGL((fp8_gemm_v2_w8_kernel<FA, FB, OF>), dim3(nwg2), dim3(512), 0, stream, ap, bptr, sap, sbp, bp, \
-                         cp, M, N, K);                                                                                \
+      hipLaunchKernelGGL((fp8_gemm_v2_w8_kernel<FA, FB, OF>), dim3(nwg2), dim3(512), 0, stream, ap, bptr, sap, sbp, (float)smul, bp, \
+                         cp, M, N, K, accum);                                                                                \
     else                                                                                                              \
-      hipLaunchKernelGGL((fp8_gemm_v2_w4_kernel<FA, FB, OF>), dim3(nwg2), dim3(256), 0, stream, ap, bptr, sap, sbp, bp, \
-                         cp, M, N, K);                                                                                \
+      hipLaunchKernelGGL((fp8_gemm_v2_w4_kernel<FA, FB, OF>), dim3(nwg2), dim3(256), 0, stream, ap, bptr, sap, sbp, (float)smul, bp, \
+                         cp, M, N, K, accum);                                                                                \
   } while (0)
     if (!a_e5m2 && !b_e5m2) { if (out_fp32) GEMM2_LAUNCH(0, 0, true); else GEMM2_LAUNCH(0, 0, false); }
     else if (!a_e5m2 && b_e5m2) { if (out_fp32) GEMM2_LAUNCH(0, 1, true); else GEMM2_LAUNCH(0, 1, false); }
@@ -458,7 +524,7 @@ torch::Tensor fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor a_scale_i
   }
   const int nwg = (M / BM) * (N / BN);
 #define GEMM_LAUNCH(FA, FB, OF) \
-  hipLaunchKernelGGL((fp8_gemm_kernel<FA, FB, OF>), dim3(nwg), dim3(256), 0, stream, ap, bptr, sap, sbp, bp, cp, M, N, K)
+  hipLaunchKernelGGL((fp8_gemm_kernel<FA, FB, OF>), dim3(nwg), dim3(256), 0, stream, ap, bptr, sap, sbp, (float)smul, bp, cp, M, N, K, accum)
   if (!a_e5m2 && !b_e5m2) { if (out_fp32) GEMM_LAUNCH(0, 0, true); else GEMM_LAUNCH(0, 0, false); }
   else if (!a_e5m2 && b_e5m2) { if (out_fp32) GEMM_LAUNCH(0, 1, true); else GEMM_LAUNCH(0, 1, false); }
   else if (a_e5m2 && !b_e5m2) { if (out_fp32) GEMM_LAUNCH(1, 0, true); else GEMM_LAUNCH(1, 0, false); }

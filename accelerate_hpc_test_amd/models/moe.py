@@ -106,11 +106,13 @@ class _GroupedExpertsFn(torch.autograd.Function):
         x, w_gu, w_down = ctx.saved_tensors
         dy = dy.contiguous()
         dx = torch.empty_like(x)
-        dw_gu = torch.zeros_like(w_gu)
-        dw_down = torch.zeros_like(w_down)
+        dw_gu = torch.empty_like(w_gu)  # every expert's slice is written below (zeroed when it got no tokens)
+        dw_down = torch.empty_like(w_down)
         off = 0
         for e, c in enumerate(ctx.counts):
             if c == 0:
+                dw_gu[e].zero_()
+                dw_down[e].zero_()
                 continue
             xe, dye = x[off : off + c], dy[off : off + c]
             if ctx.fp8:
@@ -137,13 +139,13 @@ def _fp8_expert_fwd(xe, w_gu, w_down, recipe, e):
     sgu = recipe.scale(f"wgu{e}", w_gu, E4M3_MAX)
     x8, x8t = cast(xp, sx, False, transpose=True)
     gu8, gu8t = cast(w_gu.contiguous(), sgu, False, transpose=True)
-    h = gemm(x8, gu8, 1.0 / sx, 1.0 / sgu, None, torch.bfloat16)  # [cp, 2I]; padded rows stay 0
+    h = gemm(x8, gu8, sx, sgu, None, torch.bfloat16)  # [cp, 2I]; padded rows stay 0
     a = _swiglu_fwd(h)
     sa = recipe.scale(f"a{e}", a, E4M3_MAX)
     sd = recipe.scale(f"wd{e}", w_down, E4M3_MAX)
     a8, a8t = cast(a, sa, False, transpose=True)
     d8, d8t = cast(w_down.contiguous(), sd, False, transpose=True)
-    yp = gemm(a8, d8, 1.0 / sa, 1.0 / sd, None, torch.bfloat16)
+    yp = gemm(a8, d8, sa, sd, None, torch.bfloat16)
     return yp[:c], (h, x8t, gu8t, a8t, d8t, sx, sgu, sa, sd)
 
 
@@ -157,13 +159,13 @@ def _fp8_expert_bwd(dye, st, recipe, e, dw_gu_e, dw_down_e):
     dyp = _pad_rows(dye.to(torch.bfloat16), cp)
     sg = recipe.scale(f"gy{e}", dyp, gmax)
     dy8, dy8t = cast(dyp, sg, e5, transpose=True)
-    dw_down_e.copy_(gemm(dy8t, a8t, 1.0 / sg, 1.0 / sa, None, torch.float32 if dw_down_e.dtype == torch.float32 else torch.bfloat16))
-    da = gemm(dy8, d8t, 1.0 / sg, 1.0 / sd, None, torch.bfloat16)  # [cp, I]
+    gemm(dy8t, a8t, sg, sa, None, out=dw_down_e)
+    da = gemm(dy8, d8t, sg, sd, None, torch.bfloat16)  # [cp, I]
     dh = _swiglu_bwd(h, da)  # [cp, 2I]
     sh = recipe.scale(f"gh{e}", dh, gmax)
     dh8, dh8t = cast(dh, sh, e5, transpose=True)
-    dw_gu_e.copy_(gemm(dh8t, x8t, 1.0 / sh, 1.0 / sx, None, torch.float32 if dw_gu_e.dtype == torch.float32 else torch.bfloat16))
-    return gemm(dh8, gu8t, 1.0 / sh, 1.0 / sgu, None, torch.bfloat16)[:c]
+    gemm(dh8t, x8t, sh, sx, None, out=dw_gu_e)
+    return gemm(dh8, gu8t, sh, sgu, None, torch.bfloat16)[:c]
 
 
 class MoEExperts(nn.Module):

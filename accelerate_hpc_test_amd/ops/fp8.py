@@ -18,7 +18,7 @@ The module filter follows the reference: first and last `nn.Linear` are skipped 
 
 from __future__ import annotations
 
-from typing import Callable, Optional
+from typing import Callable, NamedTuple, Optional
 
 import torch
 import torch.nn as nn
@@ -44,29 +44,68 @@ def scale_from_amax(a: torch.Tensor, fp8_max: float, margin: int = 0) -> torch.T
     return (fp8_max / (2.0**margin)) / a.clamp_min(1e-12)
 
 
-def cast(x: torch.Tensor, scale: torch.Tensor, e5m2: bool = False, transpose: bool = False):
-    """sat(x * scale) → fp8 (and its transpose when `transpose`)."""
+class Scale(NamedTuple):
+    """A per-tensor fp8 scale kept as (amax buffer, qmax = fp8_max / 2^margin): the cast kernel computes
+    qmax / amax and the GEMM epilogue amax / qmax on the device, so no scale arithmetic is launched separately."""
+
+    amax: torch.Tensor
+    qmax: float
+
+    def scale(self) -> torch.Tensor:
+        return self.qmax / self.amax.clamp_min(1e-12)
+
+    def inv(self) -> torch.Tensor:
+        return self.amax.clamp_min(1e-12) / self.qmax
+
+
+def cast(x: torch.Tensor, scale, e5m2: bool = False, transpose: bool = False):
+    """sat(x * scale) → fp8 (and its transpose when `transpose`). `scale` is a `Scale` or a plain fp32 [1] tensor."""
     if use_native(x) and x.dtype == torch.bfloat16 and x.dim() == 2:
-        outs = ext().fp8_cast(x.contiguous(), scale, e5m2, transpose)
+        if isinstance(scale, Scale):
+            outs = ext().fp8_cast(x.contiguous(), scale.amax, scale.qmax, True, e5m2, transpose)
+        else:
+            outs = ext().fp8_cast(x.contiguous(), scale.float().reshape(1), 1.0, False, e5m2, transpose)
         return (outs[0], outs[1]) if transpose else outs[0]
+    s = scale.scale() if isinstance(scale, Scale) else scale
     mx = E5M2_MAX if e5m2 else E4M3_MAX
     dt = torch.float8_e5m2 if e5m2 else torch.float8_e4m3fn
-    y = (x.float() * scale).clamp(-mx, mx).to(dt)
+    y = (x.float() * s).clamp(-mx, mx).to(dt)
     if transpose:
         return y, y.t().contiguous()
     return y
 
 
-def gemm(a8: torch.Tensor, b8: torch.Tensor, a_scale_inv: torch.Tensor, b_scale_inv: torch.Tensor, bias=None, out_dtype=torch.bfloat16):
-    """C = (a8 · b8ᵀ) · a_scale_inv · b_scale_inv (+ bias); a8 [M,K], b8 [N,K]."""
+def _inv_parts(si):
+    if isinstance(si, Scale):
+        return si.amax, 1.0 / si.qmax
+    return si.float().reshape(1), 1.0
+
+
+def gemm(a8: torch.Tensor, b8: torch.Tensor, a_scale_inv, b_scale_inv, bias=None, out_dtype=torch.bfloat16,
+         out: Optional[torch.Tensor] = None, accumulate: bool = False):
+    """C = (a8 · b8ᵀ) · a_scale_inv · b_scale_inv (+ bias); a8 [M,K], b8 [N,K]. Inverse scales are `Scale`s (the
+    operand's cast scale) or plain fp32 [1] tensors. With `out`, the result is written (or with `accumulate` added)
+    into that contiguous [M, N] tensor — e.g. a weight-gradient slot of the FSDP flat gradient buffer."""
+    if out is not None:
+        out_dtype = out.dtype
     if a8.is_cuda and use_native(a8):
         e5a = a8.dtype == torch.float8_e5m2
         e5b = b8.dtype == torch.float8_e5m2
-        return ext().fp8_gemm(a8, b8, a_scale_inv, b_scale_inv, e5a, e5b, bias, out_dtype == torch.float32)
-    out = (a8.float() @ b8.float().t()) * a_scale_inv * b_scale_inv
+        ta, ma = _inv_parts(a_scale_inv)
+        tb, mb = _inv_parts(b_scale_inv)
+        return ext().fp8_gemm(a8, b8, ta, tb, ma * mb, e5a, e5b, bias, out_dtype == torch.float32, out, accumulate)
+    ia = a_scale_inv.inv() if isinstance(a_scale_inv, Scale) else a_scale_inv
+    ib = b_scale_inv.inv() if isinstance(b_scale_inv, Scale) else b_scale_inv
+    res = (a8.float() @ b8.float().t()) * ia * ib
     if bias is not None:
-        out = out + bias.float()
-    return out.to(out_dtype)
+        res = res + bias.float()
+    if out is None:
+        return res.to(out_dtype)
+    if accumulate:
+        out.add_(res.to(out.dtype))
+    else:
+        out.copy_(res)
+    return out
 
 
 def _gemm_ok(M, N, K):
@@ -90,52 +129,62 @@ class Fp8Recipe:
     def fwd_e5m2(self):
         return self.fmt == "E5M2"
 
-    def scale(self, key: str, x: torch.Tensor, fp8_max: float) -> torch.Tensor:
+    def scale(self, key: str, x: torch.Tensor, fp8_max: float) -> Scale:
+        """Dynamic: this tensor's amax. Delayed: the history's max (or most recent), then the history is rolled."""
         cur = amax(x)
+        qmax = fp8_max / (2.0**self.margin)
         if not self.delayed:
-            return scale_from_amax(cur, fp8_max, self.margin)
+            return Scale(cur, qmax)
         h = self.hist.get(key)
         if h is None:
             h = cur.repeat(self.history_len).clone()
             self.hist[key] = h
         past = h.max().reshape(1) if self.algo == "max" else h[-1:].clone()
-        s = scale_from_amax(past, fp8_max, self.margin)
         self.hist[key] = torch.cat([h[1:], cur])
-        return s
+        return Scale(past, qmax)
 
 
 class _Fp8LinearFn(torch.autograd.Function):
+    """fp8 linear. With an FSDP `slot` (parallel/fsdp.py `_WgradSlot`) the weight-gradient GEMM writes straight into
+    the engine's gradient destination (fp32 grad shard at world size 1, the flat bf16 grad buffer otherwise) and
+    reports the parameter's gradient as ready — no separate dW tensor, no AccumulateGrad add."""
+
     @staticmethod
-    def forward(ctx, x, w, bias, recipe: Fp8Recipe):
+    def forward(ctx, x, w, bias, recipe: Fp8Recipe, slot=None):
         shape = x.shape
         x2 = x.reshape(-1, shape[-1])
-        M, K = x2.shape
         N = w.shape[0]
         fwd_max = E5M2_MAX if recipe.fwd_e5m2() else E4M3_MAX
         sx = recipe.scale("x", x2, fwd_max)
         sw = recipe.scale("w", w, fwd_max)
         x8, x8t = cast(x2, sx, recipe.fwd_e5m2(), transpose=True)
         w8, w8t = cast(w, sw, recipe.fwd_e5m2(), transpose=True)
-        y = gemm(x8, w8, 1.0 / sx, 1.0 / sw, bias, torch.bfloat16)
-        ctx.save_for_backward(x8t, w8t, sx, sw)
-        ctx.recipe = recipe
-        ctx.shape = shape
-        ctx.has_bias = bias is not None
+        y = gemm(x8, w8, sx, sw, bias, torch.bfloat16)
+        ctx.save_for_backward(x8t, w8t, sx.amax, sw.amax)
+        ctx.qmax = (sx.qmax, sw.qmax)
+        ctx.recipe, ctx.shape, ctx.has_bias, ctx.slot = recipe, shape, bias is not None, slot
         return y.view(*shape[:-1], N)
 
     @staticmethod
     def backward(ctx, dy):
-        x8t, w8t, sx, sw = ctx.saved_tensors
+        x8t, w8t, ax, aw = ctx.saved_tensors
+        sx, sw = Scale(ax, ctx.qmax[0]), Scale(aw, ctx.qmax[1])
         recipe = ctx.recipe
         N = dy.shape[-1]
         dy2 = dy.reshape(-1, N).contiguous().to(torch.bfloat16)
         gmax = E5M2_MAX if recipe.grad_e5m2() else E4M3_MAX
         sg = recipe.scale("g", dy2, gmax)
         dy8, dy8t = cast(dy2, sg, recipe.grad_e5m2(), transpose=True)
-        dx = gemm(dy8, w8t, 1.0 / sg, 1.0 / sw, None, torch.bfloat16)
-        dw = gemm(dy8t, x8t, 1.0 / sg, 1.0 / sx, None, torch.bfloat16)
+        dx = gemm(dy8, w8t, sg, sw, None, torch.bfloat16)
         db = dy2.float().sum(0).to(dy.dtype) if ctx.has_bias else None
-        return dx.view(ctx.shape), dw, db, None
+        slot = ctx.slot
+        if slot is not None:
+            dest, acc = slot.engine._fused_slot_dest(slot)
+            gemm(dy8t, x8t, sg, sx, None, out=dest, accumulate=acc)
+            slot.engine._fused_slot_done(slot)
+            return dx.view(ctx.shape), None, db, None, None
+        dw = gemm(dy8t, x8t, sg, sx, None, torch.bfloat16)
+        return dx.view(ctx.shape), dw, db, None, None
 
 
 _FP8_ON = [True]
@@ -169,7 +218,16 @@ class Fp8Linear(nn.Linear):
             return nn.functional.linear(x, self.weight.to(x.dtype), None if self.bias is None else self.bias.to(x.dtype))
         w = self.weight if self.weight.dtype == torch.bfloat16 else self.weight.to(torch.bfloat16)
         b = None if self.bias is None else self.bias.to(torch.bfloat16)
-        return _Fp8LinearFn.apply(x, w, b, self.fp8_recipe)
+        return _Fp8LinearFn.apply(x, w, b, self.fp8_recipe, self._fp8_wgrad_slot(x))
+
+    def _fp8_wgrad_slot(self, x):
+        """The FSDP fused-wgrad slot of this weight (parallel/fsdp.py), when the gradient can be written in place."""
+        slot = getattr(self.weight, "_acc_wgrad_slot", None)
+        if slot is None or not torch.is_grad_enabled() or self.weight.dtype != torch.bfloat16:
+            return None
+        if torch._C._current_graph_task_id() == -1:
+            slot.uses += 1
+        return slot
 
 
 def filter_linear_layers(module: nn.Module, fqn: str, layers_to_filter: list[str]) -> bool:
@@ -241,6 +299,6 @@ def has_fp8_layers(model: nn.Module) -> bool:
 
 def fp8_linear_reference_check(a: torch.Tensor, b: torch.Tensor):
     """Quantise a [M,K] and b [N,K] with dynamic per-tensor scaling and multiply in fp8 (test helper)."""
-    sa = scale_from_amax(amax(a), E4M3_MAX)
-    sb = scale_from_amax(amax(b), E4M3_MAX)
-    return gemm(cast(a, sa), cast(b, sb), 1.0 / sa, 1.0 / sb, None, torch.float32)
+    sa = Scale(amax(a), E4M3_MAX)
+    sb = Scale(amax(b), E4M3_MAX)
+    return gemm(cast(a, sa), cast(b, sb), sa, sb, None, torch.float32)

@@ -43,6 +43,7 @@ import torch.nn as nn
 from ..utils.dataclasses import FullyShardedDataParallelPlugin, MixedPrecisionPolicy
 from ..utils.fault_tolerance import record_collective
 from ..utils.tracing import trace_range
+from ..ops.fp8 import Fp8Linear
 
 _ALIGN = 64  # elements; keeps every rank's shard 128-B aligned for bf16 / 256-B for fp32
 
@@ -216,11 +217,13 @@ class FSDPEngine:
         for unit in self.units:
             for info in unit.infos:
                 m = info.module
-                if (type(m) is nn.Linear and info.attr == "weight" and info.param.requires_grad
+                plain = type(m) is nn.Linear
+                if ((plain or isinstance(m, Fp8Linear)) and info.attr == "weight" and info.param.requires_grad
                         and refs.get(id(info.param), 0) == 1 and getattr(info.param, "_tp_spec", None) is None):
                     info.fused = True
                     info.param._acc_wgrad_slot = _WgradSlot(self, unit, info)
-                    m.__class__ = _FusedWgradLinear
+                    if plain:  # Fp8Linear routes its fp8 weight-gradient GEMM to the slot itself (ops/fp8.py)
+                        m.__class__ = _FusedWgradLinear
 
     def _replace_param(self, info: _ParamInfo, new: nn.Parameter):
         """Swap a (meta) Parameter object for `new` in every module that registers it (tied weights included)."""
@@ -478,13 +481,28 @@ class FSDPEngine:
         info.fused_written = True
         return dest, acc
 
+    def _fused_slot_dest(self, slot: "_WgradSlot"):
+        """(destination view, accumulate?) for a weight-gradient GEMM that writes its result in place (the bf16 path
+        below, and the fp8 GEMM of ops/fp8.py)."""
+        unit = slot.unit
+        if unit.full_grad is None:
+            self._prepare_grad_buffer(unit)
+        return self._fused_dest(unit, slot.info)
+
+    def _fused_slot_done(self, slot: "_WgradSlot"):
+        """The slot's gradient for this backward is written: counts as the parameter's grad-ready event."""
+        unit = slot.unit
+        slot.uses -= 1
+        if slot.uses <= 0:
+            slot.uses = 0
+            unit.pending_grads -= 1
+            if unit.pending_grads == 0 and self.requires_grad_sync:
+                self._reduce_unit(unit)
+
     def _fused_wgrad(self, slot: "_WgradSlot", dy2: torch.Tensor, x2: torch.Tensor):
         """dW = dy2ᵀ · x2 written into the unit's flat grad buffer (or fp32 grad shard at world size 1); counts as the
         parameter's grad-ready event."""
-        unit, info = slot.unit, slot.info
-        if unit.full_grad is None:
-            self._prepare_grad_buffer(unit)
-        dest, acc = self._fused_dest(unit, info)
+        dest, acc = self._fused_slot_dest(slot)
         a, b = dy2.t(), x2
         if a.dtype != b.dtype:
             b = b.to(a.dtype)
@@ -495,12 +513,7 @@ class FSDPEngine:
         else:
             g = (a @ b).to(dest.dtype)
             dest.add_(g) if acc else dest.copy_(g)
-        slot.uses -= 1
-        if slot.uses <= 0:
-            slot.uses = 0
-            unit.pending_grads -= 1
-            if unit.pending_grads == 0 and self.requires_grad_sync:
-                self._reduce_unit(unit)
+        self._fused_slot_done(slot)
 
     def _make_grad_hook(self, unit: FlatUnit):
         def hook(param):

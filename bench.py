@@ -20,6 +20,7 @@ import time
 import torch
 
 BASELINE_TOKENS_PER_SEC_PER_DEVICE = 8000.0  # BASELINE.md P1 (8x H100, Llama-3.1-8B FSDP2 bf16)
+BASELINE_FP8_TOKENS_PER_SEC_PER_DEVICE = 10000.0  # BASELINE.md P2 (same, torchao fp8)
 
 
 def parse():
@@ -158,6 +159,7 @@ def main():
     flops_tok = cfg.flops_per_token(args.seq)
     peak = torch.cuda.max_memory_allocated() / 2**30
     headline = not is_moe and args.parallel == "fsdp"
+    base_dev = BASELINE_FP8_TOKENS_PER_SEC_PER_DEVICE if args.precision == "fp8" else BASELINE_TOKENS_PER_SEC_PER_DEVICE
     if accelerator.is_main_process:
         rec = {
             "metric": _metric_name(args, is_moe),
@@ -169,7 +171,7 @@ def main():
             "ms_per_step": round(ms, 2),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": round(tps / (BASELINE_TOKENS_PER_SEC_PER_DEVICE * world), 3) if headline else None,
+            "vs_baseline": round(tps / (base_dev * world), 3) if headline else None,
             "dtype": args.precision,
             "data": "synthetic (random token ids, random-init weights)",
             "config": {
@@ -185,7 +187,7 @@ def main():
             "tflops_per_gpu": round(flops_tok * tps / world / 1e12, 1),
             "peak_mem_gib": round(peak, 1),
             "final_loss": round(last_loss.item(), 4) if last_loss is not None else None,
-            "baseline_tokens_per_sec": BASELINE_TOKENS_PER_SEC_PER_DEVICE * world if headline else None,
+            "baseline_tokens_per_sec": base_dev * world if headline else None,
             "gemm_table": os.path.basename(gemm_table) if gemm_table else None,
         }
         print(json.dumps(rec), flush=True)

@@ -271,7 +271,83 @@ def test_moe_grouped_experts_fp8_matches_bf16():
         emu.append(q(a) @ q(ex.w_down[e]).t())
         off += c
     emu = torch.cat(emu)
-    assert _rel(res[1][0], emu) < 1e-2, _rel(res[1][0], emu)
+    # same quantisation; the residue is bf16 rounding of h / a flipping a few fp8 roundings (≈1 %)
+    assert _rel(res[1][0], emu) < 1.5e-2, _rel(res[1][0], emu)
     for name, ref, out, tol in zip(("y", "dx", "dw_gu", "dw_down"), res[0], res[1], (0.12, 0.15, 0.15, 0.15)):
         assert _rel(out, ref) < tol, (name, _rel(out, ref))
     assert res[1][2][1].abs().max() == 0 and res[1][3][1].abs().max() == 0
+
+
+@pytest.mark.parametrize("e5m2", [False, True])
+@pytest.mark.parametrize("M,N", [(256, 384), (320, 640), (1024, 4096)])
+def test_fp8_cast_matches_torch_and_transposes(M, N, e5m2):
+    """The 128²-tile cast kernel (and its edge-tile path) quantises exactly like torch and writes yᵀ; the scale comes
+    from the amax buffer on the device."""
+    from accelerate_hpc_test_amd.ops import fp8
+
+    torch.manual_seed(0)
+    x = torch.randn(M, N, device=DEV, dtype=torch.bfloat16) * 3
+    qmax = fp8.E5M2_MAX if e5m2 else fp8.E4M3_MAX
+    sc = fp8.Scale(fp8.amax(x), qmax)
+    y, yt = fp8.cast(x, sc, e5m2=e5m2, transpose=True)
+    dt = torch.float8_e5m2 if e5m2 else torch.float8_e4m3fn
+    ref = (x.float() * sc.scale()).clamp(-qmax, qmax).to(dt)
+    assert torch.equal(y.view(torch.uint8), ref.view(torch.uint8))
+    assert torch.equal(yt.view(torch.uint8), ref.t().contiguous().view(torch.uint8))
+
+
+def test_fp8_gemm_into_out_accumulates():
+    from accelerate_hpc_test_amd.ops import fp8
+
+    torch.manual_seed(0)
+    a = torch.randn(512, 256, device=DEV, dtype=torch.bfloat16)
+    b = torch.randn(256, 256, device=DEV, dtype=torch.bfloat16)
+    sa, sb = fp8.Scale(fp8.amax(a), fp8.E4M3_MAX), fp8.Scale(fp8.amax(b), fp8.E4M3_MAX)
+    a8, b8 = fp8.cast(a, sa), fp8.cast(b, sb)
+    fresh = fp8.gemm(a8, b8, sa, sb, out_dtype=torch.float32)
+    for dt in (torch.float32, torch.bfloat16):
+        base = torch.randn(512, 256, device=DEV).to(dt)
+        out = base.clone()
+        fp8.gemm(a8, b8, sa, sb, out=out, accumulate=True)
+        assert torch.allclose(out.float(), base.float() + fresh, rtol=2e-2, atol=2e-2)
+        fp8.gemm(a8, b8, sa, sb, out=out)
+        assert torch.allclose(out.float(), fresh, rtol=1e-2, atol=1e-2)
+    ref = a.float() @ b.float().t()
+    assert _rel(fresh, ref) < 6e-2
+
+
+def test_fp8_llama_fsdp_fused_wgrad_trains():
+    """mixed_precision='fp8' under the FSDP engine: Fp8Linear weight-gradient GEMMs write straight into the grad shard
+    (no dW tensor); the loss must fall and match the bf16 run's first-step loss closely."""
+    from accelerate_hpc_test_amd import Accelerator, FullyShardedDataParallelPlugin
+    from accelerate_hpc_test_amd.models.llama import LLAMA_PRESETS, LlamaForCausalLM
+    from accelerate_hpc_test_amd.state import AcceleratorState, GradientState
+
+    first = {}
+    for prec in ("bf16", "fp8"):
+        AcceleratorState._reset_state(True)
+        GradientState._reset_state()
+        plugin = FullyShardedDataParallelPlugin(fsdp_version=2, auto_wrap_policy="transformer_based_wrap",
+                                                transformer_cls_names_to_wrap=["LlamaDecoderLayer"])
+        acc = Accelerator(mixed_precision=prec, fsdp_plugin=plugin)
+        torch.manual_seed(0)
+        with torch.device("meta"):
+            model = LlamaForCausalLM(LLAMA_PRESETS["llama-tiny"])
+        opt = torch.optim.AdamW(model.parameters(), lr=3e-3)
+        model, opt = acc.prepare(model, opt)
+        ids = torch.randint(0, 512, (2, 256), generator=torch.Generator().manual_seed(1)).to(DEV)
+        losses = []
+        for _ in range(4):
+            out = model(ids, labels=ids)
+            acc.backward(out.loss)
+            opt.step()
+            opt.zero_grad()
+            losses.append(out.loss.item())
+        if prec == "fp8":
+            from accelerate_hpc_test_amd.ops.fp8 import Fp8Linear
+
+            fused = [m for m in acc.unwrap_model(model).modules() if isinstance(m, Fp8Linear) and hasattr(m.weight, "_acc_wgrad_slot")]
+            assert fused, "no Fp8Linear took the fused weight-gradient path"
+        assert all(l == l for l in losses) and losses[-1] < losses[0], (prec, losses)
+        first[prec] = losses[0]
+    assert abs(first["fp8"] - first["bf16"]) < 0.05 * abs(first["bf16"]), first
