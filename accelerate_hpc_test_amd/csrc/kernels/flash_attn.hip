@@ -79,6 +79,12 @@ __device__ __forceinline__ v8bf tr_frag(const char* img, int rb, int db, int lan
 
 __device__ __forceinline__ int acc_row(int i, int hf) { return (i & 3) + 8 * (i >> 2) + 4 * hf; }
 
+// Query head of workgroup x in a (Hq, S/128, B) grid. Workgroups are dealt round-robin over the 8 XCDs and the
+// linear id is x + Hq * (y + ...), so with Hq % 8 == 0 workgroup x runs on XCD x % 8. Mapping x to head
+// (x % 8) * (Hq / 8) + x / 8 (a bijection) puts Hq / 8 consecutive heads — one whole GQA group for Llama-3's 32 q /
+// 8 kv heads — on one XCD, whose L2 then serves the K/V tiles they share instead of four XCDs each fetching them.
+__device__ __forceinline__ int xcd_head(int x, int Hq) { return (Hq & 7) == 0 ? (x & 7) * (Hq >> 3) + (x >> 3) : x; }
+
 __device__ __forceinline__ v8bf pack8(const f32x16& x, int s) {
   v8bf r;
 #pragma unroll
@@ -129,7 +135,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(FwdParams p) {
   const int nqt = p.S / 128;
   // grid = (Hq, S/128, B): heads vary fastest, so the heaviest causal tiles of EVERY head are dispatched first
   const int qt = CAUSAL ? (nqt - 1 - (int)blockIdx.y) : (int)blockIdx.y;
-  const int h = blockIdx.x, b = blockIdx.z;
+  const int h = xcd_head(blockIdx.x, p.Hq), b = blockIdx.z;
   const int kh = h / (p.Hq / p.Hkv);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hf = lane >> 5;
   const int qw0 = qt * 128 + wave * 32;
@@ -171,32 +177,40 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(FwdParams p) {
 #pragma unroll
         for (int s = 0; s < 8; ++s) sc[kb] = mfma(row_frag(k_img, kb * 32 + r, 2 * s + hf), qf[s], sc[kb]);
       }
-      float mx = m;
+      // Only tiles that reach past the wave's first query need the mask (wave-uniform branch): the others skip
+      // the per-element compare/select.
+      if (CAUSAL && k0 + 63 > qw0) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if (k0 + kb * 32 + acc_row(i, hf) > qw0 + r) sc[kb][i] = -INFINITY;
+      }
+      // Max over the RAW scores (the positive scale commutes with max), then one fma per element feeds exp2:
+      // p = exp2(s * scale_log2 - m).
+      float mx = -INFINITY;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          float x = sc[kb][i] * p.scale_log2;
-          if (CAUSAL) {
-            const int key = k0 + kb * 32 + acc_row(i, hf);
-            if (key > qw0 + r) x = -INFINITY;
-          }
-          sc[kb][i] = x;
-          mx = fmaxf(mx, x);
-        }
+        for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sc[kb][i]);
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float alpha = fast_exp2(m - mx);
-      m = mx;
-      l *= alpha;
+      const float m_new = fmaxf(m, mx * p.scale_log2);
+      // Lazy rescale: once the running maxima settle, most tiles raise no lane's max and skip the O rescale.
+      if (__any(m_new > m)) {
+        const float alpha = fast_exp2(m - m_new);
+        l *= alpha;
 #pragma unroll
-      for (int d = 0; d < 4; ++d)
+        for (int d = 0; d < 4; ++d)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) o[d][i] *= alpha;
+          for (int i = 0; i < 16; ++i) o[d][i] *= alpha;
+      }
+      m = m_new;
+      const float neg_m = -m;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const float pv = fast_exp2(sc[kb][i] - m);
+          const float pv = fast_exp2(fmaf(sc[kb][i], p.scale_log2, neg_m));
           sc[kb][i] = pv;
           l += pv;
         }
@@ -267,7 +281,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(BwdParams p) {
   constexpr int kTile = 64 * kRow;
   const int nqt = p.S / 128;
   const int qt = CAUSAL ? (nqt - 1 - (int)blockIdx.y) : (int)blockIdx.y;  // grid (Hq, S/128, B), heavy first
-  const int h = blockIdx.x, b = blockIdx.z;
+  const int h = xcd_head(blockIdx.x, p.Hq), b = blockIdx.z;
   const int kh = h / (p.Hq / p.Hkv);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hf = lane >> 5;
   const int qw0 = qt * 128 + wave * 32;
