@@ -858,6 +858,8 @@ class Accelerator:
             optimizer.optimizer._accelerate_post_step = lambda _o=optimizer, _e=eng: _e.on_optimizer_step(
                 bool(getattr(_o.optimizer, "_acc_last_step_fused", False))
             )
+            if self.rccl_handler.fsdp_optimizer_overlap:
+                optimizer.enable_overlap(eng)
         self._optimizers.append(optimizer)
         return optimizer
 

@@ -79,7 +79,9 @@ class FusedAdamStep:
         self.adamw = isinstance(optimizer, torch.optim.AdamW)
 
     @torch.no_grad()
-    def step(self, grad_scale: Optional[torch.Tensor] = None):
+    def step(self, grad_scale: Optional[torch.Tensor] = None, only: Optional[set] = None, skip: Optional[set] = None):
+        """Update every param with a grad, or only those whose id() is in `only` / not in `skip` (the per-unit
+        updates of `fsdp_optimizer_overlap`, and the remainder at `optimizer.step()`)."""
         opt = self.optimizer
         e = ext()
         for group in opt.param_groups:
@@ -93,6 +95,8 @@ class FusedAdamStep:
             step_val = None
             for p in group["params"]:
                 if p.grad is None or p.numel() == 0:
+                    continue
+                if (only is not None and id(p) not in only) or (skip is not None and id(p) in skip):
                     continue
                 st = opt.state[p]
                 if len(st) == 0:

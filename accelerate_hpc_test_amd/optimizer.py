@@ -139,13 +139,36 @@ class AcceleratedOptimizer(torch.optim.Optimizer):
         if hasattr(self.optimizer, "eval") and callable(self.optimizer.eval):
             self.optimizer.eval()
 
+    # ---- optimizer / backward overlap (RcclKwargs.fsdp_optimizer_overlap) ---------------------------------------
+    def enable_overlap(self, engine) -> bool:
+        """Let the FSDP engine apply this optimizer unit by unit during backward (see
+        `FSDPEngine.attach_overlapped_optimizer`). Not with a GradScaler: fp16 overflow is only known at the end."""
+        if self.scaler is not None:
+            return False
+        self._overlap_engine = engine
+        engine.attach_overlapped_optimizer(self._step_subset)
+        return True
+
+    def _step_subset(self, params):
+        ids = {id(p) for p in params}
+        fused = self._maybe_fused()
+        if fused:
+            fused.step(only=ids)
+        else:
+            _step_filtered(self.optimizer, only=ids)
+
     def _inner_step(self, closure=None):
+        eng = getattr(self, "_overlap_engine", None)
+        done = eng.take_overlapped() if eng is not None else set()
         fused = self._maybe_fused()
         if fused and closure is None:
-            fused.step()
+            fused.step(skip=done or None)
             self.optimizer._acc_last_step_fused = True
         else:
-            self.optimizer.step(closure)
+            if done:
+                _step_filtered(self.optimizer, skip=done)
+            else:
+                self.optimizer.step(closure)
             self.optimizer._acc_last_step_fused = False
 
     def step(self, closure=None):
@@ -180,7 +203,8 @@ class AcceleratedOptimizer(torch.optim.Optimizer):
         return self._is_overflow
 
     def __getstate__(self):
-        _ignored_keys = ["_accelerate_step_called", "_optimizer_original_step_method", "_optimizer_patched_step_method", "_fused_step"]
+        _ignored_keys = ["_accelerate_step_called", "_optimizer_original_step_method", "_optimizer_patched_step_method", "_fused_step",
+                         "_overlap_engine"]
         return {k: v for k, v in self.__dict__.items() if k not in _ignored_keys}
 
     def __setstate__(self, state):
@@ -190,6 +214,19 @@ class AcceleratedOptimizer(torch.optim.Optimizer):
             self._accelerate_step_called = False
             self._optimizer_original_step_method = self.optimizer.step
             self._optimizer_patched_step_method = patch_optimizer_step(self, self.optimizer.step)
+
+
+def _step_filtered(optimizer, only=None, skip=None):
+    """`optimizer.step()` restricted to the params whose id() is in `only` / not in `skip` (any torch optimizer: the
+    param lists are narrowed for the call, per-param state is keyed by the param itself)."""
+    saved = [g["params"] for g in optimizer.param_groups]
+    try:
+        for g in optimizer.param_groups:
+            g["params"] = [p for p in g["params"] if (only is None or id(p) in only) and (skip is None or id(p) not in skip)]
+        optimizer.step()
+    finally:
+        for g, ps in zip(optimizer.param_groups, saved):
+            g["params"] = ps
 
 
 def patch_optimizer_step(accelerated_optimizer: AcceleratedOptimizer, method):

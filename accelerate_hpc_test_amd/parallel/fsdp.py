@@ -582,6 +582,7 @@ class FSDPEngine:
             unit.grad_valid = True
             self._release_grad(unit)
             self._expose_unit_grads(unit)
+            self._overlap_step(unit, torch.cuda.current_stream(self.device) if self.is_cuda else None)
             return
         src = unit.full_grad if unit.full_grad.dtype == self.reduce_dtype else unit.full_grad.to(self.reduce_dtype)
         out = torch.empty(unit.shard_numel, dtype=self.reduce_dtype, device=self.device)
@@ -597,8 +598,49 @@ class FSDPEngine:
         unit.grad_valid = True
         self._release_grad(unit)
         self._expose_unit_grads(unit)
+        self._overlap_step(unit, self.rs_stream)
         if not unit.is_root and self.world_size > 1:
             self._free_full(unit)  # block done with backward: drop its gathered params
+
+    # =========================================================================================== optimizer overlap
+    def attach_overlapped_optimizer(self, step_fn: Callable[[list], None]):
+        """Overlap the optimizer with the backward (`RcclKwargs.fsdp_optimizer_overlap`): `step_fn(shard_params)`
+        updates the given shard parameters and is called for each unit as soon as its gradient shard is final — on a
+        side HIP stream ordered after the stream that produced the gradient (reduce-scatter stream, or the compute
+        stream at world size 1). The update is memory-bound (fp32 master, grad, Adam moments, bf16 shadow) and the
+        backward GEMM/attention kernels are compute-bound, so the two share the CUs. A unit's weights are not read
+        again in this backward once its gradient is final, and the next all-gather / forward runs after
+        `take_overlapped()` has ordered the compute stream behind the side stream."""
+        self._overlap_fn = step_fn
+        self._overlap_done: set[int] = set()
+        if self.is_cuda and getattr(self, "opt_stream", None) is None:
+            self.opt_stream = torch.cuda.Stream(device=self.device)
+
+    def _overlap_step(self, unit: FlatUnit, src_stream):
+        fn = getattr(self, "_overlap_fn", None)
+        if fn is None or not self.requires_grad_sync:
+            return
+        params = [i.shard_param for i in unit.infos if i.shard_param.requires_grad and i.shard_param.grad is not None
+                  and id(i.shard_param) not in self._overlap_done]
+        if not params:
+            return
+        if self.is_cuda:
+            self.opt_stream.wait_stream(src_stream)
+            with torch.cuda.stream(self.opt_stream), trace_range(f"fsdp.optimizer_overlap[{unit.idx}]"):
+                fn(params)
+        else:
+            fn(params)
+        self._overlap_done.update(id(p) for p in params)
+
+    def take_overlapped(self) -> set:
+        """ids of the shard params already updated during this backward; orders the current stream after them."""
+        done = getattr(self, "_overlap_done", None)
+        if not done:
+            return set()
+        self._overlap_done = set()
+        if self.is_cuda:
+            torch.cuda.current_stream(self.device).wait_stream(self.opt_stream)
+        return done
 
     def _rs_and_accumulate(self, unit, src, out, first):
         W = self.world_size
@@ -734,6 +776,11 @@ class FSDPEngine:
 
         if norm_type != 2.0:
             raise NotImplementedError("Only the L2 norm is supported by the FSDP engine.")
+        if getattr(self, "_overlap_done", None):
+            raise RuntimeError(
+                "clip_grad_norm_ needs every gradient before any update, but `fsdp_optimizer_overlap` already applied the "
+                "optimizer to some units during backward. Disable RcclKwargs(fsdp_optimizer_overlap) to clip gradients."
+            )
         flat_params = []
         for unit in self.units:
             if unit.grad_valid:

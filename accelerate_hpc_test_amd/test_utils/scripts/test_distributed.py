@@ -150,6 +150,50 @@ def check_fsdp_matches_single(reshard: bool = True, state_dict_type: str = "SHAR
         assert torch.allclose(full3[n], q, atol=1e-5), (n, (full3[n] - q).abs().max())
 
 
+def check_fsdp_optimizer_overlap(grad_accum: int = 1):
+    """`RcclKwargs(fsdp_optimizer_overlap=True)`: the per-unit updates applied during backward must give exactly the
+    single-process AdamW trajectory (with a LR schedule and gradient accumulation), and clipping must refuse."""
+    from accelerate_hpc_test_amd.utils import RcclKwargs
+
+    plugin = FullyShardedDataParallelPlugin(fsdp_version=2, auto_wrap_policy="transformer_based_wrap", transformer_cls_names_to_wrap=["Block"])
+    acc = Accelerator(cpu=True, fsdp_plugin=plugin, gradient_accumulation_steps=grad_accum,
+                      kwargs_handlers=[RcclKwargs(fsdp_optimizer_overlap=True)])
+    W, r = acc.num_processes, acc.process_index
+    set_seed(0)
+    base = TinyMLP()
+    model = copy.deepcopy(base)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-2, weight_decay=0.01)
+    sched = torch.optim.lr_scheduler.LambdaLR(opt, lambda s: 1.0 / (1 + s))
+    base_opt = torch.optim.AdamW(base.parameters(), lr=1e-2, weight_decay=0.01)
+    base_sched = torch.optim.lr_scheduler.LambdaLR(base_opt, lambda s: 1.0 / (1 + s))
+    model, opt, sched = acc.prepare(model, opt, sched)
+    assert getattr(opt, "_overlap_engine", None) is not None
+    bs = 4
+    batches = _global_batches(3 * grad_accum, bs, W)
+    for i, (x, y) in enumerate(batches):
+        xl, yl = x[r * bs : (r + 1) * bs], y[r * bs : (r + 1) * bs]
+        with acc.accumulate(model):
+            acc.backward(F.mse_loss(model(xl), yl))
+            if acc.sync_gradients:
+                try:
+                    acc.clip_grad_norm_(model.parameters(), 1.0)
+                    raise AssertionError("clip_grad_norm_ must refuse after overlapped updates")
+                except RuntimeError:
+                    pass
+            opt.step()
+            sched.step()
+            opt.zero_grad()
+        (F.mse_loss(base(x), y) / grad_accum).backward()
+        if (i + 1) % grad_accum == 0:
+            base_opt.step()
+            for _ in range(W):  # AcceleratedScheduler steps num_processes times (split_batches=False)
+                base_sched.step()
+            base_opt.zero_grad()
+    full = acc.get_state_dict(model)
+    for n, q in base.named_parameters():
+        assert torch.allclose(full[n], q, atol=1e-5), (n, (full[n] - q).abs().max())
+
+
 def check_fsdp_no_sync_accumulation():
     plugin = FullyShardedDataParallelPlugin(fsdp_version=2, auto_wrap_policy="transformer_based_wrap", transformer_cls_names_to_wrap=["Block"])
     acc = Accelerator(cpu=True, fsdp_plugin=plugin, gradient_accumulation_steps=2)

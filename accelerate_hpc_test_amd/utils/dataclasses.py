@@ -298,6 +298,11 @@ class RcclKwargs(KwargsHandler):
       (utils/fault_tolerance.py); `ACCELERATE_WATCHDOG_TIMEOUT`; None = off.
     - `collective_check_interval`: in debug mode, compare every rank's collective-sequence digest each N backward
       passes (`ACCELERATE_COLLECTIVE_CHECK_INTERVAL`, default 50).
+    - `fsdp_optimizer_overlap`: run the optimizer update of each FSDP unit on a side HIP stream as soon as that unit's
+      gradient shard is final, overlapped with the rest of the backward; `optimizer.step()` then only updates what is
+      left and waits for the side stream (`ACCELERATE_FSDP_OPTIMIZER_OVERLAP`). Incompatible with gradient clipping
+      (the norm needs every gradient before any update: `clip_grad_norm_` raises) and with fp16 loss scaling (not
+      enabled then).
     """
 
     ddp_bucket_mb: int = None
@@ -305,6 +310,7 @@ class RcclKwargs(KwargsHandler):
     comm_stream_priority: int = None
     watchdog_timeout: float = None
     collective_check_interval: int = None
+    fsdp_optimizer_overlap: bool = None
 
     def __post_init__(self):
         if self.ddp_bucket_mb is None:
@@ -317,6 +323,8 @@ class RcclKwargs(KwargsHandler):
             self.watchdog_timeout = float(os.environ["ACCELERATE_WATCHDOG_TIMEOUT"])
         if self.collective_check_interval is None:
             self.collective_check_interval = int(os.environ.get("ACCELERATE_COLLECTIVE_CHECK_INTERVAL", 50))
+        if self.fsdp_optimizer_overlap is None:
+            self.fsdp_optimizer_overlap = parse_flag_from_env("ACCELERATE_FSDP_OPTIMIZER_OVERLAP", False)
 
 
 # ---------------------------------------------------------------------------------------------------

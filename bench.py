@@ -38,6 +38,10 @@ def parse():
     p.add_argument("--ddp-comm-hook", default="no", choices=["no", "bf16", "fp16"])
     p.add_argument("--activation-checkpointing", action="store_true")
     p.add_argument("--prefetch", type=int, default=1)
+    p.add_argument("--optimizer-overlap", default="on", choices=["on", "off"],
+                   help="on: each FSDP unit's AdamW update runs on a side HIP stream as soon as its gradient is final, "
+                        "overlapped with the rest of the backward (RcclKwargs.fsdp_optimizer_overlap); optimizer.step() "
+                        "still ends every step inside the timed region")
     p.add_argument("--verbose", action="store_true")
     p.add_argument("--gemm-tuning", default="auto", choices=["auto", "off", "tune"],
                    help="auto: load the committed hipBLASLt per-shape table (ops/tuned); tune: search and write it")
@@ -84,7 +88,8 @@ def main():
         reshard_after_forward=True,
         activation_checkpointing=args.activation_checkpointing,
     )
-    handlers = [RcclKwargs(fsdp_prefetch_depth=args.prefetch)]
+    overlap = args.optimizer_overlap == "on" and args.parallel == "fsdp"
+    handlers = [RcclKwargs(fsdp_prefetch_depth=args.prefetch, fsdp_optimizer_overlap=overlap)]
     if args.parallel == "ddp":
         from accelerate_hpc_test_amd.utils import DDPCommunicationHookType, DistributedDataParallelKwargs
 
@@ -180,7 +185,7 @@ def main():
                 "global_batch": args.mbs * world,
                 "seq_len": args.seq,
                 "parallelism": f"{args.parallel}{world}",
-                "optimizer": "AdamW(lr=1e-5), fp32 master",
+                "optimizer": "AdamW(lr=1e-5), fp32 master" + (", per-unit update overlapped with backward" if overlap else ""),
                 "activation_checkpointing": args.activation_checkpointing,
             },
             "tokens_per_sec_per_gpu": round(tps / world, 1),

@@ -351,3 +351,39 @@ def test_fp8_llama_fsdp_fused_wgrad_trains():
         assert all(l == l for l in losses) and losses[-1] < losses[0], (prec, losses)
         first[prec] = losses[0]
     assert abs(first["fp8"] - first["bf16"]) < 0.05 * abs(first["bf16"]), first
+
+
+def test_fsdp_optimizer_overlap_matches_plain_step():
+    """RcclKwargs(fsdp_optimizer_overlap=True): the fused AdamW runs per unit on a side stream during backward; the
+    parameters after a few steps must equal those of the plain end-of-step update bit for bit (same kernels, same
+    inputs, only the schedule differs)."""
+    from accelerate_hpc_test_amd import Accelerator, FullyShardedDataParallelPlugin
+    from accelerate_hpc_test_amd.models.llama import LLAMA_PRESETS, LlamaForCausalLM
+    from accelerate_hpc_test_amd.state import AcceleratorState, GradientState
+    from accelerate_hpc_test_amd.utils import RcclKwargs
+
+    finals = {}
+    for overlap in (False, True):
+        AcceleratorState._reset_state(True)
+        GradientState._reset_state()
+        plugin = FullyShardedDataParallelPlugin(fsdp_version=2, auto_wrap_policy="transformer_based_wrap",
+                                                transformer_cls_names_to_wrap=["LlamaDecoderLayer"])
+        acc = Accelerator(mixed_precision="bf16", fsdp_plugin=plugin, kwargs_handlers=[RcclKwargs(fsdp_optimizer_overlap=overlap)])
+        with torch.device("meta"):
+            model = LlamaForCausalLM(LLAMA_PRESETS["llama-tiny"])
+        opt = torch.optim.AdamW(model.parameters(), lr=3e-3)
+        model, opt = acc.prepare(model, opt)
+        assert (getattr(opt, "_overlap_engine", None) is not None) == overlap
+        ids = torch.randint(0, 512, (2, 256), generator=torch.Generator().manual_seed(1)).to(DEV)
+        losses = []
+        for _ in range(4):
+            out = model(ids, labels=ids)
+            acc.backward(out.loss)
+            opt.step()
+            opt.zero_grad()
+            losses.append(out.loss.item())
+        assert losses[-1] < losses[0], losses
+        finals[overlap] = (losses, acc.get_state_dict(model))
+    assert finals[False][0] == finals[True][0], (finals[False][0], finals[True][0])
+    for n, t in finals[False][1].items():
+        assert torch.equal(t, finals[True][1][n]), n

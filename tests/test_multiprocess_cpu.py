@@ -37,6 +37,11 @@ def test_fsdp_no_sync_accumulation(world):
     debug_launcher(td.check_fsdp_no_sync_accumulation, num_processes=world)
 
 
+@pytest.mark.parametrize("world,ga", [(1, 1), (2, 1), (2, 2)])
+def test_fsdp_optimizer_overlap_matches_single_process(world, ga):
+    debug_launcher(td.check_fsdp_optimizer_overlap, args=(ga,), num_processes=world)
+
+
 def test_fsdp_single_rank_matches_torch():
     """World size 1: fused weight grads go straight to the fp32 grad shard (no flat-buffer copy)."""
     debug_launcher(td.check_fsdp_matches_single, args=(True, "SHARDED_STATE_DICT"), num_processes=1)
