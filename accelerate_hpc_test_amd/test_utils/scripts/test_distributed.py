@@ -131,6 +131,18 @@ def check_fsdp_matches_single(reshard: bool = True, state_dict_type: str = "SHAR
     d = tempfile.mkdtemp() if r == 0 else None
     d = gather_object([d])[0]
     acc.save_state(d)
+    if state_dict_type == "SHARDED_STATE_DICT" and r == 0:
+        # `accelerate merge-weights`: the per-rank shard files merge into the full state dict (reference
+        # tests/test_merge_weights.py strategy)
+        from safetensors.torch import load_file
+
+        from accelerate_hpc_test_amd.utils import merge_fsdp_weights
+
+        merged = load_file(merge_fsdp_weights(os.path.join(d, "pytorch_model_fsdp_0"), os.path.join(d, "merged")))
+        assert set(merged) == set(full), (sorted(merged), sorted(full))
+        for n in full:
+            assert torch.equal(merged[n], full[n]), n
+    acc.wait_for_everyone()
     for p in model.parameters():
         p.data.add_(1.0)
     acc.load_state(d)
