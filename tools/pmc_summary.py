@@ -1,0 +1,52 @@
+"""Summarise `rocprofv3 --pmc ... --output-format csv` runs (tools/pmc_steps.sh) as a markdown table per kernel.
+
+    python tools/pmc_summary.py gpurun_out/pmc/attn gpurun_out/pmc/gemm
+
+Derived columns (MI355X: 256 CUs x 4 SIMDs, counters summed over the 8 XCDs):
+  * clock GHz      = GRBM_GUI_ACTIVE / 8 / kernel wall time
+  * MFMA busy %    = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 * 1024 SIMDs) - share of SIMD-cycles the matrix
+                     cores were busy
+  * LDS conflict % = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE - extra LDS-array cycles caused by bank conflicts
+"""
+
+import csv
+import glob
+import os
+import sys
+from collections import defaultdict
+
+
+def short(name: str) -> str:
+    name = name.replace("(anonymous namespace)::", "").replace("void ", "")
+    cut = name.find("(")
+    if cut > 0 and not name.startswith("Cijk") and not name.startswith("Custom"):
+        name = name[:cut]
+    return name[:72].replace("|", "/")
+
+
+def main(dirs):
+    for d in dirs:
+        files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+        ctr = defaultdict(lambda: defaultdict(float))
+        wall = defaultdict(dict)
+        for f in files:
+            for r in csv.DictReader(open(f)):
+                k = short(r["Kernel_Name"])
+                ctr[k][r["Counter_Name"]] += float(r["Counter_Value"])
+                wall[k][r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        print(f"### {d}\n")
+        print("| kernel | dispatches | wall ms | clock GHz | MFMA busy % | LDS instr (M) | LDS conflict % |")
+        print("|---|---:|---:|---:|---:|---:|---:|")
+        for k, c in sorted(ctr.items(), key=lambda kv: -kv[1].get("SQ_VALU_MFMA_BUSY_CYCLES", 0)):
+            grbm = c.get("GRBM_GUI_ACTIVE", 0) / 8
+            ns = sum(wall[k].values())
+            mfma = 100 * c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / (grbm * 1024) if grbm else 0
+            lds = c.get("SQ_LDS_IDX_ACTIVE", 0)
+            confl = 100 * c.get("SQ_LDS_BANK_CONFLICT", 0) / lds if lds else 0
+            clk = grbm / ns if ns else 0
+            print(f"| `{k}` | {len(wall[k])} | {ns / 1e6:.2f} | {clk:.2f} | {mfma:.1f} | {c.get('SQ_INSTS_LDS', 0) / 1e6:.1f} | {confl:.1f} |")
+        print()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])
