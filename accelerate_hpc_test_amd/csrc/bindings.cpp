@@ -35,6 +35,8 @@ torch::Tensor fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor a_scale_i
                        c10::optional<torch::Tensor> out, bool accumulate);
 // runtime/*.cpp
 void register_runtime(pybind11::module& m);
+bool blaslt_wgrad_f32(torch::Tensor dy, torch::Tensor x, torch::Tensor out, bool accumulate);
+std::vector<std::tuple<int64_t, int64_t, int64_t, int64_t, double>> blaslt_wgrad_plans();
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "MI355X (gfx950) native kernels and runtime for accelerate_hpc_test_amd";
@@ -57,4 +59,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("smul"), pybind11::arg("a_e5m2"), pybind11::arg("b_e5m2"), pybind11::arg("bias"), pybind11::arg("out_fp32"),
         pybind11::arg("out") = pybind11::none(), pybind11::arg("accumulate") = false);
   register_runtime(m);
+  m.def("blaslt_wgrad_f32", &blaslt_wgrad_f32);
+  m.def("blaslt_wgrad_plans", &blaslt_wgrad_plans);
 }

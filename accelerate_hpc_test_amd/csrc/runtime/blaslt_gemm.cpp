@@ -1,0 +1,148 @@
+// Weight-gradient GEMM with an fp32 destination, straight on hipBLASLt with per-shape algorithm search.
+//
+//   out[N, K] (+)= dy[T, N]^T . x[T, K]        dy, x: row-major bf16; out: row-major fp32 (the FSDP fp32 grad shard)
+//
+// Why: at FSDP world size 1 the weight gradients are written in fp32 directly into the grad shard (no bf16 buffer and
+// no bf16 -> fp32 pass). torch's `mm(..., out_dtype=float32)` reaches hipBLASLt through its default heuristic only
+// (TunableOp does not cover mixed-precision outputs) and lands on a depth-32 tile for these NT shapes. Here the first
+// call of each (T, N, K) asks hipBLASLt for its candidate algorithms, times them on a scratch output, and caches the
+// fastest; every later call is one hipblasLtMatmul on the current HIP stream. Column-major view used for the call:
+//   D (K x N, ld K) = X (K x T, ld K, op N) . DY^T (DY: N x T, ld N, op T), beta = accumulate ? 1 : 0.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <hip/hip_runtime.h>
+#include <hipblaslt/hipblaslt.h>
+
+#include <cstdlib>
+#include <map>
+#include <mutex>
+#include <tuple>
+#include <vector>
+
+namespace {
+
+constexpr size_t kWorkspace = size_t(64) << 20;
+
+struct Plan {
+  hipblasLtMatmulDesc_t desc = nullptr;
+  hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, lc = nullptr;
+  hipblasLtMatmulAlgo_t algo;
+  bool ok = false;
+  float ms = 0.f;
+  int candidates = 0;
+};
+
+struct State {
+  hipblasLtHandle_t handle = nullptr;
+  torch::Tensor workspace;
+  std::map<std::tuple<int64_t, int64_t, int64_t, int>, Plan> plans;
+  std::mutex mu;
+};
+
+State& state() {
+  static State s;
+  return s;
+}
+
+bool check(hipblasStatus_t st) { return st == HIPBLAS_STATUS_SUCCESS; }
+
+bool build_plan(State& s, Plan& p, int64_t T, int64_t N, int64_t K, hipStream_t stream, const torch::Tensor& like) {
+  const hipblasOperation_t ta = HIPBLAS_OP_N, tb = HIPBLAS_OP_T;
+  if (!check(hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F))) return false;
+  if (!check(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta)))) return false;
+  if (!check(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb)))) return false;
+  if (!check(hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16BF, K, T, K))) return false;
+  if (!check(hipblasLtMatrixLayoutCreate(&p.lb, HIP_R_16BF, N, T, N))) return false;
+  if (!check(hipblasLtMatrixLayoutCreate(&p.lc, HIP_R_32F, K, N, K))) return false;
+  hipblasLtMatmulPreference_t pref;
+  if (!check(hipblasLtMatmulPreferenceCreate(&pref))) return false;
+  uint64_t ws = kWorkspace;
+  hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &ws, sizeof(ws));
+  std::vector<hipblasLtMatmulHeuristicResult_t> res(32);
+  int got = 0;
+  const bool okh = check(hipblasLtMatmulAlgoGetHeuristic(s.handle, p.desc, p.la, p.lb, p.lc, p.lc, pref, (int)res.size(),
+                                                         res.data(), &got));
+  hipblasLtMatmulPreferenceDestroy(pref);
+  if (!okh || got <= 0) return false;
+  p.candidates = got;
+  // time every candidate on scratch operands of the real shape (beta = 0, so nothing real is touched)
+  auto a = torch::empty({T, K}, like.options().dtype(torch::kBFloat16)).normal_();
+  auto b = torch::empty({T, N}, like.options().dtype(torch::kBFloat16)).normal_();
+  auto d = torch::empty({N, K}, like.options().dtype(torch::kFloat32));
+  const float one = 1.f, zero = 0.f;
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  float best = 1e30f;
+  for (int i = 0; i < got; ++i) {
+    if (res[i].state != HIPBLAS_STATUS_SUCCESS || res[i].workspaceSize > kWorkspace) continue;
+    auto run = [&]() {
+      return hipblasLtMatmul(s.handle, p.desc, &one, a.data_ptr(), p.la, b.data_ptr(), p.lb, &zero, d.data_ptr(), p.lc,
+                             d.data_ptr(), p.lc, &res[i].algo, s.workspace.data_ptr(), kWorkspace, stream);
+    };
+    if (!check(run())) continue;
+    hipEventRecord(e0, stream);
+    for (int r = 0; r < 3; ++r) run();
+    hipEventRecord(e1, stream);
+    hipEventSynchronize(e1);
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, e0, e1);
+    if (ms < best) {
+      best = ms;
+      p.algo = res[i].algo;
+      p.ok = true;
+    }
+  }
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  p.ms = best / 3.f;
+  return p.ok;
+}
+
+}  // namespace
+
+// Returns false (and does nothing) when hipBLASLt offers no working algorithm: the caller falls back to torch.
+bool blaslt_wgrad_f32(torch::Tensor dy, torch::Tensor x, torch::Tensor out, bool accumulate) {
+  TORCH_CHECK(dy.is_cuda() && x.is_cuda() && out.is_cuda(), "blaslt_wgrad_f32: HIP tensors expected");
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16 && out.scalar_type() == at::kFloat,
+              "blaslt_wgrad_f32: bf16 operands and an fp32 output expected");
+  TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && out.dim() == 2 && dy.is_contiguous() && x.is_contiguous() && out.is_contiguous(),
+              "blaslt_wgrad_f32: 2-D contiguous tensors expected");
+  const int64_t T = dy.size(0), N = dy.size(1), K = x.size(1);
+  TORCH_CHECK(x.size(0) == T && out.size(0) == N && out.size(1) == K, "blaslt_wgrad_f32: shape mismatch");
+  State& s = state();
+  hipStream_t stream = at::hip::getCurrentHIPStream();
+  Plan* plan = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(s.mu);
+    if (s.handle == nullptr) {
+      if (!check(hipblasLtCreate(&s.handle))) return false;
+      s.workspace = torch::empty({(int64_t)kWorkspace}, out.options().dtype(torch::kUInt8));
+    }
+    const int dev = out.get_device();
+    auto key = std::make_tuple(T, N, K, dev);
+    auto it = s.plans.find(key);
+    if (it == s.plans.end()) {
+      Plan p;
+      build_plan(s, p, T, N, K, stream, out);
+      it = s.plans.emplace(key, p).first;
+    }
+    plan = &it->second;
+  }
+  if (!plan->ok) return false;
+  const float one = 1.f, beta = accumulate ? 1.f : 0.f;
+  return check(hipblasLtMatmul(s.handle, plan->desc, &one, x.data_ptr(), plan->la, dy.data_ptr(), plan->lb, &beta,
+                               out.data_ptr(), plan->lc, out.data_ptr(), plan->lc, &plan->algo, s.workspace.data_ptr(),
+                               kWorkspace, stream));
+}
+
+// [(T, N, K, candidates, best ms)] of every shape searched so far (diagnostics / bench logs).
+std::vector<std::tuple<int64_t, int64_t, int64_t, int64_t, double>> blaslt_wgrad_plans() {
+  std::vector<std::tuple<int64_t, int64_t, int64_t, int64_t, double>> out;
+  State& s = state();
+  std::lock_guard<std::mutex> lk(s.mu);
+  for (auto& kv : s.plans)
+    out.emplace_back(std::get<0>(kv.first), std::get<1>(kv.first), std::get<2>(kv.first), kv.second.candidates,
+                     kv.second.ok ? kv.second.ms : -1.0);
+  return out;
+}

@@ -43,9 +43,11 @@ import torch.nn as nn
 from ..utils.dataclasses import FullyShardedDataParallelPlugin, MixedPrecisionPolicy
 from ..utils.fault_tolerance import record_collective
 from ..utils.tracing import trace_range
+from ..ops._ext import ext
 from ..ops.fp8 import Fp8Linear
 
 _ALIGN = 64  # elements; keeps every rank's shard 128-B aligned for bf16 / 256-B for fp32
+_BLASLT_WGRAD = os.environ.get("ACCELERATE_BLASLT_WGRAD", "1") != "0"
 
 
 def _round_up(x, m):
@@ -509,7 +511,11 @@ class FSDPEngine:
         if dest.dtype == a.dtype:
             dest.addmm_(a, b) if acc else torch.mm(a, b, out=dest)
         elif dest.is_cuda and dest.dtype == torch.float32:
-            torch.addmm(dest, a, b, out_dtype=torch.float32, out=dest) if acc else torch.mm(a, b, out_dtype=torch.float32, out=dest)
+            # hipBLASLt with a per-shape algorithm search (csrc/runtime/blaslt_gemm.cpp); torch's fp32-output path
+            # only reaches hipBLASLt's default heuristic
+            if not (_BLASLT_WGRAD and a.dtype == torch.bfloat16 and dy2.is_contiguous() and x2.is_contiguous()
+                    and ext().blaslt_wgrad_f32(dy2, x2 if x2.dtype == a.dtype else b, dest, acc)):
+                torch.addmm(dest, a, b, out_dtype=torch.float32, out=dest) if acc else torch.mm(a, b, out_dtype=torch.float32, out=dest)
         else:
             g = (a @ b).to(dest.dtype)
             dest.add_(g) if acc else dest.copy_(g)

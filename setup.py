@@ -30,6 +30,7 @@ if os.environ.get("ACCELERATE_SKIP_NATIVE_BUILD", "0") != "1":
             name="accelerate_hpc_test_amd._C",
             sources=sources,
             include_dirs=[os.path.join(root, "kernels")],
+            libraries=["hipblaslt"],
             extra_compile_args={
                 "cxx": ["-O3", "-std=c++17"],
                 "nvcc": ["-O3", "-std=c++17", "--offload-arch=gfx950", "-munsafe-fp-atomics"],

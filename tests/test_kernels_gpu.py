@@ -387,3 +387,20 @@ def test_fsdp_optimizer_overlap_matches_plain_step():
     assert finals[False][0] == finals[True][0], (finals[False][0], finals[True][0])
     for n, t in finals[False][1].items():
         assert torch.equal(t, finals[True][1][n]), n
+
+
+@pytest.mark.parametrize("T,N,K", [(512, 384, 256), (1024, 768, 512)])
+def test_blaslt_wgrad_f32_matches_torch(T, N, K):
+    """csrc/runtime/blaslt_gemm.cpp: out (+)= dyᵀ·x in fp32 via hipBLASLt with a per-shape algorithm search."""
+    from accelerate_hpc_test_amd.ops._ext import ext
+
+    torch.manual_seed(0)
+    dy = torch.randn(T, N, device=DEV, dtype=torch.bfloat16)
+    x = torch.randn(T, K, device=DEV, dtype=torch.bfloat16)
+    ref = dy.float().t() @ x.float()
+    out = torch.empty(N, K, device=DEV, dtype=torch.float32)
+    assert ext().blaslt_wgrad_f32(dy, x, out, False)
+    assert _rel(out, ref) < 1e-3, _rel(out, ref)
+    assert ext().blaslt_wgrad_f32(dy, x, out, True)
+    assert _rel(out, 2 * ref) < 1e-3
+    assert any(p[:3] == (T, N, K) and p[4] > 0 for p in ext().blaslt_wgrad_plans())
