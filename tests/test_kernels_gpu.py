@@ -404,3 +404,19 @@ def test_blaslt_wgrad_f32_matches_torch(T, N, K):
     assert ext().blaslt_wgrad_f32(dy, x, out, True)
     assert _rel(out, 2 * ref) < 1e-3
     assert any(p[:3] == (T, N, K) and p[4] > 0 for p in ext().blaslt_wgrad_plans())
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp8"])
+def test_fsdp2_fp8_example_runs(precision):
+    """examples/torch_native_parallelism/fsdp2_fp8.py (the reference's headline script) on the toy Llama."""
+    import os
+    import sys
+
+    from accelerate_hpc_test_amd.state import AcceleratorState, GradientState
+
+    AcceleratorState._reset_state(True)
+    GradientState._reset_state()
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples", "torch_native_parallelism"))
+    import fsdp2_fp8
+
+    fsdp2_fp8.main(["--model", "llama-tiny", "--sequence-length", "256", "--num-steps", "4", "--precision", precision])
