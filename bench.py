@@ -38,7 +38,7 @@ def parse():
     p.add_argument("--ddp-comm-hook", default="no", choices=["no", "bf16", "fp16"])
     p.add_argument("--activation-checkpointing", action="store_true")
     p.add_argument("--prefetch", type=int, default=1)
-    p.add_argument("--optimizer-overlap", default="on", choices=["on", "off"],
+    p.add_argument("--optimizer-overlap", default="off", choices=["on", "off"],
                    help="on: each FSDP unit's AdamW update runs on a side HIP stream as soon as its gradient is final, "
                         "overlapped with the rest of the backward (RcclKwargs.fsdp_optimizer_overlap); optimizer.step() "
                         "still ends every step inside the timed region")
