@@ -26,7 +26,20 @@ __global__ void amax_kernel(const bf16_t* __restrict__ x, long n, unsigned int* 
   __shared__ float scratch[16];
   float m = 0.f;
   const long nvec = n >> 3;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  // four independent 16-B loads in flight per lane per iteration (a single dependent load per trip left the
+  // grid-stride loop latency-bound at ~3 TB/s)
+  for (; i + 3 * stride < nvec; i += 4 * stride) {
+    bf16x8 a[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) a[u] = reinterpret_cast<const bf16x8*>(x)[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(bf2f(a[u].v[j])));
+  }
+  for (; i < nvec; i += stride) {
     const bf16x8 a = reinterpret_cast<const bf16x8*>(x)[i];
 #pragma unroll
     for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(bf2f(a.v[j])));

@@ -420,3 +420,17 @@ def test_fsdp2_fp8_example_runs(precision):
     import fsdp2_fp8
 
     fsdp2_fp8.main(["--model", "llama-tiny", "--sequence-length", "256", "--num-steps", "4", "--precision", precision])
+
+
+@pytest.mark.parametrize("n", [1000003, 8 * 256 * 2048 * 5 + 13])
+def test_fp8_amax_large_and_ragged(n):
+    """amax over sizes that exercise the 4-deep unrolled grid-stride loop, its remainder loop and the scalar tail."""
+    from accelerate_hpc_test_amd.ops import fp8
+
+    torch.manual_seed(0)
+    x = torch.randn(n, device=DEV, dtype=torch.bfloat16)
+    for pos in (0, n // 3, n - 1):
+        y = x.clone()
+        y[pos] = -1000.0
+        assert fp8.amax(y).item() == 1000.0, pos
+    assert fp8.amax(x).item() == x.float().abs().max().item()
