@@ -7,6 +7,7 @@ std::vector<torch::Tensor> rmsnorm_fwd(torch::Tensor x, c10::optional<torch::Ten
 std::vector<torch::Tensor> rmsnorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor w, torch::Tensor rstd,
                                        c10::optional<torch::Tensor> dres);
 torch::Tensor swiglu_fwd(torch::Tensor gu);
+torch::Tensor transpose_bf16(torch::Tensor x);
 torch::Tensor swiglu_bwd(torch::Tensor gu, torch::Tensor dh);
 void rope_inplace(torch::Tensor qkv, torch::Tensor cos, torch::Tensor sin, c10::optional<torch::Tensor> pos,
                   int64_t n_rot_heads, int64_t n_heads_total, int64_t head_dim, double sign);
@@ -43,6 +44,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rmsnorm_fwd", &rmsnorm_fwd);
   m.def("rmsnorm_bwd", &rmsnorm_bwd);
   m.def("swiglu_fwd", &swiglu_fwd);
+  m.def("transpose_bf16", &transpose_bf16);
   m.def("swiglu_bwd", &swiglu_bwd);
   m.def("rope_inplace", &rope_inplace);
   m.def("xent_fwd", &xent_fwd);

@@ -363,3 +363,42 @@ void rope_inplace(torch::Tensor qkv, torch::Tensor cos, torch::Tensor sin, c10::
                      reinterpret_cast<bf16_t*>(qkv.data_ptr()), cos.data_ptr<float>(), sin.data_ptr<float>(), posp, T,
                      S, (int)n_rot_heads, (int)n_heads_total, (int)head_dim, (float)sign);
 }
+
+// ------------------------------------------------------------------------------------------------ transpose
+// out[c, r] = in[r, c] for a row-major bf16 [R, C] with R, C multiples of 64: 64x64 tile per 256-thread workgroup,
+// 16-B global loads and stores on both sides, the turn done through a padded LDS tile (row pitch 72 elements).
+// Used to hand the weight-gradient GEMM a token-contiguous copy of the layer input (parallel/fsdp.py), which moves
+// that GEMM from the slow both-token-major layout to the dgrad-class layout.
+namespace {
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16_t* __restrict__ in, bf16_t* __restrict__ out, int R,
+                                                             int C) {
+  __shared__ __attribute__((aligned(16))) bf16_t tile[64][72];
+  const int tr = blockIdx.y * 64, tc = blockIdx.x * 64, tid = threadIdx.x, ch = tid & 7;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int row = (tid >> 3) + 32 * p;
+    *reinterpret_cast<bf16x8*>(&tile[row][ch * 8]) = *reinterpret_cast<const bf16x8*>(in + (long)(tr + row) * C + tc + ch * 8);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int c = (tid >> 3) + 32 * p;
+    bf16x8 w;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w.v[j] = tile[ch * 8 + j][c];
+    *reinterpret_cast<bf16x8*>(out + (long)(tc + c) * R + tr + ch * 8) = w;
+  }
+}
+}  // namespace
+
+torch::Tensor transpose_bf16(torch::Tensor x) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.is_contiguous(),
+              "transpose_bf16: 2-D contiguous bf16 HIP tensor expected");
+  const int R = x.size(0), C = x.size(1);
+  TORCH_CHECK(R % 64 == 0 && C % 64 == 0, "transpose_bf16: both dims must be multiples of 64");
+  auto out = torch::empty({C, R}, x.options());
+  if (R == 0 || C == 0) return out;
+  hipLaunchKernelGGL(transpose_bf16_kernel, dim3(C / 64, R / 64), dim3(256), 0, at::hip::getCurrentHIPStream(),
+                     reinterpret_cast<const bf16_t*>(x.data_ptr()), reinterpret_cast<bf16_t*>(out.data_ptr()), R, C);
+  return out;
+}

@@ -434,3 +434,40 @@ def test_fp8_amax_large_and_ragged(n):
         y[pos] = -1000.0
         assert fp8.amax(y).item() == 1000.0, pos
     assert fp8.amax(x).item() == x.float().abs().max().item()
+
+
+def test_transpose_bf16_matches_torch():
+    from accelerate_hpc_test_amd.ops._ext import ext
+
+    x = torch.randn(8192 + 64, 448, device=DEV, dtype=torch.bfloat16)
+    assert torch.equal(ext().transpose_bf16(x), x.t().contiguous())
+
+
+def test_fsdp_wgrad_from_transposed_input_matches(monkeypatch):
+    """World size 1, fp32-direct weight gradients computed from the saved token-contiguous xᵀ (default) vs from x:
+    same parameters after two AdamW steps up to fp32 summation order."""
+    from accelerate_hpc_test_amd import Accelerator, FullyShardedDataParallelPlugin
+    from accelerate_hpc_test_amd.models.llama import LLAMA_PRESETS, LlamaForCausalLM
+    from accelerate_hpc_test_amd.parallel import fsdp as fsdp_mod
+    from accelerate_hpc_test_amd.state import AcceleratorState, GradientState
+
+    finals = {}
+    for xt in (True, False):
+        monkeypatch.setattr(fsdp_mod, "_WGRAD_XT", xt)
+        AcceleratorState._reset_state(True)
+        GradientState._reset_state()
+        plugin = FullyShardedDataParallelPlugin(fsdp_version=2, auto_wrap_policy="transformer_based_wrap",
+                                                transformer_cls_names_to_wrap=["LlamaDecoderLayer"])
+        acc = Accelerator(mixed_precision="bf16", fsdp_plugin=plugin)
+        with torch.device("meta"):
+            model = LlamaForCausalLM(LLAMA_PRESETS["llama-tiny"])
+        opt = torch.optim.AdamW(model.parameters(), lr=1e-3)
+        model, opt = acc.prepare(model, opt)
+        ids = torch.randint(0, 512, (2, 256), generator=torch.Generator().manual_seed(1)).to(DEV)
+        for _ in range(2):
+            acc.backward(model(ids, labels=ids).loss)
+            opt.step()
+            opt.zero_grad()
+        finals[xt] = acc.get_state_dict(model)
+    for n, t in finals[False].items():
+        assert torch.allclose(t, finals[True][n], atol=2e-4, rtol=1e-3), (n, (t - finals[True][n]).abs().max())
