@@ -1037,11 +1037,12 @@ class _FusedWgradLinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, slot):
         x2 = x.reshape(-1, x.shape[-1])
-        # fp32-direct weight gradients (world size 1): keep a token-contiguous copy xᵀ instead of x. dW = dyᵀ·x then
-        # runs in the dgrad-class layout (one operand contiguous along the contraction) instead of the both-token-major
-        # one: measured 2.93 vs 3.50 ms per Llama-3-8B layer for the four GEMMs, the HIP transpose costs ~0.2 ms.
+        # Keep a token-contiguous copy xᵀ instead of x: dW = dyᵀ·x then runs in the dgrad-class layout (one operand
+        # contiguous along the contraction) instead of the both-token-major one. Llama-3-8B layer, four GEMMs
+        # (tools/bench_wgrad_layout.py): fp32 output (world size 1) 2.93 vs 3.50 ms, bf16 output (flat grad buffer,
+        # world size > 1) 2.86 vs 3.44 ms; the HIP transpose costs ~0.2 ms.
         ctx.x_transposed = (_WGRAD_XT and x2.is_cuda and x2.dtype == torch.bfloat16 and x2.is_contiguous()
-                            and x2.shape[0] % 64 == 0 and x2.shape[1] % 64 == 0 and slot.engine._direct_grads())
+                            and x2.shape[0] % 64 == 0 and x2.shape[1] % 64 == 0)
         ctx.save_for_backward(ext().transpose_bf16(x2) if ctx.x_transposed else x, weight)
         ctx.slot = slot
         ctx.has_bias = bias is not None

@@ -443,9 +443,13 @@ def test_transpose_bf16_matches_torch():
     assert torch.equal(ext().transpose_bf16(x), x.t().contiguous())
 
 
-def test_fsdp_wgrad_from_transposed_input_matches(monkeypatch):
-    """World size 1, fp32-direct weight gradients computed from the saved token-contiguous xᵀ (default) vs from x:
-    same parameters after two AdamW steps up to fp32 summation order."""
+@pytest.mark.parametrize("direct", [True, False])
+def test_fsdp_wgrad_from_transposed_input_matches(monkeypatch, direct):
+    """Weight gradients computed from the saved token-contiguous xᵀ (default) vs from x — fp32-direct grad shard
+    (world size 1) and the bf16 flat-buffer path used at world size > 1 (forced here with ACCELERATE_FSDP_WGRAD_FP32=0):
+    same parameters after two AdamW steps up to summation order."""
+    if not direct:
+        monkeypatch.setenv("ACCELERATE_FSDP_WGRAD_FP32", "0")
     from accelerate_hpc_test_amd import Accelerator, FullyShardedDataParallelPlugin
     from accelerate_hpc_test_amd.models.llama import LLAMA_PRESETS, LlamaForCausalLM
     from accelerate_hpc_test_amd.parallel import fsdp as fsdp_mod
