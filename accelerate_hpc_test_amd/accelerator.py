@@ -811,6 +811,7 @@ class Accelerator:
             replicate_group=replicate_group,
             init_fn=init_fn,
             prefetch_depth=self.rccl_handler.fsdp_prefetch_depth,
+            force_sharded=self.rccl_handler.fsdp_force_sharded,
         )
         self._fsdp_engines.append(wrapped.engine)
         return wrapped

@@ -34,6 +34,8 @@ std::vector<torch::Tensor> fp8_cast(torch::Tensor x, torch::Tensor t, double qma
 torch::Tensor fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor a_scale_inv, torch::Tensor b_scale_inv,
                        double smul, bool a_e5m2, bool b_e5m2, c10::optional<torch::Tensor> bias, bool out_fp32,
                        c10::optional<torch::Tensor> out, bool accumulate);
+// comm_pack.hip
+void grad_shard_update(torch::Tensor dst, torch::Tensor src, double scale, bool accumulate);
 // runtime/*.cpp
 void register_runtime(pybind11::module& m);
 bool blaslt_wgrad_f32(torch::Tensor dy, torch::Tensor x, torch::Tensor out, bool accumulate);
@@ -60,6 +62,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fp8_gemm", &fp8_gemm, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("a_scale_inv"), pybind11::arg("b_scale_inv"),
         pybind11::arg("smul"), pybind11::arg("a_e5m2"), pybind11::arg("b_e5m2"), pybind11::arg("bias"), pybind11::arg("out_fp32"),
         pybind11::arg("out") = pybind11::none(), pybind11::arg("accumulate") = false);
+  m.def("grad_shard_update", &grad_shard_update);
   register_runtime(m);
   m.def("blaslt_wgrad_f32", &blaslt_wgrad_f32);
   m.def("blaslt_wgrad_plans", &blaslt_wgrad_plans);

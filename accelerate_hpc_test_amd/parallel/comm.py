@@ -26,6 +26,28 @@ def _is_gloo(group) -> bool:
     return dist.get_backend(group) == "gloo"
 
 
+def duplicate_group(group=None):
+    """A new process group over exactly the ranks of `group`, i.e. a separate RCCL communicator.
+
+    Each purpose that issues collectives from its own HIP stream (FSDP all-gather, FSDP reduce-scatter, DDP bucket
+    all-reduce) gets one: a synchronous collective runs on the issuing stream, and one communicator must not be driven
+    from two streams at once, so separate communicators are what lets those streams really overlap. `new_group` has to
+    be entered by every rank of the world for every group created, so the member lists of all ranks are exchanged
+    first and each distinct list is created, in the same order everywhere (HSDP / mesh sub-groups included)."""
+    ranks = tuple(dist.get_process_group_ranks(group if group is not None else dist.group.WORLD))
+    world = dist.get_world_size()
+    if world == 1:
+        return dist.new_group([0])
+    lists = [None] * world
+    dist.all_gather_object(lists, ranks)
+    mine = None
+    for rl in sorted(set(tuple(r) for r in lists)):
+        g = dist.new_group(list(rl))
+        if rl == ranks:
+            mine = g
+    return mine
+
+
 # ------------------------------------------------------------------------------------------------ raw collectives
 def all_reduce_(t: torch.Tensor, group=None, op=dist.ReduceOp.SUM) -> torch.Tensor:
     if group_size(group) > 1:

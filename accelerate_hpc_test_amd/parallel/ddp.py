@@ -9,10 +9,12 @@ with kwargs from `DistributedDataParallelKwargs` (`utils/dataclasses.py:154-237`
 * Buckets are filled in reverse registration order (≈ the order gradients become ready) up to
   `bucket_cap_mb` — by default 128 MB (16 MB per peer at 8 GPUs) so each RCCL all-reduce is large enough to drive
   all 7 xGMI links, instead of torch's 25 MB.
-* A bucket's all-reduce is launched from a post-accumulate-grad hook as soon as its last gradient lands, on a
-  dedicated high-priority HIP stream (overlapping the rest of backward); an autograd final callback flushes the
-  remaining buckets (this also covers `find_unused_parameters`) and orders the compute stream after the comm
-  stream — no host blocking.
+* Bucket all-reduces are launched from post-accumulate-grad hooks strictly in bucket-index order (a ready bucket
+  waits until every lower-index bucket has launched, like torch's `next_bucket_`), on a dedicated high-priority HIP
+  stream and a communicator of its own (overlapping the rest of backward). An autograd final callback flushes the
+  remaining buckets in the same order — this covers `find_unused_parameters` even when ranks leave DIFFERENT
+  parameters unused (MoE experts, data-dependent branches): every rank issues the same collective sequence — and
+  orders the compute stream after the comm stream, with no host blocking.
 * Communication hooks: `bf16`/`fp16` compression casts the bucket once, all-reduces in 16-bit and casts back;
   averaging (1/W) is folded into that pass (or done with ReduceOp.AVG on RCCL).
 * `no_sync()` skips the launches (grads keep accumulating in the buckets); `broadcast_buffers` re-broadcasts
@@ -91,6 +93,14 @@ class DistributedDataParallel(nn.Module):
             bucket_bytes = int((bucket_cap_mb if bucket_cap_mb is not None else 128) * (1 << 20))
         self.bucket_bytes = bucket_bytes
         self.comm_stream = torch.cuda.Stream(device=self.device, priority=-1) if self.is_cuda else None
+        # bucket all-reduces run on comm_stream through their own communicator (parallel/comm.duplicate_group), so
+        # they never share an RCCL communicator with collectives issued from other streams
+        self.comm_group = process_group
+        if self.is_cuda and not self.is_gloo and self.world_size > 1:
+            from .comm import duplicate_group
+
+            self.comm_group = duplicate_group(process_group)
+        self._next_bucket = 0
         self._cb_queued = False
         self._sync_params_and_buffers()
         self._build_buckets()
@@ -170,6 +180,7 @@ class DistributedDataParallel(nn.Module):
         for b in self.buckets:
             b.pending = len(b.params)
             b.launched = False
+        self._next_bucket = 0
         if torch.is_grad_enabled():
             self._sync_pending = self.require_backward_grad_sync
         return self.module(*inputs, **kwargs)
@@ -193,7 +204,13 @@ class DistributedDataParallel(nn.Module):
         join = getattr(self, "_join", None)
         deferred = join is not None and join["active"] < self.world_size  # joined ranks shadow in bucket order
         if b.pending == 0 and self._sync_pending and not deferred:
-            self._launch(b)
+            self._launch_ready()
+
+    def _launch_ready(self):
+        """Launch the ready buckets at the front of the index order (never out of order)."""
+        while self._next_bucket < len(self.buckets) and self.buckets[self._next_bucket].pending == 0:
+            self._launch(self.buckets[self._next_bucket])
+            self._next_bucket += 1
 
     def _slot(self, b, p):
         i = next(j for j, q in enumerate(b.params) if q is p)
@@ -222,6 +239,7 @@ class DistributedDataParallel(nn.Module):
 
     def _allreduce_buffer(self, buf, key: int = 0):
         W = self.world_size
+        group = self.comm_group
         record_collective("ddp_all_reduce", buf, self.process_group)
         if self.comm_hook in (DDPCommunicationHookType.POWER_SGD, DDPCommunicationHookType.BATCHED_POWER_SGD) and buf.dtype.is_floating_point:
             self._powersgd(buf, key)
@@ -229,14 +247,14 @@ class DistributedDataParallel(nn.Module):
         if self.comm_hook in (DDPCommunicationHookType.BF16, DDPCommunicationHookType.FP16) and buf.dtype == torch.float32:
             dt = torch.bfloat16 if self.comm_hook == DDPCommunicationHookType.BF16 else torch.float16
             tmp = buf.to(dt).div_(W)
-            dist.all_reduce(tmp, group=self.process_group)
+            dist.all_reduce(tmp, group=group)
             buf.copy_(tmp)
             return
         if self.is_gloo:
-            dist.all_reduce(buf, group=self.process_group)
+            dist.all_reduce(buf, group=group)
             buf.div_(W)
         else:
-            dist.all_reduce(buf, op=dist.ReduceOp.AVG, group=self.process_group)
+            dist.all_reduce(buf, op=dist.ReduceOp.AVG, group=group)
 
     @torch.no_grad()
     def _powersgd(self, buf, key: int):
@@ -256,12 +274,13 @@ class DistributedDataParallel(nn.Module):
         m = max(1, int(n_el ** 0.5))
         n = -(-n_el // m)
         compressible = (n * m) / max(1, r * (n + m)) >= min_rate
+        group = self.comm_group
         if st["iter"] <= start_iter or not compressible:
             if self.is_gloo:
-                dist.all_reduce(buf, group=self.process_group)
+                dist.all_reduce(buf, group=group)
                 buf.div_(W)
             else:
-                dist.all_reduce(buf, op=dist.ReduceOp.AVG, group=self.process_group)
+                dist.all_reduce(buf, op=dist.ReduceOp.AVG, group=group)
             return
         M = torch.zeros(n * m, dtype=torch.float32, device=buf.device)
         M[:n_el] = buf.float()
@@ -276,10 +295,10 @@ class DistributedDataParallel(nn.Module):
             g = torch.Generator(device="cpu").manual_seed(int(opt.get("random_seed", 0)) + key)
             Q = torch.randn(m, r, generator=g).to(buf.device)
         P = M @ Q
-        dist.all_reduce(P, group=self.process_group)
+        dist.all_reduce(P, group=group)
         P, _ = torch.linalg.qr(P)
         Q = M.t() @ P
-        dist.all_reduce(Q, group=self.process_group)
+        dist.all_reduce(Q, group=group)
         Q.div_(W)
         approx = P @ Q.t()
         if opt.get("use_error_feedback", True):
@@ -290,9 +309,9 @@ class DistributedDataParallel(nn.Module):
     def _finalize(self):
         self._cb_queued = False
         if self._sync_pending:
-            for b in self.buckets:
-                if not b.launched:
-                    self._launch(b)
+            for b in self.buckets[self._next_bucket :]:  # unused params never fired: flush the rest in index order
+                self._launch(b)
+            self._next_bucket = len(self.buckets)
             if self.is_cuda:
                 torch.cuda.current_stream(self.device).wait_stream(self.comm_stream)
 

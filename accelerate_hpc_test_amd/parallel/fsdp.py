@@ -121,6 +121,7 @@ class FSDPEngine:
         init_fn: Optional[Callable[[nn.Module], None]] = None,
         seed: int = 0,
         prefetch_depth: int = 1,
+        force_sharded: bool = False,
     ):
         self.model = model
         self.plugin = plugin
@@ -133,11 +134,16 @@ class FSDPEngine:
         else:
             self.world_size, self.rank = 1, 0
         self.replicate_size = dist.get_world_size(replicate_group) if replicate_group is not None else 1
+        # `sharded`: the unit buffers are sharded and every collective of the W>1 path runs. At world size 1 this is the
+        # degenerate no-collective path unless `force_sharded` (RcclKwargs.fsdp_force_sharded): then the one GPU runs
+        # exactly the multi-GPU code (separate full buffer resized 0 <-> full, RCCL all-gather / reduce-scatter with
+        # nranks=1, bf16 flat grads reduced into the fp32 shard, reshard-after-forward and prefetch).
+        self.sharded = self.world_size > 1 or (bool(force_sharded) and dist.is_available() and dist.is_initialized())
         mp = plugin.mixed_precision_policy or MixedPrecisionPolicy()
         self.param_dtype = mp.param_dtype or torch.float32
         self.reduce_dtype = mp.reduce_dtype or self.param_dtype
         self.output_dtype = mp.output_dtype
-        self.reshard_after_forward = bool(plugin.reshard_after_forward) and self.world_size > 1
+        self.reshard_after_forward = bool(plugin.reshard_after_forward) and self.sharded
         self.prefetch_depth = max(0, prefetch_depth)
         self.requires_grad_sync = True
         self.is_cuda = device.type == "cuda"
@@ -147,6 +153,15 @@ class FSDPEngine:
             self.rs_stream = torch.cuda.Stream(device=device, priority=-1)
         else:
             self.ag_stream = self.rs_stream = None
+        # All-gather and reduce-scatter get communicators of their own (same ranks as `group`): a synchronous RCCL
+        # collective runs on the stream that issues it, and two streams must not drive one communicator
+        # concurrently, so only separate communicators let the backward prefetch AG(i-1) overlap RS(i+1).
+        self.ag_group = self.rs_group = process_group
+        if self.sharded and self.is_cuda and dist.get_backend(process_group) != "gloo":
+            from .comm import duplicate_group
+
+            self.ag_group = duplicate_group(process_group)
+            self.rs_group = duplicate_group(process_group)
         self.units: list[FlatUnit] = []
         self.exec_order: list[FlatUnit] = []
         self._recording_order = True
@@ -296,7 +311,7 @@ class FSDPEngine:
         unit.grad_valid = False
         del full32
         unit.shard_lp = unit.master.to(self.param_dtype) if self.param_dtype != torch.float32 else unit.master
-        if W == 1:
+        if not self.sharded:
             unit.full = unit.shard_lp  # degenerate: no collective, the shard is the full buffer
         else:
             unit.full = torch.empty(unit.padded, dtype=self.param_dtype, device=dev)
@@ -316,7 +331,7 @@ class FSDPEngine:
             sp._acc_fsdp_full_shape = info.shape
             sp._acc_fsdp_param_lo = info.param_lo
             info.shard_param = sp
-        if W > 1:
+        if self.sharded:
             unit.state = "unsharded"
             self._free_full(unit)
         else:
@@ -324,7 +339,7 @@ class FSDPEngine:
 
     # =========================================================================================== storage
     def _free_full(self, unit: FlatUnit):
-        if self.world_size == 1 or unit.state == "sharded":
+        if not self.sharded or unit.state == "sharded":
             return
         unit.full.untyped_storage().resize_(0)
         unit.state = "sharded"
@@ -332,7 +347,7 @@ class FSDPEngine:
 
     def _unshard(self, unit: FlatUnit):
         """Issue the all-gather of `unit` on the AG stream (no host wait). Idempotent."""
-        if self.world_size == 1 or unit.state != "sharded":
+        if not self.sharded or unit.state != "sharded":
             return
         nbytes = unit.padded * unit.full.element_size()
         unit.full.untyped_storage().resize_(nbytes)
@@ -341,7 +356,7 @@ class FSDPEngine:
             self.ag_stream.wait_stream(cur)
             record_collective("fsdp_all_gather", unit.shard_lp, self.group)
             with torch.cuda.stream(self.ag_stream), trace_range(f"fsdp.all_gather[{unit.idx}]"):
-                dist.all_gather_into_tensor(unit.full, unit.shard_lp, group=self.group)
+                dist.all_gather_into_tensor(unit.full, unit.shard_lp, group=self.ag_group)
                 ev = torch.cuda.Event()
                 ev.record(self.ag_stream)
             unit.ag_event = ev
@@ -384,7 +399,7 @@ class FSDPEngine:
         return hook
 
     def _prefetch_forward(self, unit):
-        if self.world_size == 1 or self.prefetch_depth == 0:
+        if not self.sharded or self.prefetch_depth == 0:
             return
         try:
             i = self.exec_order.index(unit)
@@ -424,7 +439,7 @@ class FSDPEngine:
             t.register_hook(pre_backward)
 
     def _prefetch_backward(self, unit):
-        if self.world_size == 1 or self.prefetch_depth == 0:
+        if not self.sharded or self.prefetch_depth == 0:
             return
         try:
             i = self.exec_order.index(unit)
@@ -467,7 +482,7 @@ class FSDPEngine:
 
     def _direct_grads(self):
         """World size 1 (no replicas): fused weight grads go straight to the fp32 grad shard (the GEMM writes fp32)."""
-        return self.world_size == 1 and self.replicate_size == 1 and os.environ.get("ACCELERATE_FSDP_WGRAD_FP32", "1") != "0"
+        return not self.sharded and self.replicate_size == 1 and os.environ.get("ACCELERATE_FSDP_WGRAD_FP32", "1") != "0"
 
     def _fused_dest(self, unit, info):
         """(destination view, accumulate?) for a fused weight gradient."""
@@ -574,7 +589,7 @@ class FSDPEngine:
         W = self.world_size
         # torch semantics: grads accumulate until the optimizer (or user) sets them to None.
         first = (not unit.grad_valid) or all(i.shard_param.grad is None for i in unit.infos if i.shard_param.requires_grad)
-        if W == 1 and self.replicate_size == 1:
+        if not self.sharded and self.replicate_size == 1:
             if any(i.fused for i in unit.infos) and self._direct_grads():
                 for info in unit.infos:  # fused weights are already in the fp32 shard
                     if info.fused or not info.param.requires_grad:
@@ -583,11 +598,7 @@ class FSDPEngine:
                     d = unit.grad_shard[info.local_lo : info.local_hi]
                     d.copy_(g) if info.shard_param.grad is None else d.add_(g)
             else:
-                g = unit.full_grad[: unit.shard_numel]
-                if first:
-                    unit.grad_shard.copy_(g)
-                else:
-                    unit.grad_shard.add_(g)
+                _grad_update(unit.grad_shard, unit.full_grad[: unit.shard_numel], 1.0, accumulate=not first)
             unit.grad_valid = True
             self._release_grad(unit)
             self._expose_unit_grads(unit)
@@ -608,7 +619,7 @@ class FSDPEngine:
         self._release_grad(unit)
         self._expose_unit_grads(unit)
         self._overlap_step(unit, self.rs_stream)
-        if not unit.is_root and self.world_size > 1:
+        if not unit.is_root and self.sharded:
             self._free_full(unit)  # block done with backward: drop its gathered params
 
     # =========================================================================================== optimizer overlap
@@ -653,21 +664,18 @@ class FSDPEngine:
 
     def _rs_and_accumulate(self, unit, src, out, first):
         W = self.world_size
-        if W > 1:
+        if self.sharded:
             record_collective("fsdp_reduce_scatter", src, self.group)
             if self._uses_gloo and self._gloo():
                 self._gloo_rs(out, src)
             else:
-                dist.reduce_scatter_tensor(out, src, group=self.group)
+                dist.reduce_scatter_tensor(out, src, group=self.rs_group)
         else:
             out.copy_(src[: unit.shard_numel])
         if self.replicate_group is not None and self.replicate_size > 1:
             dist.all_reduce(out, group=self.replicate_group)
         scale = 1.0 / (W * self.replicate_size)
-        if first:
-            torch.mul(out, scale, out=unit.grad_shard) if out.dtype == torch.float32 else unit.grad_shard.copy_(out).mul_(scale)
-        else:
-            unit.grad_shard.add_(out.float(), alpha=scale)
+        _grad_update(unit.grad_shard, out, scale, accumulate=not first)
 
     def _gloo_rs(self, out, src):
         # gloo has no reduce_scatter: all-reduce then slice (CPU test path only).
@@ -693,11 +701,11 @@ class FSDPEngine:
                     info.param._acc_wgrad_slot.uses = 0  # forwards whose outputs never reached this backward
             if self.requires_grad_sync and unit.full_grad is not None and not unit.reduced:
                 self._reduce_unit(unit)
-        if self.is_cuda and self.world_size * self.replicate_size > 1:
+        if self.is_cuda and (self.sharded or self.replicate_size > 1):
             torch.cuda.current_stream(self.device).wait_stream(self.rs_stream)
         for unit in self.units:
             if self.reshard_after_forward or not unit.is_root:
-                if self.world_size > 1 and self.reshard_after_forward:
+                if self.sharded and self.reshard_after_forward:
                     self._free_full(unit)
         if self.requires_grad_sync:
             self._expose_grads()
@@ -767,7 +775,7 @@ class FSDPEngine:
         if self.param_dtype != torch.float32 and not fused_wrote_shadow:
             for unit in self.units:
                 unit.shard_lp.copy_(unit.master)
-        if self.world_size > 1:
+        if self.sharded:
             for unit in self.units:
                 if unit.state == "unsharding" and unit.ag_event is not None and self.is_cuda:
                     torch.cuda.current_stream(self.device).wait_event(unit.ag_event)
@@ -804,7 +812,7 @@ class FSDPEngine:
         for p in extra:
             sq = p.grad.detach().float().pow(2).sum()
             total += sq if getattr(p, "_ep_spec", None) is not None else sq / self.world_size
-        if self.world_size > 1:
+        if self.sharded:
             dist.all_reduce(total, group=self.group)
         clip_grads_by_total_sq(flat_params + extra, total, max_norm)
         return total.sqrt().reshape(())
@@ -815,7 +823,7 @@ class FSDPEngine:
         """Gather the fp32 master weights unit by unit (one all-gather per unit) → {fqn: full tensor}."""
         out = OrderedDict()
         for unit in self.units:
-            if self.world_size > 1:
+            if self.sharded:
                 full = torch.empty(unit.padded, dtype=torch.float32, device=self.device)
                 if self._uses_gloo and self._gloo():
                     dist.all_gather(list(full.chunk(self.world_size)), unit.master, group=self.group)
@@ -937,6 +945,16 @@ class FSDPEngine:
                 for u in self.units:
                     if not u.is_root:
                         self._free_full(u)
+
+
+def _grad_update(dst: torch.Tensor, src: torch.Tensor, scale: float, accumulate: bool):
+    """fp32 grad shard (=|+=) scale * src in one pass (HIP `grad_shard_update` on GPU)."""
+    if dst.is_cuda and src.numel() % 8 == 0 and os.environ.get("ACCELERATE_NATIVE_KERNELS", "1") != "0":
+        ext().grad_shard_update(dst, src.contiguous(), float(scale), bool(accumulate))
+    elif accumulate:
+        dst.add_(src.to(dst.dtype), alpha=scale)
+    else:
+        torch.mul(src.to(dst.dtype), scale, out=dst)
 
 
 class _GradHolder:
@@ -1089,6 +1107,7 @@ def fully_shard(
     init_fn=None,
     seed: int = 0,
     prefetch_depth: int = 1,
+    force_sharded: Optional[bool] = None,
 ) -> FullyShardedModule:
     """Shard `model` with the native engine and return the wrapper."""
     if plugin is None:
@@ -1099,7 +1118,9 @@ def fully_shard(
         plugin.set_auto_wrap_policy(model)
     if plugin.activation_checkpointing:
         apply_activation_checkpointing(model, plugin)
-    engine = FSDPEngine(model, plugin, device, process_group, replicate_group, init_fn, seed, prefetch_depth)
+    if force_sharded is None:
+        force_sharded = os.environ.get("ACCELERATE_FSDP_FORCE_SHARDED", "0") == "1"
+    engine = FSDPEngine(model, plugin, device, process_group, replicate_group, init_fn, seed, prefetch_depth, force_sharded)
     return FullyShardedModule(model, engine)
 
 

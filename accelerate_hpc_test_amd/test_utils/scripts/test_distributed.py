@@ -93,7 +93,9 @@ def check_ddp_matches_single(grad_accum: int = 1):
         assert torch.allclose(p, q, atol=1e-5), (n, (p - q).abs().max())
 
 
-def check_fsdp_matches_single(reshard: bool = True, state_dict_type: str = "SHARDED_STATE_DICT"):
+def check_fsdp_matches_single(reshard: bool = True, state_dict_type: str = "SHARDED_STATE_DICT", force_sharded: bool = False):
+    if force_sharded:  # world size 1 running the multi-rank code (RcclKwargs.fsdp_force_sharded)
+        os.environ["ACCELERATE_FSDP_FORCE_SHARDED"] = "1"
     plugin = FullyShardedDataParallelPlugin(
         fsdp_version=2,
         auto_wrap_policy="transformer_based_wrap",
@@ -109,6 +111,7 @@ def check_fsdp_matches_single(reshard: bool = True, state_dict_type: str = "SHAR
     opt = torch.optim.AdamW(model.parameters(), lr=1e-2, weight_decay=0.01)
     base_opt = torch.optim.AdamW(base.parameters(), lr=1e-2, weight_decay=0.01)
     model, opt = acc.prepare(model, opt)
+    assert model.engine.sharded == (W > 1 or force_sharded)
     bs = 4
     for x, y in _global_batches(3, bs, W):
         xl, yl = x[r * bs : (r + 1) * bs], y[r * bs : (r + 1) * bs]
@@ -585,6 +588,50 @@ def check_join_uneven_inputs():
     inner = acc.unwrap_model(model)
     for (n, p), q in zip(inner.named_parameters(), base.parameters()):
         assert torch.allclose(p, q, atol=1e-5), (n, (p - q).abs().max())
+
+
+class _TwoExperts(torch.nn.Module):
+    """Each rank routes through a different same-shaped expert: with find_unused_parameters the ranks leave different
+    parameters unused, so their buckets become ready in different orders."""
+
+    def __init__(self):
+        super().__init__()
+        self.inp = torch.nn.Linear(4, 8)
+        self.experts = torch.nn.ModuleList([torch.nn.Linear(8, 8) for _ in range(3)])
+        self.out = torch.nn.Linear(8, 1)
+
+    def forward(self, x, expert: int):
+        return self.out(torch.relu(self.experts[expert](torch.relu(self.inp(x))))).squeeze(-1)
+
+
+def check_ddp_unused_params_differ_by_rank():
+    """Advisor finding: buckets must be all-reduced in the same order on every rank. Tiny buckets (one parameter
+    each) and rank-dependent unused experts; the result must equal the single-process average of the per-rank grads."""
+    from accelerate_hpc_test_amd.utils import DistributedDataParallelKwargs
+
+    acc = Accelerator(cpu=True, kwargs_handlers=[DistributedDataParallelKwargs(find_unused_parameters=True, bucket_cap_mb=1e-5)])
+    W, r = acc.num_processes, acc.process_index
+    set_seed(0)
+    base = _TwoExperts()
+    model = copy.deepcopy(base)
+    opt = torch.optim.SGD(model.parameters(), lr=0.1)
+    base_opt = torch.optim.SGD(base.parameters(), lr=0.1)
+    model, opt = acc.prepare(model, opt)
+    assert len(acc.unwrap_model(model).__class__.__name__) and len(model.buckets) == len(list(base.parameters()))
+    bs = 4
+    for step, (x, y) in enumerate(_global_batches(3, bs, W)):
+        e = (r + step) % 3
+        loss = F.mse_loss(model(x[r * bs : (r + 1) * bs], e), y[r * bs : (r + 1) * bs])
+        acc.backward(loss)
+        opt.step()
+        opt.zero_grad()
+        for q in range(W):  # oracle: mean over ranks of each rank's loss on its own expert
+            bl = F.mse_loss(base(x[q * bs : (q + 1) * bs], (q + step) % 3), y[q * bs : (q + 1) * bs]) / W
+            bl.backward()
+        base_opt.step()
+        base_opt.zero_grad()
+    for (n, p), (_, q) in zip(acc.unwrap_model(model).named_parameters(), base.named_parameters()):
+        assert torch.allclose(p, q, atol=1e-6), (n, (p - q).abs().max())
 
 
 def check_ddp_powersgd():

@@ -303,6 +303,10 @@ class RcclKwargs(KwargsHandler):
       left and waits for the side stream (`ACCELERATE_FSDP_OPTIMIZER_OVERLAP`). Incompatible with gradient clipping
       (the norm needs every gradient before any update: `clip_grad_norm_` raises) and with fp16 loss scaling (not
       enabled then).
+    - `fsdp_force_sharded`: at world size 1, run the FSDP engine's multi-GPU code anyway (separate full buffers, RCCL
+      all-gather / reduce-scatter with nranks=1, bf16 flat gradient buffers) instead of the degenerate no-collective
+      path; needs an initialised process group (`ACCELERATE_FSDP_FORCE_SHARDED`). Used to measure and test the sharded
+      path on one GPU.
     """
 
     ddp_bucket_mb: int = None
@@ -311,6 +315,7 @@ class RcclKwargs(KwargsHandler):
     watchdog_timeout: float = None
     collective_check_interval: int = None
     fsdp_optimizer_overlap: bool = None
+    fsdp_force_sharded: bool = None
 
     def __post_init__(self):
         if self.ddp_bucket_mb is None:
@@ -325,6 +330,8 @@ class RcclKwargs(KwargsHandler):
             self.collective_check_interval = int(os.environ.get("ACCELERATE_COLLECTIVE_CHECK_INTERVAL", 50))
         if self.fsdp_optimizer_overlap is None:
             self.fsdp_optimizer_overlap = parse_flag_from_env("ACCELERATE_FSDP_OPTIMIZER_OVERLAP", False)
+        if self.fsdp_force_sharded is None:
+            self.fsdp_force_sharded = parse_flag_from_env("ACCELERATE_FSDP_FORCE_SHARDED", False)
 
 
 # ---------------------------------------------------------------------------------------------------

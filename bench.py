@@ -42,6 +42,9 @@ def parse():
                    help="on: each FSDP unit's AdamW update runs on a side HIP stream as soon as its gradient is final, "
                         "overlapped with the rest of the backward (RcclKwargs.fsdp_optimizer_overlap); optimizer.step() "
                         "still ends every step inside the timed region")
+    p.add_argument("--fsdp-force-sharded", action="store_true",
+                   help="at 1 GPU: run the FSDP engine's multi-GPU code path (full buffers resized 0<->full, RCCL "
+                        "all-gather / reduce-scatter with nranks=1, bf16 flat grads) instead of the no-collective shortcut")
     p.add_argument("--verbose", action="store_true")
     p.add_argument("--gemm-tuning", default="auto", choices=["auto", "off", "tune"],
                    help="auto: load the committed hipBLASLt per-shape table (ops/tuned); tune: search and write it")
@@ -89,7 +92,14 @@ def main():
         activation_checkpointing=args.activation_checkpointing,
     )
     overlap = args.optimizer_overlap == "on" and args.parallel == "fsdp"
-    handlers = [RcclKwargs(fsdp_prefetch_depth=args.prefetch, fsdp_optimizer_overlap=overlap)]
+    force = args.fsdp_force_sharded and args.parallel == "fsdp"
+    if force and int(os.environ.get("WORLD_SIZE", "1")) == 1 and not torch.distributed.is_initialized():
+        # a one-rank RCCL process group so the sharded path has real collectives to issue
+        torch.cuda.set_device(0)
+        port = int(os.environ.get("MASTER_PORT", "29533"))
+        torch.distributed.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                             device_id=torch.device("cuda", 0))
+    handlers = [RcclKwargs(fsdp_prefetch_depth=args.prefetch, fsdp_optimizer_overlap=overlap, fsdp_force_sharded=force)]
     if args.parallel == "ddp":
         from accelerate_hpc_test_amd.utils import DDPCommunicationHookType, DistributedDataParallelKwargs
 
@@ -184,7 +194,7 @@ def main():
                 "moe": {"experts": cfg.num_local_experts, "top_k": cfg.num_experts_per_tok} if is_moe else None,
                 "global_batch": args.mbs * world,
                 "seq_len": args.seq,
-                "parallelism": f"{args.parallel}{world}",
+                "parallelism": f"{args.parallel}{world}" + ("-forced-sharded" if force else ""),
                 "optimizer": "AdamW(lr=1e-5), fp32 master" + (", per-unit update overlapped with backward" if overlap else ""),
                 "activation_checkpointing": args.activation_checkpointing,
             },

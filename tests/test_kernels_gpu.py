@@ -475,3 +475,92 @@ def test_fsdp_wgrad_from_transposed_input_matches(monkeypatch, direct):
         finals[xt] = acc.get_state_dict(model)
     for n, t in finals[False].items():
         assert torch.allclose(t, finals[True][n], atol=2e-4, rtol=1e-3), (n, (t - finals[True][n]).abs().max())
+
+
+def _llama_tiny_run(steps, handlers=(), preset="llama-tiny", lr=1e-3, seed_ids=1, clip=None):
+    from accelerate_hpc_test_amd import Accelerator, FullyShardedDataParallelPlugin
+    from accelerate_hpc_test_amd.models.llama import LLAMA_PRESETS, LlamaForCausalLM
+    from accelerate_hpc_test_amd.state import AcceleratorState, GradientState
+
+    AcceleratorState._reset_state(True)
+    GradientState._reset_state()
+    plugin = FullyShardedDataParallelPlugin(fsdp_version=2, auto_wrap_policy="transformer_based_wrap",
+                                            transformer_cls_names_to_wrap=["LlamaDecoderLayer"])
+    acc = Accelerator(mixed_precision="bf16", fsdp_plugin=plugin, kwargs_handlers=list(handlers))
+    with torch.device("meta"):
+        model = LlamaForCausalLM(LLAMA_PRESETS[preset])
+    opt = torch.optim.AdamW(model.parameters(), lr=lr)
+    model, opt = acc.prepare(model, opt)
+    ids = torch.randint(0, LLAMA_PRESETS[preset].vocab_size, (2, 256), generator=torch.Generator().manual_seed(seed_ids)).to(DEV)
+    losses, norms = [], []
+    for _ in range(steps):
+        out = model(ids, labels=ids)
+        acc.backward(out.loss)
+        if clip is not None:
+            norms.append(acc.clip_grad_norm_(model.parameters(), clip).item())
+        opt.step()
+        opt.zero_grad()
+        losses.append(out.loss.item())
+    torch.cuda.synchronize()
+    return acc, model, losses, norms
+
+
+@pytest.fixture
+def one_rank_rccl():
+    """A world-size-1 RCCL process group in this process (for the forced-sharded FSDP path)."""
+    import torch.distributed as dist
+
+    from accelerate_hpc_test_amd.utils.other import get_free_port
+
+    created = not dist.is_initialized()
+    if created:
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{get_free_port()}", rank=0, world_size=1,
+                                device_id=torch.device("cuda", torch.cuda.current_device()))
+    yield
+    if created:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("wgrad_fp32", ["1", "0"])
+def test_fsdp_forced_sharded_matches_degenerate(one_rank_rccl, monkeypatch, wgrad_fp32):
+    """RcclKwargs(fsdp_force_sharded=True) runs the W>1 engine code on one GPU (full buffer resized 0<->full, RCCL
+    all-gather / reduce-scatter with nranks=1 on their own communicators, bf16 flat grads, reshard + prefetch). Against
+    the world-size-1 shortcut: identical losses and parameters with the bf16 flat-buffer wgrad (WGRAD_FP32=0), and
+    within bf16 rounding of the grads when the shortcut writes fp32 weight grads directly."""
+    from accelerate_hpc_test_amd.utils import RcclKwargs
+
+    monkeypatch.setenv("ACCELERATE_FSDP_WGRAD_FP32", wgrad_fp32)
+    res = {}
+    for force in (False, True):
+        acc, model, losses, norms = _llama_tiny_run(3, [RcclKwargs(fsdp_force_sharded=force)], clip=1e9)
+        eng = model.engine
+        assert eng.sharded == force
+        if force:
+            assert eng.ag_group is not eng.rs_group and eng.ag_group is not None
+            assert all(u.full.untyped_storage().size() == 0 for u in eng.units[1:]), "blocks not resharded after step"
+        res[force] = (losses, norms, acc.get_state_dict(model))
+    (l0, n0, s0), (l1, n1, s1) = res[False], res[True]
+    if wgrad_fp32 == "0":
+        assert l0 == l1, (l0, l1)
+        assert n0 == n1, (n0, n1)
+        for n, t in s0.items():
+            assert torch.equal(t, s1[n]), n
+    else:
+        assert all(abs(a - b) < 2e-3 * abs(a) for a, b in zip(l0, l1)), (l0, l1)
+        for n, t in s0.items():  # Adam turns a near-zero grad's rounding into up to +-lr per step
+            d = (t - s1[n]).abs()
+            assert d.max() <= 2 * 3 * 1e-3 and d.mean() < 5e-5, (n, d.max(), d.mean())
+
+
+@pytest.mark.parametrize("src_dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_grad_shard_update_matches_torch(src_dtype, accumulate):
+    """comm_pack.hip: fp32 shard (=|+=) scale * reduce-scatter output, one pass."""
+    from accelerate_hpc_test_amd.ops._ext import ext
+
+    n = 8 * 1000003
+    src = torch.randn(n, device=DEV).to(src_dtype)
+    dst = torch.randn(n, device=DEV)
+    ref = (dst if accumulate else torch.zeros_like(dst)) + src.float() * 0.125
+    ext().grad_shard_update(dst, src, 0.125, accumulate)
+    assert torch.allclose(dst, ref, rtol=1e-6, atol=1e-6)

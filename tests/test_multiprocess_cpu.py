@@ -42,6 +42,13 @@ def test_fsdp_optimizer_overlap_matches_single_process(world, ga):
     debug_launcher(td.check_fsdp_optimizer_overlap, args=(ga,), num_processes=world)
 
 
+@pytest.mark.parametrize("reshard", [True, False])
+def test_fsdp_forced_sharded_single_rank_matches_torch(reshard):
+    """RcclKwargs.fsdp_force_sharded at world size 1: the W>1 code (full-buffer resize, all-gather, flat grads,
+    reduce-scatter) against the single-process oracle."""
+    debug_launcher(td.check_fsdp_matches_single, args=(reshard, "SHARDED_STATE_DICT", True), num_processes=1)
+
+
 def test_fsdp_single_rank_matches_torch():
     """World size 1: fused weight grads go straight to the fp32 grad shard (no flat-buffer copy)."""
     debug_launcher(td.check_fsdp_matches_single, args=(True, "SHARDED_STATE_DICT"), num_processes=1)
@@ -96,6 +103,11 @@ def test_expert_parallel_mixtral():
 @pytest.mark.parametrize("world", [2, 3])
 def test_ddp_join_uneven_inputs(world):
     debug_launcher(td.check_join_uneven_inputs, num_processes=world)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_ddp_unused_params_differ_by_rank(world):
+    debug_launcher(td.check_ddp_unused_params_differ_by_rank, num_processes=world)
 
 
 def test_ddp_powersgd_hook():

@@ -16,11 +16,13 @@ run() {  # name timeout cmd...
   echo "$name rc=$rc"; tail -3 "gpurun_out/$name.log" | cut -c1-900
   [ $rc -eq 0 ] || exit $rc
 }
-prof() {  # name timeout bench-args...
+prof() {  # name timeout bench-args...   (PROF_EXTRA: more rocprofv3 trace flags, e.g. --memory-copy-trace)
   local name=$1 t=$2; shift 2
   rm -rf "gpurun_out/$name"
-  run "$name" "$t" rocprofv3 --kernel-trace --stats --output-format csv -d "gpurun_out/$name" -o run -- python3 "$@"
+  run "$name" "$t" rocprofv3 --kernel-trace $PROF_EXTRA --stats --output-format csv -d "gpurun_out/$name" -o run -- python3 "$@"
   python3 tools/prof_summary.py "gpurun_out/$name" > "gpurun_out/$name.md" && head -40 "gpurun_out/$name.md"
+  python3 tools/prof_overlap.py "gpurun_out/$name" --pattern "${OVERLAP_PATTERN:-nccl|rccl}" > "gpurun_out/${name}_overlap.md" && cat "gpurun_out/${name}_overlap.md"
+  find "gpurun_out/$name" -name '*kernel_trace.csv' -size +20M -delete  # keep the pull under the 64 MiB cap
 }
 for step in "$@"; do
   case $step in
@@ -29,6 +31,8 @@ for step in "$@"; do
     bench8b) run bench8b 600 python bench.py --steps 5 --warmup 2 $BENCH_ARGS ;;
     bench8b_noblaslt) ACCELERATE_BLASLT_WGRAD=0 run bench8b_noblaslt 600 python bench.py --steps 5 --warmup 2 $BENCH_ARGS ;;
     bench8b_nooverlap) run bench8b_nooverlap 600 python bench.py --steps 5 --warmup 2 --optimizer-overlap off $BENCH_ARGS ;;
+    bench8b_sharded) run bench8b_sharded 600 python bench.py --steps 5 --warmup 2 --fsdp-force-sharded $BENCH_ARGS ;;
+    prof8b_sharded) OVERLAP_PATTERN="nccl|rccl|copyBuffer" PROF_EXTRA=--memory-copy-trace prof prof8b_sharded 600 bench.py --steps 3 --warmup 2 --fsdp-force-sharded $BENCH_ARGS ;;
     bench8b_fp8) run bench8b_fp8 600 python bench.py --steps 5 --warmup 2 --precision fp8 $BENCH_ARGS ;;
     bench8b_ddp) run bench8b_ddp 600 python bench.py --parallel ddp --steps 5 --warmup 2 $BENCH_ARGS ;;
     mixtral_bf16) run mixtral_bf16 600 python bench.py --model mixtral-8x7b-4l --steps 3 --warmup 2 $BENCH_ARGS ;;
