@@ -38,6 +38,8 @@ torch::Tensor fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor a_scale_i
 void grad_shard_update(torch::Tensor dst, torch::Tensor src, double scale, bool accumulate);
 // runtime/*.cpp
 void register_runtime(pybind11::module& m);
+void cpu_adam_step(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, c10::optional<torch::Tensor> shadow,
+                   double lr, double beta1, double beta2, double eps, double wd, double bc1, double bc2_sqrt, bool adamw);
 bool blaslt_wgrad_f32(torch::Tensor dy, torch::Tensor x, torch::Tensor out, bool accumulate);
 std::vector<std::tuple<int64_t, int64_t, int64_t, int64_t, double>> blaslt_wgrad_plans();
 
@@ -65,5 +67,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("grad_shard_update", &grad_shard_update);
   register_runtime(m);
   m.def("blaslt_wgrad_f32", &blaslt_wgrad_f32);
+  m.def("cpu_adam_step", &cpu_adam_step);
   m.def("blaslt_wgrad_plans", &blaslt_wgrad_plans);
 }

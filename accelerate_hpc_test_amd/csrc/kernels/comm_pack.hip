@@ -2,6 +2,7 @@
 //
 //  * grad_shard_update: fp32 gradient shard (=|+=) scale * reduce-scatter output (bf16 or fp32) in ONE pass. It
 //    replaces "bf16 -> fp32 copy, then multiply by 1/W" (two full passes over the shard, profiles/r2_*).
+#include <hip/hip_runtime.h>
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 
@@ -72,16 +73,16 @@ void grad_shard_update(torch::Tensor dst, torch::Tensor src, double scale, bool 
     auto* d = dst.data_ptr<float>();
     auto* x = reinterpret_cast<const bf16_t*>(src.data_ptr());
     if (accumulate)
-      grad_update_bf16_kernel<true><<<grid_for(n8, 256), 256, 0, stream>>>(d, x, s, n8);
+      hipLaunchKernelGGL(grad_update_bf16_kernel<true>, dim3(grid_for(n8, 256)), dim3(256), 0, stream, d, x, s, n8);
     else
-      grad_update_bf16_kernel<false><<<grid_for(n8, 256), 256, 0, stream>>>(d, x, s, n8);
+      hipLaunchKernelGGL(grad_update_bf16_kernel<false>, dim3(grid_for(n8, 256)), dim3(256), 0, stream, d, x, s, n8);
   } else {
     TORCH_CHECK(src.scalar_type() == at::kFloat, "grad_shard_update: src must be bf16 or fp32");
     const int64_t n4 = n / 4;
     if (accumulate)
-      grad_update_f32_kernel<true><<<grid_for(n4, 256), 256, 0, stream>>>(dst.data_ptr<float>(), src.data_ptr<float>(), s, n4);
+      hipLaunchKernelGGL(grad_update_f32_kernel<true>, dim3(grid_for(n4, 256)), dim3(256), 0, stream, dst.data_ptr<float>(), src.data_ptr<float>(), s, n4);
     else
-      grad_update_f32_kernel<false><<<grid_for(n4, 256), 256, 0, stream>>>(dst.data_ptr<float>(), src.data_ptr<float>(), s, n4);
+      hipLaunchKernelGGL(grad_update_f32_kernel<false>, dim3(grid_for(n4, 256)), dim3(256), 0, stream, dst.data_ptr<float>(), src.data_ptr<float>(), s, n4);
   }
   C10_HIP_KERNEL_LAUNCH_CHECK();
 }

@@ -1,0 +1,78 @@
+// Host AdamW for FSDP CPU offload (the optimizer step of offloaded fp32 master shards runs on the host CPUs).
+//
+// One OpenMP-parallel, vectorised pass over (param, grad, exp_avg, exp_avg_sq) fp32 shard ranges — torch.optim.AdamW
+// / Adam semantics, bit-compatible state layout — that also writes the bf16 copy of the updated parameters into a
+// pinned staging buffer. The FSDP engine then uploads 2 bytes per parameter (instead of the 4-byte master) with one
+// non-blocking H2D copy per unit into the bf16 all-gather source on the GPU. The loop is compiled for AVX-512, AVX2
+// and baseline x86-64 (`target_clones`), picked at load time for the host it runs on.
+#include <torch/extension.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+
+namespace {
+
+struct Hyper {
+  float lr, beta1, beta2, eps, wd, bc1, bc2_sqrt;
+  bool adamw;
+};
+
+inline uint16_t to_bf16_rne(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fc0;  // NaN stays NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return static_cast<uint16_t>(u >> 16);
+}
+
+__attribute__((target_clones("avx512f", "avx2", "default")))
+void adam_range(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
+                uint16_t* __restrict__ shadow, int64_t n, Hyper h) {
+  const float step_size = h.lr / h.bc1, bc2s = h.bc2_sqrt, decay = 1.f - h.lr * h.wd;
+  const float b1 = h.beta1, b2 = h.beta2, c1 = 1.f - h.beta1, c2 = 1.f - h.beta2;
+  constexpr int64_t kBlock = 1 << 14;
+  const int64_t nblk = (n + kBlock - 1) / kBlock;
+#pragma omp parallel for schedule(static)
+  for (int64_t b = 0; b < nblk; ++b) {
+    const int64_t lo = b * kBlock, hi = std::min(n, lo + kBlock);
+#pragma omp simd
+    for (int64_t i = lo; i < hi; ++i) {
+      float pf = p[i], gf = g[i];
+      if (!h.adamw) gf += h.wd * pf;
+      const float mf = b1 * m[i] + c1 * gf;
+      const float vf = b2 * v[i] + c2 * gf * gf;
+      if (h.adamw) pf *= decay;
+      pf -= step_size * mf / (std::sqrt(vf) / bc2s + h.eps);
+      m[i] = mf;
+      v[i] = vf;
+      p[i] = pf;
+    }
+    if (shadow != nullptr) {
+#pragma omp simd
+      for (int64_t i = lo; i < hi; ++i) shadow[i] = to_bf16_rne(p[i]);
+    }
+  }
+}
+
+}  // namespace
+
+// In-place AdamW/Adam step over contiguous fp32 CPU tensors; `shadow` (bf16, same numel) receives the updated params.
+void cpu_adam_step(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, c10::optional<torch::Tensor> shadow,
+                   double lr, double beta1, double beta2, double eps, double wd, double bc1, double bc2_sqrt, bool adamw) {
+  for (const auto* t : {&p, &g, &m, &v}) {
+    TORCH_CHECK(t->device().is_cpu() && t->scalar_type() == at::kFloat && t->is_contiguous(),
+                "cpu_adam_step: contiguous fp32 CPU tensors required");
+    TORCH_CHECK(t->numel() == p.numel(), "cpu_adam_step: size mismatch");
+  }
+  uint16_t* sh = nullptr;
+  if (shadow.has_value() && shadow->defined()) {
+    TORCH_CHECK(shadow->device().is_cpu() && shadow->scalar_type() == at::kBFloat16 && shadow->is_contiguous() &&
+                    shadow->numel() == p.numel(),
+                "cpu_adam_step: shadow must be a contiguous bf16 CPU tensor of the same size");
+    sh = reinterpret_cast<uint16_t*>(shadow->data_ptr());
+  }
+  Hyper h{(float)lr, (float)beta1, (float)beta2, (float)eps, (float)wd, (float)bc1, (float)bc2_sqrt, adamw};
+  pybind11::gil_scoped_release nogil;
+  adam_range(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), sh, p.numel(), h);
+}

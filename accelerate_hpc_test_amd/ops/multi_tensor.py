@@ -195,7 +195,7 @@ def clip_grads_by_total_sq(params, total_sq: torch.Tensor, max_norm: float):
     if not use_native(params[0].grad):
         coef = (max_norm / (total_sq.sqrt() + 1e-6)).clamp(max=1.0)
         for p in params:
-            p.grad.mul_(coef.to(p.grad.dtype))
+            p.grad.mul_(coef.to(p.grad.device, p.grad.dtype))
         return
     e = ext()
     dev = params[0].grad.device
@@ -204,3 +204,36 @@ def clip_grads_by_total_sq(params, total_sq: torch.Tensor, max_norm: float):
         if rows:
             meta, prefix, nb = _CACHE.get(rows, dev)
             e.clip_multi_tensor(meta, prefix, nb, _DT[dt], total_sq, max_norm)
+
+
+class CpuFusedAdamStep:
+    """Adam/AdamW for CPU-resident fp32 params (FSDP CPU offload): the native OpenMP kernel
+    (`csrc/runtime/cpu_adam.cpp`), one call per parameter, also writing the bf16 upload copy when the engine attached
+    one (`p._acc_bf16_shadow_host`). Same `state` layout as torch."""
+
+    def __init__(self, optimizer: torch.optim.Optimizer):
+        self.optimizer = optimizer
+        self.adamw = isinstance(optimizer, torch.optim.AdamW)
+
+    @torch.no_grad()
+    def step(self, grad_scale=None, only: Optional[set] = None, skip: Optional[set] = None):
+        opt, e = self.optimizer, ext()
+        for group in opt.param_groups:
+            lr = float(group["lr"])
+            beta1, beta2 = group["betas"]
+            for p in group["params"]:
+                if p.grad is None or p.numel() == 0:
+                    continue
+                if (only is not None and id(p) not in only) or (skip is not None and id(p) in skip):
+                    continue
+                st = opt.state[p]
+                if len(st) == 0:
+                    st["step"] = torch.tensor(0.0, dtype=torch.float32)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["step"] += 1
+                s = float(st["step"])
+                g = p.grad if grad_scale is None else p.grad / float(grad_scale)
+                e.cpu_adam_step(p.data, g, st["exp_avg"], st["exp_avg_sq"], getattr(p, "_acc_bf16_shadow_host", None),
+                                lr, beta1, beta2, group["eps"], group["weight_decay"], 1.0 - beta1**s,
+                                math.sqrt(1.0 - beta2**s), self.adamw)

@@ -34,20 +34,28 @@ def move_to_device(state, device):
     return state
 
 
-def _fused_adam_eligible(optimizer) -> bool:
+def _fused_adam_eligible(optimizer):
+    """"gpu" (HIP multi-tensor kernel), "cpu" (native OpenMP kernel over CPU-offloaded fp32 shards) or None."""
     if os.environ.get("ACCELERATE_FUSED_ADAMW", "1") == "0":
-        return False
+        return None
     if type(optimizer) not in (torch.optim.AdamW, torch.optim.Adam):
-        return False
+        return None
+    devs = set()
     for g in optimizer.param_groups:
         if g.get("amsgrad", False) or g.get("maximize", False) or g.get("capturable", False):
-            return False
+            return None
         if g.get("differentiable", False):
-            return False
+            return None
         for p in g["params"]:
-            if not p.is_cuda:
-                return False
-    return True
+            devs.add("gpu" if p.is_cuda else ("cpu" if p.device.type == "cpu" and p.dtype == torch.float32 else "other"))
+    if devs == {"gpu"}:
+        return "gpu"
+    if devs == {"cpu"} and any(hasattr(p, "_acc_bf16_shadow_host") or getattr(p, "_acc_offloaded", False)
+                               for g in optimizer.param_groups for p in g["params"]):
+        from .ops import _ext
+
+        return "cpu" if _ext.available() else None
+    return None
 
 
 class AcceleratedOptimizer(torch.optim.Optimizer):
@@ -73,10 +81,15 @@ class AcceleratedOptimizer(torch.optim.Optimizer):
     # ---- fused HIP AdamW -------------------------------------------------------------------------
     def _maybe_fused(self):
         if self._fused_step is None:
-            if _fused_adam_eligible(self.optimizer):
+            kind = _fused_adam_eligible(self.optimizer)
+            if kind == "gpu":
                 from .ops.multi_tensor import FusedAdamStep
 
                 self._fused_step = FusedAdamStep(self.optimizer)
+            elif kind == "cpu":
+                from .ops.multi_tensor import CpuFusedAdamStep
+
+                self._fused_step = CpuFusedAdamStep(self.optimizer)
             else:
                 self._fused_step = False
         return self._fused_step

@@ -22,6 +22,11 @@ Parity: the reference wraps `torch.distributed.fsdp.fully_shard` (`/root/referen
   the reduce stream; its output is scaled by 1/W and accumulated into the fp32 gradient shard. HSDP adds an
   all-reduce across the replicate group. `no_sync` (`set_requires_gradient_sync(False)`) keeps the flat grads.
 * **World size 1** degenerates to zero collectives: the bf16 shard IS the full buffer (no copies).
+* **CPU offload** (`plugin.cpu_offload`, reference `fsdp_utils.py:648` offload_policy): the fp32 master shard, the fp32
+  gradient shard and the optimizer state live in pinned host memory and the optimizer step runs on the host (native
+  OpenMP AdamW, `csrc/runtime/cpu_adam.cpp`, which also writes the bf16 upload copy). Only the bf16 all-gather
+  source (2 B/param/W) stays in HBM: on a 288 GB MI355X that is the cheap part, and keeping it resident avoids an H2D
+  per all-gather. Reduced gradients go D2H from the reduce stream; the host waits for them at the end of backward.
 
 Messages are one transformer block each (≈436 MB bf16 for Llama-3-8B), large enough for RCCL to spread over all 7
 xGMI links; streams and events order everything on the device — the host never blocks.
@@ -148,6 +153,9 @@ class FSDPEngine:
         self.requires_grad_sync = True
         self.is_cuda = device.type == "cuda"
         self._uses_gloo = self.is_cuda is False
+        self.offload = plugin.cpu_offload not in (None, False)
+        self._pin = self.offload and torch.cuda.is_available() and getattr(plugin.cpu_offload, "pin_memory", True)
+        self._d2h_pending = []
         if self.is_cuda:
             self.ag_stream = torch.cuda.Stream(device=device, priority=-1)
             self.rs_stream = torch.cuda.Stream(device=device, priority=-1)
@@ -281,7 +289,16 @@ class FSDPEngine:
         dev, W, r = self.device, self.world_size, self.rank
         full32 = torch.zeros(unit.padded, dtype=torch.float32, device=dev)
         on_meta = any(i.param.is_meta for i in unit.infos)
-        if on_meta:
+        # cpu_ram_efficient_loading (reference fsdp_utils.py:467-554,664-719): only rank 0 holds the real (pretrained)
+        # weights — the other ranks built the model on the meta device — and rank 0's unit is broadcast over the
+        # shard group straight into HBM, one unit at a time (one RCCL broadcast per block instead of one per tensor).
+        ram_efficient = bool(getattr(self.plugin, "cpu_ram_efficient_loading", False)) and W > 1
+        if ram_efficient and r != 0:
+            for info in unit.infos:
+                if info.param.is_meta:
+                    view = full32[info.offset : info.offset + info.numel].view(info.shape)
+                    self._replace_param(info, nn.Parameter(view, requires_grad=info.param.requires_grad))
+        elif on_meta:
             # Materialise the whole unit on the GPU with a per-unit seed: every rank generates the identical unit
             # (deterministic regardless of world size) and keeps its slice.
             if init_fn is None:
@@ -303,14 +320,21 @@ class FSDPEngine:
         else:
             for info in unit.infos:
                 full32[info.offset : info.offset + info.numel].copy_(info.param.detach().reshape(-1).to(dev, torch.float32))
-            if self.plugin.sync_module_states and W > 1:
-                dist.broadcast(full32, src=dist.get_global_rank(self.group, 0) if self.group is not None else 0, group=self.group)
+        if W > 1 and (ram_efficient or (self.plugin.sync_module_states and not on_meta)):
+            dist.broadcast(full32, src=dist.get_global_rank(self.group, 0) if self.group is not None else 0, group=self.group)
         lo, hi = r * unit.shard_numel, (r + 1) * unit.shard_numel
-        unit.master = full32[lo:hi].clone()
-        unit.grad_shard = torch.zeros_like(unit.master)
+        if self.offload:
+            unit.master = self._host(full32[lo:hi])
+            unit.grad_shard = self._host(torch.zeros(unit.shard_numel, dtype=torch.float32))
+            unit.shard_lp = full32[lo:hi].to(self.param_dtype, copy=True)  # HBM-resident all-gather source
+            # what the host optimizer writes for upload (bf16), or None: upload the fp32 master and cast on the GPU
+            unit.shadow_host = self._host(torch.empty(unit.shard_numel, dtype=self.param_dtype)) if self.param_dtype != torch.float32 else None
+        else:
+            unit.master = full32[lo:hi].clone()
+            unit.grad_shard = torch.zeros_like(unit.master)
+            unit.shard_lp = unit.master.to(self.param_dtype) if self.param_dtype != torch.float32 else unit.master
         unit.grad_valid = False
         del full32
-        unit.shard_lp = unit.master.to(self.param_dtype) if self.param_dtype != torch.float32 else unit.master
         if not self.sharded:
             unit.full = unit.shard_lp  # degenerate: no collective, the shard is the full buffer
         else:
@@ -325,7 +349,11 @@ class FSDPEngine:
                 a = b = max(min(plo, hi), lo)
             info.local_lo, info.local_hi, info.param_lo = a - lo, b - lo, a - plo
             sp = nn.Parameter(unit.master[info.local_lo : info.local_hi], requires_grad=info.param.requires_grad)
-            if self.param_dtype != torch.float32:
+            if self.offload:
+                sp._acc_offloaded = True
+                if unit.shadow_host is not None:
+                    sp._acc_bf16_shadow_host = unit.shadow_host[info.local_lo : info.local_hi]
+            elif self.param_dtype != torch.float32:
                 sp._acc_bf16_shadow = unit.shard_lp[info.local_lo : info.local_hi]
             sp._acc_fsdp_fqn = info.fqn
             sp._acc_fsdp_full_shape = info.shape
@@ -336,6 +364,11 @@ class FSDPEngine:
             self._free_full(unit)
         else:
             unit.state = "unsharded"
+
+    def _host(self, t: torch.Tensor) -> torch.Tensor:
+        """A host copy of `t` (pinned when offloading to a GPU run, so D2H/H2D are true async DMA)."""
+        h = t.detach().to("cpu", copy=True)
+        return h.pin_memory() if self._pin else h
 
     # =========================================================================================== storage
     def _free_full(self, unit: FlatUnit):
@@ -482,7 +515,7 @@ class FSDPEngine:
 
     def _direct_grads(self):
         """World size 1 (no replicas): fused weight grads go straight to the fp32 grad shard (the GEMM writes fp32)."""
-        return not self.sharded and self.replicate_size == 1 and os.environ.get("ACCELERATE_FSDP_WGRAD_FP32", "1") != "0"
+        return not self.sharded and not self.offload and self.replicate_size == 1 and os.environ.get("ACCELERATE_FSDP_WGRAD_FP32", "1") != "0"
 
     def _fused_dest(self, unit, info):
         """(destination view, accumulate?) for a fused weight gradient."""
@@ -598,7 +631,7 @@ class FSDPEngine:
                     d = unit.grad_shard[info.local_lo : info.local_hi]
                     d.copy_(g) if info.shard_param.grad is None else d.add_(g)
             else:
-                _grad_update(unit.grad_shard, unit.full_grad[: unit.shard_numel], 1.0, accumulate=not first)
+                self._deliver_grad(unit, unit.full_grad[: unit.shard_numel], 1.0, first)
             unit.grad_valid = True
             self._release_grad(unit)
             self._expose_unit_grads(unit)
@@ -631,6 +664,8 @@ class FSDPEngine:
         backward GEMM/attention kernels are compute-bound, so the two share the CUs. A unit's weights are not read
         again in this backward once its gradient is final, and the next all-gather / forward runs after
         `take_overlapped()` has ordered the compute stream behind the side stream."""
+        if self.offload:
+            raise ValueError("fsdp_optimizer_overlap cannot be combined with FSDP CPU offload (the step runs on the host).")
         self._overlap_fn = step_fn
         self._overlap_done: set[int] = set()
         if self.is_cuda and getattr(self, "opt_stream", None) is None:
@@ -675,7 +710,28 @@ class FSDPEngine:
         if self.replicate_group is not None and self.replicate_size > 1:
             dist.all_reduce(out, group=self.replicate_group)
         scale = 1.0 / (W * self.replicate_size)
-        _grad_update(unit.grad_shard, out, scale, accumulate=not first)
+        self._deliver_grad(unit, out, scale, first)
+
+    def _deliver_grad(self, unit, src, scale, first):
+        """grad shard (=|+=) scale * src. Offloaded: scale into a transient fp32 HBM buffer, then DMA it to the pinned
+        host shard (or a staging buffer that the host adds at the end of backward when accumulating)."""
+        if not (self.offload and self.is_cuda):
+            _grad_update(unit.grad_shard, src, scale, accumulate=not first)
+            return
+        g32 = torch.empty(unit.shard_numel, dtype=torch.float32, device=self.device)
+        _grad_update(g32, src, scale, accumulate=False)
+        stage = unit.grad_shard if first else torch.empty(unit.shard_numel, dtype=torch.float32, pin_memory=self._pin)
+        stage.copy_(g32, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._d2h_pending.append((ev, unit, None if first else stage, g32))
+
+    def _drain_d2h(self):
+        for ev, unit, stage, _ in self._d2h_pending:
+            ev.synchronize()
+            if stage is not None:
+                unit.grad_shard.add_(stage)
+        self._d2h_pending.clear()
 
     def _gloo_rs(self, out, src):
         # gloo has no reduce_scatter: all-reduce then slice (CPU test path only).
@@ -703,6 +759,8 @@ class FSDPEngine:
                 self._reduce_unit(unit)
         if self.is_cuda and (self.sharded or self.replicate_size > 1):
             torch.cuda.current_stream(self.device).wait_stream(self.rs_stream)
+        if self._d2h_pending:
+            self._drain_d2h()  # offload: the host optimizer reads the gradient shards next
         for unit in self.units:
             if self.reshard_after_forward or not unit.is_root:
                 if self.sharded and self.reshard_after_forward:
@@ -772,7 +830,13 @@ class FSDPEngine:
     def on_optimizer_step(self, fused_wrote_shadow: bool):
         """Refresh the bf16 all-gather source from the fp32 master when the optimizer did not write it, and drop any
         gathered copies (they are stale now; the next forward re-gathers)."""
-        if self.param_dtype != torch.float32 and not fused_wrote_shadow:
+        if self.offload:
+            for unit in self.units:  # upload the updated shard into the HBM all-gather source
+                if fused_wrote_shadow and unit.shadow_host is not None:
+                    unit.shard_lp.copy_(unit.shadow_host, non_blocking=True)
+                else:
+                    unit.shard_lp.copy_(unit.master.to(unit.shard_lp.device, non_blocking=True))
+        elif self.param_dtype != torch.float32 and not fused_wrote_shadow:
             for unit in self.units:
                 unit.shard_lp.copy_(unit.master)
         if self.sharded:
@@ -825,10 +889,11 @@ class FSDPEngine:
         for unit in self.units:
             if self.sharded:
                 full = torch.empty(unit.padded, dtype=torch.float32, device=self.device)
+                master = unit.master.to(self.device) if self.offload else unit.master
                 if self._uses_gloo and self._gloo():
-                    dist.all_gather(list(full.chunk(self.world_size)), unit.master, group=self.group)
+                    dist.all_gather(list(full.chunk(self.world_size)), master, group=self.group)
                 else:
-                    dist.all_gather_into_tensor(full, unit.master, group=self.group)
+                    dist.all_gather_into_tensor(full, master, group=self.group)
             else:
                 full = unit.master
             if rank0_only and self.rank != 0:
@@ -896,7 +961,7 @@ class FSDPEngine:
                 piece = full[info.param_lo : info.param_lo + (info.local_hi - info.local_lo)]
                 unit.master[info.local_lo : info.local_hi].copy_(piece.to(unit.master.device, torch.float32))
             if unit.shard_lp is not unit.master:
-                unit.shard_lp.copy_(unit.master)
+                unit.shard_lp.copy_(unit.master.to(unit.shard_lp.device))
         for name, _ in self._extras():
             if name in sd:
                 self._load_extra(name, sd[name])
@@ -922,7 +987,7 @@ class FSDPEngine:
                         src = tensors[info.fqn][a - s_lo : b - s_lo]
                         unit.master[info.local_lo + (a - lo_need) : info.local_lo + (b - lo_need)].copy_(src.to(unit.master.device))
             if unit.shard_lp is not unit.master:
-                unit.shard_lp.copy_(unit.master)
+                unit.shard_lp.copy_(unit.master.to(unit.shard_lp.device))
         for name, p in self._extras():
             found = [(m.get("extra", {}).get(name), t) for t, m in pieces if name in m.get("extra", {})]
             if not found:

@@ -45,6 +45,8 @@ def parse():
     p.add_argument("--fsdp-force-sharded", action="store_true",
                    help="at 1 GPU: run the FSDP engine's multi-GPU code path (full buffers resized 0<->full, RCCL "
                         "all-gather / reduce-scatter with nranks=1, bf16 flat grads) instead of the no-collective shortcut")
+    p.add_argument("--fsdp-cpu-offload", action="store_true",
+                   help="FSDP CPU offload: fp32 master/grad shards + AdamW state in pinned host memory, host AdamW")
     p.add_argument("--verbose", action="store_true")
     p.add_argument("--gemm-tuning", default="auto", choices=["auto", "off", "tune"],
                    help="auto: load the committed hipBLASLt per-shape table (ops/tuned); tune: search and write it")
@@ -90,6 +92,7 @@ def main():
         transformer_cls_names_to_wrap=list(model_cls._no_split_modules),
         reshard_after_forward=True,
         activation_checkpointing=args.activation_checkpointing,
+        cpu_offload=args.fsdp_cpu_offload,
     )
     overlap = args.optimizer_overlap == "on" and args.parallel == "fsdp"
     force = args.fsdp_force_sharded and args.parallel == "fsdp"
@@ -195,7 +198,8 @@ def main():
                 "global_batch": args.mbs * world,
                 "seq_len": args.seq,
                 "parallelism": f"{args.parallel}{world}" + ("-forced-sharded" if force else ""),
-                "optimizer": "AdamW(lr=1e-5), fp32 master" + (", per-unit update overlapped with backward" if overlap else ""),
+                "optimizer": "AdamW(lr=1e-5), fp32 master" + (", per-unit update overlapped with backward" if overlap else "")
+                + (", CPU-offloaded (host AdamW)" if args.fsdp_cpu_offload else ""),
                 "activation_checkpointing": args.activation_checkpointing,
             },
             "tokens_per_sec_per_gpu": round(tps / world, 1),

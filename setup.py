@@ -31,8 +31,9 @@ if os.environ.get("ACCELERATE_SKIP_NATIVE_BUILD", "0") != "1":
             sources=sources,
             include_dirs=[os.path.join(root, "kernels")],
             libraries=["hipblaslt"],
+            extra_link_args=["-fopenmp"],
             extra_compile_args={
-                "cxx": ["-O3", "-std=c++17"],
+                "cxx": ["-O3", "-std=c++17", "-fopenmp"],
                 "nvcc": ["-O3", "-std=c++17", "--offload-arch=gfx950", "-munsafe-fp-atomics"],
             },
         )

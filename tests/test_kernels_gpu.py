@@ -477,7 +477,7 @@ def test_fsdp_wgrad_from_transposed_input_matches(monkeypatch, direct):
         assert torch.allclose(t, finals[True][n], atol=2e-4, rtol=1e-3), (n, (t - finals[True][n]).abs().max())
 
 
-def _llama_tiny_run(steps, handlers=(), preset="llama-tiny", lr=1e-3, seed_ids=1, clip=None):
+def _llama_tiny_run(steps, handlers=(), preset="llama-tiny", lr=1e-3, seed_ids=1, clip=None, **plugin_kw):
     from accelerate_hpc_test_amd import Accelerator, FullyShardedDataParallelPlugin
     from accelerate_hpc_test_amd.models.llama import LLAMA_PRESETS, LlamaForCausalLM
     from accelerate_hpc_test_amd.state import AcceleratorState, GradientState
@@ -485,7 +485,7 @@ def _llama_tiny_run(steps, handlers=(), preset="llama-tiny", lr=1e-3, seed_ids=1
     AcceleratorState._reset_state(True)
     GradientState._reset_state()
     plugin = FullyShardedDataParallelPlugin(fsdp_version=2, auto_wrap_policy="transformer_based_wrap",
-                                            transformer_cls_names_to_wrap=["LlamaDecoderLayer"])
+                                            transformer_cls_names_to_wrap=["LlamaDecoderLayer"], **plugin_kw)
     acc = Accelerator(mixed_precision="bf16", fsdp_plugin=plugin, kwargs_handlers=list(handlers))
     with torch.device("meta"):
         model = LlamaForCausalLM(LLAMA_PRESETS[preset])
@@ -564,3 +564,30 @@ def test_grad_shard_update_matches_torch(src_dtype, accumulate):
     ref = (dst if accumulate else torch.zeros_like(dst)) + src.float() * 0.125
     ext().grad_shard_update(dst, src, 0.125, accumulate)
     assert torch.allclose(dst, ref, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("force", [False, True])
+def test_fsdp_cpu_offload_matches_gpu_resident(one_rank_rccl, monkeypatch, force):
+    """plugin.cpu_offload: fp32 master / grad shards and Adam state in pinned host memory, reduced grads D2H from the
+    reduce stream, native host AdamW writing the bf16 upload copy. Against the HBM-resident engine with the same
+    bf16 flat-buffer gradients: same losses and parameters up to fp32 summation order in the optimizer."""
+    from accelerate_hpc_test_amd.ops.multi_tensor import CpuFusedAdamStep
+    from accelerate_hpc_test_amd.utils import RcclKwargs
+
+    monkeypatch.setenv("ACCELERATE_FSDP_WGRAD_FP32", "0")
+    res = {}
+    for off in (False, True):
+        acc, model, losses, norms = _llama_tiny_run(3, [RcclKwargs(fsdp_force_sharded=force)], clip=1e9, cpu_offload=off)
+        eng = model.engine
+        assert eng.offload == off
+        if off:
+            assert all(u.master.device.type == "cpu" and u.master.is_pinned() for u in eng.units)
+            assert all(u.shard_lp.is_cuda for u in eng.units)
+            assert isinstance(acc._optimizers[0]._maybe_fused(), CpuFusedAdamStep)
+        res[off] = (losses, norms, acc.get_state_dict(model))
+    (l0, n0, s0), (l1, n1, s1) = res[False], res[True]
+    assert all(abs(a - b) <= 1e-4 * abs(a) for a, b in zip(l0, l1)), (l0, l1)
+    assert all(abs(a - b) <= 1e-4 * abs(a) for a, b in zip(n0, n1)), (n0, n1)
+    for n, t in s0.items():
+        d = (t - s1[n]).abs()
+        assert d.max() <= 2 * 3 * 1e-3 and d.mean() < 1e-6, (n, d.max(), d.mean())

@@ -49,6 +49,17 @@ def test_fsdp_forced_sharded_single_rank_matches_torch(reshard):
     debug_launcher(td.check_fsdp_matches_single, args=(reshard, "SHARDED_STATE_DICT", True), num_processes=1)
 
 
+@pytest.mark.parametrize("world", [1, 2])
+def test_fsdp_cpu_offload_matches_single_process(world):
+    """plugin.cpu_offload: master/grad shards + optimizer state on the host, native host AdamW."""
+    debug_launcher(td.check_fsdp_matches_single, args=(True, "SHARDED_STATE_DICT", False, True), num_processes=world)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_fsdp_cpu_ram_efficient_loading(world):
+    debug_launcher(td.check_fsdp_cpu_ram_efficient_loading, num_processes=world)
+
+
 def test_fsdp_single_rank_matches_torch():
     """World size 1: fused weight grads go straight to the fp32 grad shard (no flat-buffer copy)."""
     debug_launcher(td.check_fsdp_matches_single, args=(True, "SHARDED_STATE_DICT"), num_processes=1)
