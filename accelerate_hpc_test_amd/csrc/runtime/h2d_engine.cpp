@@ -55,6 +55,8 @@ class H2DEngine {
     for (auto& w : workers_) w.join();
     hipSetDevice(device_);
     hipStreamSynchronize(stream_);
+    for (auto& f : inflight_) hipEventDestroy(f.ev);
+    inflight_.clear();
     for (auto& s : slots_) {
       hipEventDestroy(s.ev);
       hipHostFree(s.ptr);
@@ -74,8 +76,14 @@ class H2DEngine {
     if (src.is_pinned()) {  // already DMA-able: one async copy, no staging
       std::lock_guard<std::mutex> g(mu_);
       HIP_OK(hipSetDevice(device_));
+      retire_completed();
       HIP_OK(hipMemcpyAsync(d, s, n, hipMemcpyHostToDevice, stream_));
-      keep_.push_back(src);
+      // torch's pinned allocator does not see this DMA: the source stays referenced until the copy's own event has
+      // completed (not merely been enqueued), so its block cannot be recycled mid-transfer
+      hipEvent_t ev;
+      HIP_OK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+      HIP_OK(hipEventRecord(ev, stream_));
+      inflight_.push_back({src, ev});
       return;
     }
     {
@@ -85,7 +93,7 @@ class H2DEngine {
         tasks_.push_back({s + off, d + off, len});
         ++pending_;
       }
-      keep_.push_back(src);
+      staged_.push_back(src);  // pageable: read by the workers' memcpy into the pinned ring, released at drain
     }
     cv_.notify_all();
   }
@@ -98,7 +106,8 @@ class H2DEngine {
     HIP_OK(hipSetDevice(device_));
     HIP_OK(hipEventRecord(done_, stream_));
     HIP_OK(hipStreamWaitEvent(at::hip::getCurrentHIPStream().stream(), done_, 0));
-    keep_.clear();
+    staged_.clear();  // every staged piece has been memcpy'd into the ring (drain_issue)
+    retire_completed();  // pinned sources: only those whose DMA has finished
   }
 
   void synchronize() {
@@ -106,7 +115,14 @@ class H2DEngine {
     HIP_OK(hipSetDevice(device_));
     HIP_OK(hipStreamSynchronize(stream_));
     std::lock_guard<std::mutex> g(mu_);
-    keep_.clear();
+    staged_.clear();
+    retire_completed();
+  }
+
+  int64_t inflight() {
+    std::lock_guard<std::mutex> g(mu_);
+    retire_completed();
+    return (int64_t)inflight_.size();
   }
 
   int64_t slot_bytes() const { return slot_bytes_; }
@@ -123,6 +139,14 @@ class H2DEngine {
     char* dst;
     int64_t len;
   };
+
+  // caller holds mu_
+  void retire_completed() {
+    while (!inflight_.empty() && hipEventQuery(inflight_.front().ev) == hipSuccess) {
+      hipEventDestroy(inflight_.front().ev);
+      inflight_.pop_front();
+    }
+  }
 
   void drain_issue() {
     std::unique_lock<std::mutex> lk(mu_);
@@ -182,7 +206,12 @@ class H2DEngine {
   std::vector<Slot> slots_;
   std::vector<bool> reclaimable_;
   std::deque<Task> tasks_;
-  std::vector<torch::Tensor> keep_;
+  struct Inflight {
+    torch::Tensor src;
+    hipEvent_t ev;
+  };
+  std::deque<Inflight> inflight_;       // pinned sources of DMAs not yet known complete (in stream order)
+  std::vector<torch::Tensor> staged_;   // pageable sources still being copied into the ring
   std::vector<std::thread> workers_;
   std::mutex mu_;
   std::condition_variable cv_, idle_cv_;
@@ -225,6 +254,7 @@ void register_runtime(pybind11::module& m) {
       .def("copy", &H2DEngine::copy, pybind11::call_guard<pybind11::gil_scoped_release>())
       .def("wait_on_current_stream", &H2DEngine::wait_on_current_stream, pybind11::call_guard<pybind11::gil_scoped_release>())
       .def("synchronize", &H2DEngine::synchronize, pybind11::call_guard<pybind11::gil_scoped_release>())
+      .def("inflight", &H2DEngine::inflight)
       .def_property_readonly("slot_bytes", &H2DEngine::slot_bytes)
       .def_property_readonly("num_slots", &H2DEngine::num_slots);
   pybind11::class_<CollectiveSeq>(m, "CollectiveSeq")

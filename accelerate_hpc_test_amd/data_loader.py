@@ -285,19 +285,56 @@ class DevicePrefetcher:
     A daemon thread pulls CPU batches, pins them, launches non-blocking copies on `copy_stream` and records an
     event; `__next__` makes the *current* stream wait on that event (no host sync) and marks each tensor as used
     by the current stream (`record_stream`) so the caching allocator never recycles it early.
+
+    A consumer that stops early (`break`, an exception, a partially consumed iterator) must not strand the worker in
+    a blocking `queue.put` holding `depth` staged device batches: `close()` (called by `DataLoaderShard` when its
+    iterator is closed or collected, and by `__del__`) sets a stop flag the worker polls between bounded puts, drains
+    the queue and joins the thread.
     """
 
     _SENTINEL = object()
 
     def __init__(self, iterator, device: torch.device, depth: int = 2):
         self.iterator = iterator
+        device = torch.device(device)
+        if device.index is None:
+            device = torch.device(device.type, torch.cuda.current_device())
         self.device = device
         self.depth = max(1, depth)
         self.copy_stream = torch.cuda.Stream(device=device, priority=-1)
         self.queue: queue.Queue = queue.Queue(maxsize=self.depth)
         self.error: Optional[BaseException] = None
+        self._stop = threading.Event()
         self.thread = threading.Thread(target=self._worker, daemon=True)
         self.thread.start()
+
+    def _put(self, item) -> bool:
+        """Bounded put that gives up once the consumer has closed the prefetcher."""
+        while not self._stop.is_set():
+            try:
+                self.queue.put(item, timeout=0.05)
+                return True
+            except queue.Full:
+                continue
+        return False
+
+    def close(self, timeout: float = 5.0):
+        if self._stop.is_set():
+            return
+        self._stop.set()
+        while True:  # release staged batches (and unblock a worker waiting on a full queue)
+            try:
+                self.queue.get_nowait()
+            except queue.Empty:
+                break
+        if self.thread.is_alive() and threading.current_thread() is not self.thread:
+            self.thread.join(timeout)
+
+    def __del__(self):
+        try:
+            self.close(timeout=0.5)
+        except Exception:
+            pass
 
     def _pin(self, batch):
         def _p(t):
@@ -311,6 +348,8 @@ class DevicePrefetcher:
         try:
             torch.cuda.set_device(self.device)
             for batch in self.iterator:
+                if self._stop.is_set():
+                    return
                 with torch.cuda.stream(self.copy_stream):
                     try:
                         staged = send_to_device(self._pin(batch), self.device, non_blocking=True)
@@ -318,10 +357,11 @@ class DevicePrefetcher:
                         staged = send_to_device(batch, self.device, non_blocking=True)
                     event = torch.cuda.Event()
                     event.record(self.copy_stream)
-                self.queue.put((staged, event))
+                if not self._put((staged, event)):
+                    return
         except BaseException as e:  # surfaced on the consumer thread
             self.error = e
-        self.queue.put(self._SENTINEL)
+        self._put(self._SENTINEL)
 
     def __iter__(self):
         return self
@@ -395,28 +435,32 @@ class DataLoaderShard(DataLoaderStateMixin, DataLoader):
         base = super().__iter__()
         it = self._device_iter(base)
         try:
-            current = next(it)
-        except StopIteration:
-            self.end()
-            return
-        index = 0
-        self._batches_yielded = 0
-        while True:
             try:
-                nxt = next(it)
+                current = next(it)
             except StopIteration:
-                self.end_of_dataloader = True
+                self.end()
+                return
+            index = 0
+            self._batches_yielded = 0
+            while True:
+                try:
+                    nxt = next(it)
+                except StopIteration:
+                    self.end_of_dataloader = True
+                    if index >= skip:
+                        self._batches_yielded = index + 1
+                        yield current
+                    break
                 if index >= skip:
                     self._batches_yielded = index + 1
                     yield current
-                break
-            if index >= skip:
-                self._batches_yielded = index + 1
-                yield current
-            index += 1
-            current = nxt
-        self.iteration += 1
-        self.end()
+                index += 1
+                current = nxt
+            self.iteration += 1
+            self.end()
+        finally:  # also on early exit (break / exception / generator collected): stop the prefetch worker
+            if isinstance(it, DevicePrefetcher):
+                it.close()
 
     def __reduce__(self):
         args = super().__reduce__()

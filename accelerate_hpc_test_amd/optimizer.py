@@ -36,7 +36,7 @@ def move_to_device(state, device):
 
 def _fused_adam_eligible(optimizer):
     """"gpu" (HIP multi-tensor kernel), "cpu" (native OpenMP kernel over CPU-offloaded fp32 shards) or None."""
-    if os.environ.get("ACCELERATE_FUSED_ADAMW", "1") == "0":
+    if os.environ.get("ACCELERATE_FUSED_ADAMW", "1") == "0" or os.environ.get("ACCELERATE_NATIVE_KERNELS", "1") == "0":
         return None
     if type(optimizer) not in (torch.optim.AdamW, torch.optim.Adam):
         return None

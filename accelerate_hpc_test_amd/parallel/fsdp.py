@@ -48,7 +48,7 @@ import torch.nn as nn
 from ..utils.dataclasses import FullyShardedDataParallelPlugin, MixedPrecisionPolicy
 from ..utils.fault_tolerance import record_collective
 from ..utils.tracing import trace_range
-from ..ops._ext import ext
+from ..ops._ext import ext, native_enabled
 from ..ops.fp8 import Fp8Linear
 
 _ALIGN = 64  # elements; keeps every rank's shard 128-B aligned for bf16 / 256-B for fp32
@@ -1014,7 +1014,7 @@ class FSDPEngine:
 
 def _grad_update(dst: torch.Tensor, src: torch.Tensor, scale: float, accumulate: bool):
     """fp32 grad shard (=|+=) scale * src in one pass (HIP `grad_shard_update` on GPU)."""
-    if dst.is_cuda and src.numel() % 8 == 0 and os.environ.get("ACCELERATE_NATIVE_KERNELS", "1") != "0":
+    if dst.is_cuda and src.numel() % 8 == 0 and native_enabled():
         ext().grad_shard_update(dst, src.contiguous(), float(scale), bool(accumulate))
     elif accumulate:
         dst.add_(src.to(dst.dtype), alpha=scale)
@@ -1124,7 +1124,7 @@ class _FusedWgradLinearFn(torch.autograd.Function):
         # contiguous along the contraction) instead of the both-token-major one. Llama-3-8B layer, four GEMMs
         # (tools/bench_wgrad_layout.py): fp32 output (world size 1) 2.93 vs 3.50 ms, bf16 output (flat grad buffer,
         # world size > 1) 2.86 vs 3.44 ms; the HIP transpose costs ~0.2 ms.
-        ctx.x_transposed = (_WGRAD_XT and x2.is_cuda and x2.dtype == torch.bfloat16 and x2.is_contiguous()
+        ctx.x_transposed = (_WGRAD_XT and x2.is_cuda and x2.dtype == torch.bfloat16 and x2.is_contiguous() and native_enabled()
                             and x2.shape[0] % 64 == 0 and x2.shape[1] % 64 == 0)
         ctx.save_for_backward(ext().transpose_bf16(x2) if ctx.x_transposed else x, weight)
         ctx.slot = slot

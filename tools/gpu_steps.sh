@@ -42,6 +42,8 @@ for step in "$@"; do
     prof8b_fp8) prof prof8b_fp8 600 bench.py --steps 3 --warmup 2 --precision fp8 $BENCH_ARGS ;;
     prof_mixtral_fp8) prof prof_mixtral_fp8 600 bench.py --model mixtral-8x7b-4l --steps 2 --warmup 1 --precision fp8 ;;
     attn) run attn 300 python tools/bench_attn.py ;;
+    attn_long) run attn_long 300 python tools/bench_attn.py --S 32768 --iters 3 ;;
+    pmc_attn) run pmc_attn 200 bash tools/pmc_attn.sh ;;
     gemm) run gemm 300 python tools/bench_gemm.py ;;
     big70b) run big70b 900 python tools/bench_big_model.py --model llama3-70b --tokens 2048 --iters 3 ;;
     big70b_offload) run big70b_offload 900 python tools/bench_big_model.py --model llama3-70b --gpu-mem 100GiB --tokens 2048 --iters 3 ;;

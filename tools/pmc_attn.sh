@@ -1,0 +1,12 @@
+#!/bin/bash
+# Stall anatomy of the attention kernels (one rocprofv3 --pmc pass, <= 8 SQ counters):
+#   gpurun -- bash tools/pmc_attn.sh [bench_attn args]
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out/pmc
+export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
+CTR="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES"
+rm -rf gpurun_out/pmc/attn_stall
+timeout -s KILL 120 rocprofv3 --pmc $CTR --output-format csv -d gpurun_out/pmc/attn_stall -o run -- python3 tools/bench_attn.py --iters 2 "$@" > gpurun_out/pmc/attn_stall.log 2>&1
+rc=$?; echo "pmc rc=$rc"; tail -3 gpurun_out/pmc/attn_stall.log | cut -c1-300
+[ $rc -eq 0 ] && python3 tools/pmc_summary.py --stall gpurun_out/pmc/attn_stall
+exit $rc

@@ -24,7 +24,37 @@ def short(name: str) -> str:
     return name[:72].replace("|", "/")
 
 
+def stall(dirs):
+    """Wave-cycle anatomy (SQ_* counters count quad-cycles except SQ_VALU_MFMA_BUSY_CYCLES): share of wave cycles
+    parked on s_waitcnt / barrier (WAIT_ANY), issue-stalled (WAIT_INST_ANY) and issuing (ACTIVE_INST_ANY), plus VALU
+    and LDS instruction-issue shares and MFMA busy per SIMD-cycle of the kernel's busy time."""
+    for d in dirs:
+        files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+        ctr = defaultdict(lambda: defaultdict(float))
+        wall = defaultdict(dict)
+        for f in files:
+            for r in csv.DictReader(open(f)):
+                k = short(r["Kernel_Name"])
+                ctr[k][r["Counter_Name"]] += float(r["Counter_Value"])
+                wall[k][r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        print(f"### {d}\n")
+        print("| kernel | dispatches | wall ms | wait (waitcnt/barrier) % | issue-stall % | issuing % | VALU issue % | LDS issue % | MFMA busy % of SQ busy |")
+        print("|---|---:|---:|---:|---:|---:|---:|---:|---:|")
+        for k, c in sorted(ctr.items(), key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", 0)):
+            wc = c.get("SQ_WAVE_CYCLES", 0)
+            if not wc:
+                continue
+            busy = c.get("SQ_BUSY_CYCLES", 0)
+            pct = lambda n: 100 * c.get(n, 0) / wc  # noqa: E731
+            mf = 100 * c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / (busy * 4 * 4) if busy else 0
+            print(f"| `{k}` | {len(wall[k])} | {sum(wall[k].values()) / 1e6:.2f} | {pct('SQ_WAIT_ANY'):.1f} | {pct('SQ_WAIT_INST_ANY'):.1f} | "
+                  f"{pct('SQ_ACTIVE_INST_ANY'):.1f} | {pct('SQ_ACTIVE_INST_VALU'):.1f} | {pct('SQ_ACTIVE_INST_LDS'):.1f} | {mf:.1f} |")
+        print()
+
+
 def main(dirs):
+    if dirs and dirs[0] == "--stall":
+        return stall(dirs[1:])
     for d in dirs:
         files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
         ctr = defaultdict(lambda: defaultdict(float))
