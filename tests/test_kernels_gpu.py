@@ -123,6 +123,14 @@ def test_flash_attention(causal, B, S, Hq, Hkv):
         assert err < 3e-2, (name, err)
 
 
+@pytest.mark.parametrize("causal,B,S,Hq,Hkv", [(True, 1, 8192, 32, 8), (False, 1, 8192, 32, 8), (True, 1, 32768, 4, 1)])
+def test_flash_attention_bench_and_long_shapes(causal, B, S, Hq, Hkv):
+    """The headline bench's exact attention shape (S=8192, 32 q / 8 kv heads, D=128) and a 32k-token causal sequence
+    (the single-GPU long-context anchor) against the fp32 reference, forward and backward."""
+    test_flash_attention(causal, B, S, Hq, Hkv)
+    torch.cuda.empty_cache()
+
+
 def test_flash_attention_lse():
     torch.manual_seed(0)
     B, S, H, D = 1, 256, 2, 128

@@ -34,6 +34,8 @@ for step in "$@"; do
     bench8b_sharded) run bench8b_sharded 600 python bench.py --steps 5 --warmup 2 --fsdp-force-sharded $BENCH_ARGS ;;
     prof8b_sharded) OVERLAP_PATTERN="nccl|rccl|copyBuffer" PROF_EXTRA=--memory-copy-trace prof prof8b_sharded 600 bench.py --steps 3 --warmup 2 --fsdp-force-sharded $BENCH_ARGS ;;
     bench8b_offload) run bench8b_offload 900 python bench.py --steps 2 --warmup 1 --fsdp-cpu-offload --verbose $BENCH_ARGS ;;
+    long32k) run long32k 900 python bench.py --seq 32768 --steps 2 --warmup 1 --activation-checkpointing --verbose $BENCH_ARGS ;;
+    long64k) run long64k 900 python bench.py --seq 65536 --steps 2 --warmup 1 --activation-checkpointing --verbose $BENCH_ARGS ;;
     bench8b_fp8) run bench8b_fp8 600 python bench.py --steps 5 --warmup 2 --precision fp8 $BENCH_ARGS ;;
     bench8b_ddp) run bench8b_ddp 600 python bench.py --parallel ddp --steps 5 --warmup 2 $BENCH_ARGS ;;
     mixtral_bf16) run mixtral_bf16 600 python bench.py --model mixtral-8x7b-4l --steps 3 --warmup 2 $BENCH_ARGS ;;
