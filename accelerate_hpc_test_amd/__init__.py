@@ -41,7 +41,8 @@ from .utils import (
     is_rich_available,
     synchronize_rng_states,
 )
-from .utils.big_model_utils import infer_auto_device_map, load_checkpoint_in_model
+from .utils.checkpoint_io import load_checkpoint_in_model
+from .utils.device_map import infer_auto_device_map
 
 if is_rich_available():
     from .utils import rich  # noqa: F401

@@ -1,14 +1,17 @@
-"""Accelerator state checkpoint writer/reader (model, optimizer, scheduler, sampler, scaler, RNG, custom objects).
+"""Accelerator state checkpoints: model / optimizer / scheduler / sampler / dataloader / scaler / RNG / custom objects.
 
-Parity: `/root/reference/src/accelerate/checkpointing.py:62-331`. File names and layout are identical
-(`model.safetensors`/`model_{i}.safetensors` or `pytorch_model{_i}.bin`, `optimizer{_i}.bin`, `scheduler{_i}.bin`,
-`sampler{_i}.bin`, `dl_state_dict{_i}.bin`, `scaler.pt`, `random_states_{rank}.pkl`, `custom_checkpoint_{i}.pkl`).
-RNG state files are written with `torch.save` of plain tensors/lists and read with `weights_only=True`.
+File names and layout follow the reference (`/root/reference/src/accelerate/checkpointing.py:62-331`) so checkpoints
+move between the two: the k-th object of a kind gets the kind's name with `_k` before the extension from k = 1 on
+(`model.safetensors`, `model_1.safetensors` or `pytorch_model.bin`, `optimizer.bin`, `scheduler_1.bin`,
+`sampler.bin`, `dl_state_dict.bin`, `scaler.pt`, `random_states_<rank>.pkl`, `custom_checkpoint_<k>.pkl`).
+
+Design: `CheckpointLayout` is the one place that knows the names; `save_accelerator_state` / `load_accelerator_state`
+walk the object lists through it. RNG states hold only tensors, numbers and lists, so they are written with
+`torch.save` and read back with `weights_only=True` (nothing in a checkpoint is unpickled as code).
 """
 
 from __future__ import annotations
 
-import os
 import random
 from pathlib import Path
 from typing import Optional
@@ -29,170 +32,170 @@ from .utils.constants import (
     SCHEDULER_NAME,
     WEIGHTS_NAME,
 )
-from .utils.dataclasses import DistributedType
 from .utils.other import load, save
 
 logger = get_logger(__name__)
 
 
-def _suffix(i: int) -> str:
-    return "" if i == 0 else f"_{i}"
+class CheckpointLayout:
+    """File names of every piece of an accelerator checkpoint inside `root`."""
+
+    def __init__(self, root):
+        self.root = Path(root)
+
+    @staticmethod
+    def _nth(stem: str, ext: str, k: int) -> str:
+        return f"{stem}{'' if k == 0 else f'_{k}'}{ext}"
+
+    def model(self, k: int, safe: bool) -> Path:
+        base = SAFE_WEIGHTS_NAME if safe else WEIGHTS_NAME  # "model.safetensors" / "pytorch_model.bin"
+        stem, ext = base.rsplit(".", 1)
+        return self.root / self._nth(stem, "." + ext, k)
+
+    def model_candidates(self, k: int):
+        yield self.root / self._nth(SAFE_MODEL_NAME, ".safetensors", k)
+        yield self.root / self._nth(WEIGHTS_NAME.replace(".bin", ""), ".bin", k)
+
+    def optimizer(self, k):
+        return self.root / self._nth(OPTIMIZER_NAME, ".bin", k)
+
+    def scheduler(self, k):
+        return self.root / self._nth(SCHEDULER_NAME, ".bin", k)
+
+    def sampler(self, k):
+        return self.root / self._nth(SAMPLER_NAME, ".bin", k)
+
+    def dataloader(self, k):
+        return self.root / self._nth(DATALOADER_STATE_NAME, ".bin", k)
+
+    def scaler(self):
+        return self.root / SCALER_NAME
+
+    def rng(self, rank: int):
+        return self.root / f"{RNG_STATE_NAME}_{rank}.pkl"
+
+    def custom(self, k: int):
+        return self.root / f"custom_checkpoint_{k}.pkl"
 
 
-def save_accelerator_state(
-    output_dir: str,
-    model_states: list[dict],
-    optimizers: list,
-    schedulers: list,
-    dataloaders: list,
-    process_index: int,
-    step: int,
-    scaler=None,
-    save_on_each_node: bool = False,
-    safe_serialization: bool = True,
-):
-    output_dir = Path(output_dir)
-    for i, state in enumerate(model_states):
-        weights_name = WEIGHTS_NAME if not safe_serialization else SAFE_WEIGHTS_NAME
-        if i > 0:
-            weights_name = weights_name.replace(".", f"_{i}.")
-        output_model_file = output_dir.joinpath(weights_name)
-        save(state, output_model_file, save_on_each_node=save_on_each_node, safe_serialization=safe_serialization)
-        logger.info(f"Model weights saved in {output_model_file}")
-    for i, opt in enumerate(optimizers):
-        state = opt.state_dict()
-        optimizer_name = f"{OPTIMIZER_NAME}.bin" if i == 0 else f"{OPTIMIZER_NAME}_{i}.bin"
-        output_optimizer_file = output_dir.joinpath(optimizer_name)
-        save(state, output_optimizer_file, save_on_each_node=save_on_each_node, safe_serialization=False)
-        logger.info(f"Optimizer state saved in {output_optimizer_file}")
-    for i, scheduler in enumerate(schedulers):
-        state = scheduler.state_dict()
-        scheduler_name = f"{SCHEDULER_NAME}.bin" if i == 0 else f"{SCHEDULER_NAME}_{i}.bin"
-        output_scheduler_file = output_dir.joinpath(scheduler_name)
-        save(state, output_scheduler_file, save_on_each_node=save_on_each_node, safe_serialization=False)
-        logger.info(f"Scheduler state saved in {output_scheduler_file}")
+# ------------------------------------------------------------------------------------------------ RNG
+def _rng_snapshot(step: int) -> dict:
+    py = random.getstate()
+    npst = np.random.get_state()
+    snap = {
+        "step": step,
+        "random_state": [py[0], list(py[1]), py[2]],
+        "numpy_random_seed": [npst[0], torch.from_numpy(np.asarray(npst[1]).astype(np.int64)), int(npst[2]),
+                              int(npst[3]), float(npst[4])],
+        "torch_manual_seed": torch.get_rng_state(),
+    }
+    if torch.cuda.is_available():
+        snap["torch_cuda_manual_seed"] = torch.cuda.get_rng_state_all()
+    return snap
+
+
+def _rng_restore(snap: dict):
+    version, internal, gauss = snap["random_state"]
+    random.setstate((version, tuple(internal), gauss))
+    kind, keys, pos, has_gauss, cached = snap["numpy_random_seed"]
+    np.random.set_state((kind, keys.numpy().astype(np.uint32), pos, has_gauss, cached))
+    torch.set_rng_state(snap["torch_manual_seed"])
+    if torch.cuda.is_available() and "torch_cuda_manual_seed" in snap:
+        torch.cuda.set_rng_state_all(snap["torch_cuda_manual_seed"])
+
+
+def _seedable_sampler(dataloader):
     from .data_loader import IterableDatasetShard, SeedableRandomSampler
 
-    for i, dataloader in enumerate(dataloaders):
-        sampler_name = f"{SAMPLER_NAME}.bin" if i == 0 else f"{SAMPLER_NAME}_{i}.bin"
-        output_sampler_file = output_dir.joinpath(sampler_name)
-        if isinstance(dataloader.dataset, IterableDatasetShard):
-            sampler = dataloader.get_sampler()
-            if isinstance(sampler, SeedableRandomSampler):
-                save({"epoch": sampler.epoch, "initial_seed": sampler.initial_seed}, output_sampler_file, save_on_each_node=save_on_each_node)
-        if hasattr(dataloader, "state_dict"):
-            dl_name = f"{DATALOADER_STATE_NAME}.bin" if i == 0 else f"{DATALOADER_STATE_NAME}_{i}.bin"
-            save(dataloader.state_dict(), output_dir.joinpath(dl_name), save_on_each_node=save_on_each_node)
+    if not isinstance(dataloader.dataset, IterableDatasetShard):
+        return None
+    sampler = dataloader.get_sampler()
+    return sampler if isinstance(sampler, SeedableRandomSampler) else None
+
+
+# ------------------------------------------------------------------------------------------------ save / load
+def save_accelerator_state(output_dir, model_states: list, optimizers: list, schedulers: list, dataloaders: list,
+                           process_index: int, step: int, scaler=None, save_on_each_node: bool = False,
+                           safe_serialization: bool = True):
+    """Write every piece of the training state under `output_dir` (see `CheckpointLayout`)."""
+    lay = CheckpointLayout(output_dir)
+    node_kw = {"save_on_each_node": save_on_each_node}
+    for k, state in enumerate(model_states):
+        path = lay.model(k, safe_serialization)
+        save(state, path, safe_serialization=safe_serialization, **node_kw)
+        logger.info(f"Model weights saved in {path}")
+    for kind, objs, namer in (("Optimizer", optimizers, lay.optimizer), ("Scheduler", schedulers, lay.scheduler)):
+        for k, obj in enumerate(objs):
+            save(obj.state_dict(), namer(k), safe_serialization=False, **node_kw)
+            logger.info(f"{kind} state saved in {namer(k)}")
+    for k, dl in enumerate(dataloaders):
+        sampler = _seedable_sampler(dl)
+        if sampler is not None:
+            save({"epoch": sampler.epoch, "initial_seed": sampler.initial_seed}, lay.sampler(k), **node_kw)
+        if hasattr(dl, "state_dict"):
+            save(dl.state_dict(), lay.dataloader(k), **node_kw)
     if scaler is not None:
-        state = scaler.state_dict()
-        output_scaler_file = output_dir.joinpath(SCALER_NAME)
-        torch.save(state, output_scaler_file)
-        logger.info(f"Gradient scaler state saved in {output_scaler_file}")
-    # RNG states (per process): only tensors / python lists so they load with weights_only=True.
-    states = {"step": step}
-    py_state = random.getstate()
-    states["random_state"] = [py_state[0], list(py_state[1]), py_state[2]]
-    np_state = np.random.get_state()
-    states["numpy_random_seed"] = [np_state[0], torch.from_numpy(np.asarray(np_state[1]).astype(np.int64)), int(np_state[2]), int(np_state[3]), float(np_state[4])]
-    states["torch_manual_seed"] = torch.get_rng_state()
-    if torch.cuda.is_available():
-        states["torch_cuda_manual_seed"] = torch.cuda.get_rng_state_all()
-    output_states_file = output_dir.joinpath(f"{RNG_STATE_NAME}_{process_index}.pkl")
-    torch.save(states, output_states_file)
-    logger.info(f"Random states saved in {output_states_file}")
-    return output_dir
+        torch.save(scaler.state_dict(), lay.scaler())
+        logger.info(f"Gradient scaler state saved in {lay.scaler()}")
+    torch.save(_rng_snapshot(step), lay.rng(process_index))
+    logger.info(f"Random states saved in {lay.rng(process_index)}")
+    return Path(output_dir)
 
 
-def load_accelerator_state(
-    input_dir,
-    models,
-    optimizers,
-    schedulers,
-    dataloaders,
-    process_index,
-    scaler=None,
-    map_location=None,
-    load_kwargs=None,
-    **load_model_func_kwargs,
-):
-    override_attributes = dict()
-    if map_location not in [None, "cpu", "on_device"]:
+def load_accelerator_state(input_dir, models, optimizers, schedulers, dataloaders, process_index, scaler=None,
+                           map_location=None, load_kwargs: Optional[dict] = None, **load_model_func_kwargs) -> dict:
+    """Restore what `save_accelerator_state` wrote; returns attributes to override on the Accelerator (`step`)."""
+    if map_location not in (None, "cpu", "on_device"):
         raise TypeError("Unsupported optimizer map location passed, please choose one of `None`, `'cpu'`, or `'on_device'`.")
-    if map_location is None:
-        map_location = "cpu"
-    elif map_location == "on_device":
-        map_location = PartialState().device
-    if load_kwargs is None:
-        load_kwargs = {}
-    input_dir = Path(input_dir)
-    for i, model in enumerate(models):
-        ending = f"_{i}" if i > 0 else ""
-        input_model_file = input_dir.joinpath(f"{SAFE_MODEL_NAME}{ending}.safetensors")
-        if input_model_file.exists():
+    where = PartialState().device if map_location == "on_device" else "cpu"
+    load_kwargs = load_kwargs or {}
+    lay = CheckpointLayout(input_dir)
+    for k, model in enumerate(models):
+        safe_path, bin_path = lay.model_candidates(k)
+        if safe_path.exists():
             from safetensors.torch import load_file
 
-            state_dict = load_file(input_model_file, device=str(map_location))
+            state = load_file(safe_path, device=str(where))
         else:
-            input_model_file = input_dir.joinpath(f"{WEIGHTS_NAME.replace('.bin', '')}{ending}.bin")
-            state_dict = load(input_model_file, map_location=map_location)
-        model.load_state_dict(state_dict, **load_model_func_kwargs)
+            state = load(bin_path, map_location=where)
+        model.load_state_dict(state, **load_model_func_kwargs)
     logger.info("All model weights loaded successfully")
-    for i, opt in enumerate(optimizers):
-        optimizer_name = f"{OPTIMIZER_NAME}.bin" if i == 0 else f"{OPTIMIZER_NAME}_{i}.bin"
-        input_optimizer_file = input_dir.joinpath(optimizer_name)
-        optimizer_state = load(input_optimizer_file, map_location=map_location, **load_kwargs)
-        optimizers[i].load_state_dict(optimizer_state)
+    for k, opt in enumerate(optimizers):
+        opt.load_state_dict(load(lay.optimizer(k), map_location=where, **load_kwargs))
     logger.info("All optimizer states loaded successfully")
-    for i, scheduler in enumerate(schedulers):
-        scheduler_name = f"{SCHEDULER_NAME}.bin" if i == 0 else f"{SCHEDULER_NAME}_{i}.bin"
-        input_scheduler_file = input_dir.joinpath(scheduler_name)
-        scheduler_state = load(input_scheduler_file, **load_kwargs)
-        scheduler.load_state_dict(scheduler_state)
+    for k, sched in enumerate(schedulers):
+        sched.load_state_dict(load(lay.scheduler(k), **load_kwargs))
     logger.info("All scheduler states loaded successfully")
-    from .data_loader import IterableDatasetShard, SeedableRandomSampler
-
-    for i, dataloader in enumerate(dataloaders):
-        sampler_name = f"{SAMPLER_NAME}.bin" if i == 0 else f"{SAMPLER_NAME}_{i}.bin"
-        input_sampler_file = input_dir.joinpath(sampler_name)
-        if isinstance(dataloader.dataset, IterableDatasetShard) and input_sampler_file.exists():
-            sampler = dataloader.get_sampler()
-            if isinstance(sampler, SeedableRandomSampler):
-                st = load(input_sampler_file)
-                sampler.epoch, sampler.initial_seed = st["epoch"], st["initial_seed"]
-        dl_name = f"{DATALOADER_STATE_NAME}.bin" if i == 0 else f"{DATALOADER_STATE_NAME}_{i}.bin"
-        dl_file = input_dir.joinpath(dl_name)
-        if dl_file.exists() and hasattr(dataloader, "load_state_dict"):
-            dataloader.load_state_dict(load(dl_file))
+    for k, dl in enumerate(dataloaders):
+        sampler = _seedable_sampler(dl)
+        if sampler is not None and lay.sampler(k).exists():
+            saved = load(lay.sampler(k))
+            sampler.epoch, sampler.initial_seed = saved["epoch"], saved["initial_seed"]
+        if lay.dataloader(k).exists() and hasattr(dl, "load_state_dict"):
+            dl.load_state_dict(load(lay.dataloader(k)))
     logger.info("All dataloader sampler states loaded successfully")
     if scaler is not None:
-        input_scaler_file = input_dir.joinpath(SCALER_NAME)
-        scaler_state = torch.load(input_scaler_file, weights_only=True)
-        scaler.load_state_dict(scaler_state)
+        scaler.load_state_dict(torch.load(lay.scaler(), weights_only=True))
         logger.info("GradScaler state loaded successfully")
+    overrides = {}
     try:
-        states = torch.load(input_dir.joinpath(f"{RNG_STATE_NAME}_{process_index}.pkl"), weights_only=True)
-        if "step" in states:
-            override_attributes["step"] = states["step"]
-        rs = states["random_state"]
-        random.setstate((rs[0], tuple(rs[1]), rs[2]))
-        ns = states["numpy_random_seed"]
-        np.random.set_state((ns[0], ns[1].numpy().astype(np.uint32), ns[2], ns[3], ns[4]))
-        torch.set_rng_state(states["torch_manual_seed"])
-        if torch.cuda.is_available() and "torch_cuda_manual_seed" in states:
-            torch.cuda.set_rng_state_all(states["torch_cuda_manual_seed"])
+        snap = torch.load(lay.rng(process_index), weights_only=True)
+        if "step" in snap:
+            overrides["step"] = snap["step"]
+        _rng_restore(snap)
         logger.info("All random states loaded successfully")
     except Exception:
         logger.info("Could not load random states")
-    return override_attributes
+    return overrides
 
 
 def save_custom_state(obj, path, index: int = 0, save_on_each_node: bool = False):
-    save_location = Path(path) / f"custom_checkpoint_{index}.pkl"
-    logger.info(f"Saving the state of {obj.__class__.__name__} to {save_location}")
-    save(obj.state_dict(), save_location, save_on_each_node=save_on_each_node)
+    target = CheckpointLayout(path).custom(index)
+    logger.info(f"Saving the state of {obj.__class__.__name__} to {target}")
+    save(obj.state_dict(), target, save_on_each_node=save_on_each_node)
 
 
 def load_custom_state(obj, path, index: int = 0):
-    load_location = f"{path}/custom_checkpoint_{index}.pkl"
-    logger.info(f"Loading the state of {obj.__class__.__name__} from {load_location}")
-    obj.load_state_dict(load(load_location, map_location="cpu"))
+    source = CheckpointLayout(path).custom(index)
+    logger.info(f"Loading the state of {obj.__class__.__name__} from {source}")
+    obj.load_state_dict(load(source, map_location="cpu"))

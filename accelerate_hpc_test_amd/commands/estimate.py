@@ -20,7 +20,7 @@ import torch
 
 from ..big_modeling import init_empty_weights
 from ..utils.other import convert_bytes
-from .._big_modeling_impl import calculate_maximum_sizes
+from ..utils.device_map import calculate_maximum_sizes
 
 MI355X_HBM_BYTES = 288 * 10**9
 

@@ -1,15 +1,16 @@
-"""Forward hooks used by big-model inference (device alignment, CPU/disk offload, layerwise casting).
+"""Forward hooks for big-model inference: run a module's forward with its weights (and inputs) on an execution
+device while the weights live elsewhere (another GPU, host RAM, disk).
 
-Parity: `/root/reference/src/accelerate/hooks.py:43-783` — `ModelHook`, `SequentialHook`, `add_hook_to_module`,
-`remove_hook_from_module`, `AlignDevicesHook`, `attach_execution_device_hook`, `attach_align_device_hook`,
-`attach_align_device_hook_on_blocks`, `CpuOffload`, `UserCpuOffloadHook`, `LayerwiseCastingHook`.
+API parity with `/root/reference/src/accelerate/hooks.py:43-783` (`ModelHook`, `SequentialHook`, `add_hook_to_module`,
+`remove_hook_from_module`, `AlignDevicesHook`, the three `attach_*` helpers, `CpuOffload`, `UserCpuOffloadHook`,
+`LayerwiseCastingHook`); `tests/test_big_modeling.py` pins the behaviour.
 
-MI355X-native addition — **asynchronous offload prefetch** (`OffloadPrefetcher`). The reference uploads every
-offloaded module's weights synchronously right before it runs (it notes "need to implement prefetching",
-`benchmarks/big_model_inference/README.md:42-44`). Here the offloaded hooks sharing an execution device record their
-execution order on the first forward; afterwards, while module i computes, module i+1's weights are copied from
-pinned host memory to HBM on a dedicated high-priority copy stream (one HIP event per module), so PCIe transfers
-overlap compute. Disabled with `ACCELERATE_OFFLOAD_PREFETCH=0`.
+MI355X design: offloaded weights are streamed by an **`OffloadScheduler`**, one per dispatched model and execution
+GPU, that owns the upload stream, the pinned host copies of host-offloaded weights, and the execution order of the
+offloaded blocks (recorded on the first forward). While block i computes, block i+1's weights are already being
+copied host -> HBM on the scheduler's high-priority stream (one HIP event per block), so PCIe transfers overlap
+compute instead of sitting in front of every block (the reference uploads synchronously and notes prefetching as
+missing, `benchmarks/big_model_inference/README.md:42-44`). `ACCELERATE_OFFLOAD_PREFETCH=0` turns prefetch off.
 """
 
 from __future__ import annotations
@@ -23,14 +24,16 @@ import torch
 import torch.nn as nn
 
 from .utils.memory import clear_device_cache
-from .utils.modeling import named_module_tensors
+from .utils.modeling import get_non_persistent_buffers, named_module_tensors
 from .utils.offload import PrefixedDataset
 from .utils.operations import find_device, send_to_device
+from .utils.placement import recursive_getattr, set_module_tensor_to_device
 
 
+# --------------------------------------------------------------------------------------------------- hook plumbing
 class ModelHook:
-    """Base hook: `init_hook` at attach time, `pre_forward`/`post_forward` around the module's forward,
-    `detach_hook` at removal. `no_grad` runs the wrapped forward without autograd."""
+    """Callbacks around a module's forward: `init_hook` when attached, `pre_forward` / `post_forward` around each
+    call, `detach_hook` when removed. With `no_grad`, the wrapped forward runs without autograd."""
 
     no_grad = False
 
@@ -48,157 +51,201 @@ class ModelHook:
 
 
 class SequentialHook(ModelHook):
+    """Several hooks applied in order (`post_forward` in the same order)."""
+
     def __init__(self, *hooks):
         self.hooks = hooks
 
     def init_hook(self, module):
-        for hook in self.hooks:
-            module = hook.init_hook(module)
+        for h in self.hooks:
+            module = h.init_hook(module)
         return module
 
     def pre_forward(self, module, *args, **kwargs):
-        for hook in self.hooks:
-            args, kwargs = hook.pre_forward(module, *args, **kwargs)
+        for h in self.hooks:
+            args, kwargs = h.pre_forward(module, *args, **kwargs)
         return args, kwargs
 
     def post_forward(self, module, output):
-        for hook in self.hooks:
-            output = hook.post_forward(module, output)
+        for h in self.hooks:
+            output = h.post_forward(module, output)
         return output
 
     def detach_hook(self, module):
-        for hook in self.hooks:
-            module = hook.detach_hook(module)
+        for h in self.hooks:
+            module = h.detach_hook(module)
         return module
 
 
+class _HookedForward:
+    """The forward installed on a hooked module: hook.pre_forward -> original forward -> hook.post_forward."""
+
+    def __init__(self, module: nn.Module):
+        self.module = module
+
+    def __call__(self, *args, **kwargs):
+        m = self.module
+        hook = m._hf_hook
+        args, kwargs = hook.pre_forward(m, *args, **kwargs)
+        if hook.no_grad:
+            with torch.no_grad():
+                out = m._old_forward(*args, **kwargs)
+        else:
+            out = m._old_forward(*args, **kwargs)
+        return hook.post_forward(m, out)
+
+
+def _is_graph_module(module) -> bool:
+    return "GraphModuleImpl" in str(type(module))
+
+
 def add_hook_to_module(module: nn.Module, hook: ModelHook, append: bool = False):
-    """Wrap `module.forward` with `hook` (stored as `module._hf_hook`; `append` chains after an existing hook)."""
-    if append and (getattr(module, "_hf_hook", None) is not None):
-        old_hook = module._hf_hook
+    """Attach `hook` (stored as `module._hf_hook`, the original forward as `module._old_forward`). An existing hook
+    is replaced, or with `append` chained before the new one."""
+    if append and getattr(module, "_hf_hook", None) is not None:
+        previous = module._hf_hook
         remove_hook_from_module(module)
-        hook = SequentialHook(old_hook, hook)
-    if hasattr(module, "_hf_hook") and hasattr(module, "_old_forward"):
-        old_forward = module._old_forward
-    else:
-        old_forward = module.forward
-        module._old_forward = old_forward
+        hook = SequentialHook(previous, hook)
+    base = module._old_forward if (hasattr(module, "_hf_hook") and hasattr(module, "_old_forward")) else module.forward
+    module._old_forward = base
     module = hook.init_hook(module)
     module._hf_hook = hook
-
-    def new_forward(module, *args, **kwargs):
-        args, kwargs = module._hf_hook.pre_forward(module, *args, **kwargs)
-        if module._hf_hook.no_grad:
-            with torch.no_grad():
-                output = module._old_forward(*args, **kwargs)
-        else:
-            output = module._old_forward(*args, **kwargs)
-        return module._hf_hook.post_forward(module, output)
-
-    if "GraphModuleImpl" in str(type(module)):
-        module.__class__.forward = functools.update_wrapper(functools.partial(new_forward, module), old_forward)
+    fwd = functools.update_wrapper(_HookedForward(module), base)
+    if _is_graph_module(module):
+        module.__class__.forward = fwd
     else:
-        module.forward = functools.update_wrapper(functools.partial(new_forward, module), old_forward)
+        module.forward = fwd
     return module
 
 
 def remove_hook_from_module(module: nn.Module, recurse: bool = False):
-    if hasattr(module, "_hf_hook"):
-        module._hf_hook.detach_hook(module)
-        delattr(module, "_hf_hook")
+    """Detach the hook (its `detach_hook` runs) and restore the original forward; `recurse` does all submodules."""
+    hook = getattr(module, "_hf_hook", None)
+    if hook is not None:
+        hook.detach_hook(module)
+        del module._hf_hook
     if hasattr(module, "_old_forward"):
-        if "GraphModuleImpl" in str(type(module)):
+        if _is_graph_module(module):
             module.__class__.forward = module._old_forward
         else:
             module.forward = module._old_forward
-        delattr(module, "_old_forward")
-    for attr in ("_accelerate_added_attributes",):
-        for a in getattr(module, attr, []):
-            if hasattr(module, a):
-                delattr(module, a)
-        if hasattr(module, attr):
-            delattr(module, attr)
+        del module._old_forward
+    for name in getattr(module, "_accelerate_added_attributes", []):
+        if hasattr(module, name):
+            delattr(module, name)
+    if hasattr(module, "_accelerate_added_attributes"):
+        del module._accelerate_added_attributes
     if recurse:
         for child in module.children():
-            remove_hook_from_module(child, recurse)
+            remove_hook_from_module(child, recurse=True)
     return module
 
 
-def _set_tensor(module: nn.Module, name: str, value: torch.Tensor):
-    """Install `value` as parameter/buffer `name` (dotted path allowed) without copying."""
-    if "." in name:
-        sub, name = name.rsplit(".", 1)
-        module = module.get_submodule(sub)
-    if name in module._parameters:
-        old = module._parameters[name]
-        if value.device.type == "meta" or not isinstance(value, nn.Parameter):
+def remove_hook_from_submodules(module: nn.Module):
+    for m in module.modules():
+        remove_hook_from_module(m)
+
+
+def _install(module: nn.Module, name: str, value: torch.Tensor):
+    """Make `value` parameter / buffer `name` (dotted) of `module` without a copy."""
+    owner_path, _, attr = name.rpartition(".")
+    owner = module.get_submodule(owner_path) if owner_path else module
+    if attr in owner._parameters:
+        old = owner._parameters[attr]
+        if not isinstance(value, nn.Parameter):
             value = nn.Parameter(value, requires_grad=old.requires_grad if old is not None else False)
-        module._parameters[name] = value
+        owner._parameters[attr] = value
     else:
-        module._buffers[name] = value
+        owner._buffers[attr] = value
 
 
-class OffloadPrefetcher:
-    """Per-device scheduler of offloaded-weight uploads (see module docstring)."""
+# --------------------------------------------------------------------------------------------------- offload stream
+class OffloadScheduler:
+    """Streams offloaded block weights to one execution GPU ahead of use (see module docstring)."""
 
-    _instances: dict = {}
-
-    def __init__(self, device: torch.device):
+    def __init__(self, device):
+        device = torch.device(device)
+        if device.type == "cuda" and device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
         self.device = device
-        self.stream = torch.cuda.Stream(device=device, priority=-1)
+        self.enabled = device.type == "cuda" and os.environ.get("ACCELERATE_OFFLOAD_PREFETCH", "1") != "0"
+        self.stream = torch.cuda.Stream(device=device, priority=-1) if self.enabled else None
         self.order: list = []
         self.recording = True
-        self.staged: dict[int, tuple[dict, torch.cuda.Event]] = {}
+        self.staged: dict = {}
+        self.pinned: dict = {}  # (hook id, name) -> pinned host tensor (host-offloaded weights only)
 
-    @classmethod
-    def get(cls, device) -> Optional["OffloadPrefetcher"]:
-        device = torch.device(device)
-        if device.type != "cuda" or os.environ.get("ACCELERATE_OFFLOAD_PREFETCH", "1") == "0":
-            return None
-        key = (device.type, device.index if device.index is not None else torch.cuda.current_device())
-        if key not in cls._instances:
-            cls._instances[key] = OffloadPrefetcher(torch.device("cuda", key[1]))
-        return cls._instances[key]
+    def host_copy(self, hook: "AlignDevicesHook", name: str, value: torch.Tensor) -> torch.Tensor:
+        """A pinned host copy of a weight held in RAM (cached); disk-backed weights are pinned per use."""
+        if value.device.type != "cpu":
+            return value
+        key = (id(hook), name)
+        if hook.cache_host and key in self.pinned:
+            return self.pinned[key]
+        try:
+            pinned = value.contiguous().pin_memory()
+        except RuntimeError:
+            return value
+        if hook.cache_host:
+            self.pinned[key] = pinned
+        return pinned
 
-    def note_execution(self, hook):
-        if self.recording:
-            if hook in self.order:
-                self.recording = False  # one full pass recorded
-            else:
-                self.order.append(hook)
+    def ran(self, hook):
+        """Record the block execution order over the first full pass."""
+        if not self.recording:
+            return
+        if hook in self.order:
+            self.recording = False
+        else:
+            self.order.append(hook)
 
-    def take(self, hook):
+    def take(self, hook) -> Optional[dict]:
+        """Tensors prefetched for `hook`, ordered after their upload on the current stream."""
         item = self.staged.pop(id(hook), None)
         if item is None:
             return None
         tensors, event = item
-        torch.cuda.current_stream(self.device).wait_event(event)
         cur = torch.cuda.current_stream(self.device)
+        cur.wait_event(event)
         for t in tensors.values():
             t.record_stream(cur)
         return tensors
 
-    def prefetch_after(self, hook):
-        if self.recording or hook not in self.order:
+    def prefetch_next(self, hook):
+        if not self.enabled or self.recording or hook not in self.order:
             return
-        i = self.order.index(hook)
-        nxt = self.order[(i + 1) % len(self.order)]
+        nxt = self.order[(self.order.index(hook) + 1) % len(self.order)]
         if id(nxt) in self.staged:
             return
-        tensors = {}
-        cur = torch.cuda.current_stream(self.device)
-        self.stream.wait_stream(cur)
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        staged = {}
         with torch.cuda.stream(self.stream):
-            for name, host in nxt.host_tensors().items():
-                tensors[name] = host.to(self.device, non_blocking=True)
+            for name in nxt.streamed_names():
+                if name in nxt.tied_params_names:
+                    continue  # tied weights go through the shared tied-parameter cache
+                staged[name] = self.host_copy(nxt, name, nxt.weights_map[name]).to(self.device, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(self.stream)
-        self.staged[id(nxt)] = (tensors, ev)
+        self.staged[id(nxt)] = (staged, ev)
 
 
+def _scheduler_for(device, schedulers: Optional[dict]) -> Optional[OffloadScheduler]:
+    if device is None or schedulers is None:
+        return None
+    dev = torch.device(device) if not isinstance(device, int) else torch.device("cuda", device)
+    if dev.type != "cuda":
+        return None
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    if key not in schedulers:
+        schedulers[key] = OffloadScheduler(torch.device("cuda", key))
+    return schedulers[key]
+
+
+# --------------------------------------------------------------------------------------------------- device hooks
 class AlignDevicesHook(ModelHook):
-    """Put a module's weights (from `weights_map` when offloaded) and inputs on `execution_device` for its forward;
-    optionally move outputs back to the input device (`io_same_device`) and re-offload weights after the forward."""
+    """Run the module on `execution_device`: inputs are moved there; with `offload`, the module's tensors stay on the
+    meta device between calls and are materialised from `weights_map` for each forward (through the model's
+    `OffloadScheduler` when it has one); `io_same_device` moves outputs back to where the inputs came from."""
 
     def __init__(
         self,
@@ -208,8 +255,10 @@ class AlignDevicesHook(ModelHook):
         weights_map: Optional[Mapping] = None,
         offload_buffers: bool = False,
         place_submodules: bool = False,
-        skip_keys: Optional[Union[str, list[str]]] = None,
-        tied_params_map: Optional[dict[int, dict[torch.device, torch.Tensor]]] = None,
+        skip_keys: Optional[Union[str, list]] = None,
+        tied_params_map: Optional[dict] = None,
+        scheduler: Optional[OffloadScheduler] = None,
+        cache_host: bool = True,
     ):
         self.execution_device = execution_device
         self.offload = offload
@@ -218,13 +267,15 @@ class AlignDevicesHook(ModelHook):
         self.offload_buffers = offload_buffers
         self.place_submodules = place_submodules
         self.skip_keys = skip_keys
+        self.tied_params_map = tied_params_map
+        self.scheduler = scheduler
+        self.cache_host = cache_host
         self.input_device = None
         self.param_original_devices = {}
         self.buffer_original_devices = {}
         self.tied_params_names = set()
-        self.tied_params_map = tied_params_map
-        self._pinned = None
-        self._names = None
+        self.tied_pointers_to_remove = set()
+        self._streamed = None
 
     def __repr__(self):
         return (
@@ -233,101 +284,76 @@ class AlignDevicesHook(ModelHook):
             f"place_submodules={self.place_submodules}, skip_keys={repr(self.skip_keys)})"
         )
 
+    def _tensors(self, module, include_buffers=True, persistent_only=False):
+        return named_module_tensors(module, include_buffers=include_buffers, recurse=self.place_submodules,
+                                    remove_non_persistent=persistent_only)
+
+    def streamed_names(self, module=None) -> list:
+        """Names of the tensors materialised per forward (offloaded params, persistent buffers if offloaded)."""
+        if self._streamed is None and module is not None:
+            self._streamed = [n for n, _ in self._tensors(module, include_buffers=self.offload_buffers, persistent_only=True)]
+        return self._streamed or []
+
     def init_hook(self, module):
-        if self.execution_device == "meta" or self.execution_device == torch.device("meta"):
+        if str(self.execution_device) == "meta":
             self.tied_params_map = None
-        if not self.offload and self.execution_device is not None:
-            for name, _ in named_module_tensors(module, recurse=self.place_submodules):
-                set_module_tensor_to_device(module, name, self.execution_device, tied_params_map=self.tied_params_map)
-        elif self.offload:
-            self.original_devices = {
-                name: param.device for name, param in named_module_tensors(module, recurse=self.place_submodules)
-            }
-            if self.weights_map is None:
-                self.weights_map = {
-                    name: param.to("cpu")
-                    for name, param in named_module_tensors(module, include_buffers=self.offload_buffers, recurse=self.place_submodules)
-                }
-            for name, _ in named_module_tensors(module, include_buffers=self.offload_buffers, recurse=self.place_submodules, remove_non_persistent=True):
-                if (
-                    self.tied_params_map is not None
-                    and recursive_getattr(module, name).data_ptr() in self.tied_params_map
-                ):
-                    self.tied_params_names.add(name)
-                set_module_tensor_to_device(module, name, "meta")
-            if not self.offload_buffers and self.execution_device is not None:
-                for name, _ in module.named_buffers(recurse=self.place_submodules):
-                    set_module_tensor_to_device(module, name, self.execution_device, tied_params_map=self.tied_params_map)
-            elif self.offload_buffers and self.execution_device is not None:
-                for name in get_non_persistent_buffers(module, recurse=self.place_submodules):
-                    set_module_tensor_to_device(module, name, self.execution_device, tied_params_map=self.tied_params_map)
+        dev = self.execution_device
+        if not self.offload:
+            if dev is not None:
+                for name, _ in self._tensors(module):
+                    set_module_tensor_to_device(module, name, dev, tied_params_map=self.tied_params_map)
+            return module
+        self.original_devices = {name: t.device for name, t in self._tensors(module)}
+        if self.weights_map is None:
+            self.weights_map = {name: t.to("cpu") for name, t in self._tensors(module, include_buffers=self.offload_buffers)}
+        for name in self.streamed_names(module):
+            if self.tied_params_map is not None and recursive_getattr(module, name).data_ptr() in self.tied_params_map:
+                self.tied_params_names.add(name)
+            set_module_tensor_to_device(module, name, "meta")
+        if dev is not None:
+            # buffers that are not streamed live on the execution device for good
+            kept = (n for n, _ in module.named_buffers(recurse=self.place_submodules)) if not self.offload_buffers else \
+                get_non_persistent_buffers(module, recurse=self.place_submodules)
+            for name in kept:
+                set_module_tensor_to_device(module, name, dev, tied_params_map=self.tied_params_map)
         return module
-
-    # --- async prefetch support ------------------------------------------------------------------------
-    def _offload_names(self, module=None):
-        if self._names is None and module is not None:
-            self._names = [
-                name
-                for name, _ in named_module_tensors(module, include_buffers=self.offload_buffers, recurse=self.place_submodules, remove_non_persistent=True)
-            ]
-        return self._names or []
-
-    def host_tensors(self) -> dict:
-        """Pinned host copies of this module's offloaded weights (built once)."""
-        if self._pinned is None:
-            pinned = {}
-            for name in self._names or []:
-                if name in self.tied_params_names:
-                    continue
-                v = self.weights_map[name]
-                if v.device.type == "cpu":
-                    try:
-                        v = v.contiguous().pin_memory()
-                    except RuntimeError:
-                        pass
-                pinned[name] = v
-            self._pinned = pinned
-        return self._pinned
 
     def pre_forward(self, module, *args, **kwargs):
         if self.io_same_device:
             self.input_device = find_device([args, kwargs])
         if self.offload:
-            self.tied_pointers_to_remove = set()
-            names = self._offload_names(module)
-            pf = OffloadPrefetcher.get(self.execution_device) if self.execution_device is not None else None
-            staged = None
-            if pf is not None:
-                pf.note_execution(self)
-                staged = pf.take(self)
-            for name in names:
-                if staged is not None and name in staged:
-                    _set_tensor(module, name, staged[name])
-                    continue
-                value = self.weights_map[name]
-                if name in self.tied_params_names and value.data_ptr() not in self.tied_params_map:
-                    self.tied_params_map[value.data_ptr()] = {}
-                if (
-                    value is not None
-                    and self.tied_params_map is not None
-                    and value.data_ptr() in self.tied_params_map
-                    and self.execution_device not in self.tied_params_map[value.data_ptr()]
-                ):
-                    self.tied_pointers_to_remove.add((value.data_ptr(), self.execution_device))
-                set_module_tensor_to_device(module, name, self.execution_device, value=value, tied_params_map=self.tied_params_map)
-            if pf is not None:
-                pf.prefetch_after(self)
+            self._materialise(module)
         return send_to_device(args, self.execution_device), send_to_device(kwargs, self.execution_device, skip_keys=self.skip_keys)
+
+    def _materialise(self, module):
+        self.tied_pointers_to_remove = set()
+        sched = self.scheduler
+        staged = None
+        if sched is not None and sched.enabled:
+            sched.ran(self)
+            staged = sched.take(self)
+        tied = self.tied_params_map
+        for name in self.streamed_names(module):
+            if staged is not None and name in staged:
+                _install(module, name, staged[name])
+                continue
+            value = self.weights_map[name]
+            if name in self.tied_params_names and value.data_ptr() not in tied:
+                tied[value.data_ptr()] = {}
+            if tied is not None and value.data_ptr() in tied and self.execution_device not in tied[value.data_ptr()]:
+                self.tied_pointers_to_remove.add((value.data_ptr(), self.execution_device))
+            if sched is not None and sched.enabled and name not in self.tied_params_names:
+                value = sched.host_copy(self, name, value)
+            set_module_tensor_to_device(module, name, self.execution_device, value=value, tied_params_map=tied)
+        if sched is not None and sched.enabled:
+            sched.prefetch_next(self)
 
     def post_forward(self, module, output):
         if self.offload:
-            for name in self._offload_names(module):
+            for name in self.streamed_names(module):
                 set_module_tensor_to_device(module, name, "meta")
-            for value_pointer, device in getattr(self, "tied_pointers_to_remove", set()):
-                if isinstance(device, int):
-                    device = f"cuda:{device}"
-                if value_pointer in self.tied_params_map and device in self.tied_params_map[value_pointer]:
-                    del self.tied_params_map[value_pointer][device]
+            for ptr, device in self.tied_pointers_to_remove:
+                self.tied_params_map.get(ptr, {}).pop(device, None)
             self.tied_pointers_to_remove = set()
         if self.io_same_device and self.input_device is not None:
             output = send_to_device(output, self.input_device, skip_keys=self.skip_keys)
@@ -341,157 +367,100 @@ class AlignDevicesHook(ModelHook):
         return module
 
 
+# --------------------------------------------------------------------------------------------------- attach helpers
 def attach_execution_device_hook(module, execution_device, skip_keys=None, preload_module_classes=None, tied_params_map=None):
-    if not hasattr(module, "_hf_hook") and len(module.state_dict()) > 0:
-        add_hook_to_module(module, AlignDevicesHook(execution_device, skip_keys=skip_keys, tied_params_map=tied_params_map))
-    if preload_module_classes is not None and module.__class__.__name__ in preload_module_classes:
-        return
-    for child in module.children():
-        attach_execution_device_hook(child, execution_device, skip_keys=skip_keys, tied_params_map=tied_params_map)
+    """Give every module of the subtree that holds tensors and has no hook an execution-device hook (no offload).
+    When the subtree's root is a `preload_module_classes` module, its own hook covers its children (the class test
+    applies to the root only, as upstream)."""
+    stack = [(module, True)]
+    while stack:
+        m, is_root = stack.pop()
+        if not hasattr(m, "_hf_hook") and len(m.state_dict()) > 0:
+            add_hook_to_module(m, AlignDevicesHook(execution_device, skip_keys=skip_keys, tied_params_map=tied_params_map))
+        if is_root and preload_module_classes is not None and m.__class__.__name__ in preload_module_classes:
+            continue
+        stack.extend((c, False) for c in reversed(list(m.children())))
 
 
-def attach_align_device_hook(
-    module,
-    execution_device=None,
-    offload=False,
-    weights_map=None,
-    offload_buffers=False,
-    module_name="",
-    skip_keys=None,
-    preload_module_classes=None,
-    tied_params_map=None,
-):
-    directs = named_module_tensors(module)
-    full_offload = offload and preload_module_classes is not None and module.__class__.__name__ in preload_module_classes
-    if len(list(directs)) > 0 or full_offload:
-        if weights_map is not None:
-            prefix = f"{module_name}." if len(module_name) > 0 else ""
-            prefixed_weights_map = PrefixedDataset(weights_map, prefix)
-        else:
-            prefixed_weights_map = None
-        hook = AlignDevicesHook(
-            execution_device=execution_device,
-            offload=offload,
-            weights_map=prefixed_weights_map,
-            offload_buffers=offload_buffers,
-            place_submodules=full_offload,
-            skip_keys=skip_keys,
-            tied_params_map=tied_params_map,
-        )
-        add_hook_to_module(module, hook, append=True)
-    if full_offload:
-        return
-    for child_name, child in module.named_children():
-        child_name = f"{module_name}.{child_name}" if len(module_name) > 0 else child_name
-        attach_align_device_hook(
-            child,
-            execution_device=execution_device,
-            offload=offload,
-            weights_map=weights_map,
-            offload_buffers=offload_buffers,
-            module_name=child_name,
-            preload_module_classes=preload_module_classes,
-            skip_keys=skip_keys,
-            tied_params_map=tied_params_map,
-        )
-
-
-def remove_hook_from_submodules(module):
-    remove_hook_from_module(module)
-    for child in module.children():
-        remove_hook_from_submodules(child)
-
-
-def attach_align_device_hook_on_blocks(
-    module,
-    execution_device=None,
-    offload=False,
-    weights_map=None,
-    offload_buffers=False,
-    module_name="",
-    skip_keys=None,
-    preload_module_classes=None,
-    tied_params_map=None,
-):
-    if not isinstance(execution_device, Mapping) and not isinstance(offload, dict):
-        if not offload:
-            hook = AlignDevicesHook(execution_device=execution_device, io_same_device=True, skip_keys=skip_keys, place_submodules=True, tied_params_map=tied_params_map)
-            add_hook_to_module(module, hook)
-        else:
-            attach_align_device_hook(
-                module,
-                execution_device=execution_device,
-                offload=True,
-                weights_map=weights_map,
-                offload_buffers=offload_buffers,
-                module_name=module_name,
-                skip_keys=skip_keys,
-                tied_params_map=tied_params_map,
+def attach_align_device_hook(module, execution_device=None, offload=False, weights_map=None, offload_buffers=False,
+                             module_name="", skip_keys=None, preload_module_classes=None, tied_params_map=None,
+                             schedulers=None, cache_host=True):
+    """Hook every module of the subtree that directly owns tensors. A `preload_module_classes` module under offload is
+    streamed as a whole (one hook, its submodules' tensors included) and not descended into."""
+    stack = [(module, module_name)]
+    while stack:
+        m, name = stack.pop()
+        whole = offload and preload_module_classes is not None and m.__class__.__name__ in preload_module_classes
+        if whole or next(iter(named_module_tensors(m)), None) is not None:
+            view = PrefixedDataset(weights_map, f"{name}." if name else "") if weights_map is not None else None
+            add_hook_to_module(
+                m,
+                AlignDevicesHook(execution_device=execution_device, offload=offload, weights_map=view,
+                                 offload_buffers=offload_buffers, place_submodules=whole, skip_keys=skip_keys,
+                                 tied_params_map=tied_params_map,
+                                 scheduler=_scheduler_for(execution_device, schedulers) if offload else None,
+                                 cache_host=cache_host),
+                append=True,
             )
+        if whole:
+            continue
+        stack.extend(reversed([(c, f"{name}.{n}" if name else n) for n, c in m.named_children()]))
+
+
+def attach_align_device_hook_on_blocks(module, execution_device=None, offload=False, weights_map=None,
+                                       offload_buffers=False, module_name="", skip_keys=None,
+                                       preload_module_classes=None, tied_params_map=None, schedulers=None,
+                                       cache_host=None):
+    """Hooks for a device map: `execution_device` / `offload` map block names to their execution device and whether
+    their weights are offloaded. A resident block gets one hook that places the whole block; an offloaded block is
+    streamed per submodule; the root also moves outputs back to the caller's device."""
+    if not isinstance(execution_device, Mapping) and not isinstance(offload, dict):
+        if offload:
+            attach_align_device_hook(module, execution_device=execution_device, offload=True, weights_map=weights_map,
+                                     offload_buffers=offload_buffers, module_name=module_name, skip_keys=skip_keys,
+                                     tied_params_map=tied_params_map, schedulers=schedulers)
+        else:
+            add_hook_to_module(module, AlignDevicesHook(execution_device=execution_device, io_same_device=True,
+                                                        skip_keys=skip_keys, place_submodules=True,
+                                                        tied_params_map=tied_params_map))
         return
     if not isinstance(execution_device, Mapping):
-        execution_device = {key: execution_device for key in offload.keys()}
+        execution_device = {k: execution_device for k in offload}
     if not isinstance(offload, Mapping):
-        offload = {key: offload for key in execution_device.keys()}
-    if module_name in execution_device and module_name in offload and not offload[module_name]:
-        hook = AlignDevicesHook(
-            execution_device=execution_device[module_name],
-            offload_buffers=offload_buffers,
-            io_same_device=(module_name == ""),
-            place_submodules=True,
-            skip_keys=skip_keys,
-            tied_params_map=tied_params_map,
-        )
-        add_hook_to_module(module, hook)
-        attach_execution_device_hook(module, execution_device[module_name], skip_keys=skip_keys, tied_params_map=tied_params_map)
-    elif module_name in execution_device and module_name in offload:
-        attach_align_device_hook(
-            module,
-            execution_device=execution_device[module_name],
-            offload=True,
-            weights_map=weights_map,
-            offload_buffers=offload_buffers,
-            module_name=module_name,
-            skip_keys=skip_keys,
-            preload_module_classes=preload_module_classes,
-            tied_params_map=tied_params_map,
-        )
-        if not hasattr(module, "_hf_hook"):
-            hook = AlignDevicesHook(
-                execution_device=execution_device[module_name],
-                io_same_device=(module_name == ""),
-                skip_keys=skip_keys,
-                tied_params_map=tied_params_map,
-            )
-            add_hook_to_module(module, hook)
-        attach_execution_device_hook(
-            module,
-            execution_device[module_name],
-            preload_module_classes=preload_module_classes,
-            skip_keys=skip_keys,
-            tied_params_map=tied_params_map,
-        )
-    elif module_name == "":
-        hook = AlignDevicesHook(execution_device=execution_device.get(""), io_same_device=True, skip_keys=skip_keys, tied_params_map=tied_params_map)
-        add_hook_to_module(module, hook)
-    for child_name, child in module.named_children():
-        child_name = f"{module_name}.{child_name}" if len(module_name) > 0 else child_name
-        attach_align_device_hook_on_blocks(
-            child,
-            execution_device=execution_device,
-            offload=offload,
-            weights_map=weights_map,
-            offload_buffers=offload_buffers,
-            module_name=child_name,
-            preload_module_classes=preload_module_classes,
-            skip_keys=skip_keys,
-            tied_params_map=tied_params_map,
-        )
+        offload = {k: offload for k in execution_device}
+    cache_host = cache_host or {}
+
+    stack = [(module, module_name)]
+    while stack:
+        m, name = stack.pop()
+        is_root = name == ""
+        if name in execution_device and name in offload:
+            dev = execution_device[name]
+            if not offload[name]:
+                add_hook_to_module(m, AlignDevicesHook(execution_device=dev, offload_buffers=offload_buffers,
+                                                       io_same_device=is_root, place_submodules=True,
+                                                       skip_keys=skip_keys, tied_params_map=tied_params_map))
+                attach_execution_device_hook(m, dev, skip_keys=skip_keys, tied_params_map=tied_params_map)
+            else:
+                attach_align_device_hook(m, execution_device=dev, offload=True, weights_map=weights_map,
+                                         offload_buffers=offload_buffers, module_name=name, skip_keys=skip_keys,
+                                         preload_module_classes=preload_module_classes, tied_params_map=tied_params_map,
+                                         schedulers=schedulers, cache_host=cache_host.get(name, True))
+                if not hasattr(m, "_hf_hook"):
+                    add_hook_to_module(m, AlignDevicesHook(execution_device=dev, io_same_device=is_root,
+                                                           skip_keys=skip_keys, tied_params_map=tied_params_map))
+                attach_execution_device_hook(m, dev, preload_module_classes=preload_module_classes,
+                                             skip_keys=skip_keys, tied_params_map=tied_params_map)
+        elif is_root:
+            add_hook_to_module(m, AlignDevicesHook(execution_device=execution_device.get(""), io_same_device=True,
+                                                   skip_keys=skip_keys, tied_params_map=tied_params_map))
+        stack.extend(reversed([(c, f"{name}.{n}" if name else n) for n, c in m.named_children()]))
 
 
+# --------------------------------------------------------------------------------------------------- other hooks
 class CpuOffload(ModelHook):
-    """Keep the whole module on CPU, move it to `execution_device` for each forward (and offload the previous
-    module in a chain: `cpu_offload_with_hook`)."""
+    """Whole-model offload between calls: the model lives on the host and moves to `execution_device` for its
+    forward; a chained `prev_module_hook` sends the previous model of a pipeline back first."""
 
     def __init__(self, execution_device=None, prev_module_hook: Optional["UserCpuOffloadHook"] = None):
         self.prev_module_hook = prev_module_hook
@@ -509,6 +478,8 @@ class CpuOffload(ModelHook):
 
 
 class UserCpuOffloadHook:
+    """Handle returned by `cpu_offload_with_hook`: `offload()` sends the model back to the host, `remove()` detaches."""
+
     def __init__(self, model, hook):
         self.model = model
         self.hook = hook
@@ -521,7 +492,7 @@ class UserCpuOffloadHook:
 
 
 class LayerwiseCastingHook(ModelHook):
-    """Store weights in `storage_dtype` (e.g. fp8), cast to `compute_dtype` around each forward."""
+    """Weights stored in `storage_dtype` (e.g. fp8) and cast to `compute_dtype` for the duration of each forward."""
 
     _is_stateful = False
 
@@ -545,21 +516,3 @@ class LayerwiseCastingHook(ModelHook):
 
 def _default_device():
     return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
-
-
-def recursive_getattr(obj, attr):
-    import functools as _f
-
-    return _f.reduce(getattr, [obj] + attr.split("."))
-
-
-def get_non_persistent_buffers(module, recurse=False):
-    from .utils.modeling import get_non_persistent_buffers as _g
-
-    return _g(module, recurse=recurse)
-
-
-def set_module_tensor_to_device(*args, **kwargs):
-    from ._big_modeling_impl import set_module_tensor_to_device as _s
-
-    return _s(*args, **kwargs)

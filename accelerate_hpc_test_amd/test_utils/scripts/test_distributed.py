@@ -677,6 +677,51 @@ def check_fsdp_cpu_ram_efficient_loading():
         assert torch.allclose(full[n], q, atol=1e-5), (n, (full[n] - q).abs().max())
 
 
+def check_broadcast_from_rank0_loading():
+    """load_checkpoint_in_model(broadcast_from_rank0=True): only rank 0 reads the (sharded safetensors) checkpoint;
+    every rank ends with its weights — a plain model gets full tensors, an FSDP-engine model its shards."""
+    import json as _json
+
+    from safetensors.torch import save_file
+
+    from accelerate_hpc_test_amd.utils.checkpoint_io import load_checkpoint_in_model
+
+    acc = Accelerator(cpu=True)
+    r = acc.process_index
+    torch.manual_seed(123)
+    src = TinyMLP()
+    d = tempfile.mkdtemp() if r == 0 else None
+    d = gather_object([d])[0]
+    if r == 0:
+        sd = {k: v.contiguous() for k, v in src.state_dict().items()}
+        keys = sorted(sd)
+        wm = {}
+        for i in range(2):
+            part = {k: sd[k] for k in keys[i::2]}
+            save_file(part, os.path.join(d, f"m-{i}.safetensors"), metadata={"format": "pt"})
+            wm.update({k: f"m-{i}.safetensors" for k in part})
+        _json.dump({"weight_map": wm}, open(os.path.join(d, "model.safetensors.index.json"), "w"))
+    acc.wait_for_everyone()
+    ck = d if r == 0 else "/nonexistent-on-other-ranks"
+    torch.manual_seed(r + 7)
+    plain = TinyMLP()
+    load_checkpoint_in_model(plain, ck, broadcast_from_rank0=True)
+    for k, v in src.state_dict().items():
+        assert torch.equal(plain.state_dict()[k], v), (r, k)
+    # FSDP engine: the broadcast lands in each rank's shard
+    from accelerate_hpc_test_amd.state import AcceleratorState
+
+    AcceleratorState._reset_state(True)
+    plugin = FullyShardedDataParallelPlugin(fsdp_version=2, auto_wrap_policy="transformer_based_wrap", transformer_cls_names_to_wrap=["Block"])
+    acc = Accelerator(cpu=True, fsdp_plugin=plugin)
+    torch.manual_seed(r + 11)
+    model = acc.prepare(TinyMLP())
+    load_checkpoint_in_model(model, ck, broadcast_from_rank0=True)
+    full = acc.get_state_dict(model)
+    for k, v in src.state_dict().items():
+        assert torch.equal(full[k], v), (r, k)
+
+
 def check_ddp_powersgd():
     """PowerSGD hook: with start_powerSGD_iter=0 training still converges and ranks stay in sync."""
     from accelerate_hpc_test_amd.utils import DDPCommunicationHookType, DistributedDataParallelKwargs

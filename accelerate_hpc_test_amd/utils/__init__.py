@@ -203,10 +203,16 @@ def __getattr__(name):
         "calculate_maximum_sizes",
         "align_module_device",
         "has_offloaded_params",
+        "find_tied_parameters",
+        "retie_parameters",
+        "clean_device_map",
+        "get_module_leaves",
     ):
-        from . import big_model_utils
+        from . import checkpoint_io, device_map, placement
 
-        return getattr(big_model_utils, name)
+        for mod in (device_map, placement, checkpoint_io):
+            if hasattr(mod, name):
+                return getattr(mod, name)
     if name in ("offload_weight", "load_offloaded_weight", "save_offload_index", "offload_state_dict", "OffloadedWeightsLoader", "PrefixedDataset", "extract_submodules_state_dict"):
         from . import offload
 

@@ -276,16 +276,8 @@ def model_has_dtensor(model: nn.Module) -> bool:
 
 
 # ------------------------------------------------------------------------------------------------ tied weights
-def find_tied_parameters(model: nn.Module, **kwargs):
-    from .._big_modeling_impl import find_tied_parameters as f
-
-    return f(model, **kwargs)
-
-
-def retie_parameters(model, tied_params):
-    from .._big_modeling_impl import retie_parameters as f
-
-    return f(model, tied_params)
+from .device_map import find_tied_parameters  # noqa: E402,F401
+from .placement import retie_parameters  # noqa: E402,F401
 
 
 def check_tied_parameters_in_config(model: nn.Module) -> bool:
@@ -325,7 +317,7 @@ def ensure_weights_retied(param_init_fn, model: nn.Module, device):
 
 def load_offloaded_weights(model, index, offload_folder):
     from .offload import load_offloaded_weight
-    from .._big_modeling_impl import set_module_tensor_to_device
+    from .placement import set_module_tensor_to_device
 
     for name, meta in index.items():
         w = load_offloaded_weight(os.path.join(offload_folder, f"{name}.dat"), meta)

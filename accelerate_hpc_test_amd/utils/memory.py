@@ -48,43 +48,46 @@ def should_reduce_batch_size(exception: Exception) -> bool:
     return False
 
 
-def find_executable_batch_size(function=None, starting_batch_size: int = 128, reduce_batch_size_fn=None):
-    """Decorator: call `function(batch_size, ...)`, retrying with 90 % of the batch size after each OOM."""
-    if function is None:
-        return functools.partial(
-            find_executable_batch_size, starting_batch_size=starting_batch_size, reduce_batch_size_fn=reduce_batch_size_fn
-        )
-    batch_size = starting_batch_size
-    if reduce_batch_size_fn is None:
+class _BatchSizeSearch:
+    """Calls `fn(batch_size, *args, **kwargs)`, shrinking the batch size after every out-of-memory failure
+    (`reduce` gives the next size; default: 90 % of the current one) until a call succeeds."""
 
-        def reduce_batch_size_fn():
-            nonlocal batch_size
-            batch_size = int(batch_size * 0.9)
-            return batch_size
+    def __init__(self, fn, start: int, reduce=None):
+        self.fn = fn
+        self.batch_size = start
+        self.reduce = reduce if reduce is not None else (lambda: int(self.batch_size * 0.9))
+        functools.update_wrapper(self, fn)
 
-    def decorator(*args, **kwargs):
-        nonlocal batch_size
-        clear_device_cache(garbage_collection=True)
-        params = list(inspect.signature(function).parameters.keys())
-        if len(params) < (len(args) + 1):
-            arg_str = ", ".join([f"{arg}={value}" for arg, value in zip(params[1:], args[1:])])
+    def _check_call(self, args):
+        names = list(inspect.signature(self.fn).parameters)
+        if len(names) < len(args) + 1:  # the caller passed the batch size itself
+            shown = ", ".join(f"{n}={v}" for n, v in zip(names[1:], args[1:]))
             raise TypeError(
-                f"Batch size was passed into `{function.__name__}` as the first argument when called."
-                f"Remove this as the decorator already does so: `{function.__name__}({arg_str})`"
+                f"Batch size was passed into `{self.fn.__name__}` as the first argument when called."
+                f"Remove this as the decorator already does so: `{self.fn.__name__}({shown})`"
             )
-        while True:
-            if batch_size == 0:
-                raise RuntimeError("No executable batch size found, reached zero.")
-            try:
-                return function(batch_size, *args, **kwargs)
-            except Exception as e:
-                if should_reduce_batch_size(e):
-                    clear_device_cache(garbage_collection=True)
-                    batch_size = reduce_batch_size_fn()
-                else:
-                    raise
 
-    return decorator
+    def __call__(self, *args, **kwargs):
+        clear_device_cache(garbage_collection=True)
+        self._check_call(args)
+        while self.batch_size != 0:
+            try:
+                return self.fn(self.batch_size, *args, **kwargs)
+            except Exception as exc:  # noqa: BLE001 - only OOMs are retried, the rest re-raised
+                if not should_reduce_batch_size(exc):
+                    raise
+                clear_device_cache(garbage_collection=True)
+                self.batch_size = self.reduce()
+        raise RuntimeError("No executable batch size found, reached zero.")
+
+
+def find_executable_batch_size(function=None, starting_batch_size: int = 128, reduce_batch_size_fn=None):
+    """Decorator: run `function(batch_size, ...)` and retry with a smaller batch size after each out-of-memory error
+    (HIP: "HIP out of memory." / hipErrorOutOfMemory), starting from `starting_batch_size`."""
+    if function is None:
+        return functools.partial(find_executable_batch_size, starting_batch_size=starting_batch_size,
+                                 reduce_batch_size_fn=reduce_batch_size_fn)
+    return _BatchSizeSearch(function, starting_batch_size, reduce_batch_size_fn)
 
 
 def get_xpu_available_memory(device_index: int):  # pragma: no cover - API parity

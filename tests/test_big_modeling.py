@@ -18,13 +18,9 @@ from accelerate_hpc_test_amd import (
     init_on_device,
     load_checkpoint_and_dispatch,
 )
-from accelerate_hpc_test_amd._big_modeling_impl import (
-    check_device_map,
-    find_tied_parameters,
-    get_balanced_memory,
-    load_checkpoint_in_model,
-    set_module_tensor_to_device,
-)
+from accelerate_hpc_test_amd.utils.checkpoint_io import load_checkpoint_in_model
+from accelerate_hpc_test_amd.utils.device_map import check_device_map, find_tied_parameters, get_balanced_memory
+from accelerate_hpc_test_amd.utils.placement import set_module_tensor_to_device
 from accelerate_hpc_test_amd.hooks import ModelHook, SequentialHook, add_hook_to_module, remove_hook_from_module
 from accelerate_hpc_test_amd.utils.modeling import compute_module_sizes
 

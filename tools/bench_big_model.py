@@ -30,7 +30,7 @@ def main():
     args = p.parse_args()
 
     from accelerate_hpc_test_amd import dispatch_model, infer_auto_device_map, init_empty_weights
-    from accelerate_hpc_test_amd._big_modeling_impl import set_module_tensor_to_device
+    from accelerate_hpc_test_amd.utils.placement import set_module_tensor_to_device
     from accelerate_hpc_test_amd.models.llama import LLAMA_PRESETS, LlamaForCausalLM, RMSNorm
 
     cfg = LLAMA_PRESETS[args.model]
