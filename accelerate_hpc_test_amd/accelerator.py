@@ -812,9 +812,17 @@ class Accelerator:
             init_fn=init_fn,
             prefetch_depth=self.rccl_handler.fsdp_prefetch_depth,
             force_sharded=self.rccl_handler.fsdp_force_sharded,
+            fp8_all_gather=self._fsdp_fp8_all_gather(),
         )
         self._fsdp_engines.append(wrapped.engine)
         return wrapped
+
+    def _fsdp_fp8_all_gather(self) -> bool:
+        """torchao-style fp8 all-gather of the FSDP shards (reference examples/torch_native_parallelism/fsdp2_fp8.py:69-75):
+        on with the AO (dynamic scaling) fp8 backend when `enable_fsdp_float8_all_gather` is set."""
+        if self.state.mixed_precision != "fp8" or self._fp8_backend != "AO" or self.ao_recipe_handler is None:
+            return False
+        return bool(self.ao_recipe_handler.enable_fsdp_float8_all_gather)
 
     def prepare_data_loader(self, data_loader: torch.utils.data.DataLoader, device_placement=None, slice_fn_for_dispatch=None):
         if getattr(data_loader, "_is_accelerate_prepared", False):

@@ -34,6 +34,10 @@ std::vector<torch::Tensor> fp8_cast(torch::Tensor x, torch::Tensor t, double qma
 torch::Tensor fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor a_scale_inv, torch::Tensor b_scale_inv,
                        double smul, bool a_e5m2, bool b_e5m2, c10::optional<torch::Tensor> bias, bool out_fp32,
                        c10::optional<torch::Tensor> out, bool accumulate);
+void fp8_segment_amax(torch::Tensor x, torch::Tensor lo, torch::Tensor hi, torch::Tensor out, int64_t max_len);
+void fp8_segment_cast(torch::Tensor x, torch::Tensor lo, torch::Tensor hi, torch::Tensor amax, double qmax, torch::Tensor y,
+                      int64_t max_len);
+torch::Tensor u8_transpose(torch::Tensor x);
 // comm_pack.hip
 void grad_shard_update(torch::Tensor dst, torch::Tensor src, double scale, bool accumulate);
 // runtime/*.cpp
@@ -65,6 +69,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("smul"), pybind11::arg("a_e5m2"), pybind11::arg("b_e5m2"), pybind11::arg("bias"), pybind11::arg("out_fp32"),
         pybind11::arg("out") = pybind11::none(), pybind11::arg("accumulate") = false);
   m.def("grad_shard_update", &grad_shard_update);
+  m.def("fp8_segment_amax", &fp8_segment_amax);
+  m.def("fp8_segment_cast", &fp8_segment_cast);
+  m.def("u8_transpose", &u8_transpose);
   register_runtime(m);
   m.def("blaslt_wgrad_f32", &blaslt_wgrad_f32);
   m.def("cpu_adam_step", &cpu_adam_step);

@@ -142,6 +142,70 @@ __global__ __launch_bounds__(256) void cast_kernel(const bf16_t* __restrict__ x,
     *reinterpret_cast<uint4*>(yt + (long)(tn + n4 + j) * M + tm + m16) = make_uint4(col[j][0], col[j][1], col[j][2], col[j][3]);
 }
 
+
+// ------------------------------------------------------------------------------------------------ FSDP fp8 all-gather
+// The sharded flat buffer holds several weights back to back; each weight gets its own per-tensor scale. Segment k =
+// elements [lo[k], hi[k]) of the flat bf16 shard. One workgroup per (segment, 4096-element chunk).
+constexpr int kSegChunk = 4096;
+
+__global__ __launch_bounds__(256) void seg_amax_kernel(const bf16_t* __restrict__ x, const long* __restrict__ lo,
+                                                       const long* __restrict__ hi, unsigned int* __restrict__ out) {
+  __shared__ float scratch[16];
+  const int k = blockIdx.y;
+  const long a = lo[k] + (long)blockIdx.x * kSegChunk, b = min(hi[k], a + kSegChunk);
+  float m = 0.f;
+  for (long i = a + threadIdx.x; i < b; i += 256) m = fmaxf(m, fabsf(bf2f(x[i])));
+  m = block_max(m, scratch);
+  if (threadIdx.x == 0 && a < b) atomicMax(out + k, __float_as_uint(m));
+}
+
+// y[i] = e4m3(sat(x[i] * 448 / amax[k])) for i in segment k: the same conversion as cast_kernel, so a weight cast from
+// its shard with the all-reduced amax is bit-identical to the weight cast whole.
+__global__ __launch_bounds__(256) void seg_cast_kernel(const bf16_t* __restrict__ x, const long* __restrict__ lo,
+                                                       const long* __restrict__ hi, const float* __restrict__ amax,
+                                                       float qmax, uint8_t* __restrict__ y) {
+  const int k = blockIdx.y;
+  const long a = lo[k] + (long)blockIdx.x * kSegChunk, b = min(hi[k], a + kSegChunk);
+  const float s = cast_scale(amax + k, qmax, true);
+  for (long i = a + threadIdx.x; i < b; i += 256) y[i] = cvt_pair<false>(bf2f(x[i]) * s, 0.f) & 0xff;
+}
+
+// y = x^T for a [R, C] byte matrix (fp8 weights: the K-major copy the dgrad GEMM reads). 128x128 tiles through a
+// padded LDS tile; 4x4 byte transposes in registers (v_perm_b32), 16-B stores. Edge tiles per element.
+__global__ __launch_bounds__(256) void u8_transpose_kernel(const uint8_t* __restrict__ x, uint8_t* __restrict__ y, int R, int C) {
+  __shared__ __attribute__((aligned(16))) uint8_t tile[kCT * kCTP];
+  const int tr = blockIdx.y * kCT, tc = blockIdx.x * kCT, tid = threadIdx.x;
+  if (!(tr + kCT <= R && tc + kCT <= C && (R % 16) == 0 && (C % 16) == 0)) {
+    for (int e = tid; e < kCT * kCT; e += 256) {
+      const int r = tr + e / kCT, c = tc + e % kCT;
+      if (r < R && c < C) y[(long)c * R + r] = x[(long)r * C + c];
+    }
+    return;
+  }
+#pragma unroll
+  for (int pass = 0; pass < 4; ++pass) {
+    const int r = (tid >> 3) + pass * 32, c = (tid & 7) * 16;
+    const uint4 w = *reinterpret_cast<const uint4*>(x + (long)(tr + r) * C + tc + c);
+    uint32_t* t = reinterpret_cast<uint32_t*>(tile + r * kCTP + c);
+    t[0] = w.x; t[1] = w.y; t[2] = w.z; t[3] = w.w;
+  }
+  __syncthreads();
+  const int m16 = (tid & 7) * 16, n4 = (tid >> 3) * 4;
+  uint32_t col[4][4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t w[4], c[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = *reinterpret_cast<const uint32_t*>(tile + (m16 + 4 * q + i) * kCTP + n4);
+    transpose4x4(w, c);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) col[j][q] = c[j];
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    *reinterpret_cast<uint4*>(y + (long)(tc + n4 + j) * R + tr + m16) = make_uint4(col[j][0], col[j][1], col[j][2], col[j][3]);
+}
+
 // ------------------------------------------------------------------------------------------------ GEMM
 constexpr int BM = 128, BN = 128, BK = 64;  // BK in fp8 elements (= bytes)
 
@@ -447,6 +511,50 @@ torch::Tensor fp8_amax(torch::Tensor x, c10::optional<torch::Tensor> out) {
   hipLaunchKernelGGL(amax_kernel, dim3(g), dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(x.data_ptr()), n,
                      reinterpret_cast<unsigned int*>(o.data_ptr()));
   return o;
+}
+
+
+// Per-segment amax of a flat bf16 shard: out[k] = max |x[lo[k]:hi[k]]| (0 for empty segments). lo/hi: int64 device;
+// max_len: the longest segment (sizes the grid; every segment must be no longer).
+void fp8_segment_amax(torch::Tensor x, torch::Tensor lo, torch::Tensor hi, torch::Tensor out, int64_t max_len) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous(), "fp8_segment_amax: contiguous bf16 x");
+  TORCH_CHECK(lo.scalar_type() == at::kLong && hi.scalar_type() == at::kLong && lo.numel() == hi.numel() &&
+              out.scalar_type() == at::kFloat && out.numel() == lo.numel(), "fp8_segment_amax: bad segment tensors");
+  auto stream = at::hip::getCurrentHIPStream();
+  hipMemsetAsync(out.data_ptr(), 0, out.numel() * sizeof(float), stream);
+  const long nseg = lo.numel();
+  if (nseg == 0 || x.numel() == 0) return;
+  TORCH_CHECK(max_len >= 0 && max_len <= x.numel(), "fp8_segment_amax: max_len");
+  const long chunks = std::max<long>(1, (max_len + kSegChunk - 1) / kSegChunk);  // chunks of the longest segment
+  hipLaunchKernelGGL(seg_amax_kernel, dim3(chunks, nseg), dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(x.data_ptr()),
+                     lo.data_ptr<long>(), hi.data_ptr<long>(), reinterpret_cast<unsigned int*>(out.data_ptr()));
+}
+
+// y[lo[k]:hi[k]] = e4m3(x * qmax / amax[k]) segment by segment (y: fp8 e4m3 flat buffer of x's size).
+void fp8_segment_cast(torch::Tensor x, torch::Tensor lo, torch::Tensor hi, torch::Tensor amax, double qmax, torch::Tensor y,
+                      int64_t max_len) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous(), "fp8_segment_cast: contiguous bf16 x");
+  TORCH_CHECK(y.scalar_type() == at::kFloat8_e4m3fn && y.is_contiguous() && y.numel() == x.numel(), "fp8_segment_cast: y");
+  TORCH_CHECK(amax.scalar_type() == at::kFloat && amax.numel() == lo.numel(), "fp8_segment_cast: amax");
+  const long nseg = lo.numel();
+  if (nseg == 0 || x.numel() == 0) return;
+  TORCH_CHECK(max_len >= 0 && max_len <= x.numel(), "fp8_segment_cast: max_len");
+  const long chunks = std::max<long>(1, (max_len + kSegChunk - 1) / kSegChunk);
+  hipLaunchKernelGGL(seg_cast_kernel, dim3(chunks, nseg), dim3(256), 0, at::hip::getCurrentHIPStream(),
+                     reinterpret_cast<const bf16_t*>(x.data_ptr()), lo.data_ptr<long>(), hi.data_ptr<long>(),
+                     amax.data_ptr<float>(), (float)qmax, reinterpret_cast<uint8_t*>(y.data_ptr()));
+}
+
+// x^T of a 2-D one-byte tensor (fp8 / uint8).
+torch::Tensor u8_transpose(torch::Tensor x) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.is_contiguous() && x.element_size() == 1, "u8_transpose: 2-D contiguous byte tensor");
+  const int R = x.size(0), C = x.size(1);
+  auto y = torch::empty({C, R}, x.options());
+  if (R == 0 || C == 0) return y;
+  dim3 grid((C + kCT - 1) / kCT, (R + kCT - 1) / kCT);
+  hipLaunchKernelGGL(u8_transpose_kernel, grid, dim3(256), 0, at::hip::getCurrentHIPStream(),
+                     reinterpret_cast<const uint8_t*>(x.data_ptr()), reinterpret_cast<uint8_t*>(y.data_ptr()), R, C);
+  return y;
 }
 
 // scale = from_amax ? qmax / max(t, 1e-12) : t * qmax, read on the device (t: fp32 [1]).

@@ -108,6 +108,13 @@ def gemm(a8: torch.Tensor, b8: torch.Tensor, a_scale_inv, b_scale_inv, bias=None
     return out
 
 
+def transpose_fp8(w8: torch.Tensor) -> torch.Tensor:
+    """K-major copy of a 2-D fp8 tensor (HIP byte transpose on GPU)."""
+    if w8.is_cuda and use_native(w8):
+        return ext().u8_transpose(w8.contiguous())
+    return w8.t().contiguous()
+
+
 def _gemm_ok(M, N, K):
     return M % 128 == 0 and N % 128 == 0 and K % 64 == 0
 
@@ -150,17 +157,26 @@ class _Fp8LinearFn(torch.autograd.Function):
     reports the parameter's gradient as ready — no separate dW tensor, no AccumulateGrad add."""
 
     @staticmethod
-    def forward(ctx, x, w, bias, recipe: Fp8Recipe, slot=None):
+    def forward(ctx, x, w, bias, recipe: Fp8Recipe, slot=None, w_amax=None):
         shape = x.shape
         x2 = x.reshape(-1, shape[-1])
         N = w.shape[0]
         fwd_max = E5M2_MAX if recipe.fwd_e5m2() else E4M3_MAX
         sx = recipe.scale("x", x2, fwd_max)
-        sw = recipe.scale("w", w, fwd_max)
         x8, x8t = cast(x2, sx, recipe.fwd_e5m2(), transpose=True)
-        w8, w8t = cast(w, sw, recipe.fwd_e5m2(), transpose=True)
-        y = gemm(x8, w8, sx, sw, bias, torch.bfloat16)
-        ctx.save_for_backward(x8t, w8t, sx.amax, sw.amax)
+        ctx.pre_quantised = w_amax is not None
+        if ctx.pre_quantised:
+            # FSDP fp8 all-gather: `w` already IS the e4m3 weight (gathered, scale 448 / w_amax); its K-major copy
+            # for the dgrad GEMM is made in backward from the (re-gathered) weight instead of being kept alive.
+            sw = Scale(w_amax, E4M3_MAX)
+            w8 = w
+            y = gemm(x8, w8, sx, sw, bias, torch.bfloat16)
+            ctx.save_for_backward(x8t, w, sx.amax, sw.amax)
+        else:
+            sw = recipe.scale("w", w, fwd_max)
+            w8, w8t = cast(w, sw, recipe.fwd_e5m2(), transpose=True)
+            y = gemm(x8, w8, sx, sw, bias, torch.bfloat16)
+            ctx.save_for_backward(x8t, w8t, sx.amax, sw.amax)
         ctx.qmax = (sx.qmax, sw.qmax)
         ctx.recipe, ctx.shape, ctx.has_bias, ctx.slot = recipe, shape, bias is not None, slot
         return y.view(*shape[:-1], N)
@@ -168,6 +184,8 @@ class _Fp8LinearFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x8t, w8t, ax, aw = ctx.saved_tensors
+        if ctx.pre_quantised:
+            w8t = transpose_fp8(w8t)
         sx, sw = Scale(ax, ctx.qmax[0]), Scale(aw, ctx.qmax[1])
         recipe = ctx.recipe
         N = dy.shape[-1]
@@ -182,9 +200,9 @@ class _Fp8LinearFn(torch.autograd.Function):
             dest, acc = slot.engine._fused_slot_dest(slot)
             gemm(dy8t, x8t, sg, sx, None, out=dest, accumulate=acc)
             slot.engine._fused_slot_done(slot)
-            return dx.view(ctx.shape), None, db, None, None
+            return dx.view(ctx.shape), None, db, None, None, None
         dw = gemm(dy8t, x8t, sg, sx, None, torch.bfloat16)
-        return dx.view(ctx.shape), dw, db, None, None
+        return dx.view(ctx.shape), dw, db, None, None, None
 
 
 _FP8_ON = [True]
@@ -211,19 +229,32 @@ class Fp8Linear(nn.Linear):
 
     def forward(self, x):
         M = x.numel() // x.shape[-1]
+        gathered = getattr(self.weight, "_acc_fp8_ag", None)  # FSDP fp8 all-gather: the weight arrives as e4m3
         if (
             not self.training
             and not getattr(self, "fp8_in_eval", True)
         ) or not _FP8_ON[0] or not _gemm_ok(M, self.out_features, self.in_features) or x.dtype != torch.bfloat16:
-            return nn.functional.linear(x, self.weight.to(x.dtype), None if self.bias is None else self.bias.to(x.dtype))
-        w = self.weight if self.weight.dtype == torch.bfloat16 else self.weight.to(torch.bfloat16)
+            w = self._dequantised(gathered) if gathered is not None else self.weight
+            return nn.functional.linear(x, w.to(x.dtype), None if self.bias is None else self.bias.to(x.dtype))
         b = None if self.bias is None else self.bias.to(torch.bfloat16)
+        if gathered is not None:
+            unit, info = gathered
+            return _Fp8LinearFn.apply(x, self.weight, b, self.fp8_recipe, self._fp8_wgrad_slot(x),
+                                      unit.engine.fp8_weight_scale(unit, info))
+        w = self.weight if self.weight.dtype == torch.bfloat16 else self.weight.to(torch.bfloat16)
         return _Fp8LinearFn.apply(x, w, b, self.fp8_recipe, self._fp8_wgrad_slot(x))
+
+    def _dequantised(self, gathered):
+        """bf16 value of an fp8-gathered weight (non-fp8 fallback paths: eval, unsupported shapes)."""
+        unit, info = gathered
+        amax = unit.engine.fp8_weight_scale(unit, info)
+        return (self.weight.detach().float() * (amax.clamp_min(1e-12) / E4M3_MAX)).to(torch.bfloat16)
 
     def _fp8_wgrad_slot(self, x):
         """The FSDP fused-wgrad slot of this weight (parallel/fsdp.py), when the gradient can be written in place."""
         slot = getattr(self.weight, "_acc_wgrad_slot", None)
-        if slot is None or not torch.is_grad_enabled() or self.weight.dtype != torch.bfloat16:
+        ok_dtype = self.weight.dtype == torch.bfloat16 or getattr(self.weight, "_acc_fp8_ag", None) is not None
+        if slot is None or not torch.is_grad_enabled() or not ok_dtype:
             return None
         if torch._C._current_graph_task_id() == -1:
             slot.uses += 1

@@ -64,7 +64,7 @@ def _round_up(x, m):
 
 class _ParamInfo:
     __slots__ = ("fqn", "module", "attr", "param", "orig_param", "offset", "numel", "shape", "shard_param", "local_lo", "local_hi",
-                 "param_lo", "fused", "fused_written")
+                 "param_lo", "fused", "fused_written", "region", "f8_index")
 
     def __init__(self, fqn, module, attr, param, offset):
         self.fqn = fqn
@@ -79,21 +79,63 @@ class _ParamInfo:
         self.local_lo = self.local_hi = self.param_lo = 0
         self.fused = False  # weight-gradient GEMM writes straight into the flat grad buffer (see _WgradSlot)
         self.fused_written = False
+        self.region = None
+        self.f8_index = -1
+
+
+class _Region:
+    """A contiguous span [base, base + length) of a unit's flat buffer, sharded on its own: rank r owns
+    [base + r * shard_len, base + (r + 1) * shard_len), stored at [shard_base, shard_base + shard_len) of its shard."""
+
+    __slots__ = ("base", "length", "shard_len", "shard_base", "fp8")
+
+    def __init__(self, base, length, world, shard_base, fp8=False):
+        self.base, self.length, self.fp8 = base, length, fp8
+        self.shard_len = length // world
+        self.shard_base = shard_base
+
+    def slice_of(self, rank):
+        lo = self.base + rank * self.shard_len
+        return lo, lo + self.shard_len
 
 
 class FlatUnit:
-    """One sharding unit (e.g. a decoder layer)."""
+    """One sharding unit (e.g. a decoder layer).
 
-    def __init__(self, engine: "FSDPEngine", idx: int, module: nn.Module, infos: list[_ParamInfo]):
+    Its parameters are laid out in one flat buffer made of one or two `_Region`s. Normally a single region; with the
+    fp8 all-gather the unit's fp8 GEMM weights form region 0 (all-gathered as e4m3 bytes) and everything else
+    region 1 (all-gathered in bf16). Each rank's shard is the concatenation of its slice of every region."""
+
+    def __init__(self, engine: "FSDPEngine", idx: int, module: nn.Module, infos: list[_ParamInfo], fp8_count: int = 0):
         self.engine = engine
         self.idx = idx
         self.module = module
-        self.infos = infos
         W = engine.world_size
-        total = sum(i.numel for i in infos)
-        self.numel = total
-        self.padded = _round_up(max(total, 1), W * _ALIGN)
-        self.shard_numel = self.padded // W
+        quantum = W * _ALIGN
+        groups = [infos[:fp8_count], infos[fp8_count:]] if fp8_count else [infos]
+        self.infos, self.regions = [], []
+        base = shard_base = 0
+        for gi, group in enumerate(groups):
+            off = base
+            for info in group:  # pack the group's parameters from the region base
+                info.offset = off
+                off += info.numel
+                self.infos.append(info)
+            length = _round_up(max(off - base, 1), quantum)
+            region = _Region(base, length, W, shard_base, fp8=bool(fp8_count) and gi == 0)
+            self.regions.append(region)
+            base += length
+            shard_base += region.shard_len
+        for info in self.infos:
+            info.region = next(r for r in self.regions if r.base <= info.offset < r.base + r.length) if info.numel else self.regions[-1]
+        self.numel = sum(i.numel for i in infos)
+        self.padded = base
+        self.shard_numel = shard_base
+        self.f8 = self.regions[0] if fp8_count else None
+        self.f8_infos = [i for i in self.infos if self.f8 is not None and i.region is self.f8]
+        # bf16 compute buffer covers the non-fp8 regions only
+        self.bf_base = self.regions[1].base if fp8_count else 0
+        self.f8_shard = self.f8_full = self.f8_amax = None
         self.is_root = False
         self.state = "sharded"  # or "unsharding" / "unsharded"
         self.ag_event: Optional[torch.cuda.Event] = None
@@ -105,14 +147,21 @@ class FlatUnit:
         self.bwd_prefetched = False
         self.in_backward = False
 
-    # --- sizes/ranges ---------------------------------------------------------------------------------
-    @property
-    def shard_lo(self):
-        return self.engine.rank * self.shard_numel
+    # --- layout -------------------------------------------------------------------------------------------
+    def local_of_full(self, full: torch.Tensor) -> torch.Tensor:
+        """This rank's shard (region slices concatenated) cut out of a full-layout tensor."""
+        r = self.engine.rank
+        parts = [full[slice(*reg.slice_of(r))] for reg in self.regions]
+        return parts[0].clone() if len(parts) == 1 else torch.cat(parts)
 
-    @property
-    def shard_hi(self):
-        return self.shard_lo + self.shard_numel
+    def local_range(self, info):
+        """(local_lo, local_hi, param_lo) of `info`'s piece in this rank's shard."""
+        reg = info.region
+        lo, hi = reg.slice_of(self.engine.rank)
+        a, b = max(info.offset, lo), min(info.offset + info.numel, hi)
+        if b <= a:
+            a = b = max(min(info.offset, hi), lo)
+        return reg.shard_base + (a - lo), reg.shard_base + (b - lo), a - info.offset
 
 
 class FSDPEngine:
@@ -127,8 +176,11 @@ class FSDPEngine:
         seed: int = 0,
         prefetch_depth: int = 1,
         force_sharded: bool = False,
+        fp8_all_gather: bool = False,
     ):
         self.model = model
+        self.fp8_all_gather = bool(fp8_all_gather)
+        self.f8_units: list = []
         self.plugin = plugin
         self.device = device
         self.group = process_group
@@ -211,12 +263,21 @@ class FSDPEngine:
         root_infos = self._collect(self.model, "", owned, ignored)
         # Units are created in module order; the root goes first so its index is 0.
         all_units = [(self.model, root_infos, True)] + [(m, infos, False) for m, infos in assigned_units]
+        refs = {}
+        if self.fp8_all_gather:
+            for mod in self.model.modules():
+                for p in mod._parameters.values():
+                    if p is not None:
+                        refs[id(p)] = refs.get(id(p), 0) + 1
         for idx, (m, infos, is_root) in enumerate(all_units):
-            unit = FlatUnit(self, idx, m, infos)
+            f8 = [i for i in infos if self._fp8_gathered(i, refs)]
+            f8_ids = {id(i) for i in f8}
+            unit = FlatUnit(self, idx, m, f8 + [i for i in infos if id(i) not in f8_ids], fp8_count=len(f8))
             unit.is_root = is_root
             self._materialize(unit, init_fn, seed)
             self.units.append(unit)
         self.root = self.units[0]
+        self._init_fp8_all_gather()
         # parameters the engine does not own (ignored modules, expert-parallel experts): kept as plain device
         # tensors; they still take part in the global grad-norm (see clip_grad_norm_)
         self.extra_names = [n for n, p in self.model.named_parameters() if id(p) in ignored]
@@ -233,6 +294,78 @@ class FSDPEngine:
                     info.param.register_post_accumulate_grad_hook(self._make_grad_hook(unit))
         if os.environ.get("ACCELERATE_FSDP_FUSED_WGRAD", "1") != "0":
             self._install_fused_wgrad()
+
+    # =========================================================================================== fp8 all-gather
+    def _fp8_gathered(self, info: _ParamInfo, refs: dict) -> bool:
+        """Whether `info` is an fp8 GEMM weight that travels as e4m3 in the all-gather (torchao
+        `enable_fsdp_float8_all_gather` semantics: dynamic per-tensor scaling from the global amax)."""
+        if not self.fp8_all_gather or self.param_dtype != torch.bfloat16 or self.offload:
+            return False
+        m = info.module
+        rec = getattr(m, "fp8_recipe", None)
+        return (isinstance(m, Fp8Linear) and info.attr == "weight" and info.param.requires_grad and len(info.shape) == 2
+                and refs.get(id(info.param), 0) == 1 and getattr(info.param, "_tp_spec", None) is None
+                and rec is not None and not rec.delayed and not rec.fwd_e5m2())
+
+    def _init_fp8_all_gather(self):
+        """Index the fp8-gathered weights (one amax slot each, in one engine-wide buffer so the global amax is ONE
+        all-reduce per step) and quantise the initial shards."""
+        self.f8_units = [u for u in self.units if u.f8 is not None]
+        if not self.f8_units:
+            return
+        n = 0
+        for u in self.f8_units:
+            lo, hi = [], []
+            for info in u.f8_infos:
+                info.f8_index = n
+                n += 1
+                lo.append(info.local_lo)
+                hi.append(info.local_hi)
+                info.param._acc_fp8_ag = (u, info)  # read by Fp8Linear.forward
+            assert max(hi, default=0) <= u.f8.shard_len and min(lo, default=0) >= 0, "fp8 segment outside the fp8 region"
+            u.f8_seg = (torch.tensor(lo, dtype=torch.long, device=self.device), torch.tensor(hi, dtype=torch.long, device=self.device),
+                        max((b - a for a, b in zip(lo, hi)), default=0), n - len(lo))
+        self.f8_amax_all = torch.zeros(n, dtype=torch.float32, device=self.device)
+        for u in self.f8_units:
+            first = u.f8_seg[3]
+            u.f8_amax = self.f8_amax_all[first : first + len(u.f8_infos)]
+        self.refresh_fp8()
+
+    @torch.no_grad()
+    def refresh_fp8(self):
+        """Re-quantise the fp8-gathered weights from the bf16 shards: per-weight amax of the local pieces, ONE
+        all-reduce(MAX) over the shard group for every weight of the model (torchao's
+        `precompute_float8_dynamic_scale_for_fsdp`, reference accelerator.py:2061-2066), then the per-weight scaled
+        cast of each shard into its e4m3 all-gather source. Runs after every optimizer step."""
+        if not self.f8_units:
+            return
+        from ..ops._ext import use_native
+
+        for u in self.f8_units:
+            lo, hi, max_len, _ = u.f8_seg
+            src = u.shard_lp[: u.f8.shard_len]
+            if use_native(src):
+                ext().fp8_segment_amax(src, lo, hi, u.f8_amax, max_len)
+            else:
+                for k, info in enumerate(u.f8_infos):
+                    piece = src[info.local_lo : info.local_hi]
+                    u.f8_amax[k] = piece.abs().max().float() if piece.numel() else 0.0
+        if self.sharded and self.world_size > 1:
+            dist.all_reduce(self.f8_amax_all, op=dist.ReduceOp.MAX, group=self.group)
+        for u in self.f8_units:
+            lo, hi, max_len, _ = u.f8_seg
+            src = u.shard_lp[: u.f8.shard_len]
+            if use_native(src):
+                ext().fp8_segment_cast(src, lo, hi, u.f8_amax, 448.0, u.f8_shard, max_len)
+            else:
+                for k, info in enumerate(u.f8_infos):
+                    s = 448.0 / u.f8_amax[k].clamp_min(1e-12)
+                    piece = (src[info.local_lo : info.local_hi].float() * s).clamp(-448.0, 448.0)
+                    u.f8_shard[info.local_lo : info.local_hi] = piece.to(torch.float8_e4m3fn)
+
+    def fp8_weight_scale(self, unit: FlatUnit, info: _ParamInfo) -> torch.Tensor:
+        """The amax (fp32 [1], device) whose scale 448 / amax quantised this gathered weight."""
+        return unit.f8_amax[info.f8_index - unit.f8_seg[3] : info.f8_index - unit.f8_seg[3] + 1]
 
     def _install_fused_wgrad(self):
         """Route the weight gradient of every plain `nn.Linear` whose weight this engine owns (and that no other module
@@ -322,32 +455,33 @@ class FSDPEngine:
                 full32[info.offset : info.offset + info.numel].copy_(info.param.detach().reshape(-1).to(dev, torch.float32))
         if W > 1 and (ram_efficient or (self.plugin.sync_module_states and not on_meta)):
             dist.broadcast(full32, src=dist.get_global_rank(self.group, 0) if self.group is not None else 0, group=self.group)
-        lo, hi = r * unit.shard_numel, (r + 1) * unit.shard_numel
+        local32 = unit.local_of_full(full32)  # this rank's slice of every region, concatenated
         if self.offload:
-            unit.master = self._host(full32[lo:hi])
+            unit.master = self._host(local32)
             unit.grad_shard = self._host(torch.zeros(unit.shard_numel, dtype=torch.float32))
-            unit.shard_lp = full32[lo:hi].to(self.param_dtype, copy=True)  # HBM-resident all-gather source
+            unit.shard_lp = local32.to(self.param_dtype, copy=True)  # HBM-resident all-gather source
             # what the host optimizer writes for upload (bf16), or None: upload the fp32 master and cast on the GPU
             unit.shadow_host = self._host(torch.empty(unit.shard_numel, dtype=self.param_dtype)) if self.param_dtype != torch.float32 else None
         else:
-            unit.master = full32[lo:hi].clone()
+            unit.master = local32
             unit.grad_shard = torch.zeros_like(unit.master)
             unit.shard_lp = unit.master.to(self.param_dtype) if self.param_dtype != torch.float32 else unit.master
         unit.grad_valid = False
-        del full32
+        del full32, local32
         if not self.sharded:
-            unit.full = unit.shard_lp  # degenerate: no collective, the shard is the full buffer
+            # degenerate: no collective, the shard is the full buffer (its bf16 regions start at bf_base)
+            unit.full = unit.shard_lp[unit.bf_base :]
         else:
-            unit.full = torch.empty(unit.padded, dtype=self.param_dtype, device=dev)
-        # Point every original parameter at its slice of the full buffer (views survive storage resizes).
+            unit.full = torch.empty(unit.padded - unit.bf_base, dtype=self.param_dtype, device=dev)
+        if unit.f8 is not None:
+            unit.f8_shard = torch.zeros(unit.f8.shard_len, dtype=torch.float8_e4m3fn, device=dev)
+            unit.f8_full = unit.f8_shard if not self.sharded else torch.zeros(unit.f8.length, dtype=torch.float8_e4m3fn, device=dev)
+        # Point every original parameter at its slice of the full buffer (views survive storage resizes): fp8
+        # all-gathered weights at their e4m3 copy, everything else at the compute-dtype buffer.
         for info in unit.infos:
-            info.param.data = unit.full[info.offset : info.offset + info.numel].view(info.shape)
+            info.param.data = self._full_view(unit, info)
             # per-parameter views of the local shard, exposed to the optimizer
-            plo, phi = info.offset, info.offset + info.numel
-            a, b = max(plo, lo), min(phi, hi)
-            if b <= a:
-                a = b = max(min(plo, hi), lo)
-            info.local_lo, info.local_hi, info.param_lo = a - lo, b - lo, a - plo
+            info.local_lo, info.local_hi, info.param_lo = unit.local_range(info)
             sp = nn.Parameter(unit.master[info.local_lo : info.local_hi], requires_grad=info.param.requires_grad)
             if self.offload:
                 sp._acc_offloaded = True
@@ -365,6 +499,28 @@ class FSDPEngine:
         else:
             unit.state = "unsharded"
 
+    def _full_view(self, unit: FlatUnit, info: _ParamInfo) -> torch.Tensor:
+        if unit.f8 is not None and info.region is unit.f8:
+            return unit.f8_full[info.offset : info.offset + info.numel].view(info.shape)
+        o = info.offset - unit.bf_base
+        return unit.full[o : o + info.numel].view(info.shape)
+
+    def _bf_regions(self, unit: FlatUnit):
+        return [reg for reg in unit.regions if not reg.fp8]
+
+    def gather_full(self, unit: FlatUnit, local: torch.Tensor) -> torch.Tensor:
+        """A full-layout tensor assembled from every rank's shard-layout `local` (one all-gather per region)."""
+        if not self.sharded:
+            return local
+        full = torch.empty(unit.padded, dtype=local.dtype, device=local.device)
+        for reg in unit.regions:
+            dst, src = full[reg.base : reg.base + reg.length], local[reg.shard_base : reg.shard_base + reg.shard_len]
+            if self._uses_gloo and self._gloo():
+                dist.all_gather(list(dst.chunk(self.world_size)), src, group=self.group)
+            else:
+                dist.all_gather_into_tensor(dst, src, group=self.group)
+        return full
+
     def _host(self, t: torch.Tensor) -> torch.Tensor:
         """A host copy of `t` (pinned when offloading to a GPU run, so D2H/H2D are true async DMA)."""
         h = t.detach().to("cpu", copy=True)
@@ -375,6 +531,8 @@ class FSDPEngine:
         if not self.sharded or unit.state == "sharded":
             return
         unit.full.untyped_storage().resize_(0)
+        if unit.f8 is not None:
+            unit.f8_full.untyped_storage().resize_(0)
         unit.state = "sharded"
         unit.ag_event = None
 
@@ -382,28 +540,38 @@ class FSDPEngine:
         """Issue the all-gather of `unit` on the AG stream (no host wait). Idempotent."""
         if not self.sharded or unit.state != "sharded":
             return
-        nbytes = unit.padded * unit.full.element_size()
-        unit.full.untyped_storage().resize_(nbytes)
+        unit.full.untyped_storage().resize_(unit.full.numel() * unit.full.element_size())
+        if unit.f8 is not None:
+            unit.f8_full.untyped_storage().resize_(unit.f8_full.numel())
         if self.is_cuda:
             cur = torch.cuda.current_stream(self.device)
             self.ag_stream.wait_stream(cur)
             record_collective("fsdp_all_gather", unit.shard_lp, self.group)
             with torch.cuda.stream(self.ag_stream), trace_range(f"fsdp.all_gather[{unit.idx}]"):
-                dist.all_gather_into_tensor(unit.full, unit.shard_lp, group=self.ag_group)
+                self._all_gather_unit(unit, self.ag_group)
                 ev = torch.cuda.Event()
                 ev.record(self.ag_stream)
             unit.ag_event = ev
         else:
-            dist.all_gather_into_tensor(unit.full, unit.shard_lp, group=self.group) if not self._gloo() else self._gloo_allgather(unit)
+            self._all_gather_unit(unit, self.group)
             unit.ag_event = None
         unit.state = "unsharding"
 
+    def _all_gather_unit(self, unit: FlatUnit, group):
+        """bf16 regions into `unit.full`; the fp8 region (e4m3 bytes, half the traffic) into `unit.f8_full`."""
+        gloo = self._uses_gloo and self._gloo()
+        pairs = [(unit.full[reg.base - unit.bf_base : reg.base - unit.bf_base + reg.length],
+                  unit.shard_lp[reg.shard_base : reg.shard_base + reg.shard_len]) for reg in self._bf_regions(unit)]
+        if unit.f8 is not None:
+            pairs.append((unit.f8_full.view(torch.uint8), unit.f8_shard.view(torch.uint8)))
+        for dst, src in pairs:
+            if gloo:
+                dist.all_gather(list(dst.chunk(self.world_size)), src, group=group)
+            else:
+                dist.all_gather_into_tensor(dst, src, group=group)
+
     def _gloo(self):
         return dist.get_backend(self.group) == "gloo"
-
-    def _gloo_allgather(self, unit):
-        chunks = list(unit.full.chunk(self.world_size))
-        dist.all_gather(chunks, unit.shard_lp, group=self.group)
 
     def _wait_unsharded(self, unit: FlatUnit):
         if unit.state == "sharded":
@@ -701,10 +869,13 @@ class FSDPEngine:
         W = self.world_size
         if self.sharded:
             record_collective("fsdp_reduce_scatter", src, self.group)
-            if self._uses_gloo and self._gloo():
-                self._gloo_rs(out, src)
-            else:
-                dist.reduce_scatter_tensor(out, src, group=self.rs_group)
+            for reg in unit.regions:  # one reduce-scatter per region (a single one in the plain layout)
+                o = out[reg.shard_base : reg.shard_base + reg.shard_len]
+                i = src[reg.base : reg.base + reg.length]
+                if self._uses_gloo and self._gloo():
+                    self._gloo_rs(o, i)
+                else:
+                    dist.reduce_scatter_tensor(o, i, group=self.rs_group)
         else:
             out.copy_(src[: unit.shard_numel])
         if self.replicate_group is not None and self.replicate_size > 1:
@@ -839,6 +1010,7 @@ class FSDPEngine:
         elif self.param_dtype != torch.float32 and not fused_wrote_shadow:
             for unit in self.units:
                 unit.shard_lp.copy_(unit.master)
+        self.refresh_fp8()  # the bf16 shards are current: re-quantise the fp8 all-gather sources
         if self.sharded:
             for unit in self.units:
                 if unit.state == "unsharding" and unit.ag_event is not None and self.is_cuda:
@@ -887,15 +1059,8 @@ class FSDPEngine:
         """Gather the fp32 master weights unit by unit (one all-gather per unit) → {fqn: full tensor}."""
         out = OrderedDict()
         for unit in self.units:
-            if self.sharded:
-                full = torch.empty(unit.padded, dtype=torch.float32, device=self.device)
-                master = unit.master.to(self.device) if self.offload else unit.master
-                if self._uses_gloo and self._gloo():
-                    dist.all_gather(list(full.chunk(self.world_size)), master, group=self.group)
-                else:
-                    dist.all_gather_into_tensor(full, master, group=self.group)
-            else:
-                full = unit.master
+            master = unit.master.to(self.device) if self.offload else unit.master
+            full = self.gather_full(unit, master)
             if rank0_only and self.rank != 0:
                 continue
             for info in unit.infos:
@@ -962,6 +1127,7 @@ class FSDPEngine:
                 unit.master[info.local_lo : info.local_hi].copy_(piece.to(unit.master.device, torch.float32))
             if unit.shard_lp is not unit.master:
                 unit.shard_lp.copy_(unit.master.to(unit.shard_lp.device))
+        self.refresh_fp8()
         for name, _ in self._extras():
             if name in sd:
                 self._load_extra(name, sd[name])
@@ -988,6 +1154,7 @@ class FSDPEngine:
                         unit.master[info.local_lo + (a - lo_need) : info.local_lo + (b - lo_need)].copy_(src.to(unit.master.device))
             if unit.shard_lp is not unit.master:
                 unit.shard_lp.copy_(unit.master.to(unit.shard_lp.device))
+        self.refresh_fp8()
         for name, p in self._extras():
             found = [(m.get("extra", {}).get(name), t) for t, m in pieces if name in m.get("extra", {})]
             if not found:
@@ -1173,6 +1340,7 @@ def fully_shard(
     seed: int = 0,
     prefetch_depth: int = 1,
     force_sharded: Optional[bool] = None,
+    fp8_all_gather: bool = False,
 ) -> FullyShardedModule:
     """Shard `model` with the native engine and return the wrapper."""
     if plugin is None:
@@ -1185,7 +1353,8 @@ def fully_shard(
         apply_activation_checkpointing(model, plugin)
     if force_sharded is None:
         force_sharded = os.environ.get("ACCELERATE_FSDP_FORCE_SHARDED", "0") == "1"
-    engine = FSDPEngine(model, plugin, device, process_group, replicate_group, init_fn, seed, prefetch_depth, force_sharded)
+    engine = FSDPEngine(model, plugin, device, process_group, replicate_group, init_fn, seed, prefetch_depth, force_sharded,
+                        fp8_all_gather)
     return FullyShardedModule(model, engine)
 
 

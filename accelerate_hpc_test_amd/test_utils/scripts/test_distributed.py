@@ -722,6 +722,76 @@ def check_broadcast_from_rank0_loading():
         assert torch.equal(full[k], v), (r, k)
 
 
+class _F8Block(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.norm = torch.nn.LayerNorm(128)
+        self.fc1 = torch.nn.Linear(128, 256)
+        self.fc2 = torch.nn.Linear(256, 128)
+
+    def forward(self, x):
+        return x + self.fc2(torch.relu(self.fc1(self.norm(x))))
+
+
+class _F8Net(torch.nn.Module):
+    """128-wide blocks so every inner linear takes the fp8 GEMM path (M % 128, N % 128, K % 64)."""
+
+    def __init__(self):
+        super().__init__()
+        self.inp = torch.nn.Linear(128, 128)
+        self.blocks = torch.nn.ModuleList([_F8Block() for _ in range(2)])
+        self.out = torch.nn.Linear(128, 1)
+
+    def forward(self, x):
+        x = self.inp(x)
+        for b in self.blocks:
+            x = b(x)
+        return self.out(x).squeeze(-1)
+
+
+def check_fsdp_fp8_all_gather(force_sharded: bool = False):
+    """AORecipeKwargs(enable_fsdp_float8_all_gather=True): the fp8 GEMM weights travel as e4m3 shards quantised with
+    the all-reduced global amax. That is the same quantisation as casting the gathered bf16 weight, so losses and
+    weights must equal the bf16-all-gather run exactly."""
+    from accelerate_hpc_test_amd.state import AcceleratorState, GradientState
+    from accelerate_hpc_test_amd.utils import AORecipeKwargs
+
+    if force_sharded:
+        os.environ["ACCELERATE_FSDP_FORCE_SHARDED"] = "1"
+    results = {}
+    for ag in (False, True):
+        AcceleratorState._reset_state(True)
+        GradientState._reset_state()
+        plugin = FullyShardedDataParallelPlugin(fsdp_version=2, auto_wrap_policy="transformer_based_wrap",
+                                                transformer_cls_names_to_wrap=["_F8Block"])
+        acc = Accelerator(cpu=True, mixed_precision="fp8", fsdp_plugin=plugin,
+                          kwargs_handlers=[AORecipeKwargs(enable_fsdp_float8_all_gather=ag)])
+        W, r = acc.num_processes, acc.process_index
+        torch.manual_seed(0)
+        model = _F8Net()
+        opt = torch.optim.AdamW(model.parameters(), lr=1e-2)
+        model, opt = acc.prepare(model, opt)
+        eng = model.engine
+        assert bool(eng.f8_units) == ag and eng.fp8_all_gather == ag
+        if ag:
+            f8_names = sorted(i.fqn for u in eng.f8_units for i in u.f8_infos)
+            assert f8_names == sorted(f"blocks.{b}.{n}.weight" for b in range(2) for n in ("fc1", "fc2")), f8_names
+        losses = []
+        g = torch.Generator().manual_seed(1)
+        for _ in range(3):
+            x = torch.randn(128 * W, 128, generator=g)
+            y = torch.randn(128 * W, generator=g)
+            loss = F.mse_loss(model(x[r * 128 : (r + 1) * 128]).float(), y[r * 128 : (r + 1) * 128])
+            acc.backward(loss)
+            opt.step()
+            opt.zero_grad()
+            losses.append(loss.item())
+        results[ag] = (losses, acc.get_state_dict(model))
+    assert results[False][0] == results[True][0], (results[False][0], results[True][0])
+    for n, t in results[False][1].items():
+        assert torch.equal(t, results[True][1][n]), n
+
+
 def check_ddp_powersgd():
     """PowerSGD hook: with start_powerSGD_iter=0 training still converges and ranks stay in sync."""
     from accelerate_hpc_test_amd.utils import DDPCommunicationHookType, DistributedDataParallelKwargs

@@ -117,14 +117,7 @@ def _optim_full_state(eng, optimizer):
                 t = opt.state.get(info.shard_param, {}).get(key)
                 if t is not None and info.local_hi > info.local_lo:
                     local[info.local_lo : info.local_hi].copy_(t.reshape(-1).float())
-            if eng.world_size > 1:
-                full = torch.empty(unit.padded, dtype=torch.float32, device=eng.device)
-                if eng._uses_gloo and eng._gloo():
-                    dist.all_gather(list(full.chunk(eng.world_size)), local, group=eng.group)
-                else:
-                    dist.all_gather_into_tensor(full, local, group=eng.group)
-            else:
-                full = local
+            full = eng.gather_full(unit, local)
             for info in unit.infos:
                 out.setdefault(info.fqn, {})[key] = full[info.offset : info.offset + info.numel].view(info.shape).cpu().clone()
     groups = []

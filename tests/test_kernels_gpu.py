@@ -486,7 +486,7 @@ def test_fsdp_wgrad_from_transposed_input_matches(monkeypatch, direct):
         assert torch.allclose(t, finals[True][n], atol=2e-4, rtol=1e-3), (n, (t - finals[True][n]).abs().max())
 
 
-def _llama_tiny_run(steps, handlers=(), preset="llama-tiny", lr=1e-3, seed_ids=1, clip=None, **plugin_kw):
+def _llama_tiny_run(steps, handlers=(), preset="llama-tiny", lr=1e-3, seed_ids=1, clip=None, precision="bf16", **plugin_kw):
     from accelerate_hpc_test_amd import Accelerator, FullyShardedDataParallelPlugin
     from accelerate_hpc_test_amd.models.llama import LLAMA_PRESETS, LlamaForCausalLM
     from accelerate_hpc_test_amd.state import AcceleratorState, GradientState
@@ -495,7 +495,7 @@ def _llama_tiny_run(steps, handlers=(), preset="llama-tiny", lr=1e-3, seed_ids=1
     GradientState._reset_state()
     plugin = FullyShardedDataParallelPlugin(fsdp_version=2, auto_wrap_policy="transformer_based_wrap",
                                             transformer_cls_names_to_wrap=["LlamaDecoderLayer"], **plugin_kw)
-    acc = Accelerator(mixed_precision="bf16", fsdp_plugin=plugin, kwargs_handlers=list(handlers))
+    acc = Accelerator(mixed_precision=precision, fsdp_plugin=plugin, kwargs_handlers=list(handlers))
     with torch.device("meta"):
         model = LlamaForCausalLM(LLAMA_PRESETS[preset])
     opt = torch.optim.AdamW(model.parameters(), lr=lr)
@@ -701,3 +701,50 @@ def test_device_prefetcher_stops_on_early_exit():
     it.close()  # what `break` does to a for-loop's generator
     time.sleep(0.2)
     assert not any(p.thread.is_alive() for p in pref)
+
+
+@pytest.mark.parametrize("force", [False, True])
+def test_fsdp_fp8_all_gather_matches_bf16_all_gather(one_rank_rccl, force):
+    """AORecipeKwargs(enable_fsdp_float8_all_gather=True) (reference examples/torch_native_parallelism/fsdp2_fp8.py:69-75):
+    fp8 GEMM weights all-gathered as e4m3 (half the bytes), quantised from the shards with one batched all-reduce(MAX) of
+    the per-weight amaxes after each step (HIP segment amax / cast kernels), dgrad operand by the HIP byte transpose.
+    Identical quantisation to casting the gathered bf16 weight, so losses, grad norms and weights match bit for bit."""
+    from accelerate_hpc_test_amd.utils import AORecipeKwargs, RcclKwargs
+
+    res = {}
+    for ag in (False, True):
+        acc, model, losses, norms = _llama_tiny_run(3, [RcclKwargs(fsdp_force_sharded=force),
+                                                        AORecipeKwargs(enable_fsdp_float8_all_gather=ag)],
+                                                    clip=1e9, precision="fp8")
+        eng = model.engine
+        assert bool(eng.f8_units) == ag
+        if ag:
+            assert all(i.param.dtype == torch.float8_e4m3fn for u in eng.f8_units for i in u.f8_infos)
+        res[ag] = (losses, norms, acc.get_state_dict(model))
+    assert res[False][0] == res[True][0], (res[False][0], res[True][0])
+    assert res[False][1] == res[True][1], (res[False][1], res[True][1])
+    for n, t in res[False][2].items():
+        assert torch.equal(t, res[True][2][n]), n
+
+
+def test_fp8_segment_kernels_and_byte_transpose():
+    from accelerate_hpc_test_amd.ops._ext import ext
+
+    torch.manual_seed(0)
+    x = torch.randn(100_003, device=DEV, dtype=torch.bfloat16) * 3
+    lo = torch.tensor([0, 17, 5000, 5000, 70_000], device=DEV)
+    hi = torch.tensor([17, 5000, 5000, 70_000, 100_003], device=DEV)
+    amax = torch.empty(5, device=DEV)
+    ext().fp8_segment_amax(x, lo, hi, amax, 65_000)
+    ref = [x[a:b].float().abs().max().item() if b > a else 0.0 for a, b in zip(lo.tolist(), hi.tolist())]
+    assert amax.tolist() == ref
+    y = torch.empty(x.numel(), device=DEV, dtype=torch.float8_e4m3fn)
+    ext().fp8_segment_cast(x, lo, hi, amax, 448.0, y, 65_000)
+    for k, (a, b) in enumerate(zip(lo.tolist(), hi.tolist())):
+        if b > a:  # same bytes as the whole-tensor cast kernel with that segment's amax
+            whole = ext().fp8_cast(x[a:b].view(1, -1).contiguous(), amax[k : k + 1], 448.0, True, False, False)[0]
+            assert torch.equal(y[a:b].view(torch.uint8), whole.view(-1).view(torch.uint8)), k
+    w = torch.randint(0, 255, (384, 640), device=DEV, dtype=torch.uint8)
+    assert torch.equal(ext().u8_transpose(w), w.t().contiguous())
+    w2 = torch.randint(0, 255, (200, 136), device=DEV, dtype=torch.uint8)  # edge tiles
+    assert torch.equal(ext().u8_transpose(w2), w2.t().contiguous())

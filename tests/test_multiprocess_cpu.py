@@ -65,6 +65,11 @@ def test_broadcast_from_rank0_checkpoint_loading(world):
     debug_launcher(td.check_broadcast_from_rank0_loading, num_processes=world)
 
 
+@pytest.mark.parametrize("world,force", [(1, False), (1, True), (2, False)])
+def test_fsdp_fp8_all_gather_matches_bf16_all_gather(world, force):
+    debug_launcher(td.check_fsdp_fp8_all_gather, args=(force,), num_processes=world)
+
+
 def test_fsdp_single_rank_matches_torch():
     """World size 1: fused weight grads go straight to the fp32 grad shard (no flat-buffer copy)."""
     debug_launcher(td.check_fsdp_matches_single, args=(True, "SHARDED_STATE_DICT"), num_processes=1)
