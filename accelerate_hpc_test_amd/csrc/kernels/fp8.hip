@@ -497,6 +497,175 @@ __global__ __launch_bounds__(512, 1) void fp8_gemm_v2_w8_kernel(const uint8_t* _
   fp8_gemm_v2_body<FA, FB, OUT_F32, 2, 4>(A, B, sa, sb, smul, bias, C, M, N, K, accum);
 }
 
+// ------------------------------------------------------------------------------------------------ GEMM v3
+// 256x256 output tile, 8 waves (2 x 4, 128x64 per wave = 8 MX 32x32x64 accumulators, 128 AGPRs, two waves per SIMD),
+// BK = 64 fp8 bytes per K-tile (32 KiB of A+B), a FOUR-deep LDS ring filled by global_load_lds. Per K-tile t:
+//   MFMAs on the first half of the wave's tile (fragments of t already in registers)
+//   s_waitcnt vmcnt(8)   -- only tile t+1 must have landed; t+2, t+3 stay in flight ACROSS the barrier
+//   s_barrier            -- t+1 visible to every wave; every wave's reads of t retired (lgkmcnt(0) before it)
+//   DMA of tile t+4 into t's slot; ds_reads of t+1's fragments into the second register set
+//   MFMAs on the second half (the fragment reads and the DMA issue hide under them)
+// so no K-tile ever starts with an exposed LDS-read latency or a drained DMA queue (v2's vmcnt(0) + barrier per K-step
+// left the MFMA pipe idle for both at one wave per SIMD). Image rows are 64 B; 16-B chunk swizzle c ^ ((row >> 2) & 3)
+// makes every 16-lane ds_read_b128 group of a 32x32x64 fragment cover the 16 slots of a 256-B bank row.
+constexpr int V3_BM = 256, V3_BN = 256, V3_BK = 64;
+constexpr int V3_TILE = (V3_BM + V3_BN) * V3_BK;  // 32 KiB per K-tile: A 256x64 | B 256x64
+constexpr int V3_BOFF = V3_BM * V3_BK;
+
+__device__ __forceinline__ int v3_swz(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }
+
+template <int FA, int FB, bool OUT_F32>
+__global__ __launch_bounds__(512, 1) void fp8_gemm_v3_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
+                                                             const float* __restrict__ sa, const float* __restrict__ sb, float smul,
+                                                             const bf16_t* __restrict__ bias, void* __restrict__ C, int M, int N,
+                                                             int K, int accum) {
+  // one LDS object per ring slot, each addressed with a compile-time identity (the loop is unrolled by the ring
+  // depth): distinct objects carry distinct alias scopes, so hipcc does not drain the other slots' DMA (vmcnt(0))
+  // before a slot's ds_reads
+  __shared__ __attribute__((aligned(1024))) uint8_t ring0[V3_TILE];
+  __shared__ __attribute__((aligned(1024))) uint8_t ring1[V3_TILE];
+  __shared__ __attribute__((aligned(1024))) uint8_t ring2[V3_TILE];
+  __shared__ __attribute__((aligned(1024))) uint8_t ring3[V3_TILE];
+  constexpr int TI = 4, TJ = 2;
+  const int tiles_n = N / V3_BN;
+  const int nwg = (M / V3_BM) * tiles_n;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int tm = (bid / tiles_n) * V3_BM, tn = (bid % tiles_n) * V3_BN;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hf = lane >> 5;
+  const int wm = (wave >> 2) * 128, wn = (wave & 3) * 64;
+
+  f32x16 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  // DMA: each operand image is 256 rows x 64 B = 16 blocks of 16 rows (1 KiB), two per wave per operand. Lane l of a
+  // block writes row 16 b + l / 4, physical chunk l % 4, which holds logical chunk (l % 4) ^ ((row >> 2) & 3).
+  int voff[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int row = (wave * 2 + t) * 16 + (lane >> 2);
+    voff[t] = row * K + v3_swz(row, lane & 3) * 16;
+  }
+  const uint8_t* const a_tile = A + (long)tm * K;
+  const uint8_t* const b_tile = B + (long)tn * K;
+  auto stage = [&](int kt, uint8_t* base) {
+    const uint8_t* a0 = a_tile + kt * V3_BK;
+    const uint8_t* b0 = b_tile + kt * V3_BK;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int blk = wave * 2 + t;
+      __builtin_amdgcn_global_load_lds(a0 + voff[t], base + blk * 1024, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(b0 + voff[t], base + V3_BOFF + blk * 1024, 16, 0, 0);
+    }
+  };
+  // fragment rows wm + 32 i + r / wn + 32 j + r all have (row >> 2) & 3 == (r >> 2) & 3
+  const int sw = (r >> 2) & 3;
+  const int lo0 = ((2 * hf) ^ sw) * 16, lo1 = ((2 * hf + 1) ^ sw) * 16;
+  const int arow = (wm + r) * V3_BK, brow = V3_BOFF + (wn + r) * V3_BK;
+  auto frag = [&](const uint8_t* p) -> v8i {
+    const uint4 lo = *reinterpret_cast<const uint4*>(p + lo0);
+    const uint4 hi = *reinterpret_cast<const uint4*>(p + lo1);
+    v8i v;
+    v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w; v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+    return v;
+  };
+  auto load = [&](const uint8_t* img, v8i (&fa)[TI], v8i (&fb)[TJ]) {
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) fb[j] = frag(img + brow + j * 32 * V3_BK);
+#pragma unroll
+    for (int i = 0; i < TI; ++i) fa[i] = frag(img + arow + i * 32 * V3_BK);
+  };
+  auto mfma_rows = [&](const v8i (&fa)[TI], const v8i (&fb)[TJ], int i0) {
+#pragma unroll
+    for (int i = i0; i < i0 + 2; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)  // swapped operands: acc holds the C^T tile (lane <-> m, registers <-> n)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fb[j], fa[i], acc[i][j], FB, FA, 0, 0x7f7f7f7f, 0,
+                                                                    0x7f7f7f7f);
+  };
+
+  const int nk = K / V3_BK;
+  // prologue: tiles 0..3 in flight, wait for tile 0, read its fragments
+  stage(0, ring0);
+  if (nk > 1) stage(1, ring1);
+  if (nk > 2) stage(2, ring2);
+  if (nk > 3) stage(3, ring3);
+  if (nk > 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if (nk > 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (nk > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  v8i xa[TI], xb[TJ], ya[TI], yb[TJ];
+  load(ring0, xa, xb);
+
+  // one K-tile: `cur` fragments (tile t, in registers) -> MFMAs; `nxt` <- fragments of tile t+1 from slot `nslot`;
+  // DMA of tile t+4 into `slot` (tile t's, free once every wave passed the barrier)
+  auto step = [&](int t, uint8_t* slot, const uint8_t* nslot, v8i (&ca)[TI], v8i (&cb)[TJ], v8i (&na)[TI], v8i (&nb)[TJ]) {
+    mfma_rows(ca, cb, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    const int ahead = min(nk - 1, t + 3) - (t + 1);  // tiles after t+1 still allowed in flight
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + 4 < nk) stage(t + 4, slot);
+    if (t + 1 < nk) load(nslot, na, nb);
+    mfma_rows(ca, cb, 2);
+  };
+  for (int t = 0; t < nk; t += 4) {
+    step(t, ring0, ring1, xa, xb, ya, yb);
+    if (t + 1 >= nk) break;
+    step(t + 1, ring1, ring2, ya, yb, xa, xb);
+    if (t + 2 >= nk) break;
+    step(t + 2, ring2, ring3, xa, xb, ya, yb);
+    if (t + 3 >= nk) break;
+    step(t + 3, ring3, ring0, ya, yb, xa, xb);
+  }
+
+  const float s = sa[0] * sb[0] * smul;
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int m = tm + wm + i * 32 + r;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n = tn + wn + j * 32 + 8 * g + 4 * hf;
+        float v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          v[u] = acc[i][j][4 * g + u] * s;
+          if (bias != nullptr) v[u] += bf2f(bias[n + u]);
+        }
+        if (OUT_F32) {
+          float4* cp4 = reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + (long)m * N + n);
+          if (accum) {
+            const float4 o = *cp4;
+            v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+          }
+          *cp4 = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+          bf16x4* cp4 = reinterpret_cast<bf16x4*>(reinterpret_cast<bf16_t*>(C) + (long)m * N + n);
+          if (accum) {
+            const bf16x4 o = *cp4;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] += bf2f(o.v[u]);
+          }
+          bf16x4 w;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) w.v[u] = f2bf(v[u]);
+          *cp4 = w;
+        }
+      }
+    }
+}
+
 }  // namespace
 
 torch::Tensor fp8_amax(torch::Tensor x, c10::optional<torch::Tensor> out) {

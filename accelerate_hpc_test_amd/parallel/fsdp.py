@@ -443,8 +443,11 @@ class FSDPEngine:
             torch.manual_seed(seed * 100003 + unit.idx)
             if dev.type == "cuda":
                 torch.cuda.manual_seed(seed * 100003 + unit.idx)
+            # init in module-registration order, not the (fp8-first) flat layout order: the values each module draws
+            # from the seeded stream must not depend on the layout
             mods = {id(i.module): i.module for i in unit.infos}
-            for m in mods.values():
+            order = {id(m): k for k, m in enumerate(unit.module.modules())}
+            for m in sorted(mods.values(), key=lambda m: order.get(id(m), -1)):
                 init_fn(m)
             if dev.type == "cuda":
                 torch.cuda.set_rng_state(gen_state, dev)

@@ -722,7 +722,8 @@ def test_fsdp_fp8_all_gather_matches_bf16_all_gather(one_rank_rccl, force):
             assert all(i.param.dtype == torch.float8_e4m3fn for u in eng.f8_units for i in u.f8_infos)
         res[ag] = (losses, norms, acc.get_state_dict(model))
     assert res[False][0] == res[True][0], (res[False][0], res[True][0])
-    assert res[False][1] == res[True][1], (res[False][1], res[True][1])
+    # the grad norm sums squares over the flat layout, which the fp8 region reorders: equal up to summation order
+    assert res[False][1] == pytest.approx(res[True][1], rel=1e-6), (res[False][1], res[True][1])
     for n, t in res[False][2].items():
         assert torch.equal(t, res[True][2][n]), n
 
