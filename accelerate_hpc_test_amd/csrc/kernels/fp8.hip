@@ -11,6 +11,7 @@
 #include <ATen/hip/HIPContext.h>
 #include "common.h"
 #include <cstdlib>
+#include <type_traits>
 
 using namespace acc;
 
@@ -498,27 +499,30 @@ __global__ __launch_bounds__(512, 1) void fp8_gemm_v2_w8_kernel(const uint8_t* _
 }
 
 // ------------------------------------------------------------------------------------------------ GEMM v3
-// 256x256 output tile, 8 waves (2 x 4, 128x64 per wave = 8 MX 32x32x64 accumulators, 128 AGPRs, two waves per SIMD),
-// BK = 64 fp8 bytes per K-tile (32 KiB of A+B), a FOUR-deep LDS ring filled by global_load_lds. Per K-tile t:
-//   MFMAs on the first half of the wave's tile (fragments of t already in registers)
-//   s_waitcnt vmcnt(8)   -- only tile t+1 must have landed; t+2, t+3 stay in flight ACROSS the barrier
+// 256x256 output tile, 4 waves (2 x 2, one per SIMD: 128x128 per wave = 16 MX 32x32x64 accumulators in the 256
+// AGPRs), BK = 64 fp8 bytes per K-tile (32 KiB of A+B), a FOUR-deep LDS ring filled by global_load_lds. Per K-tile t:
+//   MFMAs on rows 0-63 of the wave's tile (fragments of t already in VGPRs)
+//   s_waitcnt vmcnt(16)  -- only tile t+1 must have landed; t+2, t+3 stay in flight ACROSS the barrier
 //   s_barrier            -- t+1 visible to every wave; every wave's reads of t retired (lgkmcnt(0) before it)
-//   DMA of tile t+4 into t's slot; ds_reads of t+1's fragments into the second register set
-//   MFMAs on the second half (the fragment reads and the DMA issue hide under them)
-// so no K-tile ever starts with an exposed LDS-read latency or a drained DMA queue (v2's vmcnt(0) + barrier per K-step
-// left the MFMA pipe idle for both at one wave per SIMD). Image rows are 64 B; 16-B chunk swizzle c ^ ((row >> 2) & 3)
-// makes every 16-lane ds_read_b128 group of a 32x32x64 fragment cover the 16 slots of a 256-B bank row.
+//   DMA of tile t+4 into t's slot and ds_reads of t+1's fragments into the second VGPR set, interleaved one DMA and
+//   two ds_reads per MFMA with the MFMAs on rows 64-127
+// so no K-tile starts with an exposed LDS-read latency or a drained DMA queue (v2's vmcnt(0) + barrier per K-step
+// left the MFMA pipe idle for both at one wave per SIMD). Image rows are 64 B; the 16-B chunk swizzle
+// c ^ ((row >> 2) & 3) makes every 16-lane ds_read_b128 group of a 32x32x64 fragment cover the 16 slots of a 256-B
+// bank row.
 constexpr int V3_BM = 256, V3_BN = 256, V3_BK = 64;
 constexpr int V3_TILE = (V3_BM + V3_BN) * V3_BK;  // 32 KiB per K-tile: A 256x64 | B 256x64
 constexpr int V3_BOFF = V3_BM * V3_BK;
 
 __device__ __forceinline__ int v3_swz(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }
 
-template <int FA, int FB, bool OUT_F32>
-__global__ __launch_bounds__(512, 1) void fp8_gemm_v3_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
-                                                             const float* __restrict__ sa, const float* __restrict__ sb, float smul,
-                                                             const bf16_t* __restrict__ bias, void* __restrict__ C, int M, int N,
-                                                             int K, int accum) {
+// NW = 4: 2 x 2 waves of 128x128 (one per SIMD, accumulators in the 512-entry file); NW = 8: 2 x 4 waves of 128x64
+// (two per SIMD, so one wave's DMA / LDS issue overlaps the other's MFMAs).
+template <int FA, int FB, bool OUT_F32, int NW>
+__device__ __forceinline__ void fp8_gemm_v3_body(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
+                                                 const float* __restrict__ sa, const float* __restrict__ sb, float smul,
+                                                 const bf16_t* __restrict__ bias, void* __restrict__ C, int M, int N,
+                                                 int K, int accum, int group_m) {
   // one LDS object per ring slot, each addressed with a compile-time identity (the loop is unrolled by the ring
   // depth): distinct objects carry distinct alias scopes, so hipcc does not drain the other slots' DMA (vmcnt(0))
   // before a slot's ds_reads
@@ -526,13 +530,30 @@ __global__ __launch_bounds__(512, 1) void fp8_gemm_v3_kernel(const uint8_t* __re
   __shared__ __attribute__((aligned(1024))) uint8_t ring1[V3_TILE];
   __shared__ __attribute__((aligned(1024))) uint8_t ring2[V3_TILE];
   __shared__ __attribute__((aligned(1024))) uint8_t ring3[V3_TILE];
-  constexpr int TI = 4, TJ = 2;
+  constexpr int WN = NW / 2;                        // waves along N (2 along M)
+  constexpr int TI = 4, TJ = 4 / (NW / 4);          // 32x32 tiles per wave along M / N
+  constexpr int DPW = 16 / NW;                      // 1-KiB DMA blocks per wave per operand per K-tile
+  constexpr int RD = 2 * (TI + TJ);                 // ds_read_b128 per wave per K-tile
+  constexpr int HALF = 2 * TJ;                      // MFMAs per half K-tile
   const int tiles_n = N / V3_BN;
   const int nwg = (M / V3_BM) * tiles_n;
-  const int bid = xcd_remap(blockIdx.x, nwg);
-  const int tm = (bid / tiles_n) * V3_BM, tn = (bid % tiles_n) * V3_BN;
+  const int bid = xcd_remap(blockIdx.x, nwg);  // each XCD gets a contiguous range of tile ids
+  // tile id -> (row, col) in column-major groups of group_m tile rows: the ~32 tiles an XCD runs at once then cover
+  // a group_m x (32 / group_m) block (A and B panels both re-read from that XCD's L2) instead of one row of 32
+  // tiles, each with its own B panel
+  int tile_m, tile_n;
+  if (group_m > 1) {
+    const int tiles_m = M / V3_BM, per_group = group_m * tiles_n;
+    const int g = bid / per_group, first = g * group_m, rows = min(tiles_m - first, group_m), in = bid % per_group;
+    tile_m = first + in % rows;
+    tile_n = in / rows;
+  } else {
+    tile_m = bid / tiles_n;
+    tile_n = bid % tiles_n;
+  }
+  const int tm = tile_m * V3_BM, tn = tile_n * V3_BN;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hf = lane >> 5;
-  const int wm = (wave >> 2) * 128, wn = (wave & 3) * 64;
+  const int wm = (wave / WN) * 128, wn = (wave % WN) * (V3_BN / WN);
 
   f32x16 acc[TI][TJ];
 #pragma unroll
@@ -542,24 +563,31 @@ __global__ __launch_bounds__(512, 1) void fp8_gemm_v3_kernel(const uint8_t* __re
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-  // DMA: each operand image is 256 rows x 64 B = 16 blocks of 16 rows (1 KiB), two per wave per operand. Lane l of a
+  // DMA: each operand image is 256 rows x 64 B = 16 blocks of 16 rows (1 KiB), DPW per wave per operand. Lane l of a
   // block writes row 16 b + l / 4, physical chunk l % 4, which holds logical chunk (l % 4) ^ ((row >> 2) & 3).
-  int voff[2];
+  // buffer_load ... lds off one buffer descriptor per operand panel (SGPRs): the per-lane source offset is a
+  // loop-invariant 32-bit VGPR and the K position rides in soffset, so staging costs no VALU address math (the
+  // flat form needs a 64-bit VGPR address per instruction); out-of-range rows would read zeros, not fault.
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  unsigned voff[DPW];
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int row = (wave * 2 + t) * 16 + (lane >> 2);
-    voff[t] = row * K + v3_swz(row, lane & 3) * 16;
+  for (int t = 0; t < DPW; ++t) {
+    const int row = (wv * DPW + t) * 16 + (lane >> 2);
+    voff[t] = (unsigned)(row * K + v3_swz(row, lane & 3) * 16);
   }
-  const uint8_t* const a_tile = A + (long)tm * K;
-  const uint8_t* const b_tile = B + (long)tn * K;
+  const auto a_rs = __builtin_amdgcn_make_buffer_rsrc((void*)(A + (long)tm * K), (short)0, V3_BM * K, 0x00020000);
+  const auto b_rs = __builtin_amdgcn_make_buffer_rsrc((void*)(B + (long)tn * K), (short)0, V3_BN * K, 0x00020000);
+  const int nk = K / V3_BK;
+  // Past the last K-tile the DMA is still issued (so every wait below has ONE count and the loop body has no branch
+  // for hipcc to sink the MFMAs across), but with an soffset beyond the descriptor: the hardware range check returns
+  // zeros without touching memory, into a ring slot nobody reads again.
   auto stage = [&](int kt, uint8_t* base) {
-    const uint8_t* a0 = a_tile + kt * V3_BK;
-    const uint8_t* b0 = b_tile + kt * V3_BK;
+    const int so = kt < nk ? kt * V3_BK : 0x40000000;
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int blk = wave * 2 + t;
-      __builtin_amdgcn_global_load_lds(a0 + voff[t], base + blk * 1024, 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(b0 + voff[t], base + V3_BOFF + blk * 1024, 16, 0, 0);
+    for (int t = 0; t < DPW; ++t) {
+      const int blk = wv * DPW + t;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rs, base + blk * 1024, 16, voff[t], so, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rs, base + V3_BOFF + blk * 1024, 16, voff[t], so, 0, 0);
     }
   };
   // fragment rows wm + 32 i + r / wn + 32 j + r all have (row >> 2) & 3 == (r >> 2) & 3
@@ -588,82 +616,114 @@ __global__ __launch_bounds__(512, 1) void fp8_gemm_v3_kernel(const uint8_t* __re
                                                                     0x7f7f7f7f);
   };
 
-  const int nk = K / V3_BK;
   // prologue: tiles 0..3 in flight, wait for tile 0, read its fragments
   stage(0, ring0);
-  if (nk > 1) stage(1, ring1);
-  if (nk > 2) stage(2, ring2);
-  if (nk > 3) stage(3, ring3);
-  if (nk > 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-  else if (nk > 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if (nk > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  stage(1, ring1);
+  stage(2, ring2);
+  stage(3, ring3);
+  if constexpr (NW == 4) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // 3 tiles x 2 DPW DMAs in flight
+  else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
   v8i xa[TI], xb[TJ], ya[TI], yb[TJ];
   load(ring0, xa, xb);
 
-  // one K-tile: `cur` fragments (tile t, in registers) -> MFMAs; `nxt` <- fragments of tile t+1 from slot `nslot`;
-  // DMA of tile t+4 into `slot` (tile t's, free once every wave passed the barrier)
+  // one K-tile: `cur` fragments (tile t, in VGPRs) -> MFMAs; `nxt` <- fragments of tile t+1 from slot `nslot`;
+  // DMA of tile t+4 into `slot` (tile t's, free once every wave passed the barrier). Straight-line code only.
   auto step = [&](int t, uint8_t* slot, const uint8_t* nslot, v8i (&ca)[TI], v8i (&cb)[TJ], v8i (&na)[TI], v8i (&nb)[TJ]) {
     mfma_rows(ca, cb, 0);
     __builtin_amdgcn_sched_barrier(0);
-    const int ahead = min(nk - 1, t + 3) - (t + 1);  // tiles after t+1 still allowed in flight
-    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
-    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    // tile t+1 landed (t+2, t+3 in flight)
+    if constexpr (NW == 4) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (t + 4 < nk) stage(t + 4, slot);
-    if (t + 1 < nk) load(nslot, na, nb);
+    stage(t + 4, slot);
+    load(nslot, na, nb);  // past the last tile this reads a stale slot into registers nobody uses
     mfma_rows(ca, cb, 2);
+    // issue order of this region: per MFMA one DMA and two fragment reads, so the reads of t+1 start right after the
+    // barrier and their latency hides under this half's MFMAs (left alone, hipcc issues the MFMAs first)
+#pragma unroll
+    for (int k = 0; k < HALF; ++k) {
+      __builtin_amdgcn_sched_group_barrier(0x10, 2 * DPW / HALF, 0);  // VMEM (buffer_load ... lds)
+      __builtin_amdgcn_sched_group_barrier(0x100, RD / HALF, 0);      // DS read
+      __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);                // MFMA
+    }
+    __builtin_amdgcn_sched_barrier(0);
   };
-  for (int t = 0; t < nk; t += 4) {
+  for (int t = 0; t < nk; t += 4) {  // nk % 4 == 0 (host check)
     step(t, ring0, ring1, xa, xb, ya, yb);
-    if (t + 1 >= nk) break;
     step(t + 1, ring1, ring2, ya, yb, xa, xb);
-    if (t + 2 >= nk) break;
     step(t + 2, ring2, ring3, xa, xb, ya, yb);
-    if (t + 3 >= nk) break;
     step(t + 3, ring3, ring0, ya, yb, xa, xb);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA left in flight past the loop
 
   const float s = sa[0] * sb[0] * smul;
+  // epilogue: bias / accumulate resolved once per kernel, not per element (per-element `if (bias)` became a branch
+  // around every bias load)
+  auto epilogue = [&](auto has_bias, auto acc_in) {
 #pragma unroll
-  for (int i = 0; i < TI; ++i)
+    for (int i = 0; i < TI; ++i)
 #pragma unroll
-    for (int j = 0; j < TJ; ++j) {
-      const int m = tm + wm + i * 32 + r;
+      for (int j = 0; j < TJ; ++j) {
+        const int m = tm + wm + i * 32 + r;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int n = tn + wn + j * 32 + 8 * g + 4 * hf;
-        float v[4];
+        for (int g = 0; g < 4; ++g) {
+          const int n = tn + wn + j * 32 + 8 * g + 4 * hf;
+          float v[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          v[u] = acc[i][j][4 * g + u] * s;
-          if (bias != nullptr) v[u] += bf2f(bias[n + u]);
-        }
-        if (OUT_F32) {
-          float4* cp4 = reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + (long)m * N + n);
-          if (accum) {
-            const float4 o = *cp4;
-            v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+          for (int u = 0; u < 4; ++u) v[u] = acc[i][j][4 * g + u] * s;
+          if constexpr (decltype(has_bias)::value) {
+            const bf16x4 b4 = *reinterpret_cast<const bf16x4*>(bias + n);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] += bf2f(b4.v[u]);
           }
-          *cp4 = make_float4(v[0], v[1], v[2], v[3]);
-        } else {
-          bf16x4* cp4 = reinterpret_cast<bf16x4*>(reinterpret_cast<bf16_t*>(C) + (long)m * N + n);
-          if (accum) {
-            const bf16x4 o = *cp4;
+          if constexpr (OUT_F32) {
+            float4* cp4 = reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + (long)m * N + n);
+            if constexpr (decltype(acc_in)::value) {
+              const float4 o = *cp4;
+              v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+            }
+            *cp4 = make_float4(v[0], v[1], v[2], v[3]);
+          } else {
+            bf16x4* cp4 = reinterpret_cast<bf16x4*>(reinterpret_cast<bf16_t*>(C) + (long)m * N + n);
+            if constexpr (decltype(acc_in)::value) {
+              const bf16x4 o = *cp4;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) v[u] += bf2f(o.v[u]);
+              for (int u = 0; u < 4; ++u) v[u] += bf2f(o.v[u]);
+            }
+            bf16x4 w;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) w.v[u] = f2bf(v[u]);
+            *cp4 = w;
           }
-          bf16x4 w;
-#pragma unroll
-          for (int u = 0; u < 4; ++u) w.v[u] = f2bf(v[u]);
-          *cp4 = w;
         }
       }
-    }
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  if (bias != nullptr) {
+    if (accum) epilogue(T_{}, T_{}); else epilogue(T_{}, F_{});
+  } else {
+    if (accum) epilogue(F_{}, T_{}); else epilogue(F_{}, F_{});
+  }
+}
+
+template <int FA, int FB, bool OUT_F32>
+__global__ __launch_bounds__(256, 1) void fp8_gemm_v3_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
+                                                             const float* __restrict__ sa, const float* __restrict__ sb, float smul,
+                                                             const bf16_t* __restrict__ bias, void* __restrict__ C, int M, int N,
+                                                             int K, int accum, int group_m) {
+  fp8_gemm_v3_body<FA, FB, OUT_F32, 4>(A, B, sa, sb, smul, bias, C, M, N, K, accum, group_m);
+}
+
+template <int FA, int FB, bool OUT_F32>
+__global__ __launch_bounds__(512, 1) void fp8_gemm_v3_w8_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
+                                                                const float* __restrict__ sa, const float* __restrict__ sb,
+                                                                float smul, const bf16_t* __restrict__ bias, void* __restrict__ C,
+                                                                int M, int N, int K, int accum, int group_m) {
+  fp8_gemm_v3_body<FA, FB, OUT_F32, 8>(A, B, sa, sb, smul, bias, C, M, N, K, accum, group_m);
 }
 
 }  // namespace
@@ -755,6 +815,19 @@ std::vector<torch::Tensor> fp8_cast(torch::Tensor x, torch::Tensor t, double qma
   return {y};
 }
 
+// Kernel choice of fp8_gemm: 0 = default, 1 = v1 (128x128), 2 = v2 4 waves, 3 = v2 8 waves, 4 = v3 (4-deep ring),
+// 5 = v3 8 waves.
+// Shapes a variant cannot tile fall back to the next one that can (v3 -> v2 -> v1).
+constexpr int kFp8GemmDefault = 4;
+static int g_fp8_gemm_variant = 0;
+static int g_fp8_gemm_group_m = 4;  // v3 tile-row grouping (1 = plain row-major tile order)
+void fp8_gemm_select(int64_t variant, int64_t group_m) {
+  TORCH_CHECK(variant >= 0 && variant <= 5, "fp8_gemm_select: variant 0..5");
+  TORCH_CHECK(group_m >= 0 && group_m <= 64, "fp8_gemm_select: group_m 0..64");
+  g_fp8_gemm_variant = (int)variant;
+  if (group_m > 0) g_fp8_gemm_group_m = (int)group_m;
+}
+
 // C = (a . b^T) * sa[0] * sb[0] * smul (+ bias): sa / sb are inverse scales, or amax buffers with smul = 1/(qa*qb).
 // `out` (optional): write into this contiguous [M, N] tensor (fp32 when out_fp32, else bf16) instead of a new one, adding
 // to its contents when `accumulate` (the FSDP flat-grad / fp32 grad-shard destination of a weight gradient).
@@ -790,12 +863,39 @@ torch::Tensor fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor a_scale_i
   const float* sbp = b_scale_inv.data_ptr<float>();
   void* cp = out.data_ptr();
   static const bool force_v1 = std::getenv("ACCELERATE_FP8_GEMM_V1") != nullptr;
-  if (!force_v1 && M % V2_BM == 0 && N % V2_BN == 0 && K % V2_BK == 0) {
+  static const bool env_w8 = [] {
+    const char* e = std::getenv("ACCELERATE_FP8_GEMM_WAVES");
+    return e != nullptr && std::atoi(e) == 8;
+  }();
+  int variant = g_fp8_gemm_variant;
+  if (variant == 0) variant = force_v1 ? 1 : (env_w8 ? 3 : kFp8GemmDefault);
+  const bool v3 = variant == 4 || variant == 5;
+  if (v3 && !(M % V3_BM == 0 && N % V3_BN == 0 && K % (4 * V3_BK) == 0)) variant = 2;
+  if (v3 && (reinterpret_cast<uintptr_t>(bp) & 7) != 0) variant = 2;  // v3 reads the bias 4 at a time
+  // v3's buffer descriptors hold one 256-row panel: its byte size must fit the 32-bit record count
+  if (v3 && (long)V3_BM * K >= (1L << 31)) variant = 2;
+  if (variant == 4 || variant == 5) {
+    const int nwg3 = (M / V3_BM) * (N / V3_BN);
+    const bool w8_3 = variant == 5;
+#define GEMM3_LAUNCH(FA, FB, OF)                                                                                        \
+  do {                                                                                                                  \
+    if (w8_3)                                                                                                           \
+      hipLaunchKernelGGL((fp8_gemm_v3_w8_kernel<FA, FB, OF>), dim3(nwg3), dim3(512), 0, stream, ap, bptr, sap, sbp, (float)smul, bp, \
+                         cp, M, N, K, accum, g_fp8_gemm_group_m);                                                        \
+    else                                                                                                                \
+      hipLaunchKernelGGL((fp8_gemm_v3_kernel<FA, FB, OF>), dim3(nwg3), dim3(256), 0, stream, ap, bptr, sap, sbp, (float)smul, bp, \
+                         cp, M, N, K, accum, g_fp8_gemm_group_m);                                                        \
+  } while (0)
+    if (!a_e5m2 && !b_e5m2) { if (out_fp32) GEMM3_LAUNCH(0, 0, true); else GEMM3_LAUNCH(0, 0, false); }
+    else if (!a_e5m2 && b_e5m2) { if (out_fp32) GEMM3_LAUNCH(0, 1, true); else GEMM3_LAUNCH(0, 1, false); }
+    else if (a_e5m2 && !b_e5m2) { if (out_fp32) GEMM3_LAUNCH(1, 0, true); else GEMM3_LAUNCH(1, 0, false); }
+    else { if (out_fp32) GEMM3_LAUNCH(1, 1, true); else GEMM3_LAUNCH(1, 1, false); }
+#undef GEMM3_LAUNCH
+    return out;
+  }
+  if (variant != 1 && M % V2_BM == 0 && N % V2_BN == 0 && K % V2_BK == 0) {
     const int nwg2 = (M / V2_BM) * (N / V2_BN);
-    static const bool w8 = [] {
-      const char* e = std::getenv("ACCELERATE_FP8_GEMM_WAVES");
-      return e != nullptr && std::atoi(e) == 8;
-    }();
+    const bool w8 = variant == 3;
 #define GEMM2_LAUNCH(FA, FB, OF)                                                                                      \
   do {                                                                                                                \
     if (w8)                                                                                                           \

@@ -239,6 +239,46 @@ def test_fp8_gemm_v2_matches_v1_random():
     assert torch.allclose(outs[0], outs[1], rtol=1e-5, atol=1e-3), (outs[0] - outs[1]).abs().max()
 
 
+@pytest.mark.parametrize("M,N,K", [(256, 256, 256), (512, 768, 1024), (1024, 512, 4096), (256, 1280, 768)])
+def test_fp8_gemm_v3_ring_kernel_matches_reference(M, N, K):
+    """The 4-deep-ring kernel (v3: buffer_load...lds, counted vmcnt, one barrier per K-tile) on exact small integers
+    (bit-exact vs fp32 matmul) and on random scaled operands with bias / accumulate / fp32 out / e5m2 (== v2 and the
+    fp32 reference of the dequantised operands). All variants selected in ONE process (ext().fp8_gemm_select)."""
+    from accelerate_hpc_test_amd.ops import fp8
+    from accelerate_hpc_test_amd.ops._ext import ext
+
+    torch.manual_seed(0)
+    one = torch.ones(1, device=DEV)
+    ai = torch.randint(-3, 4, (M, K), device=DEV).to(torch.bfloat16)
+    bi = torch.randint(-3, 4, (N, K), device=DEV).to(torch.bfloat16)
+    a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    b = torch.randn(N, K, device=DEV, dtype=torch.bfloat16)
+    bias = torch.randn(N, device=DEV, dtype=torch.bfloat16)
+    sa, sb = fp8.Scale(fp8.amax(a), fp8.E4M3_MAX), fp8.Scale(fp8.amax(b), fp8.E5M2_MAX)
+    a8, b8 = fp8.cast(a, sa), fp8.cast(b, sb, e5m2=True)
+    ref = (a8.float() * sa.inv()) @ (b8.float() * sb.inv()).t() + bias.float()
+    base = torch.randn(M, N, device=DEV)
+    res = {}
+    try:
+        for v in (2, 4, 5):
+            ext().fp8_gemm_select(v)
+            exact = fp8.gemm(fp8.cast(ai, one), fp8.cast(bi, one), one, one, out_dtype=torch.float32)
+            assert torch.equal(exact, ai.float() @ bi.float().t()), (v, (exact - ai.float() @ bi.float().t()).abs().max())
+            o32 = fp8.gemm(a8, b8, sa, sb, bias, torch.float32)
+            o16 = fp8.gemm(a8, b8, sa, sb, bias, torch.bfloat16)
+            acc = base.clone()
+            fp8.gemm(a8, b8, sa, sb, bias, out=acc, accumulate=True)
+            res[v] = (o32, o16, acc)
+    finally:
+        ext().fp8_gemm_select(0)
+    for v in (4, 5):  # v3 with 4 and with 8 waves
+        o32, o16, acc = res[v]
+        assert torch.allclose(o32, ref, rtol=1e-4, atol=1e-3 * ref.abs().max().item()), (v, (o32 - ref).abs().max())
+        assert torch.allclose(o32, res[2][0], rtol=1e-5, atol=1e-4), (v, (o32 - res[2][0]).abs().max())
+        assert torch.allclose(o16.float(), o32, rtol=8e-3, atol=1e-2)  # bf16 rounding of the same fp32 result
+        assert torch.allclose(acc, base + o32, rtol=1e-5, atol=1e-4)
+
+
 def test_moe_grouped_experts_fp8_matches_bf16():
     """fp8 grouped experts (padded segments, 6 MX-fp8 GEMMs per expert): the forward equals a PyTorch emulation of
     the same per-tensor e4m3 quantisation; output and gradients stay within fp8 error of the bf16 path (e5m2

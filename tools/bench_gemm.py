@@ -1,12 +1,18 @@
-"""GEMM throughput at the Llama-3-8B linear shapes: fp8 (our MX-MFMA kernels, v1 128² / v2 256² glds) vs bf16
-hipBLASLt (torch.matmul). Prints one JSON line per shape and variant.
+"""GEMM throughput at the Llama-3-8B linear shapes: our MX-fp8 MFMA kernels vs bf16 hipBLASLt (torch.matmul).
 
-    python tools/bench_gemm.py [--tokens 8192] [--iters 20]
+All kernel variants run in ONE process, in interleaved rounds (`ext().fp8_gemm_select`), on random data; one JSON
+line per shape with the median ms / TFLOP/s of each variant over the rounds.
+
+    python tools/bench_gemm.py [--tokens 8192] [--iters 20] [--rounds 3] [--variants 2,4] [--shapes qkv,o]
+
+variants: 1 = v1 128x128, 2 = v2 256x256 4 waves, 3 = v2 8 waves, 4 = v3 4-deep ring, 5 = v3 8 waves; "4g8" = v3 with tile rows
+grouped by 8 (ext().fp8_gemm_select(variant, group_m)).
 """
 
 import argparse
 import json
 import os
+import statistics
 import sys
 
 import torch
@@ -31,12 +37,23 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--tokens", type=int, default=8192)
     p.add_argument("--iters", type=int, default=20)
+    p.add_argument("--rounds", type=int, default=3)
+    p.add_argument("--variants", default="2,4")
+    p.add_argument("--shapes", default="qkv,o,gate_up,down")
+    p.add_argument("--no-bf16", action="store_true")
     args = p.parse_args()
     from accelerate_hpc_test_amd.ops import fp8, gemm_tuning
+    from accelerate_hpc_test_amd.ops._ext import ext
 
     gemm_tuning.load_tuned_gemms()
     T = args.tokens
-    shapes = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336)}
+    variants = args.variants.split(",")
+
+    def select(v):
+        num, _, g = v.partition("g")
+        ext().fp8_gemm_select(int(num), int(g) if g else 0)
+    all_shapes = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336)}
+    shapes = {k: all_shapes[k] for k in args.shapes.split(",")}
     one = torch.ones(1, device="cuda")
     for name, (N, K) in shapes.items():
         # forward (x·Wᵀ), dgrad (dy·W → [T,K] from [T,N]·[N,K]), wgrad (dyᵀ·x → [N,K])
@@ -44,13 +61,25 @@ def main():
             a = torch.randn(m, k, device="cuda", dtype=torch.bfloat16)
             b = torch.randn(n, k, device="cuda", dtype=torch.bfloat16)
             flops = 2.0 * m * n * k
-            ms_bf16 = timeit(lambda: a @ b.t(), args.iters)
             a8, b8 = fp8.cast(a, one), fp8.cast(b, one)
-            # the kernel choice (v2, or v1 with ACCELERATE_FP8_GEMM_V1=1) is fixed per process
-            ms_v2 = timeit(lambda: fp8.gemm(a8, b8, one, one), args.iters)
-            print(json.dumps({"gemm": f"{name}.{kind}", "M": m, "N": n, "K": k, "fp8_kernel": "v1" if os.environ.get("ACCELERATE_FP8_GEMM_V1") else "v2",
-                              "bf16_ms": round(ms_bf16, 3), "bf16_tflops": round(flops / ms_bf16 / 1e9, 1),
-                              "fp8_ms": round(ms_v2, 3), "fp8_tflops": round(flops / ms_v2 / 1e9, 1)}), flush=True)
+            times = {v: [] for v in variants}
+            bf = []
+            for _ in range(args.rounds):
+                if not args.no_bf16:
+                    bf.append(timeit(lambda: a @ b.t(), args.iters))
+                for v in variants:
+                    select(v)
+                    times[v].append(timeit(lambda: fp8.gemm(a8, b8, one, one), args.iters))
+            ext().fp8_gemm_select(0, 4)
+            row = {"gemm": f"{name}.{kind}", "M": m, "N": n, "K": k}
+            if bf:
+                ms = statistics.median(bf)
+                row.update(bf16_ms=round(ms, 3), bf16_tflops=round(flops / ms / 1e9, 1))
+            for v in variants:
+                ms = statistics.median(times[v])
+                row[f"v{v}_ms"] = round(ms, 3)
+                row[f"v{v}_tflops"] = round(flops / ms / 1e9, 1)
+            print(json.dumps(row), flush=True)
             del a, b, a8, b8
 
 
