@@ -23,7 +23,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr float kE4M3Max = 448.f;
 constexpr float kE5M2Max = 57344.f;
 
-__global__ void amax_kernel(const bf16_t* __restrict__ x, long n, unsigned int* __restrict__ out) {
+__global__ __launch_bounds__(1024) void amax_kernel(const bf16_t* __restrict__ x, long n, unsigned int* __restrict__ out) {
   __shared__ float scratch[16];
   float m = 0.f;
   const long nvec = n >> 3;
@@ -146,29 +146,71 @@ __global__ __launch_bounds__(256) void cast_kernel(const bf16_t* __restrict__ x,
 
 // ------------------------------------------------------------------------------------------------ FSDP fp8 all-gather
 // The sharded flat buffer holds several weights back to back; each weight gets its own per-tensor scale. Segment k =
-// elements [lo[k], hi[k]) of the flat bf16 shard. One workgroup per (segment, 4096-element chunk).
-constexpr int kSegChunk = 4096;
+// elements [lo[k], hi[k]) of the flat bf16 shard. One workgroup per (segment, 64 Ki-element chunk): 16-B loads (8
+// bf16 per lane per load, four in flight), the chunk's unaligned head / tail element-wise, and ONE atomic max per
+// 128 KB chunk (a 4 Ki-element chunk made ~7.6k same-address atomics per weight and the kernel ran 7x under HBM speed).
+constexpr long kSegChunk = 65536;
 
 __global__ __launch_bounds__(256) void seg_amax_kernel(const bf16_t* __restrict__ x, const long* __restrict__ lo,
                                                        const long* __restrict__ hi, unsigned int* __restrict__ out) {
   __shared__ float scratch[16];
   const int k = blockIdx.y;
   const long a = lo[k] + (long)blockIdx.x * kSegChunk, b = min(hi[k], a + kSegChunk);
+  if (a >= b) return;  // workgroup-uniform: past the end of a shorter segment
+  const long a8 = min(b, (a + 7) & ~7L), b8 = max(a8, b & ~7L);
   float m = 0.f;
-  for (long i = a + threadIdx.x; i < b; i += 256) m = fmaxf(m, fabsf(bf2f(x[i])));
+  const int tid = threadIdx.x;
+  if (tid < a8 - a) m = fabsf(bf2f(x[a + tid]));
+  if (tid < b - b8) m = fmaxf(m, fabsf(bf2f(x[b8 + tid])));
+  const bf16x8* xv = reinterpret_cast<const bf16x8*>(x + a8);
+  const long nv = (b8 - a8) >> 3;
+  long i = tid;
+  for (; i + 768 < nv; i += 1024) {
+    bf16x8 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = xv[i + 256 * u];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(bf2f(v[u].v[j])));
+  }
+  for (; i < nv; i += 256) {
+    const bf16x8 v = xv[i];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(bf2f(v.v[j])));
+  }
   m = block_max(m, scratch);
-  if (threadIdx.x == 0 && a < b) atomicMax(out + k, __float_as_uint(m));
+  if (tid == 0) atomicMax(out + k, __float_as_uint(m));
 }
 
 // y[i] = e4m3(sat(x[i] * 448 / amax[k])) for i in segment k: the same conversion as cast_kernel, so a weight cast from
-// its shard with the all-reduced amax is bit-identical to the weight cast whole.
+// its shard with the all-reduced amax is bit-identical to the weight cast whole. 16-B loads, 8-B stores.
 __global__ __launch_bounds__(256) void seg_cast_kernel(const bf16_t* __restrict__ x, const long* __restrict__ lo,
                                                        const long* __restrict__ hi, const float* __restrict__ amax,
                                                        float qmax, uint8_t* __restrict__ y) {
   const int k = blockIdx.y;
   const long a = lo[k] + (long)blockIdx.x * kSegChunk, b = min(hi[k], a + kSegChunk);
+  if (a >= b) return;
   const float s = cast_scale(amax + k, qmax, true);
-  for (long i = a + threadIdx.x; i < b; i += 256) y[i] = cvt_pair<false>(bf2f(x[i]) * s, 0.f) & 0xff;
+  const long a8 = min(b, (a + 7) & ~7L), b8 = max(a8, b & ~7L);
+  const int tid = threadIdx.x;
+  if (tid < a8 - a) y[a + tid] = cvt_pair<false>(bf2f(x[a + tid]) * s, 0.f) & 0xff;
+  if (tid < b - b8) y[b8 + tid] = cvt_pair<false>(bf2f(x[b8 + tid]) * s, 0.f) & 0xff;
+  const bf16x8* xv = reinterpret_cast<const bf16x8*>(x + a8);
+  uint2* yv = reinterpret_cast<uint2*>(y + a8);
+  const long nv = (b8 - a8) >> 3;
+  long i = tid;
+  for (; i + 768 < nv; i += 1024) {
+    bf16x8 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = xv[i + 256 * u];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) yv[i + 256 * u] = make_uint2(cvt4<false>(v[u].v, s), cvt4<false>(v[u].v + 4, s));
+  }
+  for (; i < nv; i += 256) {
+    const bf16x8 v = xv[i];
+    yv[i] = make_uint2(cvt4<false>(v.v, s), cvt4<false>(v.v + 4, s));
+  }
 }
 
 // y = x^T for a [R, C] byte matrix (fp8 weights: the K-major copy the dgrad GEMM reads). 128x128 tiles through a
@@ -735,9 +777,11 @@ torch::Tensor fp8_amax(torch::Tensor x, c10::optional<torch::Tensor> out) {
   hipMemsetAsync(o.data_ptr(), 0, sizeof(float), stream);
   const long n = x.numel();
   if (n == 0) return o;
-  long g = (n / 8 + 255) / 256;
-  g = std::max<long>(1, std::min<long>(g, 2048));
-  hipLaunchKernelGGL(amax_kernel, dim3(g), dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(x.data_ptr()), n,
+  // at most one 1024-thread workgroup per CU: every workgroup ends in one same-address atomic max, and 2048 of them
+  // (the old 256-thread grid) queued ~40 us of serialised atomics behind a ~12 us stream of a 64 MB activation
+  long g = (n / 8 + 1023) / 1024;
+  g = std::max<long>(1, std::min<long>(g, 256));
+  hipLaunchKernelGGL(amax_kernel, dim3(g), dim3(1024), 0, stream, reinterpret_cast<const bf16_t*>(x.data_ptr()), n,
                      reinterpret_cast<unsigned int*>(o.data_ptr()));
   return o;
 }
@@ -755,6 +799,7 @@ void fp8_segment_amax(torch::Tensor x, torch::Tensor lo, torch::Tensor hi, torch
   if (nseg == 0 || x.numel() == 0) return;
   TORCH_CHECK(max_len >= 0 && max_len <= x.numel(), "fp8_segment_amax: max_len");
   const long chunks = std::max<long>(1, (max_len + kSegChunk - 1) / kSegChunk);  // chunks of the longest segment
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "fp8_segment_amax: x must be 16-B aligned");
   hipLaunchKernelGGL(seg_amax_kernel, dim3(chunks, nseg), dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(x.data_ptr()),
                      lo.data_ptr<long>(), hi.data_ptr<long>(), reinterpret_cast<unsigned int*>(out.data_ptr()));
 }
@@ -769,6 +814,8 @@ void fp8_segment_cast(torch::Tensor x, torch::Tensor lo, torch::Tensor hi, torch
   if (nseg == 0 || x.numel() == 0) return;
   TORCH_CHECK(max_len >= 0 && max_len <= x.numel(), "fp8_segment_cast: max_len");
   const long chunks = std::max<long>(1, (max_len + kSegChunk - 1) / kSegChunk);
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(y.data_ptr()) % 8 == 0,
+              "fp8_segment_cast: x / y alignment");
   hipLaunchKernelGGL(seg_cast_kernel, dim3(chunks, nseg), dim3(256), 0, at::hip::getCurrentHIPStream(),
                      reinterpret_cast<const bf16_t*>(x.data_ptr()), lo.data_ptr<long>(), hi.data_ptr<long>(),
                      amax.data_ptr<float>(), (float)qmax, reinterpret_cast<uint8_t*>(y.data_ptr()));

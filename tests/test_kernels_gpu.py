@@ -772,15 +772,19 @@ def test_fp8_segment_kernels_and_byte_transpose():
     from accelerate_hpc_test_amd.ops._ext import ext
 
     torch.manual_seed(0)
-    x = torch.randn(100_003, device=DEV, dtype=torch.bfloat16) * 3
-    lo = torch.tensor([0, 17, 5000, 5000, 70_000], device=DEV)
-    hi = torch.tensor([17, 5000, 5000, 70_000, 100_003], device=DEV)
-    amax = torch.empty(5, device=DEV)
-    ext().fp8_segment_amax(x, lo, hi, amax, 65_000)
+    x = torch.randn(400_003, device=DEV, dtype=torch.bfloat16) * 3
+    x[250_001] = 77.0  # the max of a multi-chunk segment sits in its third 64 Ki-element chunk
+    # empty, tiny, unaligned and multi-chunk (several 65536-element workgroups, unaligned head and tail) segments
+    lo = torch.tensor([0, 17, 5000, 5000, 70_000, 100_003, 131_075], device=DEV)
+    hi = torch.tensor([17, 5000, 5000, 70_000, 100_003, 131_075, 400_003], device=DEV)
+    n = lo.numel()
+    max_len = int((hi - lo).max())
+    amax = torch.empty(n, device=DEV)
+    ext().fp8_segment_amax(x, lo, hi, amax, max_len)
     ref = [x[a:b].float().abs().max().item() if b > a else 0.0 for a, b in zip(lo.tolist(), hi.tolist())]
     assert amax.tolist() == ref
     y = torch.empty(x.numel(), device=DEV, dtype=torch.float8_e4m3fn)
-    ext().fp8_segment_cast(x, lo, hi, amax, 448.0, y, 65_000)
+    ext().fp8_segment_cast(x, lo, hi, amax, 448.0, y, max_len)
     for k, (a, b) in enumerate(zip(lo.tolist(), hi.tolist())):
         if b > a:  # same bytes as the whole-tensor cast kernel with that segment's amax
             whole = ext().fp8_cast(x[a:b].view(1, -1).contiguous(), amax[k : k + 1], 448.0, True, False, False)[0]
