@@ -39,6 +39,10 @@ void fp8_segment_cast(torch::Tensor x, torch::Tensor lo, torch::Tensor hi, torch
                       int64_t max_len);
 torch::Tensor u8_transpose(torch::Tensor x);
 void fp8_gemm_select(int64_t variant, int64_t group_m);
+// grouped_gemm.hip
+void grouped_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor out, torch::Tensor seg, int64_t mode, torch::Tensor sa,
+                  torch::Tensor sb, double smul, bool accumulate);
+torch::Tensor batched_transpose(torch::Tensor x);
 // comm_pack.hip
 void grad_shard_update(torch::Tensor dst, torch::Tensor src, double scale, bool accumulate);
 // runtime/*.cpp
@@ -73,6 +77,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fp8_segment_amax", &fp8_segment_amax);
   m.def("fp8_segment_cast", &fp8_segment_cast);
   m.def("u8_transpose", &u8_transpose);
+  m.def("grouped_gemm", &grouped_gemm);
+  m.def("batched_transpose", &batched_transpose);
   m.def("fp8_gemm_select", &fp8_gemm_select, pybind11::arg("variant"), pybind11::arg("group_m") = 0);
   register_runtime(m);
   m.def("blaslt_wgrad_f32", &blaslt_wgrad_f32);

@@ -218,6 +218,8 @@ __global__ __launch_bounds__(256) void seg_cast_kernel(const bf16_t* __restrict_
 __global__ __launch_bounds__(256) void u8_transpose_kernel(const uint8_t* __restrict__ x, uint8_t* __restrict__ y, int R, int C) {
   __shared__ __attribute__((aligned(16))) uint8_t tile[kCT * kCTP];
   const int tr = blockIdx.y * kCT, tc = blockIdx.x * kCT, tid = threadIdx.x;
+  x += (long)blockIdx.z * R * C;  // batched [E, R, C] -> [E, C, R]
+  y += (long)blockIdx.z * R * C;
   if (!(tr + kCT <= R && tc + kCT <= C && (R % 16) == 0 && (C % 16) == 0)) {
     for (int e = tid; e < kCT * kCT; e += 256) {
       const int r = tr + e / kCT, c = tc + e % kCT;
@@ -821,13 +823,14 @@ void fp8_segment_cast(torch::Tensor x, torch::Tensor lo, torch::Tensor hi, torch
                      amax.data_ptr<float>(), (float)qmax, reinterpret_cast<uint8_t*>(y.data_ptr()));
 }
 
-// x^T of a 2-D one-byte tensor (fp8 / uint8).
+// x^T of a 2-D one-byte tensor (fp8 / uint8), or of every matrix of a 3-D [E, R, C] one.
 torch::Tensor u8_transpose(torch::Tensor x) {
-  TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.is_contiguous() && x.element_size() == 1, "u8_transpose: 2-D contiguous byte tensor");
-  const int R = x.size(0), C = x.size(1);
-  auto y = torch::empty({C, R}, x.options());
-  if (R == 0 || C == 0) return y;
-  dim3 grid((C + kCT - 1) / kCT, (R + kCT - 1) / kCT);
+  TORCH_CHECK(x.is_cuda() && (x.dim() == 2 || x.dim() == 3) && x.is_contiguous() && x.element_size() == 1,
+              "u8_transpose: 2-D / 3-D contiguous byte tensor");
+  const int E = x.dim() == 3 ? x.size(0) : 1, R = x.size(-2), C = x.size(-1);
+  auto y = x.dim() == 3 ? torch::empty({E, C, R}, x.options()) : torch::empty({C, R}, x.options());
+  if (x.numel() == 0) return y;
+  dim3 grid((C + kCT - 1) / kCT, (R + kCT - 1) / kCT, E);
   hipLaunchKernelGGL(u8_transpose_kernel, grid, dim3(256), 0, at::hip::getCurrentHIPStream(),
                      reinterpret_cast<const uint8_t*>(x.data_ptr()), reinterpret_cast<uint8_t*>(y.data_ptr()), R, C);
   return y;
@@ -919,8 +922,8 @@ torch::Tensor fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor a_scale_i
   const bool v3 = variant == 4 || variant == 5;
   if (v3 && !(M % V3_BM == 0 && N % V3_BN == 0 && K % (4 * V3_BK) == 0)) variant = 2;
   if (v3 && (reinterpret_cast<uintptr_t>(bp) & 7) != 0) variant = 2;  // v3 reads the bias 4 at a time
-  // v3's buffer descriptors hold one 256-row panel: its byte size must fit the 32-bit record count
-  if (v3 && (long)V3_BM * K >= (1L << 31)) variant = 2;
+  // v3's buffer descriptors hold one 256-row panel: its byte size must stay below the zero-fill soffset (2^30)
+  if (v3 && (long)V3_BM * K >= (1L << 30)) variant = 2;
   if (variant == 4 || variant == 5) {
     const int nwg3 = (M / V3_BM) * (N / V3_BN);
     const bool w8_3 = variant == 5;

@@ -374,6 +374,8 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16_t* __res
                                                              int C) {
   __shared__ __attribute__((aligned(16))) bf16_t tile[64][72];
   const int tr = blockIdx.y * 64, tc = blockIdx.x * 64, tid = threadIdx.x, ch = tid & 7;
+  in += (long)blockIdx.z * R * C;  // batched [E, R, C] -> [E, C, R]
+  out += (long)blockIdx.z * R * C;
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
     const int row = (tid >> 3) + 32 * p;
@@ -391,14 +393,15 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16_t* __res
 }
 }  // namespace
 
+// [R, C] -> [C, R], or batched [E, R, C] -> [E, C, R].
 torch::Tensor transpose_bf16(torch::Tensor x) {
-  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.is_contiguous(),
-              "transpose_bf16: 2-D contiguous bf16 HIP tensor expected");
-  const int R = x.size(0), C = x.size(1);
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && (x.dim() == 2 || x.dim() == 3) && x.is_contiguous(),
+              "transpose_bf16: 2-D or 3-D contiguous bf16 HIP tensor expected");
+  const int E = x.dim() == 3 ? x.size(0) : 1, R = x.size(-2), C = x.size(-1);
   TORCH_CHECK(R % 64 == 0 && C % 64 == 0, "transpose_bf16: both dims must be multiples of 64");
-  auto out = torch::empty({C, R}, x.options());
-  if (R == 0 || C == 0) return out;
-  hipLaunchKernelGGL(transpose_bf16_kernel, dim3(C / 64, R / 64), dim3(256), 0, at::hip::getCurrentHIPStream(),
+  auto out = x.dim() == 3 ? torch::empty({E, C, R}, x.options()) : torch::empty({C, R}, x.options());
+  if (x.numel() == 0) return out;
+  hipLaunchKernelGGL(transpose_bf16_kernel, dim3(C / 64, R / 64, E), dim3(256), 0, at::hip::getCurrentHIPStream(),
                      reinterpret_cast<const bf16_t*>(x.data_ptr()), reinterpret_cast<bf16_t*>(out.data_ptr()), R, C);
   return out;
 }

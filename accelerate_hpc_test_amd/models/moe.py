@@ -7,8 +7,12 @@ expert GEMMs. Design:
 
   * experts are stored *stacked* (`w_gate_up [E, 2I, H]`, `w_down [E, H, I]`) so FSDP flat-shards them like any
     parameter and the backward writes all expert weight-gradients into one preallocated buffer;
-  * tokens are sorted by expert once (stable argsort), each expert runs two large hipBLASLt GEMMs on its contiguous
-    segment (no per-token work, no capacity padding, no dropped tokens) with the fused SwiGLU kernel between them;
+  * routing is laid out ON THE DEVICE (`expert_layout`: bincount / cumsum / stable argsort, no `.tolist()`): the
+    (token, slot) entries are copied into one buffer where expert e owns rows [seg[e], seg[e+1]) (its count rounded
+    up to 64 rows, zero pad); no capacity factor, no dropped tokens;
+  * each projection and direction is ONE grouped GEMM launch over the device segment table
+    (csrc/kernels/grouped_gemm.hip, bf16 or MX-fp8 MFMA): forward gate_up + down, backward 2 dgrad + 2
+    weight-gradient GEMMs (K-segmented), with the fused SwiGLU kernels between them — no per-expert launch loop;
   * gradients for the whole expert group come from one custom autograd op (`_GroupedExpertsFn`) — indexing
     `w[e]` under autograd would materialise an [E, …]-sized zero gradient per expert;
   * expert parallelism (`ep_group` of size W): rank r owns experts [r·E/W, (r+1)·E/W). Tokens go to their expert's
@@ -49,123 +53,221 @@ def _swiglu_bwd(h, da):
     return torch.cat([dg, du], -1).to(h.dtype)
 
 
-_FP8_ROW_PAD = 256  # the 256x256-tile fp8 GEMM (csrc/kernels/fp8.hip v2) needs M, N % 256 and K % 128
+SEG_ALIGN = 64  # every expert's segment of the routed-token buffer starts at a multiple of 64 rows
 
 
-def _pad_rows(t, rows):
-    if t.shape[0] == rows:
-        return t.contiguous()
-    out = t.new_zeros(rows, t.shape[1])
-    out[: t.shape[0]] = t
+def _round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+def expert_layout(flat_e: torch.Tensor, num_experts: int, align: int = SEG_ALIGN):
+    """Device-side routing layout (no host synchronisation): for the (token, slot) entries sorted stably by expert,
+    `dest[j]` is entry j's row in a buffer where expert e owns rows [seg[e], seg[e + 1]) — its token count rounded
+    up to `align` (the pad rows stay zero). `R`, the buffer's row count, is a host-side bound that does not depend on
+    the routing: N + (align - 1) * E, rounded up to 256."""
+    N = flat_e.numel()
+    counts = torch.bincount(flat_e, minlength=num_experts)
+    padded = (counts + align - 1) // align * align
+    seg = torch.zeros(num_experts + 1, dtype=torch.int32, device=flat_e.device)
+    seg[1:] = torch.cumsum(padded, 0)
+    order = torch.argsort(flat_e, stable=True)
+    e_sorted = flat_e[order]
+    start = torch.cumsum(counts, 0) - counts
+    dest = seg[:-1].long()[e_sorted] + (torch.arange(N, device=flat_e.device) - start[e_sorted])
+    R = _round_up(N + (align - 1) * num_experts, 256)
+    return order, dest, seg, R
+
+
+_ONES = {}
+
+
+def _ones(n, device):
+    key = (n, str(device))
+    if key not in _ONES:
+        _ONES[key] = torch.ones(n, dtype=torch.float32, device=device)
+    return _ONES[key]
+
+
+def _native_ok(x, *dims):
+    return x.is_cuda and use_native(x) and x.dtype == torch.bfloat16 and all(d % 256 == 0 for d in dims)
+
+
+def _gg_native_ok(a, b, mode, out) -> bool:
+    """Shapes / dtypes the grouped MFMA kernel tiles (256x256 output tiles, 256-byte K steps)."""
+    if not (a.is_cuda and use_native(a) and a.dtype in (torch.bfloat16, torch.float8_e4m3fn, torch.float8_e5m2)):
+        return False
+    if out.dtype not in (torch.bfloat16, torch.float32):
+        return False
+    es = a.element_size()
+    if mode == 1:
+        return b.shape[1] % 256 == 0 and (a.shape[1] * es) % 256 == 0
+    return a.shape[0] % 256 == 0 and b.shape[0] % 256 == 0 and (a.shape[1] * es) % 16 == 0
+
+
+def grouped_mm(a, b, seg, mode, out, sa=None, sb=None, smul=1.0, accumulate=False):
+    """One grouped GEMM over the expert segment table `seg` (csrc/kernels/grouped_gemm.hip):
+    mode 1: out[r] = a[r] . b[e]^T for rows r of segment e (a [R, K], b [E, N, K], out [R, N]; rows past seg[E] -> 0);
+    mode 2: out[e] = a[:, seg_e] . b[:, seg_e]^T (a [M, T], b [N, T], out [E, M, N]).
+    sa / sb: fp32 amax-style scale tensors ([1] and [E] (mode 1) / [1] (mode 2)), times `smul`. Off the GPU (and for
+    shapes the kernel does not tile) the same product runs in PyTorch from a host copy of `seg`."""
+    E = seg.numel() - 1
+    if _gg_native_ok(a, b, mode, out):
+        sa = sa if sa is not None else _ones(1, a.device)
+        sb = sb if sb is not None else _ones(E if mode == 1 else 1, a.device)
+        ext().grouped_gemm(a, b, out, seg, mode, sa, sb, float(smul), bool(accumulate))
+        return out
+    bounds = seg.tolist()
+    s_a = 1.0 if sa is None else float(sa.reshape(-1)[0])
+    res = torch.zeros(out.shape, dtype=torch.float32, device=out.device)
+    if mode == 1:
+        for e in range(E):
+            lo, hi = bounds[e], bounds[e + 1]
+            if hi > lo:
+                res[lo:hi] = (a[lo:hi].float() @ b[e].float().t()) * (s_a * smul * (1.0 if sb is None else float(sb[e])))
+    else:
+        s = s_a * smul * (1.0 if sb is None else float(sb.reshape(-1)[0]))
+        for e in range(E):
+            lo, hi = bounds[e], bounds[e + 1]
+            res[e] = (a[:, lo:hi].float() @ b[:, lo:hi].float().t()) * s
+    if accumulate:
+        out.add_(res.to(out.dtype))
+    else:
+        out.copy_(res)
     return out
 
 
-def _fp8_ok(x, recipe, dims):
-    from ..ops.fp8 import _gemm_ok
+def _t(x):
+    """Transposed contiguous copy of a 2-D bf16 activation (the K-contiguous operand of a weight-gradient GEMM)."""
+    if x.is_cuda and use_native(x) and x.dtype == torch.bfloat16 and x.shape[0] % 64 == 0 and x.shape[1] % 64 == 0:
+        return ext().transpose_bf16(x)
+    return x.t().contiguous()
 
-    return recipe is not None and x.is_cuda and use_native(x) and x.dtype == torch.bfloat16 and all(
-        _gemm_ok(128, d, 64) for d in dims
-    )
+
+def _bt(w):
+    """[E, N, K] -> [E, K, N] (expert weight stacks; bf16 or fp8)."""
+    if w.is_cuda and use_native(w) and (w.element_size() == 1 or (w.shape[1] % 64 == 0 and w.shape[2] % 64 == 0)):
+        return ext().batched_transpose(w.contiguous())
+    return w.transpose(1, 2).contiguous()
 
 
 class _GroupedExpertsFn(torch.autograd.Function):
-    """y_e = down_e(swiglu(gate_up_e(x_e))) for contiguous token segments x_e (sizes `counts`).
+    """y = down_e(swiglu(gate_up_e(x))) for the rows of each expert segment of the routed buffer `x` [R, H].
 
-    bf16: hipBLASLt GEMMs on the raw segments. fp8 (a recipe is attached): each segment is zero-padded to a multiple
-    of 256 rows so all six GEMMs per expert (2 fwd, 2 dgrad, 2 wgrad) run on the 256² MX-fp8 MFMA kernel; zero rows add
-    nothing to the wgrad sums and the padded output rows are dropped. Forward operands are e4m3, gradients e5m2
-    (HYBRID), per-expert per-tensor scales, and the transposed fp8 copies the backward needs come out of the same
-    cast kernel as the forward copies.
+    Every projection and direction is ONE grouped GEMM over the device segment table (forward: 2, backward: 2 dgrad
+    + 2 weight-gradient), so the expert count costs no launches and no host syncs. The weight gradients are the
+    K-segmented form (each expert's K range = its token rows) on transposed activations.
+
+    bf16: bf16 MFMA grouped kernel. fp8 (a recipe is attached): operands e4m3 (forward) / e5m2 (gradients, HYBRID),
+    one per-tensor scale per activation buffer and one per expert weight (segment amax over the stacked weights), and
+    the transposed fp8 copies the backward needs come out of the same cast pass as the forward copies.
     """
 
     @staticmethod
-    def forward(ctx, x, w_gu, w_down, counts, recipe):
-        y = torch.empty(x.shape[0], w_down.shape[1], dtype=x.dtype, device=x.device)
-        fp8 = _fp8_ok(x, recipe, (w_gu.shape[1], w_gu.shape[2], w_down.shape[2]))
-        saved = []
-        off = 0
-        for e, c in enumerate(counts):
-            if c == 0:
-                saved.append(None)
-                continue
-            xe = x[off : off + c]
-            if fp8:
-                y[off : off + c], st = _fp8_expert_fwd(xe, w_gu[e], w_down[e], recipe, e)
-                saved.append(st)
-            else:
-                h = xe @ w_gu[e].t()
-                y[off : off + c] = _swiglu_fwd(h) @ w_down[e].t()
-                saved.append(h)
-            off += c
-        ctx.save_for_backward(x, w_gu, w_down)
-        ctx.saved, ctx.counts, ctx.recipe, ctx.fp8 = saved, counts, recipe, fp8
+    def forward(ctx, x, w_gu, w_down, seg, recipe, slots=(None, None)):
+        R, H = x.shape
+        E, I2, _ = w_gu.shape
+        I = w_down.shape[2]
+        fp8 = recipe is not None and _native_ok(x, H, I2, I)
+        if fp8:
+            y, st = _fp8_fwd(x, w_gu, w_down, seg, recipe)
+            ctx.st = st
+        else:
+            h = grouped_mm(x, w_gu, seg, 1, x.new_empty(R, I2))
+            y = grouped_mm(_swiglu_fwd(h), w_down, seg, 1, x.new_empty(R, H))
+            ctx.st = h
+        ctx.save_for_backward(x, w_gu, w_down, seg)
+        ctx.recipe, ctx.fp8, ctx.slots = recipe, fp8, slots
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, w_gu, w_down = ctx.saved_tensors
-        dy = dy.contiguous()
-        dx = torch.empty_like(x)
-        dw_gu = torch.empty_like(w_gu)  # every expert's slice is written below (zeroed when it got no tokens)
-        dw_down = torch.empty_like(w_down)
-        off = 0
-        for e, c in enumerate(ctx.counts):
-            if c == 0:
-                dw_gu[e].zero_()
-                dw_down[e].zero_()
-                continue
-            xe, dye = x[off : off + c], dy[off : off + c]
-            if ctx.fp8:
-                dx[off : off + c] = _fp8_expert_bwd(dye, ctx.saved[e], ctx.recipe, e, dw_gu[e], dw_down[e])
+        x, w_gu, w_down, seg = ctx.saved_tensors
+        dy = dy.contiguous().to(x.dtype)
+        # weight-gradient destinations: the FSDP engine's slot (fp32 grad shard at world size 1, flat bf16 grad buffer
+        # otherwise; the grouped GEMM accumulates into it) or a fresh tensor returned to autograd
+        dsts = []
+        for w, slot in zip((w_gu, w_down), ctx.slots):
+            if slot is not None:
+                dest, acc = slot.engine._fused_slot_dest(slot)
+                dsts.append((dest, acc, slot))
             else:
-                h = ctx.saved[e]
-                a = _swiglu_fwd(h)
-                torch.mm(dye.t(), a, out=dw_down[e]) if dw_down.dtype == dye.dtype else dw_down[e].copy_(dye.t() @ a)
-                dh = _swiglu_bwd(h, dye @ w_down[e])
-                torch.mm(dh.t(), xe, out=dw_gu[e]) if dw_gu.dtype == dh.dtype else dw_gu[e].copy_(dh.t() @ xe)
-                dx[off : off + c] = dh @ w_gu[e]
-            off += c
-        ctx.saved = None
-        return dx, dw_gu, dw_down, None, None
+                dsts.append((w.new_empty(w.shape), False, None))
+        (g_gu, acc_gu, _), (g_d, acc_d, _) = dsts
+        if ctx.fp8:
+            dx = _fp8_bwd(dy, x, w_gu, w_down, seg, ctx.st, ctx.recipe, (g_gu, acc_gu), (g_d, acc_d))
+        else:
+            h = ctx.st
+            R, H = x.shape
+            I = w_down.shape[2]
+            a = _swiglu_fwd(h)
+            da = grouped_mm(dy, _bt(w_down), seg, 1, x.new_empty(R, I))
+            grouped_mm(_t(dy), _t(a), seg, 2, g_d, accumulate=acc_d)
+            dh = _swiglu_bwd(h, da)
+            grouped_mm(_t(dh), _t(x), seg, 2, g_gu, accumulate=acc_gu)
+            dx = grouped_mm(dh, _bt(w_gu), seg, 1, x.new_empty(R, H))
+        ctx.st = None
+        grads = []
+        for dest, _, slot in dsts:
+            if slot is not None:
+                slot.engine._fused_slot_done(slot)
+                grads.append(None)
+            else:
+                grads.append(dest)
+        return dx, grads[0], grads[1], None, None, None
 
 
-def _fp8_expert_fwd(xe, w_gu, w_down, recipe, e):
-    from ..ops.fp8 import E4M3_MAX, cast, gemm
+def _expert_weight_fp8(w, recipe, key):
+    """Per-expert e4m3 copy of a stacked weight [E, N, K] (one scale per expert: segment amax over the flat stack)
+    and its [E, K, N] transpose. Returns (w8, w8t, amax [E])."""
+    from ..ops.fp8 import E4M3_MAX
 
-    c = xe.shape[0]
-    cp = (c + _FP8_ROW_PAD - 1) // _FP8_ROW_PAD * _FP8_ROW_PAD
-    xp = _pad_rows(xe, cp)
-    sx = recipe.scale(f"x{e}", xp, E4M3_MAX)
-    sgu = recipe.scale(f"wgu{e}", w_gu, E4M3_MAX)
-    x8, x8t = cast(xp, sx, False, transpose=True)
-    gu8, gu8t = cast(w_gu.contiguous(), sgu, False, transpose=True)
-    h = gemm(x8, gu8, sx, sgu, None, torch.bfloat16)  # [cp, 2I]; padded rows stay 0
+    E = w.shape[0]
+    flat = w.contiguous().view(-1)
+    n = flat.numel() // E
+    lo = torch.arange(E, device=w.device, dtype=torch.long) * n
+    amax = torch.empty(E, dtype=torch.float32, device=w.device)
+    ext().fp8_segment_amax(flat, lo, lo + n, amax, n)
+    w8 = torch.empty(flat.numel(), dtype=torch.float8_e4m3fn, device=w.device)
+    ext().fp8_segment_cast(flat, lo, lo + n, amax, E4M3_MAX, w8, n)
+    w8 = w8.view(w.shape)
+    return w8, _bt(w8), amax
+
+
+def _fp8_fwd(x, w_gu, w_down, seg, recipe):
+    from ..ops.fp8 import E4M3_MAX, cast
+
+    R, H = x.shape
+    sx = recipe.scale("x", x, E4M3_MAX)
+    x8, x8t = cast(x, sx, False, transpose=True)
+    gu8, gu8t, a_gu = _expert_weight_fp8(w_gu, recipe, "wgu")
+    d8, d8t, a_d = _expert_weight_fp8(w_down, recipe, "wd")
+    q2 = 1.0 / (E4M3_MAX * sx.qmax)
+    h = grouped_mm(x8, gu8, seg, 1, x.new_empty(R, w_gu.shape[1]), sx.amax, a_gu, q2)
     a = _swiglu_fwd(h)
-    sa = recipe.scale(f"a{e}", a, E4M3_MAX)
-    sd = recipe.scale(f"wd{e}", w_down, E4M3_MAX)
+    sa = recipe.scale("a", a, E4M3_MAX)
     a8, a8t = cast(a, sa, False, transpose=True)
-    d8, d8t = cast(w_down.contiguous(), sd, False, transpose=True)
-    yp = gemm(a8, d8, sa, sd, None, torch.bfloat16)
-    return yp[:c], (h, x8t, gu8t, a8t, d8t, sx, sgu, sa, sd)
+    y = grouped_mm(a8, d8, seg, 1, x.new_empty(R, H), sa.amax, a_d, 1.0 / (E4M3_MAX * sa.qmax))
+    return y, (h, x8t, a8t, gu8t, d8t, sx, sa, a_gu, a_d)
 
 
-def _fp8_expert_bwd(dye, st, recipe, e, dw_gu_e, dw_down_e):
-    from ..ops.fp8 import E4M3_MAX, E5M2_MAX, cast, gemm
+def _fp8_bwd(dy, x, w_gu, w_down, seg, st, recipe, gu_out, d_out):
+    from ..ops.fp8 import E4M3_MAX, E5M2_MAX, cast
 
-    h, x8t, gu8t, a8t, d8t, sx, sgu, sa, sd = st
-    c, cp = dye.shape[0], h.shape[0]
+    h, x8t, a8t, gu8t, d8t, sx, sa, a_gu, a_d = st
+    R, H = x.shape
+    E, I2, _ = w_gu.shape
+    I = w_down.shape[2]
     e5 = recipe.grad_e5m2()
     gmax = E5M2_MAX if e5 else E4M3_MAX
-    dyp = _pad_rows(dye.to(torch.bfloat16), cp)
-    sg = recipe.scale(f"gy{e}", dyp, gmax)
-    dy8, dy8t = cast(dyp, sg, e5, transpose=True)
-    gemm(dy8t, a8t, sg, sa, None, out=dw_down_e)
-    da = gemm(dy8, d8t, sg, sd, None, torch.bfloat16)  # [cp, I]
-    dh = _swiglu_bwd(h, da)  # [cp, 2I]
-    sh = recipe.scale(f"gh{e}", dh, gmax)
+    sg = recipe.scale("gy", dy, gmax)
+    dy8, dy8t = cast(dy, sg, e5, transpose=True)
+    da = grouped_mm(dy8, d8t, seg, 1, x.new_empty(R, I), sg.amax, a_d, 1.0 / (sg.qmax * E4M3_MAX))
+    grouped_mm(dy8t, a8t, seg, 2, d_out[0], sg.amax, sa.amax, 1.0 / (sg.qmax * sa.qmax), accumulate=d_out[1])
+    dh = _swiglu_bwd(h, da)
+    sh = recipe.scale("gh", dh, gmax)
     dh8, dh8t = cast(dh, sh, e5, transpose=True)
-    gemm(dh8t, x8t, sh, sx, None, out=dw_gu_e)
-    return gemm(dh8, gu8t, sh, sgu, None, torch.bfloat16)[:c]
+    grouped_mm(dh8t, x8t, seg, 2, gu_out[0], sh.amax, sx.amax, 1.0 / (sh.qmax * sx.qmax), accumulate=gu_out[1])
+    return grouped_mm(dh8, gu8t, seg, 1, x.new_empty(R, H), sh.amax, a_gu, 1.0 / (sh.qmax * E4M3_MAX))
 
 
 class MoEExperts(nn.Module):
@@ -178,11 +280,20 @@ class MoEExperts(nn.Module):
         self.w_down = nn.Parameter(torch.empty(num_experts, hidden, intermediate))
         self.fp8_recipe = None
 
-    def forward(self, x_sorted, counts):
+    def forward(self, x_routed, seg):
+        """x_routed: [R, H] routed-token buffer (expert e's rows are [seg[e], seg[e+1]), zero pad rows)."""
         w_gu, w_down = self.w_gate_up, self.w_down
-        if w_gu.dtype != x_sorted.dtype:
-            w_gu, w_down = w_gu.to(x_sorted.dtype), w_down.to(x_sorted.dtype)
-        return _GroupedExpertsFn.apply(x_sorted, w_gu, w_down, counts, self.fp8_recipe)
+        slots = (None, None)
+        if w_gu.dtype != x_routed.dtype:
+            w_gu, w_down = w_gu.to(x_routed.dtype), w_down.to(x_routed.dtype)
+        elif torch.is_grad_enabled():
+            # FSDP fused weight-gradient slots (parallel/fsdp.py): the grouped wgrad GEMMs write into the grad shard
+            slots = tuple(getattr(w, "_acc_wgrad_slot", None) for w in (w_gu, w_down))
+            if torch._C._current_graph_task_id() == -1:
+                for sl in slots:
+                    if sl is not None:
+                        sl.uses += 1
+        return _GroupedExpertsFn.apply(x_routed, w_gu, w_down, seg, self.fp8_recipe, slots)
 
 
 class MoELayer(nn.Module):
@@ -232,15 +343,17 @@ class MoELayer(nn.Module):
             w = w / w.sum(-1, keepdim=True)
         w = w.to(t.dtype)
         flat_e = idx.reshape(-1)
-        order = torch.argsort(flat_e, stable=True)
-        src_tok = order // self.top_k
-        w_sorted = w.reshape(-1)[order]
-        x_sorted = t.index_select(0, src_tok)
         if self.ep_group is None or comm.group_size(self.ep_group) == 1:
-            counts = torch.bincount(flat_e, minlength=self.num_experts).tolist()
-            y_sorted = self.experts(x_sorted, counts)
+            order, dest, seg, R = expert_layout(flat_e, self.num_experts)
+            src_tok = order // self.top_k
+            w_sorted = w.reshape(-1)[order]
+            x_routed = t.new_zeros(R, t.shape[1]).index_copy(0, dest, t.index_select(0, src_tok))
+            y_sorted = self.experts(x_routed, seg).index_select(0, dest)
         else:
-            y_sorted = self._ep_experts(x_sorted, flat_e[order])
+            order = torch.argsort(flat_e, stable=True)
+            src_tok = order // self.top_k
+            w_sorted = w.reshape(-1)[order]
+            y_sorted = self._ep_experts(t.index_select(0, src_tok), flat_e[order])
         out = torch.zeros_like(t).index_add_(0, src_tok, y_sorted * w_sorted.unsqueeze(-1))
         return out.view(shape)
 
@@ -261,9 +374,10 @@ class MoELayer(nn.Module):
         sc, rc = send_counts.tolist(), recv_counts.tolist()
         x_recv = comm.all_to_all_var(x_sorted, sc, rc, group)
         e_recv = comm.all_to_all_varlen((e_sorted % El).unsqueeze(-1).to(torch.float32), sc, rc, group).squeeze(-1).long()
-        order2 = torch.argsort(e_recv, stable=True)
-        counts2 = torch.bincount(e_recv, minlength=El).tolist()
-        y_local_sorted = self.experts(x_recv.index_select(0, order2), counts2)
+        # local experts: the same device-side layout + grouped GEMMs as the single-rank path
+        order2, dest2, seg2, R2 = expert_layout(e_recv, El)
+        x_routed = x_recv.new_zeros(R2, x_recv.shape[1]).index_copy(0, dest2, x_recv.index_select(0, order2))
+        y_local_sorted = self.experts(x_routed, seg2).index_select(0, dest2)
         inv = torch.empty_like(order2)
         inv[order2] = torch.arange(order2.numel(), device=order2.device)
         y_recv = y_local_sorted.index_select(0, inv)

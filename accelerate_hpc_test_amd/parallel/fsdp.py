@@ -369,7 +369,9 @@ class FSDPEngine:
 
     def _install_fused_wgrad(self):
         """Route the weight gradient of every plain `nn.Linear` whose weight this engine owns (and that no other module
-        shares) through `_FusedWgradLinearFn`."""
+        shares) through `_FusedWgradLinearFn`; Fp8Linear weights and MoE expert stacks get a slot their own backward
+        writes into."""
+        from ..models.moe import MoEExperts  # lazy: models import parallel.comm
         refs = {}
         for m in self.model.modules():
             for p in m._parameters.values():
@@ -379,11 +381,14 @@ class FSDPEngine:
             for info in unit.infos:
                 m = info.module
                 plain = type(m) is nn.Linear
-                if ((plain or isinstance(m, Fp8Linear)) and info.attr == "weight" and info.param.requires_grad
-                        and refs.get(id(info.param), 0) == 1 and getattr(info.param, "_tp_spec", None) is None):
+                experts = isinstance(m, MoEExperts) and info.attr in ("w_gate_up", "w_down")
+                if (((plain or isinstance(m, Fp8Linear)) and info.attr == "weight") or experts) and info.param.requires_grad \
+                        and refs.get(id(info.param), 0) == 1 and getattr(info.param, "_tp_spec", None) is None:
                     info.fused = True
                     info.param._acc_wgrad_slot = _WgradSlot(self, unit, info)
-                    if plain:  # Fp8Linear routes its fp8 weight-gradient GEMM to the slot itself (ops/fp8.py)
+                    # Fp8Linear routes its fp8 weight-gradient GEMM to the slot itself (ops/fp8.py), MoEExperts its
+                    # grouped weight-gradient GEMMs (models/moe.py)
+                    if plain:
                         m.__class__ = _FusedWgradLinear
 
     def _replace_param(self, info: _ParamInfo, new: nn.Parameter):

@@ -565,6 +565,46 @@ def check_expert_parallel_mixtral(steps: int = 2):
         assert torch.allclose(full[n], full2[n]), n
 
 
+def check_fsdp_mixtral_expert_slots(steps: int = 2):
+    """Mixtral under FSDP without expert parallelism: the stacked expert weights are FSDP-sharded and their grouped
+    weight-gradient GEMMs write straight into the engine's gradient slots (models/moe.py) == one process."""
+    from accelerate_hpc_test_amd.models.mixtral import MixtralConfig, MixtralForCausalLM
+
+    W = int(os.environ["WORLD_SIZE"])
+    r = int(os.environ["RANK"])
+    plugin = FullyShardedDataParallelPlugin(fsdp_version=2, auto_wrap_policy="transformer_based_wrap",
+                                            transformer_cls_names_to_wrap=["MixtralDecoderLayer"])
+    acc = Accelerator(cpu=True, fsdp_plugin=plugin)
+    cfg = MixtralConfig(vocab_size=128, hidden_size=32, intermediate_size=48, num_hidden_layers=2, num_attention_heads=4,
+                        num_key_value_heads=2, head_dim=8, num_local_experts=4, num_experts_per_tok=2, max_position_embeddings=64)
+    set_seed(0)
+    base = MixtralForCausalLM(cfg)
+    base.init_weights()
+    model = copy.deepcopy(base)
+    opt = torch.optim.SGD(model.parameters(), lr=0.2, momentum=0.9)
+    base_opt = torch.optim.SGD(base.parameters(), lr=0.2, momentum=0.9)
+    model, opt = acc.prepare(model, opt)
+    eng = model.engine
+    fused = sorted(i.fqn for u in eng.units for i in u.infos if i.fused and "experts" in i.fqn)
+    assert fused == sorted(f"layers.{l}.block_sparse_moe.experts.{n}" for l in range(2) for n in ("w_gate_up", "w_down")), fused
+    g = torch.Generator().manual_seed(5)
+    bs, S = 2, 8
+    for _ in range(steps):
+        ids = torch.randint(0, 128, (bs * W, S), generator=g)
+        local = ids[r * bs : (r + 1) * bs]
+        out = model(local, labels=local)
+        acc.backward(out.loss)
+        opt.step()
+        opt.zero_grad()
+        ref = base(ids, labels=ids)
+        ref.loss.backward()
+        base_opt.step()
+        base_opt.zero_grad()
+    full = acc.get_state_dict(model)
+    for n, q in base.state_dict().items():
+        assert torch.allclose(full[n].float(), q.float(), atol=5e-5), (n, (full[n] - q).abs().max())
+
+
 def check_join_uneven_inputs():
     """Rank r gets 2 + r batches; with `join_uneven_inputs` the short rank shadows the long rank's all-reduces.
     Oracle: grads of each step = sum over active ranks / W (divide_by_initial_world_size)."""

@@ -279,52 +279,132 @@ def test_fp8_gemm_v3_ring_kernel_matches_reference(M, N, K):
         assert torch.allclose(acc, base + o32, rtol=1e-5, atol=1e-4)
 
 
-def test_moe_grouped_experts_fp8_matches_bf16():
-    """fp8 grouped experts (padded segments, 6 MX-fp8 GEMMs per expert): the forward equals a PyTorch emulation of
-    the same per-tensor e4m3 quantisation; output and gradients stay within fp8 error of the bf16 path (e5m2
-    gradients); a zero-token expert keeps a zero gradient."""
+def _routed(counts, H, dtype=torch.bfloat16, seed=0):
+    """A routed-token buffer with the MoE layout: expert e's rows start at a multiple of 64 (zero pad rows)."""
+    from accelerate_hpc_test_amd.models.moe import expert_layout
+
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    flat_e = torch.cat([torch.full((c,), e, dtype=torch.long) for e, c in enumerate(counts)]).to(DEV)
+    flat_e = flat_e[torch.randperm(flat_e.numel(), device=DEV, generator=g)]
+    order, dest, seg, R = expert_layout(flat_e, len(counts))
+    rows = torch.randn(flat_e.numel(), H, device=DEV, generator=g).to(dtype)
+    x = torch.zeros(R, H, device=DEV, dtype=dtype).index_copy(0, dest, rows)
+    return x, seg, dest
+
+
+@pytest.mark.parametrize("dt", ["bf16", "fp8"])
+def test_grouped_gemm_kernel_both_modes(dt):
+    """Grouped GEMM over a device segment table (one launch): GROUP_M (rows of segment e times expert e's weight;
+    tail rows zeroed) and GROUP_K (per-expert weight gradients over each segment's K range), with empty and
+    non-multiple-of-256 segments, vs fp32 PyTorch per segment. bf16 operands, and e4m3 / e5m2 with per-expert scales."""
+    from accelerate_hpc_test_amd.ops import fp8
+    from accelerate_hpc_test_amd.ops._ext import ext
+
+    torch.manual_seed(0)
+    counts = [300, 0, 77, 513, 64, 1]
+    E, H, N = len(counts), 512, 768
+    x, seg, _ = _routed(counts, H)
+    R = x.shape[0]
+    w = torch.randn(E, N, H, device=DEV, dtype=torch.bfloat16) * 0.05
+    bounds = seg.tolist()
+    if dt == "bf16":
+        a, b, sa, sb, smul = x, w, torch.ones(1, device=DEV), torch.ones(E, device=DEV), 1.0
+        af, bf = x.float(), w.float()
+    else:
+        sx = fp8.Scale(fp8.amax(x), fp8.E5M2_MAX)
+        a = fp8.cast(x, sx, e5m2=True)
+        sb = torch.stack([w[e].float().abs().max() for e in range(E)])
+        b = torch.stack([fp8.cast(w[e].contiguous(), fp8.Scale(sb[e : e + 1], fp8.E4M3_MAX)) for e in range(E)])
+        sa, smul = sx.amax, 1.0 / (fp8.E5M2_MAX * fp8.E4M3_MAX)
+        af = a.float() * sx.inv()
+        bf = torch.stack([b[e].float() * sb[e] / fp8.E4M3_MAX for e in range(E)])
+    out = torch.full((R, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+    ext().grouped_gemm(a, b, out, seg, 1, sa, sb, smul, False)
+    ref = torch.zeros(R, N, device=DEV)
+    for e in range(E):
+        lo, hi = bounds[e], bounds[e + 1]
+        ref[lo:hi] = af[lo:hi] @ bf[e].t()
+    assert not out.isnan().any(), "rows left unwritten"
+    assert _rel(out, ref) < 1e-2, _rel(out, ref)
+    # GROUP_K: dW_e = dY[:, seg_e] . X[:, seg_e]^T over the transposed buffers
+    dyT = torch.randn(N, R, device=DEV, dtype=torch.bfloat16)
+    xT = x.t().contiguous()
+    if dt == "bf16":
+        ga, gb, gsa, gsb, gsm, gaf, gbf = dyT, xT, torch.ones(1, device=DEV), torch.ones(1, device=DEV), 1.0, dyT.float(), xT.float()
+    else:
+        s1, s2 = fp8.Scale(fp8.amax(dyT), fp8.E5M2_MAX), fp8.Scale(fp8.amax(xT), fp8.E4M3_MAX)
+        ga, gb = fp8.cast(dyT, s1, e5m2=True), fp8.cast(xT, s2)
+        gsa, gsb, gsm = s1.amax, s2.amax, 1.0 / (fp8.E5M2_MAX * fp8.E4M3_MAX)
+        gaf, gbf = ga.float() * s1.inv(), gb.float() * s2.inv()
+    dw = torch.full((E, N, H), float("nan"), device=DEV, dtype=torch.float32)
+    ext().grouped_gemm(ga, gb, dw, seg, 2, gsa, gsb, gsm, False)
+    for e in range(E):
+        lo, hi = bounds[e], bounds[e + 1]
+        r = gaf[:, lo:hi] @ gbf[:, lo:hi].t()
+        if hi == lo:
+            assert dw[e].abs().max() == 0, e
+        else:
+            assert _rel(dw[e], r) < 1e-3, (e, _rel(dw[e], r))
+
+
+@pytest.mark.parametrize("fp8_on", [False, True])
+def test_moe_grouped_experts_match_per_expert_reference(fp8_on):
+    """MoEExperts on the routed buffer (6 grouped GEMM launches per step, device segment table) against a per-expert
+    fp32 PyTorch reference: forward, dx, dW_gate_up, dW_down; fp8 within fp8 error of it (forward vs an exact
+    emulation of the per-tensor / per-expert e4m3 quantisation); an expert with no tokens gets a zero gradient."""
     import torch.nn.functional as F
 
     from accelerate_hpc_test_amd.models.moe import MoEExperts
     from accelerate_hpc_test_amd.ops.fp8 import E4M3_MAX, Fp8Recipe
 
     torch.manual_seed(0)
-    E, H, I = 4, 256, 384
     counts = [200, 0, 77, 300]
+    E, H, I = len(counts), 256, 512  # fp8 needs every GEMM dim % 256 (bf16 also runs I = 384: K only needs 256 B)
     ex = MoEExperts(E, H, I).to(DEV, torch.bfloat16)
     with torch.no_grad():
         ex.w_gate_up.normal_(0, 0.05)
         ex.w_down.normal_(0, 0.05)
-    x = torch.randn(sum(counts), H, device=DEV, dtype=torch.bfloat16)
-    dy = torch.randn(sum(counts), H, device=DEV, dtype=torch.bfloat16)
-    res = []
-    for recipe in (None, Fp8Recipe()):
-        ex.fp8_recipe = recipe
-        ex.zero_grad()
-        xi = x.clone().requires_grad_(True)
-        y = ex(xi, counts)
-        y.backward(dy)
-        res.append((y.float(), xi.grad.float(), ex.w_gate_up.grad.float(), ex.w_down.grad.float()))
-
-    def q(t):  # per-tensor e4m3 round trip, as the cast kernel does it
-        s = E4M3_MAX / t.float().abs().max().clamp_min(1e-12)
-        return (t.float() * s).clamp(-E4M3_MAX, E4M3_MAX).to(torch.float8_e4m3fn).float() / s
-
-    emu, off = [], 0
-    for e, c in enumerate(counts):
-        if c == 0:
-            continue
-        h = (q(x[off : off + c]) @ q(ex.w_gate_up[e]).t()).to(torch.bfloat16)
-        g, u = h.float().chunk(2, -1)
-        a = (F.silu(g) * u).to(torch.bfloat16)
-        emu.append(q(a) @ q(ex.w_down[e]).t())
-        off += c
-    emu = torch.cat(emu)
-    # same quantisation; the residue is bf16 rounding of h / a flipping a few fp8 roundings (≈1 %)
-    assert _rel(res[1][0], emu) < 1.5e-2, _rel(res[1][0], emu)
-    for name, ref, out, tol in zip(("y", "dx", "dw_gu", "dw_down"), res[0], res[1], (0.12, 0.15, 0.15, 0.15)):
+    ex.fp8_recipe = Fp8Recipe() if fp8_on else None
+    x, seg, dest = _routed(counts, H, seed=1)
+    dy = torch.zeros_like(x).index_copy(0, dest, torch.randn(dest.numel(), H, device=DEV, dtype=torch.bfloat16))
+    xi = x.clone().requires_grad_(True)
+    y = ex(xi, seg)
+    y.backward(dy)
+    bounds = seg.tolist()
+    xr = x.float().requires_grad_(True)
+    wgu = ex.w_gate_up.detach().float().requires_grad_(True)
+    wd = ex.w_down.detach().float().requires_grad_(True)
+    yr = torch.zeros(x.shape[0], H, device=DEV)
+    for e in range(E):
+        lo, hi = bounds[e], bounds[e + 1]
+        if hi > lo:
+            g, u = (xr[lo:hi] @ wgu[e].t()).chunk(2, -1)
+            yr = yr.index_add(0, torch.arange(lo, hi, device=DEV), (F.silu(g) * u) @ wd[e].t())
+    yr.backward(dy.float())
+    tol = 0.15 if fp8_on else 2e-2
+    for name, out, ref in (("y", y, yr), ("dx", xi.grad, xr.grad), ("dw_gu", ex.w_gate_up.grad, wgu.grad),
+                           ("dw_down", ex.w_down.grad, wd.grad)):
         assert _rel(out, ref) < tol, (name, _rel(out, ref))
-    assert res[1][2][1].abs().max() == 0 and res[1][3][1].abs().max() == 0
+    assert ex.w_gate_up.grad[1].abs().max() == 0 and ex.w_down.grad[1].abs().max() == 0
+    if fp8_on:
+        def q(t):  # per-tensor e4m3 round trip, as the cast kernels do it
+            s = E4M3_MAX / t.float().abs().max().clamp_min(1e-12)
+            return (t.float() * s).clamp(-E4M3_MAX, E4M3_MAX).to(torch.float8_e4m3fn).float() / s
+
+        xq = q(x)
+        hs = torch.zeros(x.shape[0], 2 * I, device=DEV)
+        for e in range(E):
+            lo, hi = bounds[e], bounds[e + 1]
+            if hi > lo:
+                hs[lo:hi] = xq[lo:hi] @ q(ex.w_gate_up[e]).t()
+        g, u = hs.to(torch.bfloat16).float().chunk(2, -1)
+        aq = q((F.silu(g) * u).to(torch.bfloat16))
+        emu = torch.zeros(x.shape[0], H, device=DEV)
+        for e in range(E):
+            lo, hi = bounds[e], bounds[e + 1]
+            if hi > lo:
+                emu[lo:hi] = aq[lo:hi] @ q(ex.w_down[e]).t()
+        assert _rel(y, emu) < 1.5e-2, _rel(y, emu)
 
 
 @pytest.mark.parametrize("e5m2", [False, True])

@@ -121,6 +121,10 @@ def test_expert_parallel_mixtral():
     debug_launcher(td.check_expert_parallel_mixtral, num_processes=2)
 
 
+def test_fsdp_mixtral_expert_wgrad_slots():
+    debug_launcher(td.check_fsdp_mixtral_expert_slots, num_processes=2)
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_ddp_join_uneven_inputs(world):
     debug_launcher(td.check_join_uneven_inputs, num_processes=world)
