@@ -43,6 +43,15 @@ void fp8_gemm_select(int64_t variant, int64_t group_m);
 void grouped_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor out, torch::Tensor seg, int64_t mode, torch::Tensor sa,
                   torch::Tensor sb, double smul, bool accumulate);
 torch::Tensor batched_transpose(torch::Tensor x);
+// small_allreduce.hip
+std::tuple<int64_t, pybind11::bytes> sar_create(int64_t rank, int64_t world, int64_t max_bytes);
+void sar_open(int64_t id, std::vector<std::string> handles);
+void sar_link_local(std::vector<int64_t> ids);
+void sar_allreduce(int64_t id, torch::Tensor in, torch::Tensor out, int64_t op, double timeout_ms);
+int64_t sar_status(int64_t id);
+void sar_allreduce_local_group(std::vector<int64_t> ids, std::vector<torch::Tensor> ins, std::vector<torch::Tensor> outs,
+                               int64_t op, double timeout_ms);
+void sar_destroy(int64_t id);
 // comm_pack.hip
 void grad_shard_update(torch::Tensor dst, torch::Tensor src, double scale, bool accumulate);
 // runtime/*.cpp
@@ -79,6 +88,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("u8_transpose", &u8_transpose);
   m.def("grouped_gemm", &grouped_gemm);
   m.def("batched_transpose", &batched_transpose);
+  m.def("sar_create", &sar_create);
+  m.def("sar_open", &sar_open);
+  m.def("sar_link_local", &sar_link_local);
+  m.def("sar_allreduce", &sar_allreduce);
+  m.def("sar_status", &sar_status);
+  m.def("sar_allreduce_local_group", &sar_allreduce_local_group);
+  m.def("sar_destroy", &sar_destroy);
   m.def("fp8_gemm_select", &fp8_gemm_select, pybind11::arg("variant"), pybind11::arg("group_m") = 0);
   register_runtime(m);
   m.def("blaslt_wgrad_f32", &blaslt_wgrad_f32);

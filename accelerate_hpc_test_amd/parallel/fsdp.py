@@ -50,6 +50,7 @@ from ..utils.fault_tolerance import record_collective
 from ..utils.tracing import trace_range
 from ..ops._ext import ext, native_enabled
 from ..ops.fp8 import Fp8Linear
+from . import small_allreduce
 
 _ALIGN = 64  # elements; keeps every rank's shard 128-B aligned for bf16 / 256-B for fp32
 # opt-in: on MI355X the searched algorithms measured 0.3-0.6 % slower end to end than torch's default pick (interleaved A/B,
@@ -351,7 +352,7 @@ class FSDPEngine:
                     piece = src[info.local_lo : info.local_hi]
                     u.f8_amax[k] = piece.abs().max().float() if piece.numel() else 0.0
         if self.sharded and self.world_size > 1:
-            dist.all_reduce(self.f8_amax_all, op=dist.ReduceOp.MAX, group=self.group)
+            small_allreduce.all_reduce_(self.f8_amax_all, op=dist.ReduceOp.MAX, group=self.group)
         for u in self.f8_units:
             lo, hi, max_len, _ = u.f8_seg
             src = u.shard_lp[: u.f8.shard_len]
@@ -1057,7 +1058,7 @@ class FSDPEngine:
             sq = p.grad.detach().float().pow(2).sum()
             total += sq if getattr(p, "_ep_spec", None) is not None else sq / self.world_size
         if self.sharded:
-            dist.all_reduce(total, group=self.group)
+            small_allreduce.all_reduce_(total, group=self.group)  # 4 bytes: IPC one-shot kernel, not an RCCL ring
         clip_grads_by_total_sq(flat_params + extra, total, max_norm)
         return total.sqrt().reshape(())
 

@@ -524,7 +524,10 @@ def reduce(tensor, reduction="mean", scale=1.0):
     if _coalescable(leaves):
         flat = torch.cat([t.reshape(-1) for t in leaves])
         record_collective("all_reduce", flat)
-        torch.distributed.all_reduce(flat, torch.distributed.ReduceOp.SUM)
+        # small (loss / metric / trigger-flag) reductions take the IPC one-shot kernel (parallel/small_allreduce.py)
+        from ..parallel import small_allreduce
+
+        small_allreduce.all_reduce_(flat, torch.distributed.ReduceOp.SUM)
         _finish(flat)
         outs, off = [], 0
         for t in leaves:

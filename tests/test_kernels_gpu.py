@@ -873,3 +873,100 @@ def test_fp8_segment_kernels_and_byte_transpose():
     assert torch.equal(ext().u8_transpose(w), w.t().contiguous())
     w2 = torch.randint(0, 255, (200, 136), device=DEV, dtype=torch.uint8)  # edge tiles
     assert torch.equal(ext().u8_transpose(w2), w2.t().contiguous())
+
+
+_SAR_CASES = [(torch.float32, 1, 0), (torch.float32, 1000, 0), (torch.bfloat16, 4099, 0), (torch.int64, 3, 0),
+              (torch.float32, 262144, 1), (torch.int32, 77, 1), (torch.bfloat16, 65536, 0)]
+
+
+def _sar_inputs(W, dtype, n, seed):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    if dtype.is_floating_point:
+        return [torch.randn(n, device=DEV, generator=g).to(dtype) for _ in range(W)]
+    return [torch.randint(-1000, 1000, (n,), device=DEV, generator=g).to(dtype) for _ in range(W)]
+
+
+def _sar_ref(ins, op):
+    st = torch.stack([x.double() if not x.dtype.is_floating_point else x.float() for x in ins])
+    return st.sum(0) if op == 0 else st.max(0).values
+
+
+@pytest.mark.parametrize("W", [2, 3, 4, 8])
+def test_small_allreduce_virtual_peers(W):
+    """The IPC one-shot all-reduce kernel with W 'virtual peer' ranks in ONE process on one GPU: W communicators linked
+    without IPC, every rank's workgroups in one launch (co-resident: each waits for the others' flags, bounded by a
+    10 s timeout), several calls in a row (alternating data slots), sum / max, fp32 / bf16 / int32 / int64, 1 element
+    to 1 MiB, against torch."""
+    from accelerate_hpc_test_amd.ops._ext import ext
+
+    ids = [ext().sar_create(r, W, 1 << 20)[0] for r in range(W)]
+    try:
+        ext().sar_link_local(ids)
+        for case, (dtype, n, op) in enumerate(_SAR_CASES):
+            for rep in range(3):
+                ins = _sar_inputs(W, dtype, n, 100 * case + rep)
+                outs = [torch.empty_like(x) for x in ins]
+                ext().sar_allreduce_local_group(ids, ins, outs, op, 10_000.0)
+                torch.cuda.synchronize()
+                assert all(ext().sar_status(i) == 0 for i in ids), "a rank timed out waiting for its peers"
+                ref = _sar_ref(ins, op)
+                for r in range(W):
+                    if dtype.is_floating_point:
+                        tol = 1e-2 if dtype == torch.bfloat16 else 1e-5
+                        assert torch.allclose(outs[r].float(), ref, rtol=tol, atol=tol), (dtype, n, op, r)
+                    else:
+                        assert torch.equal(outs[r].double(), ref), (dtype, n, op, r)
+                assert all(torch.equal(outs[0], o) for o in outs[1:]), "ranks disagree"
+    finally:
+        for i in ids:
+            ext().sar_destroy(i)
+
+
+def _sar_ipc_worker(rank, world, port, q):
+    import os
+
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ACCELERATE_SMALL_ALLREDUCE_TIMEOUT_S="20")
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from accelerate_hpc_test_amd.parallel.small_allreduce import SmallAllReduce
+
+        c = SmallAllReduce(None)
+        assert c.ok, "IPC setup failed"
+        res = []
+        for case, (dtype, n, op) in enumerate(_SAR_CASES):
+            ins = _sar_inputs(world, dtype, n, case)
+            t = ins[rank].clone()
+            c.all_reduce_(t, dist.ReduceOp.SUM if op == 0 else dist.ReduceOp.MAX)
+            torch.cuda.synchronize()
+            ref = _sar_ref(ins, op)
+            ok = torch.allclose(t.double(), ref.double(), rtol=1e-2, atol=1e-2) if dtype.is_floating_point else torch.equal(t.double(), ref)
+            res.append(bool(ok))
+        c.close()
+        dist.destroy_process_group()
+        q.put((rank, res, None))
+    except Exception as exc:  # noqa: BLE001
+        q.put((rank, None, repr(exc)))
+
+
+def test_small_allreduce_two_processes_over_ipc():
+    """Two processes on the one GPU exchange real HIP IPC handles of their buffers (gloo for the handle exchange) and
+    run the one-shot kernel concurrently: the multi-process path the 8-GPU node uses, minus xGMI."""
+    import torch.multiprocessing as mp
+
+    from accelerate_hpc_test_amd.utils.other import get_free_port
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = get_free_port()
+    procs = [ctx.Process(target=_sar_ipc_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=100) for _ in procs]
+    for p in procs:
+        p.join(timeout=30)
+    for rank, res, err in out:
+        assert err is None, (rank, err)
+        assert all(res), (rank, res)
