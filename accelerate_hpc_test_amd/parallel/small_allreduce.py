@@ -61,6 +61,16 @@ class SmallAllReduce:
         votes = [None] * self.world
         dist.all_gather_object(votes, ok, group=group)
         self.ok = all(votes)
+        if self.ok:
+            # self-test on the real peers (short timeout): a mapping that opens but does not deliver stores across the
+            # fabric is caught here and the group stays on RCCL
+            t = torch.full((64,), float(self.rank + 1), device=torch.cuda.current_device())
+            ext().sar_allreduce(self.id, t, t, 0, 10_000.0)
+            torch.cuda.synchronize()
+            good = ext().sar_status(self.id) == 0 and bool((t == self.world * (self.world + 1) / 2).all())
+            votes = [None] * self.world
+            dist.all_gather_object(votes, good, group=group)
+            self.ok = all(votes)
         if not self.ok and self.id is not None:
             ext().sar_destroy(self.id)
             self.id = None
