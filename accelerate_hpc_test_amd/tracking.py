@@ -170,7 +170,7 @@ class TensorBoardTracker(GeneralTracker):
 
     @on_main_process
     def log(self, values: dict, step: Optional[int] = None, **kwargs):
-        for k, v in values.items():
+        for k, v in _scalars(values).items():
             if isinstance(v, (int, float)):
                 self.writer.add_scalar(k, v, global_step=step, **kwargs)
             elif isinstance(v, str):
@@ -180,8 +180,25 @@ class TensorBoardTracker(GeneralTracker):
         self.writer.flush()
 
     @on_main_process
+    def log_images(self, values: dict, step: Optional[int] = None, **kwargs):
+        """`values`: {tag: stacked images [N, C, H, W] (array or tensor)}."""
+        for k, v in values.items():
+            self.writer.add_images(k, v, global_step=step, **kwargs)
+        self.writer.flush()
+
+    @on_main_process
     def finish(self):
         self.writer.close()
+
+
+def _scalars(values: dict) -> dict:
+    """0-d tensors / numpy scalars -> Python numbers (tracker libraries reject tensors)."""
+    out = {}
+    for k, v in values.items():
+        if hasattr(v, "item") and getattr(v, "ndim", 0) == 0:
+            v = v.item()
+        out[k] = v
+    return out
 
 
 class _LazyTracker(GeneralTracker):
@@ -191,9 +208,10 @@ class _LazyTracker(GeneralTracker):
     requires_logging_directory = False
 
     @on_main_process
-    def __init__(self, run_name: str, **kwargs):
+    def __init__(self, run_name: str, /, **kwargs):
+        # positional-only: a library's own `run_name` option (MLflow, ...) can travel in **kwargs
         super().__init__()
-        self.run_name = run_name
+        self.run_name = run_name  # the project / experiment name the Accelerator passes
         self.init_kwargs = kwargs
         self.run = None
 
@@ -220,7 +238,22 @@ class WandBTracker(_LazyTracker):
 
     @on_main_process
     def log(self, values: dict, step: Optional[int] = None, **kwargs):
-        self.run.log(values, step=step, **kwargs)
+        self.run.log(_scalars(values), step=step, **kwargs)
+
+    @on_main_process
+    def log_images(self, values: dict, step: Optional[int] = None, **kwargs):
+        """`values`: {key: list of images (arrays / PIL)} -> wandb.Image panels."""
+        import wandb
+
+        self.log({k: [wandb.Image(img) for img in imgs] for k, imgs in values.items()}, step=step, **kwargs)
+
+    @on_main_process
+    def log_table(self, table_name: str, columns: Optional[list] = None, data: Optional[list] = None, dataframe=None,
+                  step: Optional[int] = None, **kwargs):
+        """One wandb.Table from `columns` + `data` rows, or from a pandas `dataframe`."""
+        import wandb
+
+        self.log({table_name: wandb.Table(columns=columns, data=data, dataframe=dataframe)}, step=step, **kwargs)
 
     @on_main_process
     def finish(self):
@@ -238,7 +271,7 @@ class TrackioTracker(_LazyTracker):
 
     @on_main_process
     def log(self, values, step=None, **kwargs):
-        self.run.log(values, **kwargs)
+        self.run.log(_scalars(values), **kwargs)
 
     @on_main_process
     def finish(self):
@@ -260,7 +293,15 @@ class CometMLTracker(_LazyTracker):
 
     @on_main_process
     def log(self, values, step=None, **kwargs):
-        self.run.log_metrics(values, step=step, **kwargs)
+        if step is not None:
+            self.run.set_step(step)
+        for k, v in _scalars(values).items():
+            if isinstance(v, (int, float)):
+                self.run.log_metric(k, v, step=step, **kwargs)
+            elif isinstance(v, str):
+                self.run.log_other(k, v, **kwargs)
+            elif isinstance(v, dict):
+                self.run.log_metrics(v, step=step, **kwargs)
 
     @on_main_process
     def finish(self):
@@ -272,7 +313,7 @@ class AimTracker(_LazyTracker):
     requires_logging_directory = True
 
     @on_main_process
-    def __init__(self, run_name: str, logging_dir=".", **kwargs):
+    def __init__(self, run_name: str, /, logging_dir=".", **kwargs):
         super().__init__(run_name, **kwargs)
         self.aim_repo_path = logging_dir
 
@@ -289,8 +330,19 @@ class AimTracker(_LazyTracker):
 
     @on_main_process
     def log(self, values, step=None, **kwargs):
-        for key, value in values.items():
+        for key, value in _scalars(values).items():
             self.run.track(value, name=key, step=step, **kwargs)
+
+    @on_main_process
+    def log_images(self, values: dict, step: Optional[int] = None, kwargs: Optional[dict] = None):
+        """`values`: {name: image or (image, caption)}; `kwargs` = {"aim_image": {...}, "track": {...}}."""
+        import aim
+
+        kwargs = kwargs or {}
+        for name, val in values.items():
+            img, caption = val if isinstance(val, tuple) else (val, "")
+            self.run.track(aim.Image(img, caption=caption, **kwargs.get("aim_image", {})), name=name, step=step,
+                           **kwargs.get("track", {}))
 
     @on_main_process
     def finish(self):
@@ -318,7 +370,29 @@ class MLflowTracker(_LazyTracker):
     def log(self, values, step=None, **kwargs):
         import mlflow
 
-        mlflow.log_metrics({k: v for k, v in values.items() if isinstance(v, (int, float))}, step=step)
+        vals = _scalars(values)
+        skipped = [k for k, v in vals.items() if not isinstance(v, (int, float))]
+        if skipped:
+            logger.warning_once(f"MLflow logs numbers only; not logged: {skipped}")
+        mlflow.log_metrics({k: v for k, v in vals.items() if isinstance(v, (int, float))}, step=step)
+
+    @on_main_process
+    def log_figure(self, figure, artifact_file: str, **kwargs):
+        import mlflow
+
+        mlflow.log_figure(figure=figure, artifact_file=artifact_file, **kwargs)
+
+    @on_main_process
+    def log_artifact(self, local_path: str, artifact_path: Optional[str] = None):
+        import mlflow
+
+        mlflow.log_artifact(local_path=local_path, artifact_path=artifact_path)
+
+    @on_main_process
+    def log_artifacts(self, local_dir: str, artifact_path: Optional[str] = None):
+        import mlflow
+
+        mlflow.log_artifacts(local_dir=local_dir, artifact_path=artifact_path)
 
     @on_main_process
     def finish(self):
@@ -340,13 +414,45 @@ class ClearMLTracker(_LazyTracker):
     def store_init_configuration(self, values):
         self.run.connect_configuration(values)
 
+    @staticmethod
+    def _title_series(key: str):
+        """"eval_loss" -> ("loss", "eval"); keys without a split prefix -> (key, "train")."""
+        for prefix in ("eval", "test", "train"):
+            if key.startswith(prefix + "_"):
+                return key[len(prefix) + 1 :], prefix
+        return key, "train"
+
     @on_main_process
     def log(self, values, step=None, **kwargs):
         clearml_logger = self.run.get_logger()
+        for k, v in _scalars(values).items():
+            if not isinstance(v, (int, float)):
+                logger.warning_once(f"ClearML logs numbers only; not logged: {k}")
+                continue
+            if step is None:
+                clearml_logger.report_single_value(name=k, value=v, **kwargs)
+            else:
+                title, series = self._title_series(k)
+                clearml_logger.report_scalar(title=title, series=series, value=v, iteration=step, **kwargs)
+
+    @on_main_process
+    def log_images(self, values: dict, step: Optional[int] = None, **kwargs):
+        clearml_logger = self.run.get_logger()
         for k, v in values.items():
-            if isinstance(v, (int, float)):
-                title, _, series = k.partition("_")
-                clearml_logger.report_scalar(title=title, series=series or title, value=v, iteration=step or 0)
+            title, series = self._title_series(k)
+            clearml_logger.report_image(title=title, series=series, iteration=step, image=v, **kwargs)
+
+    @on_main_process
+    def log_table(self, table_name: str, columns: Optional[list] = None, data: Optional[list] = None, dataframe=None,
+                  step: Optional[int] = None, **kwargs):
+        """A table from `columns` + `data` rows (header row first) or a pandas `dataframe`."""
+        table = dataframe
+        if table is None:
+            if data is None:
+                raise ValueError("`ClearMLTracker.log_table` needs `data` or `dataframe`.")
+            table = ([list(columns)] if columns is not None else []) + [list(r) for r in data]
+        title, series = self._title_series(table_name)
+        self.run.get_logger().report_table(title=title, series=series, table_plot=table, iteration=step, **kwargs)
 
     @on_main_process
     def finish(self):
@@ -370,7 +476,7 @@ class DVCLiveTracker(_LazyTracker):
     def log(self, values, step=None, **kwargs):
         if step is not None:
             self.run.step = step
-        for k, v in values.items():
+        for k, v in _scalars(values).items():
             self.run.log_metric(k, v, **kwargs)
         self.run.next_step()
 
@@ -396,7 +502,13 @@ class SwanLabTracker(_LazyTracker):
 
     @on_main_process
     def log(self, values, step=None, **kwargs):
-        self.run.log(values, step=step, **kwargs)
+        self.run.log(_scalars(values), step=step, **kwargs)
+
+    @on_main_process
+    def log_images(self, values: dict, step: Optional[int] = None, **kwargs):
+        import swanlab
+
+        self.log({k: [swanlab.Image(img) for img in imgs] for k, imgs in values.items()}, step=step, **kwargs)
 
     @on_main_process
     def finish(self):
