@@ -1,8 +1,9 @@
 """`accelerate-amd` root CLI (parity: reference commands/accelerate_cli.py): config, env, estimate-memory,
-launch, merge-weights, test, to-fsdp2."""
+launch, merge-weights, test, to-fsdp2, aliases (opt-in upstream-style command names)."""
 
 from argparse import ArgumentParser
 
+from .aliases import aliases_command_parser
 from .config import get_config_parser
 from .env import env_command_parser
 from .estimate import estimate_command_parser
@@ -22,6 +23,7 @@ def build_parser() -> ArgumentParser:
     merge_command_parser(subparsers=subparsers)
     test_command_parser(subparsers=subparsers)
     to_fsdp2_command_parser(subparsers=subparsers)
+    aliases_command_parser(subparsers=subparsers)
     return parser
 
 

@@ -40,21 +40,31 @@ if os.environ.get("ACCELERATE_SKIP_NATIVE_BUILD", "0") != "1":
     )
     cmdclass = {"build_ext": BuildExtension.with_options(use_ninja=True)}
 
+console_scripts = [
+    "accelerate-amd=accelerate_hpc_test_amd.commands.accelerate_cli:main",
+    "accelerate-amd-launch=accelerate_hpc_test_amd.commands.launch:main",
+    "accelerate-amd-config=accelerate_hpc_test_amd.commands.config:main",
+    "accelerate-amd-estimate-memory=accelerate_hpc_test_amd.commands.estimate:main",
+    "accelerate-amd-merge-weights=accelerate_hpc_test_amd.commands.merge:main",
+]
+# Opt-in drop-in names of the reference (setup.py:70-78); off by default so an installed upstream `accelerate` is not
+# shadowed. Also available after installation: `accelerate-amd aliases install`.
+if os.environ.get("ACCELERATE_AMD_INSTALL_ALIASES", "0") == "1":
+    console_scripts += [
+        "accelerate=accelerate_hpc_test_amd.commands.accelerate_cli:main",
+        "accelerate-launch=accelerate_hpc_test_amd.commands.launch:main",
+        "accelerate-config=accelerate_hpc_test_amd.commands.config:main",
+        "accelerate-estimate-memory=accelerate_hpc_test_amd.commands.estimate:main",
+        "accelerate-merge-weights=accelerate_hpc_test_amd.commands.merge:main",
+    ]
+
 setup(
     name="accelerate_hpc_test_amd",
     version="0.1.0",
     description="MI355X-native training-loop framework with the Accelerate API (RCCL/xGMI, HIP/CDNA4 kernels)",
     packages=find_packages(include=["accelerate_hpc_test_amd", "accelerate_hpc_test_amd.*"]),
     python_requires=">=3.10",
-    entry_points={
-        "console_scripts": [
-            "accelerate-amd=accelerate_hpc_test_amd.commands.accelerate_cli:main",
-            "accelerate-amd-launch=accelerate_hpc_test_amd.commands.launch:main",
-            "accelerate-amd-config=accelerate_hpc_test_amd.commands.config:main",
-            "accelerate-amd-estimate-memory=accelerate_hpc_test_amd.commands.estimate:main",
-            "accelerate-amd-merge-weights=accelerate_hpc_test_amd.commands.merge:main",
-        ]
-    },
+    entry_points={"console_scripts": console_scripts},
     ext_modules=ext_modules,
     cmdclass=cmdclass,
 )

@@ -327,3 +327,30 @@ def test_env_command(cfgdir):
     r = _run([sys.executable, "-m", "accelerate_hpc_test_amd.commands.accelerate_cli", "env", "--config_file", str(cfgdir / "fp8.yaml")])
     assert r.returncode == 0, r.stderr[-2000:]
     assert "PyTorch version" in r.stdout and "mixed_precision: fp8" in r.stdout
+
+
+def test_opt_in_upstream_command_aliases(tmp_path):
+    """`accelerate-amd aliases install --dir D` writes the reference's command names (accelerate, accelerate-launch,
+    ...) as launchers of this CLI; they run, refuse to overwrite foreign files, and `remove` deletes only ours."""
+    import subprocess
+    import sys
+
+    from accelerate_hpc_test_amd.commands import aliases
+    from accelerate_hpc_test_amd.commands.accelerate_cli import main
+
+    d = tmp_path / "bin"
+    main(["aliases", "install", "--dir", str(d)])
+    assert sorted(p.name for p in d.iterdir()) == sorted(aliases.ALIASES)
+    out = subprocess.run([str(d / "accelerate"), "env"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0 and "accelerate_hpc_test_amd" in out.stdout + out.stderr
+    out = subprocess.run([str(d / "accelerate-launch"), "--help"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0 and "num_processes" in out.stdout
+    assert aliases.listed(str(d))["accelerate-config"] == "installed"
+    foreign = tmp_path / "other"
+    foreign.mkdir()
+    (foreign / "accelerate").write_text("#!/bin/sh\necho upstream\n")
+    with pytest.raises(FileExistsError):
+        aliases.install(str(foreign))
+    assert aliases.remove(str(foreign)) == [] and (foreign / "accelerate").exists()
+    main(["aliases", "remove", "--dir", str(d)])
+    assert list(d.iterdir()) == []
