@@ -109,6 +109,68 @@ _even_batches = object()
 _use_seedable_sampler = object()
 
 
+
+
+def _delegate(path: str, settable: bool = False) -> property:
+    """A property reading (and, when `settable`, writing) `self.<owner>.<attr>` for `path` = "owner.attr" (or a plain
+    attribute name)."""
+    owner, _, attr = path.rpartition(".")
+
+    def _target(self):
+        return getattr(self, owner) if owner else self
+
+    def fget(self):
+        return getattr(_target(self), attr)
+
+    def fset(self, value):
+        setattr(_target(self), attr, value)
+
+    return property(fget, fset if settable else None, doc=f"`{path}`")
+
+class _CheckpointRotation:
+    """Automatic checkpoint naming of `ProjectConfiguration`: `<project_dir>/checkpoints/checkpoint_<k>` directories,
+    ordered by the number in their name, at most `total_limit` kept."""
+
+    _NUM = re.compile(r"(\d+)(?!.*\d)")
+
+    def __init__(self, project_configuration):
+        self.cfg = project_configuration
+        self.enabled = bool(project_configuration.automatic_checkpoint_naming)
+        self.root = os.path.join(project_configuration.project_dir or ".", "checkpoints")
+
+    def existing(self) -> list:
+        if not os.path.isdir(self.root):
+            return []
+        dirs = [os.path.join(self.root, d) for d in os.listdir(self.root)]
+        return sorted((d for d in dirs if self._NUM.search(os.path.basename(d))),
+                      key=lambda d: int(self._NUM.search(os.path.basename(d)).group(1)))
+
+    def prune_for_one_more(self):
+        limit = self.cfg.total_limit
+        have = self.existing()
+        if limit is not None and len(have) + 1 > limit:
+            drop = have[: len(have) + 1 - limit]
+            logger.warning(f"Deleting {len(drop)} checkpoints to make room for new checkpoint.")
+            for d in drop:
+                shutil.rmtree(d)
+
+    def next_dir(self, iteration: int) -> str:
+        out = os.path.join(self.root, f"checkpoint_{iteration}")
+        if os.path.exists(out):
+            raise ValueError(f"Checkpoint directory {out} ({iteration}) already exists. Please manually override "
+                             "`self.save_iteration` with what iteration to start with.")
+        return out
+
+    def latest(self) -> str:
+        have = self.existing()
+        if not have:
+            raise ValueError(f"No checkpoints found in {self.root}")
+        return have[-1]
+
+    @staticmethod
+    def custom_state_files(folder: str) -> list:
+        return [f for f in os.listdir(folder) if re.fullmatch(r"custom_checkpoint_\d+\.pkl", f)]
+
 class Accelerator:
     def __init__(
         self,
@@ -295,93 +357,41 @@ class Accelerator:
         check_os_kernel()
 
     # ============================================================================== properties
-    @property
-    def deepspeed_plugin(self):
-        return None
+    # Read-through views of the process state and the dataloader / project configurations (`_delegate`, module
+    # level); derived properties follow.
+    use_distributed = _delegate("state.use_distributed")
+    distributed_type = _delegate("state.distributed_type")
+    num_processes = _delegate("state.num_processes")
+    process_index = _delegate("state.process_index")
+    local_process_index = _delegate("state.local_process_index")
+    device = _delegate("state.device")
+    is_main_process = _delegate("state.is_main_process")
+    is_local_main_process = _delegate("state.is_local_main_process")
+    mixed_precision = _delegate("state.mixed_precision")
+    torch_device_mesh = _delegate("state.device_mesh")
+    split_batches = _delegate("dataloader_config.split_batches")
+    dispatch_batches = _delegate("dataloader_config.dispatch_batches")
+    even_batches = _delegate("dataloader_config.even_batches", settable=True)
+    use_seedable_sampler = _delegate("dataloader_config.use_seedable_sampler")
+    non_blocking = _delegate("dataloader_config.non_blocking")
+    use_stateful_dataloader = _delegate("dataloader_config.use_stateful_dataloader")
+    project_dir = _delegate("project_configuration.project_dir")
+    logging_dir = _delegate("project_configuration.logging_dir")
+    save_iteration = _delegate("project_configuration.iteration")
+    sync_gradients = _delegate("gradient_state.sync_gradients", settable=True)
+    fp8_backend = _delegate("_fp8_backend")
 
     @property
-    def use_distributed(self):
-        return self.state.use_distributed
+    def deepspeed_plugin(self):
+        return None  # DeepSpeed is not part of this build
 
     @property
     def multi_device(self):
         return self.use_distributed and self.distributed_type in (DistributedType.MULTI_GPU, DistributedType.FSDP)
 
     @property
-    def distributed_type(self):
-        return self.state.distributed_type
-
-    @property
-    def num_processes(self):
-        return self.state.num_processes
-
-    @property
-    def process_index(self):
-        return self.state.process_index
-
-    @property
-    def local_process_index(self):
-        return self.state.local_process_index
-
-    @property
-    def device(self):
-        return self.state.device
-
-    @property
-    def split_batches(self):
-        return self.dataloader_config.split_batches
-
-    @property
-    def dispatch_batches(self):
-        return self.dataloader_config.dispatch_batches
-
-    @property
-    def even_batches(self):
-        return self.dataloader_config.even_batches
-
-    @even_batches.setter
-    def even_batches(self, value: bool):
-        self.dataloader_config.even_batches = value
-
-    @property
-    def use_seedable_sampler(self):
-        return self.dataloader_config.use_seedable_sampler
-
-    @property
-    def non_blocking(self):
-        return self.dataloader_config.non_blocking
-
-    @property
-    def use_stateful_dataloader(self):
-        return self.dataloader_config.use_stateful_dataloader
-
-    @property
-    def project_dir(self):
-        return self.project_configuration.project_dir
-
-    @property
-    def logging_dir(self):
-        return self.project_configuration.logging_dir
-
-    @property
-    def save_iteration(self):
-        return self.project_configuration.iteration
-
-    @property
-    def is_main_process(self):
-        return self.state.is_main_process
-
-    @property
-    def is_local_main_process(self):
-        return self.state.is_local_main_process
-
-    @property
     def is_last_process(self):
         return self.process_index == self.num_processes - 1
-
-    @property
-    def mixed_precision(self):
-        return self.state.mixed_precision
 
     @property
     def is_fsdp2(self):
@@ -390,10 +400,6 @@ class Accelerator:
     @property
     def is_composable_parallelism_enabled(self):
         return self.is_fsdp2
-
-    @property
-    def torch_device_mesh(self):
-        return self.state.device_mesh
 
     @property
     def should_save_model(self):
@@ -428,24 +434,12 @@ class Accelerator:
         raise RuntimeError("Data parallelism sharding is not enabled. Please check your configuration.")
 
     @property
-    def fp8_backend(self):
-        return self._fp8_backend
-
-    @property
     def gradient_accumulation_steps(self):
         return self.gradient_state.num_steps
 
     @gradient_accumulation_steps.setter
     def gradient_accumulation_steps(self, gradient_accumulation_steps):
         self.gradient_state.plugin_kwargs.update({"num_steps": gradient_accumulation_steps})
-
-    @property
-    def sync_gradients(self):
-        return self.gradient_state.sync_gradients
-
-    @sync_gradients.setter
-    def sync_gradients(self, sync_gradients):
-        self.gradient_state.sync_gradients = sync_gradients
 
     @property
     def optimizer_step_was_skipped(self):
@@ -1125,129 +1119,88 @@ class Accelerator:
         self._load_model_state_pre_hook[handle.id] = hook
         return handle
 
+    # --- checkpoints: automatic naming / rotation lives in `_CheckpointRotation`, file names in checkpointing.py
+    def _split_for_checkpoint(self):
+        """(fsdp models, other models, engine-managed optimizers, other optimizers): FSDP-wrapped models and the
+        optimizers over their shard parameters are saved by utils/fsdp_utils.py (per-rank shards or a gathered full
+        state), everything else by checkpointing.py."""
+        from .parallel.fsdp import FullyShardedModule
+
+        fsdp = [(i, m) for i, m in enumerate(self._models) if isinstance(m, FullyShardedModule)]
+        plain = [m for m in self._models if not isinstance(m, FullyShardedModule)]
+        eng_opts, plain_opts = [], []
+        for i, opt in enumerate(self._optimizers):
+            managed = fsdp and getattr(opt.optimizer, "_acc_fsdp_engine", None) is not None
+            (eng_opts if managed else plain_opts).append((i, opt) if managed else opt)
+        return fsdp, plain, eng_opts, plain_opts
+
     def save_state(self, output_dir: str = None, safe_serialization: bool = True, **save_model_func_kwargs):
-        """Save model(s), optimizer(s), scheduler(s), dataloader positions, scaler and RNG states."""
-        if self.project_configuration.automatic_checkpoint_naming:
-            output_dir = os.path.join(self.project_dir, "checkpoints")
-        os.makedirs(output_dir, exist_ok=True)
-        if self.project_configuration.automatic_checkpoint_naming:
-            folders = [os.path.join(output_dir, folder) for folder in os.listdir(output_dir)]
-            if self.project_configuration.total_limit is not None and (len(folders) + 1 > self.project_configuration.total_limit) and self.is_main_process:
+        """Save model(s), optimizer(s), scheduler(s), dataloader positions, scaler, RNG and registered custom states.
+        With `ProjectConfiguration(automatic_checkpoint_naming=True)` the state goes to
+        `<project_dir>/checkpoints/checkpoint_<iteration>` and the oldest checkpoints beyond `total_limit` are pruned."""
+        from .utils.fsdp_utils import save_fsdp_model, save_fsdp_optimizer
 
-                def _inner(folder):
-                    return list(map(int, re.findall(r"[\/]?([0-9]+)(?=[^\/]*$)", folder)))[0]
-
-                folders.sort(key=_inner)
-                logger.warning(f"Deleting {len(folders) + 1 - self.project_configuration.total_limit} checkpoints to make room for new checkpoint.")
-                for folder in folders[: len(folders) + 1 - self.project_configuration.total_limit]:
-                    shutil.rmtree(folder)
-            output_dir = os.path.join(output_dir, f"checkpoint_{self.save_iteration}")
-            if os.path.exists(output_dir):
-                raise ValueError(f"Checkpoint directory {output_dir} ({self.save_iteration}) already exists. Please manually override `self.save_iteration` with what iteration to start with.")
+        rot = _CheckpointRotation(self.project_configuration)
+        if rot.enabled:
+            if self.is_main_process:
+                rot.prune_for_one_more()
+            output_dir = rot.next_dir(self.save_iteration)
             self.wait_for_everyone()
         os.makedirs(output_dir, exist_ok=True)
         logger.info(f"Saving current state to {output_dir}")
-        from .parallel.fsdp import FullyShardedModule
-        from .utils.fsdp_utils import save_fsdp_model, save_fsdp_optimizer
-
-        weights = []
-        fsdp_models = []
-        for i, model in enumerate(self._models):
-            if isinstance(model, FullyShardedModule):
-                save_fsdp_model(self.state.fsdp_plugin, self, model, output_dir, i)
-                fsdp_models.append(model)
-            else:
-                weights.append(self.get_state_dict(model, unwrap=False))
-        optimizers = []
-        for i, opt in enumerate(self._optimizers):
-            if fsdp_models and getattr(opt.optimizer, "_acc_fsdp_engine", None) is not None:
-                save_fsdp_optimizer(self.state.fsdp_plugin, self, opt, fsdp_models[0], output_dir, i)
-            else:
-                optimizers.append(opt)
-        schedulers = self._schedulers
-        dataloaders = self._dataloaders
+        fsdp, plain, eng_opts, plain_opts = self._split_for_checkpoint()
+        for i, model in fsdp:
+            save_fsdp_model(self.state.fsdp_plugin, self, model, output_dir, i)
+        for i, opt in eng_opts:
+            save_fsdp_optimizer(self.state.fsdp_plugin, self, opt, fsdp[0][1], output_dir, i)
+        weights = [self.get_state_dict(m, unwrap=False) for m in plain]
         for hook in self._save_model_state_pre_hook.values():
             hook(self._models, weights, output_dir)
-        save_location = save_accelerator_state(
-            output_dir,
-            weights,
-            optimizers,
-            schedulers,
-            dataloaders,
-            self.state.process_index,
-            self.step,
-            self.scaler,
-            save_on_each_node=self.project_configuration.save_on_each_node,
-            safe_serialization=safe_serialization,
-        )
+        node_kw = {"save_on_each_node": self.project_configuration.save_on_each_node}
+        location = save_accelerator_state(output_dir, weights, plain_opts, self._schedulers, self._dataloaders,
+                                          self.state.process_index, self.step, self.scaler,
+                                          safe_serialization=safe_serialization, **node_kw)
         for i, obj in enumerate(self._custom_objects):
-            save_custom_state(obj, output_dir, i, save_on_each_node=self.project_configuration.save_on_each_node)
+            save_custom_state(obj, output_dir, i, **node_kw)
         self.project_configuration.iteration += 1
-        return save_location
+        return location
 
     def load_state(self, input_dir: str = None, load_kwargs: dict | None = None, **load_model_func_kwargs):
+        """Restore what `save_state` wrote (the newest automatic checkpoint when `input_dir` is None)."""
+        from .utils.fsdp_utils import load_fsdp_model, load_fsdp_optimizer
+
         if input_dir is not None:
             input_dir = os.path.expanduser(input_dir)
             if not os.path.isdir(input_dir):
                 raise ValueError(f"Tried to find {input_dir} but folder does not exist")
-        elif self.project_configuration.automatic_checkpoint_naming:
-            input_dir = os.path.join(self.project_dir, "checkpoints")
-            folders = [os.path.join(input_dir, folder) for folder in os.listdir(input_dir)]
-
-            def _inner(folder):
-                return list(map(int, re.findall(r"[\/]?([0-9]+)(?=[^\/]*$)", folder)))[0]
-
-            folders.sort(key=_inner)
-            input_dir = folders[-1]
         else:
-            raise ValueError("No input_dir provided and automatic checkpoint naming is disabled.")
+            rot = _CheckpointRotation(self.project_configuration)
+            if not rot.enabled:
+                raise ValueError("No input_dir provided and automatic checkpoint naming is disabled.")
+            input_dir = rot.latest()
         logger.info(f"Loading states from {input_dir}")
-        from .parallel.fsdp import FullyShardedModule
-        from .utils.fsdp_utils import load_fsdp_model, load_fsdp_optimizer
-
-        models = []
-        fsdp_models = []
-        for i, model in enumerate(self._models):
-            if isinstance(model, FullyShardedModule):
-                load_fsdp_model(self.state.fsdp_plugin, self, model, input_dir, i)
-                fsdp_models.append(model)
-            else:
-                models.append(model)
-        optimizers = []
-        for i, opt in enumerate(self._optimizers):
-            if fsdp_models and getattr(opt.optimizer, "_acc_fsdp_engine", None) is not None:
-                load_fsdp_optimizer(self.state.fsdp_plugin, self, opt, fsdp_models[0], input_dir, i)
-            else:
-                optimizers.append(opt)
+        fsdp, plain, eng_opts, plain_opts = self._split_for_checkpoint()
+        for i, model in fsdp:
+            load_fsdp_model(self.state.fsdp_plugin, self, model, input_dir, i)
+        for i, opt in eng_opts:
+            load_fsdp_optimizer(self.state.fsdp_plugin, self, opt, fsdp[0][1], input_dir, i)
         for hook in self._load_model_state_pre_hook.values():
-            hook(models, input_dir)
+            hook(plain, input_dir)
         map_location = load_model_func_kwargs.pop("map_location", None)
-        if map_location is None:
+        if map_location is None:  # multi-GPU: optimizer state straight onto the device
             map_location = "on_device" if self.num_processes > 1 and self.device.type == "cuda" else "cpu"
-        override_attributes = load_accelerator_state(
-            input_dir,
-            [self.unwrap_model(m) for m in models],
-            optimizers,
-            self._schedulers,
-            self._dataloaders,
-            self.state.process_index,
-            self.scaler,
-            map_location,
-            load_kwargs,
-            **load_model_func_kwargs,
-        )
-        if "step" in override_attributes:
-            self.step = override_attributes["step"]
-        custom_checkpoints = [f for f in os.listdir(input_dir) if re.search(r"^custom_checkpoint_\d+\.pkl$", f) is not None]
-        if len(custom_checkpoints) != len(self._custom_objects):
-            err = (
-                f"Number of custom checkpoints in folder {input_dir} does not match the number of registered objects:"
-                f"\n\tFound checkpoints: {len(custom_checkpoints)}\n\tRegistered objects: {len(self._custom_objects)}\n"
-                "Please make sure to only load checkpoints from folders that were created with the same set of registered objects,"
-                "or avoid using `custom_checkpoint` in the filename for files in that same directory and load them in manually."
-            )
-            raise RuntimeError(err)
-        logger.info(f"Loading in {len(custom_checkpoints)} custom states")
+        overrides = load_accelerator_state(input_dir, [self.unwrap_model(m) for m in plain], plain_opts, self._schedulers,
+                                           self._dataloaders, self.state.process_index, self.scaler, map_location,
+                                           load_kwargs, **load_model_func_kwargs)
+        self.step = overrides.get("step", self.step)
+        found = _CheckpointRotation.custom_state_files(input_dir)
+        if len(found) != len(self._custom_objects):
+            raise RuntimeError(
+                f"Number of custom checkpoints in folder {input_dir} does not match the number of registered objects:\n"
+                f"\tFound checkpoints: {len(found)}\n\tRegistered objects: {len(self._custom_objects)}\n"
+                "Load checkpoints only from folders written with the same set of registered objects, or keep other "
+                "files named `custom_checkpoint_<k>.pkl` out of that folder.")
+        logger.info(f"Loading in {len(found)} custom states")
         for index, obj in enumerate(self._custom_objects):
             load_custom_state(obj, input_dir, index)
 
