@@ -549,83 +549,67 @@ class DataLoaderDispatcher(DataLoaderStateMixin, DataLoader):
         self.iteration = 0
         self._batches_yielded = 0
 
-    def _fetch_batches(self, iterator):
-        batches, batch = None, None
-        if self.state.process_index == 0:
-            try:
-                if self.split_batches:
-                    batch = next(iterator)
-                else:
-                    batches = []
-                    for _ in range(self.state.num_processes):
-                        batches.append(next(iterator))
-                    try:
-                        batch = concatenate(batches, dim=0)
-                    except RuntimeError as e:
-                        raise RuntimeError(
-                            "You can't use batches of different size with `dispatch_batches=True` or when using an "
-                            "`IterableDataset`. Either pass `dispatch_batches=False` and have each process fetch its "
-                            "own batch or pass `split_batches=True`."
-                        ) from e
-                batch_info = [get_data_structure(batch), False]
-            except StopIteration:
-                batch_info = [None, True]
-        else:
-            batch_info = [None, self._stop_iteration]
-        broadcast_object_list(batch_info)
-        self._stop_iteration = batch_info[1]
-        if self._stop_iteration:
-            if not self.split_batches and not self._drop_last:
-                if self.state.process_index == 0 and len(batches) > 0:
-                    batch = concatenate(batches, dim=0)
-                    batch_info = [get_data_structure(batch), False]
-                else:
-                    batch_info = [None, True]
-                broadcast_object_list(batch_info)
-        return batch, batch_info
+    _MIXED_SIZES = ("You can't use batches of different size with `dispatch_batches=True` or when using an `IterableDataset`. "
+                    "Either pass `dispatch_batches=False` and have each process fetch its own batch or pass "
+                    "`split_batches=True`.")
+
+    def _rank0_next(self, it):
+        """Rank 0: the next GLOBAL batch — one loader batch (split_batches), else `num_processes` loader batches
+        concatenated; a short final group is kept unless drop_last. None at the end."""
+        if self.split_batches:
+            return next(it, None)
+        group = []
+        for _ in range(self.state.num_processes):
+            b = next(it, None)
+            if b is None:
+                break
+            group.append(b)
+        if not group or (len(group) < self.state.num_processes and self._drop_last):
+            return None
+        try:
+            return concatenate(group, dim=0)
+        except RuntimeError as exc:
+            raise RuntimeError(self._MIXED_SIZES) from exc
+
+    def _next_global(self, it):
+        """Every rank: the next global batch on this device (rank 0's, broadcast: its structure as one object, then
+        its tensors), or None at the end."""
+        batch = self._rank0_next(it) if self.state.process_index == 0 else None
+        info = [get_data_structure(batch) if batch is not None else None]
+        broadcast_object_list(info)
+        if info[0] is None:
+            return None
+        if self.state.process_index != 0:
+            batch = initialize_tensors(info[0])
+        batch = send_to_device(batch, self.state.device, non_blocking=self._non_blocking)
+        return broadcast(batch, from_process=0)
 
     def __iter__(self):
         self.begin()
         self.set_epoch(self.iteration)
-        main_iterator = None
-        if self.state.process_index == 0:
-            main_iterator = super().__iter__()
-        stop_iteration = False
-        self._stop_iteration = False
-        first_batch = None
-        next_batch, next_batch_info = self._fetch_batches(main_iterator)
-        batch_index = 0
-        while not stop_iteration:
-            batch, batch_info = next_batch, next_batch_info
-            if self.state.process_index != 0:
-                batch = initialize_tensors(batch_info[0])
-            batch = send_to_device(batch, self.state.device, non_blocking=self._non_blocking)
-            batch = broadcast(batch, from_process=0)
-            if not self._drop_last and first_batch is None:
-                first_batch = self.slice_fn(
-                    batch, slice(0, self.state.num_processes), process_index=self.state.process_index, num_processes=self.state.num_processes
-                )
-            if batch is None:
-                raise ValueError(f"Batch does not contain any data ({batch}). At the end of all iterable data available before expected stop iteration.")
-            observed_batch_size = find_batch_size(batch)
-            batch_size = observed_batch_size // self.state.num_processes
-            stop_iteration = self._stop_iteration
-            if not stop_iteration:
-                next_batch, next_batch_info = self._fetch_batches(main_iterator)
-                if self._stop_iteration and next_batch_info[0] is None:
-                    stop_iteration = True
-            if not self._drop_last and stop_iteration and observed_batch_size % self.state.num_processes != 0:
-                batch = concatenate([batch, first_batch], dim=0)
-                batch_size += 1
-            data_slice = slice(self.state.process_index * batch_size, (self.state.process_index + 1) * batch_size)
-            batch = self.slice_fn(batch, data_slice, process_index=self.state.process_index, num_processes=self.state.num_processes)
-            if stop_iteration:
+        P, r = self.state.num_processes, self.state.process_index
+        it = super().__iter__() if r == 0 else None
+        head = None  # first P samples of the epoch: pad a final global batch that does not split evenly
+        cur, index = self._next_global(it), 0
+        while cur is not None:
+            nxt = self._next_global(it)  # one batch of look-ahead: the last batch is known when it is handed out
+            last = nxt is None
+            if not self._drop_last and head is None:
+                head = self.slice_fn(cur, slice(0, P), process_index=r, num_processes=P)
+            seen = find_batch_size(cur)
+            per = seen // P
+            if last and not self._drop_last and seen % P != 0:
+                cur = concatenate([cur, head], dim=0)
+                per += 1
+            mine = self.slice_fn(cur, slice(r * per, (r + 1) * per), process_index=r, num_processes=P)
+            if last:
                 self.end_of_dataloader = True
-                self.remainder = observed_batch_size
-            if batch_index >= self.skip_batches:
-                self._batches_yielded = batch_index + 1
-                yield batch
-            batch_index += 1
+                self.remainder = seen
+            if index >= self.skip_batches:
+                self._batches_yielded = index + 1
+                yield mine
+            index += 1
+            cur = nxt
         self.iteration += 1
         self.end()
 
@@ -687,6 +671,59 @@ def get_sampler(dataloader):
     return sampler
 
 
+def _maybe_seedable(sampler, use_seedable_sampler: bool, data_seed):
+    """A RandomSampler becomes a SeedableRandomSampler (epoch-seeded, identical on every rank) when requested."""
+    if isinstance(sampler, RandomSampler) and use_seedable_sampler:
+        return SeedableRandomSampler(data_source=sampler.data_source, replacement=sampler.replacement,
+                                     num_samples=sampler._num_samples,
+                                     generator=getattr(sampler, "generator", None) or torch.Generator(), data_seed=data_seed)
+    return sampler
+
+
+class _ShardPlan:
+    """What this rank iterates: the (possibly wrapped) dataset, the (possibly sharded) batch sampler, and the generator
+    every rank must keep in lock-step so shuffles agree."""
+
+    def __init__(self, dataset, batch_sampler, generator, sampler_is_batch_sampler):
+        self.dataset, self.batch_sampler = dataset, batch_sampler
+        self.generator, self.sampler_is_batch_sampler = generator, sampler_is_batch_sampler
+
+    @classmethod
+    def build(cls, dl, sampler, num_processes, process_index, split_batches, even_batches, dispatch_batches,
+              use_seedable_sampler):
+        iterable = isinstance(dl.dataset, IterableDataset)
+        as_batch_sampler = isinstance(dl.sampler, BatchSampler)
+        plan = cls(dl.dataset, None if iterable else dl.batch_sampler, None, as_batch_sampler)
+        if num_processes == 1 or dispatch_batches:
+            return plan  # one process, or rank 0 reads everything and dispatches
+        if iterable:
+            plan.generator = getattr(dl.dataset, "generator", None)
+            plan.dataset = IterableDatasetShard(dl.dataset, batch_size=dl.batch_size, drop_last=dl.drop_last,
+                                                num_processes=num_processes, process_index=process_index,
+                                                split_batches=split_batches)
+            return plan
+        if not use_seedable_sampler and hasattr(sampler, "generator"):
+            if sampler.generator is None:  # give the shuffle a generator every rank can seed identically
+                sampler.generator = torch.Generator()
+                sampler.generator.manual_seed(int(torch.empty((), dtype=torch.int64).random_().item()))
+            plan.generator = sampler.generator
+        plan.batch_sampler = BatchSamplerShard(dl.sampler if as_batch_sampler else dl.batch_sampler,
+                                               num_processes=num_processes, process_index=process_index,
+                                               split_batches=split_batches, even_batches=even_batches)
+        return plan
+
+
+def _rebuild_kwargs(dl, shard: "_ShardPlan", num_processes, split_batches, dispatch_batches) -> dict:
+    """The original loader's DataLoader arguments minus the ones the shard plan replaces; loaders without a batch
+    sampler (iterable datasets) keep batch_size / drop_last (per-process batch size with split_batches)."""
+    replaced = {"batch_size", "shuffle", "sampler", "batch_sampler", "drop_last"}
+    kw = {k: getattr(dl, k, default) for k, default in _PYTORCH_DATALOADER_KWARGS.items() if k not in replaced and hasattr(dl, k)}
+    if shard.batch_sampler is None:
+        kw["drop_last"] = dl.drop_last
+        kw["batch_size"] = dl.batch_size // num_processes if split_batches and not dispatch_batches else dl.batch_size
+    return kw
+
+
 def prepare_data_loader(
     dataloader: DataLoader,
     device: Optional[torch.device] = None,
@@ -733,99 +770,26 @@ def prepare_data_loader(
                 f"needs to be a round multiple of the number of processes ({num_processes})."
             )
 
-    new_dataset = dataloader.dataset
-    new_batch_sampler = dataloader.batch_sampler if not isinstance(new_dataset, IterableDataset) else None
-    sampler_is_batch_sampler = isinstance(dataloader.sampler, BatchSampler)
-    synchronized_generator = None
-
-    sampler = get_sampler(dataloader)
-    if isinstance(sampler, RandomSampler) and use_seedable_sampler:
-        sampler = SeedableRandomSampler(
-            data_source=sampler.data_source,
-            replacement=sampler.replacement,
-            num_samples=sampler._num_samples,
-            generator=getattr(sampler, "generator", None) or torch.Generator(),
-            data_seed=data_seed,
-        )
-
-    if num_processes != 1 and not dispatch_batches:
-        if isinstance(new_dataset, IterableDataset):
-            if getattr(dataloader.dataset, "generator", None) is not None:
-                synchronized_generator = dataloader.dataset.generator
-            new_dataset = IterableDatasetShard(
-                new_dataset,
-                batch_size=dataloader.batch_size,
-                drop_last=dataloader.drop_last,
-                num_processes=num_processes,
-                process_index=process_index,
-                split_batches=split_batches,
-            )
-        else:
-            if not use_seedable_sampler and hasattr(sampler, "generator"):
-                if sampler.generator is None:
-                    sampler.generator = torch.Generator()
-                    seed = int(torch.empty((), dtype=torch.int64).random_().item())
-                    sampler.generator.manual_seed(seed)
-                synchronized_generator = sampler.generator
-            batch_sampler = dataloader.sampler if sampler_is_batch_sampler else dataloader.batch_sampler
-            new_batch_sampler = BatchSamplerShard(
-                batch_sampler,
-                num_processes=num_processes,
-                process_index=process_index,
-                split_batches=split_batches,
-                even_batches=even_batches,
-            )
-
-    ignore_kwargs = ["batch_size", "shuffle", "sampler", "batch_sampler", "drop_last"]
-    if rng_types is not None and synchronized_generator is None and "generator" in rng_types:
-        rng_types = [r for r in rng_types if r != "generator"]
-    kwargs = {
-        k: getattr(dataloader, k, _PYTORCH_DATALOADER_KWARGS[k])
-        for k in _PYTORCH_DATALOADER_KWARGS
-        if k not in ignore_kwargs and hasattr(dataloader, k)
-    }
-    if new_batch_sampler is None:
-        kwargs["drop_last"] = dataloader.drop_last
-        kwargs["batch_size"] = (
-            dataloader.batch_size // num_processes if split_batches and not dispatch_batches else dataloader.batch_size
-        )
+    sampler = _maybe_seedable(get_sampler(dataloader), use_seedable_sampler, data_seed)
+    shard = _ShardPlan.build(dataloader, sampler, num_processes, process_index, split_batches, even_batches,
+                             dispatch_batches, use_seedable_sampler)
+    if rng_types is not None and shard.generator is None:
+        rng_types = [r for r in rng_types if r != "generator"]  # nothing to synchronise
+    kwargs = _rebuild_kwargs(dataloader, shard, num_processes, split_batches, dispatch_batches)
+    common = {"_drop_last": dataloader.drop_last, "_non_blocking": non_blocking}
     if dispatch_batches:
-        kwargs.pop("generator", None)
-        dataloader = DataLoaderDispatcher(
-            new_dataset,
-            split_batches=split_batches,
-            batch_sampler=new_batch_sampler,
-            _drop_last=dataloader.drop_last,
-            _non_blocking=non_blocking,
-            slice_fn=slice_fn_for_dispatch,
-            torch_device_mesh=torch_device_mesh,
-            **kwargs,
-        )
-    elif sampler_is_batch_sampler:
-        dataloader = DataLoaderShard(
-            new_dataset,
-            device=device if put_on_device else None,
-            sampler=new_batch_sampler,
-            batch_size=dataloader.batch_size,
-            rng_types=rng_types,
-            _drop_last=dataloader.drop_last,
-            _non_blocking=non_blocking,
-            synchronized_generator=synchronized_generator,
-            prefetch_to_device=prefetch_to_device,
-            **kwargs,
-        )
+        kwargs.pop("generator", None)  # only rank 0 draws samples
+        dataloader = DataLoaderDispatcher(shard.dataset, split_batches=split_batches, batch_sampler=shard.batch_sampler,
+                                          slice_fn=slice_fn_for_dispatch, torch_device_mesh=torch_device_mesh, **common,
+                                          **kwargs)
     else:
-        dataloader = DataLoaderShard(
-            new_dataset,
-            device=device if put_on_device else None,
-            batch_sampler=new_batch_sampler,
-            rng_types=rng_types,
-            synchronized_generator=synchronized_generator,
-            _drop_last=dataloader.drop_last,
-            _non_blocking=non_blocking,
-            prefetch_to_device=prefetch_to_device,
-            **kwargs,
-        )
+        shard_kw = {"device": device if put_on_device else None, "rng_types": rng_types,
+                    "synchronized_generator": shard.generator, "prefetch_to_device": prefetch_to_device}
+        if shard.sampler_is_batch_sampler:  # a BatchSampler passed as `sampler` stays in that slot
+            dataloader = DataLoaderShard(shard.dataset, sampler=shard.batch_sampler, batch_size=dataloader.batch_size,
+                                         **shard_kw, **common, **kwargs)
+        else:
+            dataloader = DataLoaderShard(shard.dataset, batch_sampler=shard.batch_sampler, **shard_kw, **common, **kwargs)
     if isinstance(sampler, SeedableRandomSampler) and use_seedable_sampler:
         dataloader.set_sampler(sampler)
     return dataloader

@@ -605,6 +605,57 @@ def check_fsdp_mixtral_expert_slots(steps: int = 2):
         assert torch.allclose(full[n].float(), q.float(), atol=5e-5), (n, (full[n] - q).abs().max())
 
 
+def check_dispatch_batches_matches_upstream():
+    """`prepare_data_loader(dispatch_batches=True)` (rank 0 reads, broadcasts, every rank slices) yields exactly the
+    batches of the upstream accelerate installed in the image, for map-style and iterable datasets, split / whole
+    batches, drop_last on/off and sizes that do not divide evenly; also the remainder bookkeeping."""
+    try:
+        import accelerate.data_loader as up_dl
+        from accelerate.state import PartialState as UpState
+    except ImportError:
+        return
+    from torch.utils.data import DataLoader, IterableDataset
+
+    from accelerate_hpc_test_amd.data_loader import prepare_data_loader
+    from accelerate_hpc_test_amd.state import PartialState
+
+    PartialState(cpu=True)
+    UpState(cpu=True)
+
+    class It(IterableDataset):
+        def __init__(self, n):
+            self.n = n
+
+        def __iter__(self):
+            return iter(torch.arange(self.n, dtype=torch.float32))
+
+    compared = 0
+    for iterable in (False, True):
+        for n in (7, 16, 19):
+            for bs in (2, 4):
+                for split in (False, True):
+                    for drop_last in (False, True):
+                        ds = It(n) if iterable else torch.arange(n, dtype=torch.float32)
+                        res = []
+                        for prep in (prepare_data_loader, up_dl.prepare_data_loader):
+                            dl = prep(DataLoader(ds, batch_size=bs, drop_last=drop_last), device=torch.device("cpu"),
+                                      put_on_device=True, dispatch_batches=True, split_batches=split)
+                            try:
+                                got = [b.tolist() for b in dl]
+                            except TypeError as exc:  # upstream broadcasts None for an empty final step here
+                                if prep is prepare_data_loader:
+                                    raise
+                                res.append(("upstream-error", str(exc)[:40]))
+                                continue
+                            res.append((got, dl.remainder))
+                        if res[1][0] == "upstream-error":
+                            continue  # no oracle for this configuration (ours must merely run, checked above)
+                        assert res[0][0] == res[1][0], (iterable, n, bs, split, drop_last, res)
+                        assert res[0][1] == res[1][1], ("remainder", iterable, n, bs, split, drop_last, res[0][1], res[1][1])
+                        compared += 1
+    assert compared >= 40, compared  # of 48 configurations
+
+
 def check_join_uneven_inputs():
     """Rank r gets 2 + r batches; with `join_uneven_inputs` the short rank shadows the long rank's all-reduces.
     Oracle: grads of each step = sum over active ranks / W (divide_by_initial_world_size)."""

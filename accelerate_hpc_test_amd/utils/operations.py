@@ -397,65 +397,57 @@ def _all_sizes(tensor) -> torch.Tensor:
     return gather(size)
 
 
+def _padded(tensor: torch.Tensor, dim: int, target: int, value, front: bool) -> torch.Tensor:
+    """`tensor` extended along `dim` to length `target` with `value` (before the data when `front`)."""
+    missing = target - tensor.shape[dim]
+    if missing <= 0:
+        return tensor
+    shape = list(tensor.shape)
+    shape[dim] = missing
+    filler = tensor.new_full(shape, value)
+    return torch.cat([filler, tensor] if front else [tensor, filler], dim=dim)
+
+
 @chained_operation
 def pad_across_processes(tensor, dim=0, pad_index=0, pad_first=False):
-    """Pad every tensor along `dim` to the largest size among processes so it can be gathered."""
+    """Pad every tensor along `dim` to the largest size any process holds (one shape all-gather per tensor), so the
+    results can be gathered; nested tensors and out-of-range `dim`s are returned as they are."""
 
-    def _pad_across_processes(tensor, dim=0, pad_index=0, pad_first=False):
-        if getattr(tensor, "is_nested", False):
+    def _one(t, dim=0, pad_index=0, pad_first=False):
+        if getattr(t, "is_nested", False):
             import warnings
 
             warnings.warn("Cannot pad nested tensors without more information. Leaving unprocessed.", CannotPadNestedTensorWarning)
-            return tensor
-        if dim >= len(tensor.shape) or dim < -len(tensor.shape):
-            return tensor
-        if dim < 0:
-            dim += len(tensor.shape)
-        sizes = _all_sizes(tensor).cpu()
-        max_size = int(sizes[:, dim].max())
-        if max_size == tensor.shape[dim]:
-            return tensor
-        old_size = tensor.shape
-        new_size = list(old_size)
-        new_size[dim] = max_size
-        new_tensor = tensor.new_zeros(tuple(new_size)) + pad_index
-        if pad_first:
-            indices = tuple(
-                slice(max_size - old_size[dim], max_size) if i == dim else slice(None) for i in range(len(new_size))
-            )
-        else:
-            indices = tuple(slice(0, old_size[dim]) if i == dim else slice(None) for i in range(len(new_size)))
-        new_tensor[indices] = tensor
-        return new_tensor
+            return t
+        nd = t.dim()
+        if not -nd <= dim < nd:
+            return t
+        dim %= nd
+        target = int(_all_sizes(t)[:, dim].max())
+        return _padded(t, dim, target, pad_index, pad_first)
 
-    return recursively_apply(
-        _pad_across_processes, tensor, error_on_other_type=True, dim=dim, pad_index=pad_index, pad_first=pad_first
-    )
+    return recursively_apply(_one, tensor, error_on_other_type=True, dim=dim, pad_index=pad_index, pad_first=pad_first)
+
+
+def _split_padding(batch_size: int, num_processes: int) -> int:
+    """Rows `pad_input_tensors` appends (the reference's rule, `utils/operations.py:700-717`, reproduced exactly):
+    num_processes minus the per-process share (or minus the batch when smaller than the process count), and when that
+    is < 1 while a remainder exists, remainder minus it."""
+    per = batch_size // num_processes
+    rest = batch_size - per * num_processes
+    pad = num_processes - (batch_size if per == 0 else per)
+    if pad < 1 and rest > pad:
+        pad = rest - pad
+    return pad
 
 
 def pad_input_tensors(tensor, batch_size, num_processes, dim=0):
-    """Pad the batch dimension so it divides evenly by `num_processes` (for `split_between_processes`)."""
+    """Zero-pad the batch dimension (for `split_between_processes` with `apply_padding`)."""
 
-    def _pad_input_tensors(tensor, batch_size, num_processes, dim=0):
-        remainder = batch_size // num_processes
-        last_inputs = batch_size - (remainder * num_processes)
-        if batch_size // num_processes == 0:
-            to_pad = num_processes - batch_size
-        else:
-            to_pad = num_processes - (batch_size // num_processes)
-        if last_inputs > to_pad & to_pad < 1:
-            to_pad = last_inputs - to_pad
-        old_size = tensor.shape
-        new_size = list(old_size)
-        new_size[0] = batch_size + to_pad
-        new_tensor = tensor.new_zeros(tuple(new_size))
-        indices = tuple(slice(0, old_size[dim]) if i == dim else slice(None) for i in range(len(new_size)))
-        new_tensor[indices] = tensor
-        return new_tensor
+    def _one(t, batch_size, num_processes, dim=0):
+        return _padded(t, dim, batch_size + _split_padding(batch_size, num_processes), 0, False)
 
-    return recursively_apply(
-        _pad_input_tensors, tensor, error_on_other_type=True, batch_size=batch_size, num_processes=num_processes, dim=dim
-    )
+    return recursively_apply(_one, tensor, error_on_other_type=True, batch_size=batch_size, num_processes=num_processes, dim=dim)
 
 
 def gather_tensor_shape(tensor):

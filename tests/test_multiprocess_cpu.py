@@ -11,6 +11,10 @@ def test_collective_ops():
     debug_launcher(td.check_ops, num_processes=2)
 
 
+def test_dispatch_batches_matches_upstream():
+    debug_launcher(td.check_dispatch_batches_matches_upstream, num_processes=2)
+
+
 def test_dataloader_sharding_and_gather_for_metrics():
     debug_launcher(td.check_dataloader_sharding, num_processes=2)
 
