@@ -1,0 +1,110 @@
+"""Data-loader sharding tables against the upstream `accelerate` installed in the image (skipped when absent): the
+reference pins these behaviours with hand-written tables (`/root/reference/tests/test_data_loader.py:98-441`); here
+every configuration of a grid is compared to upstream directly.
+
+  * BatchSamplerShard: dataset sizes x batch sizes x process counts x split_batches x even_batches x drop_last,
+    batches AND __len__ of every rank;
+  * IterableDatasetShard: the same grid for iterable datasets (incl. drop_last / split_batches);
+  * SkipBatchSampler / skip_first_batches / prepare_data_loader on one process (kwargs carried over, length);
+  * SeedableRandomSampler: same epoch-seeded permutation as upstream.
+"""
+
+import itertools
+
+import pytest
+import torch
+from torch.utils.data import BatchSampler, DataLoader, IterableDataset, SequentialSampler
+
+import accelerate_hpc_test_amd.data_loader as ours
+
+up = pytest.importorskip("accelerate.data_loader")
+
+
+def _shard_table(lib, n, bs, P, split, even, drop_last):
+    sampler = BatchSampler(SequentialSampler(range(n)), batch_size=bs, drop_last=drop_last)
+    rows = []
+    for r in range(P):
+        try:
+            s = lib.BatchSamplerShard(sampler, num_processes=P, process_index=r, split_batches=split, even_batches=even)
+            batches = list(s)
+            try:
+                length = len(s)
+            except Exception as exc:  # noqa: BLE001 - the error itself is part of the behaviour
+                length = type(exc).__name__
+            rows.append((batches, length))
+        except Exception as exc:  # noqa: BLE001
+            rows.append(type(exc).__name__)
+    return rows
+
+
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("split", [False, True])
+def test_batch_sampler_shard_table_matches_upstream(P, split):
+    checked = 0
+    for n, bs, even, drop_last in itertools.product(range(0, 41, 3), (1, 2, 3, 4, 8), (True, False), (False, True)):
+        if split and bs % P != 0:
+            continue  # upstream refuses split batches that do not divide (both raise; compared below anyway)
+        a = _shard_table(ours, n, bs, P, split, even, drop_last)
+        b = _shard_table(up, n, bs, P, split, even, drop_last)
+        assert a == b, (n, bs, P, split, even, drop_last)
+        checked += 1
+    assert checked > 50
+
+
+class _Range(IterableDataset):
+    def __init__(self, n):
+        self.n = n
+
+    def __iter__(self):
+        return iter(range(self.n))
+
+
+@pytest.mark.parametrize("P", [1, 2, 3, 4])
+def test_iterable_dataset_shard_table_matches_upstream(P):
+    for n, bs, split, drop_last in itertools.product(range(0, 30, 2), (1, 2, 4), (False, True), (False, True)):
+        if split and bs % P != 0:
+            continue
+        for r in range(P):
+            a = list(ours.IterableDatasetShard(_Range(n), batch_size=bs, drop_last=drop_last, num_processes=P,
+                                               process_index=r, split_batches=split))
+            b = list(up.IterableDatasetShard(_Range(n), batch_size=bs, drop_last=drop_last, num_processes=P,
+                                             process_index=r, split_batches=split))
+            assert a == b, (n, bs, P, r, split, drop_last)
+
+
+def test_skip_helpers_match_upstream():
+    for n, bs, skip in itertools.product((10, 17), (2, 3), (0, 1, 3)):
+        sampler = BatchSampler(SequentialSampler(range(n)), batch_size=bs, drop_last=False)
+        a, b = ours.SkipBatchSampler(sampler, skip), up.SkipBatchSampler(sampler, skip)
+        assert list(a) == list(b) and len(a) == len(b)
+        dl = DataLoader(list(range(n)), batch_size=bs)
+        x = [t.tolist() for t in ours.skip_first_batches(dl, skip)]
+        y = [t.tolist() for t in up.skip_first_batches(dl, skip)]
+        assert x == y, (n, bs, skip)
+
+
+def test_seedable_sampler_permutations_match_upstream():
+    for seed, epoch in itertools.product((0, 7), (0, 1, 5)):
+        a = ours.SeedableRandomSampler(data_source=range(23), generator=torch.Generator(), data_seed=seed)
+        b = up.SeedableRandomSampler(data_source=range(23), generator=torch.Generator(), data_seed=seed)
+        a.set_epoch(epoch)
+        b.set_epoch(epoch)
+        assert list(a) == list(b), (seed, epoch)
+
+
+def test_prepare_single_process_matches_upstream():
+    from accelerate.state import PartialState as UpState
+
+    from accelerate_hpc_test_amd.state import PartialState
+
+    PartialState(cpu=True)
+    UpState(cpu=True)
+    for n, bs, drop_last, shuffle in itertools.product((9, 16), (2, 4), (False, True), (False, True)):
+        g1, g2 = torch.Generator().manual_seed(3), torch.Generator().manual_seed(3)
+        dl1 = DataLoader(list(range(n)), batch_size=bs, drop_last=drop_last, shuffle=shuffle, generator=g1, num_workers=0)
+        dl2 = DataLoader(list(range(n)), batch_size=bs, drop_last=drop_last, shuffle=shuffle, generator=g2, num_workers=0)
+        a = ours.prepare_data_loader(dl1, num_processes=1, process_index=0, use_seedable_sampler=shuffle)
+        b = up.prepare_data_loader(dl2, num_processes=1, process_index=0, use_seedable_sampler=shuffle)
+        assert len(a) == len(b)
+        assert [t.tolist() for t in a] == [t.tolist() for t in b], (n, bs, drop_last, shuffle)
+        assert a.total_batch_size == b.total_batch_size and a.total_dataset_length == b.total_dataset_length
