@@ -43,6 +43,7 @@ void fp8_gemm_select(int64_t variant, int64_t group_m);
 void grouped_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor out, torch::Tensor seg, int64_t mode, torch::Tensor sa,
                   torch::Tensor sb, double smul, bool accumulate);
 torch::Tensor batched_transpose(torch::Tensor x);
+void attn_debug_mode(int64_t mode);
 // small_allreduce.hip
 std::tuple<int64_t, pybind11::bytes> sar_create(int64_t rank, int64_t world, int64_t max_bytes);
 void sar_open(int64_t id, std::vector<std::string> handles);
@@ -88,6 +89,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("u8_transpose", &u8_transpose);
   m.def("grouped_gemm", &grouped_gemm);
   m.def("batched_transpose", &batched_transpose);
+  m.def("attn_debug_mode", &attn_debug_mode);
   m.def("sar_create", &sar_create);
   m.def("sar_open", &sar_open);
   m.def("sar_link_local", &sar_link_local);

@@ -118,6 +118,45 @@ struct Stage {
   }
 };
 
+// LDS-DMA staging of a ROWS x 128 bf16 tile of a token-strided [S, ..., 128] tensor into the dual image: buffer_load
+// ... lds (no VGPR round trip, no ds_write), one 1-KiB piece = 4 image rows per wave-instruction, NW waves share the
+// ROWS / 4 pieces. The DMA writes lane-linearly (lane l -> row 4p + l / 16, physical chunk l % 16), so each lane
+// fetches the LOGICAL chunk that img_off places there: the swizzle is an XOR, its own inverse. The descriptor covers
+// the head's column of the whole sequence; the tile's first row rides in soffset.
+__device__ __forceinline__ int img_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+
+template <int ROWS, int NW>
+struct TileDMA {
+  static constexpr int kPer = ROWS / 4 / NW;  // pieces per wave
+  unsigned voff[kPer];
+  int first;  // this wave's first piece (wave-uniform)
+  __device__ __forceinline__ void init(int wave, int lane, int ts_bytes) {
+    first = __builtin_amdgcn_readfirstlane(wave) * kPer;
+#pragma unroll
+    for (int t = 0; t < kPer; ++t) {
+      const int row = 4 * (first + t) + (lane >> 4), pc = lane & 15;
+      voff[t] = (unsigned)(row * ts_bytes + ((pc ^ img_swz(row)) << 4));
+    }
+  }
+  __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, int row0, int ts_bytes, char* img) const {
+    const int so = row0 * ts_bytes;
+#pragma unroll
+    for (int t = 0; t < kPer; ++t)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, img + (first + t) * 1024, 16, voff[t], so, 0, 0);
+  }
+};
+
+// Buffer descriptor over one head's [S, 128] column of a token-strided tensor (the range check bounds every DMA).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t head_rsrc(const bf16_t* base, int S, long ts) {
+  const long bytes = (long)S * ts * 2;
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)(bytes > 0x7fffffffL ? 0x7fffffffL : bytes), 0x00020000);
+}
+
+__device__ __forceinline__ void wait_dma_and_sync() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA landed ...
+  __syncthreads();                                   // ... and every wave's, and every wave is done reading
+}
+
 struct FwdParams {
   const bf16_t *q, *k, *v;
   long q_ts, k_ts, v_ts, q_bs, k_bs, v_bs;
@@ -130,8 +169,10 @@ struct FwdParams {
 
 template <bool CAUSAL>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(FwdParams p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+  // K / V tiles of 64 keys, double buffered; one static object per buffer so hipcc sees that the DMA into one never
+  // feeds the ds_reads of the other (no vmcnt(0) before every read)
   constexpr int kTile = 64 * kRow;  // 16 KB per operand image
+  __shared__ __attribute__((aligned(1024))) char k0s[kTile], v0s[kTile], k1s[kTile], v1s[kTile];
   const int nqt = p.S / 128;
   // grid = (Hq, S/128, B): heads vary fastest, so the heaviest causal tiles of EVERY head are dispatched first
   const int qt = CAUSAL ? (nqt - 1 - (int)blockIdx.y) : (int)blockIdx.y;
@@ -153,21 +194,20 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(FwdParams p) {
   float m = -INFINITY, l = 0.f;
   const int n_kt = CAUSAL ? (qt + 1) * 2 : p.S / 64;
 
-  Stage<64> sk, sv;
-  sk.load(kb_, p.k_ts, 0, tid);
-  sv.load(vb_, p.v_ts, 0, tid);
-  sk.store(smem, tid);
-  sv.store(smem + kTile, tid);
-  __syncthreads();
+  TileDMA<64, 4> dk, dv_;
+  const int kts = (int)(p.k_ts * 2), vts = (int)(p.v_ts * 2);
+  dk.init(wave, lane, kts);
+  dv_.init(wave, lane, vts);
+  const auto krs = head_rsrc(kb_, p.S, p.k_ts), vrs = head_rsrc(vb_, p.S, p.v_ts);
+  dk.issue(krs, 0, kts, k0s);
+  dv_.issue(vrs, 0, vts, v0s);
+  wait_dma_and_sync();
 
-  for (int kt = 0; kt < n_kt; ++kt) {
+  auto tile = [&](int kt, const char* k_img, const char* v_img, char* nk, char* nv) {
     const int k0 = kt * 64;
-    char* k_img = smem + (kt & 1) * 2 * kTile;
-    char* v_img = k_img + kTile;
-    const bool more = kt + 1 < n_kt;
-    if (more) {
-      sk.load(kb_, p.k_ts, k0 + 64, tid);
-      sv.load(vb_, p.v_ts, k0 + 64, tid);
+    if (kt + 1 < n_kt) {  // next tile's DMA overlaps this tile's MFMAs
+      dk.issue(krs, k0 + 64, kts, nk);
+      dv_.issue(vrs, k0 + 64, vts, nv);
     }
     if (!CAUSAL || k0 <= qw0 + 31) {
       f32x16 sc[2];
@@ -227,12 +267,14 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(FwdParams p) {
 #pragma unroll
           for (int s2 = 0; s2 < 2; ++s2) o[d] = mfma(tr_frag(v_img, kb * 32 + 16 * s2, d, lane), pb[kb][s2], o[d]);
     }
-    if (more) {
-      char* nk = smem + ((kt + 1) & 1) * 2 * kTile;
-      sk.store(nk, tid);
-      sv.store(nk + kTile, tid);
-    }
-    __syncthreads();
+    wait_dma_and_sync();
+  };
+  for (int kt = 0; kt < n_kt; kt += 2) {
+    tile(kt, k0s, v0s, k1s, v1s);
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + 1 >= n_kt) break;
+    tile(kt + 1, k1s, v1s, k0s, v0s);
+    __builtin_amdgcn_sched_barrier(0);
   }
   l += __shfl_xor(l, 32, 64);
   const float inv = 1.f / l;
@@ -277,8 +319,8 @@ struct BwdParams {
 
 template <bool CAUSAL>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(BwdParams p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int kTile = 64 * kRow;
+  __shared__ __attribute__((aligned(1024))) char k0s[kTile], v0s[kTile], k1s[kTile], v1s[kTile];  // as in the forward
   const int nqt = p.S / 128;
   const int qt = CAUSAL ? (nqt - 1 - (int)blockIdx.y) : (int)blockIdx.y;  // grid (Hq, S/128, B), heavy first
   const int h = xcd_head(blockIdx.x, p.Hq), b = blockIdx.z;
@@ -304,23 +346,25 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(BwdParams p) {
   for (int d = 0; d < 4; ++d) zero(dq[d]);
   const int n_kt = CAUSAL ? (qt + 1) * 2 : p.S / 64;
 
-  Stage<64> sk, sv;
-  sk.load(kb_, p.k_ts, 0, tid);
-  sv.load(vb_, p.v_ts, 0, tid);
-  sk.store(smem, tid);
-  sv.store(smem + kTile, tid);
-  __syncthreads();
+  TileDMA<64, 4> dk, dv_;
+  const int kts = (int)(p.k_ts * 2), vts = (int)(p.v_ts * 2);
+  dk.init(wave, lane, kts);
+  dv_.init(wave, lane, vts);
+  const auto krs = head_rsrc(kb_, p.S, p.k_ts), vrs = head_rsrc(vb_, p.S, p.v_ts);
+  dk.issue(krs, 0, kts, k0s);
+  dv_.issue(vrs, 0, vts, v0s);
+  wait_dma_and_sync();
 
-  for (int kt = 0; kt < n_kt; ++kt) {
+  auto tile = [&](int kt, const char* k_img, const char* v_img, char* nk, char* nv) {
     const int k0 = kt * 64;
-    char* k_img = smem + (kt & 1) * 2 * kTile;
-    char* v_img = k_img + kTile;
-    const bool more = kt + 1 < n_kt;
-    if (more) {
-      sk.load(kb_, p.k_ts, k0 + 64, tid);
-      sv.load(vb_, p.v_ts, k0 + 64, tid);
+    if (kt + 1 < n_kt) {
+      dk.issue(krs, k0 + 64, kts, nk);
+      dv_.issue(vrs, k0 + 64, vts, nv);
     }
-    if (!CAUSAL || k0 <= qw0 + 31) {
+    int ln = lane;  // opaque lane id: keeps the per-tile LDS offsets from being hoisted (see the dK / dV kernel)
+    asm volatile("" : "+v"(ln));
+    const int r = ln & 31, hf = ln >> 5;
+    if (CAUSAL ? k0 <= qw0 + 31 : ln >= 0) {
       v8bf dsb[2][2];
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
@@ -349,14 +393,16 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(BwdParams p) {
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) dq[d] = mfma(tr_frag(k_img, kb * 32 + 16 * s2, d, lane), dsb[kb][s2], dq[d]);
+          for (int s2 = 0; s2 < 2; ++s2) dq[d] = mfma(tr_frag(k_img, kb * 32 + 16 * s2, d, ln), dsb[kb][s2], dq[d]);
     }
-    if (more) {
-      char* nk = smem + ((kt + 1) & 1) * 2 * kTile;
-      sk.store(nk, tid);
-      sv.store(nk + kTile, tid);
-    }
-    __syncthreads();
+    wait_dma_and_sync();
+  };
+  for (int kt = 0; kt < n_kt; kt += 2) {
+    tile(kt, k0s, v0s, k1s, v1s);
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + 1 >= n_kt) break;
+    tile(kt + 1, k1s, v1s, k0s, v0s);
+    __builtin_amdgcn_sched_barrier(0);
   }
   bf16_t* out = p.dq + b * p.dq_bs + (long)h * kD + (long)(qw0 + r) * p.dq_ts;
 #pragma unroll
@@ -376,13 +422,18 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(BwdParams p) {
 // of every 64-query slice. K and V stay in LDS for the whole sweep (dual images, row reads for S = Q K^T and
 // dP = dO V^T); Q / dO slices (+ lse, delta) are double buffered with the async-stage split (global loads issued
 // before the MFMAs, LDS writes after them). The two query halves' partial dK / dV meet in LDS at the end.
-template <bool CAUSAL>
+// DBG (diagnostic builds, selected by attn_debug_mode; results are NOT valid unless DBG == 0): 1 = every Q / dO
+// fetch reads slice 0 (cache-hot: removes HBM/L2 latency), 2 = no prefetch DMA at all (stale slices), 3 = both.
+template <bool CAUSAL, int DBG = 0>
 __global__ __launch_bounds__(512) void attn_bwd_dkdv_kernel(BwdParams p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int kSlice = 64;
-  constexpr int kImg = kSlice * kRow;              // 16 KB: one 64-row Q or dO image
-  constexpr int kKV = 128 * kRow;                  // 32 KB: the key tile's K (or V) image
-  constexpr int kBuf = 2 * kImg + 2 * kSlice * 4;  // Q, dO images + lse, delta
+  constexpr int kImg = kSlice * kRow;  // 16 KB: one 64-row Q or dO image
+  constexpr int kKV = 128 * kRow;      // 32 KB: the key tile's K (or V) image
+  // K | V of the key tile (one object: the epilogue reuses it as one 64 KB reduction buffer), and two slice buffers
+  // (Q image, dO image, lse[64] | delta[64]) filled by LDS-DMA, one static object each (see TileDMA)
+  __shared__ __attribute__((aligned(1024))) char smem[2 * kKV];
+  __shared__ __attribute__((aligned(1024))) char qs0[kImg], ds0[kImg], qs1[kImg], ds1[kImg];
+  __shared__ __attribute__((aligned(16))) float ls0[2 * kSlice], ls1[2 * kSlice];
   // grid.x = Hkv * nkt with the kv head fastest: key tile 0 (the most causal work) of every head is dispatched first,
   // and all tiles of one head share blockIdx.x % 8 (one XCD under round-robin dispatch), whose L2 then serves that
   // head's Q / dO stream to all of them.
@@ -393,7 +444,6 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_kernel(BwdParams p) {
   const int kw0 = kt * 128 + kr;
   char* k_img = smem;
   char* v_img = smem + kKV;
-  char* bufs = smem + 2 * kKV;
   {
     Stage<128, 512> sk, sv;
     sk.load(p.k + b * p.k_bs + (long)kh * kD, p.k_ts, kt * 128, tid);
@@ -405,50 +455,55 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_kernel(BwdParams p) {
 #pragma unroll
   for (int d = 0; d < 4; ++d) { zero(dk[d]); zero(dv[d]); }
 
-  const int qs0 = CAUSAL ? kt * 2 : 0;  // first 64-query slice that can see this key tile
-  const int per = p.S / kSlice - qs0;   // slices per query head
+  const int qs0_ = CAUSAL ? kt * 2 : 0;  // first 64-query slice that can see this key tile
+  const int per = p.S / kSlice - qs0_;   // slices per query head
   const int n_it = grp * per;
-  Stage<kSlice, 512> sq, sd;
-  float st = 0.f;
-  auto issue = [&](int it) {
-    const int h = kh * grp + it / per, q0 = (qs0 + it % per) * kSlice;
-    sq.load(p.q + b * p.q_bs + (long)h * kD, p.q_ts, q0, tid);
-    sd.load(p.dout + b * p.do_bs + (long)h * kD, p.do_ts, q0, tid);
-    const long row = ((long)b * p.Hq + h) * p.S + q0;
-    // row constants, pre-negated: they seed the S and dP accumulators (S' = Q K^T - LSE/scale, dP' = dO V^T - delta)
-    if (tid < kSlice) st = -p.lse[row + tid] * p.inv_scale;
-    else if (tid < 2 * kSlice) st = -p.delta[row + tid - kSlice];
+  // Q / dO slices by LDS-DMA (2 pieces per wave per operand); lse / delta rows by two 256-B DMAs (waves 0 and 1),
+  // raw values: the S / dP accumulators are seeded with -lse/scale and -delta at use
+  TileDMA<kSlice, 8> dmq, dmd;
+  const int qts = (int)(p.q_ts * 2), dts = (int)(p.do_ts * 2);
+  dmq.init(wave, lane, qts);
+  dmd.init(wave, lane, dts);
+  const long rc_bytes = (long)gridDim.y * p.Hq * p.S * 4;
+  const int rc = (int)(rc_bytes > 0x7fffffffL ? 0x7fffffffL : rc_bytes);
+  const auto lrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.lse, (short)0, rc, 0x00020000);
+  const auto drs = __builtin_amdgcn_make_buffer_rsrc((void*)p.delta, (short)0, rc, 0x00020000);
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  auto issue = [&](int it, char* qi, char* di, float* ld) {
+    if (DBG & 1) it = 0;
+    const int h = kh * grp + it / per, q0 = (qs0_ + it % per) * kSlice;
+    const bf16_t* qh_ = p.q + b * p.q_bs + (long)h * kD;
+    const bf16_t* dh_ = p.dout + b * p.do_bs + (long)h * kD;
+    dmq.issue(head_rsrc(qh_, p.S, p.q_ts), q0, qts, qi);
+    dmd.issue(head_rsrc(dh_, p.S, p.do_ts), q0, dts, di);
+    const int row = (int)((((long)b * p.Hq + h) * p.S + q0) * 4);
+    if (wv == 0) __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, ld, 4, lane * 4, row, 0, 0);
+    else if (wv == 1) __builtin_amdgcn_raw_ptr_buffer_load_lds(drs, ld + kSlice, 4, lane * 4, row, 0, 0);
   };
-  auto commit = [&](int buf) {
-    char* base = bufs + buf * kBuf;
-    sq.store(base, tid);
-    sd.store(base + kImg, tid);
-    if (tid < 2 * kSlice) reinterpret_cast<float*>(base + 2 * kImg)[tid] = st;  // lse [0, 64), delta [64, 128)
-  };
-  issue(0);
-  commit(0);
-  __syncthreads();
+  issue(0, qs0, ds0, ls0);
+  wait_dma_and_sync();
   // The second-dispatched half loses VALU arbitration to its SIMD partner on every segment; one static priority
   // bump before the loop (no per-segment flips) evens the two halves out.
   if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
 
-  for (int it = 0; it < n_it; ++it) {
-    const int cur = it & 1;
-    const char* q_img = bufs + cur * kBuf;
-    const char* d_img = q_img + kImg;
-    const float* lse_s = reinterpret_cast<const float*>(q_img + 2 * kImg);
+  // non-causal: the lane id is made opaque once per slice (lv), so the lane-derived LDS fragment offsets are
+  // recomputed per slice instead of being hoisted out of the loop for both buffers and held live (96 VGPRs of spill).
+  // The causal kernel fits the hoisted offsets (256 VGPRs, ~7% faster than recomputing them), so lv stays `lane` there.
+  int lv = lane;
+  auto slice = [&](int it, const char* q_img, const char* d_img, const float* lse_s, char* nq, char* nd, float* nl) {
     const float* dlt_s = lse_s + kSlice;
-    const bool more = it + 1 < n_it;
-    if (more) issue(it + 1);
-    const int q0 = (qs0 + it % per) * kSlice;
-    if (!CAUSAL || q0 + qh + 31 >= kw0) {
+    if (it + 1 < n_it && !(DBG & 2)) issue(it + 1, nq, nd, nl);  // next slice's DMA overlaps this slice's MFMAs
+    const int q0 = (qs0_ + it % per) * kSlice;
+    if (CAUSAL ? q0 + qh + 31 >= kw0 : lv >= 0) {  // non-causal: an opaque always-true test keeps the block shape
+      const int r = lv & 31, hf = lv >> 5;
       f32x16 sc, dp;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {  // rows qh + 8g + 4hf .. +3 of the slice: one 16-B LDS read per constant
         const float4 l4 = *reinterpret_cast<const float4*>(lse_s + qh + 8 * g + 4 * hf);
         const float4 d4 = *reinterpret_cast<const float4*>(dlt_s + qh + 8 * g + 4 * hf);
-        sc[4 * g] = l4.x; sc[4 * g + 1] = l4.y; sc[4 * g + 2] = l4.z; sc[4 * g + 3] = l4.w;
-        dp[4 * g] = d4.x; dp[4 * g + 1] = d4.y; dp[4 * g + 2] = d4.z; dp[4 * g + 3] = d4.w;
+        const float ni = -p.inv_scale;
+        sc[4 * g] = l4.x * ni; sc[4 * g + 1] = l4.y * ni; sc[4 * g + 2] = l4.z * ni; sc[4 * g + 3] = l4.w * ni;
+        dp[4 * g] = -d4.x; dp[4 * g + 1] = -d4.y; dp[4 * g + 2] = -d4.z; dp[4 * g + 3] = -d4.w;
       }
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
@@ -466,17 +521,27 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_kernel(BwdParams p) {
         dp[i] = pv * dp[i];
       }
       const v8bf pb0 = pack8(sc, 0), pb1 = pack8(sc, 1);
-      const v8bf ds0 = pack8(dp, 0), ds1 = pack8(dp, 1);
+      const v8bf ds0_ = pack8(dp, 0), ds1_ = pack8(dp, 1);
+      // keep the transposed-fragment reads of the dV / dK phase from being hoisted into the S / dP phase (without the
+      // causal branch hipcc otherwise pipelines them early and spills)
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
-        dv[d] = mfma(tr_frag(d_img, qh, d, lane), pb0, dv[d]);
-        dv[d] = mfma(tr_frag(d_img, qh + 16, d, lane), pb1, dv[d]);
-        dk[d] = mfma(tr_frag(q_img, qh, d, lane), ds0, dk[d]);
-        dk[d] = mfma(tr_frag(q_img, qh + 16, d, lane), ds1, dk[d]);
+        dv[d] = mfma(tr_frag(d_img, qh, d, lv), pb0, dv[d]);
+        dv[d] = mfma(tr_frag(d_img, qh + 16, d, lv), pb1, dv[d]);
+        dk[d] = mfma(tr_frag(q_img, qh, d, lv), ds0_, dk[d]);
+        dk[d] = mfma(tr_frag(q_img, qh + 16, d, lv), ds1_, dk[d]);
       }
     }
-    if (more) commit(cur ^ 1);
-    __syncthreads();
+    wait_dma_and_sync();
+  };
+  for (int it = 0; it < n_it; it += 2) {  // unrolled by the two static slice buffers; no motion between the halves
+    if (!CAUSAL) asm volatile("" : "+v"(lv));
+    slice(it, qs0, ds0, ls0, qs1, ds1, ls1);
+    __builtin_amdgcn_sched_barrier(0);
+    if (it + 1 >= n_it) break;
+    slice(it + 1, qs1, ds1, ls1, qs0, ds0, ls0);
+    __builtin_amdgcn_sched_barrier(0);
   }
   __builtin_amdgcn_s_setprio(0);
 
@@ -519,17 +584,24 @@ void check_qkv(const torch::Tensor& t, const char* name) {
   TORCH_CHECK((reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0, name, " must be 16-byte aligned");
 }
 
-constexpr size_t kFwdSmem = 2 * 2 * 64 * kRow;                    // 64 KB
-constexpr size_t kDqSmem = 2 * 2 * 64 * kRow;                     // 64 KB
-constexpr size_t kDkdvSmem = 2 * 128 * kRow + 2 * (2 * 64 * kRow + 2 * 64 * 4);  // 129 KB
-
-template <typename K>
-void allow_smem(K kernel, size_t bytes) {
-  // > 64 KB of dynamic LDS must be opted into explicitly (MI355X has 160 KB per CU).
-  hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-}
+// Explicit instantiations: hipcc emits the host launch stub of only the first instantiation a launch chain names for
+// kernels with function-scope static LDS; naming every variant here makes each stub definite.
+template __global__ void attn_fwd_kernel<true>(FwdParams);
+template __global__ void attn_fwd_kernel<false>(FwdParams);
+template __global__ void attn_bwd_dq_kernel<true>(BwdParams);
+template __global__ void attn_bwd_dq_kernel<false>(BwdParams);
+template __global__ void attn_bwd_dkdv_kernel<true, 0>(BwdParams);
+template __global__ void attn_bwd_dkdv_kernel<true, 1>(BwdParams);
+template __global__ void attn_bwd_dkdv_kernel<true, 2>(BwdParams);
+template __global__ void attn_bwd_dkdv_kernel<true, 3>(BwdParams);
+template __global__ void attn_bwd_dkdv_kernel<false, 0>(BwdParams);
 
 }  // namespace
+
+// Diagnostic switch for the causal backward (tools/bench_attn.py --dbg): bit 3 = run the dQ kernel, bit 2 = run the
+// normal dK/dV kernel, bits 0-1 = run a dK/dV DBG variant instead. 0 = normal operation.
+static int g_attn_dbg = 0;
+void attn_debug_mode(int64_t mode) { g_attn_dbg = (int)mode; }
 
 // q: [B, S, Hq, D], k/v: [B, S, Hkv, D] (views into a fused QKV buffer are fine). Returns (O [B,S,Hq,D], LSE [B,Hq,S]).
 std::vector<torch::Tensor> flash_attn_fwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, double softmax_scale,
@@ -549,8 +621,8 @@ std::vector<torch::Tensor> flash_attn_fwd(torch::Tensor q, torch::Tensor k, torc
               lse.data_ptr<float>(), S, Hq, Hkv, (float)(softmax_scale * kLog2e)};
   dim3 grid(Hq, S / 128, B);
   auto stream = at::hip::getCurrentHIPStream();
-  if (causal) hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(256), kFwdSmem, stream, p);
-  else hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(256), kFwdSmem, stream, p);
+  if (causal) hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(256), 0, stream, p);
+  else hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(256), 0, stream, p);
   return {o, lse};
 }
 
@@ -586,18 +658,21 @@ void flash_attn_bwd(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch:
               reinterpret_cast<bf16_t*>(dk.data_ptr()), reinterpret_cast<bf16_t*>(dv.data_ptr()), dq.stride(1),
               dq.stride(0), dk.stride(1), dk.stride(0), dv.stride(1), dv.stride(0), S, Hq, Hkv,
               (float)(softmax_scale * kLog2e), (float)softmax_scale, (float)(1.0 / softmax_scale)};
-  static bool attrs = false;
-  if (!attrs) {
-    allow_smem(attn_bwd_dkdv_kernel<true>, kDkdvSmem);
-    allow_smem(attn_bwd_dkdv_kernel<false>, kDkdvSmem);
-    attrs = true;
-  }
   const dim3 dq_grid(Hq, S / 128, B), kv_grid(Hkv * (S / 128), B);
+  if (causal && g_attn_dbg != 0) {  // diagnostic timing variants (tools/bench_attn.py --dbg)
+    if (g_attn_dbg & 8) hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, dq_grid, dim3(256), 0, stream, p);
+    const int m = g_attn_dbg & 3;
+    if (m == 1) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<true, 1>), kv_grid, dim3(512), 0, stream, p);
+    else if (m == 2) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<true, 2>), kv_grid, dim3(512), 0, stream, p);
+    else if (m == 3) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<true, 3>), kv_grid, dim3(512), 0, stream, p);
+    else if (g_attn_dbg & 4) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<true, 0>), kv_grid, dim3(512), 0, stream, p);
+    return;
+  }
   if (causal) {
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, dq_grid, dim3(256), kDqSmem, stream, p);
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<true>, kv_grid, dim3(512), kDkdvSmem, stream, p);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, dq_grid, dim3(256), 0, stream, p);
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<true, 0>), kv_grid, dim3(512), 0, stream, p);
   } else {
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<false>, dq_grid, dim3(256), kDqSmem, stream, p);
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<false>, kv_grid, dim3(512), kDkdvSmem, stream, p);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<false>, dq_grid, dim3(256), 0, stream, p);
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<false, 0>), kv_grid, dim3(512), 0, stream, p);
   }
 }

@@ -11,6 +11,8 @@ p.add_argument("--Hq", type=int, default=32)
 p.add_argument("--Hkv", type=int, default=8)
 p.add_argument("--B", type=int, default=1)
 p.add_argument("--iters", type=int, default=10)
+p.add_argument("--dbg", action="store_true", help="also time the causal backward's kernels separately and the dK/dV "
+               "diagnostic variants (cache-hot fetch / no LDS commit); timing only")
 a = p.parse_args()
 e = _ext.ext()
 D = 128
@@ -35,4 +37,20 @@ for causal in (True, False):
     tb = tm(lambda: e.flash_attn_bwd(do, q, k, v, o, lse, dq, dk, dv, scale, causal))
     res["causal" if causal else "full"] = {"fwd_ms": round(tf * 1e3, 3), "fwd_tflops": round(fl_fwd / tf / 1e12, 1),
         "bwd_ms": round(tb * 1e3, 3), "bwd_tflops": round(2.5 * fl_fwd / tb / 1e12, 1)}
+if a.dbg:
+    o, lse = e.flash_attn_fwd(q, k, v, scale, True)
+    do = torch.randn_like(o)
+    dbg = {}
+    for name, mode in (("dq_only", 8), ("dkdv", 4), ("dkdv_hot_fetch", 1), ("dkdv_no_commit", 2), ("dkdv_hot_no_commit", 3)):
+        e.attn_debug_mode(mode)
+        for _ in range(2):
+            e.flash_attn_bwd(do, q, k, v, o, lse, dq, dk, dv, scale, True)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(a.iters):
+            e.flash_attn_bwd(do, q, k, v, o, lse, dq, dk, dv, scale, True)
+        torch.cuda.synchronize()
+        dbg[name + "_ms"] = round((time.perf_counter() - t) / a.iters * 1e3, 3)
+    e.attn_debug_mode(0)
+    res["causal_bwd_parts"] = dbg
 print(json.dumps({"shape": vars(a), **res}))
