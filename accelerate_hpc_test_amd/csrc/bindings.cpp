@@ -38,6 +38,9 @@ void fp8_segment_amax(torch::Tensor x, torch::Tensor lo, torch::Tensor hi, torch
 void fp8_segment_cast(torch::Tensor x, torch::Tensor lo, torch::Tensor hi, torch::Tensor amax, double qmax, torch::Tensor y,
                       int64_t max_len);
 torch::Tensor u8_transpose(torch::Tensor x);
+std::vector<torch::Tensor> mx_quant(torch::Tensor x, bool e5m2, bool colwise);
+torch::Tensor mx_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor sa, torch::Tensor sb, double smul,
+                      c10::optional<torch::Tensor> bias, bool out_fp32, c10::optional<torch::Tensor> out_opt, bool accumulate);
 void fp8_gemm_select(int64_t variant, int64_t group_m);
 // grouped_gemm.hip
 void grouped_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor out, torch::Tensor seg, int64_t mode, torch::Tensor sa,
@@ -87,6 +90,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fp8_segment_amax", &fp8_segment_amax);
   m.def("fp8_segment_cast", &fp8_segment_cast);
   m.def("u8_transpose", &u8_transpose);
+  m.def("mx_quant", &mx_quant, pybind11::arg("x"), pybind11::arg("e5m2") = false, pybind11::arg("colwise") = true);
+  m.def("mx_gemm", &mx_gemm, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("sa"), pybind11::arg("sb"),
+        pybind11::arg("smul") = 1.0, pybind11::arg("bias") = pybind11::none(), pybind11::arg("out_fp32") = false,
+        pybind11::arg("out") = pybind11::none(), pybind11::arg("accumulate") = false);
   m.def("grouped_gemm", &grouped_gemm);
   m.def("batched_transpose", &batched_transpose);
   m.def("attn_debug_mode", &attn_debug_mode);

@@ -251,6 +251,62 @@ __global__ __launch_bounds__(256) void u8_transpose_kernel(const uint8_t* __rest
     *reinterpret_cast<uint4*>(y + (long)(tc + n4 + j) * R + tr + m16) = make_uint4(col[j][0], col[j][1], col[j][2], col[j][3]);
 }
 
+// ------------------------------------------------------------------------------------------------ MXFP8 quantisation
+// OCP MX block scaling (TransformerEngine's MXFP8BlockScaling recipe): every 32 consecutive elements along a GEMM's
+// reduction dimension share one e8m0 scale 2^(e - 127); the elements are stored as sat(x / 2^(e - 127)) in e4m3 / e5m2.
+// e is rounded UP from amax / fp8_max, so the block's largest element never saturates. Scales are stored one byte per
+// block in a grouped order that matches the GEMM's fragment ownership: within each row, the 8 blocks of a 256-element
+// group g are laid out as [hf = 0: q = 0..3 | hf = 1: q = 0..3] for block 8 g + 2 q + hf, so one dword is one lane's
+// scales for four 64-wide K-tiles. mx_pos maps a block index to its byte.
+__device__ __forceinline__ int mx_pos(int b) { return (b & ~7) | ((b & 1) << 2) | ((b >> 1) & 3); }
+
+template <bool E5M2, typename Get>
+__device__ __forceinline__ void mx_quant_block(Get get, uint8_t* __restrict__ q, uint8_t* __restrict__ sc) {
+  float m = 0.f;
+#pragma unroll
+  for (int j = 0; j < 32; ++j) m = fmaxf(m, fabsf(get(j)));
+  const uint32_t bits = __float_as_uint(m * (1.f / (E5M2 ? kE5M2Max : kE4M3Max)));
+  uint32_t e = bits >> 23;              // m >= 0: the biased exponent of amax / fp8_max ...
+  if ((bits & 0x7fffffu) != 0) e += 1;  // ... rounded up to a power of two >= it
+  e = min(e, 253u);
+  const float inv = __uint_as_float((254u - e) << 23);  // 2^(127 - e); all-zero blocks get e = 0
+  *sc = (uint8_t)e;
+  uint32_t w[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+    w[k] = cvt_pair<E5M2>(get(4 * k) * inv, get(4 * k + 1) * inv) | (cvt_pair<E5M2>(get(4 * k + 2) * inv, get(4 * k + 3) * inv) << 16);
+  reinterpret_cast<uint4*>(q)[0] = make_uint4(w[0], w[1], w[2], w[3]);
+  reinterpret_cast<uint4*>(q)[1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+
+// x [R, C] bf16 -> q [R, C] + s [R, C/32] (blocks along C) and, with COL, qt [C, R] + st [C, R/32] (= x^T quantised
+// along R: the operand of the GEMMs that reduce over R). One 64x64 tile per 256-thread workgroup, staged once in LDS
+// as fp32; waves 0-1 quantise its 128 row blocks, waves 2-3 its 128 column blocks.
+constexpr int kMxT = 64;
+template <bool E5M2, bool COL>
+__global__ __launch_bounds__(256) void mx_quant_kernel(const bf16_t* __restrict__ x, int R, int C, uint8_t* __restrict__ q,
+                                                       uint8_t* __restrict__ s, uint8_t* __restrict__ qt, uint8_t* __restrict__ st) {
+  __shared__ float tile[kMxT][kMxT + 1];
+  const int r0 = blockIdx.y * kMxT, c0 = blockIdx.x * kMxT, tid = threadIdx.x;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int idx = tid + p * 256, row = idx >> 3, ch = (idx & 7) * 8;
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + (long)(r0 + row) * C + c0 + ch);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) tile[row][ch + j] = bf2f(v.v[j]);
+  }
+  __syncthreads();
+  if (tid < 128) {
+    const int row = tid >> 1, blk = tid & 1;
+    mx_quant_block<E5M2>([&](int j) { return tile[row][blk * 32 + j]; }, q + (long)(r0 + row) * C + c0 + blk * 32,
+                         s + (long)(r0 + row) * (C / 32) + mx_pos(c0 / 32 + blk));
+  } else if (COL) {
+    const int i = tid - 128, col = i >> 1, blk = i & 1;
+    mx_quant_block<E5M2>([&](int j) { return tile[blk * 32 + j][col]; }, qt + (long)(c0 + col) * R + r0 + blk * 32,
+                         st + (long)(c0 + col) * (R / 32) + mx_pos(r0 / 32 + blk));
+  }
+}
+
 // ------------------------------------------------------------------------------------------------ GEMM
 constexpr int BM = 128, BN = 128, BK = 64;  // BK in fp8 elements (= bytes)
 
@@ -562,11 +618,24 @@ __device__ __forceinline__ int v3_swz(int row, int chunk) { return chunk ^ ((row
 
 // NW = 4: 2 x 2 waves of 128x128 (one per SIMD, accumulators in the 512-entry file); NW = 8: 2 x 4 waves of 128x64
 // (two per SIMD, so one wave's DMA / LDS issue overlaps the other's MFMAs).
-template <int FA, int FB, bool OUT_F32, int NW>
+// vmcnt waits of the v3 ring (the count must be an immediate)
+template <int N>
+__device__ __forceinline__ void v3_wait() {
+  if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+  else if constexpr (N == 14) asm volatile("s_waitcnt vmcnt(14) lgkmcnt(0)" ::: "memory");
+  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory");
+  else if constexpr (N == 24) asm volatile("s_waitcnt vmcnt(24) lgkmcnt(0)" ::: "memory");
+  else static_assert(N < 0, "v3_wait: unsupported count");
+}
+
+// MX: the per-32-element e8m0 block scales of A [M, K/32] and B [N, K/32] (mx_quant's grouped layout, see below)
+// feed the MFMA's own scale operands instead of unit scales; the per-tensor sa / sb are then unused.
+template <int FA, int FB, bool OUT_F32, int NW, bool MX = false>
 __device__ __forceinline__ void fp8_gemm_v3_body(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
                                                  const float* __restrict__ sa, const float* __restrict__ sb, float smul,
                                                  const bf16_t* __restrict__ bias, void* __restrict__ C, int M, int N,
-                                                 int K, int accum, int group_m) {
+                                                 int K, int accum, int group_m, const uint8_t* __restrict__ mxa = nullptr,
+                                                 const uint8_t* __restrict__ mxb = nullptr) {
   // one LDS object per ring slot, each addressed with a compile-time identity (the loop is unrolled by the ring
   // depth): distinct objects carry distinct alias scopes, so hipcc does not drain the other slots' DMA (vmcnt(0))
   // before a slot's ds_reads
@@ -622,6 +691,24 @@ __device__ __forceinline__ void fp8_gemm_v3_body(const uint8_t* __restrict__ A, 
   const auto a_rs = __builtin_amdgcn_make_buffer_rsrc((void*)(A + (long)tm * K), (short)0, V3_BM * K, 0x00020000);
   const auto b_rs = __builtin_amdgcn_make_buffer_rsrc((void*)(B + (long)tn * K), (short)0, V3_BN * K, 0x00020000);
   const int nk = K / V3_BK;
+  // MX scales: lane (r, hf) of a 32x32x64 fragment holds K bytes 32 hf .. 32 hf + 31 of its row, i.e. exactly one
+  // 32-element block, so its scale is one byte per fragment. mx_quant groups the scales of 4 K-tiles per row and half:
+  // dword (row, g, hf) = the blocks 8 g + 2 q + hf, q = 0..3, one byte each — one buffer load per fragment row per 4
+  // K-tiles (the ring loop's unroll), issued behind the DMA of step q = 0 and waited for with the ring's counts.
+  constexpr int NS = MX ? TI + TJ : 0;  // scale loads per wave per 4 K-tiles
+  const int kb = K / 32;
+  unsigned sca[TI], scb[TJ], nsa[TI], nsb[TJ];
+  const auto sa_rs = __builtin_amdgcn_make_buffer_rsrc(MX ? (void*)(mxa + (long)tm * kb) : (void*)A, (short)0, V3_BM * kb, 0x00020000);
+  const auto sb_rs = __builtin_amdgcn_make_buffer_rsrc(MX ? (void*)(mxb + (long)tn * kb) : (void*)B, (short)0, V3_BN * kb, 0x00020000);
+  const unsigned sv_a = (unsigned)((wm + r) * kb + hf * 4), sv_b = (unsigned)((wn + r) * kb + hf * 4);
+  auto load_scales = [&](int g, unsigned (&la)[TI], unsigned (&lb)[TJ]) {
+    if constexpr (MX) {
+#pragma unroll
+      for (int i = 0; i < TI; ++i) la[i] = __builtin_amdgcn_raw_buffer_load_b32(sa_rs, sv_a, i * 32 * kb + g * 8, 0);
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) lb[j] = __builtin_amdgcn_raw_buffer_load_b32(sb_rs, sv_b, j * 32 * kb + g * 8, 0);
+    }
+  };
   // Past the last K-tile the DMA is still issued (so every wait below has ONE count and the loop body has no branch
   // for hipcc to sink the MFMAs across), but with an soffset beyond the descriptor: the hardware range check returns
   // zeros without touching memory, into a ring slot nobody reads again.
@@ -636,7 +723,10 @@ __device__ __forceinline__ void fp8_gemm_v3_body(const uint8_t* __restrict__ A, 
   };
   // fragment rows wm + 32 i + r / wn + 32 j + r all have (row >> 2) & 3 == (r >> 2) & 3
   const int sw = (r >> 2) & 3;
-  const int lo0 = ((2 * hf) ^ sw) * 16, lo1 = ((2 * hf + 1) ^ sw) * 16;
+  // The MFMA's K order: lane (r, hf) supplies K 16 hf .. +15 in its first four registers and K 32 + 16 hf .. +15 in
+  // the last four, and the block scale of lane (r, hf) covers K 32 hf .. 32 hf + 31. Reading the chunks hf and 2 + hf
+  // keeps that K order equal to the memory order, so each 32-element memory block meets its own scale.
+  const int lo0 = (hf ^ sw) * 16, lo1 = ((2 + hf) ^ sw) * 16;
   const int arow = (wm + r) * V3_BK, brow = V3_BOFF + (wn + r) * V3_BK;
   auto frag = [&](const uint8_t* p) -> v8i {
     const uint4 lo = *reinterpret_cast<const uint4*>(p + lo0);
@@ -651,16 +741,24 @@ __device__ __forceinline__ void fp8_gemm_v3_body(const uint8_t* __restrict__ A, 
 #pragma unroll
     for (int i = 0; i < TI; ++i) fa[i] = frag(img + arow + i * 32 * V3_BK);
   };
-  auto mfma_rows = [&](const v8i (&fa)[TI], const v8i (&fb)[TJ], int i0) {
+  auto mfma_rows = [&](const v8i (&fa)[TI], const v8i (&fb)[TJ], int i0, auto q) {
+    constexpr int Q = decltype(q)::value;  // K-tile within the group of 4: byte Q of the scale dwords
 #pragma unroll
     for (int i = i0; i < i0 + 2; ++i)
 #pragma unroll
-      for (int j = 0; j < TJ; ++j)  // swapped operands: acc holds the C^T tile (lane <-> m, registers <-> n)
-        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fb[j], fa[i], acc[i][j], FB, FA, 0, 0x7f7f7f7f, 0,
-                                                                    0x7f7f7f7f);
+      for (int j = 0; j < TJ; ++j) {  // swapped operands: acc holds the C^T tile (lane <-> m, registers <-> n)
+        if constexpr (MX)  // op_sel picks byte Q of the scale dword in the MFMA itself (no VALU byte shifts)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fb[j], fa[i], acc[i][j], FB, FA, Q, (int)scb[j], Q,
+                                                                      (int)sca[i]);
+        else
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fb[j], fa[i], acc[i][j], FB, FA, 0, 0x7f7f7f7f, 0,
+                                                                      0x7f7f7f7f);
+      }
   };
 
-  // prologue: tiles 0..3 in flight, wait for tile 0, read its fragments
+  // prologue: scales of K-tiles 0..3, tiles 0..3 in flight, wait for both and tile 0, read its fragments
+  load_scales(0, sca, scb);
+  __builtin_amdgcn_sched_barrier(0);  // the scale loads stay ahead of the DMA (their wait below is then free)
   stage(0, ring0);
   stage(1, ring1);
   stage(2, ring2);
@@ -668,23 +766,36 @@ __device__ __forceinline__ void fp8_gemm_v3_body(const uint8_t* __restrict__ A, 
   if constexpr (NW == 4) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // 3 tiles x 2 DPW DMAs in flight
   else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
   __builtin_amdgcn_s_barrier();
+  if constexpr (MX) {
+    // consume the first scales here: a load still pending at the loop header (preheader path) would make hipcc wait
+    // for it at the top of EVERY iteration, draining the DMA ring
+#pragma unroll
+    for (int i = 0; i < TI; ++i) asm volatile("" ::"v"(sca[i]));
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) asm volatile("" ::"v"(scb[j]));
+  }
   __builtin_amdgcn_sched_barrier(0);
   v8i xa[TI], xb[TJ], ya[TI], yb[TJ];
   load(ring0, xa, xb);
 
   // one K-tile: `cur` fragments (tile t, in VGPRs) -> MFMAs; `nxt` <- fragments of tile t+1 from slot `nslot`;
   // DMA of tile t+4 into `slot` (tile t's, free once every wave passed the barrier). Straight-line code only.
-  auto step = [&](int t, uint8_t* slot, const uint8_t* nslot, v8i (&ca)[TI], v8i (&cb)[TJ], v8i (&na)[TI], v8i (&nb)[TJ]) {
-    mfma_rows(ca, cb, 0);
+  const int ng = nk / 4;
+  auto step = [&](int t, uint8_t* slot, const uint8_t* nslot, v8i (&ca)[TI], v8i (&cb)[TJ], v8i (&na)[TI], v8i (&nb)[TJ],
+                  auto q) {
+    constexpr int Q = decltype(q)::value;
+    mfma_rows(ca, cb, 0, q);
     __builtin_amdgcn_sched_barrier(0);
-    // tile t+1 landed (t+2, t+3 in flight)
-    if constexpr (NW == 4) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+    // tile t+1 landed (t+2, t+3 in flight). MX: the next group's scales, loaded behind tile t+4 - Q's DMA in step
+    // Q = 0, stay in flight through Q = 1, 2 and have landed after the wait of Q = 3.
+    constexpr int DMA2 = NW == 4 ? 16 : 8;  // two tiles' DMA
+    v3_wait<(Q == 1 || Q == 2) ? DMA2 + NS : DMA2>();
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     stage(t + 4, slot);
+    if constexpr (Q == 0) load_scales(min(t / 4 + 1, ng - 1), nsa, nsb);  // the last group re-reads its own
     load(nslot, na, nb);  // past the last tile this reads a stale slot into registers nobody uses
-    mfma_rows(ca, cb, 2);
+    mfma_rows(ca, cb, 2, q);
     // issue order of this region: per MFMA one DMA and two fragment reads, so the reads of t+1 start right after the
     // barrier and their latency hides under this half's MFMAs (left alone, hipcc issues the MFMAs first)
 #pragma unroll
@@ -695,15 +806,25 @@ __device__ __forceinline__ void fp8_gemm_v3_body(const uint8_t* __restrict__ A, 
     }
     __builtin_amdgcn_sched_barrier(0);
   };
+  using Q0 = std::integral_constant<int, 0>;
+  using Q1 = std::integral_constant<int, 1>;
+  using Q2 = std::integral_constant<int, 2>;
+  using Q3 = std::integral_constant<int, 3>;
   for (int t = 0; t < nk; t += 4) {  // nk % 4 == 0 (host check)
-    step(t, ring0, ring1, xa, xb, ya, yb);
-    step(t + 1, ring1, ring2, ya, yb, xa, xb);
-    step(t + 2, ring2, ring3, xa, xb, ya, yb);
-    step(t + 3, ring3, ring0, ya, yb, xa, xb);
+    step(t, ring0, ring1, xa, xb, ya, yb, Q0{});
+    step(t + 1, ring1, ring2, ya, yb, xa, xb, Q1{});
+    step(t + 2, ring2, ring3, xa, xb, ya, yb, Q2{});
+    step(t + 3, ring3, ring0, ya, yb, xa, xb, Q3{});
+    if constexpr (MX) {
+#pragma unroll
+      for (int i = 0; i < TI; ++i) sca[i] = nsa[i];
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) scb[j] = nsb[j];
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA left in flight past the loop
 
-  const float s = sa[0] * sb[0] * smul;
+  const float s = MX ? smul : sa[0] * sb[0] * smul;
   // epilogue: bias / accumulate resolved once per kernel, not per element (per-element `if (bias)` became a branch
   // around every bias load)
   auto epilogue = [&](auto has_bias, auto acc_in) {
@@ -760,6 +881,15 @@ __global__ __launch_bounds__(256, 1) void fp8_gemm_v3_kernel(const uint8_t* __re
                                                              const bf16_t* __restrict__ bias, void* __restrict__ C, int M, int N,
                                                              int K, int accum, int group_m) {
   fp8_gemm_v3_body<FA, FB, OUT_F32, 4>(A, B, sa, sb, smul, bias, C, M, N, K, accum, group_m);
+}
+
+// MXFP8 GEMM: v3 4-wave body with per-block e8m0 scales (xa: [M, K/32], xb: [N, K/32], grouped layout)
+template <int FA, int FB, bool OUT_F32>
+__global__ __launch_bounds__(256, 1) void mx_gemm_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
+                                                         const uint8_t* __restrict__ xa, const uint8_t* __restrict__ xb,
+                                                         float smul, const bf16_t* __restrict__ bias, void* __restrict__ C,
+                                                         int M, int N, int K, int accum, int group_m) {
+  fp8_gemm_v3_body<FA, FB, OUT_F32, 4, true>(A, B, nullptr, nullptr, smul, bias, C, M, N, K, accum, group_m, xa, xb);
 }
 
 template <int FA, int FB, bool OUT_F32>
@@ -834,6 +964,40 @@ torch::Tensor u8_transpose(torch::Tensor x) {
   hipLaunchKernelGGL(u8_transpose_kernel, grid, dim3(256), 0, at::hip::getCurrentHIPStream(),
                      reinterpret_cast<const uint8_t*>(x.data_ptr()), reinterpret_cast<uint8_t*>(y.data_ptr()), R, C);
   return y;
+}
+
+// MXFP8 quantisation (see mx_quant_kernel): returns {q, s} or, with `colwise`, {q, s, qt, st}. q / qt: fp8
+// (e4m3fn, or e5m2), s / st: uint8 e8m0 block scales in the grouped layout. C % 256 == 0 (and R % 256 == 0 with
+// colwise) so that every row holds whole scale groups.
+std::vector<torch::Tensor> mx_quant(torch::Tensor x, bool e5m2, bool colwise) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.dim() == 2, "mx_quant: 2-D contiguous bf16");
+  const int R = x.size(0), C = x.size(1);
+  TORCH_CHECK(R % kMxT == 0 && C % 256 == 0 && (!colwise || R % 256 == 0),
+              "mx_quant: rows must be a multiple of 64 (256 with colwise) and columns of 256");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "mx_quant: x must be 16-B aligned");
+  auto dt = e5m2 ? at::kFloat8_e5m2 : at::kFloat8_e4m3fn;
+  auto q = torch::empty({R, C}, x.options().dtype(dt));
+  auto s = torch::empty({R, C / 32}, x.options().dtype(torch::kUInt8));
+  torch::Tensor qt, st;
+  if (colwise) {
+    qt = torch::empty({C, R}, x.options().dtype(dt));
+    st = torch::empty({C, R / 32}, x.options().dtype(torch::kUInt8));
+  }
+  if (R > 0 && C > 0) {
+    dim3 grid(C / kMxT, R / kMxT);
+    auto stream = at::hip::getCurrentHIPStream();
+    const bf16_t* xp = reinterpret_cast<const bf16_t*>(x.data_ptr());
+    uint8_t* qp = reinterpret_cast<uint8_t*>(q.data_ptr());
+    uint8_t* sp = s.data_ptr<uint8_t>();
+    uint8_t* qtp = colwise ? reinterpret_cast<uint8_t*>(qt.data_ptr()) : nullptr;
+    uint8_t* stp = colwise ? st.data_ptr<uint8_t>() : nullptr;
+#define MXQ(E, CW) hipLaunchKernelGGL((mx_quant_kernel<E, CW>), grid, dim3(256), 0, stream, xp, R, C, qp, sp, qtp, stp)
+    if (e5m2) { if (colwise) MXQ(true, true); else MXQ(true, false); }
+    else { if (colwise) MXQ(false, true); else MXQ(false, false); }
+#undef MXQ
+  }
+  if (colwise) return {q, s, qt, st};
+  return {q, s};
 }
 
 // scale = from_amax ? qmax / max(t, 1e-12) : t * qmax, read on the device (t: fp32 [1]).
@@ -970,5 +1134,52 @@ torch::Tensor fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor a_scale_i
   else if (a_e5m2 && !b_e5m2) { if (out_fp32) GEMM_LAUNCH(1, 0, true); else GEMM_LAUNCH(1, 0, false); }
   else { if (out_fp32) GEMM_LAUNCH(1, 1, true); else GEMM_LAUNCH(1, 1, false); }
 #undef GEMM_LAUNCH
+  return out;
+}
+
+// C = (a . b^T) * smul (+ bias) with MX block scales: a [M, K] / b [N, K] fp8, sa [M, K/32] / sb [N, K/32] uint8 e8m0
+// in mx_quant's grouped layout. Needs the v3 tiling: M, N multiples of 256, K of 256. out / accumulate as in fp8_gemm.
+torch::Tensor mx_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor sa, torch::Tensor sb, double smul,
+                      c10::optional<torch::Tensor> bias, bool out_fp32, c10::optional<torch::Tensor> out_opt, bool accumulate) {
+  TORCH_CHECK(a.is_cuda() && b.is_cuda() && a.dim() == 2 && b.dim() == 2 && a.is_contiguous() && b.is_contiguous() &&
+                  a.element_size() == 1 && b.element_size() == 1, "mx_gemm: operands must be 2-D contiguous fp8");
+  const int M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(b.size(1) == K, "mx_gemm: K mismatch");
+  TORCH_CHECK(M % V3_BM == 0 && N % V3_BN == 0 && K % (4 * V3_BK) == 0, "mx_gemm: M, N, K must be multiples of 256");
+  TORCH_CHECK((long)V3_BM * K < (1L << 30), "mx_gemm: K too large");
+  TORCH_CHECK(sa.scalar_type() == at::kByte && sb.scalar_type() == at::kByte && sa.is_contiguous() && sb.is_contiguous() &&
+                  sa.numel() == (long)M * (K / 32) && sb.numel() == (long)N * (K / 32), "mx_gemm: scales must be uint8 [rows, K/32]");
+  const bool e5a = a.scalar_type() == at::kFloat8_e5m2, e5b = b.scalar_type() == at::kFloat8_e5m2;
+  torch::Tensor out;
+  if (out_opt.has_value()) {
+    out = *out_opt;
+    TORCH_CHECK(out.is_cuda() && out.is_contiguous() && out.size(0) == M && out.size(1) == N &&
+                    out.scalar_type() == (out_fp32 ? torch::kFloat32 : torch::kBFloat16),
+                "mx_gemm: out must be a contiguous [M, N] tensor of the output dtype");
+  } else {
+    TORCH_CHECK(!accumulate, "mx_gemm: accumulate needs an out tensor");
+    out = torch::empty({M, N}, a.options().dtype(out_fp32 ? torch::kFloat32 : torch::kBFloat16));
+  }
+  const bf16_t* bp = nullptr;
+  if (bias.has_value()) {
+    TORCH_CHECK(bias->scalar_type() == at::kBFloat16 && bias->numel() == N && bias->is_contiguous(), "mx_gemm: bias must be bf16 [N]");
+    bp = reinterpret_cast<const bf16_t*>(bias->data_ptr());
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(bp) & 7) == 0, "mx_gemm: bias must be 8-B aligned");
+  }
+  const int accum = accumulate ? 1 : 0;
+  auto stream = at::hip::getCurrentHIPStream();
+  const uint8_t* ap = reinterpret_cast<const uint8_t*>(a.data_ptr());
+  const uint8_t* bq = reinterpret_cast<const uint8_t*>(b.data_ptr());
+  const uint8_t* sap = sa.data_ptr<uint8_t>();
+  const uint8_t* sbp = sb.data_ptr<uint8_t>();
+  void* cp = out.data_ptr();
+  const int nwg = (M / V3_BM) * (N / V3_BN);
+#define MXG(FA, FB, OF) \
+  hipLaunchKernelGGL((mx_gemm_kernel<FA, FB, OF>), dim3(nwg), dim3(256), 0, stream, ap, bq, sap, sbp, (float)smul, bp, cp, M, N, K, accum, g_fp8_gemm_group_m)
+  if (!e5a && !e5b) { if (out_fp32) MXG(0, 0, true); else MXG(0, 0, false); }
+  else if (!e5a && e5b) { if (out_fp32) MXG(0, 1, true); else MXG(0, 1, false); }
+  else if (e5a && !e5b) { if (out_fp32) MXG(1, 0, true); else MXG(1, 0, false); }
+  else { if (out_fp32) MXG(1, 1, true); else MXG(1, 1, false); }
+#undef MXG
   return out;
 }

@@ -6,7 +6,12 @@ recipes with our kernels:
 
 * dynamic scaling (torchao-style, `AORecipeKwargs`): scale = fp8_max / amax of the current tensor;
 * delayed scaling (TE-style, `TERecipeKwargs`): scale from the max of an amax history ring buffer kept on the device
-  (length `amax_history_len`), `margin` applied as 2^-margin; format "HYBRID" = e4m3 forward, e5m2 gradients.
+  (length `amax_history_len`), `margin` applied as 2^-margin; format "HYBRID" = e4m3 forward, e5m2 gradients;
+* MXFP8 block scaling (TE `MXFP8BlockScaling`, `TERecipeKwargs(use_mxfp8_block_scaling=True)`): one e8m0 scale per 32
+  elements along each GEMM's reduction dimension, applied by the MFMA itself (`v_mfma_scale_f32_32x32x64_f8f6f4`'s
+  block-scale operands); every tensor is quantised twice in one pass (row blocks and column blocks), so forward,
+  dgrad and wgrad each read K-contiguous operands with their own block scales. Reference:
+  `/root/reference/src/accelerate/utils/transformer_engine.py:165-186`, `utils/dataclasses.py:404,433-434`.
 
 Forward  y  = (x8 · w8ᵀ) / (sx·sw)                      — fp8 GEMM, bf16 out
 Backward dx = (dy8 · w8ᵀᵀ) / (sg·sw),  dW = (dy8ᵀ · x8ᵀᵀ) / (sg·sx) — the cast kernel writes the transposed copies
@@ -119,11 +124,125 @@ def _gemm_ok(M, N, K):
     return M % 128 == 0 and N % 128 == 0 and K % 64 == 0
 
 
+# ------------------------------------------------------------------------------------------------------------ MXFP8
+MX_BLOCK = 32
+
+
+def _mx_pos(nblk: int, device=None) -> torch.Tensor:
+    """Byte position of each 32-element block in a row of the grouped scale layout (csrc fp8.hip `mx_pos`): the 8 blocks
+    of a 256-element group are stored [hf = 0: q = 0..3 | hf = 1: q = 0..3] for block 8g + 2q + hf."""
+    b = torch.arange(nblk, device=device)
+    return (b & ~7) | ((b & 1) << 2) | ((b >> 1) & 3)
+
+
+def mx_scales_natural(s: torch.Tensor) -> torch.Tensor:
+    """Grouped-layout e8m0 scales [R, K/32] -> scales in block order."""
+    return s[:, _mx_pos(s.shape[1], s.device)]
+
+
+def _mx_quant_rows(x: torch.Tensor, e5m2: bool):
+    """Reference MX quantisation of x [R, C] along C (PyTorch; the HIP kernel's oracle and CPU path)."""
+    R, C = x.shape
+    fmax = E5M2_MAX if e5m2 else E4M3_MAX
+    blocks = x.float().reshape(R, C // MX_BLOCK, MX_BLOCK)
+    amax = blocks.abs().amax(-1)
+    v = amax * (1.0 / fmax)
+    bits = v.view(torch.int32)
+    e = (bits >> 23) + ((bits & 0x7FFFFF) != 0).to(torch.int32)  # exponent of amax / fp8_max, rounded up
+    e = e.clamp(max=253)
+    inv = torch.exp2((127 - e).float())
+    dt = torch.float8_e5m2 if e5m2 else torch.float8_e4m3fn
+    q = (blocks * inv.unsqueeze(-1)).clamp(-fmax, fmax).to(dt).reshape(R, C)
+    s = torch.empty(R, C // MX_BLOCK, dtype=torch.uint8, device=x.device)
+    s[:, _mx_pos(C // MX_BLOCK, x.device)] = e.to(torch.uint8)
+    return q, s
+
+
+def mx_quant(x: torch.Tensor, e5m2: bool = False, colwise: bool = True):
+    """MXFP8-quantise a 2-D bf16 tensor: (q, s) with 32-element blocks along its columns, plus (qt, st) = x^T quantised
+    with blocks along x's rows when `colwise` (the wgrad / dgrad operands). s / st are uint8 e8m0 in the grouped layout."""
+    if x.is_cuda and use_native(x) and x.dtype == torch.bfloat16:
+        return tuple(ext().mx_quant(x.contiguous(), e5m2, colwise))
+    q, s = _mx_quant_rows(x, e5m2)
+    if not colwise:
+        return q, s
+    qt, st = _mx_quant_rows(x.t().contiguous(), e5m2)
+    return q, s, qt, st
+
+
+def mx_dequant(q: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
+    """fp32 value of an MX tensor (q [R, K], grouped scales s [R, K/32])."""
+    R, K = q.shape
+    sc = torch.exp2(mx_scales_natural(s).float() - 127.0)
+    return (q.float().reshape(R, K // MX_BLOCK, MX_BLOCK) * sc.unsqueeze(-1)).reshape(R, K)
+
+
+def mx_gemm(a8, b8, sa, sb, bias=None, out_dtype=torch.bfloat16, out: Optional[torch.Tensor] = None,
+            accumulate: bool = False):
+    """C = (a · bᵀ) with MX block scales (+ bias): a8 [M, K], b8 [N, K] fp8 with e8m0 scales [M, K/32] / [N, K/32]. The
+    block scales ride in the MFMA (no dequantisation pass). `out` / `accumulate` as in `gemm`."""
+    if out is not None:
+        out_dtype = out.dtype
+    if a8.is_cuda and use_native(a8):
+        return ext().mx_gemm(a8, b8, sa, sb, 1.0, bias, out_dtype == torch.float32, out, accumulate)
+    res = mx_dequant(a8, sa) @ mx_dequant(b8, sb).t()
+    if bias is not None:
+        res = res + bias.float()
+    if out is None:
+        return res.to(out_dtype)
+    if accumulate:
+        out.add_(res.to(out.dtype))
+    else:
+        out.copy_(res)
+    return out
+
+
+def _mx_ok(M, N, K):
+    """Shapes the MX GEMM tiles (256 x 256 output tiles, K in 256-element scale groups) for all three GEMMs."""
+    return M % 256 == 0 and N % 256 == 0 and K % 256 == 0
+
+
+class _MxLinearFn(torch.autograd.Function):
+    """MXFP8 linear: y = x wᵀ, dx = dy w, dW = dyᵀ x, each GEMM on MX operands blocked along its own reduction dim.
+    x, w and dy are each quantised once into row-blocked and column-blocked copies (one HIP pass per tensor)."""
+
+    @staticmethod
+    def forward(ctx, x, w, bias, recipe, slot=None):
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1])
+        e5 = recipe.fwd_e5m2()
+        xq, xs, xqt, xst = mx_quant(x2, e5, True)
+        wq, ws, wqt, wst = mx_quant(w, e5, True)
+        y = mx_gemm(xq, wq, xs, ws, bias, torch.bfloat16)
+        ctx.save_for_backward(xqt, xst, wqt, wst)
+        ctx.recipe, ctx.shape, ctx.has_bias, ctx.slot = recipe, shape, bias is not None, slot
+        return y.view(*shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        xqt, xst, wqt, wst = ctx.saved_tensors
+        N = dy.shape[-1]
+        dy2 = dy.reshape(-1, N).contiguous().to(torch.bfloat16)
+        gq, gs, gqt, gst = mx_quant(dy2, ctx.recipe.grad_e5m2(), True)
+        dx = mx_gemm(gq, wqt, gs, wst, None, torch.bfloat16)
+        db = dy2.float().sum(0).to(dy.dtype) if ctx.has_bias else None
+        slot = ctx.slot
+        if slot is not None:
+            dest, acc = slot.engine._fused_slot_dest(slot)
+            mx_gemm(gqt, xqt, gst, xst, None, out=dest, accumulate=acc)
+            slot.engine._fused_slot_done(slot)
+            return dx.view(ctx.shape), None, db, None, None
+        dw = mx_gemm(gqt, xqt, gst, xst, None, torch.bfloat16)
+        return dx.view(ctx.shape), dw, db, None, None
+
+
 class Fp8Recipe:
     """Runtime scaling state of one Fp8Linear."""
 
-    def __init__(self, delayed: bool = False, history_len: int = 16, margin: int = 0, fmt: str = "HYBRID", algo: str = "max"):
-        self.delayed = delayed
+    def __init__(self, delayed: bool = False, history_len: int = 16, margin: int = 0, fmt: str = "HYBRID", algo: str = "max",
+                 mx: bool = False):
+        self.mx = mx  # MXFP8 block scaling (no per-tensor scale state)
+        self.delayed = delayed and not mx
         self.history_len = history_len
         self.margin = margin
         self.fmt = fmt.upper()
@@ -237,6 +356,12 @@ class Fp8Linear(nn.Linear):
             w = self._dequantised(gathered) if gathered is not None else self.weight
             return nn.functional.linear(x, w.to(x.dtype), None if self.bias is None else self.bias.to(x.dtype))
         b = None if self.bias is None else self.bias.to(torch.bfloat16)
+        if self.fp8_recipe.mx:
+            if _mx_ok(M, self.out_features, self.in_features) and gathered is None:
+                w = self.weight if self.weight.dtype == torch.bfloat16 else self.weight.to(torch.bfloat16)
+                return _MxLinearFn.apply(x, w, b, self.fp8_recipe, self._fp8_wgrad_slot(x))
+            w = self._dequantised(gathered) if gathered is not None else self.weight
+            return nn.functional.linear(x, w.to(x.dtype), b)  # shapes the MX tiling cannot cover run in bf16
         if gathered is not None:
             unit, info = gathered
             return _Fp8LinearFn.apply(x, self.weight, b, self.fp8_recipe, self._fp8_wgrad_slot(x),
@@ -291,7 +416,10 @@ def convert_model_to_fp8(model: nn.Module, recipe=None, backend: str = "AO", mod
 
     delayed = isinstance(recipe, TERecipeKwargs) or backend == "TE"
     kwargs = {}
-    if delayed and recipe is not None:
+    if delayed and recipe is not None and getattr(recipe, "use_mxfp8_block_scaling", False):
+        _check_mxfp8_recipe(recipe)
+        kwargs = dict(mx=True, fmt=recipe.fp8_format)
+    elif delayed and recipe is not None:
         kwargs = dict(delayed=True, history_len=max(1, min(int(recipe.amax_history_len), 1024)), margin=int(recipe.margin), fmt=recipe.fp8_format, algo=recipe.amax_compute_algo)
     else:
         kwargs = dict(delayed=False, fmt="HYBRID")
@@ -322,6 +450,17 @@ def convert_model_to_fp8(model: nn.Module, recipe=None, backend: str = "AO", mod
                 n += 1
     model._acc_fp8_linears = n
     return model
+
+
+def _check_mxfp8_recipe(recipe):
+    """MXFP8 has no amax history: like TE (reference transformer_engine.py:170-174), an explicitly set history length
+    or amax algorithm is an error rather than silently ignored. Only fields differing from the defaults count."""
+    from ..utils.dataclasses import TERecipeKwargs
+
+    default = TERecipeKwargs()
+    for field in ("amax_compute_algo", "amax_history_len"):
+        if getattr(recipe, field) != getattr(default, field):
+            raise ValueError(f"`{field}` is not supported for MXFP8 block scaling.")
 
 
 def has_fp8_layers(model: nn.Module) -> bool:

@@ -306,7 +306,7 @@ class FSDPEngine:
         rec = getattr(m, "fp8_recipe", None)
         return (isinstance(m, Fp8Linear) and info.attr == "weight" and info.param.requires_grad and len(info.shape) == 2
                 and refs.get(id(info.param), 0) == 1 and getattr(info.param, "_tp_spec", None) is None
-                and rec is not None and not rec.delayed and not rec.fwd_e5m2())
+                and rec is not None and not rec.delayed and not rec.mx and not rec.fwd_e5m2())
 
     def _init_fp8_all_gather(self):
         """Index the fp8-gathered weights (one amax slot each, in one engine-wide buffer so the global amax is ONE

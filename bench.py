@@ -31,7 +31,9 @@ def parse():
     p.add_argument("--model", default="llama3-8b")
     p.add_argument("--seq", type=int, default=8192)
     p.add_argument("--mbs", type=int, default=1)
-    p.add_argument("--precision", default="bf16", choices=["bf16", "fp8"])
+    p.add_argument("--precision", default="bf16", choices=["bf16", "fp8", "mxfp8"],
+                   help="fp8: dynamic per-tensor scaling (torchao recipe); mxfp8: TE MXFP8BlockScaling (e8m0 scale per "
+                        "32 elements, applied inside the MFMA)")
     p.add_argument("--parallel", default="fsdp", choices=["fsdp", "ddp"],
                    help="fsdp: FSDP2 full shard (headline); ddp: replicated fp32 params + bf16 autocast, RCCL all-reduce "
                         "(BASELINE config 'Llama-3 8B DDP bf16')")
@@ -108,7 +110,12 @@ def main():
 
         plugin = None
         handlers.append(DistributedDataParallelKwargs(comm_hook=DDPCommunicationHookType(args.ddp_comm_hook)))
-    accelerator = Accelerator(mixed_precision=args.precision, fsdp_plugin=plugin, kwargs_handlers=handlers)
+    if args.precision == "mxfp8":
+        from accelerate_hpc_test_amd.utils import TERecipeKwargs
+
+        handlers.append(TERecipeKwargs(use_mxfp8_block_scaling=True))
+    mp = "fp8" if args.precision == "mxfp8" else args.precision
+    accelerator = Accelerator(mixed_precision=mp, fsdp_plugin=plugin, kwargs_handlers=handlers)
     set_seed(0)
     world = accelerator.num_processes
     from accelerate_hpc_test_amd.ops import gemm_tuning
@@ -177,7 +184,7 @@ def main():
     flops_tok = cfg.flops_per_token(args.seq)
     peak = torch.cuda.max_memory_allocated() / 2**30
     headline = not is_moe and args.parallel == "fsdp"
-    base_dev = BASELINE_FP8_TOKENS_PER_SEC_PER_DEVICE if args.precision == "fp8" else BASELINE_TOKENS_PER_SEC_PER_DEVICE
+    base_dev = BASELINE_FP8_TOKENS_PER_SEC_PER_DEVICE if args.precision in ("fp8", "mxfp8") else BASELINE_TOKENS_PER_SEC_PER_DEVICE
     if accelerator.is_main_process:
         rec = {
             "metric": _metric_name(args, is_moe),

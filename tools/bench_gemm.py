@@ -6,7 +6,8 @@ line per shape with the median ms / TFLOP/s of each variant over the rounds.
     python tools/bench_gemm.py [--tokens 8192] [--iters 20] [--rounds 3] [--variants 2,4] [--shapes qkv,o]
 
 variants: 1 = v1 128x128, 2 = v2 256x256 4 waves, 3 = v2 8 waves, 4 = v3 4-deep ring, 5 = v3 8 waves; "4g8" = v3 with tile rows
-grouped by 8 (ext().fp8_gemm_select(variant, group_m)).
+grouped by 8 (ext().fp8_gemm_select(variant, group_m)); "mx" = the MXFP8 GEMM (v3 ring with per-32 block scales in the
+MFMA), whose row also reports the one-pass row+column MX quantisation of the A operand (mxq_ms).
 """
 
 import argparse
@@ -50,6 +51,8 @@ def main():
     variants = args.variants.split(",")
 
     def select(v):
+        if v == "mx":
+            return
         num, _, g = v.partition("g")
         ext().fp8_gemm_select(int(num), int(g) if g else 0)
     all_shapes = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336)}
@@ -62,14 +65,22 @@ def main():
             b = torch.randn(n, k, device="cuda", dtype=torch.bfloat16)
             flops = 2.0 * m * n * k
             a8, b8 = fp8.cast(a, one), fp8.cast(b, one)
+            if "mx" in variants:
+                aq, as_ = fp8.mx_quant(a, False, False)
+                bq, bs = fp8.mx_quant(b, False, False)
             times = {v: [] for v in variants}
+            mxq = []
             bf = []
             for _ in range(args.rounds):
                 if not args.no_bf16:
                     bf.append(timeit(lambda: a @ b.t(), args.iters))
                 for v in variants:
                     select(v)
-                    times[v].append(timeit(lambda: fp8.gemm(a8, b8, one, one), args.iters))
+                    if v == "mx":
+                        times[v].append(timeit(lambda: fp8.mx_gemm(aq, bq, as_, bs), args.iters))
+                        mxq.append(timeit(lambda: fp8.mx_quant(a, False, True), args.iters))
+                    else:
+                        times[v].append(timeit(lambda: fp8.gemm(a8, b8, one, one), args.iters))
             ext().fp8_gemm_select(0, 4)
             row = {"gemm": f"{name}.{kind}", "M": m, "N": n, "K": k}
             if bf:
@@ -79,6 +90,9 @@ def main():
                 ms = statistics.median(times[v])
                 row[f"v{v}_ms"] = round(ms, 3)
                 row[f"v{v}_tflops"] = round(flops / ms / 1e9, 1)
+            if mxq:
+                ms = statistics.median(mxq)
+                row.update(mxq_ms=round(ms, 3), mxq_gbs=round(a.numel() * 4 / ms / 1e6, 1))
             print(json.dumps(row), flush=True)
             del a, b, a8, b8
 
