@@ -3,12 +3,13 @@
 #include <torch/extension.h>
 
 // norm_act.hip
-std::vector<torch::Tensor> rmsnorm_fwd(torch::Tensor x, c10::optional<torch::Tensor> residual, torch::Tensor w, double eps);
+std::vector<torch::Tensor> rmsnorm_fwd(torch::Tensor x, c10::optional<torch::Tensor> residual, torch::Tensor w, double eps,
+                                       c10::optional<torch::Tensor> amax);
 std::vector<torch::Tensor> rmsnorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor w, torch::Tensor rstd,
-                                       c10::optional<torch::Tensor> dres);
-torch::Tensor swiglu_fwd(torch::Tensor gu);
+                                       c10::optional<torch::Tensor> dres, c10::optional<torch::Tensor> amax);
+torch::Tensor swiglu_fwd(torch::Tensor gu, c10::optional<torch::Tensor> amax);
 torch::Tensor transpose_bf16(torch::Tensor x);
-torch::Tensor swiglu_bwd(torch::Tensor gu, torch::Tensor dh);
+torch::Tensor swiglu_bwd(torch::Tensor gu, torch::Tensor dh, c10::optional<torch::Tensor> amax);
 void rope_inplace(torch::Tensor qkv, torch::Tensor cos, torch::Tensor sin, c10::optional<torch::Tensor> pos,
                   int64_t n_rot_heads, int64_t n_heads_total, int64_t head_dim, double sign);
 // xent_optim.hip
@@ -67,11 +68,13 @@ std::vector<std::tuple<int64_t, int64_t, int64_t, int64_t, double>> blaslt_wgrad
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "MI355X (gfx950) native kernels and runtime for accelerate_hpc_test_amd";
-  m.def("rmsnorm_fwd", &rmsnorm_fwd);
-  m.def("rmsnorm_bwd", &rmsnorm_bwd);
-  m.def("swiglu_fwd", &swiglu_fwd);
+  m.def("rmsnorm_fwd", &rmsnorm_fwd, pybind11::arg("x"), pybind11::arg("residual"), pybind11::arg("w"), pybind11::arg("eps"),
+        pybind11::arg("amax") = pybind11::none());
+  m.def("rmsnorm_bwd", &rmsnorm_bwd, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("rstd"),
+        pybind11::arg("dres"), pybind11::arg("amax") = pybind11::none());
+  m.def("swiglu_fwd", &swiglu_fwd, pybind11::arg("gu"), pybind11::arg("amax") = pybind11::none());
   m.def("transpose_bf16", &transpose_bf16);
-  m.def("swiglu_bwd", &swiglu_bwd);
+  m.def("swiglu_bwd", &swiglu_bwd, pybind11::arg("gu"), pybind11::arg("dh"), pybind11::arg("amax") = pybind11::none());
   m.def("rope_inplace", &rope_inplace);
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd", &xent_bwd);

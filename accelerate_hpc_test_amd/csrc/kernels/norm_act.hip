@@ -3,6 +3,9 @@
 //   * SwiGLU forward/backward on the fused [gate | up] projection output,
 //   * rotary embedding (rotate-half convention) applied in place to the Q and K heads of a fused QKV buffer.
 // All loads/stores are 16 B per lane (8 x bf16); one row per workgroup for the row-wise kernels.
+// fp8 producer amax: given an `amax_part` buffer, each kernel also writes the max |output| of every workgroup (of the
+// bf16 values it stores, so the result equals a separate amax pass bit for bit); `amax_finalize` folds the partials
+// into the fp32 [1] amax the fp8 cast and GEMM read. That replaces a full re-read of the tensor by the amax kernel.
 #include <hip/hip_runtime.h>
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
@@ -17,7 +20,8 @@ constexpr int kNormThreads = 256;
 template <int VPT>
 __global__ __launch_bounds__(kNormThreads) void rmsnorm_fwd_kernel(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ res, const bf16_t* __restrict__ w,
-    bf16_t* __restrict__ y, bf16_t* __restrict__ res_out, float* __restrict__ rstd_out, int H, float eps) {
+    bf16_t* __restrict__ y, bf16_t* __restrict__ res_out, float* __restrict__ rstd_out, int H, float eps,
+    float* __restrict__ amax_part) {
   __shared__ float scratch[16];
   const int row = blockIdx.x;
   const int nvec = H >> 3;
@@ -50,15 +54,23 @@ __global__ __launch_bounds__(kNormThreads) void rmsnorm_fwd_kernel(
   if (threadIdx.x == 0) rstd_out[row] = r;
   const bf16x8* wr = reinterpret_cast<const bf16x8*>(w);
   bf16x8* yr = reinterpret_cast<bf16x8*>(y + (size_t)row * H);
+  float m = 0.f;
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     const int c = threadIdx.x + i * kNormThreads;
     if (c < nvec) {
       bf16x8 ww = wr[c], o;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o.v[j] = f2bf(v[i][j] * r * bf2f(ww.v[j]));
+      for (int j = 0; j < 8; ++j) {
+        o.v[j] = f2bf(v[i][j] * r * bf2f(ww.v[j]));
+        m = fmaxf(m, fabsf(bf2f(o.v[j])));
+      }
       yr[c] = o;
     }
+  }
+  if (amax_part != nullptr) {
+    m = block_max(m, scratch);
+    if (threadIdx.x == 0) amax_part[row] = m;
   }
 }
 
@@ -67,8 +79,9 @@ template <int VPT>
 __global__ __launch_bounds__(kNormThreads) void rmsnorm_bwd_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
     const float* __restrict__ rstd, const bf16_t* __restrict__ dres, bf16_t* __restrict__ dx,
-    float* __restrict__ dw_part, int T, int H) {
+    float* __restrict__ dw_part, int T, int H, float* __restrict__ amax_part) {
   __shared__ float scratch[16];
+  float m = 0.f;
   const int nvec = H >> 3;
   float wv[VPT][8], dwacc[VPT][8];
   const bf16x8* wr = reinterpret_cast<const bf16x8*>(w);
@@ -116,6 +129,7 @@ __global__ __launch_bounds__(kNormThreads) void rmsnorm_bwd_kernel(
           float val = r * (g[i][j] - xh[i][j] * dot);
           if (dres != nullptr) val += bf2f(rr.v[j]);
           o.v[j] = f2bf(val);
+          m = fmaxf(m, fabsf(bf2f(o.v[j])));
         }
         reinterpret_cast<bf16x8*>(dx + (size_t)row * H)[c] = o;
       }
@@ -129,6 +143,10 @@ __global__ __launch_bounds__(kNormThreads) void rmsnorm_bwd_kernel(
       dst[0] = make_float4(dwacc[i][0], dwacc[i][1], dwacc[i][2], dwacc[i][3]);
       dst[1] = make_float4(dwacc[i][4], dwacc[i][5], dwacc[i][6], dwacc[i][7]);
     }
+  }
+  if (amax_part != nullptr) {
+    m = block_max(m, scratch);
+    if (threadIdx.x == 0) amax_part[blockIdx.x] = m;
   }
 }
 
@@ -155,7 +173,10 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ p
 // ---------------------------------------------------------------------------------------------------
 // SwiGLU on a fused [T, 2F] buffer: gate = gu[:, :F], up = gu[:, F:]; h = silu(gate) * up.
 // ---------------------------------------------------------------------------------------------------
-__global__ void swiglu_fwd_kernel(const bf16_t* __restrict__ gu, bf16_t* __restrict__ h, long T, int F) {
+__global__ __launch_bounds__(256) void swiglu_fwd_kernel(const bf16_t* __restrict__ gu, bf16_t* __restrict__ h, long T,
+                                                         int F, float* __restrict__ amax_part) {
+  __shared__ float scratch[16];
+  float m = 0.f;
   const long nvec_row = F >> 3;
   const long total = T * nvec_row;
   for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
@@ -168,14 +189,22 @@ __global__ void swiglu_fwd_kernel(const bf16_t* __restrict__ gu, bf16_t* __restr
       const float gf = bf2f(g.v[j]);
       const float s = gf / (1.f + __expf(-gf));
       o.v[j] = f2bf(s * bf2f(u.v[j]));
+      m = fmaxf(m, fabsf(bf2f(o.v[j])));
     }
     reinterpret_cast<bf16x8*>(h + row * F)[c] = o;
+  }
+  if (amax_part != nullptr) {
+    m = block_max(m, scratch);
+    if (threadIdx.x == 0) amax_part[blockIdx.x] = m;
   }
 }
 
 // dgate = dh * up * sig * (1 + g*(1-sig)), dup = dh * silu(g). Written into dgu [T, 2F].
-__global__ void swiglu_bwd_kernel(const bf16_t* __restrict__ gu, const bf16_t* __restrict__ dh,
-                                  bf16_t* __restrict__ dgu, long T, int F) {
+__global__ __launch_bounds__(256) void swiglu_bwd_kernel(const bf16_t* __restrict__ gu, const bf16_t* __restrict__ dh,
+                                                         bf16_t* __restrict__ dgu, long T, int F,
+                                                         float* __restrict__ amax_part) {
+  __shared__ float scratch[16];
+  float m = 0.f;
   const long nvec_row = F >> 3;
   const long total = T * nvec_row;
   for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
@@ -191,9 +220,14 @@ __global__ void swiglu_bwd_kernel(const bf16_t* __restrict__ gu, const bf16_t* _
       const float silu = gf * sig;
       og.v[j] = f2bf(df * uf * sig * (1.f + gf * (1.f - sig)));
       ou.v[j] = f2bf(df * silu);
+      m = fmaxf(m, fmaxf(fabsf(bf2f(og.v[j])), fabsf(bf2f(ou.v[j]))));
     }
     reinterpret_cast<bf16x8*>(dgu + row * 2 * F)[c] = og;
     reinterpret_cast<bf16x8*>(dgu + row * 2 * F + F)[c] = ou;
+  }
+  if (amax_part != nullptr) {
+    m = block_max(m, scratch);
+    if (threadIdx.x == 0) amax_part[blockIdx.x] = m;
   }
 }
 
@@ -233,6 +267,15 @@ __global__ void rope_kernel(bf16_t* __restrict__ qkv, const float* __restrict__ 
   }
 }
 
+// max over n per-workgroup partials -> out[0] (one 1024-thread workgroup; n is at most a few thousand)
+__global__ __launch_bounds__(1024) void amax_finalize_kernel(const float* __restrict__ part, int n, float* __restrict__ out) {
+  __shared__ float scratch[16];
+  float m = 0.f;
+  for (int i = threadIdx.x; i < n; i += 1024) m = fmaxf(m, part[i]);
+  m = block_max(m, scratch);
+  if (threadIdx.x == 0) out[0] = m;
+}
+
 inline int grid_for(long work, int threads) {
   long g = (work + threads - 1) / threads;
   if (g > 256 * 8) g = 256 * 8;  // 8 resident blocks per CU, grid-stride the rest
@@ -246,11 +289,33 @@ void check_bf16_cuda(const torch::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
 }
 
+// Partial-max buffer for a producer kernel with `blocks` workgroups (nullptr when no amax is requested).
+struct AmaxOut {
+  torch::Tensor part;
+  float* out = nullptr;
+  float* ptr() const { return out ? part.data_ptr<float>() : nullptr; }
+  AmaxOut(const c10::optional<torch::Tensor>& amax, long blocks, const torch::Tensor& like) {
+    if (!amax.has_value()) return;
+    TORCH_CHECK(amax->is_cuda() && amax->scalar_type() == at::kFloat && amax->numel() >= 1, "amax must be a fp32 [1] HIP tensor");
+    part = torch::empty({std::max<long>(blocks, 1)}, like.options().dtype(torch::kFloat32));
+    out = amax->data_ptr<float>();
+  }
+  void finalize(long blocks) const {
+    if (out == nullptr) return;
+    if (blocks <= 0) {
+      hipMemsetAsync(out, 0, sizeof(float), at::hip::getCurrentHIPStream());
+      return;
+    }
+    hipLaunchKernelGGL(amax_finalize_kernel, dim3(1), dim3(1024), 0, at::hip::getCurrentHIPStream(), part.data_ptr<float>(),
+                       (int)blocks, out);
+  }
+};
+
 }  // namespace
 
 // ----------------------------------------------------------------------------------------- host API
 std::vector<torch::Tensor> rmsnorm_fwd(torch::Tensor x, c10::optional<torch::Tensor> residual, torch::Tensor w,
-                                       double eps) {
+                                       double eps, c10::optional<torch::Tensor> amax) {
   check_bf16_cuda(x, "x");
   check_bf16_cuda(w, "weight");
   const int H = x.size(-1);
@@ -267,23 +332,28 @@ std::vector<torch::Tensor> rmsnorm_fwd(torch::Tensor x, c10::optional<torch::Ten
     resp = reinterpret_cast<const bf16_t*>(residual->data_ptr());
     resop = reinterpret_cast<bf16_t*>(res_out.data_ptr());
   }
-  if (T == 0) return {y, rstd, res_out};
+  const AmaxOut am(amax, T, x);
+  if (T == 0) {
+    am.finalize(0);
+    return {y, rstd, res_out};
+  }
   auto stream = at::hip::getCurrentHIPStream();
   const int vpt = (H / 8 + kNormThreads - 1) / kNormThreads;
 #define LAUNCH_FWD(V)                                                                                             \
   hipLaunchKernelGGL(rmsnorm_fwd_kernel<V>, dim3(T), dim3(kNormThreads), 0, stream,                              \
                      reinterpret_cast<const bf16_t*>(x.data_ptr()), resp, reinterpret_cast<const bf16_t*>(w.data_ptr()), \
-                     reinterpret_cast<bf16_t*>(y.data_ptr()), resop, rstd.data_ptr<float>(), H, (float)eps)
+                     reinterpret_cast<bf16_t*>(y.data_ptr()), resop, rstd.data_ptr<float>(), H, (float)eps, am.ptr())
   if (vpt <= 1) LAUNCH_FWD(1);
   else if (vpt <= 2) LAUNCH_FWD(2);
   else if (vpt <= 4) LAUNCH_FWD(4);
   else LAUNCH_FWD(8);
 #undef LAUNCH_FWD
+  am.finalize(T);
   return {y, rstd, res_out};
 }
 
 std::vector<torch::Tensor> rmsnorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor w, torch::Tensor rstd,
-                                       c10::optional<torch::Tensor> dres) {
+                                       c10::optional<torch::Tensor> dres, c10::optional<torch::Tensor> amax) {
   check_bf16_cuda(dy, "dy");
   check_bf16_cuda(x, "x");
   check_bf16_cuda(w, "weight");
@@ -299,13 +369,18 @@ std::vector<torch::Tensor> rmsnorm_bwd(torch::Tensor dy, torch::Tensor x, torch:
     check_bf16_cuda(*dres, "dres");
     dresp = reinterpret_cast<const bf16_t*>(dres->data_ptr());
   }
-  if (T == 0) { dw.zero_(); return {dx, dw}; }
+  const AmaxOut am(amax, P, x);
+  if (T == 0) {
+    dw.zero_();
+    am.finalize(0);
+    return {dx, dw};
+  }
   const int vpt = (H / 8 + kNormThreads - 1) / kNormThreads;
 #define LAUNCH_BWD(V)                                                                                             \
   hipLaunchKernelGGL(rmsnorm_bwd_kernel<V>, dim3(P), dim3(kNormThreads), 0, stream,                              \
                      reinterpret_cast<const bf16_t*>(dy.data_ptr()), reinterpret_cast<const bf16_t*>(x.data_ptr()), \
                      reinterpret_cast<const bf16_t*>(w.data_ptr()), rstd.data_ptr<float>(), dresp,               \
-                     reinterpret_cast<bf16_t*>(dx.data_ptr()), part.data_ptr<float>(), (int)T, H)
+                     reinterpret_cast<bf16_t*>(dx.data_ptr()), part.data_ptr<float>(), (int)T, H, am.ptr())
   if (vpt <= 1) LAUNCH_BWD(1);
   else if (vpt <= 2) LAUNCH_BWD(2);
   else if (vpt <= 4) LAUNCH_BWD(4);
@@ -313,10 +388,11 @@ std::vector<torch::Tensor> rmsnorm_bwd(torch::Tensor dy, torch::Tensor x, torch:
 #undef LAUNCH_BWD
   hipLaunchKernelGGL(colsum_kernel<bf16_t>, dim3((H + 31) / 32), dim3(256), 0, stream, part.data_ptr<float>(),
                      reinterpret_cast<bf16_t*>(dw.data_ptr()), P, H);
+  am.finalize(P);
   return {dx, dw};
 }
 
-torch::Tensor swiglu_fwd(torch::Tensor gu) {
+torch::Tensor swiglu_fwd(torch::Tensor gu, c10::optional<torch::Tensor> amax) {
   check_bf16_cuda(gu, "gate_up");
   const int F = gu.size(-1) / 2;
   TORCH_CHECK(F % 8 == 0, "swiglu: intermediate size must be a multiple of 8");
@@ -325,23 +401,35 @@ torch::Tensor swiglu_fwd(torch::Tensor gu) {
   sizes.back() = F;
   auto h = torch::empty(sizes, gu.options());
   const long work = T * (F / 8);
-  if (work == 0) return h;
-  hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(grid_for(work, 256)), dim3(256), 0, at::hip::getCurrentHIPStream(),
-                     reinterpret_cast<const bf16_t*>(gu.data_ptr()), reinterpret_cast<bf16_t*>(h.data_ptr()), T, F);
+  const int g = grid_for(work, 256);
+  const AmaxOut am(amax, g, gu);
+  if (work == 0) {
+    am.finalize(0);
+    return h;
+  }
+  hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(g), dim3(256), 0, at::hip::getCurrentHIPStream(),
+                     reinterpret_cast<const bf16_t*>(gu.data_ptr()), reinterpret_cast<bf16_t*>(h.data_ptr()), T, F, am.ptr());
+  am.finalize(g);
   return h;
 }
 
-torch::Tensor swiglu_bwd(torch::Tensor gu, torch::Tensor dh) {
+torch::Tensor swiglu_bwd(torch::Tensor gu, torch::Tensor dh, c10::optional<torch::Tensor> amax) {
   check_bf16_cuda(gu, "gate_up");
   check_bf16_cuda(dh, "dh");
   const int F = gu.size(-1) / 2;
   const long T = gu.numel() / (2 * F);
   auto dgu = torch::empty_like(gu);
   const long work = T * (F / 8);
-  if (work == 0) return dgu;
-  hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(grid_for(work, 256)), dim3(256), 0, at::hip::getCurrentHIPStream(),
+  const int g = grid_for(work, 256);
+  const AmaxOut am(amax, g, gu);
+  if (work == 0) {
+    am.finalize(0);
+    return dgu;
+  }
+  hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(g), dim3(256), 0, at::hip::getCurrentHIPStream(),
                      reinterpret_cast<const bf16_t*>(gu.data_ptr()), reinterpret_cast<const bf16_t*>(dh.data_ptr()),
-                     reinterpret_cast<bf16_t*>(dgu.data_ptr()), T, F);
+                     reinterpret_cast<bf16_t*>(dgu.data_ptr()), T, F, am.ptr());
+  am.finalize(g);
   return dgu;
 }
 

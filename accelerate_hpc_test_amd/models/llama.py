@@ -23,6 +23,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops.fp8 import fp8_tensorwise
 from ..ops.fused import apply_rope, cross_entropy, flash_attention_qkv, rms_norm, rope_tables, swiglu
 
 
@@ -89,10 +90,10 @@ class RMSNorm(nn.Module):
         self.weight = nn.Parameter(torch.ones(hidden_size))
         self.eps = eps
 
-    def forward(self, x, residual=None):
+    def forward(self, x, residual=None, amax: bool = False, grad_amax: bool = False):
         # fp32 weights under autocast (DDP mixed precision): the fused kernel runs in the activation dtype.
         w = self.weight if self.weight.dtype == x.dtype else self.weight.to(x.dtype)
-        return rms_norm(x, w, self.eps, residual)
+        return rms_norm(x, w, self.eps, residual, amax=amax, grad_amax=grad_amax)
 
 
 class LlamaAttention(nn.Module):
@@ -132,7 +133,8 @@ class LlamaMLP(nn.Module):
         self.down_proj = nn.Linear(cfg.intermediate_size, cfg.hidden_size, bias=False)
 
     def forward(self, x):
-        return self.down_proj(swiglu(self.gate_up_proj(x)))
+        h = swiglu(self.gate_up_proj(x), amax=fp8_tensorwise(self.down_proj), grad_amax=fp8_tensorwise(self.gate_up_proj))
+        return self.down_proj(h)
 
 
 class LlamaDecoderLayer(nn.Module):
@@ -145,10 +147,15 @@ class LlamaDecoderLayer(nn.Module):
         self.mlp = LlamaMLP(cfg)
 
     def forward(self, hidden, residual, cos, sin, position_ids=None):
-        x, residual = self.input_layernorm(hidden, residual)
-        hidden = self.self_attn(x, cos, sin, position_ids)
-        x, residual = self.post_attention_layernorm(hidden, residual)
-        hidden = self.mlp(x)
+        # fp8 producer amax: each norm tags its output for the fp8 projection it feeds and its input gradient for the
+        # fp8 projection that produced `hidden` (the previous layer's down_proj, this layer's o_proj)
+        attn, mlp = self.self_attn, self.mlp
+        x, residual = self.input_layernorm(hidden, residual, amax=fp8_tensorwise(attn.qkv_proj),
+                                           grad_amax=residual is not None and fp8_tensorwise(mlp.down_proj))
+        hidden = attn(x, cos, sin, position_ids)
+        x, residual = self.post_attention_layernorm(hidden, residual, amax=fp8_tensorwise(mlp.gate_up_proj),
+                                                    grad_amax=fp8_tensorwise(attn.o_proj))
+        hidden = mlp(x)
         return hidden, residual
 
 
@@ -219,7 +226,7 @@ class LlamaForCausalLM(nn.Module):
         residual = None
         for layer in self.layers:
             h, residual = layer(h, residual, cos, sin, position_ids)
-        h, _ = self.norm(h, residual)
+        h, _ = self.norm(h, residual, grad_amax=len(self.layers) > 0 and fp8_tensorwise(self.layers[-1].mlp.down_proj))
         logits = self.lm_head(h)
         loss = None
         if shift_labels is None and labels is not None:

@@ -23,6 +23,7 @@ The module filter follows the reference: first and last `nn.Linear` are skipped 
 
 from __future__ import annotations
 
+import os
 from typing import Callable, NamedTuple, Optional
 
 import torch
@@ -47,6 +48,28 @@ def amax(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
 
 def scale_from_amax(a: torch.Tensor, fp8_max: float, margin: int = 0) -> torch.Tensor:
     return (fp8_max / (2.0**margin)) / a.clamp_min(1e-12)
+
+
+def tag_amax(t: torch.Tensor, amax: torch.Tensor) -> torch.Tensor:
+    """Attach a producer-computed abs-max (fp32 [1], device) to `t`: an fp8 linear consuming `t` as its input (or as
+    its output gradient) then skips its own amax pass over it. Valid only while `t` is unmodified (version check)."""
+    t._acc_amax = (amax, t._version)
+    return t
+
+
+def producer_amax(t: torch.Tensor) -> Optional[torch.Tensor]:
+    a = getattr(t, "_acc_amax", None)
+    if a is None or a[1] != t._version:
+        return None
+    return a[0]
+
+
+def fp8_tensorwise(m) -> bool:
+    """Whether module `m` runs a per-tensor-scaled fp8 GEMM now (the consumer of a producer amax). Producer amax is
+    switched off with ACCELERATE_FP8_PRODUCER_AMAX=0 (then every fp8 linear runs its own amax pass)."""
+    rec = getattr(m, "fp8_recipe", None)
+    return (isinstance(m, Fp8Linear) and rec is not None and not rec.mx and _FP8_ON[0]
+            and os.environ.get("ACCELERATE_FP8_PRODUCER_AMAX", "1") != "0")
 
 
 class Scale(NamedTuple):
@@ -255,9 +278,10 @@ class Fp8Recipe:
     def fwd_e5m2(self):
         return self.fmt == "E5M2"
 
-    def scale(self, key: str, x: torch.Tensor, fp8_max: float) -> Scale:
-        """Dynamic: this tensor's amax. Delayed: the history's max (or most recent), then the history is rolled."""
-        cur = amax(x)
+    def scale(self, key: str, x: torch.Tensor, fp8_max: float, hint: Optional[torch.Tensor] = None) -> Scale:
+        """Dynamic: this tensor's amax (`hint`: already computed by the kernel that produced x). Delayed: the history's
+        max (or most recent), then the history is rolled."""
+        cur = hint if hint is not None else amax(x)
         qmax = fp8_max / (2.0**self.margin)
         if not self.delayed:
             return Scale(cur, qmax)
@@ -281,7 +305,7 @@ class _Fp8LinearFn(torch.autograd.Function):
         x2 = x.reshape(-1, shape[-1])
         N = w.shape[0]
         fwd_max = E5M2_MAX if recipe.fwd_e5m2() else E4M3_MAX
-        sx = recipe.scale("x", x2, fwd_max)
+        sx = recipe.scale("x", x2, fwd_max, producer_amax(x))
         x8, x8t = cast(x2, sx, recipe.fwd_e5m2(), transpose=True)
         ctx.pre_quantised = w_amax is not None
         if ctx.pre_quantised:
@@ -310,7 +334,7 @@ class _Fp8LinearFn(torch.autograd.Function):
         N = dy.shape[-1]
         dy2 = dy.reshape(-1, N).contiguous().to(torch.bfloat16)
         gmax = E5M2_MAX if recipe.grad_e5m2() else E4M3_MAX
-        sg = recipe.scale("g", dy2, gmax)
+        sg = recipe.scale("g", dy2, gmax, producer_amax(dy))
         dy8, dy8t = cast(dy2, sg, recipe.grad_e5m2(), transpose=True)
         dx = gemm(dy8, w8t, sg, sw, None, torch.bfloat16)
         db = dy2.float().sum(0).to(dy.dtype) if ctx.has_bias else None

@@ -24,38 +24,61 @@ def rms_norm_reference(x, weight, eps, residual=None):
     return y.to(x.dtype), x
 
 
+def _amax_buf(like: torch.Tensor, want: bool):
+    return torch.empty(1, dtype=torch.float32, device=like.device) if want else None
+
+
 class _RMSNormFn(torch.autograd.Function):
+    """`amax` / `grad_amax`: also produce max|y| (forward) / max|dx| (backward) for a consuming fp8 linear (its input /
+    its output gradient), tagged on the tensor (ops/fp8.py `tag_amax`) instead of re-read by a separate amax pass."""
+
     @staticmethod
-    def forward(ctx, x, weight, eps, residual):
+    def forward(ctx, x, weight, eps, residual, amax=False, grad_amax=False):
         e = ext()
         shape = x.shape
         x2 = x.reshape(-1, shape[-1]).contiguous()
         r2 = residual.reshape(-1, shape[-1]).contiguous() if residual is not None else None
-        y, rstd, res_out = e.rmsnorm_fwd(x2, r2, weight.contiguous(), eps)
+        am = _amax_buf(x, amax)
+        y, rstd, res_out = e.rmsnorm_fwd(x2, r2, weight.contiguous(), eps, am)
         normed_input = res_out if residual is not None else x2
         ctx.save_for_backward(normed_input, weight, rstd)
         ctx.has_res = residual is not None
         ctx.shape = shape
+        ctx.grad_amax = grad_amax
+        if am is None:
+            am = torch.empty(0, device=x.device)
+        ctx.mark_non_differentiable(am)
         if residual is not None:
-            return y.view(shape), res_out.view(shape)
-        return y.view(shape), None
+            return y.view(shape), res_out.view(shape), am
+        return y.view(shape), None, am
 
     @staticmethod
-    def backward(ctx, dy, dres):
+    def backward(ctx, dy, dres, _dam):
         x, w, rstd = ctx.saved_tensors
         e = ext()
         H = ctx.shape[-1]
         d2 = dres.reshape(-1, H).contiguous() if (dres is not None and ctx.has_res) else None
-        dx, dw = e.rmsnorm_bwd(dy.reshape(-1, H).contiguous(), x, w.contiguous(), rstd, d2)
+        am = _amax_buf(x, ctx.grad_amax)
+        dx, dw = e.rmsnorm_bwd(dy.reshape(-1, H).contiguous(), x, w.contiguous(), rstd, d2, am)
         dx = dx.view(ctx.shape)
+        if am is not None:
+            from .fp8 import tag_amax
+
+            tag_amax(dx, am)
         # d(x + residual) flows to both summands.
-        return dx, dw, None, (dx if ctx.has_res else None)
+        return dx, dw, None, (dx if ctx.has_res else None), None, None
 
 
-def rms_norm(x: torch.Tensor, weight: torch.Tensor, eps: float = 1e-6, residual: Optional[torch.Tensor] = None):
-    """y = RMSNorm(x [+ residual]) * weight. Returns (y, residual_out) where residual_out = x + residual (or x)."""
+def rms_norm(x: torch.Tensor, weight: torch.Tensor, eps: float = 1e-6, residual: Optional[torch.Tensor] = None,
+             amax: bool = False, grad_amax: bool = False):
+    """y = RMSNorm(x [+ residual]) * weight. Returns (y, residual_out) where residual_out = x + residual (or x).
+    `amax` / `grad_amax`: tag y / the input gradient with their abs-max for a consuming fp8 linear (HIP path only)."""
     if use_native(x) and x.dtype == torch.bfloat16 and x.shape[-1] % 8 == 0:
-        y, r = _RMSNormFn.apply(x, weight, eps, residual)
+        y, r, am = _RMSNormFn.apply(x, weight, eps, residual, amax, grad_amax)
+        if amax:
+            from .fp8 import tag_amax
+
+            tag_amax(y, am)
         return y, (r if residual is not None else x)
     return rms_norm_reference(x, weight, eps, residual)
 
@@ -70,20 +93,39 @@ def swiglu_reference(gu):
 
 class _SwiGLUFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, gu):
+    def forward(ctx, gu, amax=False, grad_amax=False):
         gu = gu.contiguous()
         ctx.save_for_backward(gu)
-        return ext().swiglu_fwd(gu)
+        ctx.grad_amax = grad_amax
+        am = _amax_buf(gu, amax)
+        h = ext().swiglu_fwd(gu, am)
+        if am is None:
+            am = torch.empty(0, device=gu.device)
+        ctx.mark_non_differentiable(am)
+        return h, am
 
     @staticmethod
-    def backward(ctx, dh):
+    def backward(ctx, dh, _dam):
         (gu,) = ctx.saved_tensors
-        return ext().swiglu_bwd(gu, dh.contiguous())
+        am = _amax_buf(gu, ctx.grad_amax)
+        dgu = ext().swiglu_bwd(gu, dh.contiguous(), am)
+        if am is not None:
+            from .fp8 import tag_amax
+
+            tag_amax(dgu, am)
+        return dgu, None, None
 
 
-def swiglu(gu: torch.Tensor) -> torch.Tensor:
+def swiglu(gu: torch.Tensor, amax: bool = False, grad_amax: bool = False) -> torch.Tensor:
+    """silu(gate) * up on a fused [..., 2F] projection. `amax` / `grad_amax` as in `rms_norm` (for the fp8 down / gate-up
+    projections that consume the output / produce the input)."""
     if use_native(gu) and gu.dtype == torch.bfloat16 and (gu.shape[-1] // 2) % 8 == 0:
-        return _SwiGLUFn.apply(gu)
+        h, am = _SwiGLUFn.apply(gu, amax, grad_amax)
+        if amax:
+            from .fp8 import tag_amax
+
+            tag_amax(h, am)
+        return h
     return swiglu_reference(gu)
 
 

@@ -850,6 +850,41 @@ def test_e2e_fp8_hip_training_matches_pytorch_quantisation_emulation(monkeypatch
         assert abs(a - b) <= 1e-1 * abs(b), (i, hip_n, ref_n)
 
 
+def test_fp8_producer_amax_kernels_and_bit_exact_training(monkeypatch):
+    """RMSNorm fwd/bwd and SwiGLU fwd/bwd emit the abs-max of what they store (= a separate amax pass, bit for bit),
+    and fp8 training with the producer amax is bit-identical to training with every fp8 linear's own amax pass."""
+    from accelerate_hpc_test_amd.ops import fp8
+
+    torch.manual_seed(0)
+    e = _ext.ext()
+    x = torch.randn(300, 4096, device=DEV, dtype=torch.bfloat16) * 3
+    res = torch.randn_like(x)
+    w = torch.rand(4096, device=DEV, dtype=torch.bfloat16) + 0.5
+    am = torch.empty(1, device=DEV)
+    y, rstd, ro = e.rmsnorm_fwd(x, res, w, 1e-5, am)
+    assert am.item() == y.float().abs().max().item()
+    dy = torch.randn_like(x)
+    dx, _ = e.rmsnorm_bwd(dy, ro, w, rstd, res, am)
+    assert am.item() == dx.float().abs().max().item()
+    gu = torch.randn(1000, 2 * 1024, device=DEV, dtype=torch.bfloat16) * 2
+    h = e.swiglu_fwd(gu, am)
+    assert am.item() == h.float().abs().max().item()
+    dgu = e.swiglu_bwd(gu, torch.randn_like(h), am)
+    assert am.item() == dgu.float().abs().max().item()
+    e.swiglu_fwd(gu[:0], am)
+    assert am.item() == 0.0
+    calls = []
+    orig = fp8.amax
+    monkeypatch.setattr(fp8, "amax", lambda t, out=None: calls.append(t.numel()) or orig(t, out))
+    on = _train_curve(monkeypatch, "llama-small", "fp8", native=True, steps=3, lr=3e-4)
+    n_on = len(calls)
+    monkeypatch.setenv("ACCELERATE_FP8_PRODUCER_AMAX", "0")
+    calls.clear()
+    off = _train_curve(monkeypatch, "llama-small", "fp8", native=True, steps=3, lr=3e-4)
+    assert on == off, (on, off)
+    assert n_on < len(calls) / 3, (n_on, len(calls))  # only o_proj's input and qkv's gradient keep their own pass
+
+
 def test_h2d_engine_pinned_source_lives_until_dma_completes():
     """csrc/runtime/h2d_engine.cpp: a pinned source is released only after ITS copy event completed (advisor finding:
     it used to be dropped right after enqueueing the wait), pageable sources after the staging drain."""
