@@ -27,6 +27,7 @@
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include "common.h"
+#include <cstdlib>
 
 using namespace acc;
 
@@ -174,11 +175,12 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(FwdParams p) {
   constexpr int kTile = 64 * kRow;  // 16 KB per operand image
   __shared__ __attribute__((aligned(1024))) char k0s[kTile], v0s[kTile], k1s[kTile], v1s[kTile];
   const int nqt = p.S / 128;
-  // grid = (Hq, S/128, B): heads vary fastest, so the heaviest causal tiles of EVERY head are dispatched first
-  const int qt = CAUSAL ? (nqt - 1 - (int)blockIdx.y) : (int)blockIdx.y;
   const int h = xcd_head(blockIdx.x, p.Hq), b = blockIdx.z;
   const int kh = h / (p.Hq / p.Hkv);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hf = lane >> 5;
+  // grid = (Hq, S/128, B): heads vary fastest, so the heaviest causal tiles of EVERY head are dispatched first (a
+  // paired layout — q-tiles y and nqt-1-y in one workgroup, equal work everywhere — measured 3% slower)
+  const int qt = CAUSAL ? (nqt - 1 - (int)blockIdx.y) : (int)blockIdx.y;
   const int qw0 = qt * 128 + wave * 32;
   const bf16_t* qb = p.q + b * p.q_bs + (long)h * kD;
   const bf16_t* kb_ = p.k + b * p.k_bs + (long)kh * kD;

@@ -48,6 +48,7 @@ class _RMSNormFn(torch.autograd.Function):
         if am is None:
             am = torch.empty(0, device=x.device)
         ctx.mark_non_differentiable(am)
+        ctx.set_materialize_grads(False)  # no zero-filled gradients for the amax / unused residual outputs
         if residual is not None:
             return y.view(shape), res_out.view(shape), am
         return y.view(shape), None, am
@@ -57,6 +58,8 @@ class _RMSNormFn(torch.autograd.Function):
         x, w, rstd = ctx.saved_tensors
         e = ext()
         H = ctx.shape[-1]
+        if dy is None:  # y unused: only the residual stream carries a gradient
+            dy = torch.zeros(ctx.shape, dtype=x.dtype, device=x.device)
         d2 = dres.reshape(-1, H).contiguous() if (dres is not None and ctx.has_res) else None
         am = _amax_buf(x, ctx.grad_amax)
         dx, dw = e.rmsnorm_bwd(dy.reshape(-1, H).contiguous(), x, w.contiguous(), rstd, d2, am)
@@ -102,11 +105,14 @@ class _SwiGLUFn(torch.autograd.Function):
         if am is None:
             am = torch.empty(0, device=gu.device)
         ctx.mark_non_differentiable(am)
+        ctx.set_materialize_grads(False)
         return h, am
 
     @staticmethod
     def backward(ctx, dh, _dam):
         (gu,) = ctx.saved_tensors
+        if dh is None:
+            return None, None, None
         am = _amax_buf(gu, ctx.grad_amax)
         dgu = ext().swiglu_bwd(gu, dh.contiguous(), am)
         if am is not None:
