@@ -1300,6 +1300,12 @@ class _FusedWgradLinearFn(torch.autograd.Function):
         # contiguous along the contraction) instead of the both-token-major one. Llama-3-8B layer, four GEMMs
         # (tools/bench_wgrad_layout.py): fp32 output (world size 1) 2.93 vs 3.50 ms, bf16 output (flat grad buffer,
         # world size > 1) 2.86 vs 3.44 ms; the HIP transpose costs ~0.2 ms.
+        # Memory: for q/k/v, gate/up and down projections the copy replaces the saved x (their inputs are not saved by
+        # the producing RMSNorm / SwiGLU), but o_proj's input is the attention output that flash attention also keeps,
+        # so there the copy is extra: T x 4096 bf16 = 64 MiB per layer, 2 GiB for Llama-3-8B at 8k tokens (peak
+        # 175 of 288 GiB; kept for the faster layout). ACCELERATE_FSDP_WGRAD_XT=0 disables it. The opt-in hipBLASLt
+        # wgrad runner (ACCELERATE_BLASLT_WGRAD=1) takes contiguous [T, K] inputs only, so it is bypassed (torch's GEMM
+        # runs) whenever the transposed copy is in use.
         ctx.x_transposed = (_WGRAD_XT and x2.is_cuda and x2.dtype == torch.bfloat16 and x2.is_contiguous() and native_enabled()
                             and x2.shape[0] % 64 == 0 and x2.shape[1] % 64 == 0)
         ctx.save_for_backward(ext().transpose_bf16(x2) if ctx.x_transposed else x, weight)
