@@ -620,7 +620,9 @@ def check_dispatch_batches_matches_upstream():
     from accelerate_hpc_test_amd.state import PartialState
 
     PartialState(cpu=True)
+    UpState._reset_state()  # a parent process may have left a single-process upstream state behind (forked Borg dict)
     UpState(cpu=True)
+    assert UpState().num_processes == PartialState().num_processes
 
     class It(IterableDataset):
         def __init__(self, n):

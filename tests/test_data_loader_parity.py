@@ -99,6 +99,13 @@ def test_prepare_single_process_matches_upstream():
 
     PartialState(cpu=True)
     UpState(cpu=True)
+    try:
+        _prepare_single_process_cases(PartialState, UpState)
+    finally:
+        UpState._reset_state()  # do not leak a one-process upstream state into later (forking) tests
+
+
+def _prepare_single_process_cases(PartialState, UpState):
     for n, bs, drop_last, shuffle in itertools.product((9, 16), (2, 4), (False, True), (False, True)):
         g1, g2 = torch.Generator().manual_seed(3), torch.Generator().manual_seed(3)
         dl1 = DataLoader(list(range(n)), batch_size=bs, drop_last=drop_last, shuffle=shuffle, generator=g1, num_workers=0)
