@@ -7,55 +7,10 @@
 // and baseline x86-64 (`target_clones`), picked at load time for the host it runs on.
 #include <torch/extension.h>
 
-#include <cmath>
-#include <cstdint>
-#include <cstring>
+#include "host_kernels.h"
 
-namespace {
-
-struct Hyper {
-  float lr, beta1, beta2, eps, wd, bc1, bc2_sqrt;
-  bool adamw;
-};
-
-inline uint16_t to_bf16_rne(float f) {
-  uint32_t u;
-  std::memcpy(&u, &f, 4);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fc0;  // NaN stays NaN
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return static_cast<uint16_t>(u >> 16);
-}
-
-__attribute__((target_clones("avx512f", "avx2", "default")))
-void adam_range(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
-                uint16_t* __restrict__ shadow, int64_t n, Hyper h) {
-  const float step_size = h.lr / h.bc1, bc2s = h.bc2_sqrt, decay = 1.f - h.lr * h.wd;
-  const float b1 = h.beta1, b2 = h.beta2, c1 = 1.f - h.beta1, c2 = 1.f - h.beta2;
-  constexpr int64_t kBlock = 1 << 14;
-  const int64_t nblk = (n + kBlock - 1) / kBlock;
-#pragma omp parallel for schedule(static)
-  for (int64_t b = 0; b < nblk; ++b) {
-    const int64_t lo = b * kBlock, hi = std::min(n, lo + kBlock);
-#pragma omp simd
-    for (int64_t i = lo; i < hi; ++i) {
-      float pf = p[i], gf = g[i];
-      if (!h.adamw) gf += h.wd * pf;
-      const float mf = b1 * m[i] + c1 * gf;
-      const float vf = b2 * v[i] + c2 * gf * gf;
-      if (h.adamw) pf *= decay;
-      pf -= step_size * mf / (std::sqrt(vf) / bc2s + h.eps);
-      m[i] = mf;
-      v[i] = vf;
-      p[i] = pf;
-    }
-    if (shadow != nullptr) {
-#pragma omp simd
-      for (int64_t i = lo; i < hi; ++i) shadow[i] = to_bf16_rne(p[i]);
-    }
-  }
-}
-
-}  // namespace
+using acc_host::Hyper;
+using acc_host::adam_range;
 
 // In-place AdamW/Adam step over contiguous fp32 CPU tensors; `shadow` (bf16, same numel) receives the updated params.
 void cpu_adam_step(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, c10::optional<torch::Tensor> shadow,

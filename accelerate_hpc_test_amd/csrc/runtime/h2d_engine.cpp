@@ -7,6 +7,7 @@
 // engine's own HIP stream. A per-slot HIP event gates slot reuse, so CPU copies, PCIe DMA and GPU compute all
 // overlap. Consumers order against the uploads with `wait_on_current_stream()` (hipStreamWaitEvent on the
 // caller's torch stream — no host blocking).
+#include "host_kernels.h"
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include <hip/hip_runtime.h>
@@ -219,31 +220,6 @@ class H2DEngine {
   bool stop_ = false;
 };
 
-// Rolling FNV-1a hash over the sequence of collectives a rank issued (op, group size, dtype, numel). In debug
-// mode ranks compare it every N steps, catching a desynchronised collective order before RCCL deadlocks.
-class CollectiveSeq {
- public:
-  void record(const std::string& op, int64_t group, int64_t dtype, int64_t numel) {
-    auto mix = [this](uint64_t v) {
-      for (int i = 0; i < 8; ++i) {
-        h_ ^= (v >> (8 * i)) & 0xff;
-        h_ *= 1099511628211ull;
-      }
-    };
-    for (char c : op) mix((uint64_t)(unsigned char)c);
-    mix((uint64_t)group);
-    mix((uint64_t)dtype);
-    mix((uint64_t)numel);
-    ++count_;
-  }
-  uint64_t digest() const { return h_; }
-  int64_t count() const { return count_; }
-  void reset() { h_ = 1469598103934665603ull; count_ = 0; }
-
- private:
-  uint64_t h_ = 1469598103934665603ull;
-  int64_t count_ = 0;
-};
 
 }  // namespace
 
@@ -257,10 +233,10 @@ void register_runtime(pybind11::module& m) {
       .def("inflight", &H2DEngine::inflight)
       .def_property_readonly("slot_bytes", &H2DEngine::slot_bytes)
       .def_property_readonly("num_slots", &H2DEngine::num_slots);
-  pybind11::class_<CollectiveSeq>(m, "CollectiveSeq")
+  pybind11::class_<acc_host::CollectiveSeq>(m, "CollectiveSeq")
       .def(pybind11::init<>())
-      .def("record", &CollectiveSeq::record)
-      .def("digest", &CollectiveSeq::digest)
-      .def("count", &CollectiveSeq::count)
-      .def("reset", &CollectiveSeq::reset);
+      .def("record", &acc_host::CollectiveSeq::record)
+      .def("digest", &acc_host::CollectiveSeq::digest)
+      .def("count", &acc_host::CollectiveSeq::count)
+      .def("reset", &acc_host::CollectiveSeq::reset);
 }
