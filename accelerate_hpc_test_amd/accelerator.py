@@ -330,7 +330,14 @@ class Accelerator:
         if self.state.mixed_precision == "fp16" and self.device.type != "cpu":
             self.native_amp = True
             kwargs = self.scaler_handler.to_kwargs() if self.scaler_handler is not None else {}
-            self.scaler = torch.amp.GradScaler("cuda", **kwargs)
+            from .ops._ext import native_enabled
+
+            if native_enabled():
+                from .ops.amp import HipGradScaler  # unscale + overflow check on the multi-tensor HIP kernel
+
+                self.scaler = HipGradScaler("cuda", **kwargs)
+            else:
+                self.scaler = torch.amp.GradScaler("cuda", **kwargs)
         elif self.state.mixed_precision in ("bf16", "fp8"):
             self.native_amp = True
         elif self.state.mixed_precision == "fp16" and self.device.type == "cpu":

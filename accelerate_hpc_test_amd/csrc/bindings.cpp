@@ -22,6 +22,8 @@ void adam_multi_tensor(torch::Tensor meta, torch::Tensor block_prefix, int64_t n
 int64_t multi_tensor_chunk();
 void sqnorm_multi_tensor(torch::Tensor meta, torch::Tensor block_prefix, int64_t nblocks, int64_t gdtype, torch::Tensor out,
                          bool accumulate);
+void unscale_multi_tensor(torch::Tensor meta, torch::Tensor block_prefix, int64_t nblocks, int64_t gdtype, torch::Tensor inv_scale,
+                          torch::Tensor found_inf);
 void clip_multi_tensor(torch::Tensor meta, torch::Tensor block_prefix, int64_t nblocks, int64_t gdtype, torch::Tensor total_sq,
                        double max_norm);
 // flash_attn.hip
@@ -82,6 +84,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("multi_tensor_chunk", &multi_tensor_chunk);
   m.def("sqnorm_multi_tensor", &sqnorm_multi_tensor);
   m.def("clip_multi_tensor", &clip_multi_tensor);
+  m.def("unscale_multi_tensor", &unscale_multi_tensor);
   m.def("flash_attn_fwd", &flash_attn_fwd);
   m.def("flash_attn_bwd", &flash_attn_bwd);
   m.def("fp8_amax", &fp8_amax);

@@ -231,6 +231,28 @@ __global__ __launch_bounds__(kMTThreads) void clip_mt_kernel(const TensorMeta* _
   for (int64_t i = start + threadIdx.x; i < end; i += kMTThreads) g[i] = from_f<G>(to_f<G>(g[i]) * coef);
 }
 
+// AMP unscale + overflow check (torch GradScaler's `_amp_foreach_non_finite_check_and_unscale_`): g *= inv_scale in
+// place; any non-finite result sets found_inf[0] = 1. The flag is written with a plain store by every workgroup that
+// saw one (all write the same value), so no atomics and no extra pass.
+template <typename G>
+__global__ __launch_bounds__(kMTThreads) void unscale_mt_kernel(const TensorMeta* __restrict__ meta,
+                                                                const int64_t* __restrict__ block_prefix, int ntensors,
+                                                                const float* __restrict__ inv_scale, float* __restrict__ found_inf) {
+  const int t = find_tensor(block_prefix, ntensors, blockIdx.x);
+  const TensorMeta tm = meta[t];
+  const int64_t start = (int64_t)(blockIdx.x - block_prefix[t]) * kChunk;
+  const int64_t end = min(start + (int64_t)kChunk, tm.n);
+  const float inv = inv_scale[0];
+  G* g = reinterpret_cast<G*>(tm.g);
+  bool bad = false;
+  for (int64_t i = start + threadIdx.x; i < end; i += kMTThreads) {
+    const float v = to_f<G>(g[i]) * inv;
+    bad |= !isfinite(v);
+    g[i] = from_f<G>(v);
+  }
+  if (__syncthreads_or(bad) && threadIdx.x == 0) found_inf[0] = 1.f;
+}
+
 }  // namespace
 
 // ----------------------------------------------------------------------------------------- host API
@@ -319,4 +341,21 @@ void clip_multi_tensor(torch::Tensor meta, torch::Tensor block_prefix, int64_t n
     hipLaunchKernelGGL(clip_mt_kernel<float>, dim3(nblocks), dim3(kMTThreads), 0, stream, mp, bp, nt, total_sq.data_ptr<float>(), (float)max_norm);
   else
     hipLaunchKernelGGL(clip_mt_kernel<bf16_t>, dim3(nblocks), dim3(kMTThreads), 0, stream, mp, bp, nt, total_sq.data_ptr<float>(), (float)max_norm);
+}
+
+// grads *= inv_scale[0]; found_inf[0] = 1 if any result is inf / NaN (found_inf is NOT cleared here: torch semantics).
+void unscale_multi_tensor(torch::Tensor meta, torch::Tensor block_prefix, int64_t nblocks, int64_t gdtype, torch::Tensor inv_scale,
+                          torch::Tensor found_inf) {
+  const int nt = meta.size(0);
+  if (nt == 0 || nblocks == 0) return;
+  TORCH_CHECK(inv_scale.scalar_type() == at::kFloat && found_inf.scalar_type() == at::kFloat, "unscale: fp32 scale / flag");
+  auto stream = at::hip::getCurrentHIPStream();
+  const TensorMeta* mp = reinterpret_cast<const TensorMeta*>(meta.data_ptr<int64_t>());
+  const int64_t* bp = block_prefix.data_ptr<int64_t>();
+  if (gdtype == 0)
+    hipLaunchKernelGGL(unscale_mt_kernel<float>, dim3(nblocks), dim3(kMTThreads), 0, stream, mp, bp, nt, inv_scale.data_ptr<float>(),
+                       found_inf.data_ptr<float>());
+  else
+    hipLaunchKernelGGL(unscale_mt_kernel<bf16_t>, dim3(nblocks), dim3(kMTThreads), 0, stream, mp, bp, nt, inv_scale.data_ptr<float>(),
+                       found_inf.data_ptr<float>());
 }

@@ -206,6 +206,27 @@ def clip_grads_by_total_sq(params, total_sq: torch.Tensor, max_norm: float):
             e.clip_multi_tensor(meta, prefix, nb, _DT[dt], total_sq, max_norm)
 
 
+@torch.no_grad()
+def unscale_and_check(grads: list, inv_scale: torch.Tensor, found_inf: torch.Tensor):
+    """In-place `g *= inv_scale` over a list of same-device grads, setting `found_inf` (fp32 [1]) to 1 when any result is
+    inf / NaN — one HIP launch per grad dtype (torch's `_amp_foreach_non_finite_check_and_unscale_`)."""
+    grads = [g for g in grads if g is not None and g.numel() > 0]
+    if not grads:
+        return
+    if not use_native(grads[0]):
+        torch._amp_foreach_non_finite_check_and_unscale_(grads, found_inf, inv_scale)
+        return
+    e, dev = ext(), grads[0].device
+    for dt in (torch.float32, torch.bfloat16):
+        rows = [(0, g.data_ptr(), 0, 0, 0, g.numel()) for g in grads if g.dtype == dt]
+        if rows:
+            meta, prefix, nb = _CACHE.get(rows, dev)
+            e.unscale_multi_tensor(meta, prefix, nb, _DT[dt], inv_scale, found_inf)
+    other = [g for g in grads if g.dtype not in _DT]
+    if other:  # fp16 grads (fp16 master weights): torch's kernel
+        torch._amp_foreach_non_finite_check_and_unscale_(other, found_inf, inv_scale)
+
+
 class CpuFusedAdamStep:
     """Adam/AdamW for CPU-resident fp32 params (FSDP CPU offload): the native OpenMP kernel
     (`csrc/runtime/cpu_adam.cpp`), one call per parameter, also writing the bf16 upload copy when the engine attached

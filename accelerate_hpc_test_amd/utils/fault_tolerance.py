@@ -123,6 +123,24 @@ def check_collective_sequence(group=None):
 
 
 # ------------------------------------------------------------------------------------------------ watchdog
+def abort_communicators() -> bool:
+    """Abort every RCCL communicator of this process (torch `_abort_process_group`): kernels and host waits of
+    collectives in flight end with an error here and, through RCCL's abort path, on the peers blocked in the same
+    collective, instead of hanging until the process-group timeout. Returns whether an abort was issued."""
+    try:
+        import torch.distributed as dist
+        from torch.distributed.distributed_c10d import _abort_process_group
+
+        if not (dist.is_available() and dist.is_initialized()):
+            return False
+        _abort_process_group()
+        return True
+    except Exception as exc:  # noqa: BLE001 - best effort on the way out of a hung job
+        sys.stderr.write(f"[accelerate watchdog] communicator abort failed: {exc!r}\n")
+        return False
+
+
+
 class StepWatchdog:
     """Host-side hang detector fed by training-step heartbeats (see module docstring)."""
 
@@ -130,7 +148,7 @@ class StepWatchdog:
         self.timeout = float(timeout)
         self.rank = rank
         self.exit_code = exit_code
-        self.action = action  # "exit" or "warn"
+        self.action = action  # "exit", "abort" (abort the RCCL communicators first, then exit) or "warn"
         self.poll = poll if poll is not None else max(0.05, min(5.0, self.timeout / 10))
         self._last = time.monotonic()
         self._tag = "start"
@@ -171,7 +189,9 @@ class StepWatchdog:
             faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
             sys.stderr.flush()
             self.fired = True
-            if self.action == "exit":
+            if self.action == "abort":
+                abort_communicators()
+            if self.action in ("exit", "abort"):
                 os._exit(self.exit_code)
             self._last = time.monotonic()  # warn mode: report again after another full timeout
 

@@ -885,6 +885,52 @@ def test_fp8_producer_amax_kernels_and_bit_exact_training(monkeypatch):
     assert n_on < len(calls) / 3, (n_on, len(calls))  # only o_proj's input and qkv's gradient keep their own pass
 
 
+@pytest.mark.parametrize("poison", [None, "inf", "nan"])
+def test_hip_grad_scaler_unscale_matches_torch(poison):
+    """HipGradScaler (multi-tensor HIP unscale + overflow flag) against torch.amp.GradScaler over fp32 and bf16 grads,
+    chunk-boundary sizes, and an inf / NaN planted in one tensor: same unscaled grads, same skip decision, same scale."""
+    from accelerate_hpc_test_amd.ops.amp import HipGradScaler
+
+    torch.manual_seed(0)
+    shapes = [(8191,), (8192,), (8193,), (64, 300), (3,)]
+
+    def make():
+        return [torch.nn.Parameter(torch.randn(s, device=DEV)) for s in shapes]
+
+    a, b = make(), make()
+    for x, y in zip(a, b):
+        y.data.copy_(x.data)
+        x.grad = torch.randn_like(x) * 1024
+        y.grad = x.grad.clone()
+    # bf16 grads: torch's CUDA/HIP unscale kernel does not take them, ours does (compared to the exact 1/1024 below)
+    hb = torch.nn.Parameter(torch.randn(5000, device=DEV, dtype=torch.bfloat16))
+    hb.grad = (torch.randn(5000, device=DEV) * 1024).to(torch.bfloat16)
+    hb_expect = (hb.grad.float() / 1024).to(torch.bfloat16)
+    a.append(hb)
+    if poison is not None:
+        val = float(poison)
+        a[2].grad[8192] = val
+        b[2].grad[8192] = val
+    oa, ob = torch.optim.SGD(a, lr=0.1), torch.optim.SGD(b, lr=0.1)
+    sa, sb = HipGradScaler("cuda", init_scale=1024.0), torch.amp.GradScaler("cuda", init_scale=1024.0)
+    sa.scale(torch.ones((), device=DEV))  # initialises the scale tensors, as scaler.scale(loss).backward() does
+    sb.scale(torch.ones((), device=DEV))
+    sa.unscale_(oa)
+    sb.unscale_(ob)
+    assert torch.equal(hb.grad, hb_expect)
+    for x, y in zip(a, b):
+        assert torch.equal(x.grad.isfinite(), y.grad.isfinite())
+        m = y.grad.isfinite()
+        assert torch.equal(x.grad[m], y.grad[m])
+    sa.step(oa)
+    sb.step(ob)
+    sa.update()
+    sb.update()
+    assert sa.get_scale() == sb.get_scale()
+    for x, y in zip(a, b):
+        assert torch.equal(x.data, y.data)
+
+
 def test_h2d_engine_pinned_source_lives_until_dma_completes():
     """csrc/runtime/h2d_engine.cpp: a pinned source is released only after ITS copy event completed (advisor finding:
     it used to be dropped right after enqueueing the wait), pageable sources after the staging drain."""

@@ -100,6 +100,46 @@ def test_watchdog_kills_injected_hang_in_subprocess():
     assert time.time() - t0 < 100
 
 
+def test_watchdog_abort_releases_peer_blocked_in_collective():
+    """Two gloo ranks: rank 1 hangs before its all-reduce; its watchdog (action "abort") aborts the communicators and
+    exits 86, and rank 0 — blocked in the same all-reduce — gets an error instead of hanging until the PG timeout."""
+    script = textwrap.dedent(
+        f"""
+        import os, sys, time, torch, torch.distributed as dist
+        sys.path.insert(0, {ROOT!r})
+        from accelerate_hpc_test_amd.utils.fault_tolerance import StepWatchdog
+        rank = int(sys.argv[1])
+        dist.init_process_group("gloo", init_method="tcp://127.0.0.1:" + sys.argv[2], rank=rank, world_size=2)
+        dist.barrier()
+        if rank == 1:
+            StepWatchdog(2.0, rank=1, action="abort", poll=0.1)
+            time.sleep(120)  # hung before the collective
+        try:
+            dist.all_reduce(torch.ones(4))
+            print("completed", flush=True)
+        except Exception as exc:
+            print("collective failed:", type(exc).__name__, flush=True)
+            sys.exit(3)
+        """
+    )
+    from accelerate_hpc_test_amd.utils.other import get_free_port
+
+    port = str(get_free_port())
+    t0 = time.time()
+    procs = [subprocess.Popen([sys.executable, "-c", script, str(r), port], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                              text=True) for r in range(2)]
+    try:
+        outs = [p.communicate(timeout=90) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert procs[1].returncode == 86, outs[1][1][-2000:]
+    assert "[accelerate watchdog] rank 1" in outs[1][1]
+    assert procs[0].returncode == 3 and "collective failed" in outs[0][0], (procs[0].returncode, outs[0])
+    assert time.time() - t0 < 80
+
+
 def test_collective_log_digest_is_order_sensitive():
     log = CollectiveLog()
     log.record("all_reduce", 2, torch.float32, 10)
