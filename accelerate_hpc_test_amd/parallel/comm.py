@@ -36,16 +36,32 @@ def duplicate_group(group=None):
     first and each distinct list is created, in the same order everywhere (HSDP / mesh sub-groups included)."""
     ranks = tuple(dist.get_process_group_ranks(group if group is not None else dist.group.WORLD))
     world = dist.get_world_size()
+    opts = _high_priority_options()
     if world == 1:
-        return dist.new_group([0])
+        return dist.new_group([0], pg_options=opts)
     lists = [None] * world
     dist.all_gather_object(lists, ranks)
     mine = None
     for rl in sorted(set(tuple(r) for r in lists)):
-        g = dist.new_group(list(rl))
+        g = dist.new_group(list(rl), pg_options=opts)
         if rl == ranks:
             mine = g
     return mine
+
+
+def _high_priority_options():
+    """RCCL process-group options with the communicator's internal HIP streams at high priority (the collectives'
+    kernels then win dispatch against queued compute kernels), unless ACCELERATE_RCCL_STREAM_PRIORITY=0. None on gloo."""
+    import os
+
+    if dist.get_backend() != "nccl" or os.environ.get("ACCELERATE_RCCL_STREAM_PRIORITY", "-1") == "0":
+        return None
+    try:
+        opts = dist.ProcessGroupNCCL.Options()
+        opts.is_high_priority_stream = True
+        return opts
+    except Exception:  # noqa: BLE001 - a build without the NCCL/RCCL backend
+        return None
 
 
 # ------------------------------------------------------------------------------------------------ raw collectives
