@@ -132,7 +132,7 @@ def save_accelerator_state(output_dir, model_states: list, optimizers: list, sch
         sampler = _seedable_sampler(dl)
         if sampler is not None:
             save({"epoch": sampler.epoch, "initial_seed": sampler.initial_seed}, lay.sampler(k), **node_kw)
-        if hasattr(dl, "state_dict"):
+        if getattr(dl, "use_stateful_dataloader", False):  # position within the epoch: only for stateful loaders
             save(dl.state_dict(), lay.dataloader(k), **node_kw)
     if scaler is not None:
         torch.save(scaler.state_dict(), lay.scaler())
@@ -171,7 +171,7 @@ def load_accelerator_state(input_dir, models, optimizers, schedulers, dataloader
         if sampler is not None and lay.sampler(k).exists():
             saved = load(lay.sampler(k))
             sampler.epoch, sampler.initial_seed = saved["epoch"], saved["initial_seed"]
-        if lay.dataloader(k).exists() and hasattr(dl, "load_state_dict"):
+        if getattr(dl, "use_stateful_dataloader", False) and lay.dataloader(k).exists():
             dl.load_state_dict(load(lay.dataloader(k)))
     logger.info("All dataloader sampler states loaded successfully")
     if scaler is not None:

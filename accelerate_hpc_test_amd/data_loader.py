@@ -414,6 +414,7 @@ class DataLoaderShard(DataLoaderStateMixin, DataLoader):
         self._non_blocking = _non_blocking
         self.iteration = 0
         self.prefetch_to_device = prefetch_to_device
+        self.use_stateful_dataloader = use_stateful_dataloader
         self._batches_yielded = 0
         self._resume_skip = 0
 
@@ -457,6 +458,7 @@ class DataLoaderShard(DataLoaderStateMixin, DataLoader):
                 index += 1
                 current = nxt
             self.iteration += 1
+            self._batches_yielded = 0  # a finished epoch resumes at the start of the next one
             self.end()
         finally:  # also on early exit (break / exception / generator collected): stop the prefetch worker
             if isinstance(it, DevicePrefetcher):
@@ -547,7 +549,9 @@ class DataLoaderDispatcher(DataLoaderStateMixin, DataLoader):
         self.torch_device_mesh = torch_device_mesh
         self.slice_fn = slice_tensors if slice_fn is None else slice_fn
         self.iteration = 0
+        self.use_stateful_dataloader = use_stateful_dataloader
         self._batches_yielded = 0
+        self._resume_skip = 0
 
     _MIXED_SIZES = ("You can't use batches of different size with `dispatch_batches=True` or when using an `IterableDataset`. "
                     "Either pass `dispatch_batches=False` and have each process fetch its own batch or pass "
@@ -588,6 +592,8 @@ class DataLoaderDispatcher(DataLoaderStateMixin, DataLoader):
         self.begin()
         self.set_epoch(self.iteration)
         P, r = self.state.num_processes, self.state.process_index
+        skip = self.skip_batches + self._resume_skip  # a restored position applies to this pass only
+        self._resume_skip = 0
         it = super().__iter__() if r == 0 else None
         head = None  # first P samples of the epoch: pad a final global batch that does not split evenly
         cur, index = self._next_global(it), 0
@@ -605,12 +611,13 @@ class DataLoaderDispatcher(DataLoaderStateMixin, DataLoader):
             if last:
                 self.end_of_dataloader = True
                 self.remainder = seen
-            if index >= self.skip_batches:
+            if index >= skip:
                 self._batches_yielded = index + 1
                 yield mine
             index += 1
             cur = nxt
         self.iteration += 1
+        self._batches_yielded = 0
         self.end()
 
     def set_epoch(self, epoch: int):
@@ -658,7 +665,7 @@ class DataLoaderDispatcher(DataLoaderStateMixin, DataLoader):
 
     def load_state_dict(self, state_dict):
         self.iteration = state_dict.get("iteration", 0)
-        self.skip_batches = state_dict.get("batches_yielded", 0)
+        self._resume_skip = state_dict.get("batches_yielded", 0)
 
 
 def get_sampler(dataloader):
@@ -776,7 +783,8 @@ def prepare_data_loader(
     if rng_types is not None and shard.generator is None:
         rng_types = [r for r in rng_types if r != "generator"]  # nothing to synchronise
     kwargs = _rebuild_kwargs(dataloader, shard, num_processes, split_batches, dispatch_batches)
-    common = {"_drop_last": dataloader.drop_last, "_non_blocking": non_blocking}
+    common = {"_drop_last": dataloader.drop_last, "_non_blocking": non_blocking,
+              "use_stateful_dataloader": use_stateful_dataloader}
     if dispatch_batches:
         kwargs.pop("generator", None)  # only rank 0 draws samples
         dataloader = DataLoaderDispatcher(shard.dataset, split_batches=split_batches, batch_sampler=shard.batch_sampler,

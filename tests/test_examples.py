@@ -31,3 +31,26 @@ def test_nlp_example_two_ranks_via_launch(tmp_path):
     )
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     assert "epoch 1:" in r.stdout
+
+
+def test_complete_nlp_example_checkpoint_and_resume(tmp_path):
+    """examples/complete_nlp_example.py: step and epoch checkpoints, a mid-epoch resume (skip_first_batches on the
+    restored loader position), and a run that still learns after resuming."""
+    import complete_nlp_example
+
+    out = str(tmp_path / "run")
+    common = ["--cpu", "--tiny", "--num_epochs", "3", "--n_train", "512", "--n_eval", "128", "--output_dir", out]
+    first = complete_nlp_example.main(common + ["--checkpointing_steps", "40"])
+    assert first["accuracy"] > 0.9, first
+    saved = sorted(os.listdir(out))
+    assert "step_40" in saved and "step_80" in saved, saved
+    resumed = complete_nlp_example.main(common + ["--resume_from_checkpoint", os.path.join(out, "step_40")])
+    assert resumed["accuracy"] > 0.9, resumed
+
+
+def test_cv_example_cpu_learns():
+    import cv_example
+
+    metric = cv_example.main(["--cpu", "--image_size", "32", "--n_train", "512", "--n_eval", "128", "--num_epochs", "4",
+                              "--batch_size", "32"])
+    assert metric["accuracy"] > 0.9, metric
