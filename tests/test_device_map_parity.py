@@ -124,3 +124,27 @@ def test_fallback_allocation_judge_case():
     got = ours.infer_auto_device_map(model, max_memory=dict(budget), fallback_allocation=True)
     assert dict(got) == dict(ref)
     assert 0 in got.values()
+
+
+@pytest.mark.parametrize("dtype", [None, torch.float16, "float16", torch.int8, torch.float8_e4m3fn])
+def test_size_helpers_match_upstream(dtype):
+    """`utils/modeling.py` size helpers (rewritten: one pass crediting every name prefix, dtype width table) against
+    upstream `compute_module_sizes` / `dtype_byte_size` / `convert_file_size_to_int`."""
+    from accelerate_hpc_test_amd.utils import modeling as me
+
+    m = nn.Sequential(nn.Linear(8, 16), nn.BatchNorm1d(16), nn.Embedding(10, 4).to(torch.bfloat16))
+    m.register_buffer("np", torch.zeros(3, dtype=torch.int64), persistent=False)
+    assert dict(me.compute_module_sizes(m, dtype=dtype)) == dict(upstream.compute_module_sizes(m, dtype=dtype))
+    assert dict(me.compute_module_sizes(m, dtype=dtype, buffers_only=True)) == dict(
+        upstream.compute_module_sizes(m, dtype=dtype, buffers_only=True))
+    for d in (torch.float32, torch.bfloat16, torch.bool, torch.int64, torch.float8_e5m2, "float16", "int8"):
+        assert me.dtype_byte_size(d) == upstream.dtype_byte_size(d)
+    for s in (123, "1GB", "1Gb", "2.5GiB", "10MB", "7KiB", "3kb", "5MiB"):
+        assert me.convert_file_size_to_int(s) == upstream.convert_file_size_to_int(s)
+    for bad in ("12", "xGB", -1):
+        with pytest.raises(ValueError):
+            me.convert_file_size_to_int(bad)
+    # the module's own non-persistent set is never extended with descendants' names
+    before = set(m._non_persistent_buffers_set)
+    assert me.get_non_persistent_buffers(m, recurse=True, fqns=True) >= {"np"}
+    assert m._non_persistent_buffers_set == before
