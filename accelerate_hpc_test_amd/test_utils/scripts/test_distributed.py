@@ -880,9 +880,24 @@ def check_fsdp_fp8_all_gather(force_sharded: bool = False):
             opt.zero_grad()
             losses.append(loss.item())
         results[ag] = (losses, acc.get_state_dict(model))
-    assert results[False][0] == results[True][0], (results[False][0], results[True][0])
-    for n, t in results[False][1].items():
-        assert torch.equal(t, results[True][1][n]), n
+    if W <= 2:
+        # two-rank sums are order-free, so the two layouts must agree bit for bit
+        assert results[False][0] == results[True][0], (results[False][0], results[True][0])
+        for n, t in results[False][1].items():
+            assert torch.equal(t, results[True][1][n]), n
+    else:
+        # W >= 3: the fp8 region changes the flat layout, so an element's ring reduce-scatter sums its W terms in a
+        # different order in the two runs (fp32 rounding differences only). The first step's forward uses the
+        # initial weights, so the gathered fp8 weights themselves must still match exactly; later steps see the
+        # rounding through the next per-tensor fp8 scale (the toy run climbs steeply at lr 1e-2, amplifying it)
+        assert results[False][0][0] == results[True][0][0], (results[False][0], results[True][0])
+        for a, b in zip(results[False][0], results[True][0]):
+            assert abs(a - b) <= 1e-2 * abs(a), (results[False][0], results[True][0])
+        for n, t in results[False][1].items():
+            d = (t.float() - results[True][1][n].float()).abs()
+            # Adam moves a near-zero-gradient element by up to lr per step whatever the rounding, so bound the
+            # worst element by 3 steps x lr and the average by a small fraction of the weights' size
+            assert float(d.max()) <= 3e-2 and float(d.mean()) <= 2e-2 * float(t.float().abs().mean()) + 1e-5, (n, float(d.max()), float(d.mean()), float(t.float().abs().mean()))
 
 
 def check_ddp_powersgd():

@@ -149,3 +149,12 @@ def test_local_sgd():
 
 def test_fsdp_three_ranks():
     debug_launcher(td.check_fsdp_matches_single, args=(True, "SHARDED_STATE_DICT"), num_processes=3)
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_fsdp_ddp_at_node_scale(world):
+    """The 1/2/4/8-GPU bench's rank counts on the gloo fake cluster: FSDP sharded training + checkpoint vs one process,
+    the fp8 all-gather vs the bf16 all-gather (uneven shard boundaries at W = 8), DDP vs one process."""
+    debug_launcher(td.check_fsdp_matches_single, args=(True, "SHARDED_STATE_DICT"), num_processes=world)
+    debug_launcher(td.check_fsdp_fp8_all_gather, args=(False,), num_processes=world)
+    debug_launcher(td.check_ddp_matches_single, num_processes=world)
