@@ -728,9 +728,12 @@ class Accelerator:
                 raise ValueError("Ulysses SP: the model exposes no `attention_impl` hook; wrap the step in "
                                  "`parallel.ulysses.ulysses_sdpa_context` for SDPA-based models.")
         if not evaluation_mode:
-            if self.distributed_type in (DistributedType.MULTI_GPU, DistributedType.MULTI_CPU):
+            # RcclKwargs.ddp_force: one process with an initialised group still gets the reducer (nranks=1 RCCL)
+            force_ddp = (self.rccl_handler.ddp_force and self.num_processes == 1 and self.distributed_type == DistributedType.NO
+                         and torch.distributed.is_available() and torch.distributed.is_initialized())
+            if self.distributed_type in (DistributedType.MULTI_GPU, DistributedType.MULTI_CPU) or force_ddp:
                 dp_size = self.parallelism_config.data_parallel_size if self.parallelism_config is not None else self.num_processes
-                if any(p.requires_grad for p in model.parameters()) and self.num_processes > 1 and dp_size > 1:
+                if any(p.requires_grad for p in model.parameters()) and (force_ddp or (self.num_processes > 1 and dp_size > 1)):
                     kwargs = self.ddp_handler.to_kwargs() if self.ddp_handler is not None else {}
                     from .parallel.ddp import DistributedDataParallel
 
@@ -751,6 +754,7 @@ class Accelerator:
                         comm_hook=comm_hook,
                         comm_wrapper=comm_wrapper,
                         comm_state_option=self.ddp_handler.comm_state_option if self.ddp_handler is not None else None,
+                        own_communicator=force_ddp,
                     )
                     self._models[-1] = model
             elif self.distributed_type == DistributedType.FSDP:

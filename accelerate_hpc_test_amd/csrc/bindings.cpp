@@ -12,6 +12,8 @@ torch::Tensor transpose_bf16(torch::Tensor x);
 torch::Tensor swiglu_bwd(torch::Tensor gu, torch::Tensor dh, c10::optional<torch::Tensor> amax);
 void rope_inplace(torch::Tensor qkv, torch::Tensor cos, torch::Tensor sin, c10::optional<torch::Tensor> pos,
                   int64_t n_rot_heads, int64_t n_heads_total, int64_t head_dim, double sign);
+torch::Tensor rope_out(torch::Tensor src, torch::Tensor cos, torch::Tensor sin, c10::optional<torch::Tensor> pos,
+                       int64_t n_rot_heads, int64_t n_heads_total, int64_t head_dim, double sign);
 // xent_optim.hip
 std::vector<torch::Tensor> xent_fwd(torch::Tensor logits, torch::Tensor labels, int64_t ignore_index);
 void xent_bwd(torch::Tensor logits, torch::Tensor labels, torch::Tensor lse, torch::Tensor scale, torch::Tensor out,
@@ -78,6 +80,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("transpose_bf16", &transpose_bf16);
   m.def("swiglu_bwd", &swiglu_bwd, pybind11::arg("gu"), pybind11::arg("dh"), pybind11::arg("amax") = pybind11::none());
   m.def("rope_inplace", &rope_inplace);
+  m.def("rope_out", &rope_out);
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd", &xent_bwd);
   m.def("adam_multi_tensor", &adam_multi_tensor);

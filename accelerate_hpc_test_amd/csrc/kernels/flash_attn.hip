@@ -317,6 +317,12 @@ struct BwdParams {
   long dq_ts, dq_bs, dk_ts, dk_bs, dv_ts, dv_bs;
   int S, Hq, Hkv;
   float scale_log2, scale, inv_scale;
+  // delta_out != nullptr: the dQ kernel computes delta = rowsum(dO * O) itself from the dO fragments it already holds
+  // plus O read at the same positions, and stores it for the dK / dV kernel that follows on the stream (no separate
+  // delta pass over O and dO)
+  const bf16_t* o;
+  long o_ts, o_bs;
+  float* delta_out;
 };
 
 template <bool CAUSAL>
@@ -342,7 +348,22 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(BwdParams p) {
   }
   const long st = ((long)b * p.Hq + h) * p.S + qw0 + r;
   const float lse2 = p.lse[st] * kLog2e;
-  const float dlt = p.delta[st];
+  float dlt;
+  if (p.delta_out != nullptr) {
+    // lane (r, hf) holds dO[qw0 + r, 16 s + 8 hf + j]: dot with O at the same places, then join the two halves
+    const bf16_t* ob = p.o + b * p.o_bs + (long)h * kD + (long)(qw0 + r) * p.o_ts + 8 * hf;
+    float acc = 0.f;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const v8bf of = *reinterpret_cast<const v8bf*>(ob + 16 * s);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc = fmaf(static_cast<float>(df[s][j]), static_cast<float>(of[j]), acc);
+    }
+    dlt = acc + __shfl_xor(acc, 32, 64);
+    if (hf == 0) p.delta_out[st] = dlt;
+  } else {
+    dlt = p.delta[st];
+  }
   f32x16 dq[4];
 #pragma unroll
   for (int d = 0; d < 4; ++d) zero(dq[d]);
@@ -644,7 +665,8 @@ void flash_attn_bwd(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch:
   TORCH_CHECK(S % 128 == 0, "flash_attn: sequence length must be a multiple of 128");
   auto stream = at::hip::getCurrentHIPStream();
   auto delta = torch::empty({B, Hq, S}, q.options().dtype(torch::kFloat32));
-  {
+  const bool fused_delta = g_attn_dbg == 0 || !causal;  // the diagnostic variants may skip the dQ kernel
+  if (!fused_delta) {
     const long rows = (long)B * S * Hq;
     hipLaunchKernelGGL(attn_delta_kernel, dim3((rows + 3) / 4), dim3(256), 0, stream,
                        reinterpret_cast<const bf16_t*>(o.data_ptr()), o.stride(1), o.stride(0),
@@ -659,7 +681,9 @@ void flash_attn_bwd(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch:
               dout.stride(0), lse.data_ptr<float>(), delta.data_ptr<float>(), reinterpret_cast<bf16_t*>(dq.data_ptr()),
               reinterpret_cast<bf16_t*>(dk.data_ptr()), reinterpret_cast<bf16_t*>(dv.data_ptr()), dq.stride(1),
               dq.stride(0), dk.stride(1), dk.stride(0), dv.stride(1), dv.stride(0), S, Hq, Hkv,
-              (float)(softmax_scale * kLog2e), (float)softmax_scale, (float)(1.0 / softmax_scale)};
+              (float)(softmax_scale * kLog2e), (float)softmax_scale, (float)(1.0 / softmax_scale),
+              reinterpret_cast<const bf16_t*>(o.data_ptr()), o.stride(1), o.stride(0),
+              fused_delta ? delta.data_ptr<float>() : nullptr};
   const dim3 dq_grid(Hq, S / 128, B), kv_grid(Hkv * (S / 128), B);
   if (causal && g_attn_dbg != 0) {  // diagnostic timing variants (tools/bench_attn.py --dbg)
     if (g_attn_dbg & 8) hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, dq_grid, dim3(256), 0, stream, p);

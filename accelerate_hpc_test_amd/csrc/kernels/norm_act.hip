@@ -232,38 +232,41 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const bf16_t* __restric
 }
 
 // ---------------------------------------------------------------------------------------------------
-// RoPE in place on qkv [T, (Hq + 2*Hkv) * D] (rotate-half pairs (i, i + D/2)); heads [0, Hq + Hkv) are
-// rotated (Q and K), V untouched. cos/sin tables are fp32 [S, D/2]; position = pos[t] (or t % S).
-// sign = +1 forward, -1 backward (inverse rotation of the incoming gradient).
+// RoPE on qkv [T, (Hq + 2*Hkv) * D] (rotate-half pairs (i, i + D/2)); heads [0, Hq + Hkv) are rotated (Q and K),
+// V passes through. cos/sin tables are fp32 [S, D/2]; position = pos[t] (or t % S). sign = +1 forward, -1 backward
+// (inverse rotation of the incoming gradient). Out of place (src != dst: one read + one write of the whole row, V
+// copied) or in place (src == dst, heads_iter = n_rot_heads: V never touched).
 // ---------------------------------------------------------------------------------------------------
-__global__ void rope_kernel(bf16_t* __restrict__ qkv, const float* __restrict__ cosb, const float* __restrict__ sinb,
-                            const int64_t* __restrict__ pos, long T, int S, int n_rot_heads, int n_heads_total,
-                            int D, float sign) {
+__global__ void rope_kernel(const bf16_t* __restrict__ src, bf16_t* __restrict__ dst, const float* __restrict__ cosb,
+                            const float* __restrict__ sinb, const int64_t* __restrict__ pos, long T, int S,
+                            int n_rot_heads, int heads_iter, int n_heads_total, int D, float sign) {
   const int half = D >> 1;
   const int nvec = half >> 2;  // 4 pairs per thread step (8 B of each half)
-  const long per_row = (long)n_rot_heads * nvec;
+  const long per_row = (long)heads_iter * nvec;
   const long total = T * per_row;
   for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
     const long t = idx / per_row;
     const int rem = (int)(idx - t * per_row);
     const int h = rem / nvec, c = rem - h * nvec;
-    const long p = pos != nullptr ? pos[t] : (t % S);
-    bf16_t* base = qkv + (t * n_heads_total + h) * (long)D;
-    bf16x4 a = reinterpret_cast<bf16x4*>(base)[c];
-    bf16x4 b = reinterpret_cast<bf16x4*>(base + half)[c];
-    const float4 cs = reinterpret_cast<const float4*>(cosb + p * half)[c];
-    const float4 sn = reinterpret_cast<const float4*>(sinb + p * half)[c];
-    const float cc[4] = {cs.x, cs.y, cs.z, cs.w};
-    const float ss[4] = {sn.x * sign, sn.y * sign, sn.z * sign, sn.w * sign};
-    bf16x4 oa, ob;
+    const long off = (t * n_heads_total + h) * (long)D;
+    const bf16x4 a = reinterpret_cast<const bf16x4*>(src + off)[c];
+    const bf16x4 b = reinterpret_cast<const bf16x4*>(src + off + half)[c];
+    bf16x4 oa = a, ob = b;
+    if (h < n_rot_heads) {
+      const long p = pos != nullptr ? pos[t] : (t % S);
+      const float4 cs = reinterpret_cast<const float4*>(cosb + p * half)[c];
+      const float4 sn = reinterpret_cast<const float4*>(sinb + p * half)[c];
+      const float cc[4] = {cs.x, cs.y, cs.z, cs.w};
+      const float ss[4] = {sn.x * sign, sn.y * sign, sn.z * sign, sn.w * sign};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float x1 = bf2f(a.v[j]), x2 = bf2f(b.v[j]);
-      oa.v[j] = f2bf(x1 * cc[j] - x2 * ss[j]);
-      ob.v[j] = f2bf(x2 * cc[j] + x1 * ss[j]);
+      for (int j = 0; j < 4; ++j) {
+        const float x1 = bf2f(a.v[j]), x2 = bf2f(b.v[j]);
+        oa.v[j] = f2bf(x1 * cc[j] - x2 * ss[j]);
+        ob.v[j] = f2bf(x2 * cc[j] + x1 * ss[j]);
+      }
     }
-    reinterpret_cast<bf16x4*>(base)[c] = oa;
-    reinterpret_cast<bf16x4*>(base + half)[c] = ob;
+    reinterpret_cast<bf16x4*>(dst + off)[c] = oa;
+    reinterpret_cast<bf16x4*>(dst + off + half)[c] = ob;
   }
 }
 
@@ -433,23 +436,46 @@ torch::Tensor swiglu_bwd(torch::Tensor gu, torch::Tensor dh, c10::optional<torch
   return dgu;
 }
 
-void rope_inplace(torch::Tensor qkv, torch::Tensor cos, torch::Tensor sin, c10::optional<torch::Tensor> pos,
-                  int64_t n_rot_heads, int64_t n_heads_total, int64_t head_dim, double sign) {
-  check_bf16_cuda(qkv, "qkv");
+static void rope_launch(const torch::Tensor& src, torch::Tensor& dst, const torch::Tensor& cos, const torch::Tensor& sin,
+                        const c10::optional<torch::Tensor>& pos, int64_t n_rot_heads, int64_t n_heads_total,
+                        int64_t head_dim, double sign) {
+  check_bf16_cuda(src, "qkv");
+  check_bf16_cuda(dst, "out");
+  TORCH_CHECK(src.numel() == dst.numel(), "rope: src / dst size mismatch");
   TORCH_CHECK(cos.scalar_type() == at::kFloat && sin.scalar_type() == at::kFloat, "rope tables must be fp32");
   TORCH_CHECK(head_dim % 8 == 0, "rope: head_dim must be a multiple of 8");
-  const long T = qkv.numel() / (n_heads_total * head_dim);
+  TORCH_CHECK(src.numel() % (n_heads_total * head_dim) == 0 && n_rot_heads <= n_heads_total, "rope: bad head counts");
+  const long T = src.numel() / (n_heads_total * head_dim);
   const int S = cos.size(0);
+  TORCH_CHECK(cos.numel() >= (long)S * (head_dim / 2) && sin.numel() == cos.numel(), "rope: tables must be [S, D/2]");
   const int64_t* posp = nullptr;
   if (pos.has_value()) {
     TORCH_CHECK(pos->scalar_type() == at::kLong && pos->numel() == T, "rope: positions must be int64 [T]");
     posp = pos->data_ptr<int64_t>();
   }
-  const long work = T * n_rot_heads * (head_dim / 8);
+  const bool inplace = src.data_ptr() == dst.data_ptr();
+  const int heads_iter = (int)(inplace ? n_rot_heads : n_heads_total);
+  const long work = T * heads_iter * (head_dim / 8);
   if (work == 0) return;
   hipLaunchKernelGGL(rope_kernel, dim3(grid_for(work, 256)), dim3(256), 0, at::hip::getCurrentHIPStream(),
-                     reinterpret_cast<bf16_t*>(qkv.data_ptr()), cos.data_ptr<float>(), sin.data_ptr<float>(), posp, T,
-                     S, (int)n_rot_heads, (int)n_heads_total, (int)head_dim, (float)sign);
+                     reinterpret_cast<const bf16_t*>(src.data_ptr()), reinterpret_cast<bf16_t*>(dst.data_ptr()),
+                     cos.data_ptr<float>(), sin.data_ptr<float>(), posp, T, S, (int)n_rot_heads, heads_iter,
+                     (int)n_heads_total, (int)head_dim, (float)sign);
+}
+
+void rope_inplace(torch::Tensor qkv, torch::Tensor cos, torch::Tensor sin, c10::optional<torch::Tensor> pos,
+                  int64_t n_rot_heads, int64_t n_heads_total, int64_t head_dim, double sign) {
+  TORCH_CHECK(qkv.is_contiguous(), "rope_inplace: qkv must be contiguous");
+  rope_launch(qkv, qkv, cos, sin, pos, n_rot_heads, n_heads_total, head_dim, sign);
+}
+
+// Out-of-place RoPE: a new contiguous tensor (one pass over src instead of clone + in-place rotation).
+torch::Tensor rope_out(torch::Tensor src, torch::Tensor cos, torch::Tensor sin, c10::optional<torch::Tensor> pos,
+                       int64_t n_rot_heads, int64_t n_heads_total, int64_t head_dim, double sign) {
+  auto s = src.contiguous();
+  auto out = torch::empty_like(s);
+  rope_launch(s, out, cos, sin, pos, n_rot_heads, n_heads_total, head_dim, sign);
+  return out;
 }
 
 // ------------------------------------------------------------------------------------------------ transpose

@@ -179,21 +179,19 @@ def rope_reference(qkv, cos, sin, n_rot_heads, positions=None):
 class _RopeFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qkv, cos, sin, n_rot_heads, positions):
-        qkv = qkv.contiguous().clone()
+        # out of place: one read + one write of qkv (V heads copied through), not a clone followed by an in-place pass
         B, S, Htot, D = qkv.shape
         pos = positions.reshape(-1).contiguous() if positions is not None else None
-        ext().rope_inplace(qkv, cos, sin, pos, n_rot_heads, Htot, D, 1.0)
+        out = ext().rope_out(qkv, cos, sin, pos, n_rot_heads, Htot, D, 1.0)
         ctx.save_for_backward(cos, sin, pos if pos is not None else torch.empty(0))
         ctx.meta = (n_rot_heads, Htot, D, pos is not None)
-        return qkv
+        return out
 
     @staticmethod
     def backward(ctx, g):
         cos, sin, pos = ctx.saved_tensors
         n_rot, Htot, D, has_pos = ctx.meta
-        g = g.contiguous().clone()
-        ext().rope_inplace(g, cos, sin, pos if has_pos else None, n_rot, Htot, D, -1.0)
-        return g, None, None, None, None
+        return ext().rope_out(g, cos, sin, pos if has_pos else None, n_rot, Htot, D, -1.0), None, None, None, None
 
 
 def apply_rope(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, n_rot_heads: int, positions=None):

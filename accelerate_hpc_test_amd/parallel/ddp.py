@@ -67,6 +67,7 @@ class DistributedDataParallel(nn.Module):
         comm_wrapper: DDPCommunicationHookType = DDPCommunicationHookType.NO,
         bucket_bytes: Optional[int] = None,
         comm_state_option: Optional[dict] = None,
+        own_communicator: bool = False,
         **unused,
     ):
         super().__init__()
@@ -96,7 +97,7 @@ class DistributedDataParallel(nn.Module):
         # bucket all-reduces run on comm_stream through their own communicator (parallel/comm.duplicate_group), so
         # they never share an RCCL communicator with collectives issued from other streams
         self.comm_group = process_group
-        if self.is_cuda and not self.is_gloo and self.world_size > 1:
+        if self.is_cuda and not self.is_gloo and (self.world_size > 1 or own_communicator):
             from .comm import duplicate_group
 
             self.comm_group = duplicate_group(process_group)

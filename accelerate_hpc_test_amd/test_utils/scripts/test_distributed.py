@@ -1021,3 +1021,39 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def check_ddp_forced_single_rank():
+    """RcclKwargs(ddp_force=True) at world size 1: the model goes through the DDP reducer (buckets, hooks, a one-rank
+    all-reduce) and trains exactly like the unwrapped model."""
+    import torch.nn as nn
+
+    from accelerate_hpc_test_amd import Accelerator
+    from accelerate_hpc_test_amd.parallel.ddp import DistributedDataParallel
+    from accelerate_hpc_test_amd.state import AcceleratorState, GradientState
+    from accelerate_hpc_test_amd.utils import RcclKwargs
+
+    assert torch.distributed.is_initialized() and torch.distributed.get_world_size() == 1
+    res = {}
+    for force in (False, True):
+        AcceleratorState._reset_state(True)
+        GradientState._reset_state()
+        acc = Accelerator(cpu=True, kwargs_handlers=[RcclKwargs(ddp_force=force)])
+        torch.manual_seed(0)
+        m = nn.Sequential(nn.Linear(16, 32), nn.ReLU(), nn.Linear(32, 1))
+        opt = torch.optim.AdamW(m.parameters(), lr=1e-2)
+        m, opt = acc.prepare(m, opt)
+        assert isinstance(m, DistributedDataParallel) == force, type(m)
+        g = torch.Generator().manual_seed(1)
+        losses = []
+        for _ in range(3):
+            x, y = torch.randn(8, 16, generator=g), torch.randn(8, 1, generator=g)
+            loss = ((m(x) - y) ** 2).mean()
+            acc.backward(loss)
+            opt.step()
+            opt.zero_grad()
+            losses.append(loss.item())
+        res[force] = (losses, {k: v.clone() for k, v in acc.unwrap_model(m).state_dict().items()})
+    assert res[False][0] == res[True][0], (res[False][0], res[True][0])
+    for k, v in res[False][1].items():
+        assert torch.equal(v, res[True][1][k]), k

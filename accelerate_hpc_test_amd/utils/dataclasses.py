@@ -307,6 +307,10 @@ class RcclKwargs(KwargsHandler):
       all-gather / reduce-scatter with nranks=1, bf16 flat gradient buffers) instead of the degenerate no-collective
       path; needs an initialised process group (`ACCELERATE_FSDP_FORCE_SHARDED`). Used to measure and test the sharded
       path on one GPU.
+    - `ddp_force`: at world size 1 with an initialised process group, wrap the model in this framework's DDP reducer
+      anyway (flat buckets, post-accumulate hooks, RCCL all-reduce with nranks=1 on the reducer's own communicator and
+      side stream) instead of leaving it unwrapped (`ACCELERATE_DDP_FORCE`). Used to measure and test the DDP path on
+      one GPU.
     """
 
     ddp_bucket_mb: int = None
@@ -316,6 +320,7 @@ class RcclKwargs(KwargsHandler):
     collective_check_interval: int = None
     fsdp_optimizer_overlap: bool = None
     fsdp_force_sharded: bool = None
+    ddp_force: bool = None
 
     def __post_init__(self):
         if self.ddp_bucket_mb is None:
@@ -332,6 +337,8 @@ class RcclKwargs(KwargsHandler):
             self.fsdp_optimizer_overlap = parse_flag_from_env("ACCELERATE_FSDP_OPTIMIZER_OVERLAP", False)
         if self.fsdp_force_sharded is None:
             self.fsdp_force_sharded = parse_flag_from_env("ACCELERATE_FSDP_FORCE_SHARDED", False)
+        if self.ddp_force is None:
+            self.ddp_force = parse_flag_from_env("ACCELERATE_DDP_FORCE", False)
 
 
 # ---------------------------------------------------------------------------------------------------

@@ -47,6 +47,9 @@ def parse():
     p.add_argument("--fsdp-force-sharded", action="store_true",
                    help="at 1 GPU: run the FSDP engine's multi-GPU code path (full buffers resized 0<->full, RCCL "
                         "all-gather / reduce-scatter with nranks=1, bf16 flat grads) instead of the no-collective shortcut")
+    p.add_argument("--ddp-force", action="store_true",
+                   help="with --parallel ddp at 1 GPU: wrap the model in the DDP reducer anyway (buckets, hooks, RCCL "
+                        "all-reduce with nranks=1 on its own communicator) instead of running it unwrapped")
     p.add_argument("--fsdp-cpu-offload", action="store_true",
                    help="FSDP CPU offload: fp32 master/grad shards + AdamW state in pinned host memory, host AdamW")
     p.add_argument("--verbose", action="store_true")
@@ -98,13 +101,15 @@ def main():
     )
     overlap = args.optimizer_overlap == "on" and args.parallel == "fsdp"
     force = args.fsdp_force_sharded and args.parallel == "fsdp"
-    if force and int(os.environ.get("WORLD_SIZE", "1")) == 1 and not torch.distributed.is_initialized():
+    force_ddp = args.ddp_force and args.parallel == "ddp"
+    if (force or force_ddp) and int(os.environ.get("WORLD_SIZE", "1")) == 1 and not torch.distributed.is_initialized():
         # a one-rank RCCL process group so the sharded path has real collectives to issue
         torch.cuda.set_device(0)
         port = int(os.environ.get("MASTER_PORT", "29533"))
         torch.distributed.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
                                              device_id=torch.device("cuda", 0))
-    handlers = [RcclKwargs(fsdp_prefetch_depth=args.prefetch, fsdp_optimizer_overlap=overlap, fsdp_force_sharded=force)]
+    handlers = [RcclKwargs(fsdp_prefetch_depth=args.prefetch, fsdp_optimizer_overlap=overlap, fsdp_force_sharded=force,
+                           ddp_force=force_ddp)]
     if args.parallel == "ddp":
         from accelerate_hpc_test_amd.utils import DDPCommunicationHookType, DistributedDataParallelKwargs
 
@@ -204,7 +209,8 @@ def main():
                 "moe": {"experts": cfg.num_local_experts, "top_k": cfg.num_experts_per_tok} if is_moe else None,
                 "global_batch": args.mbs * world,
                 "seq_len": args.seq,
-                "parallelism": f"{args.parallel}{world}" + ("-forced-sharded" if force else ""),
+                "parallelism": f"{args.parallel}{world}" + ("-forced-sharded" if force else "")
+                + ("-forced-reducer" if force_ddp else ""),
                 "optimizer": "AdamW(lr=1e-5), fp32 master" + (", per-unit update overlapped with backward" if overlap else "")
                 + (", CPU-offloaded (host AdamW)" if args.fsdp_cpu_offload else ""),
                 "activation_checkpointing": args.activation_checkpointing,

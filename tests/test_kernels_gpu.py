@@ -750,6 +750,44 @@ def test_fsdp_forced_sharded_matches_degenerate(one_rank_rccl, monkeypatch, wgra
             assert d.max() <= 2 * 3 * 1e-3 and d.mean() < 5e-5, (n, d.max(), d.mean())
 
 
+def test_ddp_forced_reducer_matches_unwrapped(one_rank_rccl):
+    """RcclKwargs(ddp_force=True) on one GPU: llama-tiny through the DDP reducer (flat buckets, post-accumulate hooks,
+    RCCL all-reduce with nranks=1 on the reducer's own communicator and side stream) trains bit-identically to the
+    unwrapped model (BASELINE config 'Llama-3 8B DDP bf16' path, bench.py --parallel ddp --ddp-force)."""
+    from accelerate_hpc_test_amd import Accelerator
+    from accelerate_hpc_test_amd.models.llama import LLAMA_PRESETS, LlamaForCausalLM
+    from accelerate_hpc_test_amd.parallel.ddp import DistributedDataParallel
+    from accelerate_hpc_test_amd.state import AcceleratorState, GradientState
+    from accelerate_hpc_test_amd.utils import RcclKwargs
+
+    res = {}
+    for force in (False, True):
+        AcceleratorState._reset_state(True)
+        GradientState._reset_state()
+        acc = Accelerator(mixed_precision="bf16", kwargs_handlers=[RcclKwargs(ddp_force=force)])
+        torch.manual_seed(0)
+        model = LlamaForCausalLM(LLAMA_PRESETS["llama-tiny"]).to(DEV)
+        opt = torch.optim.AdamW(model.parameters(), lr=1e-3)
+        model, opt = acc.prepare(model, opt)
+        assert isinstance(model, DistributedDataParallel) == force
+        if force:
+            assert model.comm_group is not None and model.comm_stream is not None
+        ids = torch.randint(0, LLAMA_PRESETS["llama-tiny"].vocab_size, (2, 256),
+                            generator=torch.Generator().manual_seed(1)).to(DEV)
+        losses = []
+        for _ in range(3):
+            out = model(ids, labels=ids)
+            acc.backward(out.loss)
+            opt.step()
+            opt.zero_grad()
+            losses.append(out.loss.item())
+        torch.cuda.synchronize()
+        res[force] = (losses, {k: v.detach().clone() for k, v in acc.unwrap_model(model).state_dict().items()})
+    assert res[False][0] == res[True][0], (res[False][0], res[True][0])
+    for k, v in res[False][1].items():
+        assert torch.equal(v, res[True][1][k]), k
+
+
 @pytest.mark.parametrize("src_dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("accumulate", [False, True])
 def test_grad_shard_update_matches_torch(src_dtype, accumulate):

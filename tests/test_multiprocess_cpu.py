@@ -158,3 +158,7 @@ def test_fsdp_ddp_at_node_scale(world):
     debug_launcher(td.check_fsdp_matches_single, args=(True, "SHARDED_STATE_DICT"), num_processes=world)
     debug_launcher(td.check_fsdp_fp8_all_gather, args=(False,), num_processes=world)
     debug_launcher(td.check_ddp_matches_single, num_processes=world)
+
+
+def test_ddp_forced_reducer_single_rank():
+    debug_launcher(td.check_ddp_forced_single_rank, num_processes=1)
