@@ -1029,6 +1029,34 @@ std::vector<torch::Tensor> fp8_cast(torch::Tensor x, torch::Tensor t, double qma
   return {y};
 }
 
+// fp8_cast into caller-owned outputs: y [M, N] and (optionally) yt [N, M], both 1-byte fp8 of the matching kind. Used
+// for the world-size-1 FSDP fp8 weights: one pass writes the persistent e4m3 weight and its K-major copy for dgrad.
+void fp8_cast_into(torch::Tensor x, torch::Tensor t, double qmax, bool from_amax, bool e5m2, torch::Tensor y,
+                   c10::optional<torch::Tensor> yt) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.dim() == 2, "fp8_cast_into: x must be 2-D contiguous bf16");
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.numel() >= 1, "fp8_cast_into: scale/amax must be a fp32 device tensor");
+  const int M = x.size(0), N = x.size(1);
+  TORCH_CHECK(y.is_cuda() && y.element_size() == 1 && y.is_contiguous() && y.numel() == (long)M * N, "fp8_cast_into: bad y");
+  const bool tr = yt.has_value();
+  if (tr) TORCH_CHECK(yt->is_cuda() && yt->element_size() == 1 && yt->is_contiguous() && yt->numel() == (long)M * N, "fp8_cast_into: bad yt");
+  if (M == 0 || N == 0) return;
+  dim3 grid((N + kCT - 1) / kCT, (M + kCT - 1) / kCT);
+  auto stream = at::hip::getCurrentHIPStream();
+  uint8_t* yp = reinterpret_cast<uint8_t*>(y.data_ptr());
+  uint8_t* ytp = tr ? reinterpret_cast<uint8_t*>(yt->data_ptr()) : nullptr;
+  const bf16_t* xp = reinterpret_cast<const bf16_t*>(x.data_ptr());
+  const float* tp = t.data_ptr<float>();
+  const float q = (float)qmax;
+  const int fa = from_amax ? 1 : 0;
+  if (e5m2) {
+    if (tr) hipLaunchKernelGGL((cast_kernel<true, true>), grid, dim3(256), 0, stream, xp, tp, q, fa, yp, ytp, M, N);
+    else hipLaunchKernelGGL((cast_kernel<true, false>), grid, dim3(256), 0, stream, xp, tp, q, fa, yp, ytp, M, N);
+  } else {
+    if (tr) hipLaunchKernelGGL((cast_kernel<false, true>), grid, dim3(256), 0, stream, xp, tp, q, fa, yp, ytp, M, N);
+    else hipLaunchKernelGGL((cast_kernel<false, false>), grid, dim3(256), 0, stream, xp, tp, q, fa, yp, ytp, M, N);
+  }
+}
+
 // Kernel choice of fp8_gemm: 0 = default, 1 = v1 (128x128), 2 = v2 4 waves, 3 = v2 8 waves, 4 = v3 (4-deep ring),
 // 5 = v3 8 waves.
 // Shapes a variant cannot tile fall back to the next one that can (v3 -> v2 -> v1).

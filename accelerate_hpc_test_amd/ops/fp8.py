@@ -300,7 +300,7 @@ class _Fp8LinearFn(torch.autograd.Function):
     reports the parameter's gradient as ready — no separate dW tensor, no AccumulateGrad add."""
 
     @staticmethod
-    def forward(ctx, x, w, bias, recipe: Fp8Recipe, slot=None, w_amax=None):
+    def forward(ctx, x, w, bias, recipe: Fp8Recipe, slot=None, w_amax=None, w8t_pre=None):
         shape = x.shape
         x2 = x.reshape(-1, shape[-1])
         N = w.shape[0]
@@ -314,7 +314,9 @@ class _Fp8LinearFn(torch.autograd.Function):
             sw = Scale(w_amax, E4M3_MAX)
             w8 = w
             y = gemm(x8, w8, sx, sw, bias, torch.bfloat16)
-            ctx.save_for_backward(x8t, w, sx.amax, sw.amax)
+            # world size 1: the engine keeps the K-major copy (written with the weight each step), nothing to transpose
+            ctx.transpose_w = w8t_pre is None
+            ctx.save_for_backward(x8t, w if w8t_pre is None else w8t_pre, sx.amax, sw.amax)
         else:
             sw = recipe.scale("w", w, fwd_max)
             w8, w8t = cast(w, sw, recipe.fwd_e5m2(), transpose=True)
@@ -327,7 +329,7 @@ class _Fp8LinearFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x8t, w8t, ax, aw = ctx.saved_tensors
-        if ctx.pre_quantised:
+        if ctx.pre_quantised and ctx.transpose_w:
             w8t = transpose_fp8(w8t)
         sx, sw = Scale(ax, ctx.qmax[0]), Scale(aw, ctx.qmax[1])
         recipe = ctx.recipe
@@ -343,9 +345,9 @@ class _Fp8LinearFn(torch.autograd.Function):
             dest, acc = slot.engine._fused_slot_dest(slot)
             gemm(dy8t, x8t, sg, sx, None, out=dest, accumulate=acc)
             slot.engine._fused_slot_done(slot)
-            return dx.view(ctx.shape), None, db, None, None, None
+            return dx.view(ctx.shape), None, db, None, None, None, None
         dw = gemm(dy8t, x8t, sg, sx, None, torch.bfloat16)
-        return dx.view(ctx.shape), dw, db, None, None, None
+        return dx.view(ctx.shape), dw, db, None, None, None, None
 
 
 _FP8_ON = [True]
@@ -389,7 +391,7 @@ class Fp8Linear(nn.Linear):
         if gathered is not None:
             unit, info = gathered
             return _Fp8LinearFn.apply(x, self.weight, b, self.fp8_recipe, self._fp8_wgrad_slot(x),
-                                      unit.engine.fp8_weight_scale(unit, info))
+                                      unit.engine.fp8_weight_scale(unit, info), unit.engine.fp8_weight_t(unit, info))
         w = self.weight if self.weight.dtype == torch.bfloat16 else self.weight.to(torch.bfloat16)
         return _Fp8LinearFn.apply(x, w, b, self.fp8_recipe, self._fp8_wgrad_slot(x))
 

@@ -65,7 +65,7 @@ def _round_up(x, m):
 
 class _ParamInfo:
     __slots__ = ("fqn", "module", "attr", "param", "orig_param", "offset", "numel", "shape", "shard_param", "local_lo", "local_hi",
-                 "param_lo", "fused", "fused_written", "region", "f8_index")
+                 "param_lo", "fused", "fused_written", "region", "f8_index", "f8_t")
 
     def __init__(self, fqn, module, attr, param, offset):
         self.fqn = fqn
@@ -82,6 +82,7 @@ class _ParamInfo:
         self.fused_written = False
         self.region = None
         self.f8_index = -1
+        self.f8_t = None  # world-size-1 fp8 weights: the stored K-major e4m3 copy (FSDPEngine._init_fp8_all_gather)
 
 
 class _Region:
@@ -330,6 +331,18 @@ class FSDPEngine:
         for u in self.f8_units:
             first = u.f8_seg[3]
             u.f8_amax = self.f8_amax_all[first : first + len(u.f8_infos)]
+        # World size 1 (no all-gather), opt-in with ACCELERATE_FP8_PRETRANSPOSE=1: the e4m3 weights are persistent, so
+        # their K-major copies for the dgrad GEMM can be kept too and written by the same per-step cast (one read of the
+        # bf16 weight writes both layouts) instead of a byte transpose of every weight in every backward. Measured on
+        # Llama-3-8B: 23.49k / 23.58k tok/s on vs 23.55k / 23.53k off (same box), +6.4 GiB, so it stays off.
+        from ..ops._ext import use_native
+
+        self.f8_pretransposed = (not self.sharded and os.environ.get("ACCELERATE_FP8_PRETRANSPOSE", "0") == "1"
+                                 and all(use_native(u.shard_lp) for u in self.f8_units))
+        for u in self.f8_units:
+            for info in u.f8_infos:
+                info.f8_t = (torch.empty((info.shape[1], info.shape[0]), dtype=torch.float8_e4m3fn, device=self.device)
+                             if self.f8_pretransposed else None)
         self.refresh_fp8()
 
     @torch.no_grad()
@@ -356,13 +369,22 @@ class FSDPEngine:
         for u in self.f8_units:
             lo, hi, max_len, _ = u.f8_seg
             src = u.shard_lp[: u.f8.shard_len]
-            if use_native(src):
+            if self.f8_pretransposed:
+                for k, info in enumerate(u.f8_infos):
+                    a, b = info.local_lo, info.local_hi
+                    ext().fp8_cast_into(src[a:b].view(info.shape), u.f8_amax[k : k + 1], 448.0, True, False,
+                                        u.f8_shard[a:b].view(info.shape), info.f8_t)
+            elif use_native(src):
                 ext().fp8_segment_cast(src, lo, hi, u.f8_amax, 448.0, u.f8_shard, max_len)
             else:
                 for k, info in enumerate(u.f8_infos):
                     s = 448.0 / u.f8_amax[k].clamp_min(1e-12)
                     piece = (src[info.local_lo : info.local_hi].float() * s).clamp(-448.0, 448.0)
                     u.f8_shard[info.local_lo : info.local_hi] = piece.to(torch.float8_e4m3fn)
+
+    def fp8_weight_t(self, unit: FlatUnit, info: _ParamInfo):
+        """The stored K-major e4m3 copy of an fp8-gathered weight (world size 1), or None (made in backward)."""
+        return info.f8_t
 
     def fp8_weight_scale(self, unit: FlatUnit, info: _ParamInfo) -> torch.Tensor:
         """The amax (fp32 [1], device) whose scale 448 / amax quantised this gathered weight."""

@@ -54,3 +54,32 @@ def test_cv_example_cpu_learns():
     metric = cv_example.main(["--cpu", "--image_size", "32", "--n_train", "512", "--n_eval", "128", "--num_epochs", "4",
                               "--batch_size", "32"])
     assert metric["accuracy"] > 0.9, metric
+
+
+def test_config_templates_load_and_launch(tmp_path):
+    """examples/config_yaml_templates: every file parses with the launcher's schema; run_me.py launches with the
+    single-accelerator template (on CPU) and with a 2-rank CPU variant of the DDP template."""
+    import glob
+
+    import yaml
+
+    from accelerate_hpc_test_amd.commands.config.config_args import load_config_from_file
+
+    files = sorted(glob.glob(os.path.join(REPO, "examples", "config_yaml_templates", "*.yaml")))
+    assert len(files) == 5
+    for f in files:
+        cfg = load_config_from_file(f)
+        assert cfg.num_processes >= 1, f
+    env = dict(os.environ, HF_HOME=str(tmp_path), PYTHONPATH=REPO)
+    script = os.path.join(REPO, "examples", "config_yaml_templates", "run_me.py")
+    ddp = yaml.safe_load(open(os.path.join(REPO, "examples", "config_yaml_templates", "multi_gpu.yaml")))
+    ddp.update(distributed_type="MULTI_CPU", num_processes=2, use_cpu=True, mixed_precision="no")
+    cpu2 = tmp_path / "cpu2.yaml"
+    cpu2.write_text(yaml.safe_dump(ddp))
+    for cfg, extra, expect in ((os.path.join(REPO, "examples", "config_yaml_templates", "single_accelerator.yaml"),
+                                ["--cpu"], "num_processes=1"), (str(cpu2), [], "num_processes=2")):
+        r = subprocess.run([sys.executable, "-m", "accelerate_hpc_test_amd.commands.accelerate_cli", "launch",
+                            "--config_file", cfg, *extra, script], cwd=REPO, env=env, capture_output=True, text=True,
+                           timeout=300)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+        assert expect in r.stdout and "final loss" in r.stdout, r.stdout

@@ -1012,13 +1012,14 @@ def test_device_prefetcher_stops_on_early_exit():
 
 
 @pytest.mark.parametrize("force", [False, True])
-def test_fsdp_fp8_all_gather_matches_bf16_all_gather(one_rank_rccl, force):
+def test_fsdp_fp8_all_gather_matches_bf16_all_gather(one_rank_rccl, monkeypatch, force):
     """AORecipeKwargs(enable_fsdp_float8_all_gather=True) (reference examples/torch_native_parallelism/fsdp2_fp8.py:69-75):
     fp8 GEMM weights all-gathered as e4m3 (half the bytes), quantised from the shards with one batched all-reduce(MAX) of
     the per-weight amaxes after each step (HIP segment amax / cast kernels), dgrad operand by the HIP byte transpose.
     Identical quantisation to casting the gathered bf16 weight, so losses, grad norms and weights match bit for bit."""
     from accelerate_hpc_test_amd.utils import AORecipeKwargs, RcclKwargs
 
+    monkeypatch.setenv("ACCELERATE_FP8_PRETRANSPOSE", "1")  # opt-in stored K-major weights at world size 1
     res = {}
     for ag in (False, True):
         acc, model, losses, norms = _llama_tiny_run(3, [RcclKwargs(fsdp_force_sharded=force),
@@ -1028,6 +1029,9 @@ def test_fsdp_fp8_all_gather_matches_bf16_all_gather(one_rank_rccl, force):
         assert bool(eng.f8_units) == ag
         if ag:
             assert all(i.param.dtype == torch.float8_e4m3fn for u in eng.f8_units for i in u.f8_infos)
+            # world size 1 without forcing: the K-major dgrad copies are stored and written by the per-step cast
+            assert eng.f8_pretransposed == (not force)
+            assert all((i.f8_t is not None) == (not force) for u in eng.f8_units for i in u.f8_infos)
         res[ag] = (losses, norms, acc.get_state_dict(model))
     assert res[False][0] == res[True][0], (res[False][0], res[True][0])
     # the grad norm sums squares over the flat layout, which the fp8 region reorders: equal up to summation order
