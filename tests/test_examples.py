@@ -83,3 +83,19 @@ def test_config_templates_load_and_launch(tmp_path):
                            timeout=300)
         assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
         assert expect in r.stdout and "final loss" in r.stdout, r.stdout
+
+
+@pytest.mark.parametrize("script,expect", [
+    ("examples/inference/pippy/llama.py", "max |staged - unsplit| = 0.00e+00"),
+    ("examples/inference/distributed/llama_generation.py", "generated 10 completions on 2 process(es)"),
+    ("examples/alst_ulysses_sequence_parallelism/sp_ulysses.py", "local tokens 32 of 64"),
+])
+def test_inference_and_sequence_parallel_examples_two_ranks(tmp_path, script, expect):
+    """Pipeline inference (prepare_pippy), split_between_processes generation and Ulysses SP training, each launched
+    on 2 CPU ranks through `accelerate-amd launch` (reference examples/inference/*, examples/alst_ulysses_*)."""
+    env = dict(os.environ, HF_HOME=str(tmp_path), PYTHONPATH=REPO)
+    r = subprocess.run([sys.executable, "-m", "accelerate_hpc_test_amd.commands.accelerate_cli", "launch", "--cpu",
+                        "--num_processes", "2", os.path.join(REPO, script), "--cpu"], cwd=REPO, env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    assert expect in r.stdout, r.stdout[-2000:]
