@@ -103,6 +103,7 @@ class DistributedDataParallel(nn.Module):
             self.comm_group = duplicate_group(process_group)
         self._next_bucket = 0
         self._cb_queued = False
+        self._unset: set = set()  # ids of params whose grad is None at forward (filled by the hook's copy)
         self._sync_params_and_buffers()
         self._build_buckets()
 
@@ -162,9 +163,11 @@ class DistributedDataParallel(nn.Module):
 
     # ------------------------------------------------------------------------------------------ forward
     def forward(self, *inputs, **kwargs):
-        # After `zero_grad(set_to_none=True)` the grads are None: re-point them at the (zeroed) buckets.
-        if any(p.grad is None for b in self.buckets for p in b.params):
-            self._assign_grad_views(zero=True)
+        # After `zero_grad(set_to_none=True)` the grads are None. They stay None: autograd then hands each parameter a
+        # fresh gradient, which the grad hook copies into its bucket slot (one 8 B/param copy) and re-points `.grad`
+        # at; no bucket-wide zero fill followed by an accumulate-add (4 + 12 B/param). Slots whose parameter gets no
+        # gradient this backward are zeroed in `_finalize`, before their bucket is reduced.
+        self._unset = {id(p) for b in self.buckets for p in b.params if p.grad is None}
         join = getattr(self, "_join", None)
         if join is not None:
             syncing = int(self.require_backward_grad_sync and torch.is_grad_enabled())
@@ -194,10 +197,11 @@ class DistributedDataParallel(nn.Module):
     def _grad_hook(self, p):
         b = self.buckets[self._param_bucket[p]]
         if p.grad is not None and b.buffer.numel() and p.grad.data_ptr() != self._slot_ptr(b, p):
-            with torch.no_grad():  # a grad allocated outside the bucket (e.g. set by the user): absorb it
+            with torch.no_grad():  # first gradient since zero_grad (or one set by the user): move it into the bucket
                 view = self._slot(b, p)
                 view.copy_(p.grad)
                 p.grad = view
+        self._unset.discard(id(p))
         if not self._cb_queued:
             self._cb_queued = True
             torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
@@ -309,6 +313,15 @@ class DistributedDataParallel(nn.Module):
 
     def _finalize(self):
         self._cb_queued = False
+        if self._unset:  # parameters without a gradient this backward: zero slots, grads point at them
+            with torch.no_grad():
+                for b in self.buckets:
+                    for p in b.params:
+                        if id(p) in self._unset:
+                            view = self._slot(b, p)
+                            view.zero_()
+                            p.grad = view
+            self._unset.clear()
         if self._sync_pending:
             for b in self.buckets[self._next_bucket :]:  # unused params never fired: flush the rest in index order
                 self._launch(b)
