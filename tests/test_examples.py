@@ -99,3 +99,21 @@ def test_inference_and_sequence_parallel_examples_two_ranks(tmp_path, script, ex
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     assert expect in r.stdout, r.stdout[-2000:]
+
+
+def test_complete_cv_example_epoch_checkpoint_and_resume(tmp_path):
+    """examples/complete_cv_example.py: epoch and step checkpoints, resume from both, still learns."""
+    import complete_cv_example
+
+    out = str(tmp_path / "cv")
+    common = ["--cpu", "--image_size", "32", "--n_train", "256", "--n_eval", "128", "--batch_size", "32",
+              "--num_epochs", "3", "--output_dir", out]
+    first = complete_cv_example.main(common + ["--checkpointing_steps", "epoch"])
+    assert sorted(os.listdir(out)) == ["epoch_0", "epoch_1", "epoch_2"]
+    resumed = complete_cv_example.main(common + ["--resume_from_checkpoint", os.path.join(out, "epoch_1")])
+    assert resumed["accuracy"] > 0.5 and first["accuracy"] > 0.5, (first, resumed)
+    step_out = str(tmp_path / "cv_steps")
+    steps = ["--output_dir", step_out, "--checkpointing_steps", "5"]
+    complete_cv_example.main(common[:-2] + steps)
+    res = complete_cv_example.main(common[:-2] + steps[:2] + ["--resume_from_checkpoint", os.path.join(step_out, "step_10")])
+    assert res["accuracy"] > 0.5, res
