@@ -53,6 +53,8 @@ def parse():
     p.add_argument("--fsdp-cpu-offload", action="store_true",
                    help="FSDP CPU offload: fp32 master/grad shards + AdamW state in pinned host memory, host AdamW")
     p.add_argument("--verbose", action="store_true")
+    p.add_argument("--cpu", action="store_true",
+                   help="contract check only: run the same loop on CPU ranks (gloo) with a small --model; not a benchmark")
     p.add_argument("--gemm-tuning", default="auto", choices=["auto", "off", "tune"],
                    help="auto: load the committed hipBLASLt per-shape table (ops/tuned); tune: search and write it")
     p.add_argument("--gemm-table", default=None, help="table path for --gemm-tuning auto/tune")
@@ -75,9 +77,9 @@ class SyntheticTokens(torch.utils.data.Dataset):
 
 
 def _metric_name(args, is_moe):
-    if not is_moe and args.parallel == "fsdp" and args.precision == "bf16":
+    if args.model == "llama3-8b" and args.parallel == "fsdp" and args.precision == "bf16":
         return "tokens/sec (whole node) Llama-3-8B FSDP2 bf16 at 1/2/4/8 MI355X"
-    name = "Llama-3-8B" if not is_moe else args.model
+    name = "Llama-3-8B" if args.model == "llama3-8b" else args.model
     return f"tokens/sec (whole node) {name} {'FSDP2' if args.parallel == 'fsdp' else 'DDP'} {args.precision}"
 
 
@@ -120,7 +122,8 @@ def main():
 
         handlers.append(TERecipeKwargs(use_mxfp8_block_scaling=True))
     mp = "fp8" if args.precision == "mxfp8" else args.precision
-    accelerator = Accelerator(mixed_precision=mp, fsdp_plugin=plugin, kwargs_handlers=handlers)
+    accelerator = Accelerator(mixed_precision=mp, fsdp_plugin=plugin, kwargs_handlers=handlers, cpu=args.cpu)
+    sync = (lambda: None) if args.cpu else torch.cuda.synchronize
     set_seed(0)
     world = accelerator.num_processes
     from accelerate_hpc_test_amd.ops import gemm_tuning
@@ -145,8 +148,8 @@ def main():
     dl = torch.utils.data.DataLoader(ds, batch_size=args.mbs, num_workers=2)
     model, optimizer, dl = accelerator.prepare(model, optimizer, dl)
     model.train()
-    torch.cuda.synchronize()
-    if args.verbose and accelerator.is_main_process:
+    sync()
+    if args.verbose and accelerator.is_main_process and not args.cpu:
         print(f"setup {time.time() - t0:.1f}s, mem {torch.cuda.memory_allocated() / 2**30:.1f} GiB", flush=True)
 
     it = iter(dl)
@@ -165,17 +168,17 @@ def main():
         tw = time.time()
         step()
         if args.verbose:
-            torch.cuda.synchronize()
+            sync()
             accelerator.print(f"warmup step {i}: {time.time() - tw:.3f}s loss {last_loss.item():.4f}", flush=True)
     if args.gemm_tuning == "tune":
         gemm_tuning.finish_gemm_tuning()  # search done during warmup; the timed steps use the tuned table
 
     accelerator.wait_for_everyone()
-    torch.cuda.synchronize()
+    sync()
     t_start = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize()
+    sync()
     accelerator.wait_for_everyone()
     elapsed = time.perf_counter() - t_start
 
@@ -187,8 +190,8 @@ def main():
     tps = tokens / elapsed
     ms = elapsed / args.steps * 1000
     flops_tok = cfg.flops_per_token(args.seq)
-    peak = torch.cuda.max_memory_allocated() / 2**30
-    headline = not is_moe and args.parallel == "fsdp"
+    peak = 0.0 if args.cpu else torch.cuda.max_memory_allocated() / 2**30
+    headline = args.model == "llama3-8b" and args.parallel == "fsdp"
     base_dev = BASELINE_FP8_TOKENS_PER_SEC_PER_DEVICE if args.precision in ("fp8", "mxfp8") else BASELINE_TOKENS_PER_SEC_PER_DEVICE
     if accelerator.is_main_process:
         rec = {
