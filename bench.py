@@ -192,10 +192,10 @@ def main():
     flops_tok = cfg.flops_per_token(args.seq)
     peak = 0.0 if args.cpu else torch.cuda.max_memory_allocated() / 2**30
     if args.verbose and not args.cpu:
-        ms = torch.cuda.memory_stats()
-        accelerator.print(f"allocator: alloc_retries {ms.get('num_alloc_retries', 0)}, reserved peak "
-                          f"{ms.get('reserved_bytes.all.peak', 0) / 2**30:.1f} GiB, device frees "
-                          f"{ms.get('num_device_free', 0)}", flush=True)
+        mst = torch.cuda.memory_stats()
+        accelerator.print(f"allocator: alloc_retries {mst.get('num_alloc_retries', 0)}, reserved peak "
+                          f"{mst.get('reserved_bytes.all.peak', 0) / 2**30:.1f} GiB, device frees "
+                          f"{mst.get('num_device_free', 0)}", flush=True)
     headline = args.model == "llama3-8b" and args.parallel == "fsdp"
     base_dev = BASELINE_FP8_TOKENS_PER_SEC_PER_DEVICE if args.precision in ("fp8", "mxfp8") else BASELINE_TOKENS_PER_SEC_PER_DEVICE
     if accelerator.is_main_process:
