@@ -704,10 +704,14 @@ class FSDPEngine:
         reduce-scatter stream uses recorded on it, cannot be recycled by the caching allocator until the GPU catches
         up with the host, which runs a step ahead: on Llama-3-8B at one forced-sharded GPU the reserved pool reached
         285 of 288 GiB, the allocator fell back to freeing its cache (hipFree + sync) and the step took 1.3 s instead
-        of 0.46 s."""
+        of 0.46 s. Without sharding (world size 1 shortcut: fused weight grads go to the fp32 shard, this buffer only
+        carries the few non-fused slots and is never handed to another stream) it stays transient: keeping 32 of them
+        would hold 14 GB of Llama-3-8B for nothing."""
         buf = getattr(unit, "_grad_buf", None)
         if buf is None or buf.numel() != unit.padded or buf.dtype != self.param_dtype:
-            buf = unit._grad_buf = torch.empty(unit.padded, dtype=self.param_dtype, device=self.device)
+            buf = torch.empty(unit.padded, dtype=self.param_dtype, device=self.device)
+            if self.sharded:
+                unit._grad_buf = buf
         if not any(i.fused for i in unit.infos):
             return buf.zero_()
         pos = 0
