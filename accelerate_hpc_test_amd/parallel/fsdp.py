@@ -708,6 +708,10 @@ class FSDPEngine:
         carries the few non-fused slots and is never handed to another stream) it stays transient: keeping 32 of them
         would hold 14 GB of Llama-3-8B for nothing."""
         buf = getattr(unit, "_grad_buf", None)
+        if buf is not None and self.is_cuda and getattr(unit, "_rs_done", None) is not None:
+            # reused: writes on the compute stream must follow the last reduce-scatter that read it (normally long
+            # done; this only matters if the unit is re-gradded within the backward that reduced it)
+            torch.cuda.current_stream(self.device).wait_event(unit._rs_done)
         if buf is None or buf.numel() != unit.padded or buf.dtype != self.param_dtype:
             buf = torch.empty(unit.padded, dtype=self.param_dtype, device=self.device)
             if self.sharded:
@@ -856,6 +860,8 @@ class FSDPEngine:
             self.rs_stream.wait_stream(cur)
             with torch.cuda.stream(self.rs_stream), trace_range(f"fsdp.reduce_scatter[{unit.idx}]"):
                 self._rs_and_accumulate(unit, src, out, first)
+                unit._rs_done = torch.cuda.Event()
+                unit._rs_done.record(self.rs_stream)
             src.record_stream(self.rs_stream)
             out.record_stream(self.rs_stream)
         else:
