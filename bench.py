@@ -83,9 +83,41 @@ def _metric_name(args, is_moe):
     return f"tokens/sec (whole node) {name} {'FSDP2' if args.parallel == 'fsdp' else 'DDP'} {args.precision}"
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _spawn_ranks(n: int) -> int:
+    """`python bench.py --gpus N` without a launcher: start N ranks with torch.distributed.run as a CHILD process (no
+    exec, and nothing in this parent touches the GPU) and return its exit code. Each rank re-enters this file with
+    WORLD_SIZE set, so only the ranks ever initialise HIP."""
+    import subprocess
+    import sys
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    launched_world = os.environ.get("WORLD_SIZE")
+    if launched_world is None and args.gpus > 1:
+        raise SystemExit(_spawn_ranks(args.gpus))
+    if launched_world is not None and int(launched_world) != args.gpus:
+        raise SystemExit(f"bench.py: launched with WORLD_SIZE={launched_world} but --gpus {args.gpus}; they must match")
+    # A hung collective must end the run non-zero (communicators aborted, rank exits) instead of holding the node
+    # until the outer time limit: the step watchdog fires after this many seconds without a heartbeat.
+    os.environ.setdefault("ACCELERATE_WATCHDOG_TIMEOUT", "600")
+    os.environ.setdefault("ACCELERATE_WATCHDOG_ACTION", "abort")
     from accelerate_hpc_test_amd import Accelerator, FullyShardedDataParallelPlugin
     from accelerate_hpc_test_amd.models import LLAMA_PRESETS, MIXTRAL_PRESETS, LlamaForCausalLM, MixtralForCausalLM
 
@@ -149,6 +181,7 @@ def main():
     model, optimizer, dl = accelerator.prepare(model, optimizer, dl)
     model.train()
     sync()
+    accelerator.heartbeat("prepared")
     if args.verbose and accelerator.is_main_process and not args.cpu:
         print(f"setup {time.time() - t0:.1f}s, mem {torch.cuda.memory_allocated() / 2**30:.1f} GiB", flush=True)
 

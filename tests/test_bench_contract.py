@@ -31,3 +31,25 @@ def test_bench_two_ranks_prints_one_json_line(tmp_path):
     # value is the whole-job rate: all ranks' tokens over the slowest rank's timed window
     tokens = 2 * 1 * 256 * 2
     assert abs(rec["value"] - tokens / (rec["ms_per_step"] * 2 / 1000)) / rec["value"] < 0.01, rec
+
+
+def test_bench_spawns_its_own_ranks(tmp_path):
+    """`python bench.py --gpus 2` with no launcher (the driver's SCALE form): bench.py starts torch.distributed.run as a
+    child, every rank trains, and exactly one JSON line reports n_gpus=2 on the sharded path."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1", "--model", "llama-tiny", "--seq",
+           "256", "--cpu"]
+    r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=600,
+                       env=dict(env, PYTHONPATH=REPO, HF_HOME=str(tmp_path)))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "fsdp2" and rec["config"]["global_batch"] == 2
+
+
+def test_bench_rejects_world_size_mismatch(tmp_path):
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", PYTHONPATH=REPO, HF_HOME=str(tmp_path))
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "4", "--cpu", "--model", "llama-tiny"], cwd=REPO,
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode != 0 and "must match" in r.stderr
