@@ -114,18 +114,39 @@ class DistributedDataParallel(nn.Module):
         tensors = [p.data for p in self.module.parameters()] + [b for b in self.module.buffers()]
         self._coalesced_broadcast(tensors)
 
-    def _coalesced_broadcast(self, tensors):
+    def _coalesced_broadcast(self, tensors, chunk_bytes: int = 256 << 20):
+        """Broadcast from rank 0 in packed pieces of at most `chunk_bytes` per dtype (a tensor larger than that goes
+        alone, in place). Packing keeps the call count low for many small tensors; the cap keeps the transient pack
+        buffer small (a whole-model pack of Llama-3-8B fp32 would be a 32 GB spike on every rank)."""
+        src = dist.get_global_rank(self.process_group, 0) if self.process_group else 0
         by_dtype = {}
         for t in tensors:
             by_dtype.setdefault(t.dtype, []).append(t)
-        for dt, ts in by_dtype.items():
-            flat = torch.cat([t.reshape(-1) for t in ts])
-            dist.broadcast(flat, src=dist.get_global_rank(self.process_group, 0) if self.process_group else 0, group=self.process_group)
+
+        def flush(batch):
+            if not batch:
+                return
+            if len(batch) == 1 and batch[0].is_contiguous():
+                dist.broadcast(batch[0], src=src, group=self.process_group)
+                return
+            flat = torch.cat([t.reshape(-1) for t in batch])
+            dist.broadcast(flat, src=src, group=self.process_group)
             off = 0
-            for t in ts:
+            for t in batch:
                 n = t.numel()
                 t.copy_(flat[off : off + n].view_as(t))
                 off += n
+
+        for ts in by_dtype.values():
+            batch, nbytes = [], 0
+            for t in ts:
+                b = t.numel() * t.element_size()
+                if batch and nbytes + b > chunk_bytes:
+                    flush(batch)
+                    batch, nbytes = [], 0
+                batch.append(t)
+                nbytes += b
+            flush(batch)
 
     def _build_buckets(self):
         seen = set()

@@ -206,7 +206,10 @@ class FSDPEngine:
         self.prefetch_depth = max(0, prefetch_depth)
         self.requires_grad_sync = True
         self.is_cuda = device.type == "cuda"
-        self._uses_gloo = self.is_cuda is False
+        # gloo lacks all_gather_into_tensor / reduce_scatter_tensor (CPU tensors, and HIP tensors when several ranks
+        # share one GPU over a gloo group): the list / all-reduce forms below are chosen by the group's backend
+        self._uses_gloo = (not self.is_cuda) or (dist.is_available() and dist.is_initialized()
+                                                 and dist.get_backend(process_group) == "gloo")
         self.offload = plugin.cpu_offload not in (None, False)
         self._pin = self.offload and torch.cuda.is_available() and getattr(plugin.cpu_offload, "pin_memory", True)
         self._d2h_pending = []

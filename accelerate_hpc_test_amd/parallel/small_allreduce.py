@@ -103,7 +103,11 @@ def get(group=None) -> Optional[SmallAllReduce]:
     """The group's communicator (built collectively on first use), or None when the path does not apply."""
     if not (_enabled() and dist.is_available() and dist.is_initialized()):
         return None
-    if dist.get_backend(group) == "gloo" or dist.get_world_size(group) == 1 or not torch.cuda.is_available():
+    if dist.get_world_size(group) == 1 or not torch.cuda.is_available():
+        return None
+    # gloo groups normally mean CPU ranks; ACCELERATE_SMALL_ALLREDUCE_GLOO=1 opts in for HIP ranks on a gloo group
+    # (several processes sharing one GPU: the multi-rank rehearsal of tests/test_gpu_multirank.py)
+    if dist.get_backend(group) == "gloo" and os.environ.get("ACCELERATE_SMALL_ALLREDUCE_GLOO", "0") != "1":
         return None
     if not _same_node(group):
         return None

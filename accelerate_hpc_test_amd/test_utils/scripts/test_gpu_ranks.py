@@ -1,0 +1,123 @@
+"""W ranks sharing ONE MI355X over a gloo group: the sharded engines with real partial shards, on the HIP kernels.
+
+The forced-sharded single-GPU mode runs the W>1 engine code at nranks=1, where every parameter is whole in every
+shard. Only W>1 cuts parameters across shard boundaries, and that is what this script drives: FSDP partial-parameter
+slices through the fused AdamW / bf16 shadow, `grad_shard_update` with 1/W, the fp8 all-gather's per-segment amax /
+cast kernels on partial pieces plus the batched amax all-reduce, the clip-norm reduction across processes (over the
+HIP-IPC one-shot all-reduce when `ACCELERATE_SMALL_ALLREDUCE_GLOO=1`), sharded checkpoint save -> load, and the DDP
+reducer's bucket all-reduce. RCCL refuses two ranks on one device, so the group is gloo with HIP tensors (the engine
+picks the gloo-compatible collective forms by backend).
+
+Launched as `torch.distributed.run --nproc-per-node W test_gpu_ranks.py --mode M --out DIR`, or without a launcher
+(W=1: the single-process reference). Rank 0 writes DIR/result_W{W}.json (per-step global loss and grad norm) and
+DIR/params_W{W}.pt (full fp32 state dict); `tests/test_gpu_multirank.py` compares W=2/4 against W=1.
+Reference: test_utils/scripts/test_sync.py:29-331 (sharded training equals the single-process model).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+
+import torch
+
+
+GLOBAL_BATCH = 4
+SEQ = 256
+
+
+def _batches(steps, vocab):
+    g = torch.Generator().manual_seed(7)
+    return [torch.randint(0, vocab, (GLOBAL_BATCH, SEQ), generator=g) for _ in range(steps)]
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--mode", choices=["fsdp", "fsdp_fp8", "ddp"], required=True)
+    p.add_argument("--out", required=True)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--preset", default="llama-small")
+    p.add_argument("--cpu", action="store_true", help="plumbing check of this script on CPU ranks (not the GPU test)")
+    args = p.parse_args()
+
+    from accelerate_hpc_test_amd import Accelerator, FullyShardedDataParallelPlugin
+    from accelerate_hpc_test_amd.models.llama import LLAMA_PRESETS, LlamaForCausalLM
+    from accelerate_hpc_test_amd.parallel import small_allreduce
+    from accelerate_hpc_test_amd.utils import AORecipeKwargs, InitProcessGroupKwargs, RcclKwargs
+
+    W = int(os.environ.get("WORLD_SIZE", "1"))
+    handlers = [InitProcessGroupKwargs(backend="gloo")] if W > 1 else []
+    cfg = LLAMA_PRESETS[args.preset]
+    lr = 1e-4
+    if args.mode == "ddp":
+        acc = Accelerator(mixed_precision="bf16", kwargs_handlers=handlers, cpu=args.cpu)
+        torch.manual_seed(0)
+        model = LlamaForCausalLM(cfg).to(acc.device)
+    else:
+        plugin = FullyShardedDataParallelPlugin(fsdp_version=2, auto_wrap_policy="transformer_based_wrap",
+                                                transformer_cls_names_to_wrap=["LlamaDecoderLayer"])
+        if args.mode == "fsdp_fp8":
+            handlers.append(AORecipeKwargs(enable_fsdp_float8_all_gather=True))
+        handlers.append(RcclKwargs())
+        acc = Accelerator(mixed_precision="fp8" if args.mode == "fsdp_fp8" else "bf16", fsdp_plugin=plugin,
+                          kwargs_handlers=handlers, cpu=args.cpu)
+        with torch.device("meta"):
+            model = LlamaForCausalLM(cfg)
+    r = acc.process_index
+    assert acc.num_processes == W and acc.device.type == ("cpu" if args.cpu else "cuda")
+    opt = torch.optim.AdamW(model.parameters(), lr=lr, weight_decay=0.01)
+    model, opt = acc.prepare(model, opt)
+    facts = {"world": W, "mode": args.mode}
+    if args.mode != "ddp":
+        eng = model.engine
+        facts["sharded"] = bool(eng.sharded)
+        # parameters cut by a shard boundary (the case the forced one-GPU mode never has)
+        facts["split_params"] = sum(1 for u in eng.units for i in u.infos if 0 < i.local_hi - i.local_lo < i.numel)
+        facts["fp8_units"] = len(eng.f8_units)
+    else:
+        facts["ddp_buckets"] = len(getattr(model, "buckets", []))
+    if W > 1:
+        facts["ipc_allreduce"] = small_allreduce.get(None) is not None
+    bs = GLOBAL_BATCH // W
+    losses, norms = [], []
+    for ids in _batches(args.steps, cfg.vocab_size):
+        local = ids[r * bs : (r + 1) * bs].to(acc.device)
+        out = model(local, labels=local)
+        acc.backward(out.loss)
+        norms.append(float(acc.clip_grad_norm_(model.parameters(), 1e9)))
+        opt.step()
+        opt.zero_grad()
+        losses.append(float(acc.reduce(out.loss.detach().float(), reduction="mean")))
+    if not args.cpu:
+        torch.cuda.synchronize()
+    if args.mode == "ddp":
+        state = {k: v.detach().float().cpu() for k, v in acc.unwrap_model(model).state_dict().items()}
+    else:
+        state = acc.get_state_dict(model)
+    if args.mode == "fsdp" and W > 1:
+        # sharded checkpoint round trip: every rank writes its shard files, perturb, load, compare
+        from accelerate_hpc_test_amd.utils import gather_object
+
+        d = gather_object([os.path.join(args.out, f"ckpt_W{W}")])[0]
+        acc.save_state(d)
+        with torch.no_grad():
+            for q in model.parameters():
+                q.add_(1.0)
+        acc.load_state(d)
+        back = acc.get_state_dict(model)
+        if r == 0:
+            bad = [n for n in state if not torch.equal(state[n], back[n])]
+            facts["ckpt_roundtrip_mismatch"] = bad
+    if r == 0:
+        os.makedirs(args.out, exist_ok=True)
+        torch.save({k: v.float().cpu() for k, v in state.items()}, os.path.join(args.out, f"params_{args.mode}_W{W}.pt"))
+        with open(os.path.join(args.out, f"result_{args.mode}_W{W}.json"), "w") as f:
+            json.dump(dict(facts, losses=losses, norms=norms), f)
+        print(json.dumps(dict(facts, losses=losses, norms=norms)), flush=True)
+    acc.wait_for_everyone()
+    acc.end_training()
+
+
+if __name__ == "__main__":
+    main()
