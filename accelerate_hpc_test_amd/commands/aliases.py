@@ -46,13 +46,14 @@ def _default_dir() -> str:
 
 def install(directory: str, force: bool = False) -> list:
     os.makedirs(directory, exist_ok=True)
+    if not force:  # check every target before writing any, so a refusal leaves no partial install behind
+        foreign = [n for n, st in listed(directory).items() if st == "other"]
+        if foreign:
+            raise FileExistsError(f"{', '.join(os.path.join(directory, n) for n in foreign)} exist(s) and are not "
+                                  "accelerate-amd aliases (use --force to replace)")
     written = []
     for name, prefix in ALIASES.items():
         path = os.path.join(directory, name)
-        if os.path.exists(path) and not force:
-            with open(path, errors="replace") as f:
-                if _MARK not in f.read(4096):
-                    raise FileExistsError(f"{path} exists and is not an accelerate-amd alias (use --force to replace)")
         with open(path, "w") as f:
             f.write(_script(prefix))
         os.chmod(path, os.stat(path).st_mode | stat.S_IXUSR | stat.S_IXGRP | stat.S_IXOTH)

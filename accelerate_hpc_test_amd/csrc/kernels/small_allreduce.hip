@@ -17,7 +17,9 @@
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include "common.h"
+#include <limits>
 #include <map>
+#include <type_traits>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -53,6 +55,13 @@ struct IO {
   void* out[kMaxRanks];
 };
 
+template <typename T>
+__device__ inline T poison() {
+  // bf16_t is raw uint16 storage: it is a float type here (the Acc<T> of every float type is float)
+  if constexpr (std::is_same<typename Acc<T>::type, float>::value) return store_cast<T>(__builtin_nanf(""));
+  else return std::numeric_limits<T>::min();
+}
+
 template <typename T, int OP>
 __global__ __launch_bounds__(kThreads) void one_shot_allreduce_kernel(IO io, long n, Peers peers, int rank0, int world,
                                                                       uint32_t epoch, long slot_bytes, int* err,
@@ -84,18 +93,28 @@ __global__ __launch_bounds__(kThreads) void one_shot_allreduce_kernel(IO io, lon
     __hip_atomic_store(f, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   // 3. acquire: wait for every peer's flag for this block in the local buffer (bounded)
+  __shared__ int timed_out;
+  if (tid == 0) timed_out = 0;
+  __syncthreads();
   if (tid < world) {
     const uint32_t* f = reinterpret_cast<const uint32_t*>(peers.buf[rank]) + tid * kMaxBlocks + b;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz constant clock
     while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
       if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
         __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        timed_out = 1;
         break;
       }
       __builtin_amdgcn_s_sleep(2);
     }
   }
   __syncthreads();
+  if (timed_out) {
+    // a peer never arrived: poison this chunk (NaN for floats, the minimum value for integers) so a caller that reads
+    // the result before checking sar_status cannot consume a sum of stale peer data
+    for (long i = lo + tid; i < hi; i += kThreads) out[i] = poison<T>();
+    return;
+  }
   __threadfence_system();
   // 4. reduce the peers' copies of the chunk (remote loads over xGMI) in registers, rank order fixed for determinism
   if (vec) {

@@ -350,6 +350,28 @@ class _Fp8LinearFn(torch.autograd.Function):
         return dx.view(ctx.shape), dw, db, None, None, None, None
 
 
+class _Fp8GatheredFallbackFn(torch.autograd.Function):
+    """y = x · dequant(w8)ᵀ (+ b) for an fp8-gathered weight; backward: dx = dy · w, dW = dyᵀ x into the FSDP slot."""
+
+    @staticmethod
+    def forward(ctx, x, w8, w_amax, bias, slot):
+        w = (w8.float() * (w_amax.clamp_min(1e-12) / E4M3_MAX)).to(x.dtype)
+        ctx.save_for_backward(x, w)
+        ctx.slot, ctx.has_bias = slot, bias is not None
+        return nn.functional.linear(x, w, bias)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        N, K = w.shape
+        dx = (dy @ w) if ctx.needs_input_grad[0] else None
+        dy2 = dy.reshape(-1, N)
+        if ctx.slot is not None:
+            ctx.slot.engine._fused_wgrad(ctx.slot, dy2.contiguous(), x.reshape(-1, K).contiguous())
+        db = dy2.float().sum(0).to(dy.dtype) if ctx.has_bias else None
+        return dx, None, None, db, None
+
+
 _FP8_ON = [True]
 
 
@@ -379,15 +401,18 @@ class Fp8Linear(nn.Linear):
             not self.training
             and not getattr(self, "fp8_in_eval", True)
         ) or not _FP8_ON[0] or not _gemm_ok(M, self.out_features, self.in_features) or x.dtype != torch.bfloat16:
-            w = self._dequantised(gathered) if gathered is not None else self.weight
-            return nn.functional.linear(x, w.to(x.dtype), None if self.bias is None else self.bias.to(x.dtype))
+            b = None if self.bias is None else self.bias.to(x.dtype)
+            if gathered is not None:
+                return self._gathered_fallback(x, gathered, b)
+            return nn.functional.linear(x, self.weight.to(x.dtype), b)
         b = None if self.bias is None else self.bias.to(torch.bfloat16)
         if self.fp8_recipe.mx:
             if _mx_ok(M, self.out_features, self.in_features) and gathered is None:
                 w = self.weight if self.weight.dtype == torch.bfloat16 else self.weight.to(torch.bfloat16)
                 return _MxLinearFn.apply(x, w, b, self.fp8_recipe, self._fp8_wgrad_slot(x))
-            w = self._dequantised(gathered) if gathered is not None else self.weight
-            return nn.functional.linear(x, w.to(x.dtype), b)  # shapes the MX tiling cannot cover run in bf16
+            if gathered is not None:
+                return self._gathered_fallback(x, gathered, b)
+            return nn.functional.linear(x, self.weight.to(x.dtype), b)  # shapes the MX tiling cannot cover run in bf16
         if gathered is not None:
             unit, info = gathered
             return _Fp8LinearFn.apply(x, self.weight, b, self.fp8_recipe, self._fp8_wgrad_slot(x),
@@ -395,11 +420,16 @@ class Fp8Linear(nn.Linear):
         w = self.weight if self.weight.dtype == torch.bfloat16 else self.weight.to(torch.bfloat16)
         return _Fp8LinearFn.apply(x, w, b, self.fp8_recipe, self._fp8_wgrad_slot(x))
 
-    def _dequantised(self, gathered):
-        """bf16 value of an fp8-gathered weight (non-fp8 fallback paths: eval, unsupported shapes)."""
+    def _gathered_fallback(self, x, gathered, b):
+        """Non-fp8 path (eval, a batch whose M the fp8 GEMM cannot tile, non-bf16 input) for a weight that arrived as
+        e4m3 from the FSDP fp8 all-gather: linear on its dequantised value, with the weight gradient computed in the
+        input dtype and written to the weight's FSDP slot (the e4m3 parameter itself cannot hold an autograd grad)."""
         unit, info = gathered
         amax = unit.engine.fp8_weight_scale(unit, info)
-        return (self.weight.detach().float() * (amax.clamp_min(1e-12) / E4M3_MAX)).to(torch.bfloat16)
+        slot = self._fp8_wgrad_slot(x)
+        if slot is None and torch.is_grad_enabled() and self.weight.requires_grad:
+            raise RuntimeError(f"fp8-gathered weight {info.fqn} has no FSDP gradient slot; its gradient would be lost")
+        return _Fp8GatheredFallbackFn.apply(x, self.weight, amax, b, slot)
 
     def _fp8_wgrad_slot(self, x):
         """The FSDP fused-wgrad slot of this weight (parallel/fsdp.py), when the gradient can be written in place."""

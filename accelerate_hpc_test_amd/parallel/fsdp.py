@@ -306,6 +306,9 @@ class FSDPEngine:
         `enable_fsdp_float8_all_gather` semantics: dynamic per-tensor scaling from the global amax)."""
         if not self.fp8_all_gather or self.param_dtype != torch.bfloat16 or self.offload:
             return False
+        if os.environ.get("ACCELERATE_FSDP_FUSED_WGRAD", "1") == "0":
+            # an e4m3 parameter cannot take an autograd gradient: its weight gradient must go to the fused slot
+            return False
         m = info.module
         rec = getattr(m, "fp8_recipe", None)
         return (isinstance(m, Fp8Linear) and info.attr == "weight" and info.param.requires_grad and len(info.shape) == 2
@@ -745,6 +748,7 @@ class FSDPEngine:
             flat = unit.grad_shard[info.local_lo : info.local_hi]
             acc = sp.grad is not None
             sp.grad = flat
+            info.fused_written = True
             return flat.view(info.shape), acc
         if unit.full_grad is None:
             self._prepare_grad_buffer(unit)
@@ -839,6 +843,7 @@ class FSDPEngine:
             return
         unit.reduced = True
         W = self.world_size
+        self._zero_unwritten_fused(unit)
         # torch semantics: grads accumulate until the optimizer (or user) sets them to None.
         first = (not unit.grad_valid) or all(i.shard_param.grad is None for i in unit.infos if i.shard_param.requires_grad)
         if not self.sharded and self.replicate_size == 1:
@@ -875,6 +880,20 @@ class FSDPEngine:
         self._overlap_step(unit, self.rs_stream)
         if not unit.is_root and self.sharded:
             self._free_full(unit)  # block done with backward: drop its gathered params
+
+    def _zero_unwritten_fused(self, unit: FlatUnit):
+        """A fused weight whose Linear did not run in this backward (a skipped branch, an unused head) never wrote its
+        gradient slot, which `_new_grad_buffer` leaves unzeroed (and, at world size 1, the fp32 grad shard still holds
+        the previous step's gradient): zero it so the reduction never carries a stale gradient."""
+        direct = self._direct_grads()
+        for info in unit.infos:
+            if not (info.fused and info.param.requires_grad) or info.fused_written:
+                continue
+            if direct:
+                if info.shard_param.grad is None:  # accumulating micro-batches keep their sum
+                    unit.grad_shard[info.local_lo : info.local_hi].zero_()
+            elif unit.full_grad is not None:
+                unit.full_grad[info.offset : info.offset + info.numel].zero_()
 
     # =========================================================================================== optimizer overlap
     def attach_overlapped_optimizer(self, step_fn: Callable[[list], None]):

@@ -348,9 +348,11 @@ def test_opt_in_upstream_command_aliases(tmp_path):
     assert aliases.listed(str(d))["accelerate-config"] == "installed"
     foreign = tmp_path / "other"
     foreign.mkdir()
-    (foreign / "accelerate").write_text("#!/bin/sh\necho upstream\n")
+    (foreign / "accelerate-merge-weights").write_text("#!/bin/sh\necho upstream\n")  # the LAST alias written
     with pytest.raises(FileExistsError):
         aliases.install(str(foreign))
+    assert [p.name for p in foreign.iterdir()] == ["accelerate-merge-weights"]  # refused before writing anything
+    (foreign / "accelerate-merge-weights").rename(foreign / "accelerate")
     assert aliases.remove(str(foreign)) == [] and (foreign / "accelerate").exists()
     main(["aliases", "remove", "--dir", str(d)])
     assert list(d.iterdir()) == []

@@ -162,3 +162,13 @@ def test_fsdp_ddp_at_node_scale(world):
 
 def test_ddp_forced_reducer_single_rank():
     debug_launcher(td.check_ddp_forced_single_rank, num_processes=1)
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_fsdp_skipped_fused_weight_gets_no_stale_grad(world):
+    debug_launcher(td.check_fsdp_skipped_fused_weight, num_processes=world)
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_fsdp_fp8_all_gather_ragged_batch_keeps_weight_grads(world):
+    debug_launcher(td.check_fsdp_fp8_all_gather_ragged_batch, num_processes=world)
