@@ -795,6 +795,8 @@ class Accelerator:
             group = mesh.group("dp_shard_cp") if self.parallelism_config.fsdp_dim_names else None
             if self.parallelism_config.dp_replicate_enabled:
                 replicate_group = mesh.group("dp_replicate")
+        elif self.num_processes > 1 and plugin.sharding_strategy in ("NO_SHARD", "HYBRID_SHARD", "HYBRID_SHARD_ZERO2"):
+            group, replicate_group = self._fsdp1_strategy_groups(plugin.sharding_strategy)
         init_fn = getattr(model, "init_weights", None)
         init_fn = (lambda m, _f=init_fn: _f(m)) if init_fn is not None else (lambda m: [getattr(c, "reset_parameters", lambda: None)() for c in m.modules()])
         if self.parallelism_config is not None and self.parallelism_config.ep_enabled:
@@ -821,6 +823,36 @@ class Accelerator:
         )
         self._fsdp_engines.append(wrapped.engine)
         return wrapped
+
+    def _fsdp1_strategy_groups(self, strategy: str):
+        """(shard group, replicate group) for the FSDP1 strategies that are not a plain full shard over the world
+        (reference accelerator.py:1909-1925 hands `sharding_strategy` to torch FSDP1; `commands/to_fsdp2.py:50-66`
+        maps it onto FSDP2): NO_SHARD -> every rank its own shard group (the engine's unsharded path) and one
+        replicate all-reduce over the world, i.e. DDP on the FSDP engine; HYBRID_SHARD / HYBRID_SHARD_ZERO2 -> shard
+        within a node (LOCAL_WORLD_SIZE ranks over xGMI), replicate across nodes (the HSDP path). Groups are created
+        collectively, in the same order on every rank, and cached."""
+        cached = getattr(self, "_fsdp1_groups", None)
+        if cached is not None and cached[0] == strategy:
+            return cached[1], cached[2]
+        W, r = self.num_processes, self.process_index
+        shard = 1 if strategy == "NO_SHARD" else int(os.environ.get("LOCAL_WORLD_SIZE", W) or W)
+        if shard <= 0 or W % shard:
+            raise ValueError(f"{strategy}: world size {W} is not a multiple of the node size {shard} (LOCAL_WORLD_SIZE)")
+        reps = W // shard
+        shard_group = replicate_group = None
+        for n in range(reps):  # shard groups: consecutive node-local blocks
+            ranks = list(range(n * shard, (n + 1) * shard))
+            g = torch.distributed.new_group(ranks) if shard < W else torch.distributed.group.WORLD
+            if r in ranks:
+                shard_group = g
+        if reps > 1:
+            for k in range(shard):  # replicate groups: the same local rank on every node
+                ranks = list(range(k, W, shard))
+                g = torch.distributed.new_group(ranks) if reps < W else torch.distributed.group.WORLD
+                if r in ranks:
+                    replicate_group = g
+        self._fsdp1_groups = (strategy, shard_group, replicate_group)
+        return shard_group, replicate_group
 
     def _fsdp_fp8_all_gather(self) -> bool:
         """torchao-style fp8 all-gather of the FSDP shards (reference examples/torch_native_parallelism/fsdp2_fp8.py:69-75):

@@ -193,6 +193,7 @@ class FSDPEngine:
         else:
             self.world_size, self.rank = 1, 0
         self.replicate_size = dist.get_world_size(replicate_group) if replicate_group is not None else 1
+        self.replicate_rank = dist.get_rank(replicate_group) if replicate_group is not None else 0
         # `sharded`: the unit buffers are sharded and every collective of the W>1 path runs. At world size 1 this is the
         # degenerate no-collective path unless `force_sharded` (RcclKwargs.fsdp_force_sharded): then the one GPU runs
         # exactly the multi-GPU code (separate full buffer resized 0 <-> full, RCCL all-gather / reduce-scatter with
@@ -204,6 +205,24 @@ class FSDPEngine:
         self.output_dtype = mp.output_dtype
         self.reshard_after_forward = bool(plugin.reshard_after_forward) and self.sharded
         self.prefetch_depth = max(0, prefetch_depth)
+        # FSDP1 prefetch flags (reference accelerator.py:1909-1925 passes them to torch FSDP1). FSDP2 has neither
+        # flag: the forward prefetches `prefetch_depth` units ahead and the backward prefetches before each unit's
+        # gradient computation. With fsdp_version=1:
+        #   forward_prefetch=False -> no explicit forward prefetch (the next all-gather is issued by the next unit's
+        #     pre-forward hook, which still overlaps the GPU when the host runs ahead); True -> `prefetch_depth` ahead;
+        #   backward_prefetch None (NO_PREFETCH) / BACKWARD_PRE (before this unit's gradient computation) /
+        #     BACKWARD_POST (after this unit's gradients are reduced);
+        #   limit_all_gathers=False -> at least 2 units of forward prefetch (True: the engine's inherent bound of
+        #     prefetch_depth + 1 gathered units, as each unit's buffer is freed in stream order after its use).
+        self.fsdp1 = getattr(plugin, "fsdp_version", 2) == 1
+        if self.fsdp1:
+            self.fwd_prefetch_depth = self.prefetch_depth if plugin.forward_prefetch else 0
+            if plugin.forward_prefetch and plugin.limit_all_gathers is False:
+                self.fwd_prefetch_depth = max(self.fwd_prefetch_depth, 2)
+            self.bwd_prefetch = plugin.backward_prefetch  # None, "BACKWARD_PRE" or "BACKWARD_POST"
+        else:
+            self.fwd_prefetch_depth = self.prefetch_depth
+            self.bwd_prefetch = "BACKWARD_PRE"
         self.requires_grad_sync = True
         self.is_cuda = device.type == "cuda"
         # gloo lacks all_gather_into_tensor / reduce_scatter_tensor (CPU tensors, and HIP tensors when several ranks
@@ -459,8 +478,10 @@ class FSDPEngine:
         # cpu_ram_efficient_loading (reference fsdp_utils.py:467-554,664-719): only rank 0 holds the real (pretrained)
         # weights — the other ranks built the model on the meta device — and rank 0's unit is broadcast over the
         # shard group straight into HBM, one unit at a time (one RCCL broadcast per block instead of one per tensor).
-        ram_efficient = bool(getattr(self.plugin, "cpu_ram_efficient_loading", False)) and W > 1
-        if ram_efficient and r != 0:
+        R = self.replicate_size
+        ram_efficient = bool(getattr(self.plugin, "cpu_ram_efficient_loading", False)) and (W > 1 or R > 1)
+        holds_weights = (dist.get_rank() == 0) if dist.is_available() and dist.is_initialized() else True
+        if ram_efficient and not holds_weights:
             for info in unit.infos:
                 if info.param.is_meta:
                     view = full32[info.offset : info.offset + info.numel].view(info.shape)
@@ -490,8 +511,11 @@ class FSDPEngine:
         else:
             for info in unit.infos:
                 full32[info.offset : info.offset + info.numel].copy_(info.param.detach().reshape(-1).to(dev, torch.float32))
-        if W > 1 and (ram_efficient or (self.plugin.sync_module_states and not on_meta)):
+        sync = ram_efficient or (self.plugin.sync_module_states and not on_meta)
+        if W > 1 and sync:
             dist.broadcast(full32, src=dist.get_global_rank(self.group, 0) if self.group is not None else 0, group=self.group)
+        if R > 1 and sync:  # HSDP / NO_SHARD replicas: then from replica 0 to the same shard position of every replica
+            dist.broadcast(full32, src=dist.get_global_rank(self.replicate_group, 0), group=self.replicate_group)
         local32 = unit.local_of_full(full32)  # this rank's slice of every region, concatenated
         if self.offload:
             unit.master = self._host(local32)
@@ -637,13 +661,13 @@ class FSDPEngine:
         return hook
 
     def _prefetch_forward(self, unit):
-        if not self.sharded or self.prefetch_depth == 0:
+        if not self.sharded or self.fwd_prefetch_depth == 0:
             return
         try:
             i = self.exec_order.index(unit)
         except ValueError:
             return
-        for nxt in self.exec_order[i + 1 : i + 1 + self.prefetch_depth]:
+        for nxt in self.exec_order[i + 1 : i + 1 + self.fwd_prefetch_depth]:
             self._unshard(nxt)
 
     def _make_post_forward(self, unit: FlatUnit):
@@ -669,7 +693,8 @@ class FSDPEngine:
                 unit.in_backward = True
                 self._queue_final_callback()
                 self._wait_unsharded(unit)
-                self._prefetch_backward(unit)
+                if self.bwd_prefetch == "BACKWARD_PRE":
+                    self._prefetch_backward(unit)
                 self._prepare_grad_buffer(unit)
             return grad
 
@@ -862,7 +887,7 @@ class FSDPEngine:
             self._overlap_step(unit, torch.cuda.current_stream(self.device) if self.is_cuda else None)
             return
         src = unit.full_grad if unit.full_grad.dtype == self.reduce_dtype else unit.full_grad.to(self.reduce_dtype)
-        out = torch.empty(unit.shard_numel, dtype=self.reduce_dtype, device=self.device)
+        out = self._reduce_out(unit)
         if self.is_cuda:
             cur = torch.cuda.current_stream(self.device)
             self.rs_stream.wait_stream(cur)
@@ -870,8 +895,8 @@ class FSDPEngine:
                 self._rs_and_accumulate(unit, src, out, first)
                 unit._rs_done = torch.cuda.Event()
                 unit._rs_done.record(self.rs_stream)
-            src.record_stream(self.rs_stream)
-            out.record_stream(self.rs_stream)
+            if src is not unit.full_grad:
+                src.record_stream(self.rs_stream)
         else:
             self._rs_and_accumulate(unit, src, out, first)
         unit.grad_valid = True
@@ -880,6 +905,20 @@ class FSDPEngine:
         self._overlap_step(unit, self.rs_stream)
         if not unit.is_root and self.sharded:
             self._free_full(unit)  # block done with backward: drop its gathered params
+        if self.bwd_prefetch == "BACKWARD_POST" and unit.in_backward:
+            self._prefetch_backward(unit)
+
+    def _reduce_out(self, unit: FlatUnit) -> torch.Tensor:
+        """The reduce-scatter output for `unit`: a view of ONE persistent engine-wide buffer (the largest shard). Every
+        reduce-scatter and the grad-shard update that consumes its output run in order on the reduce stream, so unit
+        i+1's reduce-scatter starts after unit i's update has read the buffer. A fresh buffer per unit per step would
+        be released with reduce-stream uses recorded on it while the host runs a step ahead of the GPU, which is how
+        the caching allocator piled up blocks before (round-2 forced-sharded blow-up to 285 of 288 GiB)."""
+        buf = getattr(self, "_rs_out_buf", None)
+        if buf is None or buf.dtype != self.reduce_dtype or buf.numel() < unit.shard_numel:
+            n = max(u.shard_numel for u in self.units)
+            buf = self._rs_out_buf = torch.empty(n, dtype=self.reduce_dtype, device=self.device)
+        return buf[: unit.shard_numel]
 
     def _zero_unwritten_fused(self, unit: FlatUnit):
         """A fused weight whose Linear did not run in this backward (a skipped branch, an unused head) never wrote its
@@ -1045,7 +1084,7 @@ class FSDPEngine:
         """Called by the wrapper before the model's forward: gather the root unit (+ prefetch the first block)."""
         self._wait_unsharded(self.root)
         if not self._recording_order and self.exec_order:
-            for u in self.exec_order[: self.prefetch_depth]:
+            for u in self.exec_order[: self.fwd_prefetch_depth]:
                 self._unshard(u)
 
     def post_root_forward(self, output):

@@ -1156,3 +1156,61 @@ def check_fsdp_fp8_all_gather_ragged_batch():
             assert d1.abs().max() > 0, f"{k}: no update with the fp8 all-gather"
             cos = float(torch.dot(d0, d1) / (d0.norm() * d1.norm()))
             assert cos > 0.98 and abs(float(d1.norm() / d0.norm()) - 1) < 0.05, (k, cos, float(d1.norm() / d0.norm()))
+
+
+def check_fsdp1_strategy(strategy: str, backward_prefetch=None, forward_prefetch: bool = False, local_world: int = 2):
+    """FSDP1 `sharding_strategy` semantics on the native engine (reference accelerator.py:1909-1925; mapping of
+    commands/to_fsdp2.py:50-66): NO_SHARD = unsharded units + a replicate all-reduce over the world; HYBRID_SHARD(_ZERO2)
+    = shard within LOCAL_WORLD_SIZE ranks, replicate across; SHARD_GRAD_OP keeps params gathered after forward. Shard
+    sizes, groups and prefetch mode are asserted, then training (with clipping) and a sharded checkpoint round trip are
+    compared with the single-process model."""
+    os.environ["LOCAL_WORLD_SIZE"] = str(local_world)
+    plugin = FullyShardedDataParallelPlugin(
+        fsdp_version=1, sharding_strategy=strategy, auto_wrap_policy="transformer_based_wrap",
+        transformer_cls_names_to_wrap=["Block"], backward_prefetch=backward_prefetch, forward_prefetch=forward_prefetch,
+        state_dict_type="SHARDED_STATE_DICT")
+    acc = Accelerator(cpu=True, fsdp_plugin=plugin)
+    W, r = acc.num_processes, acc.process_index
+    set_seed(0)
+    base = TinyMLP()
+    model = copy.deepcopy(base)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-2, weight_decay=0.01)
+    base_opt = torch.optim.AdamW(base.parameters(), lr=1e-2, weight_decay=0.01)
+    model, opt = acc.prepare(model, opt)
+    eng = model.engine
+    shard, reps = {"NO_SHARD": (1, W), "FULL_SHARD": (W, 1), "SHARD_GRAD_OP": (W, 1)}.get(strategy, (local_world, W // local_world))
+    assert (eng.world_size, eng.replicate_size) == (shard, reps), (strategy, eng.world_size, eng.replicate_size)
+    assert eng.sharded == (shard > 1)
+    assert eng.reshard_after_forward == (strategy in ("FULL_SHARD", "HYBRID_SHARD") and shard > 1)
+    for u in eng.units:
+        assert u.shard_numel * shard == u.padded, (u.shard_numel, u.padded)
+    assert eng.bwd_prefetch == backward_prefetch and eng.fwd_prefetch_depth == (eng.prefetch_depth if forward_prefetch else 0)
+    bs = 4
+    for x, y in _global_batches(3, bs, W):
+        xl, yl = x[r * bs : (r + 1) * bs], y[r * bs : (r + 1) * bs]
+        acc.backward(F.mse_loss(model(xl), yl))
+        n1 = acc.clip_grad_norm_(model.parameters(), 0.5)
+        opt.step()
+        opt.zero_grad()
+        F.mse_loss(base(x), y).backward()
+        n2 = torch.nn.utils.clip_grad_norm_(base.parameters(), 0.5)
+        assert torch.allclose(n1.reshape(()), n2, rtol=1e-4), (n1, n2)
+        base_opt.step()
+        base_opt.zero_grad()
+    full = acc.get_state_dict(model)
+    for n, q in base.named_parameters():
+        assert torch.allclose(full[n], q, atol=1e-5), (strategy, n, (full[n] - q).abs().max())
+    d = tempfile.mkdtemp() if r == 0 else None
+    d = gather_object([d])[0]
+    acc.save_state(d)
+    if r == 0:  # replicas do not duplicate shard files
+        files = sorted(f for f in os.listdir(os.path.join(d, "pytorch_model_fsdp_0")) if f.startswith("shard_"))
+        assert files == [f"shard_{i}.safetensors" for i in range(shard)], files
+    acc.wait_for_everyone()
+    with torch.no_grad():
+        for p in model.parameters():
+            p.add_(1.0)
+    acc.load_state(d)
+    back = acc.get_state_dict(model)
+    for n in full:
+        assert torch.allclose(full[n], back[n]), n

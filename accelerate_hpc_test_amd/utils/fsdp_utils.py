@@ -64,6 +64,9 @@ def save_fsdp_model(fsdp_plugin, accelerator, model, output_dir, model_index=0, 
         from safetensors.torch import save_file
 
         r = eng.rank
+        if getattr(eng, "replicate_rank", 0) != 0:  # HSDP / NO_SHARD replicas hold identical shards: replica 0 writes
+            _barrier()
+            return
         save_file({k: v.contiguous() for k, v in shard["tensors"].items()}, os.path.join(ckpt_dir, f"shard_{r}.safetensors"))
         with open(os.path.join(ckpt_dir, f"meta_{r}.json"), "w") as f:
             json.dump(shard["meta"], f)
@@ -170,7 +173,8 @@ def save_fsdp_optimizer(fsdp_plugin, accelerator, optimizer, model, output_dir, 
         fqn_of = {id(info.shard_param): info.fqn for unit in eng.units for info in unit.infos}
         groups = [{**{k: v for k, v in g.items() if k != "params"}, "params": [fqn_of.get(id(p)) for p in g["params"]]} for g in opt.param_groups]
         meta = {info.fqn: {"param_lo": info.param_lo, "numel": info.local_hi - info.local_lo} for unit in eng.units for info in unit.infos}
-        torch.save({"state": local, "param_groups": groups, "meta": meta}, os.path.join(d, f"shard_{eng.rank}.pt"))
+        if getattr(eng, "replicate_rank", 0) == 0:  # replicas hold identical optimizer shards
+            torch.save({"state": local, "param_groups": groups, "meta": meta}, os.path.join(d, f"shard_{eng.rank}.pt"))
     _barrier()
 
 

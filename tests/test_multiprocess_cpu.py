@@ -172,3 +172,15 @@ def test_fsdp_skipped_fused_weight_gets_no_stale_grad(world):
 @pytest.mark.parametrize("world", [1, 2])
 def test_fsdp_fp8_all_gather_ragged_batch_keeps_weight_grads(world):
     debug_launcher(td.check_fsdp_fp8_all_gather_ragged_batch, num_processes=world)
+
+
+@pytest.mark.parametrize("strategy,bp,fp", [
+    ("NO_SHARD", None, False),
+    ("HYBRID_SHARD", "BACKWARD_PRE", True),
+    ("HYBRID_SHARD_ZERO2", "BACKWARD_POST", False),
+    ("FULL_SHARD", "BACKWARD_POST", True),
+    ("SHARD_GRAD_OP", None, False),
+])
+def test_fsdp1_sharding_strategies_four_ranks(strategy, bp, fp):
+    """FSDP1 flags are honoured, not silently full-shard (round-2 verdict): 4 gloo ranks, node size 2."""
+    debug_launcher(td.check_fsdp1_strategy, args=(strategy, bp, fp, 2), num_processes=4)

@@ -1,4 +1,7 @@
-"""Microbenchmark of the HIP flash-attention kernels (fwd / bwd) at Llama-3-8B shapes: TFLOP/s on random data."""
+"""Microbenchmark of the HIP flash-attention kernels (fwd / bwd) at Llama-3-8B shapes: TFLOP/s on random data, next
+to `torch.nn.functional.scaled_dot_product_attention` (the reference's attention: SDPA inside the user model) with each
+ROCm backend torch ships (flash = AOTriton/CK flash kernels, efficient = memory-efficient kernels), GQA via
+`enable_gqa`, same shapes and causal masks. `--no-sdpa` skips the library rows."""
 import argparse, json, math, time
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -11,6 +14,7 @@ p.add_argument("--Hq", type=int, default=32)
 p.add_argument("--Hkv", type=int, default=8)
 p.add_argument("--B", type=int, default=1)
 p.add_argument("--iters", type=int, default=10)
+p.add_argument("--no-sdpa", action="store_true")
 p.add_argument("--dbg", action="store_true", help="also time the causal backward's kernels separately and the dK/dV "
                "diagnostic variants (cache-hot fetch / no LDS commit); timing only")
 a = p.parse_args()
@@ -53,4 +57,39 @@ if a.dbg:
         dbg[name + "_ms"] = round((time.perf_counter() - t) / a.iters * 1e3, 3)
     e.attn_debug_mode(0)
     res["causal_bwd_parts"] = dbg
+if not a.no_sdpa:
+    import torch.nn.functional as F
+    from torch.nn.attention import SDPBackend, sdpa_kernel
+
+    def tm2(fn):
+        fn(); torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(a.iters): fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t) / a.iters
+
+    qt = q.transpose(1, 2).contiguous().requires_grad_()
+    kt = k.transpose(1, 2).contiguous().requires_grad_()
+    vt = v.transpose(1, 2).contiguous().requires_grad_()
+    for bname, backend in (("sdpa_flash", SDPBackend.FLASH_ATTENTION), ("sdpa_efficient", SDPBackend.EFFICIENT_ATTENTION)):
+        for causal in (True, False):
+            key = f"{bname}_{'causal' if causal else 'full'}"
+            f = 0.5 if causal else 1.0
+            fl_fwd = 4 * a.B * a.Hq * a.S * a.S * D * f
+            try:
+                with sdpa_kernel(backend):
+                    with torch.no_grad():
+                        tf = tm2(lambda: F.scaled_dot_product_attention(qt, kt, vt, is_causal=causal, enable_gqa=True))
+                    out = F.scaled_dot_product_attention(qt, kt, vt, is_causal=causal, enable_gqa=True)
+                    go = torch.randn_like(out)
+
+                    def fb():
+                        o2 = F.scaled_dot_product_attention(qt, kt, vt, is_causal=causal, enable_gqa=True)
+                        torch.autograd.grad(o2, (qt, kt, vt), go)
+                    tfb = tm2(fb)
+                tb = max(tfb - tf, 1e-9)
+                res[key] = {"fwd_ms": round(tf * 1e3, 3), "fwd_tflops": round(fl_fwd / tf / 1e12, 1),
+                            "bwd_ms": round(tb * 1e3, 3), "bwd_tflops": round(2.5 * fl_fwd / tb / 1e12, 1)}
+            except Exception as exc:  # noqa: BLE001 - a backend that rejects the shape is reported, not fatal
+                res[key] = {"error": repr(exc)[:200]}
 print(json.dumps({"shape": vars(a), **res}))

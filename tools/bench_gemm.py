@@ -1,4 +1,6 @@
-"""GEMM throughput at the Llama-3-8B linear shapes: our MX-fp8 MFMA kernels vs bf16 hipBLASLt (torch.matmul).
+"""GEMM throughput at the Llama-3-8B linear shapes: our MX-fp8 MFMA kernels vs the libraries torch ships — bf16
+hipBLASLt (torch.matmul) and fp8 hipBLASLt through `torch._scaled_mm` with per-tensor scales, which is the GEMM the
+reference's torchao Float8Linear path calls (`/root/reference/src/accelerate/utils/ao.py:104-143`).
 
 All kernel variants run in ONE process, in interleaved rounds (`ext().fp8_gemm_select`), on random data; one JSON
 line per shape with the median ms / TFLOP/s of each variant over the rounds.
@@ -42,6 +44,7 @@ def main():
     p.add_argument("--variants", default="2,4")
     p.add_argument("--shapes", default="qkv,o,gate_up,down")
     p.add_argument("--no-bf16", action="store_true")
+    p.add_argument("--no-scaled-mm", action="store_true")
     args = p.parse_args()
     from accelerate_hpc_test_amd.ops import fp8, gemm_tuning
     from accelerate_hpc_test_amd.ops._ext import ext
@@ -71,9 +74,18 @@ def main():
             times = {v: [] for v in variants}
             mxq = []
             bf = []
+            smm = []
+            smm_ok = not args.no_scaled_mm
             for _ in range(args.rounds):
                 if not args.no_bf16:
                     bf.append(timeit(lambda: a @ b.t(), args.iters))
+                if smm_ok:
+                    try:  # hipBLASLt fp8 (e4m3 x e4m3 -> bf16, per-tensor scales), B column-major as _scaled_mm wants
+                        smm.append(timeit(lambda: torch._scaled_mm(a8, b8.t(), scale_a=one, scale_b=one,
+                                                                   out_dtype=torch.bfloat16), args.iters))
+                    except Exception as exc:  # noqa: BLE001 - report, keep benchmarking the rest
+                        smm_ok = False
+                        print(json.dumps({"scaled_mm_error": repr(exc)[:300]}), flush=True)
                 for v in variants:
                     select(v)
                     if v == "mx":
@@ -86,6 +98,9 @@ def main():
             if bf:
                 ms = statistics.median(bf)
                 row.update(bf16_ms=round(ms, 3), bf16_tflops=round(flops / ms / 1e9, 1))
+            if smm:
+                ms = statistics.median(smm)
+                row.update(scaled_mm_ms=round(ms, 3), scaled_mm_tflops=round(flops / ms / 1e9, 1))
             for v in variants:
                 ms = statistics.median(times[v])
                 row[f"v{v}_ms"] = round(ms, 3)
