@@ -71,6 +71,9 @@ void cpu_adam_step(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Ten
                    double lr, double beta1, double beta2, double eps, double wd, double bc1, double bc2_sqrt, bool adamw);
 bool blaslt_wgrad_f32(torch::Tensor dy, torch::Tensor x, torch::Tensor out, bool accumulate);
 std::vector<std::tuple<int64_t, int64_t, int64_t, int64_t, double>> blaslt_wgrad_plans();
+bool blaslt_fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor sa, torch::Tensor sb, double alpha, torch::Tensor out,
+                     bool accumulate);
+std::vector<std::tuple<int64_t, int64_t, int64_t, int64_t, double>> blaslt_fp8_plans();
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "MI355X (gfx950) native kernels and runtime for accelerate_hpc_test_amd";
@@ -121,4 +124,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("blaslt_wgrad_f32", &blaslt_wgrad_f32);
   m.def("cpu_adam_step", &cpu_adam_step);
   m.def("blaslt_wgrad_plans", &blaslt_wgrad_plans);
+  m.def("blaslt_fp8_gemm", &blaslt_fp8_gemm, "per-tensor-scaled fp8 GEMM on hipBLASLt (C = alpha sa sb A B^T)");
+  m.def("blaslt_fp8_plans", &blaslt_fp8_plans);
 }

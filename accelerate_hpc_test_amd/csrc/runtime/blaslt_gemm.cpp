@@ -136,6 +136,154 @@ bool blaslt_wgrad_f32(torch::Tensor dy, torch::Tensor x, torch::Tensor out, bool
                                kWorkspace, stream));
 }
 
+// ------------------------------------------------------------------------------------------------ fp8, per-tensor
+// C[M, N] (=|+=) alpha * sa * sb * (A[M, K] . B[N, K]^T)   A, B: row-major (K-contiguous) e4m3 / e5m2; sa, sb: device
+// fp32 [1] scale factors read by the kernel (Fp8Linear passes each operand's amax and folds 1 / (qmax_a * qmax_b)
+// into alpha, so no scale arithmetic runs on the device); C: row-major bf16 or fp32, accumulated with beta = 1.
+// This is the per-tensor-scaled fp8 GEMM the reference reaches through torchao -> torch._scaled_mm -> hipBLASLt;
+// measured on MI355X it runs the Llama-3-8B linear shapes at 2.7-3.4 PF/s (profiles/r3_gemm_fp8_library.md), so the
+// per-tensor path uses it. Column-major view: D (N x M, ld N) = op_T(B: K x N, ld K) . op_N(A: K x M, ld K) — the TN
+// form hipBLASLt's fp8 kernels are built for. Per (M, N, K, dtypes, output) the candidates are timed once.
+namespace {
+
+struct F8Plan {
+  hipblasLtMatmulDesc_t desc = nullptr;
+  hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, lc = nullptr;
+  hipblasLtMatmulAlgo_t algo;
+  bool ok = false;
+  float ms = 0.f;
+  int candidates = 0;
+};
+
+struct F8State {
+  std::map<std::tuple<int64_t, int64_t, int64_t, int, int, int, int>, F8Plan> plans;
+};
+
+F8State& f8state() {
+  static F8State s;
+  return s;
+}
+
+hipDataType f8type(at::ScalarType t) { return t == at::kFloat8_e5m2 ? HIP_R_8F_E5M2 : HIP_R_8F_E4M3; }
+
+bool set_scales(hipblasLtMatmulDesc_t desc, const void* sa, const void* sb) {
+  // hipBLASLt's matA is B (weights / second operand), matB is A
+  return check(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_A_SCALE_POINTER, &sb, sizeof(sb))) &&
+         check(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_B_SCALE_POINTER, &sa, sizeof(sa)));
+}
+
+bool build_f8_plan(State& s, F8Plan& p, int64_t M, int64_t N, int64_t K, at::ScalarType ta_, at::ScalarType tb_, bool out_f32,
+                   hipStream_t stream, const torch::Tensor& like) {
+  const hipblasOperation_t opA = HIPBLAS_OP_T, opB = HIPBLAS_OP_N;
+  const hipDataType dt = out_f32 ? HIP_R_32F : HIP_R_16BF;
+  if (!check(hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F))) return false;
+  if (!check(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &opA, sizeof(opA)))) return false;
+  if (!check(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &opB, sizeof(opB)))) return false;
+  if (!check(hipblasLtMatrixLayoutCreate(&p.la, f8type(tb_), K, N, K))) return false;
+  if (!check(hipblasLtMatrixLayoutCreate(&p.lb, f8type(ta_), K, M, K))) return false;
+  if (!check(hipblasLtMatrixLayoutCreate(&p.lc, dt, N, M, N))) return false;
+  auto one_t = torch::ones({2}, like.options().dtype(torch::kFloat32));
+  if (!set_scales(p.desc, one_t.data_ptr<float>(), one_t.data_ptr<float>() + 1)) return false;
+  hipblasLtMatmulPreference_t pref;
+  if (!check(hipblasLtMatmulPreferenceCreate(&pref))) return false;
+  uint64_t ws = kWorkspace;
+  hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &ws, sizeof(ws));
+  std::vector<hipblasLtMatmulHeuristicResult_t> res(32);
+  int got = 0;
+  const bool okh = check(hipblasLtMatmulAlgoGetHeuristic(s.handle, p.desc, p.la, p.lb, p.lc, p.lc, pref, (int)res.size(),
+                                                         res.data(), &got));
+  hipblasLtMatmulPreferenceDestroy(pref);
+  if (!okh || got <= 0) return false;
+  p.candidates = got;
+  auto a = torch::empty({M, K}, like.options().dtype(torch::kUInt8)).random_(0, 64);  // small finite fp8 values
+  auto b = torch::empty({N, K}, like.options().dtype(torch::kUInt8)).random_(0, 64);
+  auto d = torch::empty({M, N}, like.options().dtype(out_f32 ? torch::kFloat32 : torch::kBFloat16));
+  const float one = 1.f, zero = 0.f;
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  float best = 1e30f;
+  for (int i = 0; i < got; ++i) {
+    if (res[i].state != HIPBLAS_STATUS_SUCCESS || res[i].workspaceSize > kWorkspace) continue;
+    auto run = [&]() {
+      return hipblasLtMatmul(s.handle, p.desc, &one, b.data_ptr(), p.la, a.data_ptr(), p.lb, &zero, d.data_ptr(), p.lc,
+                             d.data_ptr(), p.lc, &res[i].algo, s.workspace.data_ptr(), kWorkspace, stream);
+    };
+    if (!check(run())) continue;
+    hipEventRecord(e0, stream);
+    for (int r = 0; r < 3; ++r) run();
+    hipEventRecord(e1, stream);
+    hipEventSynchronize(e1);
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, e0, e1);
+    if (ms < best) {
+      best = ms;
+      p.algo = res[i].algo;
+      p.ok = true;
+    }
+  }
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  p.ms = best / 3.f;
+  return p.ok;
+}
+
+}  // namespace
+
+// Returns false (nothing launched) when hipBLASLt has no working algorithm for the problem; the caller then uses the
+// hand-written MX-MFMA kernel.
+bool blaslt_fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor sa, torch::Tensor sb, double alpha, torch::Tensor out,
+                     bool accumulate) {
+  TORCH_CHECK(a.is_cuda() && b.is_cuda() && out.is_cuda() && sa.is_cuda() && sb.is_cuda(), "blaslt_fp8_gemm: HIP tensors expected");
+  const auto ta = a.scalar_type(), tb = b.scalar_type();
+  TORCH_CHECK((ta == at::kFloat8_e4m3fn || ta == at::kFloat8_e5m2) && (tb == at::kFloat8_e4m3fn || tb == at::kFloat8_e5m2),
+              "blaslt_fp8_gemm: e4m3 / e5m2 operands expected");
+  TORCH_CHECK(out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16, "blaslt_fp8_gemm: bf16 / fp32 output");
+  TORCH_CHECK(sa.scalar_type() == at::kFloat && sb.scalar_type() == at::kFloat && sa.numel() >= 1 && sb.numel() >= 1,
+              "blaslt_fp8_gemm: fp32 scale tensors expected");
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && out.dim() == 2 && a.is_contiguous() && b.is_contiguous() && out.is_contiguous(),
+              "blaslt_fp8_gemm: 2-D contiguous tensors expected");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(b.size(1) == K && out.size(0) == M && out.size(1) == N, "blaslt_fp8_gemm: shape mismatch");
+  const bool out_f32 = out.scalar_type() == at::kFloat;
+  State& s = state();
+  F8State& fs = f8state();
+  hipStream_t stream = at::hip::getCurrentHIPStream();
+  F8Plan* plan = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(s.mu);
+    if (s.handle == nullptr) {
+      if (!check(hipblasLtCreate(&s.handle))) return false;
+      s.workspace = torch::empty({(int64_t)kWorkspace}, out.options().dtype(torch::kUInt8));
+    }
+    auto key = std::make_tuple(M, N, K, (int)ta, (int)tb, (int)out_f32, (int)out.get_device());
+    auto it = fs.plans.find(key);
+    if (it == fs.plans.end()) {
+      F8Plan p;
+      build_f8_plan(s, p, M, N, K, ta, tb, out_f32, stream, out);
+      it = fs.plans.emplace(key, p).first;
+    }
+    plan = &it->second;
+    if (!plan->ok) return false;
+    if (!set_scales(plan->desc, sa.data_ptr(), sb.data_ptr())) return false;
+  }
+  const float al = (float)alpha, beta = accumulate ? 1.f : 0.f;
+  return check(hipblasLtMatmul(s.handle, plan->desc, &al, b.data_ptr(), plan->la, a.data_ptr(), plan->lb, &beta,
+                               out.data_ptr(), plan->lc, out.data_ptr(), plan->lc, &plan->algo, s.workspace.data_ptr(),
+                               kWorkspace, stream));
+}
+
+// [(M, N, K, candidates, best ms)] of every fp8 problem searched so far.
+std::vector<std::tuple<int64_t, int64_t, int64_t, int64_t, double>> blaslt_fp8_plans() {
+  std::vector<std::tuple<int64_t, int64_t, int64_t, int64_t, double>> out;
+  State& s = state();
+  std::lock_guard<std::mutex> lk(s.mu);
+  for (auto& kv : f8state().plans)
+    out.emplace_back(std::get<0>(kv.first), std::get<1>(kv.first), std::get<2>(kv.first), kv.second.candidates,
+                     kv.second.ok ? kv.second.ms : -1.0);
+  return out;
+}
+
 // [(T, N, K, candidates, best ms)] of every shape searched so far (diagnostics / bench logs).
 std::vector<std::tuple<int64_t, int64_t, int64_t, int64_t, double>> blaslt_wgrad_plans() {
   std::vector<std::tuple<int64_t, int64_t, int64_t, int64_t, double>> out;

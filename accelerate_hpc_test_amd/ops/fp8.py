@@ -33,6 +33,10 @@ from ._ext import ext, use_native
 
 E4M3_MAX = 448.0
 E5M2_MAX = 57344.0
+# Per-tensor-scaled fp8 GEMM backend: "blaslt" = hipBLASLt's fp8 kernels through our runner (csrc/runtime/blaslt_gemm.cpp;
+# 2.7-3.4 PF/s on the Llama-3-8B shapes vs 2.1-2.7 PF/s for the hand-written MX-MFMA kernel, profiles/r3_gemm_fp8_library.md),
+# "hip" = the hand-written kernel (csrc/kernels/fp8.hip), which also takes every problem hipBLASLt declines (bias epilogue).
+_FP8_GEMM_BACKEND = os.environ.get("ACCELERATE_FP8_GEMM", "blaslt")
 
 
 def amax(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -121,6 +125,10 @@ def gemm(a8: torch.Tensor, b8: torch.Tensor, a_scale_inv, b_scale_inv, bias=None
         e5b = b8.dtype == torch.float8_e5m2
         ta, ma = _inv_parts(a_scale_inv)
         tb, mb = _inv_parts(b_scale_inv)
+        if bias is None and _FP8_GEMM_BACKEND == "blaslt":
+            dst = out if out is not None else torch.empty((a8.shape[0], b8.shape[0]), dtype=out_dtype, device=a8.device)
+            if ext().blaslt_fp8_gemm(a8, b8, ta, tb, ma * mb, dst, accumulate):
+                return dst
         return ext().fp8_gemm(a8, b8, ta, tb, ma * mb, e5a, e5b, bias, out_dtype == torch.float32, out, accumulate)
     ia = a_scale_inv.inv() if isinstance(a_scale_inv, Scale) else a_scale_inv
     ib = b_scale_inv.inv() if isinstance(b_scale_inv, Scale) else b_scale_inv

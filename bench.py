@@ -226,6 +226,12 @@ def main():
     peak = 0.0 if args.cpu else torch.cuda.max_memory_allocated() / 2**30
     if args.verbose and not args.cpu:
         mst = torch.cuda.memory_stats()
+        if args.precision == "fp8":
+            from accelerate_hpc_test_amd.ops._ext import ext as _ext
+
+            plans = _ext().blaslt_fp8_plans()
+            accelerator.print(f"hipBLASLt fp8 problems: {len(plans)}, declined {sum(1 for p in plans if p[4] < 0)}: "
+                              f"{[p[:3] for p in plans if p[4] < 0]}", flush=True)
         accelerator.print(f"allocator: alloc_retries {mst.get('num_alloc_retries', 0)}, reserved peak "
                           f"{mst.get('reserved_bytes.all.peak', 0) / 2**30:.1f} GiB, device frees "
                           f"{mst.get('num_device_free', 0)}", flush=True)

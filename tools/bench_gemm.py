@@ -7,7 +7,7 @@ line per shape with the median ms / TFLOP/s of each variant over the rounds.
 
     python tools/bench_gemm.py [--tokens 8192] [--iters 20] [--rounds 3] [--variants 2,4] [--shapes qkv,o]
 
-variants: 1 = v1 128x128, 2 = v2 256x256 4 waves, 3 = v2 8 waves, 4 = v3 4-deep ring, 5 = v3 8 waves; "4g8" = v3 with tile rows
+variants: bl = hipBLASLt fp8 via csrc/runtime/blaslt_gemm.cpp (the default per-tensor path), 1 = v1 128x128, 2 = v2 256x256 4 waves, 3 = v2 8 waves, 4 = v3 4-deep ring, 5 = v3 8 waves; "4g8" = v3 with tile rows
 grouped by 8 (ext().fp8_gemm_select(variant, group_m)); "mx" = the MXFP8 GEMM (v3 ring with per-32 block scales in the
 MFMA), whose row also reports the one-pass row+column MX quantisation of the A operand (mxq_ms).
 """
@@ -54,7 +54,7 @@ def main():
     variants = args.variants.split(",")
 
     def select(v):
-        if v == "mx":
+        if v in ("mx", "bl"):
             return
         num, _, g = v.partition("g")
         ext().fp8_gemm_select(int(num), int(g) if g else 0)
@@ -88,11 +88,16 @@ def main():
                         print(json.dumps({"scaled_mm_error": repr(exc)[:300]}), flush=True)
                 for v in variants:
                     select(v)
-                    if v == "mx":
+                    if v == "bl":  # hipBLASLt fp8 through our runner (what Fp8Linear uses by default)
+                        dst = torch.empty(m, n, device="cuda", dtype=torch.bfloat16)
+                        times[v].append(timeit(lambda: ext().blaslt_fp8_gemm(a8, b8, one, one, 1.0, dst, False), args.iters))
+                    elif v == "mx":
                         times[v].append(timeit(lambda: fp8.mx_gemm(aq, bq, as_, bs), args.iters))
                         mxq.append(timeit(lambda: fp8.mx_quant(a, False, True), args.iters))
-                    else:
+                    else:  # the hand-written kernel variant (not the hipBLASLt default of fp8.gemm)
+                        fp8._FP8_GEMM_BACKEND = "hip"
                         times[v].append(timeit(lambda: fp8.gemm(a8, b8, one, one), args.iters))
+                        fp8._FP8_GEMM_BACKEND = "blaslt"
             ext().fp8_gemm_select(0, 4)
             row = {"gemm": f"{name}.{kind}", "M": m, "N": n, "K": k}
             if bf:
