@@ -434,27 +434,37 @@ class DataLoaderShard(DataLoaderStateMixin, DataLoader):
         skip = self.skip_batches + self._resume_skip
         self._resume_skip = 0
         base = super().__iter__()
+        # Skipped batches (resume / skip_batches) are drawn from the host iterator before the device prefetcher
+        # starts, so none of them is pinned or copied to HBM only to be discarded.
+        skipped = 0
+        for _ in range(skip):
+            try:
+                next(base)
+            except StopIteration:
+                break
+            skipped += 1
         it = self._device_iter(base)
         try:
             try:
                 current = next(it)
             except StopIteration:
+                if skipped:  # the whole epoch was skipped: it still counts as finished
+                    self.iteration += 1
+                    self._batches_yielded = 0
                 self.end()
                 return
-            index = 0
-            self._batches_yielded = 0
+            index = skipped
+            self._batches_yielded = skipped
             while True:
                 try:
                     nxt = next(it)
                 except StopIteration:
                     self.end_of_dataloader = True
-                    if index >= skip:
-                        self._batches_yielded = index + 1
-                        yield current
-                    break
-                if index >= skip:
                     self._batches_yielded = index + 1
                     yield current
+                    break
+                self._batches_yielded = index + 1
+                yield current
                 index += 1
                 current = nxt
             self.iteration += 1

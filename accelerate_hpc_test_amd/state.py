@@ -214,59 +214,55 @@ class PartialState:
 
     @contextmanager
     def split_between_processes(self, inputs: list | tuple | dict | torch.Tensor, apply_padding: bool = False):
-        """Give each process a contiguous slice of `inputs` (reference `state.py:423-512`).
-        With `apply_padding`, the last element is repeated so every process gets the same count."""
+        """Hand process i the i-th contiguous block of `inputs` (reference `state.py:423-512`): n items over p processes
+        give the first n % p processes one extra item. Lists, tuples, tensors (dim 0), dicts of those (split
+        key-wise, every value the same length) and `datasets.Dataset` (index selection) are split; anything else is
+        handed over whole. `apply_padding` makes every block as long as the longest, repeating the block's last item
+        (lists / datasets) or the input's last element along dim 0 (tensors), so a later `gather` is rectangular."""
         if self.num_processes == 1:
             yield inputs
             return
-        length = len(inputs)
         if isinstance(inputs, dict):
-            length = len(inputs[list(inputs.keys())[0]])
-            if not all(len(v) == length for v in inputs.values()):
+            lengths = {len(v) for v in inputs.values()}
+            if len(lengths) > 1:
                 raise ValueError("All values in the dictionary must have the same length")
-        num_samples_per_process, num_extras = divmod(length, self.num_processes)
-        start_index = self.process_index * num_samples_per_process + min(self.process_index, num_extras)
-        end_index = start_index + num_samples_per_process + (1 if self.process_index < num_extras else 0)
+            total = lengths.pop() if lengths else 0
+        else:
+            total = len(inputs)
+        base, extra = divmod(total, self.num_processes)
+        i = self.process_index
+        lo = i * base + min(i, extra)
+        hi = lo + base + (i < extra)
+        longest = base + (extra > 0)
+        yield self._split_block(inputs, lo, hi, longest, apply_padding)
 
-        def _split_values(inputs, start_index, end_index):
-            if isinstance(inputs, (list, tuple, torch.Tensor)):
-                if start_index >= len(inputs):
-                    result = inputs[-1:]
-                else:
-                    result = inputs[start_index:end_index]
-                if apply_padding:
-                    if isinstance(result, torch.Tensor):
-                        from .utils.operations import pad_across_processes, send_to_device
-
-                        tensorized_result = send_to_device(result, self.device)
-                        result = pad_across_processes(tensorized_result, pad_index=inputs[-1])
-                    else:
-                        result += [result[-1]] * (num_samples_per_process + (1 if num_extras > 0 else 0) - len(result))
-                return result
-            elif isinstance(inputs, dict):
-                for key in inputs.keys():
-                    inputs[key] = _split_values(inputs[key], start_index, end_index)
-                return inputs
-            else:
-                try:
-                    from datasets import Dataset
-
-                    if isinstance(inputs, Dataset):
-                        if start_index >= len(inputs):
-                            start_index = len(inputs) - 1
-                        if end_index > len(inputs):
-                            end_index = len(inputs)
-                        result_idcs = list(range(start_index, end_index))
-                        if apply_padding:
-                            result_idcs += [end_index - 1] * (
-                                num_samples_per_process + (1 if num_extras > 0 else 0) - len(result_idcs)
-                            )
-                        return inputs.select(result_idcs)
-                except ImportError:
-                    pass
-                return inputs
-
-        yield _split_values(inputs, start_index, end_index)
+    def _split_block(self, inputs, lo: int, hi: int, longest: int, pad: bool):
+        if isinstance(inputs, dict):
+            for key in inputs:
+                inputs[key] = self._split_block(inputs[key], lo, hi, longest, pad)
+            return inputs
+        if isinstance(inputs, torch.Tensor):
+            block = inputs[lo:hi] if lo < inputs.shape[0] else inputs[-1:]
+            if pad and block.shape[0] < longest:
+                filler = inputs[-1:].expand(longest - block.shape[0], *inputs.shape[1:])
+                block = torch.cat([block, filler.to(block.device)])
+            return block.to(self.device) if pad else block
+        if isinstance(inputs, (list, tuple)):
+            block = inputs[lo:hi] if lo < len(inputs) else inputs[-1:]
+            if pad and len(block) < longest:
+                block = block + type(block)([block[-1]]) * (longest - len(block))
+            return block
+        try:
+            from datasets import Dataset
+        except ImportError:
+            return inputs
+        if isinstance(inputs, Dataset):
+            n = len(inputs)
+            idx = list(range(min(lo, n - 1), min(hi, n)))
+            if pad:
+                idx += [idx[-1]] * (longest - len(idx))
+            return inputs.select(idx)
+        return inputs
 
     @contextmanager
     def main_process_first(self):

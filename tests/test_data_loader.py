@@ -173,3 +173,27 @@ def test_checkpoint_restores_loader_position_only_when_stateful(tmp_path, statef
     assert len([b for b in dl]) == 4  # the restored position applies to one pass only
     AcceleratorState._reset_state(True)
     GradientState._reset_state()
+
+
+def test_skipped_batches_are_not_uploaded(monkeypatch):
+    """Resuming mid-epoch (`skip_batches`) draws the skipped batches on the host only: the device path (prefetcher /
+    send_to_device) sees exactly the batches that are yielded."""
+    from accelerate_hpc_test_amd import data_loader as dl_mod
+
+    seen = []
+    real = dl_mod.DataLoaderShard._device_iter
+
+    def spy(self, base_iter):
+        def counted():
+            for b in base_iter:
+                seen.append(int(b[0]))
+                yield b
+        return real(self, counted())
+
+    monkeypatch.setattr(dl_mod.DataLoaderShard, "_device_iter", spy)
+    loader = dl_mod.DataLoaderShard(list(range(10)), batch_size=2, skip_batches=3)
+    out = [b.tolist() for b in loader]
+    assert out == [[6, 7], [8, 9]] and seen == [6, 8]
+    assert loader.iteration == 1
+    loader.skip_batches = 7  # more than the epoch holds: nothing yielded, the epoch still ends
+    assert list(loader) == [] and loader.iteration == 2

@@ -80,3 +80,56 @@ def test_environment_helpers():
     a, b = torch.ones(3), torch.ones(3)
     a, b = ours.release_memory(a, b)
     assert a is None and b is None
+
+
+def _split_cases():
+    return [
+        (list(range(7)), False), (tuple(range(5)), False),
+        (torch.arange(7), False), (torch.arange(7), True), (torch.arange(12).view(6, 2), True),
+        ({"a": [1, 2, 3, 4], "b": torch.arange(4)}, False),
+    ]
+
+
+def _split_parity_worker():
+    import copy
+
+    import accelerate
+
+    from accelerate_hpc_test_amd.state import PartialState
+
+    ours_state, up_state = PartialState(cpu=True), accelerate.PartialState(cpu=True)
+    for inputs, pad in _split_cases():
+        with ours_state.split_between_processes(copy.deepcopy(inputs), apply_padding=pad) as a:
+            with up_state.split_between_processes(copy.deepcopy(inputs), apply_padding=pad) as b:
+                if isinstance(a, dict):
+                    assert a.keys() == b.keys()
+                    pairs = [(a[k], b[k]) for k in a]
+                else:
+                    pairs = [(a, b)]
+                for x, y in pairs:
+                    if isinstance(x, torch.Tensor):
+                        assert torch.equal(x, y), (inputs, pad, x, y)
+                    else:
+                        assert x == y, (inputs, pad, x, y)
+    # padded lists: the reference (1.13.0.dev0, state.py:476-480) repeats the BLOCK's last item; the upstream 1.14 in
+    # the image repeats the input's last item instead, so these are pinned to the reference's output (measured by
+    # running /root/reference/src on 3 gloo ranks: [0,1,2] / [3,4,4] / [5,6,6], and [0] / [1] / [1] for 2 items)
+    W, r = ours_state.num_processes, ours_state.process_index
+    ref = {2: ([[0, 1, 2, 3], [4, 5, 6, 6]], [[0], [1]]), 3: ([[0, 1, 2], [3, 4, 4], [5, 6, 6]], [[0], [1], [1]])}[W]
+    with ours_state.split_between_processes(list(range(7)), apply_padding=True) as x:
+        assert x == ref[0][r], (x, ref[0][r])
+    with ours_state.split_between_processes(list(range(2)), apply_padding=True) as x:
+        assert x == ref[1][r], (x, ref[1][r])
+    # upstream raises TypeError padding a tuple block (list + tuple); ours pads it like a list
+    with ours_state.split_between_processes(tuple(range(5)), apply_padding=True) as t:
+        assert isinstance(t, tuple) and len(t) == -(-5 // ours_state.num_processes)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_split_between_processes_matches_upstream(world):
+    """Our `split_between_processes` (own implementation, no padding collective) against the upstream accelerate in
+    the image on 2 and 3 gloo ranks, for lists, tuples, 1-D / 2-D tensors (with and without padding) and dicts."""
+    pytest.importorskip("accelerate")
+    from accelerate_hpc_test_amd import debug_launcher
+
+    debug_launcher(_split_parity_worker, num_processes=world)
