@@ -4,6 +4,9 @@
 // no transpose/copy precedes attention. O is [B, S, Hq, D]; LSE is fp32 [B, Hq, S] (natural log of the softmax
 // normaliser of the scaled scores, used by the backward pass and by ring-attention merges). GQA: q head h
 // reads kv head h / (Hq / Hkv). head_dim D = 128.
+// Keys may outnumber queries (Sk >= Sq, both multiples of 128): the causal mask is then aligned bottom-right, query i
+// seeing keys j <= i + (Sk - Sq). That is the query chunk of a context-parallel rank attending to the whole K/V prefix
+// that precedes it in ONE call (parallel/context_parallel.py), instead of one call per chunk pair plus LSE merges.
 //
 // Common structure (v2):
 //   * every K/V (or Q/dO) tile lives in ONE LDS image per operand with a 256-B row and the XOR chunk swizzle
@@ -166,6 +169,7 @@ struct FwdParams {
   float* lse;
   int S, Hq, Hkv;
   float scale_log2;
+  int Sk, off;  // key count and causal offset Sk - S
 };
 
 template <bool CAUSAL>
@@ -194,13 +198,14 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(FwdParams p) {
 #pragma unroll
   for (int d = 0; d < 4; ++d) zero(o[d]);
   float m = -INFINITY, l = 0.f;
-  const int n_kt = CAUSAL ? (qt + 1) * 2 : p.S / 64;
+  const int off = p.off;  // query i sees keys <= i + off (causal)
+  const int n_kt = CAUSAL ? (qt + 1) * 2 + off / 64 : p.Sk / 64;
 
   TileDMA<64, 4> dk, dv_;
   const int kts = (int)(p.k_ts * 2), vts = (int)(p.v_ts * 2);
   dk.init(wave, lane, kts);
   dv_.init(wave, lane, vts);
-  const auto krs = head_rsrc(kb_, p.S, p.k_ts), vrs = head_rsrc(vb_, p.S, p.v_ts);
+  const auto krs = head_rsrc(kb_, p.Sk, p.k_ts), vrs = head_rsrc(vb_, p.Sk, p.v_ts);
   dk.issue(krs, 0, kts, k0s);
   dv_.issue(vrs, 0, vts, v0s);
   wait_dma_and_sync();
@@ -211,7 +216,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(FwdParams p) {
       dk.issue(krs, k0 + 64, kts, nk);
       dv_.issue(vrs, k0 + 64, vts, nv);
     }
-    if (!CAUSAL || k0 <= qw0 + 31) {
+    if (!CAUSAL || k0 <= qw0 + 31 + off) {
       f32x16 sc[2];
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
@@ -221,12 +226,12 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(FwdParams p) {
       }
       // Only tiles that reach past the wave's first query need the mask (wave-uniform branch): the others skip
       // the per-element compare/select.
-      if (CAUSAL && k0 + 63 > qw0) {
+      if (CAUSAL && k0 + 63 > qw0 + off) {
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
           for (int i = 0; i < 16; ++i)
-            if (k0 + kb * 32 + acc_row(i, hf) > qw0 + r) sc[kb][i] = -INFINITY;
+            if (k0 + kb * 32 + acc_row(i, hf) > qw0 + r + off) sc[kb][i] = -INFINITY;
       }
       // Max over the RAW scores (the positive scale commutes with max), then one fma per element feeds exp2:
       // p = exp2(s * scale_log2 - m).
@@ -323,6 +328,7 @@ struct BwdParams {
   const bf16_t* o;
   long o_ts, o_bs;
   float* delta_out;
+  int Sk, off;  // key count and causal offset Sk - S (see the header)
 };
 
 template <bool CAUSAL>
@@ -367,13 +373,14 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(BwdParams p) {
   f32x16 dq[4];
 #pragma unroll
   for (int d = 0; d < 4; ++d) zero(dq[d]);
-  const int n_kt = CAUSAL ? (qt + 1) * 2 : p.S / 64;
+  const int off = p.off;
+  const int n_kt = CAUSAL ? (qt + 1) * 2 + off / 64 : p.Sk / 64;
 
   TileDMA<64, 4> dk, dv_;
   const int kts = (int)(p.k_ts * 2), vts = (int)(p.v_ts * 2);
   dk.init(wave, lane, kts);
   dv_.init(wave, lane, vts);
-  const auto krs = head_rsrc(kb_, p.S, p.k_ts), vrs = head_rsrc(vb_, p.S, p.v_ts);
+  const auto krs = head_rsrc(kb_, p.Sk, p.k_ts), vrs = head_rsrc(vb_, p.Sk, p.v_ts);
   dk.issue(krs, 0, kts, k0s);
   dv_.issue(vrs, 0, vts, v0s);
   wait_dma_and_sync();
@@ -387,7 +394,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(BwdParams p) {
     int ln = lane;  // opaque lane id: keeps the per-tile LDS offsets from being hoisted (see the dK / dV kernel)
     asm volatile("" : "+v"(ln));
     const int r = ln & 31, hf = ln >> 5;
-    if (CAUSAL ? k0 <= qw0 + 31 : ln >= 0) {
+    if (CAUSAL ? k0 <= qw0 + 31 + off : ln >= 0) {
       v8bf dsb[2][2];
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
@@ -400,8 +407,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(BwdParams p) {
           dp = mfma(row_frag(v_img, kb * 32 + r, 2 * s + hf), df[s], dp);
         }
         // causal: query qw0 + r sees keys k0 + 32kb + 4hf + acc_row(i, 0) up to itself (diagonal tiles only)
-        const int lim = qw0 + r - (k0 + kb * 32 + 4 * hf);
-        const bool diag = CAUSAL && k0 + kb * 32 + 31 > qw0;
+        const int lim = qw0 + r + off - (k0 + kb * 32 + 4 * hf);
+        const bool diag = CAUSAL && k0 + kb * 32 + 31 > qw0 + off;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           float pv = fast_exp2(sc[i] * p.scale_log2 - lse2);
@@ -478,7 +485,9 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_kernel(BwdParams p) {
 #pragma unroll
   for (int d = 0; d < 4; ++d) { zero(dk[d]); zero(dv[d]); }
 
-  const int qs0_ = CAUSAL ? kt * 2 : 0;  // first 64-query slice that can see this key tile
+  const int off = p.off;
+  // first 64-query slice that can see this key tile (query q sees key k when q + off >= k)
+  const int qs0_ = CAUSAL ? max(0, (kt * 128 - off) / kSlice) : 0;
   const int per = p.S / kSlice - qs0_;   // slices per query head
   const int n_it = grp * per;
   // Q / dO slices by LDS-DMA (2 pieces per wave per operand); lse / delta rows by two 256-B DMAs (waves 0 and 1),
@@ -517,7 +526,7 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_kernel(BwdParams p) {
     const float* dlt_s = lse_s + kSlice;
     if (it + 1 < n_it && !(DBG & 2)) issue(it + 1, nq, nd, nl);  // next slice's DMA overlaps this slice's MFMAs
     const int q0 = (qs0_ + it % per) * kSlice;
-    if (CAUSAL ? q0 + qh + 31 >= kw0 : lv >= 0) {  // non-causal: an opaque always-true test keeps the block shape
+    if (CAUSAL ? q0 + qh + 31 + off >= kw0 : lv >= 0) {  // non-causal: an opaque always-true test keeps the block shape
       const int r = lv & 31, hf = lv >> 5;
       f32x16 sc, dp;
 #pragma unroll
@@ -534,8 +543,8 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_kernel(BwdParams p) {
         dp = mfma(row_frag(d_img, qh + r, 2 * s + hf), row_frag(v_img, kr + r, 2 * s + hf), dp);
       }
       // causal: key kw0 + r is masked for query rows q0 + qh + 4hf + acc_row(i, 0) below it (diagonal tiles only)
-      const int lim = kw0 + r - (q0 + qh + 4 * hf);
-      const bool diag = CAUSAL && q0 + qh < kw0 + 31;
+      const int lim = kw0 + r - (q0 + off + qh + 4 * hf);
+      const bool diag = CAUSAL && q0 + qh + off < kw0 + 31;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         float pv = fast_exp2(sc[i] * p.scale_log2);
@@ -632,16 +641,17 @@ std::vector<torch::Tensor> flash_attn_fwd(torch::Tensor q, torch::Tensor k, torc
   check_qkv(q, "q");
   check_qkv(k, "k");
   check_qkv(v, "v");
-  const int B = q.size(0), S = q.size(1), Hq = q.size(2), Hkv = k.size(2);
-  TORCH_CHECK(k.size(1) == S && v.size(1) == S, "flash_attn: q/k/v sequence lengths must match");
-  TORCH_CHECK(S % 128 == 0, "flash_attn: sequence length must be a multiple of 128");
+  const int B = q.size(0), S = q.size(1), Hq = q.size(2), Hkv = k.size(2), Sk = k.size(1);
+  TORCH_CHECK(v.size(1) == Sk && k.size(0) == B && v.size(0) == B && v.size(2) == Hkv, "flash_attn: k / v shapes differ");
+  TORCH_CHECK(S % 128 == 0 && Sk % 128 == 0, "flash_attn: sequence lengths must be multiples of 128");
+  TORCH_CHECK(Sk >= S, "flash_attn: fewer keys than queries is not supported (causal mask is bottom-right aligned)");
   TORCH_CHECK(Hq % Hkv == 0, "flash_attn: Hq must be a multiple of Hkv");
   auto o = torch::empty({B, S, Hq, kD}, q.options());
   auto lse = torch::empty({B, Hq, S}, q.options().dtype(torch::kFloat32));
   FwdParams p{reinterpret_cast<const bf16_t*>(q.data_ptr()), reinterpret_cast<const bf16_t*>(k.data_ptr()),
               reinterpret_cast<const bf16_t*>(v.data_ptr()), q.stride(1), k.stride(1), v.stride(1), q.stride(0),
               k.stride(0), v.stride(0), reinterpret_cast<bf16_t*>(o.data_ptr()), o.stride(1), o.stride(0),
-              lse.data_ptr<float>(), S, Hq, Hkv, (float)(softmax_scale * kLog2e)};
+              lse.data_ptr<float>(), S, Hq, Hkv, (float)(softmax_scale * kLog2e), Sk, Sk - S};
   dim3 grid(Hq, S / 128, B);
   auto stream = at::hip::getCurrentHIPStream();
   if (causal) hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(256), 0, stream, p);
@@ -661,8 +671,10 @@ void flash_attn_bwd(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch:
   check_qkv(dq, "dq");
   check_qkv(dk, "dk");
   check_qkv(dv, "dv");
-  const int B = q.size(0), S = q.size(1), Hq = q.size(2), Hkv = k.size(2);
-  TORCH_CHECK(S % 128 == 0, "flash_attn: sequence length must be a multiple of 128");
+  const int B = q.size(0), S = q.size(1), Hq = q.size(2), Hkv = k.size(2), Sk = k.size(1);
+  TORCH_CHECK(S % 128 == 0 && Sk % 128 == 0 && Sk >= S, "flash_attn: sequence lengths must be multiples of 128, Sk >= S");
+  TORCH_CHECK(v.size(1) == Sk && dk.size(1) == Sk && dv.size(1) == Sk && dq.size(1) == S && dout.size(1) == S &&
+              o.size(1) == S, "flash_attn: q / k / v / gradient sequence lengths");
   auto stream = at::hip::getCurrentHIPStream();
   auto delta = torch::empty({B, Hq, S}, q.options().dtype(torch::kFloat32));
   const bool fused_delta = g_attn_dbg == 0 || !causal;  // the diagnostic variants may skip the dQ kernel
@@ -673,7 +685,6 @@ void flash_attn_bwd(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch:
                        reinterpret_cast<const bf16_t*>(dout.data_ptr()), dout.stride(1), dout.stride(0),
                        delta.data_ptr<float>(), S, Hq, B);
   }
-  TORCH_CHECK(k.size(1) == S && v.size(1) == S, "flash_attn: q/k/v sequence lengths must match");
   TORCH_CHECK(Hq % Hkv == 0 && dk.size(2) == Hkv && dv.size(2) == Hkv && dq.size(2) == Hq, "flash_attn: head counts");
   BwdParams p{reinterpret_cast<const bf16_t*>(q.data_ptr()), reinterpret_cast<const bf16_t*>(k.data_ptr()),
               reinterpret_cast<const bf16_t*>(v.data_ptr()), reinterpret_cast<const bf16_t*>(dout.data_ptr()),
@@ -683,8 +694,8 @@ void flash_attn_bwd(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch:
               dq.stride(0), dk.stride(1), dk.stride(0), dv.stride(1), dv.stride(0), S, Hq, Hkv,
               (float)(softmax_scale * kLog2e), (float)softmax_scale, (float)(1.0 / softmax_scale),
               reinterpret_cast<const bf16_t*>(o.data_ptr()), o.stride(1), o.stride(0),
-              fused_delta ? delta.data_ptr<float>() : nullptr};
-  const dim3 dq_grid(Hq, S / 128, B), kv_grid(Hkv * (S / 128), B);
+              fused_delta ? delta.data_ptr<float>() : nullptr, Sk, Sk - S};
+  const dim3 dq_grid(Hq, S / 128, B), kv_grid(Hkv * (Sk / 128), B);
   if (causal && g_attn_dbg != 0) {  // diagnostic timing variants (tools/bench_attn.py --dbg)
     if (g_attn_dbg & 8) hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, dq_grid, dim3(256), 0, stream, p);
     const int m = g_attn_dbg & 3;

@@ -269,20 +269,22 @@ def flash_attention_qkv(qkv: torch.Tensor, n_q: int, n_kv: int, causal: bool = T
 
 
 def flash_attn_with_lse(q, k, v, causal=True, scale=None):
-    """Forward-only attention returning (O, LSE[B,Hq,S]) — used by ring attention's merge."""
+    """Forward-only attention returning (O, LSE[B,Hq,S]) — context parallelism's building block. k / v may be longer
+    than q (a K/V prefix): the causal mask is then aligned bottom-right."""
     D = q.shape[-1]
     if scale is None:
         scale = 1.0 / math.sqrt(D)
     if use_native(q):
         return ext().flash_attn_fwd(q, k, v, scale, causal)
     B, S, Hq, _ = q.shape
+    Sk = k.shape[1]
     rep = Hq // k.shape[2]
     qf = q.float().transpose(1, 2)
     kf = k.float().transpose(1, 2).repeat_interleave(rep, dim=1)
     vf = v.float().transpose(1, 2).repeat_interleave(rep, dim=1)
     s = torch.matmul(qf, kf.transpose(-1, -2)) * scale
-    if causal:
-        mask = torch.ones(S, k.shape[1], dtype=torch.bool, device=q.device).triu(1)
+    if causal:  # bottom-right aligned when Sk > S (query i sees keys <= i + Sk - S), as the HIP kernel
+        mask = torch.ones(S, Sk, dtype=torch.bool, device=q.device).triu(1 + Sk - S)
         s = s.masked_fill(mask, float("-inf"))
     lse = torch.logsumexp(s, dim=-1)
     o = torch.matmul(torch.softmax(s, dim=-1), vf)

@@ -7,14 +7,15 @@ variant, K/V rotated by all-gather (default) or all-to-all), and `docs/source/co
 MI355X design:
   * Load-balanced ("zig-zag") layout: the sequence is cut into 2·cp chunks and rank r keeps chunks r and
     2·cp-1-r, so every rank does the same causal work (2·cp+1 chunk-blocks).
-  * Every attention block is an L×L call of the HIP flash-attention kernel returning its log-sum-exp; the blocks of
-    one query chunk are merged in fp32 with the LSE rule. All strictly-lower (full) blocks of a query chunk are
-    stacked along the batch axis → one kernel launch per chunk, not one per block.
-  * "allgather": one RCCL all-gather of K,V per layer (xGMI all-gather, 2·4 MB/rank/layer at S=128k, cp=8), dK,dV
-    returned with one reduce-scatter. "alltoall": K,V stream around a P2P ring (`batch_isend_irecv`) overlapped
-    with the block computation in forward.
-  * Backward is block-wise with the *global* O and LSE (so every block's softmax is already normalised) —
-    the standard ring-attention identity; dQ accumulates locally, dK/dV are reduce-scattered to their owners.
+  * "allgather" (default): K,V are all-gathered straight into global sequence order in two halves (`_KVGather`); each
+    query chunk then needs exactly ONE HIP flash-attention call against its whole causal K/V prefix — the kernel
+    takes Sk > Sq with a bottom-right-aligned causal mask — so there are no per-block calls, no repeated queries and
+    no LSE merges. The second half's all-gather is in flight while the rank's first (shorter-prefix) chunk computes.
+  * "alltoall": K,V stream around a P2P ring (`batch_isend_irecv`) overlapped with the block computation in
+    forward, partial outputs merged in place in fp32 with the LSE rule.
+  * Backward re-gathers K,V (no global K/V is kept between forward and backward: saved activations stay O(local)),
+    runs one flash backward per query chunk with the *global* O and LSE, sums dK/dV in one fp32 global-order buffer
+    and reduce-scatters it to the owners in one collective. `cp_transient_bytes` gives the per-layer transient.
   * Models opt in through `attention_impl` on their attention modules (our models); any other model gets
     `torch.nn.functional.scaled_dot_product_attention` patched for the duration of the context, like torch's CP.
 """
@@ -61,36 +62,36 @@ def zigzag_unshard(parts: list, dim: int) -> torch.Tensor:
 
 # ------------------------------------------------------------------------------------------------ block math
 def _block_fwd(q, k, v, causal, scale):
-    """q [B,L,Hq,D], k/v [B,L,Hkv,D] -> (o fp32 [B,L,Hq,D], lse fp32 [B,Hq,L])."""
-    o, lse = flash_attn_with_lse(q, k, v, causal=causal, scale=scale)
-    return o.float(), lse.float()
+    """q [B,Lq,Hq,D], k/v [B,Lk,Hkv,D] (Lk >= Lq; causal mask bottom-right aligned) -> (o, lse fp32 [B,Hq,Lq])."""
+    return flash_attn_with_lse(q, k, v, causal=causal, scale=scale)
 
 
 def _merge(o, lse, o_blk, lse_blk):
-    """Combine two partial attentions over disjoint key sets (fp32)."""
+    """Combine two partial attentions over disjoint key sets (fp32 o, in place on `o`)."""
     if o is None:
-        return o_blk, lse_blk
+        return o_blk.float(), lse_blk.float()
     new = torch.logaddexp(lse, lse_blk)
     w_old = torch.exp(lse - new).transpose(1, 2).unsqueeze(-1)
     w_new = torch.exp(lse_blk - new).transpose(1, 2).unsqueeze(-1)
-    return o * w_old + o_blk * w_new, new
+    return o.mul_(w_old).add_(o_blk.float() * w_new), new
 
 
 def _block_bwd(do, q, k, v, o, lse, causal, scale):
-    """Gradients of one block given the globally-normalised O / LSE. Returns (dq, dk, dv) in q/k/v dtypes."""
+    """Gradients of attention of q against the K/V prefix k/v (Lk >= Lq, bottom-right causal) given the globally
+    normalised O / LSE. Returns (dq, dk, dv) in q/k/v dtypes; dk/dv cover the whole prefix."""
     if use_native(q) and q.dtype == torch.bfloat16:
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
         ext().flash_attn_bwd(do.contiguous(), q, k, v, o.contiguous(), lse.contiguous(), dq, dk, dv, scale, causal)
         return dq, dk, dv
-    B, L, Hq, D = q.shape
-    Hkv = k.shape[2]
+    B, Lq, Hq, D = q.shape
+    Lk, Hkv = k.shape[1], k.shape[2]
     rep = Hq // Hkv
     qf, kf, vf = (t.float().transpose(1, 2) for t in (q, k, v))
     kf, vf = kf.repeat_interleave(rep, 1), vf.repeat_interleave(rep, 1)
     dof, of = do.float().transpose(1, 2), o.float().transpose(1, 2)
     s = torch.matmul(qf, kf.transpose(-1, -2)) * scale
     if causal:
-        s = s.masked_fill(torch.ones(L, L, dtype=torch.bool, device=q.device).triu(1), float("-inf"))
+        s = s.masked_fill(torch.ones(Lq, Lk, dtype=torch.bool, device=q.device).triu(1 + Lk - Lq), float("-inf"))
     p = torch.exp(s - lse.float().unsqueeze(-1))
     dvf = torch.matmul(p.transpose(-1, -2), dof)
     dp = torch.matmul(dof, vf.transpose(-1, -2))
@@ -98,8 +99,8 @@ def _block_bwd(do, q, k, v, o, lse, causal, scale):
     ds = p * (dp - delta) * scale
     dqf = torch.matmul(ds, kf)
     dkf = torch.matmul(ds.transpose(-1, -2), qf)
-    dkf = dkf.view(B, Hkv, rep, L, D).sum(2)
-    dvf = dvf.view(B, Hkv, rep, L, D).sum(2)
+    dkf = dkf.view(B, Hkv, rep, Lk, D).sum(2)
+    dvf = dvf.view(B, Hkv, rep, Lk, D).sum(2)
     return dqf.transpose(1, 2).to(q.dtype), dkf.transpose(1, 2).to(k.dtype), dvf.transpose(1, 2).to(v.dtype)
 
 
@@ -108,97 +109,129 @@ def _chunk_plan(world: int, rank: int):
     return [rank, 2 * world - 1 - rank]
 
 
-def _attend_chunk(qc, c, kv_chunks, scale):
-    """Attention of query chunk with global id `c` against visible key chunks (ids < c full, == c causal)."""
-    o, lse = _block_fwd(qc, kv_chunks[c][0], kv_chunks[c][1], True, scale)
-    if c > 0:
-        B = qc.shape[0]
-        ks = torch.cat([kv_chunks[j][0] for j in range(c)], 0)
-        vs = torch.cat([kv_chunks[j][1] for j in range(c)], 0)
-        qs = qc.repeat(c, 1, 1, 1)
-        of, lf = _block_fwd(qs, ks, vs, False, scale)
-        # merge the c full blocks (stacked on batch) then the diagonal
-        lf = lf.view(c, B, *lf.shape[1:])
-        of = of.view(c, B, *of.shape[1:])
-        lall = torch.logsumexp(lf, dim=0)
-        w = torch.exp(lf - lall.unsqueeze(0)).transpose(2, 3).unsqueeze(-1)  # [c,B,L,Hq,1]
-        o_full = (of * w).sum(0)
-        o, lse = _merge(o, lse, o_full, lall)
-    return o, lse
+# ------------------------------------------------------------------------------------------------ K/V gather
+class _KVGather:
+    """All-gather of every rank's zig-zag K/V into GLOBAL sequence order, in two halves so compute can start early.
+
+    Rank j holds chunks j and 2W-1-j. Gathering every rank's first chunk gives chunks 0..W-1 already in global order
+    (rank order == chunk order); gathering the second chunks gives W..2W-1 in reverse chunk order, flipped by one
+    copy of that half. The first half is waited for before the rank's first query chunk (global id r < W, whose causal
+    prefix lies entirely in it); the second half is issued asynchronously and is in flight during that computation.
+    Result: K and V as [B, 2W*L, Hkv, D] (one buffer, K and V stacked on dim 0)."""
+
+    def __init__(self, k, v, group):
+        W = comm.group_size(group)
+        B, L2, H, D = k.shape
+        self.L, self.W, self.group = L2 // 2, W, group
+        kv = torch.stack([k, v], 0)  # [2, B, 2L, H, D]
+        L = self.L
+        first = kv[:, :, :L].movedim(2, 0).contiguous()  # [L, 2, B, H, D]: the gathered dim outermost
+        second = kv[:, :, L:].movedim(2, 0).contiguous()
+        self.h1 = torch.empty((W * L,) + tuple(first.shape[1:]), dtype=k.dtype, device=k.device)
+        self.h2 = torch.empty_like(self.h1)
+        self.async_ok = W > 1 and dist.get_backend(group) != "gloo"
+        if W == 1:
+            self.h1.copy_(first)
+            self.h2.copy_(second)
+            self.w2 = None
+        elif self.async_ok:
+            dist.all_gather_into_tensor(self.h1, first, group=group)
+            self.w2 = dist.all_gather_into_tensor(self.h2, second, group=group, async_op=True)
+        else:
+            self.h1.copy_(comm.all_gather_dim(first, 0, group))
+            self.h2.copy_(comm.all_gather_dim(second, 0, group))
+            self.w2 = None
+        self.full = None
+
+    def prefix(self, n_chunks):
+        """K, V of global chunks [0, n_chunks) as [B, n*L, H, D] views."""
+        L, W = self.L, self.W
+        if n_chunks <= W and self.full is None:
+            kv = self.h1[: n_chunks * L]
+        else:
+            kv = self._full()[: n_chunks * L]
+        kv = kv.movedim(0, 2)  # [2, B, n*L, H, D]
+        return kv[0], kv[1]
+
+    def _full(self):
+        if self.full is None:
+            if self.w2 is not None:
+                self.w2.wait()
+                self.w2 = None
+            L, W = self.L, self.W
+            # second half arrived as chunks 2W-1, ..., W (rank order): flip the chunk order
+            h2 = self.h2.view(W, L, *self.h2.shape[1:]).flip(0).reshape(self.h2.shape)
+            self.full = torch.cat([self.h1, h2], 0)
+            self.h1 = self.h2 = None
+        return self.full
 
 
-def _gather_kv_chunks(k, v, group):
-    """All-gather local K,V ([B,2L,Hkv,D]) and index them by global chunk id."""
-    W = comm.group_size(group)
-    kv = torch.stack([k, v], 0)  # one collective for both
-    g = comm.all_gather_dim(kv.contiguous(), 2, group)  # [2, B, W*2L, Hkv, D] in rank order
-    gk, gv = g[0], g[1]
-    L = k.shape[1] // 2
-    chunks = [None] * (2 * W)
-    for j in range(W):
-        a = slice(j * 2 * L, j * 2 * L + L)
-        b = slice(j * 2 * L + L, (j + 1) * 2 * L)
-        chunks[j] = (gk[:, a], gv[:, a])
-        chunks[2 * W - 1 - j] = (gk[:, b], gv[:, b])
-    return chunks, gk, gv
+def _rank_order_rows(t, W, L):
+    """[B, 2W*L, ...] in global chunk order -> rank order (rank j: chunks j, 2W-1-j), the reduce-scatter layout."""
+    idx = torch.cat([torch.cat([torch.arange(j * L, (j + 1) * L), torch.arange((2 * W - 1 - j) * L, (2 * W - j) * L)])
+                     for j in range(W)]).to(t.device)
+    return t.index_select(1, idx)
 
 
 class _RingAttnFn(torch.autograd.Function):
+    """Causal attention of this rank's two zig-zag query chunks against the distributed sequence.
+
+    Forward ("allgather"): the K/V all-gather (two halves, second one overlapped with the first chunk's compute), then
+    ONE flash call per query chunk against its whole causal K/V prefix (bottom-right-aligned mask; no per-block calls,
+    no repeated queries, no LSE merge). ("alltoall"): K/V stream around a P2P ring, one block per arriving chunk,
+    merged in place in fp32 with the LSE rule, the next transfer overlapped with the current blocks.
+    Backward (both): the K/V are re-gathered (nothing of the global K/V is kept between forward and backward: O(local)
+    activation memory per layer), one flash backward per query chunk against its prefix, dK/dV summed in one fp32
+    global-order buffer and reduce-scattered to their owners in one collective."""
+
     @staticmethod
     def forward(ctx, q, k, v, group, scale, strategy):
         W, r = comm.group_size(group), comm.group_rank(group)
         L = q.shape[1] // 2
         if strategy == "alltoall" and W > 1:
-            outs, gk, gv = _ring_forward(q, k, v, group, scale)
+            outs = _ring_forward(q, k, v, group, scale)
         else:
-            chunks, gk, gv = _gather_kv_chunks(k, v, group)
-            outs = [_attend_chunk(q[:, i * L : (i + 1) * L], c, chunks, scale) for i, c in enumerate(_chunk_plan(W, r))]
-        o = torch.cat([x[0] for x in outs], 1).to(q.dtype)
-        lse = torch.cat([x[1] for x in outs], 2).contiguous()
-        ctx.save_for_backward(q, gk, gv, o, lse)
-        ctx.group, ctx.scale, ctx.kshape = group, scale, k.shape
+            g = _KVGather(k, v, group)
+            outs = []
+            for i, c in enumerate(_chunk_plan(W, r)):  # chunk r (< W) first: it only needs the first half
+                kp, vp = g.prefix(c + 1)
+                outs.append(_block_fwd(q[:, i * L : (i + 1) * L], kp, vp, True, scale))
+            del g
+        o = torch.cat([x[0].to(q.dtype) for x in outs], 1)
+        lse = torch.cat([x[1].float() for x in outs], 2).contiguous()
+        ctx.save_for_backward(q, k, v, o, lse)
+        ctx.group, ctx.scale = group, scale
         return o
 
     @staticmethod
     def backward(ctx, do):
-        q, gk, gv, o, lse = ctx.saved_tensors
+        q, k, v, o, lse = ctx.saved_tensors
         group, scale = ctx.group, ctx.scale
         W, r = comm.group_size(group), comm.group_rank(group)
         L = q.shape[1] // 2
         do = do.contiguous()
-        # chunk views into the gathered K/V and matching gradient accumulators (fp32)
-        dgk = torch.zeros(gk.shape, dtype=torch.float32, device=gk.device)
-        dgv = torch.zeros(gv.shape, dtype=torch.float32, device=gv.device)
-
-        def chunk_slice(cid):
-            j = cid if cid < W else 2 * W - 1 - cid
-            base = j * 2 * L + (0 if cid < W else L)
-            return slice(base, base + L)
-
+        g = _KVGather(k, v, group)
+        B, Hkv, D = k.shape[0], k.shape[2], k.shape[3]
+        dkv = None  # fp32 [2, B, 2W*L, Hkv, D] in global order, allocated at the longest prefix
         dq = torch.empty_like(q)
-        for i, c in enumerate(_chunk_plan(W, r)):
+        for i, c in sorted(enumerate(_chunk_plan(W, r)), key=lambda x: -x[1]):  # longest prefix first
             qs = slice(i * L, (i + 1) * L)
-            qc, doc, oc = q[:, qs], do[:, qs], o[:, qs]
-            lc = lse[:, :, qs].contiguous()
-            sl = chunk_slice(c)
-            dqc, dkc, dvc = _block_bwd(doc, qc, gk[:, sl], gv[:, sl], oc, lc, True, scale)
-            dq_acc = dqc.float()
-            dgk[:, sl] += dkc.float()
-            dgv[:, sl] += dvc.float()
-            if c > 0:
-                B = q.shape[0]
-                ks = torch.cat([gk[:, chunk_slice(j)] for j in range(c)], 0)
-                vs = torch.cat([gv[:, chunk_slice(j)] for j in range(c)], 0)
-                dqs, dks, dvs = _block_bwd(doc.repeat(c, 1, 1, 1), qc.repeat(c, 1, 1, 1), ks, vs,
-                                           oc.repeat(c, 1, 1, 1), lc.repeat(c, 1, 1), False, scale)
-                dq_acc += dqs.float().view(c, B, *dqs.shape[1:]).sum(0)
-                for j in range(c):
-                    dgk[:, chunk_slice(j)] += dks[j * B : (j + 1) * B].float()
-                    dgv[:, chunk_slice(j)] += dvs[j * B : (j + 1) * B].float()
-            dq[:, qs] = dq_acc.to(q.dtype)
-        dkv = torch.stack([dgk, dgv], 0)
-        dkv = comm.reduce_scatter_dim(dkv, 2, group)  # sum contributions of all ranks, keep own [B,2L] rows
-        return dq, dkv[0].to(q.dtype), dkv[1].to(q.dtype), None, None, None
+            kp, vp = g.prefix(c + 1)
+            dqc, dkc, dvc = _block_bwd(do[:, qs], q[:, qs], kp, vp, o[:, qs], lse[:, :, qs].contiguous(), True, scale)
+            dq[:, qs] = dqc
+            n = (c + 1) * L
+            if dkv is None:
+                dkv = torch.zeros((2, B, 2 * W * L, Hkv, D), dtype=torch.float32, device=q.device)
+            dkv[0, :, :n] += dkc.float()
+            dkv[1, :, :n] += dvc.float()
+            del kp, vp
+        del g
+        if W > 1:
+            dkv = torch.stack([_rank_order_rows(dkv[0], W, L), _rank_order_rows(dkv[1], W, L)], 0)
+            dkv = comm.reduce_scatter_dim(dkv, 2, group)  # sum over ranks, keep own [B, 2L] rows
+        else:
+            dkv = torch.stack([_rank_order_rows(dkv[0], 1, L), _rank_order_rows(dkv[1], 1, L)], 0)
+        return dq, dkv[0].to(k.dtype), dkv[1].to(v.dtype), None, None, None
 
 
 def _global_rank(group, r):
@@ -206,15 +239,14 @@ def _global_rank(group, r):
 
 
 def _ring_forward(q, k, v, group, scale):
-    """Forward with K/V streamed around a P2P ring (overlap the next transfer with the current blocks)."""
+    """Forward with K/V streamed around a P2P ring (overlap the next transfer with the current blocks). Each arriving
+    rank's chunks are attended as blocks (non-causal below the diagonal, causal on it) and merged in place."""
     W, r = comm.group_size(group), comm.group_rank(group)
     L = q.shape[1] // 2
     plan = _chunk_plan(W, r)
     acc = [(None, None), (None, None)]
     cur = torch.stack([k, v], 0).contiguous()
     nxt = torch.empty_like(cur)
-    # every chunk that passes through is kept in rank order (same layout as the all-gather) for the backward
-    gkv = torch.empty((2, k.shape[0], W * 2 * L) + tuple(k.shape[2:]), dtype=k.dtype, device=k.device)
     send_to, recv_from = (r + 1) % W, (r - 1) % W
     for step in range(W):
         reqs = []
@@ -223,7 +255,6 @@ def _ring_forward(q, k, v, group, scale):
                    dist.P2POp(dist.irecv, nxt, _global_rank(group, recv_from), group)]
             reqs = dist.batch_isend_irecv(ops)
         owner = (r - step) % W
-        gkv[:, :, owner * 2 * L : (owner + 1) * 2 * L] = cur
         owned = {owner: (cur[0][:, :L], cur[1][:, :L]), 2 * W - 1 - owner: (cur[0][:, L:], cur[1][:, L:])}
         for i, c in enumerate(plan):
             qc = q[:, i * L : (i + 1) * L]
@@ -235,7 +266,18 @@ def _ring_forward(q, k, v, group, scale):
         for req in reqs:
             req.wait()
         cur, nxt = nxt, cur
-    return acc, gkv[0], gkv[1]
+    return acc
+
+
+def cp_transient_bytes(seq_len: int, cp: int, n_q_heads: int, n_kv_heads: int, head_dim: int = 128, batch: int = 1,
+                       dtype_bytes: int = 2) -> dict:
+    """Peak per-layer transient HBM of this ring attention on one rank (what `_RingAttnFn` allocates beyond its
+    inputs / outputs), for sizing long-context runs: forward = the gathered global K/V (two halves, then the flipped
+    concatenation: 2x), backward = the same plus one bf16 prefix dK/dV and the fp32 global-order dK/dV accumulator."""
+    kv = 2 * batch * seq_len * n_kv_heads * head_dim * dtype_bytes
+    fwd = 2 * kv + batch * n_q_heads * (seq_len // cp) * 4
+    bwd = 2 * kv + kv + 2 * kv + batch * n_q_heads * (seq_len // cp) * 4 * 2
+    return {"forward": fwd, "backward": bwd, "saved_per_layer": 3 * batch * (seq_len // cp) * n_q_heads * head_dim * dtype_bytes}
 
 
 def ring_attention(q, k, v, group, scale: Optional[float] = None, strategy: str = "allgather"):

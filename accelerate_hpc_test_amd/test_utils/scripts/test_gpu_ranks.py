@@ -34,13 +34,16 @@ def _batches(steps, vocab):
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--mode", choices=["fsdp", "fsdp_fp8", "ddp"], required=True)
+    p.add_argument("--mode", choices=["fsdp", "fsdp_fp8", "ddp", "cp_allgather", "cp_alltoall"], required=True)
+    p.add_argument("--seq", type=int, default=16384)
     p.add_argument("--out", required=True)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--preset", default="llama-small")
     p.add_argument("--cpu", action="store_true", help="plumbing check of this script on CPU ranks (not the GPU test)")
     args = p.parse_args()
 
+    if args.mode.startswith("cp_"):
+        return run_context_parallel(args)
     from accelerate_hpc_test_amd import Accelerator, FullyShardedDataParallelPlugin
     from accelerate_hpc_test_amd.models.llama import LLAMA_PRESETS, LlamaForCausalLM
     from accelerate_hpc_test_amd.parallel import small_allreduce
@@ -117,6 +120,76 @@ def main():
         print(json.dumps(dict(facts, losses=losses, norms=norms)), flush=True)
     acc.wait_for_everyone()
     acc.end_training()
+
+
+def run_context_parallel(args):
+    """Ring attention (parallel/context_parallel.py) of a `--seq`-token causal sequence cut into 2W zig-zag chunks over
+    W ranks, forward + backward on the HIP flash kernels; rank 0 reassembles O / dQ / dK / dV and compares them with
+    fp32 full attention. Also records each rank's peak transient HBM of the attention call."""
+    import math
+
+    import torch.distributed as dist
+
+    from accelerate_hpc_test_amd.parallel.context_parallel import ring_attention, zigzag_shard, zigzag_unshard
+
+    W = int(os.environ.get("WORLD_SIZE", "1"))
+    torch.cuda.set_device(0)
+    if W > 1:
+        dist.init_process_group("gloo")
+    r = dist.get_rank() if W > 1 else 0
+    S, Hq, Hkv, D = args.seq, 8, 2, 128
+    g = torch.Generator().manual_seed(11)
+    full = {n: torch.randn(1, S, h, D, generator=g).to(torch.bfloat16).cuda() for n, h in
+            (("q", Hq), ("k", Hkv), ("v", Hkv), ("do", Hq))}
+    local = {n: zigzag_shard(t, 1, W, r).requires_grad_(n != "do") for n, t in full.items()}
+    torch.cuda.synchronize()
+    base = torch.cuda.memory_allocated()
+    torch.cuda.reset_peak_memory_stats()
+    o = ring_attention(local["q"], local["k"], local["v"], None, strategy=args.mode[3:])
+    o.backward(local["do"])
+    torch.cuda.synchronize()
+    transient = torch.cuda.max_memory_allocated() - base
+
+    def gather(t):
+        if W == 1:
+            return t.detach()
+        parts = [torch.empty_like(t) for _ in range(W)]
+        dist.all_gather(parts, t.detach().contiguous())
+        return zigzag_unshard(parts, 1)
+
+    outs = {"o": gather(o), "dq": gather(local["q"].grad), "dk": gather(local["k"].grad), "dv": gather(local["v"].grad)}
+    peaks = [None] * W
+    if W > 1:
+        dist.all_gather_object(peaks, int(transient))
+    else:
+        peaks = [int(transient)]
+    if r == 0:
+        scale = 1 / math.sqrt(D)
+        rep = Hq // Hkv
+        ref = {"o": torch.zeros(1, S, Hq, D, device="cuda"), "dq": torch.zeros(1, S, Hq, D, device="cuda"),
+               "dk": torch.zeros(1, S, Hkv, D, device="cuda"), "dv": torch.zeros(1, S, Hkv, D, device="cuda")}
+        mask = torch.ones(S, S, device="cuda", dtype=torch.bool).triu(1)
+        for h in range(Hq):  # fp32 reference, one head at a time (a 16k x 16k fp32 score matrix per head)
+            qh = full["q"][0, :, h].float().requires_grad_()
+            kh = full["k"][0, :, h // rep].float().requires_grad_()
+            vh = full["v"][0, :, h // rep].float().requires_grad_()
+            sc = (qh @ kh.t() * scale).masked_fill(mask, float("-inf"))
+            oh = torch.softmax(sc, -1) @ vh
+            oh.backward(full["do"][0, :, h].float())
+            ref["o"][0, :, h] = oh.detach()
+            ref["dq"][0, :, h] = qh.grad
+            ref["dk"][0, :, h // rep] += kh.grad
+            ref["dv"][0, :, h // rep] += vh.grad
+            del sc, oh
+        rel = {n: ((outs[n].float() - ref[n]).norm() / ref[n].norm()).item() for n in outs}
+        res = {"world": W, "mode": args.mode, "seq": S, "rel_err": rel, "peak_transient_bytes": peaks}
+        os.makedirs(args.out, exist_ok=True)
+        with open(os.path.join(args.out, f"result_{args.mode}_W{W}.json"), "w") as f:
+            json.dump(res, f)
+        print(json.dumps(res), flush=True)
+    if W > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

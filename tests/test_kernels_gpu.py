@@ -131,6 +131,43 @@ def test_flash_attention_bench_and_long_shapes(causal, B, S, Hq, Hkv):
     torch.cuda.empty_cache()
 
 
+def _prefix_attn_ref(q, k, v, causal, scale):
+    """fp32 attention of q [B,Sq,Hq,D] against k/v [B,Sk,Hkv,D], causal mask aligned bottom-right (Sk >= Sq)."""
+    B, Sq, Hq, D = q.shape
+    Sk, rep = k.shape[1], Hq // k.shape[2]
+    qf = q.float().transpose(1, 2)
+    kf = k.float().transpose(1, 2).repeat_interleave(rep, 1)
+    vf = v.float().transpose(1, 2).repeat_interleave(rep, 1)
+    s = torch.matmul(qf, kf.transpose(-1, -2)) * scale
+    if causal:
+        s = s.masked_fill(torch.ones(Sq, Sk, device=q.device, dtype=torch.bool).triu(1 + Sk - Sq), float("-inf"))
+    return torch.matmul(torch.softmax(s, -1), vf).transpose(1, 2), torch.logsumexp(s, -1)
+
+
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("Sq,Sk", [(1024, 1024), (1024, 2048), (512, 3072), (128, 1024)])
+def test_flash_attention_kv_prefix(causal, Sq, Sk):
+    """More keys than queries (the context-parallel call: a query chunk against its whole causal K/V prefix): forward
+    O / LSE and the dQ / dK / dV backward against fp32, bottom-right-aligned causal mask."""
+    torch.manual_seed(0)
+    B, Hq, Hkv, D = 1, 8, 2, 128
+    q = torch.randn(B, Sq, Hq, D, device=DEV, dtype=torch.bfloat16)
+    k = torch.randn(B, Sk, Hkv, D, device=DEV, dtype=torch.bfloat16)
+    v = torch.randn(B, Sk, Hkv, D, device=DEV, dtype=torch.bfloat16)
+    scale = 1 / math.sqrt(D)
+    o, lse = _ext.ext().flash_attn_fwd(q, k, v, scale, causal)
+    q2, k2, v2 = (t.detach().float().requires_grad_() for t in (q, k, v))
+    o2, lse2 = _prefix_attn_ref(q2, k2, v2, causal, scale)
+    assert _rel(o, o2) < 2e-2, _rel(o, o2)
+    assert torch.allclose(lse, lse2, atol=2e-2, rtol=1e-3)
+    do = torch.randn_like(o)
+    o2.backward(do.float())
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    _ext.ext().flash_attn_bwd(do, q, k, v, o, lse, dq, dk, dv, scale, causal)
+    for name, a, b in (("dq", dq, q2.grad), ("dk", dk, k2.grad), ("dv", dv, v2.grad)):
+        assert _rel(a, b) < 3e-2, (name, _rel(a, b))
+
+
 def test_flash_attention_lse():
     torch.manual_seed(0)
     B, S, H, D = 1, 256, 2, 128
