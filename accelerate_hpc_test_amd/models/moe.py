@@ -16,7 +16,9 @@ expert GEMMs. Design:
   * gradients for the whole expert group come from one custom autograd op (`_GroupedExpertsFn`) — indexing
     `w[e]` under autograd would materialise an [E, …]-sized zero gradient per expert;
   * expert parallelism (`ep_group` of size W): rank r owns experts [r·E/W, (r+1)·E/W). Tokens go to their expert's
-    owner with one variable-size all-to-all (xGMI: direct, all 7 links), come back with the inverse all-to-all.
+    owner with one variable-size all-to-all (xGMI: direct, all 7 links), come back with the inverse all-to-all. The
+    only other exchange is one [E] per-expert count all-to-all (its host copy = the split sizes, the single host
+    sync per MoE layer); receivers derive each row's local expert from those counts, so no ids travel.
     Expert params are then excluded from FSDP (they are already sharded) and their grads are scaled 1/W (each rank's
     loss is its local mean, exactly like the data-parallel average applied to the dense params).
 """
@@ -304,6 +306,9 @@ class MoELayer(nn.Module):
         self.experts = MoEExperts(num_experts, hidden, intermediate)
         self.ep_group = None
         self.last_router_logits = None
+        # optional per-expert selection bias (DeepSeek-V3-style aux-loss-free balancing): shifts which experts are
+        # chosen, not the combine weights; None = plain top-k of the router softmax (Mixtral)
+        self.router_bias: Optional[torch.Tensor] = None
 
     # --------------------------------------------------------------------------------------------- EP setup
     def shard_experts(self, group, device=None) -> bool:
@@ -338,7 +343,11 @@ class MoELayer(nn.Module):
         logits = self.gate(t)
         self.last_router_logits = logits
         probs = torch.softmax(logits.float(), dim=-1)
-        w, idx = torch.topk(probs, self.top_k, dim=-1)
+        if self.router_bias is None:
+            w, idx = torch.topk(probs, self.top_k, dim=-1)
+        else:
+            idx = torch.topk(probs + self.router_bias.to(probs), self.top_k, dim=-1)[1]
+            w = probs.gather(-1, idx)
         if self.norm_topk:
             w = w / w.sum(-1, keepdim=True)
         w = w.to(t.dtype)
@@ -358,22 +367,21 @@ class MoELayer(nn.Module):
         return out.view(shape)
 
     def _ep_experts(self, x_sorted, e_sorted):
+        """Expert-parallel dispatch / combine. `x_sorted` rows are sorted by global expert id, so the rows bound for
+        rank d are contiguous and already grouped by d's local experts. One [E]-sized count all-to-all (how many rows
+        of each of MY local experts every source rank sends) is the only exchange besides the payload, and its host
+        copy (the split sizes `all_to_all_single` needs) is the only host sync: each receiver rebuilds the local expert
+        id of every received row from those counts, so no ids travel with the tokens."""
         group = self.ep_group
         W = comm.group_size(group)
         El = self.num_experts // W
-        dest = e_sorted // El
-        send_counts = torch.bincount(dest, minlength=W)
-        recv_counts = torch.empty_like(send_counts)
-        if dist.get_backend(group) == "gloo":
-            gathered = [torch.empty_like(send_counts) for _ in range(W)]
-            dist.all_gather(gathered, send_counts, group=group)
-            me = comm.group_rank(group)
-            recv_counts = torch.stack([g[me] for g in gathered])
-        else:
-            dist.all_to_all_single(recv_counts, send_counts, group=group)
-        sc, rc = send_counts.tolist(), recv_counts.tolist()
+        send_e = torch.bincount(e_sorted, minlength=self.num_experts).to(torch.int64)  # [W * El], rank-major
+        recv_e = self._exchange_counts(send_e, W, group)  # recv_e[s * El + j]: rows of my expert j from rank s
+        sc_rc = torch.cat([send_e.view(W, El).sum(1), recv_e.view(W, El).sum(1)]).tolist()
+        sc, rc = sc_rc[:W], sc_rc[W:]
         x_recv = comm.all_to_all_var(x_sorted, sc, rc, group)
-        e_recv = comm.all_to_all_varlen((e_sorted % El).unsqueeze(-1).to(torch.float32), sc, rc, group).squeeze(-1).long()
+        local_ids = torch.arange(El, device=x_sorted.device).repeat(W)
+        e_recv = torch.repeat_interleave(local_ids, recv_e, output_size=sum(rc))
         # local experts: the same device-side layout + grouped GEMMs as the single-rank path
         order2, dest2, seg2, R2 = expert_layout(e_recv, El)
         x_routed = x_recv.new_zeros(R2, x_recv.shape[1]).index_copy(0, dest2, x_recv.index_select(0, order2))
@@ -382,6 +390,19 @@ class MoELayer(nn.Module):
         inv[order2] = torch.arange(order2.numel(), device=order2.device)
         y_recv = y_local_sorted.index_select(0, inv)
         return comm.all_to_all_var(y_recv, rc, sc, group)
+
+    @staticmethod
+    def _exchange_counts(send_e, W, group):
+        """All-to-all of equal El-sized slices of the per-expert count vector (gloo: via all_gather)."""
+        El = send_e.numel() // W
+        if dist.get_backend(group) == "gloo":
+            gathered = [torch.empty_like(send_e) for _ in range(W)]
+            dist.all_gather(gathered, send_e, group=group)
+            me = comm.group_rank(group)
+            return torch.cat([g[me * El : (me + 1) * El] for g in gathered])
+        recv_e = torch.empty_like(send_e)
+        dist.all_to_all_single(recv_e, send_e, group=group)
+        return recv_e
 
 
 def load_balancing_loss(router_logits: list, num_experts: int, top_k: int) -> torch.Tensor:

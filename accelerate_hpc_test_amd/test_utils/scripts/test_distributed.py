@@ -511,9 +511,10 @@ def check_pipeline_inference(gather_output: bool = True, split="auto"):
     dist.barrier()
 
 
-def check_expert_parallel_mixtral(steps: int = 2):
+def check_expert_parallel_mixtral(steps: int = 2, skew: float = 0.0):
     """Mixtral with experts sharded over the FSDP group (ep = world) == one process on the global batch, incl. the
-    clipped grad norm and a sharded checkpoint round trip."""
+    clipped grad norm and a sharded checkpoint round trip. `skew` > 0 biases every router towards expert 0 and away
+    from the last expert (uneven loads: one rank receives most rows, an expert may receive none)."""
     from accelerate_hpc_test_amd import ParallelismConfig
     from accelerate_hpc_test_amd.models.mixtral import MixtralConfig, MixtralForCausalLM
 
@@ -528,7 +529,14 @@ def check_expert_parallel_mixtral(steps: int = 2):
     set_seed(0)
     base = MixtralForCausalLM(cfg)
     base.init_weights()
+    if skew:  # selection bias: expert 0 favoured, the last expert almost never chosen
+        E = cfg.num_local_experts
+        for layer in base.layers:
+            layer.block_sparse_moe.router_bias = torch.linspace(skew, -skew, E) * (torch.arange(E) % 2 == 0) + \
+                torch.tensor([skew] + [0.0] * (E - 2) + [-skew])
     model = copy.deepcopy(base)
+    captured = {}
+    base.layers[0].block_sparse_moe.gate.register_forward_hook(lambda m, i, o: captured.__setitem__("logits", o.detach()))
     opt = torch.optim.SGD(model.parameters(), lr=0.2, momentum=0.9)
     base_opt = torch.optim.SGD(base.parameters(), lr=0.2, momentum=0.9)
     model, opt = acc.prepare(model, opt)
@@ -543,6 +551,11 @@ def check_expert_parallel_mixtral(steps: int = 2):
         opt.step()
         opt.zero_grad()
         ref = base(ids, labels=ids)
+        if skew:  # the routing really is uneven: per-expert loads of the global batch differ a lot
+            sel = torch.softmax(captured["logits"].float(), -1) + base.layers[0].block_sparse_moe.router_bias
+            loads = torch.bincount(torch.topk(sel, 2, -1)[1].reshape(-1), minlength=cfg.num_local_experts)
+            assert loads.max() >= 4 * max(int(loads.min()), 1), loads
+            captured["loads"] = loads
         ref.loss.backward()
         n2 = torch.nn.utils.clip_grad_norm_(base.parameters(), 0.5)
         base_opt.step()
