@@ -26,6 +26,8 @@ from __future__ import annotations
 from contextlib import contextmanager
 from typing import Optional
 
+import weakref
+
 import torch
 import torch.distributed as dist
 import torch.nn as nn
@@ -47,6 +49,20 @@ class _Bucket:
         self.buffer = torch.zeros(n, dtype=dtype, device=device)
         self.pending = len(params)
         self.launched = False
+
+
+def _weak_method_hook(obj, name: str):
+    """A parameter hook calling `obj.<name>` through a weak reference: hooks live in the tensor's C++ autograd
+    metadata, which the cycle collector cannot traverse, so a bound method there would keep the reducer (and its
+    bucket buffers) alive after the user drops the model."""
+    ref = weakref.ref(obj)
+
+    def hook(p):
+        o = ref()
+        if o is not None:
+            getattr(o, name)(p)
+
+    return hook
 
 
 class DistributedDataParallel(nn.Module):
@@ -172,7 +188,7 @@ class DistributedDataParallel(nn.Module):
         for bi, b in enumerate(self.buckets):
             for p in b.params:
                 self._param_bucket[p] = bi
-                p.register_post_accumulate_grad_hook(self._grad_hook)
+                p.register_post_accumulate_grad_hook(_weak_method_hook(self, "_grad_hook"))
         self._assign_grad_views(zero=True)
 
     def _assign_grad_views(self, zero: bool):

@@ -37,6 +37,7 @@ from __future__ import annotations
 import json
 import math
 import os
+import weakref
 from collections import OrderedDict
 from contextlib import contextmanager
 from typing import Callable, Iterable, Optional
@@ -821,16 +822,27 @@ class FSDPEngine:
         self._fused_slot_done(slot)
 
     def _make_grad_hook(self, unit: FlatUnit):
+        # The hook lives in the parameter's C++ autograd metadata, which the Python cycle collector cannot traverse:
+        # a strong reference to the engine here would keep every shard, optimizer-visible master and buffer of the
+        # model alive after the user drops it (measured: 33 GiB of an 8-layer Llama-3-8B-width model). It therefore
+        # holds the engine weakly and finds the unit by index.
+        eng_ref, idx = weakref.ref(self), unit.idx
+
         def hook(param):
-            if param.grad is None and getattr(param, "_acc_wgrad_slot", None) is not None:
-                return  # fused weight: its Linear backward already wrote the slot and counted it
-            if unit.full_grad is None or param.grad is None or param.grad.data_ptr() != self._grad_slot_ptr(unit, param):
-                self._absorb_foreign_grad(unit, param)
-            unit.pending_grads -= 1
-            if unit.pending_grads == 0 and self.requires_grad_sync:
-                self._reduce_unit(unit)
+            eng = eng_ref()
+            if eng is not None:
+                eng._on_grad_ready(eng.units[idx], param)
 
         return hook
+
+    def _on_grad_ready(self, unit: FlatUnit, param):
+        if param.grad is None and getattr(param, "_acc_wgrad_slot", None) is not None:
+            return  # fused weight: its Linear backward already wrote the slot and counted it
+        if unit.full_grad is None or param.grad is None or param.grad.data_ptr() != self._grad_slot_ptr(unit, param):
+            self._absorb_foreign_grad(unit, param)
+        unit.pending_grads -= 1
+        if unit.pending_grads == 0 and self.requires_grad_sync:
+            self._reduce_unit(unit)
 
     def _grad_slot_ptr(self, unit, param):
         for info in unit.infos:
