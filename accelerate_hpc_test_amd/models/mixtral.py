@@ -57,6 +57,10 @@ class MixtralConfig(LlamaConfig):
 MIXTRAL_PRESETS = {
     "mixtral-8x7b": MixtralConfig(),
     "mixtral-8x7b-4l": MixtralConfig(num_hidden_layers=4),  # 1-GPU measurement slice of the full model
+    # the deepest slice whose FSDP training state (18 B/param: fp32 master + grad + Adam m, v + bf16 copy, 11.9 B params)
+    # plus seq-8192 activations fits one MI355X's 288 GB; the full 46.7 B-param model needs 783 GiB of state on one GPU
+    # (98 GiB per GPU at FSDP world size 8), and host offload of it exceeds a 270 GiB host budget as well
+    "mixtral-8x7b-8l": MixtralConfig(num_hidden_layers=8),
     "mixtral-tiny": MixtralConfig(vocab_size=512, hidden_size=256, intermediate_size=512, num_hidden_layers=2,
                                   num_attention_heads=2, num_key_value_heads=1, max_position_embeddings=1024,
                                   num_local_experts=4),
