@@ -23,6 +23,7 @@ with kwargs from `DistributedDataParallelKwargs` (`utils/dataclasses.py:154-237`
 
 from __future__ import annotations
 
+import os
 from contextlib import contextmanager
 from typing import Optional
 
@@ -63,6 +64,60 @@ def _weak_method_hook(obj, name: str):
             getattr(o, name)(p)
 
     return hook
+
+
+class _DDPWgradSlot:
+    """Per-weight state of a fused weight-gradient Linear under the reducer: `uses` counts forward applications whose
+    backward is pending (a weight applied twice reports grad-ready once)."""
+
+    __slots__ = ("ddp", "param", "uses")
+
+    def __init__(self, ddp, param):
+        self.ddp, self.param, self.uses = weakref.ref(ddp), param, 0
+
+
+class _DDPFusedLinearFn(torch.autograd.Function):
+    """y = x Wᵀ (+ b) in the autocast dtype, with dW = dyᵀ x written by the GEMM itself, in fp32, straight into the
+    weight's slot of its reducer bucket (accumulated when the slot already holds this step's gradient). Replaces the
+    autocast path's bf16 dW, its cast to fp32 and the hook's copy into the bucket (16 B/param of HBM traffic) with
+    the GEMM's one fp32 write (4 B/param)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, slot, cdtype):
+        xc = x.to(cdtype) if cdtype is not None else x
+        wc = weight.to(cdtype) if cdtype is not None else weight
+        bc = bias.to(cdtype) if (bias is not None and cdtype is not None) else bias
+        ctx.save_for_backward(xc, wc)
+        ctx.slot, ctx.xdtype = slot, x.dtype
+        ctx.bdtype = bias.dtype if bias is not None else None
+        return nn.functional.linear(xc, wc, bc)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, wc = ctx.saved_tensors
+        N, K = wc.shape
+        dy = dy.to(wc.dtype)
+        dx = (dy @ wc).to(ctx.xdtype) if ctx.needs_input_grad[0] else None
+        dy2 = dy.reshape(-1, N)
+        ddp = ctx.slot.ddp()
+        if ddp is not None:
+            ddp._fused_wgrad(ctx.slot, dy2, xc.reshape(-1, K))
+        db = dy2.float().sum(0).to(ctx.bdtype) if ctx.bdtype is not None else None
+        return dx, None, db, None, None
+
+
+class _DDPFusedLinear(nn.Linear):
+    """`nn.Linear` whose weight gradient goes to its DDP bucket slot through `_DDPFusedLinearFn`."""
+
+    def forward(self, x):
+        slot = getattr(self, "_acc_ddp_slot", None)
+        if slot is None or slot.ddp() is None or not torch.is_grad_enabled() or not self.weight.requires_grad:
+            return nn.functional.linear(x, self.weight, self.bias)
+        if torch._C._current_graph_task_id() == -1:  # not an activation-checkpoint recompute inside backward
+            slot.uses += 1
+        dev = x.device.type
+        cdtype = torch.get_autocast_dtype(dev) if torch.is_autocast_enabled(dev) else None
+        return _DDPFusedLinearFn.apply(x, self.weight, self.bias, slot, cdtype)
 
 
 class DistributedDataParallel(nn.Module):
@@ -122,6 +177,9 @@ class DistributedDataParallel(nn.Module):
         self._unset: set = set()  # ids of params whose grad is None at forward (filled by the hook's copy)
         self._sync_params_and_buffers()
         self._build_buckets()
+        self._fused_slots = []
+        if os.environ.get("ACCELERATE_DDP_FUSED_WGRAD", "1") != "0":
+            self._install_fused_wgrad()
 
     # ------------------------------------------------------------------------------------------ setup
     @torch.no_grad()
@@ -130,11 +188,11 @@ class DistributedDataParallel(nn.Module):
         tensors = [p.data for p in self.module.parameters()] + [b for b in self.module.buffers()]
         self._coalesced_broadcast(tensors)
 
-    def _coalesced_broadcast(self, tensors, chunk_bytes: int = 256 << 20):
+    def _coalesced_broadcast(self, tensors, chunk_bytes: int = 256 << 20, src: int = 0):
         """Broadcast from rank 0 in packed pieces of at most `chunk_bytes` per dtype (a tensor larger than that goes
         alone, in place). Packing keeps the call count low for many small tensors; the cap keeps the transient pack
         buffer small (a whole-model pack of Llama-3-8B fp32 would be a 32 GB spike on every rank)."""
-        src = dist.get_global_rank(self.process_group, 0) if self.process_group else 0
+        src = dist.get_global_rank(self.process_group, src) if self.process_group else src
         by_dtype = {}
         for t in tensors:
             by_dtype.setdefault(t.dtype, []).append(t)
@@ -198,6 +256,46 @@ class DistributedDataParallel(nn.Module):
             for p, off in zip(b.params, b.offsets):
                 p.grad = b.buffer[off : off + p.numel()].view_as(p)
 
+    def _install_fused_wgrad(self):
+        """Route the weight gradient of every plain `nn.Linear` (weight in a bucket, used by no other module) through
+        `_DDPFusedLinear`: its backward GEMM writes fp32 straight into the bucket slot."""
+        refs = {}
+        for m in self.module.modules():
+            for q in m._parameters.values():
+                if q is not None:
+                    refs[id(q)] = refs.get(id(q), 0) + 1
+        for m in self.module.modules():
+            w = getattr(m, "weight", None)
+            if type(m) is nn.Linear and w is not None and w.requires_grad and refs.get(id(w), 0) == 1 \
+                    and w in self._param_bucket and w.dtype == self.buckets[self._param_bucket[w]].buffer.dtype:
+                m.__class__ = _DDPFusedLinear
+                m._acc_ddp_slot = _DDPWgradSlot(self, w)
+                w._acc_ddp_fused = True
+                self._fused_slots.append(m._acc_ddp_slot)
+
+    @torch.no_grad()
+    def _fused_wgrad(self, slot: _DDPWgradSlot, dy2: torch.Tensor, x2: torch.Tensor):
+        p = slot.param
+        b = self.buckets[self._param_bucket[p]]
+        view = self._slot(b, p)
+        if p.grad is not None and p.grad.data_ptr() != view.data_ptr():  # a gradient the user set: move it in first
+            view.copy_(p.grad)
+            p.grad = view
+        acc = p.grad is not None  # torch semantics: accumulate unless zero_grad set the grad to None
+        a = dy2.t()
+        if view.dtype == a.dtype:
+            view.addmm_(a, x2) if acc else torch.mm(a, x2, out=view)
+        elif view.is_cuda and view.dtype == torch.float32:
+            torch.addmm(view, a, x2, out_dtype=torch.float32, out=view) if acc else torch.mm(a, x2, out_dtype=torch.float32, out=view)
+        else:
+            g = (a.float() @ x2.float()).to(view.dtype)
+            view.add_(g) if acc else view.copy_(g)
+        p.grad = view
+        slot.uses -= 1
+        if slot.uses <= 0:
+            slot.uses = 0
+            self._grad_ready(p)
+
     # ------------------------------------------------------------------------------------------ forward
     def forward(self, *inputs, **kwargs):
         # After `zero_grad(set_to_none=True)` the grads are None. They stay None: autograd then hands each parameter a
@@ -232,12 +330,18 @@ class DistributedDataParallel(nn.Module):
 
     # ------------------------------------------------------------------------------------------ reduce
     def _grad_hook(self, p):
+        if getattr(p, "_acc_ddp_fused", False):
+            return  # autograd still runs the hook of a weight whose Function returned no grad; the GEMM counted it
         b = self.buckets[self._param_bucket[p]]
         if p.grad is not None and b.buffer.numel() and p.grad.data_ptr() != self._slot_ptr(b, p):
             with torch.no_grad():  # first gradient since zero_grad (or one set by the user): move it into the bucket
                 view = self._slot(b, p)
                 view.copy_(p.grad)
                 p.grad = view
+        self._grad_ready(p)
+
+    def _grad_ready(self, p):
+        b = self.buckets[self._param_bucket[p]]
         self._unset.discard(id(p))
         if not self._cb_queued:
             self._cb_queued = True
@@ -350,6 +454,8 @@ class DistributedDataParallel(nn.Module):
 
     def _finalize(self):
         self._cb_queued = False
+        for slot in self._fused_slots:
+            slot.uses = 0  # forwards whose outputs never reached this backward
         if self._unset:  # parameters without a gradient this backward: zero slots, grads point at them
             with torch.no_grad():
                 for b in self.buckets:
@@ -415,17 +521,7 @@ class DistributedDataParallel(nn.Module):
                          device=self.device if not self.is_gloo else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.process_group)
         src = self.world_size - 1 - int(t.item()) % self.world_size
-        tensors = [p.data for p in self.module.parameters()] + list(self.module.buffers())
-        by_dtype = {}
-        for x in tensors:
-            by_dtype.setdefault(x.dtype, []).append(x)
-        for ts in by_dtype.values():
-            flat = torch.cat([x.reshape(-1) for x in ts])
-            dist.broadcast(flat, src=dist.get_global_rank(self.process_group, src) if self.process_group else src, group=self.process_group)
-            off = 0
-            for x in ts:
-                x.copy_(flat[off : off + x.numel()].view_as(x))
-                off += x.numel()
+        self._coalesced_broadcast([p.data for p in self.module.parameters()] + list(self.module.buffers()), src=src)
 
     def _join_counter(self, active: int, syncing: int) -> tuple[int, int]:
         t = torch.tensor([active, syncing], dtype=torch.int64, device=self.device if not self.is_gloo else "cpu")
