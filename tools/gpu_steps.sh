@@ -40,6 +40,8 @@ for step in "$@"; do
     bench8b_ddp) run bench8b_ddp 600 python bench.py --parallel ddp --steps 5 --warmup 2 $BENCH_ARGS ;;
     bench8b_ddp_forced) run bench8b_ddp_forced 600 python bench.py --parallel ddp --ddp-force --steps 5 --warmup 2 $BENCH_ARGS ;;
     prof_ddp_forced) prof prof_ddp_forced 600 bench.py --parallel ddp --ddp-force --steps 3 --warmup 2 $BENCH_ARGS ;;
+    prof_ddp) prof prof_ddp 600 bench.py --parallel ddp --steps 3 --warmup 2 $BENCH_ARGS ;;
+    prof_mixtral8l_bf16) prof prof_mixtral8l_bf16 600 bench.py --model mixtral-8x7b-8l --steps 2 --warmup 1 ;;
     mixtral_bf16) run mixtral_bf16 600 python bench.py --model mixtral-8x7b-4l --steps 3 --warmup 2 $BENCH_ARGS ;;
     mixtral_fp8) run mixtral_fp8 600 python bench.py --model mixtral-8x7b-4l --steps 3 --warmup 2 --precision fp8 $BENCH_ARGS ;;
     prof8b) prof prof8b 600 bench.py --steps 3 --warmup 2 $BENCH_ARGS ;;
