@@ -280,6 +280,8 @@ class FSDPEngine:
 
             visit(self.model)
         name_of = {id(m): n for n, m in self.model.named_modules()}
+        if wrap is not None:
+            unit_modules += self._large_root_leaves(unit_modules, ignored)
         assigned_units = []
         for m in unit_modules:
             infos = self._collect(m, name_of[id(m)], owned, ignored)
@@ -319,6 +321,36 @@ class FSDPEngine:
                     info.param.register_post_accumulate_grad_hook(self._make_grad_hook(unit))
         if os.environ.get("ACCELERATE_FSDP_FUSED_WGRAD", "1") != "0":
             self._install_fused_wgrad()
+
+    def _large_root_leaves(self, unit_modules, ignored) -> list:
+        """Large leaf modules the wrap policy left in the root (Llama's token embedding and lm_head: 525 M params each,
+        1.05 GB bf16): each becomes a unit of its own. In the root they would be all-gathered before the first block
+        (not overlapped with anything) and reduce-scattered after the last gradient of the step (2.1 GB each way,
+        ~6 ms per direction over 7 xGMI links at 8 GPUs); as units, the lm_head's gather is prefetched under the last
+        blocks' forward and its reduce-scatter overlaps the blocks' backward, leaving only the embedding's exposed.
+        Only modules whose parameters no other module shares (tied embeddings stay in the root).
+        `ACCELERATE_FSDP_SPLIT_ROOT=0` keeps everything in the root (reference FSDP2 wrap behaviour)."""
+        if os.environ.get("ACCELERATE_FSDP_SPLIT_ROOT", "1") == "0":
+            return []
+        min_params = int(os.environ.get("ACCELERATE_FSDP_SPLIT_ROOT_MIN_PARAMS", 16 << 20))
+        inside = set()
+        for m in unit_modules:
+            inside.update(id(x) for x in m.modules())
+        refs = {}
+        for m in self.model.modules():
+            for q in m._parameters.values():
+                if q is not None:
+                    refs[id(q)] = refs.get(id(q), 0) + 1
+        out = []
+        for m in self.model.modules():
+            if m is self.model or id(m) in inside or next(m.children(), None) is not None:
+                continue
+            params = [q for q in m._parameters.values() if q is not None]
+            if not params or any(refs.get(id(q), 0) != 1 or id(q) in ignored for q in params):
+                continue
+            if sum(q.numel() for q in params) >= min_params:
+                out.append(m)
+        return out
 
     # =========================================================================================== fp8 all-gather
     def _fp8_gathered(self, info: _ParamInfo, refs: dict) -> bool:

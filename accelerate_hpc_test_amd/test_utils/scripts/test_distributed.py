@@ -1227,3 +1227,56 @@ def check_fsdp1_strategy(strategy: str, backward_prefetch=None, forward_prefetch
     back = acc.get_state_dict(model)
     for n in full:
         assert torch.allclose(full[n], back[n]), n
+
+
+def check_fsdp_split_root_units(steps: int = 2):
+    """Large root leaves (token embedding, lm_head) become FSDP units of their own (ACCELERATE_FSDP_SPLIT_ROOT; the
+    threshold is lowered so llama-tiny's qualify): the unit layout has them, training equals one process, and the
+    sharded checkpoint round-trips."""
+    os.environ["ACCELERATE_FSDP_SPLIT_ROOT_MIN_PARAMS"] = "1000"
+    from accelerate_hpc_test_amd.models.llama import LLAMA_PRESETS, LlamaForCausalLM
+
+    plugin = FullyShardedDataParallelPlugin(fsdp_version=2, auto_wrap_policy="transformer_based_wrap",
+                                            transformer_cls_names_to_wrap=["LlamaDecoderLayer"],
+                                            state_dict_type="SHARDED_STATE_DICT")
+    acc = Accelerator(cpu=True, fsdp_plugin=plugin)
+    W, r = acc.num_processes, acc.process_index
+    torch.manual_seed(0)
+    base = LlamaForCausalLM(LLAMA_PRESETS["llama-tiny"])
+    base.init_weights()
+    model = copy.deepcopy(base)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-3)
+    base_opt = torch.optim.AdamW(base.parameters(), lr=1e-3)
+    model, opt = acc.prepare(model, opt)
+    eng = model.engine
+    unit_names = [sorted(i.fqn for i in u.infos) for u in eng.units]
+    assert ["embed_tokens.weight"] in unit_names and ["lm_head.weight"] in unit_names, unit_names
+    assert [i.fqn for i in eng.root.infos] == ["norm.weight"], [i.fqn for i in eng.root.infos]
+    g = torch.Generator().manual_seed(3)
+    bs = 2
+    for _ in range(steps):
+        ids = torch.randint(0, 512, (bs * W, 64), generator=g)
+        local = ids[r * bs : (r + 1) * bs]
+        out = model(local, labels=local)
+        acc.backward(out.loss)
+        opt.step()
+        opt.zero_grad()
+        base(ids, labels=ids).loss.backward()
+        base_opt.step()
+        base_opt.zero_grad()
+    full = acc.get_state_dict(model)
+    for n, q in base.state_dict().items():
+        # Adam turns fp32 summation-order noise in a near-zero gradient (rows of tokens seen on one rank) into up to
+        # +-lr per step; everything else agrees to fp32 rounding
+        d = (full[n].float() - q.float()).abs()
+        assert d.max() <= 2 * 1e-3 * steps and d.mean() <= 1e-5, (n, d.max(), d.mean())
+    d = tempfile.mkdtemp() if r == 0 else None
+    d = gather_object([d])[0]
+    acc.save_state(d)
+    with torch.no_grad():
+        for p in model.parameters():
+            p.add_(1.0)
+    acc.load_state(d)
+    back = acc.get_state_dict(model)
+    for n in full:
+        assert torch.equal(full[n], back[n]), n

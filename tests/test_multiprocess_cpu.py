@@ -191,3 +191,8 @@ def test_expert_parallel_uneven_expert_loads(world):
     """EP dispatch with a skewed router (most rows to expert 0, few or none to the last): counts-only id exchange, one
     host sync per layer, equal to one process (round-2 verdict item: uneven loads)."""
     debug_launcher(td.check_expert_parallel_mixtral, args=(2, 2.0), num_processes=world)
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_fsdp_split_root_units(world):
+    debug_launcher(td.check_fsdp_split_root_units, num_processes=world)
