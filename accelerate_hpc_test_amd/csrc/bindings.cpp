@@ -2,6 +2,27 @@
 // Kernels live in csrc/kernels/*.hip (gfx950), the host runtime pieces in csrc/runtime/*.cpp.
 #include <torch/extension.h>
 
+// device-side check words of the debug build (one per kernel file; release builds return 0), see kernels/common.h
+int64_t acc_dbg_take_flash_attn();
+int64_t acc_dbg_take_fp8();
+int64_t acc_dbg_take_grouped_gemm();
+int64_t acc_dbg_take_norm_act();
+int64_t acc_dbg_take_xent_optim();
+int64_t acc_dbg_take_small_allreduce();
+int64_t acc_dbg_take_comm_pack();
+bool debug_selftest(torch::Tensor out, int64_t overshoot);
+
+// (check id << 32 | source line) of the first failed device check since the last call, 0 if none; clears it.
+static int64_t debug_status() {
+  int64_t first = 0;
+  for (auto fn : {acc_dbg_take_flash_attn, acc_dbg_take_fp8, acc_dbg_take_grouped_gemm, acc_dbg_take_norm_act,
+                  acc_dbg_take_xent_optim, acc_dbg_take_small_allreduce, acc_dbg_take_comm_pack}) {
+    const int64_t w = fn();
+    if (first == 0) first = w;
+  }
+  return first;
+}
+
 // norm_act.hip
 std::vector<torch::Tensor> rmsnorm_fwd(torch::Tensor x, c10::optional<torch::Tensor> residual, torch::Tensor w, double eps,
                                        c10::optional<torch::Tensor> amax);
@@ -126,4 +147,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("blaslt_wgrad_plans", &blaslt_wgrad_plans);
   m.def("blaslt_fp8_gemm", &blaslt_fp8_gemm, "per-tensor-scaled fp8 GEMM on hipBLASLt (C = alpha sa sb A B^T)");
   m.def("blaslt_fp8_plans", &blaslt_fp8_plans);
+  m.def("debug_status", &debug_status, "first failed device bounds check (id << 32 | line), 0 if none; clears it");
+  m.def("debug_selftest", &debug_selftest);
+#ifdef ACC_DEBUG_BOUNDS
+  m.attr("debug_build") = true;
+#else
+  m.attr("debug_build") = false;
+#endif
 }

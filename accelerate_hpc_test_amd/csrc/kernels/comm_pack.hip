@@ -56,6 +56,8 @@ int grid_for(int64_t work, int block) {
 
 }  // namespace
 
+ACC_DEBUG_TAKE_FN(acc_dbg_take_comm_pack)
+
 // dst (fp32, contiguous, n) = or += scale * src (bf16 / fp32, contiguous, n). n must be a multiple of 8.
 void grad_shard_update(torch::Tensor dst, torch::Tensor src, double scale, bool accumulate) {
   TORCH_CHECK(dst.is_cuda() && src.is_cuda() && dst.is_contiguous() && src.is_contiguous(), "grad_shard_update: contiguous GPU tensors");

@@ -83,4 +83,51 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
 }
 
+// ---- device-side checks of the debug build ------------------------------------------------------
+// Compiled in only for the `_C_debug` extension (-DACC_DEBUG_BOUNDS; `ACCELERATE_DEBUG_KERNELS=1` loads it instead of
+// `_C`). A failed check records (check id, source line) in this translation unit's device error word and the guarded
+// access is skipped: ACC_CHECK_OR_RETURN leaves the kernel (only for block-uniform conditions, before any barrier),
+// ACC_CHECK just records (the caller then takes its safe path). Nothing traps: a trapping wave faults the GPU.
+// Each kernel file defines `ACC_DEBUG_TAKE_FN(name)`, a host function returning (id << 32 | line) of the first failed
+// check since the last call (0 = none) and clearing it; `_C.debug_status()` polls every file.
+enum AccCheck : int {
+  kChkAttnTile = 1, kChkGemmTile = 2, kChkGroupSeg = 3, kChkNormRow = 4, kChkXentLabel = 5, kChkMtChunk = 6,
+  kChkAllreduceSize = 7, kChkRopePos = 8, kChkSelfTest = 99,
+};
+#ifdef ACC_DEBUG_BOUNDS
+static __device__ int acc_dbg_word[2];
+__device__ __forceinline__ void acc_dbg_fail(int code, int line) {
+  if (atomicCAS(&acc_dbg_word[0], 0, code) == 0) atomicExch(&acc_dbg_word[1], line);
+}
+#define ACC_CHECK(cond, code) \
+  do {                         \
+    if (!(cond)) ::acc::acc_dbg_fail((code), __LINE__); \
+  } while (0)
+#define ACC_CHECK_OR_RETURN(cond, code) \
+  do {                                   \
+    if (!(cond)) {                       \
+      ::acc::acc_dbg_fail((code), __LINE__); \
+      return;                            \
+    }                                    \
+  } while (0)
+#define ACC_DEBUG_TAKE_FN(name)                                                                  \
+  int64_t name() {                                                                               \
+    int w[2] = {0, 0};                                                                           \
+    (void)hipDeviceSynchronize();                                                                \
+    (void)hipMemcpyFromSymbol(w, HIP_SYMBOL(::acc::acc_dbg_word), sizeof(w), 0, hipMemcpyDeviceToHost); \
+    if (w[0] != 0) {                                                                             \
+      const int z[2] = {0, 0};                                                                   \
+      (void)hipMemcpyToSymbol(HIP_SYMBOL(::acc::acc_dbg_word), z, sizeof(z), 0, hipMemcpyHostToDevice); \
+    }                                                                                            \
+    return ((int64_t)w[0] << 32) | (uint32_t)w[1];                                               \
+  }
+#define ACC_DEBUG_BUILD 1
+#else
+#define ACC_CHECK(cond, code) ((void)0)
+#define ACC_CHECK_OR_RETURN(cond, code) ((void)0)
+#define ACC_DEBUG_TAKE_FN(name) \
+  int64_t name() { return 0; }
+#define ACC_DEBUG_BUILD 0
+#endif
+
 }  // namespace acc

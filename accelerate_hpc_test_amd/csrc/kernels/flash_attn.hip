@@ -186,6 +186,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(FwdParams p) {
   // paired layout — q-tiles y and nqt-1-y in one workgroup, equal work everywhere — measured 3% slower)
   const int qt = CAUSAL ? (nqt - 1 - (int)blockIdx.y) : (int)blockIdx.y;
   const int qw0 = qt * 128 + wave * 32;
+  // debug build: the query tile, heads and the causal key range it will stream lie inside the tensors (block-uniform)
+  ACC_CHECK_OR_RETURN(qt * 128 + 128 <= p.S && h < p.Hq && kh < p.Hkv && p.Sk % 64 == 0 &&
+                          (!CAUSAL || (qt + 1) * 128 + p.off <= p.Sk), kChkAttnTile);
   const bf16_t* qb = p.q + b * p.q_bs + (long)h * kD;
   const bf16_t* kb_ = p.k + b * p.k_bs + (long)kh * kD;
   const bf16_t* vb_ = p.v + b * p.v_bs + (long)kh * kD;
@@ -341,6 +344,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(BwdParams p) {
   const int kh = h / (p.Hq / p.Hkv);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hf = lane >> 5;
   const int qw0 = qt * 128 + wave * 32;
+  ACC_CHECK_OR_RETURN(qt * 128 + 128 <= p.S && h < p.Hq && kh < p.Hkv && (!CAUSAL || (qt + 1) * 128 + p.off <= p.Sk),
+                      kChkAttnTile);
   const bf16_t* qb = p.q + b * p.q_bs + (long)h * kD;
   const bf16_t* dob = p.dout + b * p.do_bs + (long)h * kD;
   const bf16_t* kb_ = p.k + b * p.k_bs + (long)kh * kD;
@@ -472,6 +477,7 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_kernel(BwdParams p) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hf = lane >> 5;
   const int kr = (wave & 3) * 32, qh = (wave >> 2) * 32;
   const int kw0 = kt * 128 + kr;
+  ACC_CHECK_OR_RETURN(kt * 128 + 128 <= p.Sk && kh < p.Hkv && p.Hq % p.Hkv == 0, kChkAttnTile);
   char* k_img = smem;
   char* v_img = smem + kKV;
   {
@@ -629,6 +635,8 @@ template __global__ void attn_bwd_dkdv_kernel<true, 3>(BwdParams);
 template __global__ void attn_bwd_dkdv_kernel<false, 0>(BwdParams);
 
 }  // namespace
+
+ACC_DEBUG_TAKE_FN(acc_dbg_take_flash_attn)
 
 // Diagnostic switch for the causal backward (tools/bench_attn.py --dbg): bit 3 = run the dQ kernel, bit 2 = run the
 // normal dK/dV kernel, bits 0-1 = run a dK/dV DBG variant instead. 0 = normal operation.

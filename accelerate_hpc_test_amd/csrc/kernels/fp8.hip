@@ -665,6 +665,8 @@ __device__ __forceinline__ void fp8_gemm_v3_body(const uint8_t* __restrict__ A, 
     tile_n = bid % tiles_n;
   }
   const int tm = tile_m * V3_BM, tn = tile_n * V3_BN;
+  // debug build: the tile and its K sweep stay inside A [M, K], B [N, K], C [M, N] (block-uniform)
+  ACC_CHECK_OR_RETURN(tm + V3_BM <= M && tn + V3_BN <= N && K % 64 == 0 && bid < nwg, kChkGemmTile);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hf = lane >> 5;
   const int wm = (wave / WN) * 128, wn = (wave % WN) * (V3_BN / WN);
 
@@ -901,6 +903,8 @@ __global__ __launch_bounds__(512, 1) void fp8_gemm_v3_w8_kernel(const uint8_t* _
 }
 
 }  // namespace
+
+ACC_DEBUG_TAKE_FN(acc_dbg_take_fp8)
 
 torch::Tensor fp8_amax(torch::Tensor x, c10::optional<torch::Tensor> out) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous(), "fp8_amax: x must be contiguous bf16");

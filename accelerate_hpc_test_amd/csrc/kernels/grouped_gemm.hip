@@ -77,6 +77,8 @@ __global__ __launch_bounds__(256, 1) void grouped_gemm_kernel(GGArgs p) {
     e = -1;
     for (int i = 0; i < p.E; ++i) {  // wave-uniform scalar walk over the segment table
       const int lo = p.seg[i], hi = p.seg[i + 1];
+      // debug build: segments are ordered and inside the routed buffer (a bad table would read / write past it)
+      ACC_CHECK_OR_RETURN(lo >= 0 && hi >= lo && hi <= p.R, kChkGroupSeg);
       const int nt = (hi - lo + GG_BM - 1) / GG_BM;
       if (e < 0 && mt < acc + nt) {
         e = i;
@@ -264,6 +266,8 @@ int fmt_of(const torch::Tensor& t) {
 }
 
 }  // namespace
+
+ACC_DEBUG_TAKE_FN(acc_dbg_take_grouped_gemm)
 
 // mode 1 (GROUP_M): a [R, K], b [E, N, K], out [R, N]; seg [E+1] row boundaries.
 // mode 2 (GROUP_K): a [M, Ktot], b [N, Ktot], out [E, M, N]; seg [E+1] K boundaries.

@@ -254,6 +254,8 @@ __global__ void rope_kernel(const bf16_t* __restrict__ src, bf16_t* __restrict__
     bf16x4 oa = a, ob = b;
     if (h < n_rot_heads) {
       const long p = pos != nullptr ? pos[t] : (t % S);
+      ACC_CHECK(p >= 0 && p < S, kChkRopePos);  // debug build: a position past the cos / sin table
+      if (ACC_DEBUG_BUILD && (p < 0 || p >= S)) continue;
       const float4 cs = reinterpret_cast<const float4*>(cosb + p * half)[c];
       const float4 sn = reinterpret_cast<const float4*>(sinb + p * half)[c];
       const float cc[4] = {cs.x, cs.y, cs.z, cs.w};
@@ -315,6 +317,8 @@ struct AmaxOut {
 };
 
 }  // namespace
+
+ACC_DEBUG_TAKE_FN(acc_dbg_take_norm_act)
 
 // ----------------------------------------------------------------------------------------- host API
 std::vector<torch::Tensor> rmsnorm_fwd(torch::Tensor x, c10::optional<torch::Tensor> residual, torch::Tensor w,

@@ -71,6 +71,7 @@ __global__ __launch_bounds__(kThreads) void one_shot_allreduce_kernel(IO io, lon
   const int rank = rank0 + blockIdx.y;
   const T* __restrict__ in = reinterpret_cast<const T*>(io.in[blockIdx.y]);
   T* __restrict__ out = reinterpret_cast<T*>(io.out[blockIdx.y]);
+  ACC_CHECK_OR_RETURN(n * (long)sizeof(T) <= slot_bytes && rank < world, kChkAllreduceSize);  // debug build
   const long per = (n + nb - 1) / nb;
   const long lo = (long)b * per, hi = min(n, lo + per);
   const long data_off = kFlagBytes + (long)(epoch & 1) * slot_bytes;
@@ -172,6 +173,8 @@ Comm* get(int64_t id) {
 void check(hipError_t e, const char* what) { TORCH_CHECK(e == hipSuccess, "small_allreduce: ", what, ": ", hipGetErrorString(e)); }
 
 }  // namespace
+
+ACC_DEBUG_TAKE_FN(acc_dbg_take_small_allreduce)
 
 // Allocate this rank's buffer; returns (communicator id, IPC handle bytes of the buffer).
 std::tuple<int64_t, pybind11::bytes> sar_create(int64_t rank, int64_t world, int64_t max_bytes) {

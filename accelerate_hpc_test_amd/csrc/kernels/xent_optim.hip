@@ -48,7 +48,9 @@ __global__ __launch_bounds__(kXentThreads) void xent_fwd_kernel(const bf16_t* __
     const float lse = gm + __logf(sa);
     lse_out[row] = lse;
     const int64_t lab = labels[row];
-    loss[row] = (lab == ignore_index) ? 0.f : (lse - bf2f(x[lab]));
+    ACC_CHECK(lab == ignore_index || (lab >= 0 && lab < V), kChkXentLabel);  // debug build: label outside the vocab
+    const bool skip = lab == ignore_index || (ACC_DEBUG_BUILD && (lab < 0 || lab >= V));
+    loss[row] = skip ? 0.f : (lse - bf2f(x[lab]));
   }
 }
 
@@ -146,6 +148,8 @@ __global__ __launch_bounds__(kMTThreads) void adam_mt_kernel(const TensorMeta* _
                                                              const int64_t* __restrict__ block_prefix, int ntensors,
                                                              AdamHyper h, const float* __restrict__ grad_scale) {
   const int t = find_tensor(block_prefix, ntensors, blockIdx.x);
+  // debug build: the block maps to a listed tensor and a chunk inside it (block-uniform)
+  ACC_CHECK_OR_RETURN(t >= 0 && t < ntensors && (int64_t)(blockIdx.x - block_prefix[t]) * kChunk < meta[t].n, kChkMtChunk);
   const TensorMeta tm = meta[t];
   const int64_t start = (int64_t)(blockIdx.x - block_prefix[t]) * kChunk;
   const int64_t end = min(start + (int64_t)kChunk, tm.n);
@@ -254,6 +258,35 @@ __global__ __launch_bounds__(kMTThreads) void unscale_mt_kernel(const TensorMeta
 }
 
 }  // namespace
+
+ACC_DEBUG_TAKE_FN(acc_dbg_take_xent_optim)
+
+#ifdef ACC_DEBUG_BOUNDS
+namespace {
+// Self-test of the check mechanism itself: every lane past `n` reports a failed bounds check instead of writing.
+__global__ void acc_dbg_selftest_kernel(float* out, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  ACC_CHECK_OR_RETURN(i < n, kChkSelfTest);
+  out[i] = 1.f;
+}
+}  // namespace
+#endif
+
+// debug build: launch a kernel whose grid overshoots `out` by `overshoot` elements (the check must catch it and no
+// write may land past the end); release build: a no-op returning false.
+bool debug_selftest(torch::Tensor out, int64_t overshoot) {
+#ifdef ACC_DEBUG_BOUNDS
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.is_contiguous(), "debug_selftest: fp32 HIP tensor");
+  const int n = (int)out.numel(), total = n + (int)overshoot;
+  hipLaunchKernelGGL(acc_dbg_selftest_kernel, dim3((total + 255) / 256), dim3(256), 0, at::hip::getCurrentHIPStream(),
+                     out.data_ptr<float>(), n);
+  return true;
+#else
+  (void)out;
+  (void)overshoot;
+  return false;
+#endif
+}
 
 // ----------------------------------------------------------------------------------------- host API
 std::vector<torch::Tensor> xent_fwd(torch::Tensor logits, torch::Tensor labels, int64_t ignore_index) {

@@ -20,8 +20,11 @@ def _load():
     global _EXT, _ERR
     if _EXT is not None or _ERR is not None:
         return _EXT
+    # ACCELERATE_DEBUG_KERNELS=1: the debug build with device-side bounds checks (`_C_debug`); failed
+    # checks are read with `ext().debug_status()` (id << 32 | kernel source line)
+    name = "_C_debug" if os.environ.get("ACCELERATE_DEBUG_KERNELS", "0") == "1" else "_C"
     try:
-        _EXT = importlib.import_module("accelerate_hpc_test_amd._C")
+        _EXT = importlib.import_module(f"accelerate_hpc_test_amd.{name}")
     except Exception as e:  # pragma: no cover - depends on build state
         _ERR = e
     return _EXT
@@ -35,7 +38,7 @@ def ext():
     mod = _load()
     if mod is None:
         raise RuntimeError(
-            "accelerate_hpc_test_amd native extension (_C) is not built or failed to load: "
+            "accelerate_hpc_test_amd native extension (_C / _C_debug) is not built or failed to load: "
             f"{_ERR!r}. Build it with `PYTORCH_ROCM_ARCH=gfx950 python setup.py build_ext --inplace`."
         )
     return mod

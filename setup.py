@@ -38,6 +38,24 @@ if os.environ.get("ACCELERATE_SKIP_NATIVE_BUILD", "0") != "1":
             },
         )
     )
+    # Debug build: the same kernels with the device bounds checks compiled in (csrc/debug/* include the
+    # real sources under -DACC_DEBUG_BOUNDS), loaded instead of `_C` when ACCELERATE_DEBUG_KERNELS=1.
+    # ACCELERATE_BUILD_DEBUG_KERNELS=0 skips it.
+    if os.environ.get("ACCELERATE_BUILD_DEBUG_KERNELS", "1") != "0":
+        dbg = sorted(glob.glob(os.path.join(root, "debug", "*.hip"))) + sorted(glob.glob(os.path.join(root, "debug", "*.cpp")))
+        ext_modules.append(
+            CUDAExtension(
+                name="accelerate_hpc_test_amd._C_debug",
+                sources=[os.path.relpath(s, os.path.dirname(os.path.abspath(__file__))) for s in dbg],
+                include_dirs=[os.path.join(root, "kernels")],
+                libraries=["hipblaslt"],
+                extra_link_args=["-fopenmp"],
+                extra_compile_args={
+                    "cxx": ["-O3", "-std=c++17", "-fopenmp", "-DACC_DEBUG_BOUNDS"],
+                    "nvcc": ["-O3", "-std=c++17", "--offload-arch=gfx950", "-munsafe-fp-atomics", "-DACC_DEBUG_BOUNDS"],
+                },
+            )
+        )
     cmdclass = {"build_ext": BuildExtension.with_options(use_ninja=True)}
 
 console_scripts = [
