@@ -223,8 +223,10 @@ class H2DEngine {
 
 }  // namespace
 
+// module_local: the release (`_C`) and debug (`_C_debug`) builds register the same classes and may be loaded into one
+// process (tests/test_debug_kernels_gpu.py compares them)
 void register_runtime(pybind11::module& m) {
-  pybind11::class_<H2DEngine>(m, "H2DEngine")
+  pybind11::class_<H2DEngine>(m, "H2DEngine", pybind11::module_local())
       .def(pybind11::init<int, int64_t, int64_t, int64_t>(), pybind11::arg("device"), pybind11::arg("num_slots") = 4,
            pybind11::arg("slot_bytes") = 64 << 20, pybind11::arg("num_threads") = 4)
       .def("copy", &H2DEngine::copy, pybind11::call_guard<pybind11::gil_scoped_release>())
@@ -233,7 +235,7 @@ void register_runtime(pybind11::module& m) {
       .def("inflight", &H2DEngine::inflight)
       .def_property_readonly("slot_bytes", &H2DEngine::slot_bytes)
       .def_property_readonly("num_slots", &H2DEngine::num_slots);
-  pybind11::class_<acc_host::CollectiveSeq>(m, "CollectiveSeq")
+  pybind11::class_<acc_host::CollectiveSeq>(m, "CollectiveSeq", pybind11::module_local())
       .def(pybind11::init<>())
       .def("record", &acc_host::CollectiveSeq::record)
       .def("digest", &acc_host::CollectiveSeq::digest)
