@@ -36,6 +36,8 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--mode", choices=["fsdp", "fsdp_fp8", "ddp", "cp_allgather", "cp_alltoall"], required=True)
     p.add_argument("--seq", type=int, default=16384)
+    p.add_argument("--heads", default="8,2", help="cp modes: query,kv heads")
+    p.add_argument("--no-ref", action="store_true", help="cp modes: skip the fp32 reference (long sequences)")
     p.add_argument("--out", required=True)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--preset", default="llama-small")
@@ -137,7 +139,8 @@ def run_context_parallel(args):
     if W > 1:
         dist.init_process_group("gloo")
     r = dist.get_rank() if W > 1 else 0
-    S, Hq, Hkv, D = args.seq, 8, 2, 128
+    S, D = args.seq, 128
+    Hq, Hkv = (int(x) for x in args.heads.split(","))
     g = torch.Generator().manual_seed(11)
     full = {n: torch.randn(1, S, h, D, generator=g).to(torch.bfloat16).cuda() for n, h in
             (("q", Hq), ("k", Hkv), ("v", Hkv), ("do", Hq))}
@@ -145,10 +148,34 @@ def run_context_parallel(args):
     torch.cuda.synchronize()
     base = torch.cuda.memory_allocated()
     torch.cuda.reset_peak_memory_stats()
+    import time
+
+    t0 = time.perf_counter()
     o = ring_attention(local["q"], local["k"], local["v"], None, strategy=args.mode[3:])
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    fwd_peak = torch.cuda.max_memory_allocated() - base
     o.backward(local["do"])
     torch.cuda.synchronize()
+    t2 = time.perf_counter()
     transient = torch.cuda.max_memory_allocated() - base
+    if args.no_ref:
+        stats = [None] * W
+        mine = {"fwd_peak": int(fwd_peak), "peak": int(transient), "fwd_s": t1 - t0, "bwd_s": t2 - t1}
+        if W > 1:
+            dist.all_gather_object(stats, mine)
+        else:
+            stats = [mine]
+        if r == 0:
+            res = {"world": W, "mode": args.mode, "seq": S, "heads": [Hq, Hkv], "per_rank": stats}
+            os.makedirs(args.out, exist_ok=True)
+            with open(os.path.join(args.out, f"mem_{args.mode}_W{W}_S{S}.json"), "w") as f:
+                json.dump(res, f)
+            print(json.dumps(res), flush=True)
+        if W > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
 
     def gather(t):
         if W == 1:
