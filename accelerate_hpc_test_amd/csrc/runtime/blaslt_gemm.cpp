@@ -156,7 +156,8 @@ struct F8Plan {
 };
 
 struct F8State {
-  std::map<std::tuple<int64_t, int64_t, int64_t, int, int, int, int>, F8Plan> plans;
+  // (M, N, K, lda, ldb, dtype A, dtype B, fp32 out, device)
+  std::map<std::tuple<int64_t, int64_t, int64_t, int64_t, int64_t, int, int, int, int>, F8Plan> plans;
 };
 
 F8State& f8state() {
@@ -172,15 +173,15 @@ bool set_scales(hipblasLtMatmulDesc_t desc, const void* sa, const void* sb) {
          check(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_B_SCALE_POINTER, &sa, sizeof(sa)));
 }
 
-bool build_f8_plan(State& s, F8Plan& p, int64_t M, int64_t N, int64_t K, at::ScalarType ta_, at::ScalarType tb_, bool out_f32,
-                   hipStream_t stream, const torch::Tensor& like) {
+bool build_f8_plan(State& s, F8Plan& p, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, at::ScalarType ta_,
+                   at::ScalarType tb_, bool out_f32, hipStream_t stream, const torch::Tensor& like) {
   const hipblasOperation_t opA = HIPBLAS_OP_T, opB = HIPBLAS_OP_N;
   const hipDataType dt = out_f32 ? HIP_R_32F : HIP_R_16BF;
   if (!check(hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F))) return false;
   if (!check(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &opA, sizeof(opA)))) return false;
   if (!check(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &opB, sizeof(opB)))) return false;
-  if (!check(hipblasLtMatrixLayoutCreate(&p.la, f8type(tb_), K, N, K))) return false;
-  if (!check(hipblasLtMatrixLayoutCreate(&p.lb, f8type(ta_), K, M, K))) return false;
+  if (!check(hipblasLtMatrixLayoutCreate(&p.la, f8type(tb_), K, N, ldb))) return false;
+  if (!check(hipblasLtMatrixLayoutCreate(&p.lb, f8type(ta_), K, M, lda))) return false;
   if (!check(hipblasLtMatrixLayoutCreate(&p.lc, dt, N, M, N))) return false;
   auto one_t = torch::ones({2}, like.options().dtype(torch::kFloat32));
   if (!set_scales(p.desc, one_t.data_ptr<float>(), one_t.data_ptr<float>() + 1)) return false;
@@ -195,8 +196,8 @@ bool build_f8_plan(State& s, F8Plan& p, int64_t M, int64_t N, int64_t K, at::Sca
   hipblasLtMatmulPreferenceDestroy(pref);
   if (!okh || got <= 0) return false;
   p.candidates = got;
-  auto a = torch::empty({M, K}, like.options().dtype(torch::kUInt8)).random_(0, 64);  // small finite fp8 values
-  auto b = torch::empty({N, K}, like.options().dtype(torch::kUInt8)).random_(0, 64);
+  auto a = torch::empty({M, lda}, like.options().dtype(torch::kUInt8)).random_(0, 64);  // small finite fp8 values
+  auto b = torch::empty({N, ldb}, like.options().dtype(torch::kUInt8)).random_(0, 64);
   auto d = torch::empty({M, N}, like.options().dtype(out_f32 ? torch::kFloat32 : torch::kBFloat16));
   const float one = 1.f, zero = 0.f;
   hipEvent_t e0, e1;
@@ -241,9 +242,13 @@ bool blaslt_fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor sa, torch::
   TORCH_CHECK(out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16, "blaslt_fp8_gemm: bf16 / fp32 output");
   TORCH_CHECK(sa.scalar_type() == at::kFloat && sb.scalar_type() == at::kFloat && sa.numel() >= 1 && sb.numel() >= 1,
               "blaslt_fp8_gemm: fp32 scale tensors expected");
-  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && out.dim() == 2 && a.is_contiguous() && b.is_contiguous() && out.is_contiguous(),
-              "blaslt_fp8_gemm: 2-D contiguous tensors expected");
+  // A and B may be row slices / column windows of larger row-major matrices (leading dimension = stride(0), e.g. an
+  // expert's token range of a transposed activation for the MoE weight gradient); C is contiguous
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && out.dim() == 2 && a.stride(1) == 1 && b.stride(1) == 1 &&
+                  a.stride(0) >= a.size(1) && b.stride(0) >= b.size(1) && out.is_contiguous(),
+              "blaslt_fp8_gemm: 2-D row-major operands (unit column stride) and a contiguous output expected");
   const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  const int64_t lda = a.stride(0), ldb = b.stride(0);
   TORCH_CHECK(b.size(1) == K && out.size(0) == M && out.size(1) == N, "blaslt_fp8_gemm: shape mismatch");
   const bool out_f32 = out.scalar_type() == at::kFloat;
   State& s = state();
@@ -256,11 +261,11 @@ bool blaslt_fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor sa, torch::
       if (!check(hipblasLtCreate(&s.handle))) return false;
       s.workspace = torch::empty({(int64_t)kWorkspace}, out.options().dtype(torch::kUInt8));
     }
-    auto key = std::make_tuple(M, N, K, (int)ta, (int)tb, (int)out_f32, (int)out.get_device());
+    auto key = std::make_tuple(M, N, K, lda, ldb, (int)ta, (int)tb, (int)out_f32, (int)out.get_device());
     auto it = fs.plans.find(key);
     if (it == fs.plans.end()) {
       F8Plan p;
-      build_f8_plan(s, p, M, N, K, ta, tb, out_f32, stream, out);
+      build_f8_plan(s, p, M, N, K, lda, ldb, ta, tb, out_f32, stream, out);
       it = fs.plans.emplace(key, p).first;
     }
     plan = &it->second;

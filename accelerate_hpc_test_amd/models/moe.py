@@ -25,6 +25,7 @@ expert GEMMs. Design:
 
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -106,6 +107,58 @@ def _gg_native_ok(a, b, mode, out) -> bool:
     return a.shape[0] % 256 == 0 and b.shape[0] % 256 == 0 and (a.shape[1] * es) % 16 == 0
 
 
+# Expert GEMM backend: "blaslt" = one hipBLASLt GEMM per expert on its segment (bf16 through torch, fp8 through our
+# runner), which needs the segment table on the host: `expert_layout` callers attach it (`seg._acc_bounds`, ONE device
+# -> host copy per MoE layer forward; the backward reuses it). Measured at Mixtral-8x7B shapes (tools/bench_moe_gemm.py,
+# profiles/r3_moe_gemm.md) 1.2-1.5x faster than the HIP grouped kernel even with that sync. "grouped" = the HIP grouped
+# kernel over the device table (no host sync at all), also used whenever no host table is attached.
+_MOE_GEMM = os.environ.get("ACCELERATE_MOE_GEMM", "blaslt")
+
+
+def _per_expert_mm(a, b, bounds, mode, out, sa, sb, smul, accumulate) -> bool:
+    """grouped_mm as one library GEMM per expert; False when a problem has no library path (then the HIP kernel runs)."""
+    E = len(bounds) - 1
+    fp8 = a.dtype in (torch.float8_e4m3fn, torch.float8_e5m2)
+    if fp8 and (sa is None or sb is None):
+        return False
+    if mode == 1:
+        for e in range(E):
+            lo, hi = bounds[e], bounds[e + 1]
+            if hi <= lo:
+                continue
+            if fp8:
+                if not ext().blaslt_fp8_gemm(a[lo:hi], b[e], sa, sb[e : e + 1], smul, out[lo:hi], accumulate):
+                    return False
+            else:
+                o = out[lo:hi]
+                res = torch.mm(a[lo:hi], b[e].t(), out_dtype=out.dtype) if out.dtype != a.dtype else torch.mm(a[lo:hi], b[e].t())
+                if smul != 1.0:
+                    res = res * smul
+                o.add_(res) if accumulate else o.copy_(res)
+        if not accumulate and bounds[E] < out.shape[0]:
+            out[bounds[E] :].zero_()  # rows past the last segment are defined (zero), as the grouped kernel leaves them
+        return True
+    for e in range(E):
+        lo, hi = bounds[e], bounds[e + 1]
+        o = out[e]
+        if hi <= lo:
+            if not accumulate:
+                o.zero_()
+            continue
+        if fp8:
+            if not ext().blaslt_fp8_gemm(a[:, lo:hi], b[:, lo:hi], sa, sb, smul, o, accumulate):
+                return False
+        elif o.dtype == a.dtype and smul == 1.0:
+            o.addmm_(a[:, lo:hi], b[:, lo:hi].t()) if accumulate else torch.mm(a[:, lo:hi], b[:, lo:hi].t(), out=o)
+        elif o.dtype == torch.float32 and smul == 1.0:
+            torch.addmm(o, a[:, lo:hi], b[:, lo:hi].t(), out_dtype=torch.float32, out=o) if accumulate else \
+                torch.mm(a[:, lo:hi], b[:, lo:hi].t(), out_dtype=torch.float32, out=o)
+        else:
+            res = (a[:, lo:hi].float() @ b[:, lo:hi].float().t()) * smul
+            o.add_(res.to(o.dtype)) if accumulate else o.copy_(res)
+    return True
+
+
 def grouped_mm(a, b, seg, mode, out, sa=None, sb=None, smul=1.0, accumulate=False):
     """One grouped GEMM over the expert segment table `seg` (csrc/kernels/grouped_gemm.hip):
     mode 1: out[r] = a[r] . b[e]^T for rows r of segment e (a [R, K], b [E, N, K], out [R, N]; rows past seg[E] -> 0);
@@ -113,6 +166,10 @@ def grouped_mm(a, b, seg, mode, out, sa=None, sb=None, smul=1.0, accumulate=Fals
     sa / sb: fp32 amax-style scale tensors ([1] and [E] (mode 1) / [1] (mode 2)), times `smul`. Off the GPU (and for
     shapes the kernel does not tile) the same product runs in PyTorch from a host copy of `seg`."""
     E = seg.numel() - 1
+    bounds = getattr(seg, "_acc_bounds", None)
+    if (bounds is not None and _MOE_GEMM == "blaslt" and a.is_cuda and use_native(a)
+            and _per_expert_mm(a, b, bounds, mode, out, sa, sb, smul, accumulate)):
+        return out
     if _gg_native_ok(a, b, mode, out):
         sa = sa if sa is not None else _ones(1, a.device)
         sb = sb if sb is not None else _ones(E if mode == 1 else 1, a.device)
@@ -166,6 +223,7 @@ class _GroupedExpertsFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w_gu, w_down, seg, recipe, slots=(None, None)):
+        ctx.bounds = getattr(seg, "_acc_bounds", None)
         R, H = x.shape
         E, I2, _ = w_gu.shape
         I = w_down.shape[2]
@@ -184,6 +242,8 @@ class _GroupedExpertsFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, w_gu, w_down, seg = ctx.saved_tensors
+        if ctx.bounds is not None:
+            seg._acc_bounds = ctx.bounds  # the forward's host copy of the segment table: no second sync
         dy = dy.contiguous().to(x.dtype)
         # weight-gradient destinations: the FSDP engine's slot (fp32 grad shard at world size 1, flat bf16 grad buffer
         # otherwise; the grouped GEMM accumulates into it) or a fresh tensor returned to autograd
@@ -354,6 +414,7 @@ class MoELayer(nn.Module):
         flat_e = idx.reshape(-1)
         if self.ep_group is None or comm.group_size(self.ep_group) == 1:
             order, dest, seg, R = expert_layout(flat_e, self.num_experts)
+            _attach_bounds(seg)
             src_tok = order // self.top_k
             w_sorted = w.reshape(-1)[order]
             x_routed = t.new_zeros(R, t.shape[1]).index_copy(0, dest, t.index_select(0, src_tok))
@@ -377,13 +438,19 @@ class MoELayer(nn.Module):
         El = self.num_experts // W
         send_e = torch.bincount(e_sorted, minlength=self.num_experts).to(torch.int64)  # [W * El], rank-major
         recv_e = self._exchange_counts(send_e, W, group)  # recv_e[s * El + j]: rows of my expert j from rank s
-        sc_rc = torch.cat([send_e.view(W, El).sum(1), recv_e.view(W, El).sum(1)]).tolist()
-        sc, rc = sc_rc[:W], sc_rc[W:]
+        host = torch.cat([send_e.view(W, El).sum(1), recv_e.view(W, El).sum(1), recv_e]).tolist()
+        sc, rc, rcv = host[:W], host[W : 2 * W], host[2 * W :]
         x_recv = comm.all_to_all_var(x_sorted, sc, rc, group)
         local_ids = torch.arange(El, device=x_sorted.device).repeat(W)
         e_recv = torch.repeat_interleave(local_ids, recv_e, output_size=sum(rc))
         # local experts: the same device-side layout + grouped GEMMs as the single-rank path
         order2, dest2, seg2, R2 = expert_layout(e_recv, El)
+        if seg2.is_cuda and _MOE_GEMM == "blaslt" and use_native(seg2):  # host segment table from the same copy
+            bounds = [0]
+            for j in range(El):
+                c = sum(rcv[s_ * El + j] for s_ in range(W))
+                bounds.append(bounds[-1] + _round_up(c, SEG_ALIGN))
+            seg2._acc_bounds = bounds
         x_routed = x_recv.new_zeros(R2, x_recv.shape[1]).index_copy(0, dest2, x_recv.index_select(0, order2))
         y_local_sorted = self.experts(x_routed, seg2).index_select(0, dest2)
         inv = torch.empty_like(order2)
@@ -403,6 +470,13 @@ class MoELayer(nn.Module):
         recv_e = torch.empty_like(send_e)
         dist.all_to_all_single(recv_e, send_e, group=group)
         return recv_e
+
+
+def _attach_bounds(seg):
+    """Host copy of the segment table for the per-expert library GEMMs (one device -> host copy per MoE layer)."""
+    if seg.is_cuda and _MOE_GEMM == "blaslt" and use_native(seg):
+        seg._acc_bounds = seg.tolist()
+    return seg
 
 
 def load_balancing_loss(router_logits: list, num_experts: int, top_k: int) -> torch.Tensor:
