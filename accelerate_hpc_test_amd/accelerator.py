@@ -362,6 +362,12 @@ class Accelerator:
         self._watchdog = StepWatchdog.from_env(self.rccl_handler.watchdog_timeout, rank=self.process_index)
         self._fault_injector = FaultInjector.from_env(self.process_index)
         check_os_kernel()
+        if (self.device.type == "cuda" and self.num_processes > 1 and self.local_process_index == 0
+                and os.environ.get("ACCELERATE_CHECK_TOPOLOGY", "1") != "0"):
+            # xGMI links between this node's GPUs, P2P / IPC switches (parallel/topology.py)
+            from .parallel.topology import validate_comm_environment
+
+            validate_comm_environment(int(os.environ.get("LOCAL_WORLD_SIZE", self.num_processes) or self.num_processes))
 
     # ============================================================================== properties
     # Read-through views of the process state and the dataloader / project configurations (`_delegate`, module

@@ -63,8 +63,15 @@ def env_command(args):
     else:
         lines.append(f"\t{cfg if cfg else 'Not found'}")
     if getattr(args, "topology", False):
+        from ..parallel.topology import environment_problems, link_problems, parse_link_types
+
+        text = get_xgmi_topology()
         lines.append("- xGMI topology:")
-        lines.append(get_xgmi_topology() or "\tunavailable")
+        lines.append(text or "\tunavailable")
+        types = parse_link_types(text)
+        gpus = sorted({i for i, _ in types})
+        problems = environment_problems() + link_problems(gpus, types)
+        lines.append("- Communication checks: " + ("ok" if not problems else "; ".join(problems)))
     print("\n".join(lines))
     info["Default config"] = cfg
     return info
