@@ -9,8 +9,8 @@ raised with ACCELERATE_STRICT_TOPOLOGY=1):
 
 * link type of every local GPU pair (`rocm-smi --showtopotype`): anything but XGMI means ring steps over PCIe;
 * environment switches that silently cost bandwidth or break IPC: NCCL_P2P_DISABLE / NCCL_SHM_DISABLE /
-  NCCL_P2P_LEVEL=LOC, HSA_ENABLE_IPC_MODE_LEGACY != 0, HSA_NO_SCRATCH_RECLAIM, a RCCL channel cap below the link count;
-* HIP peer access between the devices (only where it does not initialise devices the rank does not own).
+  NCCL_P2P_LEVEL=LOC, HSA_ENABLE_IPC_MODE_LEGACY != 0, a RCCL channel cap below the link count.
+The HIP-IPC all-reduce additionally self-tests its peer mappings at setup (parallel/small_allreduce.py).
 """
 
 from __future__ import annotations
