@@ -48,6 +48,22 @@ def test_bench_spawns_its_own_ranks(tmp_path):
     assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "fsdp2" and rec["config"]["global_batch"] == 2
 
 
+def test_rccl_bench_tool_gloo_plumbing():
+    """tools/bench_rccl.py (the xGMI collective bandwidth sweep) on 2 gloo ranks: one JSON line per (op, size) from rank 0,
+    bus bandwidth following the rccl-tests factors."""
+    from accelerate_hpc_test_amd.utils.other import get_free_port
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(get_free_port()), "tools/bench_rccl.py", "--cpu", "--max-mb", "2", "--iters", "2"]
+    r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=300, env=dict(os.environ, PYTHONPATH=REPO))
+    assert r.returncode == 0, r.stderr[-3000:]
+    recs = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert {(x["op"], x["bytes"]) for x in recs} == {(op, b) for op in ("all_gather", "all_reduce") for b in (1 << 20, 2 << 20)}
+    for x in recs:
+        f = 0.5 if x["op"] == "all_gather" else 1.0
+        assert abs(x["busbw_GBs"] - x["algbw_GBs"] * f) <= 0.011 + 0.01 * x["algbw_GBs"], x
+
+
 def test_bench_rejects_world_size_mismatch(tmp_path):
     env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", PYTHONPATH=REPO, HF_HOME=str(tmp_path))
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "4", "--cpu", "--model", "llama-tiny"], cwd=REPO,
