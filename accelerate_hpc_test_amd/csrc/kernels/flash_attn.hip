@@ -161,6 +161,21 @@ __device__ __forceinline__ void wait_dma_and_sync() {
   __syncthreads();                                   // ... and every wave's, and every wave is done reading
 }
 
+// Timeline diagnostics (tools/attn_timeline.py): with a trace buffer installed every wave records, in 4 u64 at
+// trace[32 * linear block id + 4 * wave], its start and end on the constant-rate wall clock, the CU / SE / XCD it ran
+// on, and a caller tag (tile / head). Vector stores from lane 0; no cost but a kernel-argument test when off.
+__device__ __forceinline__ void wave_trace(unsigned long long* trace, long long t0, int wave, unsigned tag) {
+  if (trace != nullptr && (threadIdx.x & 63) == 0) {
+    const long long t1 = wall_clock64();
+    const unsigned long long blk = ((unsigned long long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    unsigned long long* t = trace + blk * 32 + 4 * wave;
+    t[0] = (unsigned long long)t0;
+    t[1] = (unsigned long long)t1;
+    t[2] = __smid();
+    t[3] = tag;
+  }
+}
+
 struct FwdParams {
   const bf16_t *q, *k, *v;
   long q_ts, k_ts, v_ts, q_bs, k_bs, v_bs;
@@ -170,6 +185,7 @@ struct FwdParams {
   int S, Hq, Hkv;
   float scale_log2;
   int Sk, off;  // key count and causal offset Sk - S
+  unsigned long long* trace;  // optional per-wave timeline (attn_trace), see wave_trace
 };
 
 template <bool CAUSAL>
@@ -178,6 +194,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(FwdParams p) {
   // feeds the ds_reads of the other (no vmcnt(0) before every read)
   constexpr int kTile = 64 * kRow;  // 16 KB per operand image
   __shared__ __attribute__((aligned(1024))) char k0s[kTile], v0s[kTile], k1s[kTile], v1s[kTile];
+  const long long t_start = wall_clock64();
   const int nqt = p.S / 128;
   const int h = xcd_head(blockIdx.x, p.Hq), b = blockIdx.z;
   const int kh = h / (p.Hq / p.Hkv);
@@ -299,6 +316,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(FwdParams p) {
       *reinterpret_cast<bf16x4*>(ob + d * 32 + 8 * g + 4 * hf) = w;
     }
   if (hf == 0) p.lse[((long)b * p.Hq + h) * p.S + qw0 + r] = (m + __builtin_amdgcn_logf(l)) * kLn2;
+  wave_trace(p.trace, t_start, wave, (unsigned)qt | ((unsigned)h << 16));
 }
 
 // delta[b, h, s] = sum_d dO * O (fp32), one wave per (b, s, h).
@@ -332,12 +350,14 @@ struct BwdParams {
   long o_ts, o_bs;
   float* delta_out;
   int Sk, off;  // key count and causal offset Sk - S (see the header)
+  unsigned long long* trace;  // optional per-wave timeline (attn_trace), see wave_trace
 };
 
 template <bool CAUSAL>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(BwdParams p) {
   constexpr int kTile = 64 * kRow;
   __shared__ __attribute__((aligned(1024))) char k0s[kTile], v0s[kTile], k1s[kTile], v1s[kTile];  // as in the forward
+  const long long t_start = wall_clock64();
   const int nqt = p.S / 128;
   const int qt = CAUSAL ? (nqt - 1 - (int)blockIdx.y) : (int)blockIdx.y;  // grid (Hq, S/128, B), heavy first
   const int h = xcd_head(blockIdx.x, p.Hq), b = blockIdx.z;
@@ -449,6 +469,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(BwdParams p) {
       for (int t = 0; t < 4; ++t) w.v[t] = f2bf(dq[d][4 * g + t] * p.scale);
       *reinterpret_cast<bf16x4*>(out + d * 32 + 8 * g + 4 * hf) = w;
     }
+  wave_trace(p.trace, t_start, wave, (unsigned)qt | ((unsigned)h << 16));
 }
 
 // Key-stationary dK / dV for one (batch, kv head, 128-key tile), summed over the kv head's whole GQA group of query
@@ -469,6 +490,7 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_kernel(BwdParams p) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * kKV];
   __shared__ __attribute__((aligned(1024))) char qs0[kImg], ds0[kImg], qs1[kImg], ds1[kImg];
   __shared__ __attribute__((aligned(16))) float ls0[2 * kSlice], ls1[2 * kSlice];
+  const long long t_start = wall_clock64();
   // grid.x = Hkv * nkt with the kv head fastest: key tile 0 (the most causal work) of every head is dispatched first,
   // and all tiles of one head share blockIdx.x % 8 (one XCD under round-robin dispatch), whose L2 then serves that
   // head's Q / dO stream to all of them.
@@ -612,6 +634,7 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_kernel(BwdParams p) {
   };
   finish(dk, p.dk, p.dk_ts, p.dk_bs, p.scale);
   finish(dv, p.dv, p.dv_ts, p.dv_bs, 1.f);
+  wave_trace(p.trace, t_start, wave, (unsigned)kt | ((unsigned)kh << 16));
 }
 
 void check_qkv(const torch::Tensor& t, const char* name) {
@@ -643,6 +666,26 @@ ACC_DEBUG_TAKE_FN(acc_dbg_take_flash_attn)
 static int g_attn_dbg = 0;
 void attn_debug_mode(int64_t mode) { g_attn_dbg = (int)mode; }
 
+// Timeline buffer for the next launches (tools/attn_timeline.py): an int64 HIP tensor with 32 entries per workgroup
+// of the largest grid launched, or an empty tensor to switch tracing off. The caller keeps the tensor alive.
+static unsigned long long* g_attn_trace = nullptr;
+static long g_attn_trace_len = 0;
+void attn_trace(torch::Tensor buf) {
+  if (buf.numel() == 0) {
+    g_attn_trace = nullptr;
+    g_attn_trace_len = 0;
+    return;
+  }
+  TORCH_CHECK(buf.is_cuda() && buf.scalar_type() == at::kLong && buf.is_contiguous(), "attn_trace: int64 HIP tensor");
+  g_attn_trace = reinterpret_cast<unsigned long long*>(buf.data_ptr());
+  g_attn_trace_len = buf.numel();
+}
+static unsigned long long* trace_for(const dim3& g) {
+  if (g_attn_trace == nullptr) return nullptr;
+  TORCH_CHECK((long)g.x * g.y * g.z * 32 <= g_attn_trace_len, "attn_trace: buffer too small for the grid");
+  return g_attn_trace;
+}
+
 // q: [B, S, Hq, D], k/v: [B, S, Hkv, D] (views into a fused QKV buffer are fine). Returns (O [B,S,Hq,D], LSE [B,Hq,S]).
 std::vector<torch::Tensor> flash_attn_fwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, double softmax_scale,
                                           bool causal) {
@@ -659,8 +702,9 @@ std::vector<torch::Tensor> flash_attn_fwd(torch::Tensor q, torch::Tensor k, torc
   FwdParams p{reinterpret_cast<const bf16_t*>(q.data_ptr()), reinterpret_cast<const bf16_t*>(k.data_ptr()),
               reinterpret_cast<const bf16_t*>(v.data_ptr()), q.stride(1), k.stride(1), v.stride(1), q.stride(0),
               k.stride(0), v.stride(0), reinterpret_cast<bf16_t*>(o.data_ptr()), o.stride(1), o.stride(0),
-              lse.data_ptr<float>(), S, Hq, Hkv, (float)(softmax_scale * kLog2e), Sk, Sk - S};
+              lse.data_ptr<float>(), S, Hq, Hkv, (float)(softmax_scale * kLog2e), Sk, Sk - S, nullptr};
   dim3 grid(Hq, S / 128, B);
+  p.trace = trace_for(grid);
   auto stream = at::hip::getCurrentHIPStream();
   if (causal) hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(256), 0, stream, p);
   else hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(256), 0, stream, p);
@@ -702,22 +746,27 @@ void flash_attn_bwd(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch:
               dq.stride(0), dk.stride(1), dk.stride(0), dv.stride(1), dv.stride(0), S, Hq, Hkv,
               (float)(softmax_scale * kLog2e), (float)softmax_scale, (float)(1.0 / softmax_scale),
               reinterpret_cast<const bf16_t*>(o.data_ptr()), o.stride(1), o.stride(0),
-              fused_delta ? delta.data_ptr<float>() : nullptr, Sk, Sk - S};
+              fused_delta ? delta.data_ptr<float>() : nullptr, Sk, Sk - S, nullptr};
   const dim3 dq_grid(Hq, S / 128, B), kv_grid(Hkv * (Sk / 128), B);
+  p.trace = trace_for(dq_grid);
+  BwdParams pk = p;
+  pk.trace = g_attn_trace == nullptr ? nullptr : trace_for(kv_grid) + (long)dq_grid.x * dq_grid.y * dq_grid.z * 32;
+  TORCH_CHECK(g_attn_trace == nullptr || (long)(dq_grid.x * dq_grid.y * dq_grid.z + kv_grid.x * kv_grid.y) * 32 <= g_attn_trace_len,
+              "attn_trace: buffer too small for the dQ + dK/dV grids");
   if (causal && g_attn_dbg != 0) {  // diagnostic timing variants (tools/bench_attn.py --dbg)
     if (g_attn_dbg & 8) hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, dq_grid, dim3(256), 0, stream, p);
     const int m = g_attn_dbg & 3;
-    if (m == 1) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<true, 1>), kv_grid, dim3(512), 0, stream, p);
-    else if (m == 2) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<true, 2>), kv_grid, dim3(512), 0, stream, p);
-    else if (m == 3) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<true, 3>), kv_grid, dim3(512), 0, stream, p);
-    else if (g_attn_dbg & 4) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<true, 0>), kv_grid, dim3(512), 0, stream, p);
+    if (m == 1) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<true, 1>), kv_grid, dim3(512), 0, stream, pk);
+    else if (m == 2) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<true, 2>), kv_grid, dim3(512), 0, stream, pk);
+    else if (m == 3) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<true, 3>), kv_grid, dim3(512), 0, stream, pk);
+    else if (g_attn_dbg & 4) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<true, 0>), kv_grid, dim3(512), 0, stream, pk);
     return;
   }
   if (causal) {
     hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, dq_grid, dim3(256), 0, stream, p);
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<true, 0>), kv_grid, dim3(512), 0, stream, p);
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<true, 0>), kv_grid, dim3(512), 0, stream, pk);
   } else {
     hipLaunchKernelGGL(attn_bwd_dq_kernel<false>, dq_grid, dim3(256), 0, stream, p);
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<false, 0>), kv_grid, dim3(512), 0, stream, p);
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<false, 0>), kv_grid, dim3(512), 0, stream, pk);
   }
 }
