@@ -113,13 +113,17 @@ def _gg_native_ok(a, b, mode, out) -> bool:
 # profiles/r3_moe_gemm.md) 1.2-1.5x faster than the HIP grouped kernel even with that sync. "grouped" = the HIP grouped
 # kernel over the device table (no host sync at all), also used whenever no host table is attached.
 _MOE_GEMM = os.environ.get("ACCELERATE_MOE_GEMM", "blaslt")
+# fp8 expert GEMMs stay on the HIP grouped kernel by default: the fp8 hipBLASLt runner times its candidates once per
+# exact problem, and the per-expert row counts change every step, so each step paid new searches (each one a host
+# sync): Mixtral-8x7B-8l fp8 fell from 36.7k to 14.3k tok/s with it (profiles/r3_moe_gemm.md).
+_MOE_FP8_BLASLT = os.environ.get("ACCELERATE_MOE_FP8_BLASLT", "0") == "1"
 
 
 def _per_expert_mm(a, b, bounds, mode, out, sa, sb, smul, accumulate) -> bool:
     """grouped_mm as one library GEMM per expert; False when a problem has no library path (then the HIP kernel runs)."""
     E = len(bounds) - 1
     fp8 = a.dtype in (torch.float8_e4m3fn, torch.float8_e5m2)
-    if fp8 and (sa is None or sb is None):
+    if fp8 and (sa is None or sb is None or not _MOE_FP8_BLASLT):
         return False
     if mode == 1:
         for e in range(E):

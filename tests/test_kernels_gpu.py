@@ -386,12 +386,13 @@ def test_grouped_gemm_kernel_both_modes(dt):
 
 @pytest.mark.parametrize("backend", ["grouped", "blaslt"])
 @pytest.mark.parametrize("fp8_on", [False, True])
-def test_moe_grouped_experts_match_per_expert_reference(fp8_on, backend):
+def test_moe_grouped_experts_match_per_expert_reference(fp8_on, backend, monkeypatch):
     """MoEExperts on the routed buffer against a per-expert fp32 PyTorch reference: forward, dx, dW_gate_up, dW_down;
     fp8 within fp8 error of it (forward vs an exact emulation of the per-tensor / per-expert e4m3 quantisation); an
     expert with no tokens gets a zero gradient. backend "grouped": 6 HIP grouped GEMM launches over the device segment
     table; "blaslt": the host segment table attached (as MoELayer does), one hipBLASLt GEMM per expert and projection
-    (bf16 through torch, fp8 through the runner with per-expert scales and column-window operands)."""
+    (bf16 through torch, fp8 — opt-in, ACCELERATE_MOE_FP8_BLASLT=1 — through the runner with per-expert scales and
+    column-window operands)."""
     import torch.nn.functional as F
 
     from accelerate_hpc_test_amd.models.moe import MoEExperts
@@ -408,6 +409,7 @@ def test_moe_grouped_experts_match_per_expert_reference(fp8_on, backend):
     x, seg, dest = _routed(counts, H, seed=1)
     if backend == "blaslt":
         seg._acc_bounds = seg.tolist()
+        monkeypatch.setattr("accelerate_hpc_test_amd.models.moe._MOE_FP8_BLASLT", True)  # opt-in for fp8
     dy = torch.zeros_like(x).index_copy(0, dest, torch.randn(dest.numel(), H, device=DEV, dtype=torch.bfloat16))
     xi = x.clone().requires_grad_(True)
     y = ex(xi, seg)

@@ -38,7 +38,13 @@ def analyse(name, tr, tiles_of, slots_per_cu, rate_hz):
     for cu, end in zip(smid, e):
         last[cu] = max(last.get(cu, 0.0), end)
     ends = np.array(sorted(last.values()))
-    return {"kernel": name, "workgroups": int(len(dur)), "cus_seen": ncu, "wall_us": round(float(wall), 1),
+    by_tag = {}
+    for t, d in zip(tag, dur):
+        by_tag.setdefault(int(t) & 0xFFFF, []).append(float(d))
+    keys = sorted(by_tag)
+    pick = sorted({keys[0], keys[len(keys) // 4], keys[len(keys) // 2], keys[3 * len(keys) // 4], keys[-1]})
+    tile_us = {int(k): [round(float(np.median(by_tag[k])), 1), tiles_of(k)] for k in pick}  # tile index -> [median us, tiles]
+    return {"kernel": name, "median_us_by_tile_index": tile_us, "workgroups": int(len(dur)), "cus_seen": ncu, "wall_us": round(float(wall), 1),
             "slot_busy_frac": round(float(busy), 3), "fixed_us_per_wg": round(float(a), 2),
             "us_per_tile": round(float(b), 3), "tiles_total": int(tiles.sum()),
             "ideal_us_at_fit_rate": round(float(tiles.sum() * b / (ncu * slots_per_cu)), 1),
@@ -63,9 +69,12 @@ def main():
     qkv = torch.randn(1, S, Hq + 2 * Hkv, D, device="cuda", dtype=torch.bfloat16)
     q, k, v = qkv[:, :, :Hq], qkv[:, :, Hq:Hq + Hkv], qkv[:, :, Hq + Hkv:]
     scale = D ** -0.5
-    rate = torch.cuda.get_device_properties(0).__dict__.get("wall_clock_rate", None)
-    rate_hz = 100e6 if not rate else float(rate) * 1e3  # kHz -> Hz; MI355X wall clock 100 MHz
-    nq = Hq * (S // 128)
+    rate_hz = 100e6  # the constant-rate wall clock (s_memrealtime) runs at 100 MHz on MI355X
+    # query heads per forward / dQ workgroup, as flash_attn.hip picks them (1 or 2; 2 -> one 8-wave workgroup per CU)
+    two = (Hq // Hkv) % 2 == 0
+    nh_f = 2 if two and os.environ.get("ACCELERATE_ATTN_FWD_HEADS", "2") == "2" else 1
+    nh_q = 2 if two and os.environ.get("ACCELERATE_ATTN_DQ_HEADS", "2") == "2" else 1
+    nq_f, nq = Hq // nh_f * (S // 128), Hq // nh_q * (S // 128)
     nkv = Hkv * (S // 128)
     buf = torch.zeros((nq + nkv) * 32, dtype=torch.int64, device="cuda")
     o, lse = E.flash_attn_fwd(q, k, v, scale, causal)  # warm
@@ -80,8 +89,9 @@ def main():
         E.flash_attn_fwd(q, k, v, scale, causal)
         torch.cuda.synchronize()
         E.attn_trace(torch.empty(0, dtype=torch.int64, device="cuda"))
-        tr = buf[: nq * 32].cpu().numpy()
-        print(json.dumps(dict(analyse("attn_fwd", tr, fwd_tiles, 2, rate_hz), seq=S, mask=a.mask)), flush=True)
+        tr = buf[: nq_f * 32].cpu().numpy()
+        print(json.dumps(dict(analyse("attn_fwd", tr, fwd_tiles, 2 // nh_f, rate_hz), seq=S, mask=a.mask, heads_per_wg=nh_f)),
+              flush=True)
     if a.which in ("bwd", "both"):
         buf.zero_()
         E.attn_trace(buf)
@@ -89,7 +99,8 @@ def main():
         torch.cuda.synchronize()
         E.attn_trace(torch.empty(0, dtype=torch.int64, device="cuda"))
         tr = buf.cpu().numpy()
-        print(json.dumps(dict(analyse("attn_bwd_dq", tr[: nq * 32], fwd_tiles, 2, rate_hz), seq=S, mask=a.mask)), flush=True)
+        print(json.dumps(dict(analyse("attn_bwd_dq", tr[: nq * 32], fwd_tiles, 2 // nh_q, rate_hz), seq=S, mask=a.mask,
+                              heads_per_wg=nh_q)), flush=True)
         print(json.dumps(dict(analyse("attn_bwd_dkdv", tr[nq * 32:], dkdv_tiles, 1, rate_hz), seq=S, mask=a.mask)), flush=True)
 
 

@@ -15,6 +15,7 @@ p.add_argument("--Hkv", type=int, default=8)
 p.add_argument("--B", type=int, default=1)
 p.add_argument("--iters", type=int, default=10)
 p.add_argument("--no-sdpa", action="store_true")
+p.add_argument("--isolated", action="store_true", help="also time single launches after a 50 ms idle gap")
 p.add_argument("--dbg", action="store_true", help="also time the causal backward's kernels separately and the dK/dV "
                "diagnostic variants (cache-hot fetch / no LDS commit); timing only")
 a = p.parse_args()
@@ -57,6 +58,27 @@ if a.dbg:
         dbg[name + "_ms"] = round((time.perf_counter() - t) / a.iters * 1e3, 3)
     e.attn_debug_mode(0)
     res["causal_bwd_parts"] = dbg
+if a.isolated:
+    # one kernel at a time after an idle gap (clock recovered), timed by events around the single launch: against the
+    # back-to-back loop above this separates sustained-power clock effects from the kernels' own cost
+    iso = {}
+    for causal in (True, False):
+        o, lse = e.flash_attn_fwd(q, k, v, scale, causal)
+        do = torch.randn_like(o)
+        for name, fn in (("fwd", lambda: e.flash_attn_fwd(q, k, v, scale, causal)),
+                         ("bwd", lambda: e.flash_attn_bwd(do, q, k, v, o, lse, dq, dk, dv, scale, causal))):
+            ts = []
+            for _ in range(5):
+                torch.cuda.synchronize()
+                time.sleep(0.05)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                fn()
+                e1.record()
+                e1.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            iso[f"{'causal' if causal else 'full'}_{name}_ms"] = round(sorted(ts)[2], 3)
+    res["isolated_median"] = iso
 if not a.no_sdpa:
     import torch.nn.functional as F
     from torch.nn.attention import SDPBackend, sdpa_kernel

@@ -52,9 +52,36 @@ def stall(dirs):
         print()
 
 
+def cache(dirs):
+    """L2 (TCC) hit rate and the L2 -> fabric read requests (Infinity Cache / HBM) per kernel, with clock and MFMA busy."""
+    for d in dirs:
+        files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+        ctr = defaultdict(lambda: defaultdict(float))
+        wall = defaultdict(dict)
+        for f in files:
+            for r in csv.DictReader(open(f)):
+                k = short(r["Kernel_Name"])
+                ctr[k][r["Counter_Name"]] += float(r["Counter_Value"])
+                wall[k][r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        print(f"### {d}\n")
+        print("| kernel | dispatches | wall ms | clock GHz | MFMA busy % | L2 hit % | L2 misses (M) | fabric read req (M) | fabric GB/s (x64 B) |")
+        print("|---|---:|---:|---:|---:|---:|---:|---:|---:|")
+        for k, c in sorted(ctr.items(), key=lambda kv: -kv[1].get("SQ_VALU_MFMA_BUSY_CYCLES", 0)):
+            grbm = c.get("GRBM_GUI_ACTIVE", 0) / 8
+            ns = sum(wall[k].values())
+            mfma = 100 * c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / (grbm * 1024) if grbm else 0
+            hit, miss = c.get("TCC_HIT_sum", 0), c.get("TCC_MISS_sum", 0)
+            rd = c.get("TCC_EA0_RDREQ_sum", 0)
+            print(f"| `{k}` | {len(wall[k])} | {ns / 1e6:.2f} | {grbm / ns if ns else 0:.2f} | {mfma:.1f} | "
+                  f"{100 * hit / (hit + miss) if hit + miss else 0:.1f} | {miss / 1e6:.1f} | {rd / 1e6:.1f} | {rd * 64 / ns if ns else 0:.0f} |")
+        print()
+
+
 def main(dirs):
     if dirs and dirs[0] == "--stall":
         return stall(dirs[1:])
+    if dirs and dirs[0] == "--cache":
+        return cache(dirs[1:])
     for d in dirs:
         files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
         ctr = defaultdict(lambda: defaultdict(float))
