@@ -17,7 +17,6 @@ import os
 import threading
 import warnings
 from contextlib import contextmanager
-from functools import partial
 from typing import Any, Callable
 
 import torch
@@ -57,6 +56,25 @@ class ThreadLocalSharedDict(threading.local):
 
 SharedDict = ThreadLocalSharedDict if parse_flag_from_env("ACCELERATE_THREAD_LOCAL_STATE") else dict
 
+# Attributes every initialised state carries: reading one of them after `_reset_state()` is a use-after-reset, reported
+# with a hint instead of the bare AttributeError.
+_PARTIAL_ATTRS = frozenset(
+    "_cpu _mixed_precision _shared_state backend debug device distributed_type fork_launched local_process_index "
+    "num_processes process_index".split()
+)
+_ACCELERATOR_ATTRS = _PARTIAL_ATTRS | frozenset(
+    "deepspeed_plugin use_ipex fsdp_plugin megatron_lm_plugin dynamo_plugin parallelism_config device_mesh".split()
+)
+
+
+def _missing_attribute(owner: str, name: str, known) -> AttributeError:
+    if name in known:
+        return AttributeError(
+            f"`{owner}` object has no attribute `{name}`. This happens if `{owner}._reset_state()` was called and an "
+            "`Accelerator` or `PartialState` was not reinitialized."
+        )
+    return AttributeError(f"'{owner}' object has no attribute '{name}'")
+
 
 class PartialState:
     """Process-level singleton: distributed environment, device, process indices.
@@ -66,19 +84,7 @@ class PartialState:
     """
 
     _shared_state = SharedDict()
-    _known_attrs = [
-        "_cpu",
-        "_mixed_precision",
-        "_shared_state",
-        "backend",
-        "debug",
-        "device",
-        "distributed_type",
-        "fork_launched",
-        "local_process_index",
-        "num_processes",
-        "process_index",
-    ]
+    _known_attrs = _PARTIAL_ATTRS
 
     def __init__(self, cpu: bool = False, **kwargs):
         self.__dict__ = self._shared_state
@@ -272,38 +278,35 @@ class PartialState:
     def local_main_process_first(self):
         yield from self._goes_first(self.is_local_main_process)
 
+    # ---- process-filter decorators: each returns `function` on the selected process(es) and a no-op elsewhere.
+    # Outside a distributed run every filter selects the (only) process.
+    def _selected(self, chosen: bool, function):
+        return function if (chosen or not self.use_distributed) else do_nothing
+
     def on_main_process(self, function: Callable[..., Any] | None = None):
         if not self.initialized:
             raise ValueError("The `PartialState` or `Accelerator` must be initialized before calling this function.")
-        if self.is_main_process or not self.use_distributed:
-            return function
-        return do_nothing
+        return self._selected(self.is_main_process, function)
 
     def on_local_main_process(self, function: Callable[..., Any] | None = None):
-        if self.is_local_main_process or not self.use_distributed:
-            return function
-        return do_nothing
+        return self._selected(self.is_local_main_process, function)
 
     def on_last_process(self, function: Callable[..., Any]):
-        if self.is_last_process or not self.use_distributed:
-            return function
-        return do_nothing
+        return self._selected(self.is_last_process, function)
 
     def on_process(self, function: Callable[..., Any] | None = None, process_index: int | None = None):
+        # usable bare (`@state.on_process(process_index=1)`) or applied directly
         if function is None:
-            return partial(self.on_process, process_index=process_index)
-        if (self.process_index == process_index) or (not self.use_distributed):
-            return function
-        return do_nothing
+            return lambda fn: self.on_process(fn, process_index=process_index)
+        return self._selected(self.process_index == process_index, function)
 
     def on_local_process(self, function: Callable[..., Any] | None = None, local_process_index: int | None = None):
         if function is None:
-            return partial(self.on_local_process, local_process_index=local_process_index)
-        if (self.local_process_index == local_process_index) or (not self.use_distributed):
-            return function
-        return do_nothing
+            return lambda fn: self.on_local_process(fn, local_process_index=local_process_index)
+        return self._selected(self.local_process_index == local_process_index, function)
 
     def print(self, *args, **kwargs):
+        """`print` on the local main process only."""
         if self.is_local_main_process:
             print(*args, **kwargs)
 
@@ -332,28 +335,14 @@ class PartialState:
             torch.distributed.destroy_process_group(group)
 
     def __getattr__(self, name: str):
-        if name in self._known_attrs:
-            raise AttributeError(
-                f"`PartialState` object has no attribute `{name}`. "
-                "This happens if `PartialState._reset_state()` was called and "
-                "an `Accelerator` or `PartialState` was not reinitialized."
-            )
-        raise AttributeError(f"'PartialState' object has no attribute '{name}'")
+        raise _missing_attribute("PartialState", name, self._known_attrs)
 
 
 class AcceleratorState:
     """Training-level singleton: mixed precision, plugins, and the promoted distributed type."""
 
     _shared_state = SharedDict()
-    _known_attrs = PartialState._known_attrs + [
-        "deepspeed_plugin",
-        "use_ipex",
-        "fsdp_plugin",
-        "megatron_lm_plugin",
-        "dynamo_plugin",
-        "parallelism_config",
-        "device_mesh",
-    ]
+    _known_attrs = _ACCELERATOR_ATTRS
 
     def __init__(
         self,
@@ -369,13 +358,12 @@ class AcceleratorState:
         **kwargs,
     ):
         self.__dict__ = self._shared_state
-        if parse_flag_from_env("ACCELERATE_USE_CPU"):
-            cpu = True
-        if PartialState._shared_state == {}:
-            PartialState(cpu, **kwargs)
+        cpu = cpu or parse_flag_from_env("ACCELERATE_USE_CPU")
+        PartialState(cpu, **kwargs)  # creates the process state once; later calls just share it
         self.__dict__.update(PartialState._shared_state)
-        self._check_initialized(mixed_precision, cpu)
-        if self.initialized and getattr(self, "_mixed_precision", None) is not None:
+        already_set_up = self.initialized and getattr(self, "_mixed_precision", None) is not None
+        if already_set_up:
+            self._check_initialized(mixed_precision, cpu)
             return
         self._cpu = cpu
         mixed_precision = (
@@ -430,16 +418,22 @@ class AcceleratorState:
         return self._shared_state != PartialState._shared_state
 
     def __repr__(self):
-        repr = PartialState().__repr__() + f"\nMixed precision type: {self.mixed_precision}\n"
-        return repr
+        return f"{PartialState()!r}\nMixed precision type: {self.mixed_precision}\n"
 
     def _check_initialized(self, mixed_precision=None, cpu=None):
-        if self.initialized and getattr(self, "_mixed_precision", None) is not None:
-            err = "AcceleratorState has already been initialized and cannot be changed, restart your runtime completely and pass `{flag}` to `Accelerator()`."
-            if cpu and self.device.type != "cpu":
-                raise ValueError(err.format(flag="cpu=True"))
-            if mixed_precision is not None and mixed_precision != self._mixed_precision:
-                raise ValueError(err.format(flag=f"mixed_precision='{mixed_precision}'"))
+        """A second Accelerator in the same process may not change the device kind or the precision."""
+        if not (self.initialized and getattr(self, "_mixed_precision", None) is not None):
+            return
+        conflict = None
+        if cpu and self.device.type != "cpu":
+            conflict = "cpu=True"
+        elif mixed_precision is not None and mixed_precision != self._mixed_precision:
+            conflict = f"mixed_precision='{mixed_precision}'"
+        if conflict:
+            raise ValueError(
+                "AcceleratorState has already been initialized and cannot be changed, restart your runtime completely "
+                f"and pass `{conflict}` to `Accelerator()`."
+            )
 
     @property
     def mixed_precision(self):
@@ -451,50 +445,16 @@ class AcceleratorState:
         if reset_partial_state:
             PartialState._reset_state()
 
-    def destroy_process_group(self, group=None):
-        PartialState().destroy_process_group(group)
-
-    @property
-    def fork_launched(self):
-        return PartialState().fork_launched
-
-    @property
-    def use_distributed(self):
-        return PartialState().use_distributed
-
     @property
     def is_fsdp2(self) -> bool:
         return self.distributed_type == DistributedType.FSDP and self.fsdp_plugin.fsdp_version == 2
 
-    @property
-    def is_last_process(self) -> bool:
-        return PartialState().is_last_process
-
-    @property
-    def is_main_process(self) -> bool:
-        return PartialState().is_main_process
-
-    @property
-    def is_local_main_process(self) -> bool:
-        return PartialState().is_local_main_process
-
-    def wait_for_everyone(self):
-        PartialState().wait_for_everyone()
-
-    @contextmanager
-    def split_between_processes(self, inputs, apply_padding: bool = False):
-        with PartialState().split_between_processes(inputs, apply_padding=apply_padding) as inputs:
-            yield inputs
-
-    @contextmanager
-    def main_process_first(self):
-        with PartialState().main_process_first():
-            yield
-
-    @contextmanager
-    def local_main_process_first(self):
-        with PartialState().local_main_process_first():
-            yield
+    # Process-level queries and helpers live on PartialState; AcceleratorState forwards them (see the loop after the
+    # class body) so both singletons answer the same questions the same way.
+    _FORWARDED_PROPERTIES = ("fork_launched", "use_distributed", "is_last_process", "is_main_process",
+                             "is_local_main_process")
+    _FORWARDED_METHODS = ("destroy_process_group", "wait_for_everyone", "split_between_processes",
+                          "main_process_first", "local_main_process_first", "print")
 
     @property
     def deepspeed_plugin(self):
@@ -514,50 +474,49 @@ class AcceleratorState:
             p.selected = key == name
         self.fsdp_plugin = self.deepspeed_plugins[name].to_fsdp_plugin()
 
-    def print(self, *args, **kwargs):
-        PartialState().print(*args, **kwargs)
-
     def __getattr__(self, name: str):
-        if name in self._known_attrs:
-            raise AttributeError(
-                f"`AcceleratorState` object has no attribute `{name}`. "
-                "This happens if `AcceleratorState._reset_state()` was called and "
-                "an `Accelerator` or `PartialState` was not reinitialized."
-            )
-        raise AttributeError(f"'AcceleratorState' object has no attribute '{name}'")
+        raise _missing_attribute("AcceleratorState", name, self._known_attrs)
+
+
+def _install_forwarders():
+    for _name in AcceleratorState._FORWARDED_PROPERTIES:
+        setattr(AcceleratorState, _name, property(lambda self, _n=_name: getattr(PartialState(), _n)))
+    for _name in AcceleratorState._FORWARDED_METHODS:
+        def _fwd(self, *args, _n=_name, **kwargs):
+            return getattr(PartialState(), _n)(*args, **kwargs)
+
+        _fwd.__name__ = _name
+        _fwd.__doc__ = getattr(PartialState, _name).__doc__
+        setattr(AcceleratorState, _name, _fwd)
+
+
+_install_forwarders()
 
 
 class GradientState:
-    """Gradient-accumulation bookkeeping shared by the Accelerator, dataloaders, optimizer, scheduler.
-
-    Parity: reference `state.py:1225-1365`.
-    """
+    """Gradient-accumulation bookkeeping shared by the Accelerator, dataloaders, optimizer and scheduler (reference
+    `state.py:1225-1365`): whether this step syncs gradients, the accumulation plugin's settings, and the stack of
+    dataloaders being iterated (weak references; the innermost one decides `end_of_dataloader` / `remainder`)."""
 
     _shared_state = SharedDict()
+    _PLUGIN_DEFAULTS = {"num_steps": 1, "adjust_scheduler": False, "sync_with_dataloader": True}
 
     def __init__(self, gradient_accumulation_plugin: GradientAccumulationPlugin | None = None):
         self.__dict__ = self._shared_state
+        settings = gradient_accumulation_plugin.to_kwargs() if gradient_accumulation_plugin is not None else None
         if not self.initialized:
             self.sync_gradients = True
             self._dataloader_references_ref = [None]
-            self.plugin_kwargs = (
-                gradient_accumulation_plugin.to_kwargs() if gradient_accumulation_plugin is not None else {}
-            )
-            self._is_xla_gradients_synced = False
-        if gradient_accumulation_plugin is not None and self.plugin_kwargs != gradient_accumulation_plugin.to_kwargs():
-            self.plugin_kwargs = gradient_accumulation_plugin.to_kwargs()
+            self.plugin_kwargs = settings or {}
+        elif settings is not None:
+            self.plugin_kwargs = settings  # a later plugin replaces the earlier settings
 
-    @property
-    def num_steps(self) -> int:
-        return self.plugin_kwargs.get("num_steps", 1)
+    def _setting(self, key):
+        return self.plugin_kwargs.get(key, self._PLUGIN_DEFAULTS[key])
 
-    @property
-    def adjust_scheduler(self) -> bool:
-        return self.plugin_kwargs.get("adjust_scheduler", False)
-
-    @property
-    def sync_with_dataloader(self) -> bool:
-        return self.plugin_kwargs.get("sync_with_dataloader", True)
+    num_steps = property(lambda self: self._setting("num_steps"))
+    adjust_scheduler = property(lambda self: self._setting("adjust_scheduler"))
+    sync_with_dataloader = property(lambda self: self._setting("sync_with_dataloader"))
 
     @property
     def initialized(self) -> bool:
@@ -574,23 +533,22 @@ class GradientState:
 
     @property
     def end_of_dataloader(self) -> bool:
-        if not self.in_dataloader:
-            return False
-        return self.active_dataloader.end_of_dataloader
+        dl = self.active_dataloader
+        return dl.end_of_dataloader if dl is not None else False
 
     @property
     def remainder(self) -> int:
-        if not self.in_dataloader:
-            return -1
-        return self.active_dataloader.remainder
+        dl = self.active_dataloader
+        return dl.remainder if dl is not None else -1
 
     def __repr__(self):
-        return (
-            f"Sync Gradients: {self.sync_gradients}\n"
-            f"At end of current dataloader: {self.end_of_dataloader}\n"
-            f"Extra samples added: {self.remainder}\n"
-            f"Gradient accumulation plugin: {self.plugin_kwargs}\n"
-        )
+        lines = [
+            ("Sync Gradients", self.sync_gradients),
+            ("At end of current dataloader", self.end_of_dataloader),
+            ("Extra samples added", self.remainder),
+            ("Gradient accumulation plugin", self.plugin_kwargs),
+        ]
+        return "".join(f"{k}: {v}\n" for k, v in lines)
 
     def _set_sync_gradients(self, sync_gradients):
         self.sync_gradients = sync_gradients
@@ -598,20 +556,19 @@ class GradientState:
     def _add_dataloader(self, dataloader):
         import weakref
 
-        self.dataloader_references.append(weakref.ref(dataloader))
+        self._dataloader_references_ref.append(weakref.ref(dataloader))
 
     def _remove_dataloader(self, dataloader):
-        refs = self.dataloader_references
-        for i in range(len(refs) - 1, -1, -1):
-            r = refs[i]
-            if r is not None and r() is dataloader:
-                refs.pop(i)
-                break
+        """Drop the innermost reference to `dataloader` (nested loops over one loader unwind one level)."""
+        refs = self._dataloader_references_ref
+        hit = next((i for i in reversed(range(len(refs))) if refs[i] is not None and refs[i]() is dataloader), None)
+        if hit is not None:
+            del refs[hit]
 
     @property
     def active_dataloader(self):
-        ref = self.dataloader_references[-1]
-        return ref() if ref is not None else None
+        ref = self._dataloader_references_ref[-1]
+        return None if ref is None else ref()
 
     @property
     def dataloader_references(self):

@@ -1,7 +1,7 @@
 """Pipeline-parallel inference of a Llama model: one stage per process, micro-batched (parity: reference
 examples/inference/pippy/llama.py, which splits a HF Llama with torch.distributed.pipelining).
 
-Here `prepare_pippy` (parallel/pipeline.py) cuts the decoder stack at `split_points` (or balances it, "auto"), each
+Here `prepare_pippy` (inference.py, runtime in parallel/pipeline.py) cuts the decoder stack at `split_points` (or balances it, "auto"), each
 rank materialises only its own stage, and activations move stage to stage over point-to-point sends (RCCL on GPUs,
 gloo on CPU). Weights are random-init (offline); the example checks the staged logits against the unsplit model.
 
