@@ -10,6 +10,7 @@
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include "common.h"
+#include <cstdlib>
 
 using namespace acc;
 
@@ -483,16 +484,69 @@ torch::Tensor rope_out(torch::Tensor src, torch::Tensor cos, torch::Tensor sin, 
 }
 
 // ------------------------------------------------------------------------------------------------ transpose
-// out[c, r] = in[r, c] for a row-major bf16 [R, C] with R, C multiples of 64: 64x64 tile per 256-thread workgroup,
-// 16-B global loads and stores on both sides, the turn done through a padded LDS tile (row pitch 72 elements).
-// Used to hand the weight-gradient GEMM a token-contiguous copy of the layer input (parallel/fsdp.py), which moves
-// that GEMM from the slow both-token-major layout to the dgrad-class layout.
+// out[c, r] = in[r, c] for a row-major bf16 [R, C]. Used to hand the weight-gradient GEMM a token-contiguous copy of
+// the layer input (parallel/fsdp.py), which moves that GEMM from the slow both-token-major layout to the
+// dgrad-class layout, and for the MoE expert stacks.
+//
+// 128 x 128 tile per 256-thread workgroup (R, C multiples of 128): every thread moves 8 rows x 16 B in (coalesced
+// 256-B row segments), the tile sits in LDS as 256-B rows with the 16-B chunk XOR-swizzled by the row's 8-row block,
+// then every thread takes one 8 x 8 block back with eight ds_read_b128 (conflict-free under the swizzle), turns it in
+// registers (v_perm) and writes eight 16-B pieces; the 16 threads sharing an output row write 256 contiguous bytes.
+// R or C not a multiple of 128 (but of 64) take the 64 x 64 LDS-element kernel below.
 namespace {
+__device__ __forceinline__ unsigned lo_pair(unsigned a, unsigned b) { return __builtin_amdgcn_perm(b, a, 0x05040100u); }
+__device__ __forceinline__ unsigned hi_pair(unsigned a, unsigned b) { return __builtin_amdgcn_perm(b, a, 0x07060302u); }
+
+__global__ __launch_bounds__(256) void transpose128_bf16_kernel(const bf16_t* __restrict__ in, bf16_t* __restrict__ out,
+                                                                int R, int C) {
+  __shared__ __attribute__((aligned(16))) uint4 tile[128 * 16];  // 128 rows x 16 chunks of 16 B
+  const int tid = threadIdx.x;
+  const long tr = (long)blockIdx.y * 128, tc = (long)blockIdx.x * 128;
+  in += (long)blockIdx.z * R * C;  // batched [E, R, C] -> [E, C, R]
+  out += (long)blockIdx.z * R * C;
+  // load: thread -> chunk (tid & 15) of rows (tid >> 4) + 16 p
+  {
+    const int ch = tid & 15;
+    uint4 v[8];
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const int row = (tid >> 4) + 16 * p;
+      v[p] = *reinterpret_cast<const uint4*>(in + (tr + row) * C + tc + ch * 8);
+    }
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const int row = (tid >> 4) + 16 * p;
+      tile[row * 16 + (ch ^ ((row >> 3) & 15))] = v[p];
+    }
+  }
+  __syncthreads();
+  // turn: thread -> 8 x 8 block (row block rb, column chunk cb); lanes with consecutive rb share an output row
+  const int rb = tid & 15, cb = tid >> 4;
+  unsigned x[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint4 t = tile[(rb * 8 + i) * 16 + (cb ^ rb)];
+    x[i][0] = t.x; x[i][1] = t.y; x[i][2] = t.z; x[i][3] = t.w;
+  }
+  // output row j = column cb*8 + j: elements x[0..7][j]; dword k packs rows 2k, 2k+1
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    uint4 w;
+    unsigned d[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      d[k] = (j & 1) ? hi_pair(x[2 * k][j >> 1], x[2 * k + 1][j >> 1]) : lo_pair(x[2 * k][j >> 1], x[2 * k + 1][j >> 1]);
+    w.x = d[0]; w.y = d[1]; w.z = d[2]; w.w = d[3];
+    *reinterpret_cast<uint4*>(out + (tc + cb * 8 + j) * R + tr + rb * 8) = w;
+  }
+}
+
+// 64 x 64 fallback: the turn done element-wise through a padded LDS tile (row pitch 72 elements).
 __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16_t* __restrict__ in, bf16_t* __restrict__ out, int R,
                                                              int C) {
   __shared__ __attribute__((aligned(16))) bf16_t tile[64][72];
   const int tr = blockIdx.y * 64, tc = blockIdx.x * 64, tid = threadIdx.x, ch = tid & 7;
-  in += (long)blockIdx.z * R * C;  // batched [E, R, C] -> [E, C, R]
+  in += (long)blockIdx.z * R * C;
   out += (long)blockIdx.z * R * C;
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
@@ -519,7 +573,12 @@ torch::Tensor transpose_bf16(torch::Tensor x) {
   TORCH_CHECK(R % 64 == 0 && C % 64 == 0, "transpose_bf16: both dims must be multiples of 64");
   auto out = x.dim() == 3 ? torch::empty({E, C, R}, x.options()) : torch::empty({C, R}, x.options());
   if (x.numel() == 0) return out;
-  hipLaunchKernelGGL(transpose_bf16_kernel, dim3(C / 64, R / 64, E), dim3(256), 0, at::hip::getCurrentHIPStream(),
-                     reinterpret_cast<const bf16_t*>(x.data_ptr()), reinterpret_cast<bf16_t*>(out.data_ptr()), R, C);
+  static const bool use128 = [] { const char* e = std::getenv("ACCELERATE_TRANSPOSE128"); return !e || e[0] != '0'; }();
+  if (use128 && R % 128 == 0 && C % 128 == 0)
+    hipLaunchKernelGGL(transpose128_bf16_kernel, dim3(C / 128, R / 128, E), dim3(256), 0, at::hip::getCurrentHIPStream(),
+                       reinterpret_cast<const bf16_t*>(x.data_ptr()), reinterpret_cast<bf16_t*>(out.data_ptr()), R, C);
+  else
+    hipLaunchKernelGGL(transpose_bf16_kernel, dim3(C / 64, R / 64, E), dim3(256), 0, at::hip::getCurrentHIPStream(),
+                       reinterpret_cast<const bf16_t*>(x.data_ptr()), reinterpret_cast<bf16_t*>(out.data_ptr()), R, C);
   return out;
 }

@@ -6,11 +6,15 @@ the same op (the reference is also the numerics oracle in tests/test_kernels_gpu
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
 
 from ._ext import ext, use_native
+
+# dgrad through a transposed weight copy (ACCELERATE_DGRAD_WT=0 turns it off)
+_DGRAD_WT = os.environ.get("ACCELERATE_DGRAD_WT", "1") != "0"
 
 
 # ----------------------------------------------------------------------------------------------------------
@@ -326,3 +330,18 @@ def cross_entropy(logits: torch.Tensor, labels: torch.Tensor, ignore_index: int 
     return torch.nn.functional.cross_entropy(
         logits.reshape(-1, logits.shape[-1]).float(), labels.reshape(-1), ignore_index=ignore_index
     )
+
+
+def linear_dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """dx = dy2 · W for a Linear's weight W [N, K] and output gradient dy2 [T, N].
+
+    hipBLASLt's gfx950 kernels for this product in its natural layout (both operands row-major, the NN class) ran at
+    1.35 PF/s in the Llama-3-8B step, its forward-class kernels (TN: the second operand contraction-contiguous) at
+    1.54 PF/s. So on the native path W is first turned into a contiguous Wᵀ by the HIP transpose (4.6-6.7 TB/s,
+    tools/bench_transpose.py; 436 MB of weights per Llama-3-8B layer ≈ 0.15 ms) and dx = linear(dy2, Wᵀ) runs in the
+    forward's layout: 1.1-1.5 % faster end to end on one MI355X (gpu_steps.sh bench8b vs bench8b_dgradwt, two
+    boxes). The copy is transient (freed as soon as the GEMM is enqueued)."""
+    if (_DGRAD_WT and dy2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and w.is_contiguous()
+            and w.shape[0] % 64 == 0 and w.shape[1] % 64 == 0 and use_native(dy2)):
+        return torch.nn.functional.linear(dy2, ext().transpose_bf16(w))
+    return dy2 @ w

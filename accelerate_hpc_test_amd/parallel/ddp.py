@@ -34,6 +34,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..ops._ext import ext, use_native
+from ..ops.fused import linear_dgrad
 from ..utils.dataclasses import DDPCommunicationHookType
 from ..utils.fault_tolerance import record_collective
 from ..utils.tracing import trace_range
@@ -104,8 +105,8 @@ class _DDPFusedLinearFn(torch.autograd.Function):
         xs, wc = ctx.saved_tensors
         N, K = wc.shape
         dy = dy.to(wc.dtype)
-        dx = (dy @ wc).to(ctx.xdtype) if ctx.needs_input_grad[0] else None
         dy2 = dy.reshape(-1, N)
+        dx = linear_dgrad(dy2, wc).view(*dy.shape[:-1], K).to(ctx.xdtype) if ctx.needs_input_grad[0] else None
         ddp = ctx.slot.ddp()
         if ddp is not None:
             ddp._fused_wgrad(ctx.slot, dy2, xs.t() if ctx.x_t else xs)

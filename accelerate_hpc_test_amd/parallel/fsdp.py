@@ -51,6 +51,7 @@ from ..utils.fault_tolerance import record_collective
 from ..utils.tracing import trace_range
 from ..ops._ext import ext, native_enabled
 from ..ops.fp8 import Fp8Linear
+from ..ops.fused import linear_dgrad
 from . import small_allreduce
 
 _ALIGN = 64  # elements; keeps every rank's shard 128-B aligned for bf16 / 256-B for fp32
@@ -1463,8 +1464,10 @@ class _FusedWgradLinearFn(torch.autograd.Function):
     def backward(ctx, dy):
         xs, w = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1])
-        dx = (dy2 @ w).view(*dy.shape[:-1], w.shape[1]) if ctx.needs_input_grad[0] else None
+        dx = linear_dgrad(dy2, w).view(*dy.shape[:-1], w.shape[1]) if ctx.needs_input_grad[0] else None
         db = dy2.sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        # (A contiguous dyᵀ as the left operand as well — both operands contraction-contiguous — measured no faster
+        # end to end: the transpose of dy costs what the GEMM gains.)
         if ctx.x_transposed:
             ctx.slot.engine._fused_wgrad(ctx.slot, dy2, xs.t())  # [T, K] view of the token-contiguous copy
         else:

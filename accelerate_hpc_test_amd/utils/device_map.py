@@ -71,6 +71,16 @@ def get_module_leaves(module_sizes: dict) -> list:
     return [name for name in module_sizes if name and name not in parents]
 
 
+def _class_names(classes) -> list:
+    """`no_split_module_classes` as a list of class names: None, one name, or any collection of names (transformers 5
+    declares `_no_split_modules` as a set)."""
+    if classes is None:
+        return []
+    if isinstance(classes, str):
+        return [classes]
+    return sorted(classes) if isinstance(classes, (set, frozenset)) else list(classes)
+
+
 def _class_sizes(model: nn.Module, module_sizes: dict, classes: list) -> dict:
     """Size of the first module of each class in `classes`, in `module_sizes` order."""
     wanted, found = set(classes), {}
@@ -119,11 +129,8 @@ def get_balanced_memory(
     sizes = compute_module_sizes(model, dtype=dtype, special_dtypes=special_dtypes)
     share = sizes[""] // (len(gpus) - 1 if low_zero else len(gpus))
 
-    if no_split_module_classes is None:
-        no_split_module_classes = []
-    elif not isinstance(no_split_module_classes, (list, tuple)):
-        no_split_module_classes = [no_split_module_classes]
-    block = max(_class_sizes(model, sizes, list(no_split_module_classes)).values(), default=0)
+    no_split_module_classes = _class_names(no_split_module_classes)
+    block = max(_class_sizes(model, sizes, no_split_module_classes).values(), default=0)
     # innermost modules: drop the leaf tensors first, then the leaves of what remains are the last modules
     tensor_leaves = set(get_module_leaves(sizes))
     module_only = {n: v for n, v in sizes.items() if n not in tensor_leaves}
@@ -229,11 +236,7 @@ class DeviceMapPlanner:
                  verbose=False, offload_buffers=False, fallback_allocation=False):
         self.model = model
         self.budget = get_max_memory(max_memory)
-        if no_split_module_classes is None:
-            no_split_module_classes = []
-        elif not isinstance(no_split_module_classes, (list, tuple)):
-            no_split_module_classes = [no_split_module_classes]
-        self.no_split = list(no_split_module_classes)
+        self.no_split = _class_names(no_split_module_classes)
         self.devices = list(self.budget) + ([] if "disk" in self.budget else ["disk"])
         gpus = [d for d in self.devices if d not in ("cpu", "disk")]
         self.gpus = gpus

@@ -678,11 +678,14 @@ def test_fp8_amax_large_and_ragged(n):
     assert fp8.amax(x).item() == x.float().abs().max().item()
 
 
-def test_transpose_bf16_matches_torch():
+@pytest.mark.parametrize("shape", [(8192 + 64, 448), (1024, 384), (256, 28672), (3, 384, 640), (14336, 128)])
+def test_transpose_bf16_matches_torch(shape):
+    """Both transpose kernels: 128x128 register-turn tiles (both dims multiples of 128) and the 64x64 fallback;
+    2-D and batched 3-D; bit-exact against torch."""
     from accelerate_hpc_test_amd.ops._ext import ext
 
-    x = torch.randn(8192 + 64, 448, device=DEV, dtype=torch.bfloat16)
-    assert torch.equal(ext().transpose_bf16(x), x.t().contiguous())
+    x = torch.randn(shape, device=DEV, dtype=torch.bfloat16)
+    assert torch.equal(ext().transpose_bf16(x), x.transpose(-1, -2).contiguous())
 
 
 @pytest.mark.parametrize("direct", [True, False])

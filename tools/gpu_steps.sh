@@ -29,6 +29,10 @@ for step in "$@"; do
     tests) run tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench8b) run bench8b 600 python bench.py --steps 5 --warmup 2 $BENCH_ARGS ;;
+    bench8b_nodgradwt) ACCELERATE_DGRAD_WT=0 run bench8b_nodgradwt 600 python bench.py --steps 5 --warmup 2 $BENCH_ARGS ;;
+    transpose) run transpose 300 python tools/bench_transpose.py && ACCELERATE_TRANSPOSE128=0 run transpose_old 300 python tools/bench_transpose.py ;;
+    ktest) run ktest 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "${KTEST:-transpose}" ;;
+    wgrad_layout) run wgrad_layout 300 python tools/bench_wgrad_layout.py ;;
     bench8b_noblaslt) ACCELERATE_BLASLT_WGRAD=0 run bench8b_noblaslt 600 python bench.py --steps 5 --warmup 2 $BENCH_ARGS ;;
     bench8b_nooverlap) run bench8b_nooverlap 600 python bench.py --steps 5 --warmup 2 --optimizer-overlap off $BENCH_ARGS ;;
     bench8b_sharded) run bench8b_sharded 600 python bench.py --steps 5 --warmup 2 --fsdp-force-sharded $BENCH_ARGS ;;
@@ -53,6 +57,12 @@ for step in "$@"; do
     attn_long) run attn_long 300 python tools/bench_attn.py --S 32768 --iters 3 ;;
     pmc_attn) run pmc_attn 200 bash tools/pmc_attn.sh ;;
     gemm) run gemm 300 python tools/bench_gemm.py ;;
+    gen_gptj) run gen_gptj 600 python tools/bench_generate.py --model gpt-j-6b ;;
+    gen_neox) run gen_neox 600 python tools/bench_generate.py --model gpt-neox-20b --keep-ckpt ;;
+    gen_neox_offload) run gen_neox_offload 600 python tools/bench_generate.py --model gpt-neox-20b --gpu-mem 20GiB ;;
+    gen_opt30b_offload) run gen_opt30b_offload 900 python tools/bench_generate.py --model opt-30b --gpu-mem 46GiB ;;
+    gen_neox_disk) run gen_neox_disk 900 python tools/bench_generate.py --model gpt-neox-20b --gpu-mem 14GiB --cpu-mem 10GiB --disk-offload ;;
+    gen_llama70b) run gen_llama70b 900 python tools/bench_generate.py --model llama3-70b --dtype bf16 ;;
     big70b) run big70b 900 python tools/bench_big_model.py --model llama3-70b --tokens 2048 --iters 3 ;;
     big70b_offload) run big70b_offload 900 python tools/bench_big_model.py --model llama3-70b --gpu-mem 100GiB --tokens 2048 --iters 3 ;;
     *) echo "unknown step $step"; exit 2 ;;
