@@ -8,6 +8,8 @@
 // call of each (T, N, K) asks hipBLASLt for its candidate algorithms, times them on a scratch output, and caches the
 // fastest; every later call is one hipblasLtMatmul on the current HIP stream. Column-major view used for the call:
 //   D (K x N, ld K) = X (K x T, ld K, op N) . DY^T (DY: N x T, ld N, op T), beta = accumulate ? 1 : 0.
+// With `x_t` the layer input arrives as its token-contiguous copy xT [K, T] (the FSDP / DDP engines keep that copy
+// for this GEMM): X is then the column-major T x K matrix (ld T) taken with op T.
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include <hip/hip_runtime.h>
@@ -35,7 +37,7 @@ struct Plan {
 struct State {
   hipblasLtHandle_t handle = nullptr;
   torch::Tensor workspace;
-  std::map<std::tuple<int64_t, int64_t, int64_t, int>, Plan> plans;
+  std::map<std::tuple<int64_t, int64_t, int64_t, int, bool>, Plan> plans;
   std::mutex mu;
 };
 
@@ -46,12 +48,14 @@ State& state() {
 
 bool check(hipblasStatus_t st) { return st == HIPBLAS_STATUS_SUCCESS; }
 
-bool build_plan(State& s, Plan& p, int64_t T, int64_t N, int64_t K, hipStream_t stream, const torch::Tensor& like) {
-  const hipblasOperation_t ta = HIPBLAS_OP_N, tb = HIPBLAS_OP_T;
+bool build_plan(State& s, Plan& p, int64_t T, int64_t N, int64_t K, bool x_t, hipStream_t stream,
+                const torch::Tensor& like) {
+  const hipblasOperation_t ta = x_t ? HIPBLAS_OP_T : HIPBLAS_OP_N, tb = HIPBLAS_OP_T;
   if (!check(hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F))) return false;
   if (!check(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta)))) return false;
   if (!check(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb)))) return false;
-  if (!check(hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16BF, K, T, K))) return false;
+  if (!check(x_t ? hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16BF, T, K, T)
+                 : hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16BF, K, T, K))) return false;
   if (!check(hipblasLtMatrixLayoutCreate(&p.lb, HIP_R_16BF, N, T, N))) return false;
   if (!check(hipblasLtMatrixLayoutCreate(&p.lc, HIP_R_32F, K, N, K))) return false;
   hipblasLtMatmulPreference_t pref;
@@ -102,14 +106,14 @@ bool build_plan(State& s, Plan& p, int64_t T, int64_t N, int64_t K, hipStream_t 
 }  // namespace
 
 // Returns false (and does nothing) when hipBLASLt offers no working algorithm: the caller falls back to torch.
-bool blaslt_wgrad_f32(torch::Tensor dy, torch::Tensor x, torch::Tensor out, bool accumulate) {
+bool blaslt_wgrad_f32(torch::Tensor dy, torch::Tensor x, torch::Tensor out, bool accumulate, bool x_t) {
   TORCH_CHECK(dy.is_cuda() && x.is_cuda() && out.is_cuda(), "blaslt_wgrad_f32: HIP tensors expected");
   TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16 && out.scalar_type() == at::kFloat,
               "blaslt_wgrad_f32: bf16 operands and an fp32 output expected");
   TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && out.dim() == 2 && dy.is_contiguous() && x.is_contiguous() && out.is_contiguous(),
               "blaslt_wgrad_f32: 2-D contiguous tensors expected");
-  const int64_t T = dy.size(0), N = dy.size(1), K = x.size(1);
-  TORCH_CHECK(x.size(0) == T && out.size(0) == N && out.size(1) == K, "blaslt_wgrad_f32: shape mismatch");
+  const int64_t T = dy.size(0), N = dy.size(1), K = x_t ? x.size(0) : x.size(1);
+  TORCH_CHECK((x_t ? x.size(1) : x.size(0)) == T && out.size(0) == N && out.size(1) == K, "blaslt_wgrad_f32: shape mismatch");
   State& s = state();
   hipStream_t stream = at::hip::getCurrentHIPStream();
   Plan* plan = nullptr;
@@ -120,11 +124,11 @@ bool blaslt_wgrad_f32(torch::Tensor dy, torch::Tensor x, torch::Tensor out, bool
       s.workspace = torch::empty({(int64_t)kWorkspace}, out.options().dtype(torch::kUInt8));
     }
     const int dev = out.get_device();
-    auto key = std::make_tuple(T, N, K, dev);
+    auto key = std::make_tuple(T, N, K, dev, x_t);
     auto it = s.plans.find(key);
     if (it == s.plans.end()) {
       Plan p;
-      build_plan(s, p, T, N, K, stream, out);
+      build_plan(s, p, T, N, K, x_t, stream, out);
       it = s.plans.emplace(key, p).first;
     }
     plan = &it->second;

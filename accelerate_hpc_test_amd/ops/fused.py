@@ -15,6 +15,8 @@ from ._ext import ext, use_native
 
 # dgrad through a transposed weight copy (ACCELERATE_DGRAD_WT=0 turns it off)
 _DGRAD_WT = os.environ.get("ACCELERATE_DGRAD_WT", "1") != "0"
+# fp32-output weight-gradient GEMMs through the searched hipBLASLt runner (csrc/runtime/blaslt_gemm.cpp)
+_BLASLT_WGRAD = os.environ.get("ACCELERATE_BLASLT_WGRAD", "1") != "0"
 
 
 # ----------------------------------------------------------------------------------------------------------
@@ -345,3 +347,28 @@ def linear_dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
             and w.shape[0] % 64 == 0 and w.shape[1] % 64 == 0 and use_native(dy2)):
         return torch.nn.functional.linear(dy2, ext().transpose_bf16(w))
     return dy2 @ w
+
+
+def wgrad_into(dest: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, accumulate: bool) -> None:
+    """dest (+)= dy2ᵀ · x2: a Linear's weight gradient written by the GEMM itself into its engine slot (FSDP flat grad
+    buffer / fp32 grad shard, DDP bucket). x2 is [T, K], token-major contiguous or the transposed view of the
+    token-contiguous copy xᵀ the engines save. An fp32 `dest` takes the searched hipBLASLt runner when enabled
+    (torch's fp32-output GEMM only reaches hipBLASLt's default heuristic), else torch."""
+    a, b = dy2.t(), x2
+    if b.dtype != a.dtype:
+        b = b.to(a.dtype)
+    if dest.dtype == a.dtype:
+        dest.addmm_(a, b) if accumulate else torch.mm(a, b, out=dest)
+    elif dest.is_cuda and dest.dtype == torch.float32:
+        if _BLASLT_WGRAD and a.dtype == torch.bfloat16 and dy2.is_contiguous():
+            if b.is_contiguous() and ext().blaslt_wgrad_f32(dy2, b, dest, accumulate, False):
+                return
+            if b.t().is_contiguous() and ext().blaslt_wgrad_f32(dy2, b.t(), dest, accumulate, True):
+                return
+        if accumulate:
+            torch.addmm(dest, a, b, out_dtype=torch.float32, out=dest)
+        else:
+            torch.mm(a, b, out_dtype=torch.float32, out=dest)
+    else:
+        g = (a.float() @ b.float()).to(dest.dtype)
+        dest.add_(g) if accumulate else dest.copy_(g)

@@ -34,7 +34,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..ops._ext import ext, use_native
-from ..ops.fused import linear_dgrad
+from ..ops.fused import linear_dgrad, wgrad_into
 from ..utils.dataclasses import DDPCommunicationHookType
 from ..utils.fault_tolerance import record_collective
 from ..utils.tracing import trace_range
@@ -290,14 +290,7 @@ class DistributedDataParallel(nn.Module):
             view.copy_(p.grad)
             p.grad = view
         acc = p.grad is not None  # torch semantics: accumulate unless zero_grad set the grad to None
-        a = dy2.t()
-        if view.dtype == a.dtype:
-            view.addmm_(a, x2) if acc else torch.mm(a, x2, out=view)
-        elif view.is_cuda and view.dtype == torch.float32:
-            torch.addmm(view, a, x2, out_dtype=torch.float32, out=view) if acc else torch.mm(a, x2, out_dtype=torch.float32, out=view)
-        else:
-            g = (a.float() @ x2.float()).to(view.dtype)
-            view.add_(g) if acc else view.copy_(g)
+        wgrad_into(view, dy2, x2, acc)
         p.grad = view
         slot.uses -= 1
         if slot.uses <= 0:

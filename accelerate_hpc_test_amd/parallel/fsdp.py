@@ -51,13 +51,12 @@ from ..utils.fault_tolerance import record_collective
 from ..utils.tracing import trace_range
 from ..ops._ext import ext, native_enabled
 from ..ops.fp8 import Fp8Linear
-from ..ops.fused import linear_dgrad
+from ..ops.fused import linear_dgrad, wgrad_into
 from . import small_allreduce
 
 _ALIGN = 64  # elements; keeps every rank's shard 128-B aligned for bf16 / 256-B for fp32
 # opt-in: on MI355X the searched algorithms measured 0.3-0.6 % slower end to end than torch's default pick (interleaved A/B,
 # profiles/r1_session3_benches.json), so the torch path stays the default
-_BLASLT_WGRAD = os.environ.get("ACCELERATE_BLASLT_WGRAD", "0") == "1"
 _WGRAD_XT = os.environ.get("ACCELERATE_FSDP_WGRAD_XT", "1") != "0"
 
 
@@ -838,20 +837,7 @@ class FSDPEngine:
         """dW = dy2ᵀ · x2 written into the unit's flat grad buffer (or fp32 grad shard at world size 1); counts as the
         parameter's grad-ready event."""
         dest, acc = self._fused_slot_dest(slot)
-        a, b = dy2.t(), x2
-        if a.dtype != b.dtype:
-            b = b.to(a.dtype)
-        if dest.dtype == a.dtype:
-            dest.addmm_(a, b) if acc else torch.mm(a, b, out=dest)
-        elif dest.is_cuda and dest.dtype == torch.float32:
-            # hipBLASLt with a per-shape algorithm search (csrc/runtime/blaslt_gemm.cpp); torch's fp32-output path
-            # only reaches hipBLASLt's default heuristic
-            if not (_BLASLT_WGRAD and a.dtype == torch.bfloat16 and dy2.is_contiguous() and x2.is_contiguous()
-                    and ext().blaslt_wgrad_f32(dy2, x2 if x2.dtype == a.dtype else b, dest, acc)):
-                torch.addmm(dest, a, b, out_dtype=torch.float32, out=dest) if acc else torch.mm(a, b, out_dtype=torch.float32, out=dest)
-        else:
-            g = (a @ b).to(dest.dtype)
-            dest.add_(g) if acc else dest.copy_(g)
+        wgrad_into(dest, dy2, x2, acc)
         self._fused_slot_done(slot)
 
     def _make_grad_hook(self, unit: FlatUnit):
@@ -1451,8 +1437,7 @@ class _FusedWgradLinearFn(torch.autograd.Function):
         # the producing RMSNorm / SwiGLU), but o_proj's input is the attention output that flash attention also keeps,
         # so there the copy is extra: T x 4096 bf16 = 64 MiB per layer, 2 GiB for Llama-3-8B at 8k tokens (peak
         # 175 of 288 GiB; kept for the faster layout). ACCELERATE_FSDP_WGRAD_XT=0 disables it. The opt-in hipBLASLt
-        # wgrad runner (ACCELERATE_BLASLT_WGRAD=1) takes contiguous [T, K] inputs only, so it is bypassed (torch's GEMM
-        # runs) whenever the transposed copy is in use.
+        # wgrad runner (ACCELERATE_BLASLT_WGRAD=1) takes either layout (ops/fused.py wgrad_into).
         ctx.x_transposed = (_WGRAD_XT and x2.is_cuda and x2.dtype == torch.bfloat16 and x2.is_contiguous() and native_enabled()
                             and x2.shape[0] % 64 == 0 and x2.shape[1] % 64 == 0)
         ctx.save_for_backward(ext().transpose_bf16(x2) if ctx.x_transposed else x, weight)

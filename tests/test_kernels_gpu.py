@@ -646,6 +646,12 @@ def test_blaslt_wgrad_f32_matches_torch(T, N, K):
     assert ext().blaslt_wgrad_f32(dy, x, out, True)
     assert _rel(out, 2 * ref) < 1e-3
     assert any(p[:3] == (T, N, K) and p[4] > 0 for p in ext().blaslt_wgrad_plans())
+    # the layer input as its token-contiguous copy xT [K, T] (the engines' saved layout)
+    xt = x.t().contiguous()
+    assert ext().blaslt_wgrad_f32(dy, xt, out, False, True)
+    assert _rel(out, ref) < 1e-3, _rel(out, ref)
+    assert ext().blaslt_wgrad_f32(dy, xt, out, True, True)
+    assert _rel(out, 2 * ref) < 1e-3
 
 
 @pytest.mark.parametrize("precision", ["bf16", "fp8"])

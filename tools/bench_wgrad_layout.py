@@ -35,9 +35,10 @@ for name, (N, K) in {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 
     trdy = tm(lambda: dy.t().contiguous())
     from accelerate_hpc_test_amd.ops._ext import ext
     bl = tm(lambda: ext().blaslt_wgrad_f32(dy, x, out, False))
+    blx = tm(lambda: ext().blaslt_wgrad_f32(dy, xT, out, False, True))
     ref = torch.mm(dy.t(), x, out_dtype=torch.float32)
     err = (torch.mm(dy.t(), xT.t(), out_dtype=torch.float32) - ref).abs().max().item()
     print(json.dumps({"gemm": name, "nt_ms": round(nt, 3), "nt_tflops": round(fl / nt / 1e9), "nn_ms": round(nn_, 3),
                       "nn_tflops": round(fl / nn_ / 1e9), "transpose_x_ms": round(tr, 3), "nt_bf16_ms": round(nt16, 3), "nn_bf16_ms": round(nn16, 3), "tt_ms": round(tt, 3), "tt_tflops": round(fl / tt / 1e9),
-                      "tt_bf16_ms": round(tt16, 3), "transpose_dy_ms": round(trdy, 3), "blaslt_search_nt_ms": round(bl, 3),
+                      "tt_bf16_ms": round(tt16, 3), "transpose_dy_ms": round(trdy, 3), "blaslt_search_nt_ms": round(bl, 3), "blaslt_search_xt_ms": round(blx, 3),
                       "max_abs_diff": err}), flush=True)

@@ -34,6 +34,7 @@ for step in "$@"; do
     ktest) run ktest 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "${KTEST:-transpose}" ;;
     wgrad_layout) run wgrad_layout 300 python tools/bench_wgrad_layout.py ;;
     bench8b_noblaslt) ACCELERATE_BLASLT_WGRAD=0 run bench8b_noblaslt 600 python bench.py --steps 5 --warmup 2 $BENCH_ARGS ;;
+    bench8b_blaslt) ACCELERATE_BLASLT_WGRAD=1 run bench8b_blaslt 600 python bench.py --steps 5 --warmup 2 $BENCH_ARGS ;;
     bench8b_nooverlap) run bench8b_nooverlap 600 python bench.py --steps 5 --warmup 2 --optimizer-overlap off $BENCH_ARGS ;;
     bench8b_sharded) run bench8b_sharded 600 python bench.py --steps 5 --warmup 2 --fsdp-force-sharded $BENCH_ARGS ;;
     prof8b_sharded) OVERLAP_PATTERN="nccl|rccl|copyBuffer" PROF_EXTRA=--memory-copy-trace prof prof8b_sharded 600 bench.py --steps 3 --warmup 2 --fsdp-force-sharded $BENCH_ARGS ;;
