@@ -54,7 +54,7 @@ for step in "$@"; do
     prof_mixtral_fp8) prof prof_mixtral_fp8 600 bench.py --model mixtral-8x7b-4l --steps 2 --warmup 1 --precision fp8 ;;
     prof_mixtral_bf16) prof prof_mixtral_bf16 600 bench.py --model mixtral-8x7b-4l --steps 2 --warmup 1 ;;
     moetests) run moetests 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "grouped or moe or transpose" ;;
-    attn) run attn 300 python tools/bench_attn.py ;;
+    attn) run attn 300 python tools/bench_attn.py --no-sdpa ;;
     attn_long) run attn_long 300 python tools/bench_attn.py --S 32768 --iters 3 ;;
     pmc_attn) run pmc_attn 200 bash tools/pmc_attn.sh ;;
     gemm) run gemm 300 python tools/bench_gemm.py ;;
