@@ -34,77 +34,31 @@ def _has(mod: str) -> bool:
 
 
 # ------------------------------------------------------------------------------------------------ availability
-def is_boto3_available():
-    return _has("boto3")
+# Probes of optional libraries report the truth for this environment; probes of other vendors' devices / libraries
+# (NVML, Moore Threads MUSA, Tecorigin SDAA, Intel XCCL, Habana, bitsandbytes, SageMaker) are constant False here.
+_PROBED_MODULES = {
+    "is_boto3_available": "boto3", "is_matplotlib_available": "matplotlib", "is_pytest_available": "pytest",
+    "is_torchvision_available": "torchvision", "is_torchdata_available": "torchdata",
+    "is_schedulefree_available": "schedulefree", "is_lomo_available": "lomo_optim",
+    "is_import_timer_available": "import_timer",
+    "is_triton_available": "triton",  # reported, never dispatched to
+}
+_NEVER_AVAILABLE = (
+    "is_pynvml_available", "is_sagemaker_available", "is_musa_available", "is_sdaa_available", "is_xccl_available",
+    "is_habana_gaudi1", "is_4bit_bnb_available", "is_8bit_bnb_available", "is_bitsandbytes_multi_backend_available",
+)
 
 
-def is_matplotlib_available():
-    return _has("matplotlib")
+def _make_probe(name: str, module: Optional[str]):
+    def probe(*_args, **_kwargs):
+        return module is not None and _has(module)
+
+    probe.__name__ = probe.__qualname__ = name
+    return probe
 
 
-def is_pytest_available():
-    return _has("pytest")
-
-
-def is_torchvision_available():
-    return _has("torchvision")
-
-
-def is_torchdata_available():
-    return _has("torchdata")
-
-
-def is_schedulefree_available():
-    return _has("schedulefree")
-
-
-def is_lomo_available():
-    return _has("lomo_optim")
-
-
-def is_import_timer_available():
-    return _has("import_timer")
-
-
-def is_triton_available():
-    """Reports the truth; the framework never dispatches to Triton."""
-    return _has("triton")
-
-
-def is_pynvml_available():
-    return False  # NVIDIA management library: not on ROCm (rocm-smi / sysfs are used instead)
-
-
-def is_sagemaker_available():
-    return False
-
-
-def is_musa_available(check_device=False):
-    return False
-
-
-def is_sdaa_available(check_device=False):
-    return False
-
-
-def is_xccl_available():
-    return False
-
-
-def is_habana_gaudi1():
-    return False
-
-
-def is_4bit_bnb_available():
-    return False
-
-
-def is_8bit_bnb_available():
-    return False
-
-
-def is_bitsandbytes_multi_backend_available():
-    return False
+for _name, _module in list(_PROBED_MODULES.items()) + [(n, None) for n in _NEVER_AVAILABLE]:
+    globals()[_name] = _make_probe(_name, _module)
 
 
 def is_transformer_engine_mxfp8_available():
