@@ -94,7 +94,8 @@ void cpu_adam_step(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Ten
 bool blaslt_wgrad_f32(torch::Tensor dy, torch::Tensor x, torch::Tensor out, bool accumulate, bool x_t);
 std::vector<std::tuple<int64_t, int64_t, int64_t, int64_t, double>> blaslt_wgrad_plans();
 bool blaslt_fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor sa, torch::Tensor sb, double alpha, torch::Tensor out,
-                     bool accumulate);
+                     bool accumulate, bool dynamic);
+std::vector<int64_t> blaslt_fp8_dynamic_stats();
 std::vector<std::tuple<int64_t, int64_t, int64_t, int64_t, double>> blaslt_fp8_plans();
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -148,7 +149,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("x_t") = false);
   m.def("cpu_adam_step", &cpu_adam_step);
   m.def("blaslt_wgrad_plans", &blaslt_wgrad_plans);
-  m.def("blaslt_fp8_gemm", &blaslt_fp8_gemm, "per-tensor-scaled fp8 GEMM on hipBLASLt (C = alpha sa sb A B^T)");
+  m.def("blaslt_fp8_gemm", &blaslt_fp8_gemm, "per-tensor-scaled fp8 GEMM on hipBLASLt (C = alpha sa sb A B^T)",
+        pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("sa"), pybind11::arg("sb"), pybind11::arg("alpha"),
+        pybind11::arg("out"), pybind11::arg("accumulate"), pybind11::arg("dynamic") = false);
+  m.def("blaslt_fp8_dynamic_stats", &blaslt_fp8_dynamic_stats);
   m.def("blaslt_fp8_plans", &blaslt_fp8_plans);
   m.def("debug_status", &debug_status, "first failed device bounds check (id << 32 | line), 0 if none; clears it");
   m.def("debug_selftest", &debug_selftest);

@@ -14,6 +14,7 @@
 #include <ATen/hip/HIPContext.h>
 #include <hip/hip_runtime.h>
 #include <hipblaslt/hipblaslt.h>
+#include <hipblaslt/hipblaslt-ext.hpp>
 
 #include <cstdlib>
 #include <map>
@@ -36,7 +37,10 @@ struct Plan {
 
 struct State {
   hipblasLtHandle_t handle = nullptr;
-  torch::Tensor workspace;
+  torch::Tensor workspace;  // of the first stream that called
+  // one workspace per HIP stream: GEMMs enqueued on different streams (MoE experts spread over side streams) run
+  // concurrently, and a shared workspace would be written by both
+  std::map<hipStream_t, torch::Tensor> stream_ws;
   std::map<std::tuple<int64_t, int64_t, int64_t, int, bool>, Plan> plans;
   std::mutex mu;
 };
@@ -47,6 +51,18 @@ State& state() {
 }
 
 bool check(hipblasStatus_t st) { return st == HIPBLAS_STATUS_SUCCESS; }
+
+// Workspace of `stream` (call with s.mu held).
+void* workspace_for(State& s, hipStream_t stream, const torch::Tensor& like) {
+  auto it = s.stream_ws.find(stream);
+  if (it == s.stream_ws.end()) {
+    torch::Tensor ws = s.stream_ws.empty() && s.workspace.defined()
+                           ? s.workspace
+                           : torch::empty({(int64_t)kWorkspace}, like.options().dtype(torch::kUInt8));
+    it = s.stream_ws.emplace(stream, ws).first;
+  }
+  return it->second.data_ptr();
+}
 
 bool build_plan(State& s, Plan& p, int64_t T, int64_t N, int64_t K, bool x_t, hipStream_t stream,
                 const torch::Tensor& like) {
@@ -82,7 +98,7 @@ bool build_plan(State& s, Plan& p, int64_t T, int64_t N, int64_t K, bool x_t, hi
     if (res[i].state != HIPBLAS_STATUS_SUCCESS || res[i].workspaceSize > kWorkspace) continue;
     auto run = [&]() {
       return hipblasLtMatmul(s.handle, p.desc, &one, a.data_ptr(), p.la, b.data_ptr(), p.lb, &zero, d.data_ptr(), p.lc,
-                             d.data_ptr(), p.lc, &res[i].algo, s.workspace.data_ptr(), kWorkspace, stream);
+                             d.data_ptr(), p.lc, &res[i].algo, workspace_for(s, stream, like), kWorkspace, stream);
     };
     if (!check(run())) continue;
     hipEventRecord(e0, stream);
@@ -117,6 +133,7 @@ bool blaslt_wgrad_f32(torch::Tensor dy, torch::Tensor x, torch::Tensor out, bool
   State& s = state();
   hipStream_t stream = at::hip::getCurrentHIPStream();
   Plan* plan = nullptr;
+  void* ws = nullptr;
   {
     std::lock_guard<std::mutex> lk(s.mu);
     if (s.handle == nullptr) {
@@ -132,12 +149,12 @@ bool blaslt_wgrad_f32(torch::Tensor dy, torch::Tensor x, torch::Tensor out, bool
       it = s.plans.emplace(key, p).first;
     }
     plan = &it->second;
+    ws = workspace_for(s, stream, out);
   }
   if (!plan->ok) return false;
   const float one = 1.f, beta = accumulate ? 1.f : 0.f;
   return check(hipblasLtMatmul(s.handle, plan->desc, &one, x.data_ptr(), plan->la, dy.data_ptr(), plan->lb, &beta,
-                               out.data_ptr(), plan->lc, out.data_ptr(), plan->lc, &plan->algo, s.workspace.data_ptr(),
-                               kWorkspace, stream));
+                               out.data_ptr(), plan->lc, out.data_ptr(), plan->lc, &plan->algo, ws, kWorkspace, stream));
 }
 
 // ------------------------------------------------------------------------------------------------ fp8, per-tensor
@@ -157,12 +174,26 @@ struct F8Plan {
   bool ok = false;
   float ms = 0.f;
   int candidates = 0;
+  int64_t M = 0, K = 0;  // the problem the layouts (and the timed search) were built for
 };
 
+using F8Key = std::tuple<int64_t, int64_t, int64_t, int64_t, int64_t, int, int, int, int>;
+
 struct F8State {
-  // (M, N, K, lda, ldb, dtype A, dtype B, fp32 out, device)
-  std::map<std::tuple<int64_t, int64_t, int64_t, int64_t, int64_t, int, int, int, int>, F8Plan> plans;
+  // exact problems: (M, N, K, lda, ldb, dtype A, dtype B, fp32 out, device)
+  std::map<F8Key, F8Plan> plans;
+  // problems whose M or K changes from call to call (MoE expert segments): (M bucket, N, K bucket, lda, ldb, ...),
+  // searched once on the first problem of the bucket
+  std::map<F8Key, F8Plan> dyn_plans;
+  int64_t dyn_calls = 0, dyn_reused = 0, dyn_heuristic = 0;
 };
+
+// power-of-two buckets from 256: problems within a factor of two share one timed search
+int64_t dim_bucket(int64_t x) {
+  int64_t b = 256;
+  while (b < x) b <<= 1;
+  return b;
+}
 
 F8State& f8state() {
   static F8State s;
@@ -212,7 +243,7 @@ bool build_f8_plan(State& s, F8Plan& p, int64_t M, int64_t N, int64_t K, int64_t
     if (res[i].state != HIPBLAS_STATUS_SUCCESS || res[i].workspaceSize > kWorkspace) continue;
     auto run = [&]() {
       return hipblasLtMatmul(s.handle, p.desc, &one, b.data_ptr(), p.la, a.data_ptr(), p.lb, &zero, d.data_ptr(), p.lc,
-                             d.data_ptr(), p.lc, &res[i].algo, s.workspace.data_ptr(), kWorkspace, stream);
+                             d.data_ptr(), p.lc, &res[i].algo, workspace_for(s, stream, like), kWorkspace, stream);
     };
     if (!check(run())) continue;
     hipEventRecord(e0, stream);
@@ -230,15 +261,64 @@ bool build_f8_plan(State& s, F8Plan& p, int64_t M, int64_t N, int64_t K, int64_t
   hipEventDestroy(e0);
   hipEventDestroy(e1);
   p.ms = best / 3.f;
+  p.M = M;
+  p.K = K;
   return p.ok;
+}
+
+// Run problem (M, K) of a dynamic family with the bucket plan's descriptor: the bucket's searched algorithm when
+// hipBLASLt supports it for this exact problem, else the heuristic's first choice (neither path times anything or
+// synchronises). The layouts are per call (host-side objects, read at enqueue).
+bool run_dynamic(State& s, F8State& fs, F8Plan& plan, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
+                 at::ScalarType ta_, at::ScalarType tb_, bool out_f32, const void* a, const void* b, void* out,
+                 float alpha, float beta, void* ws, hipStream_t stream) {
+  if (M == plan.M && K == plan.K)
+    return check(hipblasLtMatmul(s.handle, plan.desc, &alpha, b, plan.la, a, plan.lb, &beta, out, plan.lc, out, plan.lc,
+                                 &plan.algo, ws, kWorkspace, stream));
+  hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, lc = nullptr;
+  bool ok = check(hipblasLtMatrixLayoutCreate(&la, f8type(tb_), K, N, ldb)) &&
+            check(hipblasLtMatrixLayoutCreate(&lb, f8type(ta_), K, M, lda)) &&
+            check(hipblasLtMatrixLayoutCreate(&lc, out_f32 ? HIP_R_32F : HIP_R_16BF, N, M, N));
+  hipblasLtMatmulAlgo_t algo = plan.algo;
+  if (ok) {
+    size_t ws = 0;
+    ++fs.dyn_calls;
+    if (hipblaslt_ext::matmulIsAlgoSupported(s.handle, plan.desc, &alpha, la, lb, &beta, lc, lc, algo, ws) ==
+            HIPBLAS_STATUS_SUCCESS && ws <= kWorkspace) {
+      ++fs.dyn_reused;
+    } else {
+      hipblasLtMatmulPreference_t pref;
+      ok = check(hipblasLtMatmulPreferenceCreate(&pref));
+      if (ok) {
+        uint64_t wsl = kWorkspace;
+        hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsl, sizeof(wsl));
+        hipblasLtMatmulHeuristicResult_t r;
+        int got = 0;
+        ok = check(hipblasLtMatmulAlgoGetHeuristic(s.handle, plan.desc, la, lb, lc, lc, pref, 1, &r, &got)) && got > 0 &&
+             r.state == HIPBLAS_STATUS_SUCCESS;
+        if (ok) algo = r.algo;
+        hipblasLtMatmulPreferenceDestroy(pref);
+        ++fs.dyn_heuristic;
+      }
+    }
+  }
+  if (ok)
+    ok = check(hipblasLtMatmul(s.handle, plan.desc, &alpha, b, la, a, lb, &beta, out, lc, out, lc, &algo, ws, kWorkspace,
+                               stream));
+  if (la) hipblasLtMatrixLayoutDestroy(la);
+  if (lb) hipblasLtMatrixLayoutDestroy(lb);
+  if (lc) hipblasLtMatrixLayoutDestroy(lc);
+  return ok;
 }
 
 }  // namespace
 
 // Returns false (nothing launched) when hipBLASLt has no working algorithm for the problem; the caller then uses the
-// hand-written MX-MFMA kernel.
+// hand-written MX-MFMA kernel. `dynamic`: M and / or K change from call to call (MoE expert segments) — one timed
+// search per power-of-two bucket of (M, K), every other problem of the bucket reuses that algorithm (or, where it does
+// not apply, hipBLASLt's first heuristic choice) without a search or a host synchronisation.
 bool blaslt_fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor sa, torch::Tensor sb, double alpha, torch::Tensor out,
-                     bool accumulate) {
+                     bool accumulate, bool dynamic) {
   TORCH_CHECK(a.is_cuda() && b.is_cuda() && out.is_cuda() && sa.is_cuda() && sb.is_cuda(), "blaslt_fp8_gemm: HIP tensors expected");
   const auto ta = a.scalar_type(), tb = b.scalar_type();
   TORCH_CHECK((ta == at::kFloat8_e4m3fn || ta == at::kFloat8_e5m2) && (tb == at::kFloat8_e4m3fn || tb == at::kFloat8_e5m2),
@@ -259,27 +339,33 @@ bool blaslt_fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor sa, torch::
   F8State& fs = f8state();
   hipStream_t stream = at::hip::getCurrentHIPStream();
   F8Plan* plan = nullptr;
+  void* ws = nullptr;
   {
     std::lock_guard<std::mutex> lk(s.mu);
     if (s.handle == nullptr) {
       if (!check(hipblasLtCreate(&s.handle))) return false;
       s.workspace = torch::empty({(int64_t)kWorkspace}, out.options().dtype(torch::kUInt8));
     }
-    auto key = std::make_tuple(M, N, K, lda, ldb, (int)ta, (int)tb, (int)out_f32, (int)out.get_device());
-    auto it = fs.plans.find(key);
-    if (it == fs.plans.end()) {
+    auto& table = dynamic ? fs.dyn_plans : fs.plans;
+    auto key = dynamic ? std::make_tuple(dim_bucket(M), N, dim_bucket(K), lda, ldb, (int)ta, (int)tb, (int)out_f32, (int)out.get_device())
+                       : std::make_tuple(M, N, K, lda, ldb, (int)ta, (int)tb, (int)out_f32, (int)out.get_device());
+    auto it = table.find(key);
+    if (it == table.end()) {
       F8Plan p;
       build_f8_plan(s, p, M, N, K, lda, ldb, ta, tb, out_f32, stream, out);
-      it = fs.plans.emplace(key, p).first;
+      it = table.emplace(key, p).first;
     }
     plan = &it->second;
     if (!plan->ok) return false;
     if (!set_scales(plan->desc, sa.data_ptr(), sb.data_ptr())) return false;
+    ws = workspace_for(s, stream, out);
+    if (dynamic)
+      return run_dynamic(s, fs, *plan, M, N, K, lda, ldb, ta, tb, out_f32, a.data_ptr(), b.data_ptr(), out.data_ptr(),
+                         (float)alpha, accumulate ? 1.f : 0.f, ws, stream);
   }
   const float al = (float)alpha, beta = accumulate ? 1.f : 0.f;
   return check(hipblasLtMatmul(s.handle, plan->desc, &al, b.data_ptr(), plan->la, a.data_ptr(), plan->lb, &beta,
-                               out.data_ptr(), plan->lc, out.data_ptr(), plan->lc, &plan->algo, s.workspace.data_ptr(),
-                               kWorkspace, stream));
+                               out.data_ptr(), plan->lc, out.data_ptr(), plan->lc, &plan->algo, ws, kWorkspace, stream));
 }
 
 // [(M, N, K, candidates, best ms)] of every fp8 problem searched so far.
@@ -291,6 +377,15 @@ std::vector<std::tuple<int64_t, int64_t, int64_t, int64_t, double>> blaslt_fp8_p
     out.emplace_back(std::get<0>(kv.first), std::get<1>(kv.first), std::get<2>(kv.first), kv.second.candidates,
                      kv.second.ok ? kv.second.ms : -1.0);
   return out;
+}
+
+// (bucket searches, dynamic calls on a non-representative problem, of which the bucket algorithm was reused, of
+// which the heuristic choice ran)
+std::vector<int64_t> blaslt_fp8_dynamic_stats() {
+  State& s = state();
+  std::lock_guard<std::mutex> lk(s.mu);
+  F8State& fs = f8state();
+  return {(int64_t)fs.dyn_plans.size(), fs.dyn_calls, fs.dyn_reused, fs.dyn_heuristic};
 }
 
 // [(T, N, K, candidates, best ms)] of every shape searched so far (diagnostics / bench logs).

@@ -119,47 +119,80 @@ _MOE_GEMM = os.environ.get("ACCELERATE_MOE_GEMM", "blaslt")
 _MOE_FP8_BLASLT = os.environ.get("ACCELERATE_MOE_FP8_BLASLT", "0") == "1"
 
 
+# Expert GEMMs spread over this many side streams (round robin), joined back into the caller's stream: one expert's
+# GEMM (~2k rows at Mixtral shapes) fills only part of the 256 CUs, so consecutive experts overlap.
+_MOE_STREAMS = int(os.environ.get("ACCELERATE_MOE_STREAMS", "1"))
+_SIDE_STREAMS: dict = {}
+
+
+def _side_streams(device, n):
+    key = (str(device), n)
+    if key not in _SIDE_STREAMS:
+        _SIDE_STREAMS[key] = [torch.cuda.Stream(device=device) for _ in range(n)]
+    return _SIDE_STREAMS[key]
+
+
 def _per_expert_mm(a, b, bounds, mode, out, sa, sb, smul, accumulate) -> bool:
-    """grouped_mm as one library GEMM per expert; False when a problem has no library path (then the HIP kernel runs)."""
+    """grouped_mm as one library GEMM per expert; False when a problem has no library path (then the HIP kernel runs).
+    With ACCELERATE_MOE_STREAMS > 1 the experts run on side streams that fork from and join back into the current
+    stream (every tensor they touch was created before the fork and is only reused after the join)."""
     E = len(bounds) - 1
     fp8 = a.dtype in (torch.float8_e4m3fn, torch.float8_e5m2)
     if fp8 and (sa is None or sb is None or not _MOE_FP8_BLASLT):
         return False
-    if mode == 1:
+    if _MOE_STREAMS > 1 and a.is_cuda and E > 1:
+        main = torch.cuda.current_stream(a.device)
+        side = _side_streams(a.device, min(_MOE_STREAMS, E))
+        fork = torch.cuda.Event()
+        fork.record(main)
+        for st in side:
+            st.wait_event(fork)
+        ok = True
         for e in range(E):
-            lo, hi = bounds[e], bounds[e + 1]
-            if hi <= lo:
-                continue
-            if fp8:
-                if not ext().blaslt_fp8_gemm(a[lo:hi], b[e], sa, sb[e : e + 1], smul, out[lo:hi], accumulate):
-                    return False
-            else:
-                o = out[lo:hi]
-                res = torch.mm(a[lo:hi], b[e].t(), out_dtype=out.dtype) if out.dtype != a.dtype else torch.mm(a[lo:hi], b[e].t())
-                if smul != 1.0:
-                    res = res * smul
-                o.add_(res) if accumulate else o.copy_(res)
-        if not accumulate and bounds[E] < out.shape[0]:
-            out[bounds[E] :].zero_()  # rows past the last segment are defined (zero), as the grouped kernel leaves them
-        return True
+            with torch.cuda.stream(side[e % len(side)]):
+                ok = ok and _expert_mm(a, b, bounds, e, mode, out, sa, sb, smul, accumulate, fp8)
+        for st in side:
+            main.wait_stream(st)
+        if ok and mode == 1 and not accumulate and bounds[E] < out.shape[0]:
+            out[bounds[E] :].zero_()
+        return ok
     for e in range(E):
-        lo, hi = bounds[e], bounds[e + 1]
-        o = out[e]
+        if not _expert_mm(a, b, bounds, e, mode, out, sa, sb, smul, accumulate, fp8):
+            return False
+    if mode == 1 and not accumulate and bounds[E] < out.shape[0]:
+        out[bounds[E] :].zero_()  # rows past the last segment are defined (zero), as the grouped kernel leaves them
+    return True
+
+
+def _expert_mm(a, b, bounds, e, mode, out, sa, sb, smul, accumulate, fp8) -> bool:
+    """Expert e's GEMM of grouped_mm on the current stream (mode 1: its row segment; mode 2: its column window)."""
+    lo, hi = bounds[e], bounds[e + 1]
+    if mode == 1:
         if hi <= lo:
-            if not accumulate:
-                o.zero_()
-            continue
+            return True
         if fp8:
-            if not ext().blaslt_fp8_gemm(a[:, lo:hi], b[:, lo:hi], sa, sb, smul, o, accumulate):
-                return False
-        elif o.dtype == a.dtype and smul == 1.0:
-            o.addmm_(a[:, lo:hi], b[:, lo:hi].t()) if accumulate else torch.mm(a[:, lo:hi], b[:, lo:hi].t(), out=o)
-        elif o.dtype == torch.float32 and smul == 1.0:
-            torch.addmm(o, a[:, lo:hi], b[:, lo:hi].t(), out_dtype=torch.float32, out=o) if accumulate else \
-                torch.mm(a[:, lo:hi], b[:, lo:hi].t(), out_dtype=torch.float32, out=o)
-        else:
-            res = (a[:, lo:hi].float() @ b[:, lo:hi].float().t()) * smul
-            o.add_(res.to(o.dtype)) if accumulate else o.copy_(res)
+            return ext().blaslt_fp8_gemm(a[lo:hi], b[e], sa, sb[e : e + 1], smul, out[lo:hi], accumulate, True)
+        o = out[lo:hi]
+        res = torch.mm(a[lo:hi], b[e].t(), out_dtype=out.dtype) if out.dtype != a.dtype else torch.mm(a[lo:hi], b[e].t())
+        if smul != 1.0:
+            res = res * smul
+        o.add_(res) if accumulate else o.copy_(res)
+        return True
+    o = out[e]
+    if hi <= lo:
+        if not accumulate:
+            o.zero_()
+        return True
+    if fp8:
+        return ext().blaslt_fp8_gemm(a[:, lo:hi], b[:, lo:hi], sa, sb, smul, o, accumulate, True)
+    if o.dtype == a.dtype and smul == 1.0:
+        o.addmm_(a[:, lo:hi], b[:, lo:hi].t()) if accumulate else torch.mm(a[:, lo:hi], b[:, lo:hi].t(), out=o)
+    elif o.dtype == torch.float32 and smul == 1.0:
+        torch.addmm(o, a[:, lo:hi], b[:, lo:hi].t(), out_dtype=torch.float32, out=o) if accumulate else \
+            torch.mm(a[:, lo:hi], b[:, lo:hi].t(), out_dtype=torch.float32, out=o)
+    else:
+        res = (a[:, lo:hi].float() @ b[:, lo:hi].float().t()) * smul
+        o.add_(res.to(o.dtype)) if accumulate else o.copy_(res)
     return True
 
 

@@ -1226,3 +1226,67 @@ def test_small_allreduce_two_processes_over_ipc():
     for rank, res, err in out:
         assert err is None, (rank, err)
         assert all(res), (rank, res)
+
+
+@pytest.mark.parametrize("T,N,K", [(512, 384, 256), (1024, 6144, 4096)])
+def test_linear_dgrad_transposed_weight_matches_torch(T, N, K):
+    """ops/fused.linear_dgrad: dx = dy·W through the HIP-transposed weight and the forward-layout GEMM equals dy @ W."""
+    from accelerate_hpc_test_amd.ops.fused import linear_dgrad
+
+    torch.manual_seed(0)
+    dy = torch.randn(T, N, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16)
+    ref = dy.float() @ w.float()
+    out = linear_dgrad(dy, w)
+    assert out.shape == (T, K) and out.dtype == torch.bfloat16
+    assert _rel(out, ref) < 1e-2, _rel(out, ref)
+
+
+def test_wgrad_into_layouts_match_torch():
+    """ops/fused.wgrad_into for the engines' destinations: fp32 slot (searched hipBLASLt runner) from token-major x and
+    from the transposed view of the token-contiguous copy xT, bf16 slot, and accumulation."""
+    from accelerate_hpc_test_amd.ops.fused import wgrad_into
+
+    torch.manual_seed(0)
+    T, N, K = 1024, 768, 512
+    dy = torch.randn(T, N, device=DEV, dtype=torch.bfloat16)
+    x = torch.randn(T, K, device=DEV, dtype=torch.bfloat16)
+    ref = dy.float().t() @ x.float()
+    for xv in (x, x.t().contiguous().t()):
+        d32 = torch.empty(N, K, device=DEV, dtype=torch.float32)
+        wgrad_into(d32, dy, xv, False)
+        assert _rel(d32, ref) < 1e-3
+        wgrad_into(d32, dy, xv, True)
+        assert _rel(d32, 2 * ref) < 1e-3
+        d16 = torch.empty(N, K, device=DEV, dtype=torch.bfloat16)
+        wgrad_into(d16, dy, xv, False)
+        assert _rel(d16, ref) < 1e-2
+
+
+def test_blaslt_fp8_dynamic_shapes_match_reference():
+    """fp8 runner, dynamic mode (MoE expert segments): row counts and contraction lengths that change per call share
+    one timed search per power-of-two bucket; every problem still matches the fp32 product of the fp8 operands."""
+    from accelerate_hpc_test_amd.ops._ext import ext
+
+    torch.manual_seed(0)
+    N, K = 256, 512
+    b8 = (torch.randn(N, K, device=DEV) * 4).to(torch.float8_e4m3fn)
+    one = torch.ones(1, device=DEV)
+    before = ext().blaslt_fp8_dynamic_stats()
+    for M in (256, 200, 77, 300, 512, 1000, 256):
+        a8 = (torch.randn(M, K, device=DEV) * 4).to(torch.float8_e4m3fn)
+        out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        assert ext().blaslt_fp8_gemm(a8, b8, one, one, 1.0, out, False, True)
+        ref = a8.float() @ b8.float().t()
+        assert _rel(out, ref) < 1e-2, (M, _rel(out, ref))
+    # varying contraction length over column windows of wider operands (the expert weight-gradient form)
+    T = 2048
+    a8 = (torch.randn(N, T, device=DEV) * 4).to(torch.float8_e4m3fn)
+    c8 = (torch.randn(N, T, device=DEV) * 4).to(torch.float8_e4m3fn)
+    for lo, hi in ((0, 512), (512, 700), (700, 2048)):
+        out = torch.zeros(N, N, device=DEV, dtype=torch.float32)
+        assert ext().blaslt_fp8_gemm(a8[:, lo:hi], c8[:, lo:hi], one, one, 1.0, out, True, True)
+        ref = a8[:, lo:hi].float() @ c8[:, lo:hi].float().t()
+        assert _rel(out, ref) < 1e-3, (lo, hi, _rel(out, ref))
+    after = ext().blaslt_fp8_dynamic_stats()
+    assert after[0] > before[0] and after[1] > before[1]  # bucket searches happened and some calls ran without one
