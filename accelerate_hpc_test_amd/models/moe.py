@@ -113,49 +113,20 @@ def _gg_native_ok(a, b, mode, out) -> bool:
 # profiles/r3_moe_gemm.md) 1.2-1.5x faster than the HIP grouped kernel even with that sync. "grouped" = the HIP grouped
 # kernel over the device table (no host sync at all), also used whenever no host table is attached.
 _MOE_GEMM = os.environ.get("ACCELERATE_MOE_GEMM", "blaslt")
-# fp8 expert GEMMs stay on the HIP grouped kernel by default: the fp8 hipBLASLt runner times its candidates once per
-# exact problem, and the per-expert row counts change every step, so each step paid new searches (each one a host
-# sync): Mixtral-8x7B-8l fp8 fell from 36.7k to 14.3k tok/s with it (profiles/r3_moe_gemm.md).
+# fp8 expert GEMMs stay on the HIP grouped kernel by default. The fp8 hipBLASLt runner's dynamic-shape mode (one timed
+# search per power-of-two bucket of the changing row counts, no per-step searches) brought the per-expert path from
+# 14.3k to 34.4k tok/s on Mixtral-8x7B-8l, still under the grouped kernel's 36.2k: a ~2k-row expert GEMM fills half
+# the chip (profiles/r3_moe_gemm.md).
 _MOE_FP8_BLASLT = os.environ.get("ACCELERATE_MOE_FP8_BLASLT", "0") == "1"
-
-
-# Expert GEMMs spread over this many side streams (round robin), joined back into the caller's stream: one expert's
-# GEMM (~2k rows at Mixtral shapes) fills only part of the 256 CUs, so consecutive experts overlap.
-_MOE_STREAMS = int(os.environ.get("ACCELERATE_MOE_STREAMS", "1"))
-_SIDE_STREAMS: dict = {}
-
-
-def _side_streams(device, n):
-    key = (str(device), n)
-    if key not in _SIDE_STREAMS:
-        _SIDE_STREAMS[key] = [torch.cuda.Stream(device=device) for _ in range(n)]
-    return _SIDE_STREAMS[key]
 
 
 def _per_expert_mm(a, b, bounds, mode, out, sa, sb, smul, accumulate) -> bool:
     """grouped_mm as one library GEMM per expert; False when a problem has no library path (then the HIP kernel runs).
-    With ACCELERATE_MOE_STREAMS > 1 the experts run on side streams that fork from and join back into the current
-    stream (every tensor they touch was created before the fork and is only reused after the join)."""
+    (Spreading the experts over side HIP streams was tried: the Mixtral training step hung in its first warm-up step.)"""
     E = len(bounds) - 1
     fp8 = a.dtype in (torch.float8_e4m3fn, torch.float8_e5m2)
     if fp8 and (sa is None or sb is None or not _MOE_FP8_BLASLT):
         return False
-    if _MOE_STREAMS > 1 and a.is_cuda and E > 1:
-        main = torch.cuda.current_stream(a.device)
-        side = _side_streams(a.device, min(_MOE_STREAMS, E))
-        fork = torch.cuda.Event()
-        fork.record(main)
-        for st in side:
-            st.wait_event(fork)
-        ok = True
-        for e in range(E):
-            with torch.cuda.stream(side[e % len(side)]):
-                ok = ok and _expert_mm(a, b, bounds, e, mode, out, sa, sb, smul, accumulate, fp8)
-        for st in side:
-            main.wait_stream(st)
-        if ok and mode == 1 and not accumulate and bounds[E] < out.shape[0]:
-            out[bounds[E] :].zero_()
-        return ok
     for e in range(E):
         if not _expert_mm(a, b, bounds, e, mode, out, sa, sb, smul, accumulate, fp8):
             return False

@@ -56,9 +56,7 @@ for step in "$@"; do
     mix8_bf16) run mix8_bf16 600 python bench.py --model mixtral-8x7b-8l --steps 5 --warmup 2 --verbose $BENCH_ARGS ;;
     mix8_fp8) run mix8_fp8 600 python bench.py --model mixtral-8x7b-8l --steps 5 --warmup 2 --precision fp8 --verbose $BENCH_ARGS ;;
     mix8_fp8_blaslt) ACCELERATE_MOE_FP8_BLASLT=1 run mix8_fp8_blaslt 600 python bench.py --model mixtral-8x7b-8l --steps 5 --warmup 2 --precision fp8 --verbose $BENCH_ARGS ;;
-    mix8_bf16_s4) ACCELERATE_MOE_STREAMS=4 run mix8_bf16_s4 170 python -u bench.py --model mixtral-8x7b-8l --steps 5 --warmup 2 --verbose $BENCH_ARGS ;;
-    mix8_fp8_blaslt_s4) ACCELERATE_MOE_STREAMS=4 ACCELERATE_MOE_FP8_BLASLT=1 run mix8_fp8_blaslt_s4 600 python bench.py --model mixtral-8x7b-8l --steps 5 --warmup 2 --precision fp8 $BENCH_ARGS ;;
-    mix8_fp8_blaslt_s2) ACCELERATE_MOE_STREAMS=2 ACCELERATE_MOE_FP8_BLASLT=1 run mix8_fp8_blaslt_s2 600 python bench.py --model mixtral-8x7b-8l --steps 5 --warmup 2 --precision fp8 $BENCH_ARGS ;;
+    moegemm) run moegemm 300 python tools/bench_moe_gemm.py ;;
     prof_mix8_fp8) prof prof_mix8_fp8 600 bench.py --model mixtral-8x7b-8l --steps 2 --warmup 2 --precision fp8 ;;
     prof_mix8_fp8_blaslt) ACCELERATE_MOE_FP8_BLASLT=1 prof prof_mix8_fp8_blaslt 600 bench.py --model mixtral-8x7b-8l --steps 2 --warmup 2 --precision fp8 ;;
     mixtral_bf16) run mixtral_bf16 600 python bench.py --model mixtral-8x7b-4l --steps 3 --warmup 2 $BENCH_ARGS ;;
