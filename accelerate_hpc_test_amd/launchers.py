@@ -42,60 +42,54 @@ def notebook_launcher(
     log_line_prefix_template=None,
 ):
     """Launch `function(*args)` on `num_processes` local workers (one per GPU) with elastic fault tolerance."""
-    in_colab = False
     problematic_imports = are_libraries_initialized("bitsandbytes")
-    if len(problematic_imports) > 0:
+    if problematic_imports:
         raise RuntimeError(
             "Could not start distributed process. Libraries known to initialize the device upon import have been "
             f"imported already: {', '.join(problematic_imports)}. Import them inside the launched function instead."
         )
     if num_processes is None:
-        num_processes = torch.cuda.device_count() if torch.cuda.device_count() > 0 else 1
-    if num_processes == 1 and num_nodes == 1:
+        num_processes = max(1, torch.cuda.device_count())
+    if num_processes == 1 and num_nodes == 1:  # nothing to launch: run in this process
         with patch_environment(accelerate_mixed_precision=mixed_precision):
             function(*args)
         return
-    if len(AcceleratorState._shared_state) > 0:
+    if AcceleratorState._shared_state:
         raise ValueError(
             "To launch a multi-GPU training from your notebook, the `Accelerator` should only be initialized inside your "
             "training function. Restart your notebook and make sure no cells initializes an `Accelerator`."
         )
-    if rdzv_backend == "static" and is_port_in_use(int(use_port)) and num_nodes == 1:
+    if rdzv_backend == "static" and num_nodes == 1 and is_port_in_use(int(use_port)):
         use_port = str(get_free_port())
-    from torch.distributed.launcher.api import LaunchConfig, elastic_launch
+    config = _elastic_config(num_processes, num_nodes, node_rank, master_addr, use_port, rdzv_backend, rdzv_endpoint,
+                             rdzv_conf, rdzv_id, max_restarts, monitor_interval, log_line_prefix_template)
+    from torch.distributed.launcher.api import elastic_launch
 
-    if rdzv_conf is None:
-        rdzv_conf = {}
-    if rdzv_backend == "static":
-        rdzv_conf["rank"] = node_rank
-        if not rdzv_endpoint:
-            rdzv_endpoint = f"{master_addr}:{use_port}"
-    launch_config_kwargs = dict(
-        min_nodes=num_nodes,
-        max_nodes=num_nodes,
-        nproc_per_node=num_processes,
-        run_id=rdzv_id,
-        rdzv_endpoint=rdzv_endpoint,
-        rdzv_backend=rdzv_backend,
-        rdzv_configs=rdzv_conf,
-        max_restarts=max_restarts,
-        monitor_interval=monitor_interval,
-        start_method="fork",
-    )
-    if log_line_prefix_template is not None:
-        launch_config_kwargs["log_line_prefix_template"] = log_line_prefix_template
-    with patch_environment(
-        nproc=num_processes,
-        node_rank=node_rank,
-        world_size=num_nodes * num_processes,
-        master_addr=master_addr,
-        master_port=use_port,
-        mixed_precision=mixed_precision,
-        accelerate_mixed_precision=mixed_precision,
-        fork_launched="1",
-        hsa_enable_ipc_mode_legacy=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"),
-    ):
-        elastic_launch(config=LaunchConfig(**launch_config_kwargs), entrypoint=function)(*args)
+    worker_env = {
+        "nproc": num_processes, "node_rank": node_rank, "world_size": num_nodes * num_processes,
+        "master_addr": master_addr, "master_port": use_port, "mixed_precision": mixed_precision,
+        "accelerate_mixed_precision": mixed_precision, "fork_launched": "1",
+        # dmabuf IPC: RCCL peer buffers and HIP-tensor sharing between the forked workers
+        "hsa_enable_ipc_mode_legacy": os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"),
+    }
+    with patch_environment(**worker_env):
+        elastic_launch(config=config, entrypoint=function)(*args)
+
+
+def _elastic_config(nproc, nnodes, node_rank, master_addr, port, backend, endpoint, conf, run_id, max_restarts,
+                    monitor_interval, log_line_prefix_template):
+    """torch elastic LaunchConfig for `nproc` forked workers per node: a static rendezvous gets this node's rank and
+    defaults its endpoint to master_addr:port; restarts / monitoring follow the caller's fault-tolerance settings."""
+    from torch.distributed.launcher.api import LaunchConfig
+
+    conf = dict(conf or {})
+    if backend == "static":
+        conf["rank"] = node_rank
+        endpoint = endpoint or f"{master_addr}:{port}"
+    extra = {} if log_line_prefix_template is None else {"log_line_prefix_template": log_line_prefix_template}
+    return LaunchConfig(min_nodes=nnodes, max_nodes=nnodes, nproc_per_node=nproc, run_id=run_id, rdzv_endpoint=endpoint,
+                        rdzv_backend=backend, rdzv_configs=conf, max_restarts=max_restarts,
+                        monitor_interval=monitor_interval, start_method="fork", **extra)
 
 
 def debug_launcher(function, args=(), num_processes=2):
