@@ -17,6 +17,13 @@ pytest.importorskip("transformers")
 TINY = ["--cpu", "--tiny", "--num_epochs", "1", "--n_train", "96", "--n_eval", "40"]
 
 
+def _port() -> str:
+    """A free rendezvous port per launch: parallel test workers must not share the default 29500."""
+    from accelerate_hpc_test_amd.utils.other import get_free_port
+
+    return str(get_free_port())
+
+
 @pytest.mark.parametrize(
     "name",
     ["gradient_accumulation", "early_stopping", "local_sgd", "tracking", "memory", "multi_process_metrics",
@@ -69,7 +76,8 @@ def test_feature_example_two_ranks(name, tmp_path):
     cfg.write_text("compute_environment: LOCAL_MACHINE\ndistributed_type: MULTI_CPU\nnum_processes: 2\nuse_cpu: true\nmixed_precision: 'no'\n")
     env = dict(os.environ, HF_HOME=str(tmp_path), PYTHONPATH=REPO)
     r = subprocess.run(
-        [sys.executable, "-m", "accelerate_hpc_test_amd.commands.accelerate_cli", "launch", "--config_file", str(cfg),
+        [sys.executable, "-m", "accelerate_hpc_test_amd.commands.accelerate_cli", "launch",
+         "--main_process_port", _port(), "--config_file", str(cfg),
          os.path.join(FEAT, f"{name}.py"), *TINY],
         cwd=REPO, env=env, capture_output=True, text=True, timeout=600,
     )

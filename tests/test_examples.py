@@ -13,6 +13,13 @@ sys.path.insert(0, os.path.join(REPO, "examples"))
 transformers = pytest.importorskip("transformers")
 
 
+def _port() -> str:
+    """A free rendezvous port per launch: parallel test workers must not share the default 29500."""
+    from accelerate_hpc_test_amd.utils.other import get_free_port
+
+    return str(get_free_port())
+
+
 def test_nlp_example_cpu_learns():
     import nlp_example
 
@@ -25,7 +32,8 @@ def test_nlp_example_two_ranks_via_launch(tmp_path):
     cfg.write_text("compute_environment: LOCAL_MACHINE\ndistributed_type: MULTI_CPU\nnum_processes: 2\nuse_cpu: true\nmixed_precision: 'no'\n")
     env = dict(os.environ, HF_HOME=str(tmp_path), PYTHONPATH=REPO)
     r = subprocess.run(
-        [sys.executable, "-m", "accelerate_hpc_test_amd.commands.accelerate_cli", "launch", "--config_file", str(cfg),
+        [sys.executable, "-m", "accelerate_hpc_test_amd.commands.accelerate_cli", "launch",
+         "--main_process_port", _port(), "--config_file", str(cfg),
          os.path.join(REPO, "examples", "nlp_example.py"), "--cpu", "--tiny", "--num_epochs", "2", "--n_train", "256", "--n_eval", "64"],
         cwd=REPO, env=env, capture_output=True, text=True, timeout=600,
     )
@@ -79,6 +87,7 @@ def test_config_templates_load_and_launch(tmp_path):
     for cfg, extra, expect in ((os.path.join(REPO, "examples", "config_yaml_templates", "single_accelerator.yaml"),
                                 ["--cpu"], "num_processes=1"), (str(cpu2), [], "num_processes=2")):
         r = subprocess.run([sys.executable, "-m", "accelerate_hpc_test_amd.commands.accelerate_cli", "launch",
+         "--main_process_port", _port(),
                             "--config_file", cfg, *extra, script], cwd=REPO, env=env, capture_output=True, text=True,
                            timeout=300)
         assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
@@ -94,7 +103,8 @@ def test_inference_and_sequence_parallel_examples_two_ranks(tmp_path, script, ex
     """Pipeline inference (prepare_pippy), split_between_processes generation and Ulysses SP training, each launched
     on 2 CPU ranks through `accelerate-amd launch` (reference examples/inference/*, examples/alst_ulysses_*)."""
     env = dict(os.environ, HF_HOME=str(tmp_path), PYTHONPATH=REPO)
-    r = subprocess.run([sys.executable, "-m", "accelerate_hpc_test_amd.commands.accelerate_cli", "launch", "--cpu",
+    r = subprocess.run([sys.executable, "-m", "accelerate_hpc_test_amd.commands.accelerate_cli", "launch",
+         "--main_process_port", _port(), "--cpu",
                         "--num_processes", "2", os.path.join(REPO, script), "--cpu"], cwd=REPO, env=env,
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
