@@ -1,8 +1,9 @@
 """Multi-process aware logging.
 
-Parity: `/root/reference/src/accelerate/logging.py:23-126` — `get_logger(name, log_level)` returns an adapter
-that logs on the main process only unless `main_process_only=False`, can serialise ranks with
-`in_order=True`, and offers `warning_once`. Honors `ACCELERATE_LOG_LEVEL`.
+Parity: `/root/reference/src/accelerate/logging.py:23-126`. `get_logger(name, log_level)` returns an adapter whose
+records are emitted by the main process only, unless a call passes `main_process_only=False` (every process logs) or
+`in_order=True` (every process logs, rank by rank, with a barrier between ranks); `warning_once` deduplicates.
+`ACCELERATE_LOG_LEVEL` sets the level when none is given.
 """
 
 from __future__ import annotations
@@ -12,47 +13,50 @@ import logging
 import os
 
 
-class MultiProcessAdapter(logging.LoggerAdapter):
-    @staticmethod
-    def _should_log(main_process_only):
-        from .state import PartialState
+def _process_state():
+    from .state import PartialState
 
-        state = PartialState()
-        return not main_process_only or (main_process_only and state.is_main_process)
+    if PartialState._shared_state == {}:
+        raise RuntimeError(
+            "You must initialize the accelerate state by calling either `PartialState()` or `Accelerator()` before "
+            "using the logging utility."
+        )
+    return PartialState()
+
+
+class MultiProcessAdapter(logging.LoggerAdapter):
+    def _emit(self, level, msg, args, kwargs):
+        msg, kwargs = self.process(msg, kwargs)
+        self.logger.log(level, msg, *args, **kwargs)
 
     def log(self, level, msg, *args, **kwargs):
-        from .state import PartialState
-
-        if PartialState._shared_state == {}:
-            raise RuntimeError(
-                "You must initialize the accelerate state by calling either `PartialState()` or `Accelerator()` before using the logging utility."
-            )
-        main_process_only = kwargs.pop("main_process_only", True)
+        state = _process_state()
+        main_only = kwargs.pop("main_process_only", True)
         in_order = kwargs.pop("in_order", False)
         kwargs.setdefault("stacklevel", 2)
-        if self.isEnabledFor(level):
-            if self._should_log(main_process_only):
-                msg, kwargs = self.process(msg, kwargs)
-                self.logger.log(level, msg, *args, **kwargs)
-            elif in_order:
-                state = PartialState()
-                for i in range(state.num_processes):
-                    if i == state.process_index:
-                        msg, kwargs = self.process(msg, kwargs)
-                        self.logger.log(level, msg, *args, **kwargs)
-                    state.wait_for_everyone()
+        if not self.isEnabledFor(level):
+            return
+        if not main_only or state.is_main_process:
+            self._emit(level, msg, args, kwargs)
+            return
+        if in_order:  # every rank in turn: rank i logs, then all ranks meet before rank i + 1
+            for rank in range(state.num_processes):
+                if rank == state.process_index:
+                    self._emit(level, msg, args, kwargs)
+                state.wait_for_everyone()
 
     @functools.lru_cache(None)
     def warning_once(self, *args, **kwargs):
-        """Like `warning` but emitted only once per unique message."""
+        """`warning`, emitted once per distinct argument tuple."""
         self.warning(*args, **kwargs)
 
 
 def get_logger(name: str, log_level: str | None = None):
-    if log_level is None:
-        log_level = os.environ.get("ACCELERATE_LOG_LEVEL", None)
+    """A `MultiProcessAdapter` over `logging.getLogger(name)`; `log_level` (or ACCELERATE_LOG_LEVEL) sets its level and
+    the root logger's."""
+    level = log_level if log_level is not None else os.environ.get("ACCELERATE_LOG_LEVEL")
     logger = logging.getLogger(name)
-    if log_level is not None:
-        logger.setLevel(log_level.upper())
-        logger.root.setLevel(log_level.upper())
+    if level is not None:
+        logger.setLevel(level.upper())
+        logger.root.setLevel(level.upper())
     return MultiProcessAdapter(logger, {})
