@@ -2,7 +2,8 @@
 
 Parity: `/root/reference/src/accelerate/logging.py:23-126`. `get_logger(name, log_level)` returns an adapter whose
 records are emitted by the main process only, unless a call passes `main_process_only=False` (every process logs) or
-`in_order=True` (every process logs, rank by rank, with a barrier between ranks); `warning_once` deduplicates.
+`in_order=True` without `main_process_only` (every process logs, rank by rank, all ranks meeting at a barrier after
+each); `warning_once` deduplicates.
 `ACCELERATE_LOG_LEVEL` sets the level when none is given.
 """
 
@@ -27,23 +28,27 @@ def _process_state():
 class MultiProcessAdapter(logging.LoggerAdapter):
     def _emit(self, level, msg, args, kwargs):
         msg, kwargs = self.process(msg, kwargs)
-        self.logger.log(level, msg, *args, **kwargs)
+        # one more frame (this helper) between the caller's `stacklevel` and Logger.log
+        self.logger.log(level, msg, *args, **{**kwargs, "stacklevel": kwargs.get("stacklevel", 1) + 1})
 
     def log(self, level, msg, *args, **kwargs):
         state = _process_state()
+        explicit_main_only = "main_process_only" in kwargs
         main_only = kwargs.pop("main_process_only", True)
-        in_order = kwargs.pop("in_order", False)
+        in_order = kwargs.pop("in_order", False) and not explicit_main_only  # an explicit main_process_only wins
         kwargs.setdefault("stacklevel", 2)
         if not self.isEnabledFor(level):
             return
-        if not main_only or state.is_main_process:
-            self._emit(level, msg, args, kwargs)
-            return
-        if in_order:  # every rank in turn: rank i logs, then all ranks meet before rank i + 1
+        if in_order and state.num_processes > 1:
+            # every rank in turn, ALL ranks joining every barrier (the reference lets the main process log and return
+            # while the others wait on barriers it never enters)
             for rank in range(state.num_processes):
                 if rank == state.process_index:
                     self._emit(level, msg, args, kwargs)
                 state.wait_for_everyone()
+            return
+        if not main_only or state.is_main_process:
+            self._emit(level, msg, args, kwargs)
 
     @functools.lru_cache(None)
     def warning_once(self, *args, **kwargs):
