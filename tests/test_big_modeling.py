@@ -178,16 +178,24 @@ def test_load_checkpoint_and_dispatch_roundtrip():
 
 def test_bench_generate_tool_tiny_cpu(tmp_path):
     """tools/bench_generate.py (BASELINE #4 in the reference benchmark's terms: load s, generation s/token) end to end
-    on a tiny GPT-NeoX: synthetic sharded checkpoint -> load_checkpoint_and_dispatch -> transformers generate."""
+    on a tiny GPT-NeoX: synthetic sharded checkpoint -> load_checkpoint_and_dispatch -> transformers generate, resident
+    and with part of the model offloaded to disk (identical greedy output)."""
     import json
     import subprocess
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    out = subprocess.run([sys.executable, os.path.join(root, "tools", "bench_generate.py"), "--model", "tiny", "--cpu",
-                          "--dtype", "fp32", "--new-tokens", "4", "--ckpt-dir", str(tmp_path / "ckpt")],
-                         capture_output=True, text=True, timeout=300, env={**os.environ, "TMPDIR": str(tmp_path)})
-    assert out.returncode == 0, out.stderr[-2000:]
-    rec = json.loads(out.stdout.strip().splitlines()[-1])
+    def run(*extra):
+        out = subprocess.run([sys.executable, os.path.join(root, "tools", "bench_generate.py"), "--model", "tiny", "--cpu",
+                              "--dtype", "fp32", "--new-tokens", "4", "--ckpt-dir", str(tmp_path / "ckpt"), *extra],
+                             capture_output=True, text=True, timeout=300, env={**os.environ, "TMPDIR": str(tmp_path)})
+        assert out.returncode == 0, out.stderr[-2000:]
+        return json.loads(out.stdout.strip().splitlines()[-1])
+
+    rec = run()
     assert rec["new_tokens"] == 4 and rec["load_s"] >= 0 and rec["s_per_token"] > 0
     assert os.path.isfile(tmp_path / "ckpt" / "model.safetensors.index.json")
+    # part of the model offloaded to disk (streamed back by the offload hooks): same greedy generations
+    off = run("--cpu-mem", "600KB", "--disk-offload")
+    assert set(off["placement_gib"]) == {"cpu", "disk"}, off["placement_gib"]
+    assert off["generated_checksum"] == rec["generated_checksum"]

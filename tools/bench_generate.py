@@ -155,7 +155,7 @@ def main():
 
     main = "cpu" if args.cpu else "cuda:0"
     g = torch.Generator().manual_seed(1)
-    times, toks = [], []
+    times, toks, checksum = [], [], 0
     with torch.no_grad():
         for n in PROMPT_LENGTHS:
             ids = torch.randint(100, config.vocab_size - 100, (1, n), generator=g).to(main)
@@ -166,6 +166,7 @@ def main():
             sync()
             times.append(time.perf_counter() - t0)
             toks.append(out.shape[1] - n)
+            checksum = (checksum * 1000003 + int(out[0, n:].long().sum().item())) % (1 << 61)
     per_tok = [t / k for t, k in zip(times, toks)]
     rec = {
         "metric": "big-model load s / generation s per token (reference benchmarks/big_model_inference)",
@@ -176,6 +177,7 @@ def main():
         "s_per_token_first": round(per_tok[0], 4),
         "s_per_token_excl_first": round(sum(per_tok[1:]) / (len(per_tok) - 1), 4),
         "new_tokens": args.new_tokens,
+        "generated_checksum": checksum,  # greedy decoding: equal across placements of the same checkpoint
         "params_b": round(sum(v for k, v in sizes.items() if k == "") / (torch.finfo(dtype).bits // 8) / 1e9, 2),
         "placement_gib": {k: round(v / 2**30, 1) for k, v in per_device.items()},
         "n_gpus": n_gpu,
