@@ -96,6 +96,7 @@ std::vector<std::tuple<int64_t, int64_t, int64_t, int64_t, double>> blaslt_wgrad
 bool blaslt_fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor sa, torch::Tensor sb, double alpha, torch::Tensor out,
                      bool accumulate, bool dynamic);
 std::vector<int64_t> blaslt_fp8_dynamic_stats();
+bool blaslt_mx_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor sa, torch::Tensor sb, torch::Tensor out, bool accumulate);
 std::vector<std::tuple<int64_t, int64_t, int64_t, int64_t, double>> blaslt_fp8_plans();
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -153,6 +154,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("sa"), pybind11::arg("sb"), pybind11::arg("alpha"),
         pybind11::arg("out"), pybind11::arg("accumulate"), pybind11::arg("dynamic") = false);
   m.def("blaslt_fp8_dynamic_stats", &blaslt_fp8_dynamic_stats);
+  m.def("blaslt_mx_gemm", &blaslt_mx_gemm, "MXFP8 GEMM on hipBLASLt (VEC32_UE8M0 block scales)");
   m.def("blaslt_fp8_plans", &blaslt_fp8_plans);
   m.def("debug_status", &debug_status, "first failed device bounds check (id << 32 | line), 0 if none; clears it");
   m.def("debug_selftest", &debug_selftest);

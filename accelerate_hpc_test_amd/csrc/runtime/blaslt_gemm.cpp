@@ -368,6 +368,132 @@ bool blaslt_fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor sa, torch::
                                out.data_ptr(), plan->lc, out.data_ptr(), plan->lc, &plan->algo, ws, kWorkspace, stream));
 }
 
+// ------------------------------------------------------------------------------------------------ MXFP8 (block scales)
+// C[M, N] (=|+=) (A[M, K] . B[N, K]^T) with one e8m0 scale per 32-element K block of every row of A and B
+// (HIPBLASLT_MATMUL_MATRIX_SCALE_VEC32_UE8M0); sa / sb are the scale tensors in the layout hipBLASLt reads (the caller
+// converts from the quantiser's grouped layout). Same TN mapping and per-problem algorithm timing as the per-tensor
+// runner above. Returns false when hipBLASLt has no MX algorithm for the problem.
+namespace {
+
+struct MxState {
+  std::map<std::tuple<int64_t, int64_t, int64_t, int, int, int, int>, F8Plan> plans;
+};
+
+MxState& mxstate() {
+  static MxState s;
+  return s;
+}
+
+bool set_mx_scales(hipblasLtMatmulDesc_t desc, const void* sa, const void* sb) {
+  const int32_t mode = HIPBLASLT_MATMUL_MATRIX_SCALE_VEC32_UE8M0;
+  return check(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_A_SCALE_MODE, &mode, sizeof(mode))) &&
+         check(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_B_SCALE_MODE, &mode, sizeof(mode))) &&
+         set_scales(desc, sa, sb);
+}
+
+bool build_mx_plan(State& s, F8Plan& p, int64_t M, int64_t N, int64_t K, at::ScalarType ta_, at::ScalarType tb_,
+                   bool out_f32, hipStream_t stream, const torch::Tensor& like) {
+  const hipblasOperation_t opA = HIPBLAS_OP_T, opB = HIPBLAS_OP_N;
+  const hipDataType dt = out_f32 ? HIP_R_32F : HIP_R_16BF;
+  if (!check(hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F))) return false;
+  if (!check(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &opA, sizeof(opA)))) return false;
+  if (!check(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &opB, sizeof(opB)))) return false;
+  if (!check(hipblasLtMatrixLayoutCreate(&p.la, f8type(tb_), K, N, K))) return false;
+  if (!check(hipblasLtMatrixLayoutCreate(&p.lb, f8type(ta_), K, M, K))) return false;
+  if (!check(hipblasLtMatrixLayoutCreate(&p.lc, dt, N, M, N))) return false;
+  auto sa_s = torch::full({M * K / 32}, 127, like.options().dtype(torch::kUInt8));
+  auto sb_s = torch::full({N * K / 32}, 127, like.options().dtype(torch::kUInt8));
+  if (!set_mx_scales(p.desc, sa_s.data_ptr(), sb_s.data_ptr())) return false;
+  hipblasLtMatmulPreference_t pref;
+  if (!check(hipblasLtMatmulPreferenceCreate(&pref))) return false;
+  uint64_t ws = kWorkspace;
+  hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &ws, sizeof(ws));
+  std::vector<hipblasLtMatmulHeuristicResult_t> res(8);  // the heuristic's first 8: some MX candidates are very slow
+  int got = 0;
+  const bool okh = check(hipblasLtMatmulAlgoGetHeuristic(s.handle, p.desc, p.la, p.lb, p.lc, p.lc, pref, (int)res.size(),
+                                                         res.data(), &got));
+  hipblasLtMatmulPreferenceDestroy(pref);
+  if (!okh || got <= 0) return false;
+  p.candidates = got;
+  auto a = torch::empty({M, K}, like.options().dtype(torch::kUInt8)).random_(0, 64);
+  auto b = torch::empty({N, K}, like.options().dtype(torch::kUInt8)).random_(0, 64);
+  auto d = torch::empty({M, N}, like.options().dtype(out_f32 ? torch::kFloat32 : torch::kBFloat16));
+  const float one = 1.f, zero = 0.f;
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  float best = 1e30f;
+  for (int i = 0; i < got; ++i) {
+    if (res[i].state != HIPBLAS_STATUS_SUCCESS || res[i].workspaceSize > kWorkspace) continue;
+    auto run = [&]() {
+      return hipblasLtMatmul(s.handle, p.desc, &one, b.data_ptr(), p.la, a.data_ptr(), p.lb, &zero, d.data_ptr(), p.lc,
+                             d.data_ptr(), p.lc, &res[i].algo, workspace_for(s, stream, like), kWorkspace, stream);
+    };
+    if (!check(run())) continue;
+    hipEventRecord(e0, stream);
+    for (int r = 0; r < 2; ++r) run();
+    hipEventRecord(e1, stream);
+    hipEventSynchronize(e1);
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, e0, e1);
+    if (ms < best) {
+      best = ms;
+      p.algo = res[i].algo;
+      p.ok = true;
+    }
+  }
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  p.ms = best / 2.f;
+  p.M = M;
+  p.K = K;
+  return p.ok;
+}
+
+}  // namespace
+
+bool blaslt_mx_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor sa, torch::Tensor sb, torch::Tensor out,
+                    bool accumulate) {
+  TORCH_CHECK(a.is_cuda() && b.is_cuda() && out.is_cuda() && sa.is_cuda() && sb.is_cuda(), "blaslt_mx_gemm: HIP tensors");
+  const auto ta = a.scalar_type(), tb = b.scalar_type();
+  TORCH_CHECK((ta == at::kFloat8_e4m3fn || ta == at::kFloat8_e5m2) && (tb == at::kFloat8_e4m3fn || tb == at::kFloat8_e5m2),
+              "blaslt_mx_gemm: e4m3 / e5m2 operands expected");
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.is_contiguous() && b.is_contiguous() && out.is_contiguous() &&
+                  sa.is_contiguous() && sb.is_contiguous() && sa.scalar_type() == at::kByte && sb.scalar_type() == at::kByte,
+              "blaslt_mx_gemm: contiguous operands, uint8 e8m0 scales");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(b.size(1) == K && out.size(0) == M && out.size(1) == N && K % 32 == 0 && sa.numel() == M * K / 32 &&
+                  sb.numel() == N * K / 32, "blaslt_mx_gemm: shape mismatch");
+  const bool out_f32 = out.scalar_type() == at::kFloat;
+  TORCH_CHECK(out_f32 || out.scalar_type() == at::kBFloat16, "blaslt_mx_gemm: bf16 / fp32 output");
+  State& s = state();
+  hipStream_t stream = at::hip::getCurrentHIPStream();
+  F8Plan* plan = nullptr;
+  void* ws = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(s.mu);
+    if (s.handle == nullptr) {
+      if (!check(hipblasLtCreate(&s.handle))) return false;
+      s.workspace = torch::empty({(int64_t)kWorkspace}, out.options().dtype(torch::kUInt8));
+    }
+    auto key = std::make_tuple(M, N, K, (int)ta, (int)tb, (int)out_f32, (int)out.get_device());
+    auto& plans = mxstate().plans;
+    auto it = plans.find(key);
+    if (it == plans.end()) {
+      F8Plan p;
+      build_mx_plan(s, p, M, N, K, ta, tb, out_f32, stream, out);
+      it = plans.emplace(key, p).first;
+    }
+    plan = &it->second;
+    if (!plan->ok) return false;
+    if (!set_mx_scales(plan->desc, sa.data_ptr(), sb.data_ptr())) return false;
+    ws = workspace_for(s, stream, out);
+  }
+  const float one = 1.f, beta = accumulate ? 1.f : 0.f;
+  return check(hipblasLtMatmul(s.handle, plan->desc, &one, b.data_ptr(), plan->la, a.data_ptr(), plan->lb, &beta,
+                               out.data_ptr(), plan->lc, out.data_ptr(), plan->lc, &plan->algo, ws, kWorkspace, stream));
+}
+
 // [(M, N, K, candidates, best ms)] of every fp8 problem searched so far.
 std::vector<std::tuple<int64_t, int64_t, int64_t, int64_t, double>> blaslt_fp8_plans() {
   std::vector<std::tuple<int64_t, int64_t, int64_t, int64_t, double>> out;

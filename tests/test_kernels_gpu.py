@@ -1290,3 +1290,22 @@ def test_blaslt_fp8_dynamic_shapes_match_reference():
         assert _rel(out, ref) < 1e-3, (lo, hi, _rel(out, ref))
     after = ext().blaslt_fp8_dynamic_stats()
     assert after[0] > before[0] and after[1] > before[1]  # bucket searches happened and some calls ran without one
+
+
+def test_blaslt_mx_gemm_matches_dequantised_product():
+    """hipBLASLt block-scaled (VEC32_UE8M0) runner, the library baseline of the MXFP8 path: with the scales in block
+    order, row-major [rows, K/32], it reproduces the dequantised fp32 product of our MX quantiser's output."""
+    from accelerate_hpc_test_amd.ops import fp8
+    from accelerate_hpc_test_amd.ops._ext import ext
+
+    torch.manual_seed(0)
+    M, N, K = 512, 768, 1024
+    a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    b = torch.randn(N, K, device=DEV, dtype=torch.bfloat16)
+    qa, sa = fp8.mx_quant(a, colwise=False)[:2]
+    qb, sb = fp8.mx_quant(b, colwise=False)[:2]
+    ref = fp8.mx_dequant(qa, sa) @ fp8.mx_dequant(qb, sb).t()
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    assert ext().blaslt_mx_gemm(qa, qb, fp8.mx_scales_natural(sa).contiguous(), fp8.mx_scales_natural(sb).contiguous(),
+                                out, False)
+    assert _rel(out, ref) < 1e-2, _rel(out, ref)

@@ -50,6 +50,8 @@ for step in "$@"; do
     long32k) run long32k 900 python bench.py --seq 32768 --steps 2 --warmup 1 --activation-checkpointing --verbose $BENCH_ARGS ;;
     long64k) run long64k 900 python bench.py --seq 65536 --steps 2 --warmup 1 --activation-checkpointing --verbose $BENCH_ARGS ;;
     bench8b_fp8) run bench8b_fp8 600 python bench.py --steps 5 --warmup 2 --precision fp8 $BENCH_ARGS ;;
+    mxprobe) run mxprobe 300 python tools/debug/mx_blaslt_probe.py ;;
+    bench8b_mxfp8) run bench8b_mxfp8 600 python bench.py --steps 5 --warmup 2 --precision mxfp8 $BENCH_ARGS ;;
     bench8b_ddp) run bench8b_ddp 600 python bench.py --parallel ddp --steps 5 --warmup 2 $BENCH_ARGS ;;
     bench8b_ddp_forced) run bench8b_ddp_forced 600 python bench.py --parallel ddp --ddp-force --steps 5 --warmup 2 $BENCH_ARGS ;;
     prof_ddp_forced) prof prof_ddp_forced 600 bench.py --parallel ddp --ddp-force --steps 3 --warmup 2 $BENCH_ARGS ;;
