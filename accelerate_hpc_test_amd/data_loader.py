@@ -83,6 +83,13 @@ class SeedableRandomSampler(RandomSampler):
         self.epoch = epoch
 
 
+def _check_divisible(who: str, batch_size, num_processes: int):
+    """split_batches cuts every batch into num_processes equal slices, so the batch size must divide evenly."""
+    if batch_size is None or batch_size % num_processes:
+        raise ValueError(f"{who}: split_batches=True cuts each batch into {num_processes} equal slices, which a "
+                         f"batch size of {batch_size} does not allow")
+
+
 class BatchSamplerShard(BatchSampler):
     """Yield only this process's batches of a wrapped `BatchSampler`.
 
@@ -92,31 +99,18 @@ class BatchSamplerShard(BatchSampler):
     start of the data so that every process sees the same number of same-sized batches.
     """
 
-    def __init__(
-        self,
-        batch_sampler: BatchSampler,
-        num_processes: int = 1,
-        process_index: int = 0,
-        split_batches: bool = False,
-        even_batches: bool = True,
-    ):
-        if split_batches and batch_sampler.batch_size % num_processes != 0:
-            raise ValueError(
-                f"To use `BatchSamplerShard` in `split_batches` mode, the batch size ({batch_sampler.batch_size}) "
-                f"needs to be a round multiple of the number of processes ({num_processes})."
-            )
-        self.batch_sampler = batch_sampler
-        self.num_processes = num_processes
-        self.process_index = process_index
-        self.split_batches = split_batches
-        self.even_batches = even_batches
-        self.batch_size = getattr(batch_sampler, "batch_size", None)
+    def __init__(self, batch_sampler: BatchSampler, num_processes: int = 1, process_index: int = 0,
+                 split_batches: bool = False, even_batches: bool = True):
+        bs = getattr(batch_sampler, "batch_size", None)
+        if split_batches:
+            _check_divisible("BatchSamplerShard", bs, num_processes)
+        if bs is None and even_batches:
+            raise ValueError("BatchSamplerShard: a batch sampler without a fixed batch_size can only be sharded with "
+                             "even_batches=False (Accelerator(even_batches=False) when prepared by the Accelerator)")
+        self.batch_sampler, self.batch_size = batch_sampler, bs
+        self.num_processes, self.process_index = num_processes, process_index
+        self.split_batches, self.even_batches = split_batches, even_batches
         self.drop_last = getattr(batch_sampler, "drop_last", False)
-        if self.batch_size is None and self.even_batches:
-            raise ValueError(
-                "You need to use `even_batches=False` when the batch sampler has no batch size. If you "
-                "are not calling this method directly, set `accelerator.even_batches=False` instead."
-            )
 
     @property
     def total_length(self):
@@ -208,11 +202,8 @@ class IterableDatasetShard(IterableDataset):
         process_index: int = 0,
         split_batches: bool = False,
     ):
-        if split_batches and batch_size > 1 and batch_size % num_processes != 0:
-            raise ValueError(
-                f"To use `IterableDatasetShard` in `split_batches` mode, the batch size ({batch_size}) "
-                f"needs to be a round multiple of the number of processes ({num_processes})."
-            )
+        if split_batches and batch_size > 1:
+            _check_divisible("IterableDatasetShard", batch_size, num_processes)
         self.dataset = dataset
         self.batch_size = batch_size
         self.drop_last = drop_last
