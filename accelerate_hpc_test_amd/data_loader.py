@@ -848,60 +848,41 @@ class SkipDataLoader(DataLoaderStateMixin, DataLoader):
         return self.batch_size or 1
 
 
-def skip_first_batches(dataloader, num_batches=0):
-    """A dataloader equivalent to `dataloader` that skips its first `num_batches` batches (resume mid-epoch)."""
-    state = PartialState()
-    dataset = dataloader.dataset
-    sampler_is_batch_sampler = False
-    if isinstance(dataset, IterableDataset):
-        new_batch_sampler = None
-    else:
-        sampler_is_batch_sampler = isinstance(dataloader.sampler, BatchSampler)
-        batch_sampler = dataloader.sampler if sampler_is_batch_sampler else dataloader.batch_sampler
-        new_batch_sampler = SkipBatchSampler(batch_sampler, skip_batches=num_batches)
+_SAMPLING_KWARGS = frozenset({"batch_size", "shuffle", "sampler", "batch_sampler", "drop_last"})
 
-    ignore_kwargs = ["batch_size", "shuffle", "sampler", "batch_sampler", "drop_last"]
-    kwargs = {
-        k: getattr(dataloader, k, _PYTORCH_DATALOADER_KWARGS[k])
-        for k in _PYTORCH_DATALOADER_KWARGS
-        if k not in ignore_kwargs and hasattr(dataloader, k)
-    }
-    if new_batch_sampler is None:
-        kwargs["drop_last"] = dataloader.drop_last
-        kwargs["batch_size"] = dataloader.batch_size
+
+def skip_first_batches(dataloader, num_batches=0):
+    """A loader equivalent to `dataloader` that starts after its first `num_batches` batches (mid-epoch resume).
+
+    Map-style data: the (batch) sampler is wrapped in a `SkipBatchSampler`, so skipped batches are never loaded or
+    uploaded. Iterable data has no sampler to advance: the new loader drops the first batches it produces."""
+    dataset = dataloader.dataset
+    kw = {k: getattr(dataloader, k) for k in _PYTORCH_DATALOADER_KWARGS
+          if k not in _SAMPLING_KWARGS and hasattr(dataloader, k)}
+    if isinstance(dataset, IterableDataset):
+        kw.update(batch_size=dataloader.batch_size, drop_last=dataloader.drop_last)
+        skipped, sampler_is_batches = None, False
+    else:
+        sampler_is_batches = isinstance(dataloader.sampler, BatchSampler)
+        source = dataloader.sampler if sampler_is_batches else dataloader.batch_sampler
+        skipped = SkipBatchSampler(source, skip_batches=num_batches)
 
     if isinstance(dataloader, DataLoaderDispatcher):
-        if new_batch_sampler is None:
-            kwargs["skip_batches"] = num_batches
-        kwargs.pop("generator", None)
-        dataloader = DataLoaderDispatcher(
-            dataset,
-            split_batches=dataloader.split_batches,
-            batch_sampler=new_batch_sampler,
-            _drop_last=dataloader._drop_last,
-            **kwargs,
-        )
-    elif isinstance(dataloader, DataLoaderShard):
-        if new_batch_sampler is None:
-            kwargs["skip_batches"] = num_batches
-        elif sampler_is_batch_sampler:
-            kwargs["sampler"] = new_batch_sampler
-            kwargs["batch_size"] = dataloader.batch_size
+        kw.pop("generator", None)  # rank 0 draws the batches; the dispatcher makes its own generator
+        kw.update({"skip_batches": num_batches} if skipped is None else {"batch_sampler": skipped})
+        return DataLoaderDispatcher(dataset, split_batches=dataloader.split_batches,
+                                    _drop_last=dataloader._drop_last, **kw)
+    if isinstance(dataloader, DataLoaderShard):
+        if skipped is None:
+            kw["skip_batches"] = num_batches
+        elif sampler_is_batches:
+            kw.update(sampler=skipped, batch_size=dataloader.batch_size)
         else:
-            kwargs["batch_sampler"] = new_batch_sampler
-        dataloader = DataLoaderShard(
-            dataset,
-            device=dataloader.device,
-            rng_types=dataloader.rng_types,
-            synchronized_generator=dataloader.synchronized_generator,
-            _drop_last=dataloader._drop_last,
-            prefetch_to_device=dataloader.prefetch_to_device,
-            **kwargs,
-        )
-    else:
-        if new_batch_sampler is None:
-            dataloader = SkipDataLoader(dataset, skip_batches=num_batches, **kwargs)
-        else:
-            dataloader = DataLoader(dataset, batch_sampler=new_batch_sampler, **kwargs)
-    _ = state
-    return dataloader
+            kw["batch_sampler"] = skipped
+        return DataLoaderShard(dataset, device=dataloader.device, rng_types=dataloader.rng_types,
+                               synchronized_generator=dataloader.synchronized_generator,
+                               _drop_last=dataloader._drop_last, prefetch_to_device=dataloader.prefetch_to_device,
+                               **kw)
+    if skipped is None:
+        return SkipDataLoader(dataset, skip_batches=num_batches, **kw)
+    return DataLoader(dataset, batch_sampler=skipped, **kw)
