@@ -517,42 +517,32 @@ class DataLoaderShard(DataLoaderStateMixin, DataLoader):
         self._resume_skip = state_dict.get("batches_yielded", 0)
 
 
+def _shuffling_datapipe(dataset) -> bool:
+    try:
+        from torch.utils.data.datapipes.iter.combinatorics import ShufflerIterDataPipe
+    except ImportError:
+        return False
+    return isinstance(dataset, ShufflerIterDataPipe) and bool(dataset._shuffle_enabled)
+
+
 class DataLoaderDispatcher(DataLoaderStateMixin, DataLoader):
     """Rank 0 iterates the underlying loader and broadcasts each (concatenated or split) batch; every rank
     keeps its slice. One object broadcast (structure) + one coalesced tensor broadcast per step."""
 
-    def __init__(
-        self,
-        dataset,
-        split_batches: bool = False,
-        skip_batches=0,
-        use_stateful_dataloader=False,
-        _drop_last: bool = False,
-        _non_blocking: bool = False,
-        slice_fn=None,
-        torch_device_mesh=None,
-        **kwargs,
-    ):
-        shuffle = False
-        from torch.utils.data.datapipes.iter.combinatorics import ShufflerIterDataPipe
-
-        if isinstance(dataset, ShufflerIterDataPipe):
-            shuffle = dataset._shuffle_enabled
+    def __init__(self, dataset, split_batches: bool = False, skip_batches=0, use_stateful_dataloader=False,
+                 _drop_last: bool = False, _non_blocking: bool = False, slice_fn=None, torch_device_mesh=None,
+                 **kwargs):
+        reshuffle = _shuffling_datapipe(dataset)  # DataLoader.__init__ resets a shuffler datapipe's switch
         super().__init__(dataset, **kwargs)
-        self.split_batches = split_batches
-        if shuffle:
-            torch.utils.data.graph_settings.apply_shuffle_settings(dataset, shuffle=shuffle)
-        self.gradient_state = GradientState()
-        self.state = PartialState()
-        self._drop_last = _drop_last
-        self._non_blocking = _non_blocking
-        self.skip_batches = skip_batches
+        if reshuffle:
+            torch.utils.data.graph_settings.apply_shuffle_settings(dataset, shuffle=True)
+        self.state, self.gradient_state = PartialState(), GradientState()
+        self.split_batches, self.skip_batches = split_batches, skip_batches
+        self._drop_last, self._non_blocking = _drop_last, _non_blocking
+        self.slice_fn = slice_fn or slice_tensors
         self.torch_device_mesh = torch_device_mesh
-        self.slice_fn = slice_tensors if slice_fn is None else slice_fn
-        self.iteration = 0
         self.use_stateful_dataloader = use_stateful_dataloader
-        self._batches_yielded = 0
-        self._resume_skip = 0
+        self.iteration = self._batches_yielded = self._resume_skip = 0
 
     _MIXED_SIZES = ("You can't use batches of different size with `dispatch_batches=True` or when using an `IterableDataset`. "
                     "Either pass `dispatch_batches=False` and have each process fetch its own batch or pass "
