@@ -171,6 +171,15 @@ class _CheckpointRotation:
     def custom_state_files(folder: str) -> list:
         return [f for f in os.listdir(folder) if re.fullmatch(r"custom_checkpoint_\d+\.pkl", f)]
 
+
+def _only_tensors(data) -> bool:
+    """True when `data` is a (nested) structure of tensors only."""
+    try:
+        recursively_apply(lambda x: x, data, error_on_other_type=True)
+    except TypeError:
+        return False
+    return True
+
 class Accelerator:
     def __init__(
         self,
@@ -1023,32 +1032,20 @@ class Accelerator:
         return gather(tensor)
 
     def gather_for_metrics(self, input_data, use_gather_object=False):
-        try:
-            recursively_apply(lambda x: x, input_data, error_on_other_type=True)
-            all_tensors = True
-        except TypeError:
-            all_tensors = False
-        use_gather_object = use_gather_object or not all_tensors
-        if use_gather_object:
-            data = gather_object(input_data)
-        else:
-            data = self.gather(input_data)
-        try:
-            if self.gradient_state.end_of_dataloader:
-                if self.gradient_state.remainder == -1:
-                    logger.info("The used dataset had no length, returning gathered tensors. You should drop the remainder yourself.")
-                    return data
-                elif self.gradient_state.remainder > 0:
-                    def _adjust_samples(tensor):
-                        return tensor[: self.gradient_state.remainder]
-
-                    if use_gather_object:
-                        return _adjust_samples(data)
-                    return recursively_apply(_adjust_samples, data)
-                return data
+        """Gather `input_data` from every process for metric computation. On the last batch of a loader that
+        `even_batches` padded, the duplicated samples are dropped (`GradientState.remainder` real samples are kept).
+        Anything that is not purely tensors goes through `gather_object` (a flat list)."""
+        as_objects = use_gather_object or not _only_tensors(input_data)
+        data = gather_object(input_data) if as_objects else self.gather(input_data)
+        if not self.gradient_state.end_of_dataloader:
             return data
-        except Exception:
+        keep = self.gradient_state.remainder
+        if keep == -1:
+            logger.info("gather_for_metrics: the loader has no length, so padding duplicates in its last batch "
+                        "cannot be dropped here; returning everything gathered")
+        if keep is None or keep <= 0:
             return data
+        return data[:keep] if as_objects else recursively_apply(lambda t: t[:keep], data)
 
     def reduce(self, tensor, reduction="sum", scale=1.0):
         return reduce(tensor, reduction, scale)
