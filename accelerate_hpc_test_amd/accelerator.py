@@ -925,22 +925,14 @@ class Accelerator:
         return optimizer
 
     def prepare_scheduler(self, scheduler):
-        if getattr(scheduler, "_is_accelerate_prepared", False):
-            if scheduler not in self._schedulers:
-                self._schedulers.append(scheduler)
-            return scheduler
-        optimizer = self._optimizers
-        for opt in self._optimizers:
-            if getattr(scheduler, "optimizer", None) == opt.optimizer:
-                optimizer = opt
-                break
-        scheduler = AcceleratedScheduler(
-            scheduler,
-            optimizer,
-            step_with_optimizer=self.step_scheduler_with_optimizer,
-            split_batches=self.split_batches,
-        )
-        self._schedulers.append(scheduler)
+        """Wrap an LR scheduler so it steps with its (prepared) optimizer; an already-wrapped one is only registered."""
+        if not getattr(scheduler, "_is_accelerate_prepared", False):
+            inner = getattr(scheduler, "optimizer", None)
+            owner = next((o for o in self._optimizers if o.optimizer == inner), self._optimizers)
+            scheduler = AcceleratedScheduler(scheduler, owner, step_with_optimizer=self.step_scheduler_with_optimizer,
+                                             split_batches=self.split_batches)
+        if scheduler not in self._schedulers:
+            self._schedulers.append(scheduler)
         return scheduler
 
     # ============================================================================== training step helpers
