@@ -81,6 +81,15 @@ def test_skip_helpers_match_upstream():
         x = [t.tolist() for t in ours.skip_first_batches(dl, skip)]
         y = [t.tolist() for t in up.skip_first_batches(dl, skip)]
         assert x == y, (n, bs, skip)
+        # the other two branches: a BatchSampler passed as the sampler (batch_size=None), and iterable data
+        dl = DataLoader(list(range(n)), sampler=sampler, batch_size=None)
+        x = [torch.as_tensor(t).tolist() for t in ours.skip_first_batches(dl, skip)]
+        y = [torch.as_tensor(t).tolist() for t in up.skip_first_batches(dl, skip)]
+        assert x == y, ("batch sampler as sampler", n, bs, skip)
+        dl = DataLoader(_Range(n), batch_size=bs)
+        x = [t.tolist() for t in ours.skip_first_batches(dl, skip)]
+        y = [t.tolist() for t in up.skip_first_batches(dl, skip)]
+        assert x == y, ("iterable", n, bs, skip)
 
 
 def test_seedable_sampler_permutations_match_upstream():
