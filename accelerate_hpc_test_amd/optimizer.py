@@ -14,6 +14,7 @@ disable.
 
 from __future__ import annotations
 
+import contextlib
 import inspect
 import os
 
@@ -25,13 +26,37 @@ from .utils.operations import honor_type
 
 
 def move_to_device(state, device):
-    if isinstance(state, (list, tuple)):
-        return honor_type(state, (move_to_device(t, device) for t in state))
-    elif isinstance(state, dict):
-        return type(state)({k: move_to_device(v, device) for k, v in state.items()})
-    elif isinstance(state, torch.Tensor):
+    """Every tensor of a nested optimizer-state structure moved to `device`; containers keep their types."""
+    if isinstance(state, torch.Tensor):
         return state.to(device)
+    if isinstance(state, dict):
+        return type(state)((k, move_to_device(v, device)) for k, v in state.items())
+    if isinstance(state, (list, tuple)):
+        return honor_type(state, [move_to_device(v, device) for v in state])
     return state
+
+
+@contextlib.contextmanager
+def _record_inner_steps(optimizer):
+    """Within the block, calls of `optimizer.step` are counted into the yielded list. A GradScaler skips the inner
+    step when it found inf/nan gradients, so an empty list afterwards means the step was skipped. Whatever `step`
+    the instance carried before (e.g. an LR scheduler's call counter) is put back afterwards."""
+    own = vars(optimizer).get("step")
+    inner = optimizer.step
+    calls = []
+
+    def counted(*args, **kwargs):
+        calls.append(True)
+        return inner(*args, **kwargs)
+
+    optimizer.step = counted
+    try:
+        yield calls
+    finally:
+        if own is None:
+            del optimizer.step
+        else:
+            optimizer.step = own
 
 
 def _fused_adam_eligible(optimizer):
@@ -67,12 +92,6 @@ class AcceleratedOptimizer(torch.optim.Optimizer):
         self.device_placement = device_placement
         self._is_overflow = False
         self._fused_step = None
-
-        if self.scaler is not None:
-            self._accelerate_step_called = False
-            self._optimizer_original_step_method = self.optimizer.step
-            self._optimizer_patched_step_method = patch_optimizer_step(self, self.optimizer.step)
-
         if device_placement:
             state_dict = self.optimizer.state_dict()
             state_dict["state"] = move_to_device(state_dict["state"], self.accelerator_state.device)
@@ -130,19 +149,18 @@ class AcceleratedOptimizer(torch.optim.Optimizer):
         return self.optimizer.state_dict()
 
     def zero_grad(self, set_to_none=None):
-        if self.gradient_state.sync_gradients:
-            accept_arg = "set_to_none" in inspect.signature(self.optimizer.zero_grad).parameters
-            if accept_arg:
-                if set_to_none is None:
-                    set_to_none = True
-                self.optimizer.zero_grad(set_to_none=set_to_none)
-            else:
-                if set_to_none is not None:
-                    raise ValueError("`set_to_none` for Optimizer.zero_grad` is not supported by this optimizer.")
-                self.optimizer.zero_grad()
-            hook = getattr(self.optimizer, "_accelerate_post_zero_grad", None)
-            if hook is not None:
-                hook()
+        """Clear gradients at accumulation boundaries only (`set_to_none` defaults to True where supported)."""
+        if not self.gradient_state.sync_gradients:
+            return
+        if "set_to_none" in inspect.signature(self.optimizer.zero_grad).parameters:
+            self.optimizer.zero_grad(set_to_none=True if set_to_none is None else set_to_none)
+        elif set_to_none is None:
+            self.optimizer.zero_grad()
+        else:
+            raise ValueError(f"{type(self.optimizer).__name__}.zero_grad() takes no `set_to_none` argument")
+        hook = getattr(self.optimizer, "_accelerate_post_zero_grad", None)
+        if hook is not None:
+            hook()
 
     def train(self):
         if hasattr(self.optimizer, "train") and callable(self.optimizer.train):
@@ -188,19 +206,13 @@ class AcceleratedOptimizer(torch.optim.Optimizer):
         if not self.gradient_state.sync_gradients:
             return
         if self.scaler is not None:
-            self.optimizer.step = self._optimizer_patched_step_method
-            self.scaler.step(self.optimizer, closure)
+            with _record_inner_steps(self.optimizer) as calls:
+                self.scaler.step(self.optimizer, closure)
             self.scaler.update()
-            if not self._accelerate_step_called:
-                self._is_overflow = True
-            else:
-                self._is_overflow = False
-            self.optimizer.step = self._optimizer_original_step_method
-            self._accelerate_step_called = False
+            self._is_overflow = not calls
+            self.optimizer._acc_last_step_fused = False
         else:
             self._inner_step(closure)
-        if self.scaler is not None:
-            self.optimizer._acc_last_step_fused = False
         post = getattr(self.optimizer, "_accelerate_post_step", None)
         if post is not None:
             post()
@@ -215,18 +227,14 @@ class AcceleratedOptimizer(torch.optim.Optimizer):
         """Whether the last optimizer step was skipped because of fp16 overflow."""
         return self._is_overflow
 
+    _UNPICKLED = frozenset({"_fused_step", "_overlap_engine"})  # rebuilt lazily / re-attached by the engine
+
     def __getstate__(self):
-        _ignored_keys = ["_accelerate_step_called", "_optimizer_original_step_method", "_optimizer_patched_step_method", "_fused_step",
-                         "_overlap_engine"]
-        return {k: v for k, v in self.__dict__.items() if k not in _ignored_keys}
+        return {k: v for k, v in self.__dict__.items() if k not in self._UNPICKLED}
 
     def __setstate__(self, state):
         self.__dict__.update(state)
         self._fused_step = None
-        if self.scaler is not None:
-            self._accelerate_step_called = False
-            self._optimizer_original_step_method = self.optimizer.step
-            self._optimizer_patched_step_method = patch_optimizer_step(self, self.optimizer.step)
 
 
 def _step_filtered(optimizer, only=None, skip=None):
@@ -241,10 +249,3 @@ def _step_filtered(optimizer, only=None, skip=None):
         for g, ps in zip(optimizer.param_groups, saved):
             g["params"] = ps
 
-
-def patch_optimizer_step(accelerated_optimizer: AcceleratedOptimizer, method):
-    def patched_step(*args, **kwargs):
-        accelerated_optimizer._accelerate_step_called = True
-        return method(*args, **kwargs)
-
-    return patched_step

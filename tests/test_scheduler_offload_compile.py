@@ -108,3 +108,28 @@ def test_compile_regions_compiles_repeated_blocks():
     out = comp(x)
     assert torch.allclose(out, ref)
     assert all(type(layer).__name__ == "OptimizedModule" for layer in comp.layers), [type(l) for l in comp.layers]
+
+
+def test_accelerated_optimizer_reports_scaler_skipped_steps():
+    """With a GradScaler, an inf gradient makes the scaler skip the inner step: `step_was_skipped` says so, the
+    parameter is untouched, and whatever `step` the optimizer instance carried (an LR scheduler's counter) survives."""
+    from accelerate_hpc_test_amd.optimizer import AcceleratedOptimizer
+
+    w = torch.nn.Parameter(torch.ones(4))
+    inner = torch.optim.SGD([w], lr=0.1)
+    sched = torch.optim.lr_scheduler.StepLR(inner, step_size=1)
+    carried = vars(inner).get("step")
+    opt = AcceleratedOptimizer(inner, device_placement=False, scaler=torch.amp.GradScaler("cpu", init_scale=4.0))
+
+    opt.scaler.scale(torch.ones(()))  # a real loop scales its loss first; that initialises the scale
+    w.grad = torch.full((4,), float("inf"))
+    opt.step()
+    assert opt.step_was_skipped and torch.equal(w.detach(), torch.ones(4))
+    assert vars(inner).get("step") is carried
+
+    w.grad = torch.ones(4) * opt.scaler.get_scale()
+    opt.step()
+    assert not opt.step_was_skipped
+    assert torch.allclose(w.detach(), torch.full((4,), 0.9))
+    assert vars(inner).get("step") is carried
+    sched.step()
