@@ -186,6 +186,7 @@ class DistributedDataParallel(nn.Module):
         self._sync_params_and_buffers()
         self._build_buckets()
         self._fused_slots = []
+        self._fused_ids: set = set()  # ids of the weights whose gradient the fused GEMM writes (kept here, not on them)
         if os.environ.get("ACCELERATE_DDP_FUSED_WGRAD", "1") != "0":
             self._install_fused_wgrad()
 
@@ -251,9 +252,13 @@ class DistributedDataParallel(nn.Module):
             cur_dtype = p.dtype
         if cur:
             self.buckets.append(_Bucket(cur, cur_dtype, self.device))
+        owner = weakref.ref(self)
         for bi, b in enumerate(self.buckets):
             for p in b.params:
                 self._param_bucket[p] = bi
+                # the newest reducer owns the parameter: hooks of an earlier wrapper of the same model (re-prepared
+                # after free_memory, or by a second Accelerator) stay registered but stand down
+                p._acc_ddp_owner = owner
                 p.register_post_accumulate_grad_hook(_weak_method_hook(self, "_grad_hook"))
         self._assign_grad_views(zero=True)
 
@@ -274,11 +279,13 @@ class DistributedDataParallel(nn.Module):
                     refs[id(q)] = refs.get(id(q), 0) + 1
         for m in self.module.modules():
             w = getattr(m, "weight", None)
-            if type(m) is nn.Linear and w is not None and w.requires_grad and refs.get(id(w), 0) == 1 \
+            # a module an earlier reducer already converted is re-bound to this one (its old slot would write into
+            # the old reducer's buckets, or nowhere once that reducer is gone)
+            if type(m) in (nn.Linear, _DDPFusedLinear) and w is not None and w.requires_grad and refs.get(id(w), 0) == 1 \
                     and w in self._param_bucket and w.dtype == self.buckets[self._param_bucket[w]].buffer.dtype:
                 m.__class__ = _DDPFusedLinear
                 m._acc_ddp_slot = _DDPWgradSlot(self, w)
-                w._acc_ddp_fused = True
+                self._fused_ids.add(id(w))
                 self._fused_slots.append(m._acc_ddp_slot)
 
     @torch.no_grad()
@@ -331,7 +338,10 @@ class DistributedDataParallel(nn.Module):
 
     # ------------------------------------------------------------------------------------------ reduce
     def _grad_hook(self, p):
-        if getattr(p, "_acc_ddp_fused", False):
+        owner = getattr(p, "_acc_ddp_owner", None)
+        if owner is not None and owner() is not self:
+            return  # a later reducer wraps this parameter now
+        if id(p) in self._fused_ids:
             return  # autograd still runs the hook of a weight whose Function returned no grad; the GEMM counted it
         b = self.buckets[self._param_bucket[p]]
         if p.grad is not None and b.buffer.numel() and p.grad.data_ptr() != self._slot_ptr(b, p):
