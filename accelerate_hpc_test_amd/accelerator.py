@@ -371,12 +371,24 @@ class Accelerator:
         self._watchdog = StepWatchdog.from_env(self.rccl_handler.watchdog_timeout, rank=self.process_index)
         self._fault_injector = FaultInjector.from_env(self.process_index)
         check_os_kernel()
-        if (self.device.type == "cuda" and self.num_processes > 1 and self.local_process_index == 0
+        if (self.device.type == "cuda" and self.num_processes > 1
                 and os.environ.get("ACCELERATE_CHECK_TOPOLOGY", "1") != "0"):
-            # xGMI links between this node's GPUs, P2P / IPC switches (parallel/topology.py)
+            # xGMI links between this node's GPUs, P2P / IPC switches (parallel/topology.py). Local rank 0
+            # inspects (rocm-smi once per node); with ACCELERATE_STRICT_TOPOLOGY=1 the verdict is all-reduced so that
+            # EVERY rank raises, instead of the others hanging at their first collective
             from .parallel.topology import validate_comm_environment
 
-            validate_comm_environment(int(os.environ.get("LOCAL_WORLD_SIZE", self.num_processes) or self.num_processes))
+            strict = os.environ.get("ACCELERATE_STRICT_TOPOLOGY", "0") == "1"
+            problems = []
+            if self.local_process_index == 0:
+                problems = validate_comm_environment(
+                    int(os.environ.get("LOCAL_WORLD_SIZE", self.num_processes) or self.num_processes), strict=False)
+            if strict:
+                flag = torch.tensor([1.0 if problems else 0.0], device=self.device)
+                torch.distributed.all_reduce(flag)
+                if flag.item() > 0:
+                    raise RuntimeError("communication environment check failed on a node (ACCELERATE_STRICT_TOPOLOGY=1)"
+                                       + (": " + "; ".join(problems) if problems else ""))
 
     # ============================================================================== properties
     # Read-through views of the process state and the dataloader / project configurations (`_delegate`, module

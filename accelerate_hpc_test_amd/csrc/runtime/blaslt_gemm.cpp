@@ -33,7 +33,16 @@ struct Plan {
   bool ok = false;
   float ms = 0.f;
   int candidates = 0;
+  int64_t T = 0;  // the token count the layouts (and the timed search) were built for
 };
+
+// power-of-two buckets from 256: problems within a factor of two share one timed search (variable-length batches would
+// otherwise search — and synchronise inside backward — once per distinct token count, and grow the cache without bound)
+int64_t dim_bucket(int64_t x) {
+  int64_t b = 256;
+  while (b < x) b <<= 1;
+  return b;
+}
 
 struct State {
   hipblasLtHandle_t handle = nullptr;
@@ -116,7 +125,43 @@ bool build_plan(State& s, Plan& p, int64_t T, int64_t N, int64_t K, bool x_t, hi
   hipEventDestroy(e0);
   hipEventDestroy(e1);
   p.ms = best / 3.f;
+  p.T = T;
   return p.ok;
+}
+
+// Token count T of a bucket whose plan was searched on another T: per-call layouts (host objects), the bucket's algorithm
+// when hipBLASLt supports it for this problem, else the heuristic's first choice — no timing, no synchronisation.
+bool run_wgrad_other_t(State& s, Plan& plan, int64_t T, int64_t N, int64_t K, bool x_t, const void* x, const void* dy,
+                       void* out, float beta, void* ws, hipStream_t stream) {
+  hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, lc = nullptr;
+  bool ok = check(x_t ? hipblasLtMatrixLayoutCreate(&la, HIP_R_16BF, T, K, T) : hipblasLtMatrixLayoutCreate(&la, HIP_R_16BF, K, T, K)) &&
+            check(hipblasLtMatrixLayoutCreate(&lb, HIP_R_16BF, N, T, N)) && check(hipblasLtMatrixLayoutCreate(&lc, HIP_R_32F, K, N, K));
+  const float one = 1.f;
+  hipblasLtMatmulAlgo_t algo = plan.algo;
+  if (ok) {
+    size_t wsz = 0;
+    if (hipblaslt_ext::matmulIsAlgoSupported(s.handle, plan.desc, (void*)&one, la, lb, (void*)&beta, lc, lc, algo, wsz) !=
+            HIPBLAS_STATUS_SUCCESS || wsz > kWorkspace) {
+      hipblasLtMatmulPreference_t pref;
+      ok = check(hipblasLtMatmulPreferenceCreate(&pref));
+      if (ok) {
+        uint64_t wsl = kWorkspace;
+        hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsl, sizeof(wsl));
+        hipblasLtMatmulHeuristicResult_t r;
+        int got = 0;
+        ok = check(hipblasLtMatmulAlgoGetHeuristic(s.handle, plan.desc, la, lb, lc, lc, pref, 1, &r, &got)) && got > 0 &&
+             r.state == HIPBLAS_STATUS_SUCCESS;
+        if (ok) algo = r.algo;
+        hipblasLtMatmulPreferenceDestroy(pref);
+      }
+    }
+  }
+  if (ok)
+    ok = check(hipblasLtMatmul(s.handle, plan.desc, &one, x, la, dy, lb, &beta, out, lc, out, lc, &algo, ws, kWorkspace, stream));
+  if (la) hipblasLtMatrixLayoutDestroy(la);
+  if (lb) hipblasLtMatrixLayoutDestroy(lb);
+  if (lc) hipblasLtMatrixLayoutDestroy(lc);
+  return ok;
 }
 
 }  // namespace
@@ -141,7 +186,7 @@ bool blaslt_wgrad_f32(torch::Tensor dy, torch::Tensor x, torch::Tensor out, bool
       s.workspace = torch::empty({(int64_t)kWorkspace}, out.options().dtype(torch::kUInt8));
     }
     const int dev = out.get_device();
-    auto key = std::make_tuple(T, N, K, dev, x_t);
+    auto key = std::make_tuple(dim_bucket(T), N, K, dev, x_t);
     auto it = s.plans.find(key);
     if (it == s.plans.end()) {
       Plan p;
@@ -150,6 +195,9 @@ bool blaslt_wgrad_f32(torch::Tensor dy, torch::Tensor x, torch::Tensor out, bool
     }
     plan = &it->second;
     ws = workspace_for(s, stream, out);
+    if (plan->ok && plan->T != T)
+      return run_wgrad_other_t(s, *plan, T, N, K, x_t, x.data_ptr(), dy.data_ptr(), out.data_ptr(), accumulate ? 1.f : 0.f,
+                               ws, stream);
   }
   if (!plan->ok) return false;
   const float one = 1.f, beta = accumulate ? 1.f : 0.f;
@@ -177,6 +225,8 @@ struct F8Plan {
   int64_t M = 0, K = 0;  // the problem the layouts (and the timed search) were built for
 };
 
+constexpr size_t kMaxExactF8 = 64;
+
 using F8Key = std::tuple<int64_t, int64_t, int64_t, int64_t, int64_t, int, int, int, int>;
 
 struct F8State {
@@ -187,13 +237,6 @@ struct F8State {
   std::map<F8Key, F8Plan> dyn_plans;
   int64_t dyn_calls = 0, dyn_reused = 0, dyn_heuristic = 0;
 };
-
-// power-of-two buckets from 256: problems within a factor of two share one timed search
-int64_t dim_bucket(int64_t x) {
-  int64_t b = 256;
-  while (b < x) b <<= 1;
-  return b;
-}
 
 F8State& f8state() {
   static F8State s;
@@ -346,6 +389,11 @@ bool blaslt_fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor sa, torch::
       if (!check(hipblasLtCreate(&s.handle))) return false;
       s.workspace = torch::empty({(int64_t)kWorkspace}, out.options().dtype(torch::kUInt8));
     }
+    // exact-problem searches are capped: past kMaxExactF8 distinct problems (variable-length batches) every new
+    // problem joins the power-of-two bucket family instead of getting a timed search of its own
+    if (!dynamic && fs.plans.size() >= kMaxExactF8 &&
+        fs.plans.find(std::make_tuple(M, N, K, lda, ldb, (int)ta, (int)tb, (int)out_f32, (int)out.get_device())) == fs.plans.end())
+      dynamic = true;
     auto& table = dynamic ? fs.dyn_plans : fs.plans;
     auto key = dynamic ? std::make_tuple(dim_bucket(M), N, dim_bucket(K), lda, ldb, (int)ta, (int)tb, (int)out_f32, (int)out.get_device())
                        : std::make_tuple(M, N, K, lda, ldb, (int)ta, (int)tb, (int)out_f32, (int)out.get_device());
@@ -362,10 +410,12 @@ bool blaslt_fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor sa, torch::
     if (dynamic)
       return run_dynamic(s, fs, *plan, M, N, K, lda, ldb, ta, tb, out_f32, a.data_ptr(), b.data_ptr(), out.data_ptr(),
                          (float)alpha, accumulate ? 1.f : 0.f, ws, stream);
+    // enqueued while the lock is held: the scale pointers just written into the shared descriptor belong to THIS call
+    // (another thread using the same plan could otherwise overwrite them before hipblasLtMatmul reads them)
+    const float al = (float)alpha, beta = accumulate ? 1.f : 0.f;
+    return check(hipblasLtMatmul(s.handle, plan->desc, &al, b.data_ptr(), plan->la, a.data_ptr(), plan->lb, &beta,
+                                 out.data_ptr(), plan->lc, out.data_ptr(), plan->lc, &plan->algo, ws, kWorkspace, stream));
   }
-  const float al = (float)alpha, beta = accumulate ? 1.f : 0.f;
-  return check(hipblasLtMatmul(s.handle, plan->desc, &al, b.data_ptr(), plan->la, a.data_ptr(), plan->lb, &beta,
-                               out.data_ptr(), plan->lc, out.data_ptr(), plan->lc, &plan->algo, ws, kWorkspace, stream));
 }
 
 // ------------------------------------------------------------------------------------------------ MXFP8 (block scales)
@@ -488,10 +538,10 @@ bool blaslt_mx_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor sa, torch::T
     if (!plan->ok) return false;
     if (!set_mx_scales(plan->desc, sa.data_ptr(), sb.data_ptr())) return false;
     ws = workspace_for(s, stream, out);
+    const float one = 1.f, beta = accumulate ? 1.f : 0.f;  // enqueued under the lock (scale pointers, as above)
+    return check(hipblasLtMatmul(s.handle, plan->desc, &one, b.data_ptr(), plan->la, a.data_ptr(), plan->lb, &beta,
+                                 out.data_ptr(), plan->lc, out.data_ptr(), plan->lc, &plan->algo, ws, kWorkspace, stream));
   }
-  const float one = 1.f, beta = accumulate ? 1.f : 0.f;
-  return check(hipblasLtMatmul(s.handle, plan->desc, &one, b.data_ptr(), plan->la, a.data_ptr(), plan->lb, &beta,
-                               out.data_ptr(), plan->lc, out.data_ptr(), plan->lc, &plan->algo, ws, kWorkspace, stream));
 }
 
 // [(M, N, K, candidates, best ms)] of every fp8 problem searched so far.

@@ -37,15 +37,17 @@ class MultiProcessAdapter(logging.LoggerAdapter):
         main_only = kwargs.pop("main_process_only", True)
         in_order = kwargs.pop("in_order", False) and not explicit_main_only  # an explicit main_process_only wins
         kwargs.setdefault("stacklevel", 2)
-        if not self.isEnabledFor(level):
-            return
+        enabled = self.isEnabledFor(level)
         if in_order and state.num_processes > 1:
             # every rank in turn, ALL ranks joining every barrier (the reference lets the main process log and return
-            # while the others wait on barriers it never enters)
+            # while the others wait on barriers it never enters) — also the ranks whose level filters the record out
+            # (per-rank levels are common: INFO on main, WARNING elsewhere), or the others would block on them
             for rank in range(state.num_processes):
-                if rank == state.process_index:
+                if rank == state.process_index and enabled:
                     self._emit(level, msg, args, kwargs)
                 state.wait_for_everyone()
+            return
+        if not enabled:
             return
         if not main_only or state.is_main_process:
             self._emit(level, msg, args, kwargs)

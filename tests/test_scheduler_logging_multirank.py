@@ -77,6 +77,12 @@ def _check_logging():
     assert sum(line.startswith("in order") for line in lines) == 1, lines
     assert any(line.startswith("explicit main only wins") for line in lines) == (me == 0), lines
     assert sum(line.startswith("once") for line in lines) == (1 if me == 0 else 0), lines
+    # per-rank levels (INFO on main, WARNING elsewhere): the filtered rank still joins the in-order barriers (advisor r3)
+    logger.logger.setLevel(logging.INFO if me == 0 else logging.WARNING)
+    logger.info("in order, filtered off main", in_order=True)
+    acc.wait_for_everyone()
+    lines = buf.getvalue().splitlines()
+    assert any(line.startswith("in order, filtered") for line in lines) == (me == 0), lines
 
 
 @pytest.mark.parametrize("split_batches,step_with_optimizer", [(False, True), (True, True), (False, False)])
