@@ -23,19 +23,25 @@ from .state import PartialState
 
 
 # ------------------------------------------------------------------------------------------------ structure
-def _find_block_list(model: nn.Module, no_split_module_classes=None):
+def _find_block_lists(model: nn.Module, no_split_module_classes=None):
+    """The model's repeated block lists, in registration order: every `ModuleList` of the no-split class (HF
+    `_no_split_modules`), e.g. T5's `encoder.block` and `decoder.block`; without class names, the largest list."""
     names = set(no_split_module_classes or getattr(model, "_no_split_modules", None) or [])
-    best, best_n = None, -1
+    lists, best, best_n = [], None, -1
     for name, m in model.named_modules():
         if isinstance(m, nn.ModuleList) and len(m) > 0:
-            if names and not any(type(c).__name__ in names for c in m):
+            if names:
+                if any(type(c).__name__ in names for c in m):
+                    lists.append((name, m))
                 continue
             n = sum(p.numel() for p in m.parameters())
             if n > best_n:
                 best, best_n = (name, m), n
-    if best is None:
+    if not names and best is not None:
+        lists = [best]
+    if not lists:
         raise ValueError("prepare_pippy: could not find the model's repeated block list (pass no_split_module_classes)")
-    return best
+    return lists
 
 
 def _param_bytes(m: nn.Module) -> int:
@@ -43,8 +49,17 @@ def _param_bytes(m: nn.Module) -> int:
 
 
 def _plan(model, stages, split_points, no_split_module_classes):
-    list_name, blocks = _find_block_list(model, no_split_module_classes)
-    block_names = [f"{list_name}.{i}" if list_name else str(i) for i in range(len(blocks))]
+    """Stage of every unit. Units = the blocks of all block lists (concatenated in registration order, which is their
+    execution order for encoder -> decoder models) + every parameter-owning module outside them, which goes to the
+    stage of the block registered just before it (stage 0 before the first block). Modules registered under more
+    than one parent (T5's `shared` embedding = encoder / decoder `embed_tokens`) are used by several stages: they are
+    returned as `replicated`, real on every stage."""
+    lists = _find_block_lists(model, no_split_module_classes)
+    blocks, block_names = [], []
+    for list_name, ml in lists:
+        for i, b in enumerate(ml):
+            blocks.append(b)
+            block_names.append(f"{list_name}.{i}" if list_name else str(i))
     if stages > len(blocks):
         raise ValueError(f"prepare_pippy: {stages} stages but only {len(blocks)} blocks")
     if split_points == "auto":
@@ -68,21 +83,26 @@ def _plan(model, stages, split_points, no_split_module_classes):
         while s < len(starts) and i >= starts[s]:
             s += 1
         stage_of_block.append(s)
-    units = {}  # module -> stage
-    for b, st in zip(blocks, stage_of_block):
-        units[b] = st
-    seen_list = False
-    block_ids = {id(x) for x in blocks.modules()}
+    units = dict(zip(blocks, stage_of_block))
+    block_stage = {id(b): st for b, st in units.items()}
+    in_block = {id(x) for b in blocks for x in b.modules()}
+    list_ids = {id(ml) for _, ml in lists}
+    uses = {}
+    for _, m in model.named_modules(remove_duplicate=False):
+        uses[id(m)] = uses.get(id(m), 0) + 1
+    replicated = set()
+    cur = 0
     for name, m in model.named_modules():
-        if m is blocks:
-            seen_list = True
+        if id(m) in block_stage:
+            cur = block_stage[id(m)]
             continue
-        if id(m) in block_ids or not any(True for _ in m.parameters(recurse=False)):
+        if id(m) in list_ids or id(m) in in_block or not any(True for _ in m.parameters(recurse=False)):
             continue
-        units[m] = (stages - 1) if seen_list else 0
+        units[m] = cur
+        if uses.get(id(m), 1) > 1:
+            replicated.add(m)
     split_names = [block_names[i] for i in starts]
-    return units, list(blocks), stage_of_block, split_names
-
+    return units, blocks, stage_of_block, split_names, replicated
 
 
 # ------------------------------------------------------------------------------------------------ micro-batching
@@ -124,11 +144,13 @@ def prepare_pippy(
     stages = state.num_processes
     if num_chunks is None:
         num_chunks = stages
-    units, blocks, stage_of_block, split_names = _plan(model, stages, split_points, no_split_module_classes)
+    units, blocks, stage_of_block, split_names, replicated = _plan(model, stages, split_points, no_split_module_classes)
     stage = state.process_index
     device = state.device
     if stages > 1:
-        _place(model, units, stage, device)
+        _place(model, units, stage, device, replicated)
+        for m in replicated:  # real on every stage: neither sent nor turned into meta
+            units[m] = stage
     else:
         model.to(device)
     runtime = _PipelineRuntime(model, units, blocks, stage_of_block, stage, stages, device) if stages > 1 else None
@@ -147,7 +169,9 @@ def prepare_pippy(
         outs = []
         with torch.no_grad():
             for i in range(n):
+                runtime.reset()
                 outs.append(orig(*mb_args[i], **mb_kwargs[i]))
+            runtime.reset()
         runtime.drain()
         out = _concat_outputs(outs)
         last = stages - 1

@@ -72,20 +72,52 @@ def _concat_outputs(outs):
 
 # ------------------------------------------------------------------------------------------------ runtime
 class _PipelineRuntime:
+    """Stage-boundary transport and placeholder resolution for one rank.
+
+    Units this stage does not own run as shape propagation: their inputs go to meta on entry (their weights are meta
+    here) and their outputs come back as zero-filled tensors on the real device. Real-device placeholders keep the
+    model's own glue code working (HF mask builders move the user's masks to `inputs_embeds.device` and test them
+    with `.all()`, which a meta embedding output would break).
+
+    Boundary into stage s (s > 0) = the call of stage s's first block. Every rank executes that call, so on rank s - 1
+    the call's arguments are in hand: it sends one flag per floating tensor of the call's args / kwargs (1 = it holds
+    that value for real) and then those tensors, and rank s receives them in the same flatten order. That carries the
+    block's hidden states AND every other floating input (HF Llama's rotary `position_embeddings`, T5's position
+    biases and encoder states, extended attention masks), not just the previous block's outputs.
+
+    A received tensor replaces the placeholder it stands for in EVERY later owned unit's inputs (the model's forward
+    passes the same Python object to each block): a pre-hook on all owned units resolves placeholders through
+    `self.real`, keyed by the placeholder's identity (a strong reference keeps the id unique) and reset per
+    micro-batch."""
+
     def __init__(self, model, units, blocks, stage_of_block, stage, stages, device, group=None):
         self.model, self.stage, self.stages, self.device, self.group = model, stage, stages, device, group
         self.owned = [m for m, s in units.items() if s == stage]
-        my_blocks = [b for b, s in zip(blocks, stage_of_block) if s == stage]
-        self.first_block = my_blocks[0] if my_blocks else None
-        self.last_block = my_blocks[-1] if my_blocks else None
+        self.real: dict = {}  # id(placeholder) -> (placeholder, real tensor)
+        self.materialized: set = set()  # ids of placeholders this rank made up (zeros), kept alive in self._keep
+        self._keep: list = []
         self.pending = []
+        firsts = {}
+        for b, s in zip(blocks, stage_of_block):
+            firsts.setdefault(s, b)
+        self.first_block = firsts.get(stage)
+        nxt = firsts.get(stage + 1)
+        if nxt is not None and stage < stages - 1:
+            nxt.register_forward_pre_hook(self._send_hook, with_kwargs=True)  # before its to-meta hook below
         for m, s in units.items():
             if s != stage:
                 m.register_forward_pre_hook(self._to_meta_hook, with_kwargs=True)
-        if stage > 0 and self.first_block is not None:
-            self.first_block.register_forward_pre_hook(self._recv_hook, with_kwargs=True)
-        if stage < stages - 1 and self.last_block is not None:
-            self.last_block.register_forward_hook(self._send_hook)
+                m.register_forward_hook(self._materialize_hook)
+        for m in self.owned:
+            if m is self.first_block and stage > 0:
+                m.register_forward_pre_hook(self._recv_hook, with_kwargs=True)
+            else:
+                m.register_forward_pre_hook(self._resolve_hook, with_kwargs=True)
+
+    def reset(self):
+        self.real.clear()
+        self.materialized.clear()
+        self._keep.clear()
 
     def _peer(self, s):
         return s if self.group is None else dist.get_global_rank(self.group, s)
@@ -95,25 +127,58 @@ class _PipelineRuntime:
         conv = lambda t: t.to("meta") if t.device.type != "meta" else t  # noqa: E731
         return _map(args, conv), _map(kwargs, conv)
 
-    def _recv_hook(self, mod, args, kwargs):
-        src = self._peer(self.stage - 1)
+    def _materialize_hook(self, mod, args, out):
+        def conv(t):
+            if t.device.type != "meta":
+                return t
+            z = torch.zeros(t.shape, dtype=t.dtype, device=self.device)
+            self.materialized.add(id(z))
+            self._keep.append(z)
+            return z
 
-        def fill(t):
-            if t.device.type == "meta" and t.is_floating_point():
-                buf = torch.empty(t.shape, dtype=t.dtype, device=self.device)
-                dist.recv(buf, src=src, group=self.group)
-                return buf
-            return t
+        return _map(out, conv)
 
-        return _map(args, fill), _map(kwargs, fill)
+    def _resolve(self, t):
+        hit = self.real.get(id(t))
+        return hit[1] if hit is not None and hit[0] is t else t
 
-    def _send_hook(self, mod, args, out):
+    def _resolve_hook(self, mod, args, kwargs):
+        if not self.real:
+            return None
+        return _map(args, self._resolve), _map(kwargs, self._resolve)
+
+    @staticmethod
+    def _boundary_tensors(args, kwargs):
+        return [t for t in _flatten(list(args) + [kwargs]) if t.is_floating_point()]
+
+    def _send_hook(self, mod, args, kwargs):
         dst = self._peer(self.stage + 1)
-        for t in _flatten(out):
-            if t.is_floating_point() and t.device.type != "meta":
+        ts = [self._resolve(t) for t in self._boundary_tensors(args, kwargs)]
+        # a placeholder this rank made up (never received / computed here) is not a value: flag 0
+        keep = [t.device.type != "meta" and id(t) not in self.materialized for t in ts]
+        flags = torch.tensor(keep, dtype=torch.uint8, device=self.device)
+        self.pending.append((dist.isend(flags, dst=dst, group=self.group), flags))
+        for t, k in zip(ts, keep):
+            if k:
                 t = t.contiguous()
                 self.pending.append((dist.isend(t, dst=dst, group=self.group), t))
-        return out
+        return None
+
+    def _recv_hook(self, mod, args, kwargs):
+        src = self._peer(self.stage - 1)
+        ts = self._boundary_tensors(args, kwargs)
+        flags = torch.empty(len(ts), dtype=torch.uint8, device=self.device)
+        dist.recv(flags, src=src, group=self.group)
+        for t, f in zip(ts, flags.tolist()):
+            if f:
+                buf = torch.empty(t.shape, dtype=t.dtype, device=self.device)
+                dist.recv(buf, src=src, group=self.group)
+                self.real[id(t)] = (t, buf)
+            elif id(self._resolve(t)) in self.materialized:
+                raise RuntimeError(
+                    f"prepare_pippy: stage {self.stage - 1} holds no value for an input of stage {self.stage}'s first "
+                    f"block (shape {tuple(t.shape)}) and neither does this stage")
+        return _map(args, self._resolve), _map(kwargs, self._resolve)
 
     def drain(self):
         for work, _ in self.pending:
@@ -121,9 +186,13 @@ class _PipelineRuntime:
         self.pending.clear()
 
 
-def _place(model, units, stage, device):
-    """Owned parameters → `device`; every other parameter → meta (tied weights follow their owners)."""
-    owned_ids = {id(p) for m, s in units.items() if s == stage for p in m.parameters()}
+def _place(model, units, stage, device, replicated=()):
+    """Owned parameters → `device`; every other parameter → meta (tied weights follow their owners). Buffers of the
+    units this stage does not own go to meta with their parameters (a real buffer meeting a meta weight fails, e.g.
+    BERT's token-type ids); `replicated` units are owned by every stage."""
+    owned_ids = {id(p) for m, s in units.items() if s == stage or m in replicated for p in m.parameters()}
+    foreign_bufs = {id(b) for m, s in units.items() if s != stage and m not in replicated for b in m.buffers()}
+    own_bufs = {id(b) for m, s in units.items() if s == stage or m in replicated for b in m.buffers()}
     memo = {}
     for m in model.modules():
         for name, p in list(m._parameters.items()):
@@ -135,4 +204,19 @@ def _place(model, units, stage, device):
             m._parameters[name] = memo[id(p)]
         for name, b in list(m._buffers.items()):
             if b is not None:
-                m._buffers[name] = b.to(device)
+                meta = id(b) in foreign_bufs and id(b) not in own_bufs
+                m._buffers[name] = b.to("meta" if meta else device)
+    # A foreign unit holding a weight tied to an owned one (BERT's word embeddings = its MLM decoder, a tied lm_head)
+    # would compute with the real weight on meta inputs: on this rank it gets a meta stand-in (the tie is kept where
+    # the weight is owned; this unit never computes for real here)
+    owned_mods = {id(x) for m, s in units.items() if s == stage or m in replicated for x in m.modules()}
+    for m, s in units.items():
+        if s == stage or m in replicated:
+            continue
+        for sub in m.modules():
+            if id(sub) in owned_mods:
+                continue
+            for name, p in list(sub._parameters.items()):
+                if p is not None and p.device.type != "meta":
+                    sub._parameters[name] = nn.Parameter(torch.empty(p.shape, dtype=p.dtype, device="meta"),
+                                                         requires_grad=p.requires_grad)

@@ -1280,3 +1280,49 @@ def check_fsdp_split_root_units(steps: int = 2):
     back = acc.get_state_dict(model)
     for n in full:
         assert torch.equal(full[n], back[n]), n
+
+
+def _tiny_hf_model(kind: str):
+    """Tiny random-init transformers models of the families the reference's pippy examples run
+    (`/root/reference/examples/inference/pippy/{llama,bert,gpt2,t5}.py`), and example inputs."""
+    import transformers as tf
+
+    g = torch.Generator().manual_seed(1)
+    ids = torch.randint(1, 128, (4, 16), generator=g)
+    if kind == "llama":
+        cfg = tf.LlamaConfig(vocab_size=128, hidden_size=64, intermediate_size=96, num_hidden_layers=4,
+                             num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=64)
+        return tf.LlamaForCausalLM(cfg), {"input_ids": ids}
+    if kind == "bert":
+        cfg = tf.BertConfig(vocab_size=128, hidden_size=64, num_hidden_layers=4, num_attention_heads=4,
+                            intermediate_size=96, max_position_embeddings=64)
+        return tf.BertForMaskedLM(cfg), {"input_ids": ids, "attention_mask": torch.ones_like(ids)}
+    if kind == "gpt2":
+        cfg = tf.GPT2Config(vocab_size=128, n_embd=64, n_layer=4, n_head=4, n_positions=64, num_labels=3, pad_token_id=0)
+        return tf.GPT2ForSequenceClassification(cfg), {"input_ids": ids}
+    if kind == "t5":
+        cfg = tf.T5Config(vocab_size=128, d_model=64, d_ff=96, d_kv=16, num_layers=2, num_decoder_layers=2, num_heads=4,
+                          decoder_start_token_id=0, pad_token_id=0)
+        dec = torch.randint(1, 128, (4, 8), generator=g)
+        return tf.T5ForConditionalGeneration(cfg), {"input_ids": ids, "decoder_input_ids": dec}
+    raise ValueError(kind)
+
+
+def check_pipeline_hf(kind: str, split="auto"):
+    """prepare_pippy on a transformers model (reference inference.py:75-123 traces any HF model): the last stage's
+    logits (micro-batched, gathered to every rank) equal the unsplit model's on one process."""
+    import torch.distributed as dist
+
+    from accelerate_hpc_test_amd.inference import prepare_pippy
+
+    state = PartialState(cpu=True)
+    set_seed(0)
+    model, inputs = _tiny_hf_model(kind)
+    model.eval()
+    with torch.no_grad():
+        ref = model(**inputs).logits
+    model = prepare_pippy(model, split_points=split, gather_output=True, num_chunks=2)
+    assert len(model.hf_split_points) == state.num_processes - 1
+    out = model(**inputs)
+    assert torch.allclose(out.logits, ref, atol=1e-5), (kind, (out.logits - ref).abs().max())
+    dist.barrier()

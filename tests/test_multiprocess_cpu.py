@@ -196,3 +196,9 @@ def test_expert_parallel_uneven_expert_loads(world):
 @pytest.mark.parametrize("world", [1, 2])
 def test_fsdp_split_root_units(world):
     debug_launcher(td.check_fsdp_split_root_units, num_processes=world)
+
+
+@pytest.mark.parametrize("kind,world", [("llama", 2), ("llama", 4), ("bert", 2), ("gpt2", 2), ("t5", 2), ("t5", 3)])
+def test_pipeline_inference_hf_models(kind, world):
+    """prepare_pippy on transformers Llama / BERT / GPT2 / T5 (the reference's examples/inference/pippy models)."""
+    debug_launcher(td.check_pipeline_hf, args=(kind,), num_processes=world)
