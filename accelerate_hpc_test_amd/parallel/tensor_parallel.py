@@ -19,7 +19,7 @@ engine flat-shards the TP-local shards over `dp_shard` unchanged (2-D TP × FSDP
 
 from __future__ import annotations
 
-import fnmatch
+import re
 from dataclasses import dataclass, field
 from typing import Callable, Optional, Union
 
@@ -82,28 +82,60 @@ def _replace_param(module: nn.Module, name: str, new: torch.Tensor, spec: TPSpec
 
 
 # ------------------------------------------------------------------------------------------------ styles
+# A style shards the parameters of the module (or the single parameter) a plan entry names and installs the
+# forward hooks that move activations across the tp group. Every parameter keeps a `_tp_spec` (dim, segments) so the
+# FSDP engine shards the TP-local tensors unchanged and `gather_tp_state_dict` rebuilds full ones.
 class ParallelStyle:
     def apply(self, module: nn.Module, group, sequence_parallel: bool):
         raise NotImplementedError
 
+    def shard_parameter(self, module: nn.Module, name: str, group):
+        """A plan entry naming a parameter rather than a module (HF MoE: `...experts.gate_up_proj`): shard it only —
+        the activation hooks belong to the owning module's own entry."""
+        raise ValueError(f"TP style {type(self).__name__} cannot be applied to the parameter `{name}` alone")
+
+
+def _norm_dim(dim: int, ndim: int) -> int:
+    return dim % ndim
+
+
+def _shard_named(module, name, dim, segments, group):
+    p = getattr(module, name)
+    W, r = comm.group_size(group), comm.group_rank(group)
+    spec = TPSpec(_norm_dim(dim, p.dim()), segments, group, W)
+    return _replace_param(module, name, _shard_param_data(p, spec, r), spec)
+
 
 class ColwiseParallel(ParallelStyle):
-    def __init__(self, segments: Optional[Union[list, Callable]] = None, gather_output: bool = False):
+    """Output features sharded (weight dim -2: rows of a Linear, the per-expert output rows of a 3-D expert weight;
+    bias dim -1). Input replicated: fwd identity, bwd all-reduce. `segments` shards fused sub-blocks separately
+    (qkv, gate|up: HF `packed_colwise` = two equal segments); `gather_output` all-gathers the output (HF
+    `colwise_gather_output`, e.g. `lm_head` -> full logits)."""
+
+    def __init__(self, segments: Optional[Union[list, Callable, int]] = None, gather_output: bool = False):
         self.segments = segments
         self.gather_output = gather_output
 
-    def apply(self, module, group, sequence_parallel):
-        W, r = comm.group_size(group), comm.group_rank(group)
+    def _segs(self, module, p):
         segs = self.segments(module) if callable(self.segments) else self.segments
-        spec = TPSpec(0, segs, group, W)
-        _replace_param(module, "weight", _shard_param_data(module.weight, spec, r), spec)
+        if isinstance(segs, int):  # `packed`: this many equal sub-blocks along the sharded dim
+            n = p.shape[-2] if p.dim() > 1 else p.shape[-1]
+            segs = [n // segs] * segs
+        return segs
+
+    def shard_parameter(self, module, name, group):
+        p = getattr(module, name)
+        _shard_named(module, name, -2 if p.dim() > 1 else -1, self._segs(module, p), group)
+
+    def apply(self, module, group, sequence_parallel):
+        segs = self._segs(module, module.weight)
+        if isinstance(module, nn.Embedding):
+            raise ValueError("colwise on an nn.Embedding: use `embedding_colwise` / `embedding_rowwise`")
+        _shard_named(module, "weight", -2, segs, group)
         if getattr(module, "bias", None) is not None:
-            bspec = TPSpec(0, segs, group, W)
-            _replace_param(module, "bias", _shard_param_data(module.bias, bspec, r), bspec)
+            _shard_named(module, "bias", -1, segs, group)
         if isinstance(module, nn.Linear):
             module.out_features = module.weight.shape[0]
-        elif isinstance(module, nn.Embedding):
-            module.embedding_dim = module.weight.shape[1]
         gather = self.gather_output
 
         def pre(mod, args):
@@ -112,17 +144,42 @@ class ColwiseParallel(ParallelStyle):
             return (x,) + tuple(args[1:])
 
         def post(mod, args, out):
-            return comm.gather_along(out, -1, group, reduce_grad=False) if gather else out
+            if not gather:
+                return out
+            if segs and len(segs) > 1:  # gathered [r0 seg0 | r0 seg1 | r1 seg0 ...] -> [seg0 | seg1]
+                full = comm.gather_along(out, -1, group, reduce_grad=False)
+                per = full.chunk(comm.group_size(group), dim=-1)
+                parts = [q.split([sg // comm.group_size(group) for sg in segs], dim=-1) for q in per]
+                return torch.cat([parts[rk][si] for si in range(len(segs)) for rk in range(len(per))], dim=-1)
+            return comm.gather_along(out, -1, group, reduce_grad=False)
 
         module.register_forward_pre_hook(pre)
         module.register_forward_hook(post)
 
 
 class RowwiseParallel(ParallelStyle):
+    """Input features sharded (weight dim -1). Output partial sums: fwd all-reduce over xGMI (or reduce-scatter along
+    the sequence with `sequence_parallel=True`); the bias is added once, after the reduction. `split_input` (HF
+    `rowwise_split_input`) keeps this rank's chunk of a replicated input first; `segments` as in ColwiseParallel (HF
+    `packed_rowwise`)."""
+
+    def __init__(self, split_input: bool = False, segments: Optional[Union[list, int]] = None):
+        self.split_input = split_input
+        self.segments = segments
+
+    def _segs(self, p):
+        segs = self.segments
+        if isinstance(segs, int):
+            segs = [p.shape[-1] // segs] * segs
+        return segs
+
+    def shard_parameter(self, module, name, group):
+        p = getattr(module, name)
+        if p.dim() > 1:
+            _shard_named(module, name, -1, self._segs(p), group)
+
     def apply(self, module, group, sequence_parallel):
-        W, r = comm.group_size(group), comm.group_rank(group)
-        spec = TPSpec(1, None, group, W)
-        _replace_param(module, "weight", _shard_param_data(module.weight, spec, r), spec)
+        _shard_named(module, "weight", -1, self._segs(module.weight), group)
         if isinstance(module, nn.Linear):
             module.in_features = module.weight.shape[1]
         bias = getattr(module, "bias", None)
@@ -130,6 +187,11 @@ class RowwiseParallel(ParallelStyle):
             # bias is added once, after the reduction
             module._tp_bias = bias
             module.bias = None
+        split = self.split_input
+
+        if split:
+            module.register_forward_pre_hook(
+                lambda mod, args: (comm.split_along(args[0], -1, group),) + tuple(args[1:]))
 
         def post(mod, args, out):
             out = comm.reduce_scatter_along(out, 1, group) if sequence_parallel else comm.reduce_from_group(out, group)
@@ -140,9 +202,94 @@ class RowwiseParallel(ParallelStyle):
         module.register_forward_hook(post)
 
 
+class VocabParallelEmbedding(ParallelStyle):
+    """HF `embedding_rowwise`: the vocabulary (weight dim 0) is sharded; ids outside this rank's range look up row 0
+    and are zeroed, and the partial embeddings are all-reduced."""
+
+    def apply(self, module, group, sequence_parallel):
+        if module.weight.shape[0] % comm.group_size(group):
+            raise ValueError(f"embedding_rowwise: vocabulary {module.weight.shape[0]} not divisible by tp")
+        _shard_named(module, "weight", 0, None, group)
+        rank = comm.group_rank(group)
+
+        def pre(mod, args):
+            ids = args[0]
+            n = mod.weight.shape[0]
+            lo = rank * n
+            mask = (ids < lo) | (ids >= lo + n)
+            mod._tp_mask = mask
+            return ((ids - lo).masked_fill(mask, 0),) + tuple(args[1:])
+
+        def post(mod, args, out):
+            out = out.masked_fill(mod._tp_mask.unsqueeze(-1), 0.0)
+            del mod._tp_mask
+            return comm.reduce_from_group(out, group)
+
+        if hasattr(module, "num_embeddings"):
+            module.num_embeddings = module.weight.shape[0]
+        module.register_forward_pre_hook(pre)
+        module.register_forward_hook(post)
+
+
+class EmbeddingColwise(ParallelStyle):
+    """HF `embedding_colwise`: the embedding dim (weight dim 1) is sharded; outputs are all-gathered."""
+
+    def apply(self, module, group, sequence_parallel):
+        _shard_named(module, "weight", 1, None, group)
+        if hasattr(module, "embedding_dim"):
+            module.embedding_dim = module.weight.shape[1]
+        module.register_forward_hook(lambda mod, args, out: comm.gather_along(out, -1, group, reduce_grad=False))
+
+
 class ReplicateParallel(ParallelStyle):
     def apply(self, module, group, sequence_parallel):
         pass
+
+    def shard_parameter(self, module, name, group):
+        pass
+
+
+class ReplicatedGradAllReduce(ParallelStyle):
+    """HF `replicated_with_grad_allreduce`: replicated parameters that sit between colwise and rowwise layers (per-head
+    q/k norms) see only this rank's heads, so their gradients are summed over tp."""
+
+    def apply(self, module, group, sequence_parallel):
+        def attach(mod, args):  # lazily: engines may replace the Parameter objects after parallelize
+            for p in mod.parameters(recurse=False):
+                if p.requires_grad and not getattr(p, "_tp_grad_hooked", False):
+                    p.register_hook(lambda g, _grp=group: comm.all_reduce_(g.contiguous().clone(), _grp))
+                    p._tp_grad_hooked = True
+
+        module.register_forward_pre_hook(attach)
+
+
+class MoeExpertsParallel(ParallelStyle):
+    """HF `moe_tp_experts`: the experts module of a TP-sharded MoE layer (its `gate_up_proj` / `down_proj` parameters
+    carry their own packed_colwise / rowwise entries). Hidden states and routing weights enter replicated (bwd
+    all-reduce: the colwise expert GEMMs and the per-rank partial outputs both feed their gradients); the partial
+    expert outputs are all-reduced."""
+
+    def apply(self, module, group, sequence_parallel):
+        def pre(mod, args, kwargs):
+            args = list(args)
+            if args:
+                args[0] = comm.copy_to_group(args[0], group)
+            if len(args) > 2 and torch.is_tensor(args[2]) and args[2].is_floating_point():
+                args[2] = comm.copy_to_group(args[2], group)
+            for k in ("hidden_states", "top_k_weights", "routing_weights"):
+                if k in kwargs and torch.is_tensor(kwargs[k]):
+                    kwargs[k] = comm.copy_to_group(kwargs[k], group)
+            return tuple(args), kwargs
+
+        module.register_forward_pre_hook(pre, with_kwargs=True)
+        module.register_forward_hook(lambda mod, args, out: comm.reduce_from_group(out, group))
+
+
+class AllReduceOutput(ParallelStyle):
+    """HF `all_reduce`: the module's forward output is a partial sum over tp."""
+
+    def apply(self, module, group, sequence_parallel):
+        module.register_forward_hook(lambda mod, args, out: comm.reduce_from_group(out, group))
 
 
 class SequenceParallel(ParallelStyle):
@@ -152,15 +299,7 @@ class SequenceParallel(ParallelStyle):
     def apply(self, module, group, sequence_parallel):
         if not sequence_parallel:
             return
-
-        def attach(mod, args):
-            # attached lazily: engines (FSDP meta materialisation) may replace Parameter objects after parallelize
-            for p in mod.parameters(recurse=False):
-                if p.requires_grad and not getattr(p, "_sp_grad_hooked", False):
-                    p.register_hook(lambda g, _grp=group: comm.all_reduce_(g.contiguous().clone(), _grp))
-                    p._sp_grad_hooked = True
-
-        module.register_forward_pre_hook(attach)
+        ReplicatedGradAllReduce().apply(module, group, sequence_parallel)
 
 
 class SplitSequenceOutput(ParallelStyle):
@@ -172,6 +311,16 @@ class SplitSequenceOutput(ParallelStyle):
         module.register_forward_hook(lambda mod, args, out: comm.split_along(out, 1, group))
 
 
+class _Unsupported(ParallelStyle):
+    def __init__(self, name, why):
+        self.name, self.why = name, why
+
+    def apply(self, module, group, sequence_parallel):
+        raise ValueError(f"TP style `{self.name}` is not supported here: {self.why}")
+
+    shard_parameter = apply
+
+
 def _shard_param_data(p: torch.Tensor, spec: TPSpec, rank: int) -> torch.Tensor:
     if p.device.type == "meta":
         shape = list(p.shape)
@@ -180,18 +329,35 @@ def _shard_param_data(p: torch.Tensor, spec: TPSpec, rank: int) -> torch.Tensor:
     return _shard_tensor(p.data, spec, rank).clone()
 
 
+_EP = ("expert parallelism is configured with ParallelismConfig(ep_size=...) (models/moe.py), not through the tp "
+       "plan")
 _STYLE_BY_NAME = {
-    "colwise": lambda: ColwiseParallel(),
-    "local_colwise": lambda: ColwiseParallel(),
+    # this framework's names
     "colwise_rep": lambda: ColwiseParallel(gather_output=True),
-    "rowwise": lambda: RowwiseParallel(),
-    "local_rowwise": lambda: RowwiseParallel(),
     "rowwise_rep": lambda: RowwiseParallel(),
     "replicate": lambda: ReplicateParallel(),
     "sequence_parallel": lambda: SequenceParallel(),
     "seq_split": lambda: SplitSequenceOutput(),
-    "gather": lambda: ReplicateParallel(),
+    # transformers tp_plan names (transformers/integrations/tensor_parallel.py ParallelInterface)
+    "colwise": lambda: ColwiseParallel(),
+    "colwise_gather_output": lambda: ColwiseParallel(gather_output=True),
+    "packed_colwise": lambda: ColwiseParallel(segments=2),
+    "rowwise": lambda: RowwiseParallel(),
+    "rowwise_split_input": lambda: RowwiseParallel(split_input=True),
+    "packed_rowwise": lambda: RowwiseParallel(segments=2),
+    "embedding_rowwise": lambda: VocabParallelEmbedding(),
+    "embedding_colwise": lambda: EmbeddingColwise(),
+    "replicated_with_grad_allreduce": lambda: ReplicatedGradAllReduce(),
+    "moe_tp_experts": lambda: MoeExpertsParallel(),
+    "all_reduce": lambda: AllReduceOutput(),
     "local": lambda: ReplicateParallel(),
+    "local_colwise": lambda: ColwiseParallel(),
+    "local_rowwise": lambda: RowwiseParallel(),
+    "gather": lambda: ReplicateParallel(),
+    "grouped_gemm": lambda: _Unsupported("grouped_gemm", _EP),
+    "ep_router": lambda: _Unsupported("ep_router", _EP),
+    "moe_identity_expert": lambda: _Unsupported("moe_identity_expert", "zero / identity experts"),
+    "mla_kv_a_proj": lambda: _Unsupported("mla_kv_a_proj", "MLA (DeepSeek-V2-style) attention"),
 }
 
 
@@ -203,11 +369,19 @@ def _resolve_style(s) -> ParallelStyle:
     return _STYLE_BY_NAME[s]()
 
 
+def _match(name: str, pattern: str) -> bool:
+    """HF plan keys: `*` stands for one path component (a layer index)."""
+    return re.fullmatch(re.escape(pattern).replace(r"\*", r"[^.]+"), name) is not None
+
+
 def get_tp_plan(model: nn.Module, sequence_parallel: bool = False) -> Optional[dict]:
     """Model-provided plan: our models' `tp_plan()`, or a transformers `_tp_plan` / `config.base_model_tp_plan`."""
     if hasattr(model, "tp_plan") and callable(model.tp_plan):
         return model.tp_plan(sequence_parallel=sequence_parallel)
     plan = {}
+    if sequence_parallel:
+        raise ValueError("sequence-parallel TP needs a plan with sequence-parallel entries (this framework's models' "
+                         "`tp_plan(sequence_parallel=True)`); a transformers tp_plan has none — pass `plan=`")
     base = getattr(getattr(model, "config", None), "base_model_tp_plan", None)
     if base:
         prefix = getattr(model, "base_model_prefix", "")
@@ -230,17 +404,44 @@ def parallelize_module(model: nn.Module, group, plan: Optional[dict] = None, seq
     W = comm.group_size(group)
     if W == 1:
         return model
+    try:
+        from torch.distributed.tensor import DTensor
+    except ImportError:  # pragma: no cover
+        DTensor = ()
+    if any(isinstance(p, DTensor) for p in model.parameters()):
+        # already sharded by transformers (`from_pretrained(tp_plan="auto", device_mesh=...)`, the reference's flow):
+        # keep its DTensor layout
+        model._tp_group, model._tp_size, model._tp_sequence_parallel = group, W, False
+        return model
     _PARAM_MAP.clear()
     matched = set()
     for name, module in list(model.named_modules()):
         for pattern, style in plan.items():
-            if fnmatch.fnmatchcase(name, pattern) or fnmatch.fnmatchcase(name, pattern.replace("*", "[0-9]*")):
+            if _match(name, pattern):
                 _resolve_style(style).apply(module, group, sequence_parallel)
+                matched.add(pattern)
+                break
+    # entries that name a parameter (HF MoE experts' 3-D `gate_up_proj` / `down_proj`)
+    for pname, _ in list(model.named_parameters()):
+        for pattern, style in plan.items():
+            if _match(pname, pattern):
+                mod_name, _, leaf = pname.rpartition(".")
+                owner = model.get_submodule(mod_name) if mod_name else model
+                if getattr(getattr(owner, leaf), "_tp_spec", None) is None:
+                    _resolve_style(style).shard_parameter(owner, leaf, group)
                 matched.add(pattern)
                 break
     for m in model.modules():
         if hasattr(m, "shard_heads"):
             m.shard_heads(W)
+        hd = getattr(m, "head_dim", None)
+        if isinstance(hd, int) and hd > 0:  # HF attention: every rank must keep whole heads of q / k / v
+            for proj in ("q_proj", "k_proj", "v_proj"):
+                lin = getattr(m, proj, None)
+                w = getattr(lin, "weight", None)
+                if w is not None and getattr(w, "_tp_spec", None) is not None and w.shape[0] % hd:
+                    raise ValueError(f"TP={W}: `{proj}` keeps {w.shape[0]} output features per rank, not a whole "
+                                     f"number of heads of {hd} (its head count must be divisible by tp)")
     model._tp_param_map = dict(_PARAM_MAP)  # lets an optimizer built on the unsharded model be re-pointed
     _PARAM_MAP.clear()
     model._tp_group = group

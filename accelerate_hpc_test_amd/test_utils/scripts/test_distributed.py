@@ -1326,3 +1326,55 @@ def check_pipeline_hf(kind: str, split="auto"):
     out = model(**inputs)
     assert torch.allclose(out.logits, ref, atol=1e-5), (kind, (out.logits - ref).abs().max())
     dist.barrier()
+
+
+def _tiny_hf_causal_lm(kind: str, kv_heads: int = 2):
+    import transformers as tf
+
+    if kind == "llama":
+        cfg = tf.LlamaConfig(vocab_size=128, hidden_size=64, intermediate_size=96, num_hidden_layers=2,
+                             num_attention_heads=4, num_key_value_heads=kv_heads, max_position_embeddings=64)
+        return tf.LlamaForCausalLM(cfg)
+    if kind == "qwen3":  # per-head q/k norms: `replicated_with_grad_allreduce`
+        cfg = tf.Qwen3Config(vocab_size=128, hidden_size=64, intermediate_size=96, num_hidden_layers=2,
+                             num_attention_heads=4, num_key_value_heads=2, head_dim=16, max_position_embeddings=64)
+        return tf.Qwen3ForCausalLM(cfg)
+    if kind == "mixtral":  # 3-D expert weights: `packed_colwise` / `rowwise` parameter entries + `moe_tp_experts`
+        cfg = tf.MixtralConfig(vocab_size=128, hidden_size=64, intermediate_size=96, num_hidden_layers=2,
+                               num_attention_heads=4, num_key_value_heads=2, num_local_experts=4, num_experts_per_tok=2,
+                               max_position_embeddings=64)
+        return tf.MixtralForCausalLM(cfg)
+    raise ValueError(kind)
+
+
+def check_tp_hf(kind: str, steps: int = 2):
+    """TP over a transformers model's own `tp_plan` (the reference's `_prepare_tp` path, accelerator.py:1579-1639,
+    on models sharded by transformers `tp_plan="auto"`): loss and full weights after `steps` SGD steps equal one
+    process's on the same batch."""
+    from accelerate_hpc_test_amd import ParallelismConfig
+
+    W = int(os.environ["WORLD_SIZE"])
+    acc = Accelerator(cpu=True, parallelism_config=ParallelismConfig(tp_size=W))
+    set_seed(0)
+    base = _tiny_hf_causal_lm(kind, kv_heads=max(2, W))  # whole kv heads per rank
+    model = copy.deepcopy(base)
+    opt = torch.optim.SGD(model.parameters(), lr=0.5, momentum=0.9)
+    base_opt = torch.optim.SGD(base.parameters(), lr=0.5, momentum=0.9)
+    model, opt = acc.prepare(model, opt)
+    assert any(getattr(p, "_tp_spec", None) is not None for p in model.parameters()), "nothing was sharded"
+    g = torch.Generator().manual_seed(3)
+    for _ in range(steps):
+        ids = torch.randint(0, 128, (2, 16), generator=g)
+        out = model(input_ids=ids, labels=ids)
+        acc.backward(out.loss)
+        opt.step()
+        opt.zero_grad()
+        ref = base(input_ids=ids, labels=ids)
+        ref.loss.backward()
+        base_opt.step()
+        base_opt.zero_grad()
+        assert torch.allclose(out.loss.detach(), ref.loss.detach(), atol=2e-5), (kind, out.loss, ref.loss)
+    full = acc.get_state_dict(model)
+    for n, q in base.state_dict().items():
+        assert full[n].shape == q.shape, (n, full[n].shape, q.shape)
+        assert torch.allclose(full[n].float(), q.float(), atol=2e-5), (kind, n, (full[n] - q).abs().max())

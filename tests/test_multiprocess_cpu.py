@@ -202,3 +202,10 @@ def test_fsdp_split_root_units(world):
 def test_pipeline_inference_hf_models(kind, world):
     """prepare_pippy on transformers Llama / BERT / GPT2 / T5 (the reference's examples/inference/pippy models)."""
     debug_launcher(td.check_pipeline_hf, args=(kind,), num_processes=world)
+
+
+@pytest.mark.parametrize("kind,world", [("llama", 2), ("llama", 4), ("qwen3", 2), ("mixtral", 2)])
+def test_tp_hf_models_match_single_process(kind, world):
+    """ParallelismConfig(tp_size) on transformers models, sharded by their own tp_plan (colwise / rowwise /
+    colwise_gather_output / replicated_with_grad_allreduce / packed_colwise / moe_tp_experts)."""
+    debug_launcher(td.check_tp_hf, args=(kind,), num_processes=world)
