@@ -207,6 +207,14 @@ def launch_command_parser(subparsers=None):
     rc.add_argument("--rccl_fsdp_prefetch", type=int, default=None, help="FSDP all-gather prefetch depth.")
     rc.add_argument("--rccl_stream_priority", type=int, default=None, help="HIP priority of the comm streams.")
     rc.add_argument("--dry_run", action="store_true", help="Print the resolved command and env delta instead of running.")
+    parser.add_argument("--debug", action="store_true",
+                        help="Debug mode: every collective verifies that all ranks pass matching shapes "
+                             "(ACCELERATE_DEBUG_MODE, utils/operations.verify_operation) and failures print the "
+                             "torch.distributed stack trace.")
+    mpi = parser.add_argument_group("MPI Arguments", "Multi-CPU launches through mpirun / mpiexec")
+    mpi.add_argument("--mpirun_hostfile", type=str, default=None,
+                     help="Hostfile for a multi-CPU launch with mpirun (passed as --hostfile / -f).")
+    mpi.add_argument("--bind_to", type=str, default=None, help="Open MPI --bind-to value (default: socket).")
 
     parser.add_argument("training_script", type=str, help="The script (or module with -m) to launch.")
     parser.add_argument("training_script_args", nargs=argparse.REMAINDER, help="Arguments of the training script.")
@@ -353,6 +361,11 @@ def launch_command(args) -> int:
     distributed = args.multi_gpu or args.use_fsdp or args.use_deepspeed or args.num_processes > 1 or args.num_machines > 1
     if args.cpu and args.num_processes <= 1:
         distributed = False
+    if args.mpirun_hostfile is not None:  # multi-CPU over MPI: mpirun starts the ranks (reference launch.py)
+        if not args.cpu:
+            raise ValueError("--mpirun_hostfile launches multi-CPU jobs: add --cpu (GPU jobs launch one rank per "
+                             "MI355X through torch.distributed.run)")
+        return simple_launcher(args)
     if distributed:
         return multi_gpu_launcher(args)
     return simple_launcher(args)

@@ -2,9 +2,10 @@
 
 Parity target: `/root/reference/src/accelerate/local_sgd.py:19-106` (context manager wrapping `no_sync`, `step()`
 counting, parameter mean on every K-th step and on exit). The reference averages parameter by parameter
-(`accelerator.reduce(param, "mean")` per tensor → one collective per parameter); here all parameters of one dtype
-are packed into a single flat buffer and averaged with ONE RCCL all-reduce (a 16 GB model = one large xGMI
-all-reduce instead of ~300 small latency-bound ones), then unpacked.
+(`accelerator.reduce(param, "mean")` per tensor → one collective per parameter); here the parameters of one dtype are
+packed into flat buffers of at most `chunk_bytes` (256 MB: large enough that each 8-way xGMI ring step moves tens of
+MB per link, small enough that averaging Llama-3-8B's 32 GB of fp32 parameters never holds a whole-model copy) and
+averaged with one RCCL all-reduce per buffer; a parameter larger than a buffer is averaged in place.
 """
 
 from __future__ import annotations
@@ -29,11 +30,13 @@ class LocalSGD:
             self._sync_and_avg_model_params()
             self.model_sync_obj.__exit__(type, value, tb)
 
-    def __init__(self, accelerator: Accelerator, model: torch.nn.Module, local_sgd_steps: int, enabled: bool = True):
+    def __init__(self, accelerator: Accelerator, model: torch.nn.Module, local_sgd_steps: int, enabled: bool = True,
+                 chunk_bytes: int = 256 << 20):
         if accelerator.distributed_type not in (DistributedType.NO, DistributedType.MULTI_CPU, DistributedType.MULTI_GPU):
             raise NotImplementedError("LocalSGD is supported only for CPU and GPU data parallelism (no FSDP / DeepSpeed).")
         self.enabled = enabled and accelerator.distributed_type != DistributedType.NO
         self.num_steps = 0
+        self.chunk_bytes = int(chunk_bytes)
         if self.enabled:
             self.accelerator = accelerator
             self.model = model
@@ -53,18 +56,39 @@ class LocalSGD:
         model = self.accelerator.unwrap_model(self.model)
         group = getattr(self.model, "process_group", None)
         world = dist.get_world_size(group)
-        by_dtype: dict = {}
-        for p in model.parameters():
-            by_dtype.setdefault((p.dtype, p.device), []).append(p)
-        for (dtype, device), params in by_dtype.items():
-            flat = torch.cat([p.detach().reshape(-1) for p in params])
-            if dist.get_backend(group) == "gloo" or not dtype.is_floating_point:
-                dist.all_reduce(flat, group=group)
-                flat.div_(world)
+        gloo = dist.get_backend(group) == "gloo"
+
+        def average(buf):
+            if gloo or not buf.dtype.is_floating_point:
+                dist.all_reduce(buf, group=group)
+                buf.div_(world)
             else:
-                dist.all_reduce(flat, op=dist.ReduceOp.AVG, group=group)
+                dist.all_reduce(buf, op=dist.ReduceOp.AVG, group=group)
+
+        def flush(batch):
+            if len(batch) == 1 and batch[0].is_contiguous():
+                average(batch[0].data)
+                return
+            flat = torch.cat([p.detach().reshape(-1) for p in batch])
+            average(flat)
             off = 0
-            for p in params:
+            for p in batch:
                 n = p.numel()
                 p.copy_(flat[off : off + n].view_as(p))
                 off += n
+
+        by_dtype: dict = {}
+        for p in model.parameters():
+            if p.dtype.is_floating_point:
+                by_dtype.setdefault((p.dtype, p.device), []).append(p)
+        for params in by_dtype.values():
+            batch, nbytes = [], 0
+            for p in params:
+                b = p.numel() * p.element_size()
+                if batch and nbytes + b > self.chunk_bytes:
+                    flush(batch)
+                    batch, nbytes = [], 0
+                batch.append(p)
+                nbytes += b
+            if batch:
+                flush(batch)

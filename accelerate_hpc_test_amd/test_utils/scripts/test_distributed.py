@@ -443,9 +443,20 @@ def check_ulysses_llama_matches_single(steps: int = 2):
         assert torch.allclose(sd[n].float(), q.float(), atol=5e-5), (n, (sd[n] - q).abs().max())
 
 
-def check_local_sgd(k: int = 2, steps: int = 4):
-    """LocalSGD == every rank trains alone for k steps, then parameters are averaged (simulated locally)."""
+def check_local_sgd(k: int = 2, steps: int = 4, chunk_bytes: int = 256 << 20):
+    """LocalSGD == every rank trains alone for k steps, then parameters are averaged (simulated locally). With a
+    small `chunk_bytes` the averaging must stay in packed buffers of at most that size (or one parameter alone):
+    no whole-model transient (the reference averages per parameter, local_sgd.py:98-106)."""
+    import torch.distributed as dist
+
     from accelerate_hpc_test_amd.local_sgd import LocalSGD
+
+    sizes = []
+    real_all_reduce = dist.all_reduce
+
+    def recording_all_reduce(t, *a, **kw):
+        sizes.append(t.numel() * t.element_size())
+        return real_all_reduce(t, *a, **kw)
 
     acc = Accelerator(cpu=True)
     W, r = acc.num_processes, acc.process_index
@@ -458,7 +469,22 @@ def check_local_sgd(k: int = 2, steps: int = 4):
     model, opt = acc.prepare(model, opt)
     bs = 4
     batches = _global_batches(steps, bs, W)
-    with LocalSGD(acc, model, local_sgd_steps=k) as local_sgd:
+    dist.all_reduce = recording_all_reduce
+    try:
+        _local_sgd_loop(acc, model, opt, sims, sim_opts, batches, W, r, bs, k, chunk_bytes)
+    finally:
+        dist.all_reduce = real_all_reduce
+    largest = max(p.numel() * p.element_size() for p in sims[0].parameters())
+    assert sizes and max(sizes) <= max(chunk_bytes, largest), (sizes, chunk_bytes, largest)
+    inner = acc.unwrap_model(model)
+    for (n, p), q in zip(inner.named_parameters(), sims[0].parameters()):
+        assert torch.allclose(p, q, atol=1e-6), (n, (p - q).abs().max())
+
+
+def _local_sgd_loop(acc, model, opt, sims, sim_opts, batches, W, r, bs, k, chunk_bytes):
+    from accelerate_hpc_test_amd.local_sgd import LocalSGD
+
+    with LocalSGD(acc, model, local_sgd_steps=k, chunk_bytes=chunk_bytes) as local_sgd:
         for step, (x, y) in enumerate(batches):
             acc.backward(F.mse_loss(model(x[r * bs : (r + 1) * bs]), y[r * bs : (r + 1) * bs]))
             opt.step()
@@ -474,9 +500,6 @@ def check_local_sgd(k: int = 2, steps: int = 4):
                         avg = sum(p.detach() for p in ps) / W
                         for p in ps:
                             p.copy_(avg)
-    inner = acc.unwrap_model(model)
-    for (n, p), q in zip(inner.named_parameters(), sims[0].parameters()):
-        assert torch.allclose(p, q, atol=1e-6), (n, (p - q).abs().max())
 
 
 def check_pipeline_inference(gather_output: bool = True, split="auto"):

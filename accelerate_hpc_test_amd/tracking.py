@@ -55,23 +55,14 @@ class GeneralTracker:
 
     main_process_only = True
 
+    _REQUIRED = ("name", "requires_logging_directory", "tracker")
+
     def __init__(self, _blank=False):
-        if not _blank:
-            err = ""
-            if not hasattr(self, "name"):
-                err += "`name`"
-            if not hasattr(self, "requires_logging_directory"):
-                if len(err) > 0:
-                    err += ", "
-                err += "`requires_logging_directory`"
-            if "tracker" not in dir(self):
-                if len(err) > 0:
-                    err += ", "
-                err += "`tracker`"
-            if len(err) > 0:
-                raise NotImplementedError(
-                    f"The implementation for this tracker class is missing the following required attributes. Please define them in the class definition: {err}"
-                )
+        missing = [] if _blank else [f"`{a}`" for a in self._REQUIRED if not hasattr(type(self), a) and not hasattr(self, a)]
+        if missing:
+            raise NotImplementedError(
+                "The implementation for this tracker class is missing the following required attributes. Please "
+                f"define them in the class definition: {', '.join(missing)}")
 
     def start(self):
         pass

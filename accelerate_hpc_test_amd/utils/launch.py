@@ -19,6 +19,7 @@ import argparse
 import os
 import subprocess
 import sys
+from shutil import which
 from typing import Any, Optional
 
 import torch
@@ -232,11 +233,43 @@ def _apply_deepspeed_translation(args, env: dict):
             env[f"ACCELERATE_{attr.upper()}"] = str(getattr(args, attr))
 
 
+def _get_mpirun_args():
+    """(program, hostfile flag, process-count flag, per-node flag, bind flag) of the installed MPI launcher: Open MPI
+    spells them `--hostfile -n --npernode --bind-to`, Intel MPI and MVAPICH `-f -n -ppn` (no bind flag). Parity:
+    reference utils/launch.py:57-78."""
+    apps = [x for x in ("mpirun", "mpiexec") if which(x)]
+    if not apps:
+        raise OSError("mpirun or mpiexec were not found. Ensure that Intel MPI, Open MPI, or MVAPICH are installed.")
+    app = apps[0]
+    version = subprocess.check_output([app, "--version"])
+    if b"Open MPI" in version:
+        return app, "--hostfile", "-n", "--npernode", "--bind-to"
+    return app, "-f", "-n", "-ppn", ""
+
+
+def _mpirun_prefix(args: argparse.Namespace) -> list:
+    """`mpirun <hostfile> <per-node> [<n>] [<bind>]` for a multi-CPU launch over MPI (`--mpirun_hostfile`)."""
+    app, hostfile_arg, nproc_arg, per_node_arg, bind_arg = _get_mpirun_args()
+    n, machines = getattr(args, "num_processes", None), getattr(args, "num_machines", None)
+    per_node = str(n // machines) if n and machines else "1"
+    cmd = [app, hostfile_arg, args.mpirun_hostfile, per_node_arg, per_node]
+    if n:
+        cmd += [nproc_arg, str(n)]
+    if bind_arg:
+        cmd += [bind_arg, getattr(args, "bind_to", None) or "socket"]
+    return cmd
+
+
 def prepare_simple_launcher_cmd_env(args: argparse.Namespace) -> tuple[list, dict]:
-    """Single process: `python [-m] script args...` with the env contract applied."""
+    """Single process: `python [-m] script args...` with the env contract applied; with `--mpirun_hostfile` the
+    command is wrapped in the MPI launcher, which starts the multi-CPU ranks (each reads its rank / world size from
+    the MPI environment, utils/environment.get_cpu_distributed_information)."""
     cmd = []
     if getattr(args, "no_python", False) and getattr(args, "module", False):
         raise ValueError("--module and --no_python cannot be used together")
+    mpi = getattr(args, "mpirun_hostfile", None) is not None
+    if mpi:
+        cmd += _mpirun_prefix(args)
     if not getattr(args, "no_python", False):
         cmd.append(sys.executable)
         if getattr(args, "module", False):
@@ -244,6 +277,12 @@ def prepare_simple_launcher_cmd_env(args: argparse.Namespace) -> tuple[list, dic
     cmd.append(args.training_script)
     cmd.extend(args.training_script_args)
     env = _common_env(args)
+    if mpi:  # the MPI runtime provides every rank's identity; the rendezvous address comes from the launch args
+        for k in ("LOCAL_RANK", "RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE"):
+            env.pop(k, None)
+        env["MASTER_ADDR"] = str(getattr(args, "main_process_ip", None) or "127.0.0.1")
+        env["MASTER_PORT"] = str(getattr(args, "main_process_port", None) or 29500)
+        return cmd, env
     env.setdefault("LOCAL_RANK", "0")
     env.setdefault("RANK", "0")
     env.setdefault("WORLD_SIZE", "1")

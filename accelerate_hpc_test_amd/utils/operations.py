@@ -52,100 +52,86 @@ def is_namedtuple(data):
 
 def honor_type(obj, generator):
     """Rebuild `obj`'s container type from `generator` (namedtuples need positional construction)."""
-    if is_namedtuple(obj):
-        return type(obj)(*list(generator))
-    return type(obj)(generator)
+    items = list(generator)
+    return type(obj)(*items) if is_namedtuple(obj) else type(obj)(items)
+
+
+def _tree_map(leaf_fn, data, is_leaf, on_other=None):
+    """Map `leaf_fn` over the leaves of a list / tuple / mapping tree, keeping every container's own type. Values that
+    are neither containers nor leaves go through `on_other` (returned unchanged by default)."""
+    if isinstance(data, (list, tuple)):
+        return honor_type(data, (_tree_map(leaf_fn, x, is_leaf, on_other) for x in data))
+    if isinstance(data, Mapping):
+        return type(data)({k: _tree_map(leaf_fn, v, is_leaf, on_other) for k, v in data.items()})
+    if is_leaf(data):
+        return leaf_fn(data)
+    return on_other(data) if on_other is not None else data
+
+
+def _tree_first(data, pick):
+    """First non-None `pick(leaf)` in depth-first order over lists / tuples / mappings (None if there is none)."""
+    if isinstance(data, Mapping):
+        data = list(data.values())
+    if isinstance(data, (list, tuple)):
+        for x in data:
+            got = _tree_first(x, pick)
+            if got is not None:
+                return got
+        return None
+    return pick(data)
 
 
 def recursively_apply(func, data, *args, test_type=is_torch_tensor, error_on_other_type=False, **kwargs):
-    """Apply `func` to every leaf of a nested list/tuple/dict structure satisfying `test_type`."""
-    if isinstance(data, (tuple, list)):
-        return honor_type(
-            data,
-            (
-                recursively_apply(func, o, *args, test_type=test_type, error_on_other_type=error_on_other_type, **kwargs)
-                for o in data
-            ),
-        )
-    elif isinstance(data, Mapping):
-        return type(data)(
-            {
-                k: recursively_apply(func, v, *args, test_type=test_type, error_on_other_type=error_on_other_type, **kwargs)
-                for k, v in data.items()
-            }
-        )
-    elif test_type(data):
-        return func(data, *args, **kwargs)
-    elif error_on_other_type:
-        raise TypeError(
-            f"Unsupported types ({type(data)}) passed to `{func.__name__}`. Only nested list/tuple/dicts of "
-            f"objects that are valid for `{test_type.__name__}` should be passed."
-        )
-    return data
+    """Apply `func(leaf, *args, **kwargs)` to every leaf of a nested list / tuple / dict that passes `test_type`;
+    other leaves are kept, or rejected with `error_on_other_type`."""
+
+    def reject(x):
+        raise TypeError(f"Unsupported types ({type(x)}) passed to `{func.__name__}`. Only nested list/tuple/dicts of "
+                        f"objects that are valid for `{test_type.__name__}` should be passed.")
+
+    return _tree_map(lambda x: func(x, *args, **kwargs), data, test_type, reject if error_on_other_type else None)
 
 
 def send_to_device(tensor, device, non_blocking=False, skip_keys=None):
-    """Recursively move tensors (and objects with a `.to`) to `device`."""
-    if is_torch_tensor(tensor) or hasattr(tensor, "to"):
-        if device == "npu":
-            device = "npu:0"
+    """Move every tensor (and any object with a `.to`) in a nested structure to `device`; mapping entries named in
+    `skip_keys` stay where they are. Objects whose `.to` takes no `non_blocking` are moved synchronously."""
+    if hasattr(tensor, "to"):  # tensors, modules, BatchEncoding-like objects: the object moves itself
         try:
             return tensor.to(device, non_blocking=non_blocking)
         except TypeError:
             return tensor.to(device)
-        except AssertionError as error:
-            raise error
-    elif isinstance(tensor, (tuple, list)):
-        return honor_type(tensor, (send_to_device(t, device, non_blocking=non_blocking, skip_keys=skip_keys) for t in tensor))
-    elif isinstance(tensor, Mapping):
-        if isinstance(skip_keys, str):
-            skip_keys = [skip_keys]
-        elif skip_keys is None:
-            skip_keys = []
-        return type(tensor)(
-            {
-                k: t if k in skip_keys else send_to_device(t, device, non_blocking=non_blocking, skip_keys=skip_keys)
-                for k, t in tensor.items()
-            }
-        )
+    skip = {skip_keys} if isinstance(skip_keys, str) else set(skip_keys or ())
+    if isinstance(tensor, Mapping):
+        return type(tensor)({k: v if k in skip else send_to_device(v, device, non_blocking, skip_keys)
+                             for k, v in tensor.items()})
+    if isinstance(tensor, (list, tuple)):
+        return honor_type(tensor, (send_to_device(v, device, non_blocking, skip_keys) for v in tensor))
     return tensor
 
 
 def get_data_structure(data):
-    """Replace every tensor by its `TensorInformation` (shape + dtype)."""
-
-    def _get_data_structure(tensor):
-        return TensorInformation(shape=tensor.shape, dtype=tensor.dtype)
-
-    return recursively_apply(_get_data_structure, data)
+    """The same structure with every tensor replaced by its `TensorInformation` (shape, dtype)."""
+    return _tree_map(lambda t: TensorInformation(shape=t.shape, dtype=t.dtype), data, is_torch_tensor)
 
 
 def get_shape(data):
-    def _get_shape(tensor):
-        return list(tensor.shape)
-
-    return recursively_apply(_get_shape, data)
+    return _tree_map(lambda t: list(t.shape), data, is_torch_tensor)
 
 
 def initialize_tensors(data_structure):
-    """Allocate empty tensors matching a structure of `TensorInformation`."""
-
-    def _initialize_tensor(tensor_info):
-        return torch.empty(*tensor_info.shape, dtype=tensor_info.dtype)
-
-    return recursively_apply(_initialize_tensor, data_structure, test_type=is_tensor_information)
+    """Uninitialised tensors for a structure of `TensorInformation` (the receive side of a structure broadcast)."""
+    return _tree_map(lambda info: torch.empty(*info.shape, dtype=info.dtype), data_structure, is_tensor_information)
 
 
 def find_batch_size(data):
-    """First dimension of the first tensor found in `data`."""
-    if isinstance(data, (tuple, list, Mapping)) and (len(data) == 0):
+    """Size of dim 0 of the first tensor in `data` (depth first)."""
+    if isinstance(data, (tuple, list, Mapping)) and len(data) == 0:
         raise ValueError(f"Cannot find the batch size from empty {type(data)}.")
-    if isinstance(data, (tuple, list)):
-        return find_batch_size(data[0])
-    elif isinstance(data, Mapping):
-        for k in data.keys():
-            return find_batch_size(data[k])
-    elif not isinstance(data, torch.Tensor):
+    while isinstance(data, (tuple, list, Mapping)):
+        data = next(iter(data.values())) if isinstance(data, Mapping) else data[0]
+        if isinstance(data, (tuple, list, Mapping)) and len(data) == 0:
+            raise ValueError(f"Cannot find the batch size from empty {type(data)}.")
+    if not isinstance(data, torch.Tensor):
         raise TypeError(f"Can only find the batch size of tensors but got {type(data)}.")
     return data.shape[0]
 
@@ -154,88 +140,73 @@ def ignorant_find_batch_size(data):
     try:
         return find_batch_size(data)
     except (ValueError, TypeError):
-        pass
-    return None
+        return None
 
 
 def listify(data):
-    """Recursively convert tensors to python lists/scalars."""
+    """Tensors -> Python lists / scalars (bf16 through fp32, which `tolist` needs)."""
 
-    def _convert_to_list(tensor):
-        tensor = tensor.detach().cpu()
-        if tensor.dtype == torch.bfloat16:
-            tensor = tensor.to(torch.float32)
-        return tensor.tolist()
+    def to_list(t):
+        t = t.detach().cpu()
+        return (t.float() if t.dtype == torch.bfloat16 else t).tolist()
 
-    return recursively_apply(_convert_to_list, data)
+    return _tree_map(to_list, data, is_torch_tensor)
 
 
 # ------------------------------------------------------------------------------------------------------
-# Debug-mode cross-rank verification
+# Debug-mode cross-rank verification (SURVEY §5.2; enabled by `launch --debug` / ACCELERATE_DEBUG_MODE)
 # ------------------------------------------------------------------------------------------------------
+def _shape_report(name: str, per_rank: list) -> str:
+    rows = "\n".join(f"  - Process {i}: {shape}" for i, shape in enumerate(per_rank))
+    return (f"Cannot apply desired operation due to shape mismatches. All shapes across devices must be valid.\n\n"
+            f"Operation: `{name}`\nInput shapes:\n{rows}")
+
+
 def verify_operation(function):
-    """In debug mode (`ACCELERATE_DEBUG_MODE=1`) all-gather every rank's tensor shapes before the collective
-    and raise `DistributedOperationException` on mismatch (reference `operations.py:355-396`)."""
+    """Debug mode: before the collective, every rank's input shapes are all-gathered (one object gather) and a
+    mismatch raises `DistributedOperationException` on all ranks — instead of RCCL hanging, or silently combining
+    differently shaped buffers. Also refuses inputs on another device type than the process's. Outside debug mode
+    (and in single-process runs) it is a plain call. Reference semantics: utils/operations.py:355-396."""
+
+    name = f"{function.__module__}.{function.__name__}"
 
     @wraps(function)
     def wrapper(*args, **kwargs):
-        if PartialState().distributed_type == DistributedType.NO or not PartialState().debug:
+        state = PartialState()
+        if not state.debug or state.distributed_type == DistributedType.NO:
             return function(*args, **kwargs)
-        operation = f"{function.__module__}.{function.__name__}"
-        if "tensor" in kwargs:
-            tensor = kwargs["tensor"]
-        else:
-            tensor = args[0]
-        if PartialState().device.type != find_device(tensor).type:
+        data = kwargs["tensor"] if "tensor" in kwargs else args[0]
+        dev = find_device(data)
+        if dev is not None and dev.type != state.device.type:
             raise DistributedOperationException(
-                f"One or more of the tensors passed to {operation} were not on the {tensor.device.type} while the "
-                f"`Accelerator` is configured for {PartialState().device.type}. Please move it to the "
-                f"{PartialState().device.type} before calling {operation}."
-            )
-        shapes = get_shape(tensor)
-        output = gather_object([shapes])
-        if output[0] is not None:
-            are_same = output.count(output[0]) == len(output)
-            if not are_same:
-                process_shape_str = "\n  - ".join([f"Process {i}: {shape}" for i, shape in enumerate(output)])
-                raise DistributedOperationException(
-                    f"Cannot apply desired operation due to shape mismatches. All shapes across devices must be valid."
-                    f"\n\nOperation: `{operation}`\nInput shapes:\n  - {process_shape_str}"
-                )
+                f"One or more of the tensors passed to {name} were not on the {dev.type} while the `Accelerator` is "
+                f"configured for {state.device.type}. Please move it to the {state.device.type} before calling {name}.")
+        per_rank = gather_object([get_shape(data)])
+        if per_rank[0] is not None and any(s != per_rank[0] for s in per_rank[1:]):
+            raise DistributedOperationException(_shape_report(name, per_rank))
         return function(*args, **kwargs)
 
     return wrapper
 
 
 def chained_operation(function):
-    """Re-raise `DistributedOperationException` with the outer operation's name."""
+    """Calls made through another collective re-raise a debug-mode mismatch under the outer operation's name."""
+    name = f"{function.__module__}.{function.__name__}"
 
     @wraps(function)
     def wrapper(*args, **kwargs):
         try:
             return function(*args, **kwargs)
-        except DistributedOperationException as e:
-            operation = f"{function.__module__}.{function.__name__}"
+        except DistributedOperationException as exc:
             raise DistributedOperationException(
-                f"Error found while calling `{operation}`. Please see the earlier error for more details."
-            ) from e
+                f"Error found while calling `{name}`. Please see the earlier error for more details.") from exc
 
     return wrapper
 
 
 def find_device(data):
-    if isinstance(data, Mapping):
-        for obj in data.values():
-            device = find_device(obj)
-            if device is not None:
-                return device
-    elif isinstance(data, (tuple, list)):
-        for obj in data:
-            device = find_device(obj)
-            if device is not None:
-                return device
-    elif isinstance(data, torch.Tensor):
-        return data.device
+    """Device of the first tensor in a nested structure (None if it holds no tensor)."""
+    return _tree_first(data, lambda x: x.device if isinstance(x, torch.Tensor) else None)
 
 
 # ------------------------------------------------------------------------------------------------------

@@ -356,3 +356,73 @@ def test_opt_in_upstream_command_aliases(tmp_path):
     assert aliases.remove(str(foreign)) == [] and (foreign / "accelerate").exists()
     main(["aliases", "remove", "--dir", str(d)])
     assert list(d.iterdir()) == []
+
+
+# ---- MPI multi-CPU launches and --debug (reference tests/test_cli.py:117-146, commands/launch.py:870-892) ----------
+def _mpi_cmd(cfgdir, version: bytes):
+    from unittest.mock import patch
+
+    args = launch_command_parser().parse_args(["--config_file", str(cfgdir / "mpi.yaml"), "train.py", "--cpu"])
+    args = _validate_launch_command(args)
+    with patch("accelerate_hpc_test_amd.utils.launch.which", return_value=True), \
+            patch("accelerate_hpc_test_amd.utils.launch.subprocess.check_output", return_value=version):
+        return prepare_simple_launcher_cmd_env(args)
+
+
+def test_mpi_multicpu_config_cmd_intel(cfgdir):
+    cmd, env = _mpi_cmd(cfgdir, b"Intel(R) MPI Library")
+    expected = ["mpirun", "-f", "/tmp/hostfile", "-ppn", "4", "-n", "16"]
+    assert cmd[: len(expected)] == expected
+    assert cmd[len(expected):] == [sys.executable, "train.py", "--cpu"]
+    assert "WORLD_SIZE" not in env and env["MASTER_ADDR"] == "127.0.0.1" and env["MASTER_PORT"] == "29500"
+
+
+def test_mpi_multicpu_config_cmd_openmpi(cfgdir):
+    cmd, _ = _mpi_cmd(cfgdir, b"mpirun (Open MPI) 4.1.2")
+    assert cmd[:9] == ["mpirun", "--hostfile", "/tmp/hostfile", "--npernode", "4", "-n", "16", "--bind-to", "socket"]
+
+
+def test_mpi_launcher_missing_raises(cfgdir):
+    from unittest.mock import patch
+
+    args = _validate_launch_command(launch_command_parser().parse_args(["--config_file", str(cfgdir / "mpi.yaml"), "t.py"]))
+    with patch("accelerate_hpc_test_amd.utils.launch.which", return_value=None), pytest.raises(OSError, match="mpirun"):
+        prepare_simple_launcher_cmd_env(args)
+
+
+def test_launch_debug_flag_sets_debug_mode():
+    args = _validate_launch_command(launch_command_parser().parse_args(["--debug", "--cpu", "x.py"]))
+    assert args.debug
+    _, env = prepare_simple_launcher_cmd_env(args)
+    assert env["ACCELERATE_DEBUG_MODE"] == "true"
+
+
+_MISMATCH_SCRIPT = """
+import torch
+from accelerate_hpc_test_amd import Accelerator
+from accelerate_hpc_test_amd.utils import DistributedOperationException
+acc = Accelerator(cpu=True)
+t = torch.ones(acc.process_index + 2)  # a different shape on every rank
+try:
+    acc.gather(t)
+except DistributedOperationException as e:
+    print("MISMATCH CAUGHT", acc.process_index, "Process 1: [3]" in str(e))
+else:
+    print("NO CHECK", acc.process_index)
+"""
+
+
+def test_launch_debug_trips_verify_operation(tmp_path):
+    """`launch --debug`: a collective with mismatched shapes raises DistributedOperationException on every rank
+    instead of hanging or corrupting (SURVEY §5.2 debug-mode operation checker)."""
+    import socket
+
+    script = tmp_path / "mismatch.py"
+    script.write_text(_MISMATCH_SCRIPT)
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    r = _run([sys.executable, "-m", "accelerate_hpc_test_amd.commands.accelerate_cli", "launch", "--cpu", "--debug",
+              "--num_processes", "2", "--main_process_port", str(port), str(script)], env={"HF_HOME": str(tmp_path)})
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.stdout.count("MISMATCH CAUGHT") == 2 and "MISMATCH CAUGHT 0 True" in r.stdout, r.stdout[-2000:]

@@ -143,8 +143,9 @@ def test_ddp_powersgd_hook():
     debug_launcher(td.check_ddp_powersgd, num_processes=2)
 
 
-def test_local_sgd():
-    debug_launcher(td.check_local_sgd, num_processes=2)
+@pytest.mark.parametrize("chunk_bytes", [256 << 20, 64])
+def test_local_sgd(chunk_bytes):
+    debug_launcher(td.check_local_sgd, args=(2, 4, chunk_bytes), num_processes=2)
 
 
 def test_fsdp_three_ranks():
