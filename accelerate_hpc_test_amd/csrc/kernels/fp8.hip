@@ -902,6 +902,198 @@ __global__ __launch_bounds__(512, 1) void fp8_gemm_v3_w8_kernel(const uint8_t* _
   fp8_gemm_v3_body<FA, FB, OUT_F32, 8>(A, B, sa, sb, smul, bias, C, M, N, K, accum, group_m);
 }
 
+// ------------------------------------------------------------------------------------------------ GEMM v4
+// 256x256 output tile, 4 waves (2 x 2, one per SIMD, 128x128 per wave), v_mfma 16x16x128 f8f6f4: 8 x 8 accumulator
+// blocks of 4 registers (256 AGPR/VGPR). The 16x16 shape holds a higher clock under load than 32x32 at equal
+// cycles per FLOP (MI355X DVFS give-back, item 7), and with unit block scales the scale operands can be dropped:
+// UNSCALED passes scale 0, which hipcc lowers to the plain v_mfma_f32_16x16x128_f8f6f4 (no ld_scale prefix).
+// BK = 128 fp8 bytes per K-step = one MFMA K. Two LDS slots of 64 KiB (A 256x128 | B 256x128) filled by
+// buffer_load ... lds. Per K-step t (slot s = t % 2):
+//   rows i = 0..5 of the wave's A blocks: A fragment i+1 read while the 8 MFMAs of row i run (B fragments of t are
+//     already in registers)
+//   vmcnt(0) + barrier: the DMA of t+1 (slot s^1, issued at the start of t) landed for every wave
+//   rows i = 6, 7 + the B fragments and first A fragment of t+1 read from slot s^1 between their MFMAs
+//   lgkmcnt(0) + barrier: every wave is done with slot s -> DMA of t+2 into slot s (interleaved with the next
+//     step's first MFMAs)
+// Image rows are 128 B; the 16-B chunk swizzle c ^ ((row >> 1) & 7) makes every 16-lane ds_read_b128 group of a
+// 16x16x128 fragment read (lane (r, q): chunks q and q + 4 of row r) hit 16 distinct 16-B slots of the bank row.
+constexpr int V4_BM = 256, V4_BN = 256, V4_BK = 128;
+constexpr int V4_SLOT = (V4_BM + V4_BN) * V4_BK;  // 64 KiB
+constexpr int V4_BOFF = V4_BM * V4_BK;
+
+__device__ __forceinline__ int v4_swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int FA, int FB, bool OUT_F32, bool UNSCALED>
+__global__ __launch_bounds__(256, 1) void fp8_gemm_v4_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
+                                                             const float* __restrict__ sa, const float* __restrict__ sb,
+                                                             float smul, const bf16_t* __restrict__ bias, void* __restrict__ C,
+                                                             int M, int N, int K, int accum, int group_m) {
+  __shared__ __attribute__((aligned(1024))) uint8_t slot0[V4_SLOT];
+  __shared__ __attribute__((aligned(1024))) uint8_t slot1[V4_SLOT];
+  const int tiles_n = N / V4_BN, tiles_m = M / V4_BM;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  int tile_m, tile_n;
+  if (group_m > 1) {
+    const int per_group = group_m * tiles_n;
+    const int g = bid / per_group, first = g * group_m, rows = min(tiles_m - first, group_m), in = bid % per_group;
+    tile_m = first + in % rows;
+    tile_n = in / rows;
+  } else {
+    tile_m = bid / tiles_n;
+    tile_n = bid % tiles_n;
+  }
+  const int tm = tile_m * V4_BM, tn = tile_n * V4_BN;
+  ACC_CHECK_OR_RETURN(tm + V4_BM <= M && tn + V4_BN <= N && K % 256 == 0 && bid < nwg, kChkGemmTile);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r16 = lane & 15, q = lane >> 4;
+  const int wm = (wave >> 1) * 128, wn = (wave & 1) * 128;
+  constexpr int SC = UNSCALED ? 0 : 0x7f7f7f7f;
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // DMA: each operand image = 32 blocks of 8 rows x 128 B (1 KiB); wave w fills blocks 8w .. 8w + 7 of both. Lane l
+  // of a block writes row 8b + l / 8, physical chunk l % 8, which holds logical chunk (l % 8) ^ ((row >> 1) & 7).
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  unsigned voff[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int row = (wv * 8 + t) * 8 + (lane >> 3);
+    voff[t] = (unsigned)(row * K + v4_swz(row, lane & 7) * 16);
+  }
+  const auto a_rs = __builtin_amdgcn_make_buffer_rsrc((void*)(A + (long)tm * K), (short)0, V4_BM * K, 0x00020000);
+  const auto b_rs = __builtin_amdgcn_make_buffer_rsrc((void*)(B + (long)tn * K), (short)0, V4_BN * K, 0x00020000);
+  const int nk = K / V4_BK;
+  // past the last K-step the DMA still issues (one count for every wait) with an soffset beyond the descriptor: the
+  // range check returns zeros into a slot nobody reads again
+  auto stage = [&](int kt, uint8_t* base) {
+    const int so = kt < nk ? kt * V4_BK : 0x40000000;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rs, base + (wv * 8 + t) * 1024, 16, voff[t], so, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rs, base + V4_BOFF + (wv * 8 + t) * 1024, 16, voff[t], so, 0, 0);
+    }
+  };
+  // fragment rows (wm | wn) + 16 i + r16 share (row >> 1) & 7 == (r16 >> 1) & 7
+  const int f = (r16 >> 1) & 7;
+  const int lo = (q ^ f) * 16, hi = ((q + 4) ^ f) * 16;
+  const int arow = (wm + r16) * V4_BK, brow = V4_BOFF + (wn + r16) * V4_BK;
+  auto frag = [&](const uint8_t* p) -> v8i {
+    const uint4 a = *reinterpret_cast<const uint4*>(p + lo);
+    const uint4 b = *reinterpret_cast<const uint4*>(p + hi);
+    v8i v;
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    return v;
+  };
+  auto mfma_row = [&](const v8i& af, const v8i (&bf)[8], int i) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)  // swapped operands: acc holds C^T blocks (lane <-> m, registers <-> 4 n)
+      acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bf[j], af, acc[i][j], FB, FA, 0, SC, 0, SC);
+  };
+
+  stage(0, slot0);
+  stage(1, slot1);
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // slot 0 landed (this wave), slot 1 in flight
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  v8i bx[8], by[8], a0x, a0y;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bx[j] = frag(slot0 + brow + j * 16 * V4_BK);
+  a0x = frag(slot0 + arow);
+
+  // one K-step: `bc` / `a0c` = fragments of t (registers), `bn` / `a0n` <- fragments of t+1 from `nxt`
+  auto step = [&](int t, uint8_t* cur, const uint8_t* nxt, v8i (&bc)[8], v8i (&bn)[8], v8i& a0c, v8i& a0n) {
+    v8i ar[2];
+    ar[0] = a0c;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      ar[(i + 1) & 1] = frag(cur + arow + (i + 1) * 16 * V4_BK);
+      mfma_row(ar[i & 1], bc, i);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // t+1 landed (this wave's part)
+    __builtin_amdgcn_s_barrier();                    // ... and every wave's
+    __builtin_amdgcn_sched_barrier(0);
+    ar[1] = frag(cur + arow + 7 * 16 * V4_BK);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bn[j] = frag(nxt + brow + j * 16 * V4_BK);
+    a0n = frag(nxt + arow);
+    mfma_row(ar[0], bc, 6);
+    mfma_row(ar[1], bc, 7);
+    // 16 MFMAs, 20 ds_reads: the reads of t+1 hide under this half's MFMAs
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
+      __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);    // MFMA
+    }
+#pragma unroll
+    for (int k = 4; k < 16; ++k) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of `cur` retired
+    __builtin_amdgcn_s_barrier();                      // ... every wave's
+    __builtin_amdgcn_sched_barrier(0);
+    stage(t + 2, cur);
+  };
+  for (int t = 0; t < nk; t += 2) {  // nk even (host check: K % 256 == 0)
+    step(t, slot0, slot1, bx, by, a0x, a0y);
+    step(t + 1, slot1, slot0, by, bx, a0y, a0x);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the zero-fill DMAs past the end retire before the exit
+
+  const float s = sa[0] * sb[0] * smul;
+  auto epilogue = [&](auto has_bias, auto acc_in) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int m = tm + wm + i * 16 + r16;
+        const int n = tn + wn + j * 16 + 4 * q;
+        float v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = acc[i][j][u] * s;
+        if constexpr (decltype(has_bias)::value) {
+          const bf16x4 b4 = *reinterpret_cast<const bf16x4*>(bias + n);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) v[u] += bf2f(b4.v[u]);
+        }
+        if constexpr (OUT_F32) {
+          float4* cp4 = reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + (long)m * N + n);
+          if constexpr (decltype(acc_in)::value) {
+            const float4 o = *cp4;
+            v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+          }
+          *cp4 = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+          bf16x4* cp4 = reinterpret_cast<bf16x4*>(reinterpret_cast<bf16_t*>(C) + (long)m * N + n);
+          if constexpr (decltype(acc_in)::value) {
+            const bf16x4 o = *cp4;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] += bf2f(o.v[u]);
+          }
+          bf16x4 w;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) w.v[u] = f2bf(v[u]);
+          *cp4 = w;
+        }
+      }
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  if (bias != nullptr) {
+    if (accum) epilogue(T_{}, T_{}); else epilogue(T_{}, F_{});
+  } else {
+    if (accum) epilogue(F_{}, T_{}); else epilogue(F_{}, F_{});
+  }
+}
+
 }  // namespace
 
 ACC_DEBUG_TAKE_FN(acc_dbg_take_fp8)
@@ -1062,13 +1254,13 @@ void fp8_cast_into(torch::Tensor x, torch::Tensor t, double qmax, bool from_amax
 }
 
 // Kernel choice of fp8_gemm: 0 = default, 1 = v1 (128x128), 2 = v2 4 waves, 3 = v2 8 waves, 4 = v3 (4-deep ring),
-// 5 = v3 8 waves.
+// 5 = v3 8 waves, 6 = v4 (16x16x128 MFMA, BK 128, two slots), 7 = v4 with the unscaled MFMA opcode.
 // Shapes a variant cannot tile fall back to the next one that can (v3 -> v2 -> v1).
 constexpr int kFp8GemmDefault = 4;
 static int g_fp8_gemm_variant = 0;
 static int g_fp8_gemm_group_m = 4;  // v3 tile-row grouping (1 = plain row-major tile order)
 void fp8_gemm_select(int64_t variant, int64_t group_m) {
-  TORCH_CHECK(variant >= 0 && variant <= 5, "fp8_gemm_select: variant 0..5");
+  TORCH_CHECK(variant >= 0 && variant <= 7, "fp8_gemm_select: variant 0..7");
   TORCH_CHECK(group_m >= 0 && group_m <= 64, "fp8_gemm_select: group_m 0..64");
   g_fp8_gemm_variant = (int)variant;
   if (group_m > 0) g_fp8_gemm_group_m = (int)group_m;
@@ -1115,6 +1307,27 @@ torch::Tensor fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor a_scale_i
   }();
   int variant = g_fp8_gemm_variant;
   if (variant == 0) variant = force_v1 ? 1 : (env_w8 ? 3 : kFp8GemmDefault);
+  if ((variant == 6 || variant == 7) && M % V4_BM == 0 && N % V4_BN == 0 && K % 256 == 0 && (long)V4_BM * K < (1L << 30) &&
+      (reinterpret_cast<uintptr_t>(bp) & 7) == 0) {
+    const int nwg4 = (M / V4_BM) * (N / V4_BN);
+    const bool un = variant == 7;
+#define GEMM4_LAUNCH(FA, FB, OF)                                                                                        \
+  do {                                                                                                                  \
+    if (un)                                                                                                             \
+      hipLaunchKernelGGL((fp8_gemm_v4_kernel<FA, FB, OF, true>), dim3(nwg4), dim3(256), 0, stream, ap, bptr, sap, sbp,   \
+                         (float)smul, bp, cp, M, N, K, accum, g_fp8_gemm_group_m);                                       \
+    else                                                                                                                \
+      hipLaunchKernelGGL((fp8_gemm_v4_kernel<FA, FB, OF, false>), dim3(nwg4), dim3(256), 0, stream, ap, bptr, sap, sbp,  \
+                         (float)smul, bp, cp, M, N, K, accum, g_fp8_gemm_group_m);                                       \
+  } while (0)
+    if (!a_e5m2 && !b_e5m2) { if (out_fp32) GEMM4_LAUNCH(0, 0, true); else GEMM4_LAUNCH(0, 0, false); }
+    else if (!a_e5m2 && b_e5m2) { if (out_fp32) GEMM4_LAUNCH(0, 1, true); else GEMM4_LAUNCH(0, 1, false); }
+    else if (a_e5m2 && !b_e5m2) { if (out_fp32) GEMM4_LAUNCH(1, 0, true); else GEMM4_LAUNCH(1, 0, false); }
+    else { if (out_fp32) GEMM4_LAUNCH(1, 1, true); else GEMM4_LAUNCH(1, 1, false); }
+#undef GEMM4_LAUNCH
+    return out;
+  }
+  if (variant == 6 || variant == 7) variant = 4;  // shapes v4 cannot tile
   const bool v3 = variant == 4 || variant == 5;
   if (v3 && !(M % V3_BM == 0 && N % V3_BN == 0 && K % (4 * V3_BK) == 0)) variant = 2;
   if (v3 && (reinterpret_cast<uintptr_t>(bp) & 7) != 0) variant = 2;  // v3 reads the bias 4 at a time

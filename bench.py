@@ -53,6 +53,8 @@ def parse():
     p.add_argument("--fsdp-cpu-offload", action="store_true",
                    help="FSDP CPU offload: fp32 master/grad shards + AdamW state in pinned host memory, host AdamW")
     p.add_argument("--verbose", action="store_true")
+    p.add_argument("--no-preflight", action="store_true",
+                   help="skip the N>1 communicator self-test (known-value AG/RS/all-reduce + bus bandwidth per group)")
     p.add_argument("--cpu", action="store_true",
                    help="contract check only: run the same loop on CPU ranks (gloo) with a small --model; not a benchmark")
     p.add_argument("--gemm-tuning", default="auto", choices=["auto", "off", "tune"],
@@ -182,6 +184,16 @@ def main():
     model.train()
     sync()
     accelerator.heartbeat("prepared")
+    preflight = None
+    if world > 1 and not args.no_preflight:
+        # every communicator the run uses, checked before training: a broken one ends the run with a JSON line that
+        # names it (exit 3) instead of a hang in the first all-gather
+        from accelerate_hpc_test_amd.utils.preflight import preflight_model
+
+        preflight = preflight_model(model, accelerator.device, big_bytes=(1 << 20) if args.cpu else (436 << 20))
+        accelerator.heartbeat("preflight")
+        if args.verbose:
+            accelerator.print(f"preflight: {json.dumps(preflight)}", flush=True)
     if args.verbose and accelerator.is_main_process and not args.cpu:
         print(f"setup {time.time() - t0:.1f}s, mem {torch.cuda.memory_allocated() / 2**30:.1f} GiB", flush=True)
 
@@ -268,6 +280,7 @@ def main():
             "final_loss": round(last_loss.item(), 4) if last_loss is not None else None,
             "baseline_tokens_per_sec": base_dev * world if headline else None,
             "gemm_table": os.path.basename(gemm_table) if gemm_table else None,
+            "preflight": preflight,
         }
         print(json.dumps(rec), flush=True)
     accelerator.end_training()

@@ -28,6 +28,8 @@ def test_bench_two_ranks_prints_one_json_line(tmp_path):
     assert rec["n_gpus"] == 2 and rec["steps"] == 2 and rec["warmup"] == 1 and rec["scaling"] == "weak"
     assert rec["config"]["global_batch"] == 2 and rec["config"]["seq_len"] == 256 and rec["config"]["model"] == "llama-tiny"
     assert rec["config"]["parallelism"] == "fsdp2" and rec["vs_baseline"] is None  # not the headline model
+    pf = rec["preflight"]  # every communicator checked before training (utils/preflight.py)
+    assert pf["world"]["ok"] and pf["fsdp_all_gather"]["ok"] and pf["fsdp_reduce_scatter"]["ok"], pf
     # value is the whole-job rate: all ranks' tokens over the slowest rank's timed window
     tokens = 2 * 1 * 256 * 2
     assert abs(rec["value"] - tokens / (rec["ms_per_step"] * 2 / 1000)) / rec["value"] < 0.01, rec

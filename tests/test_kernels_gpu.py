@@ -276,6 +276,44 @@ def test_fp8_gemm_v2_matches_v1_random():
     assert torch.allclose(outs[0], outs[1], rtol=1e-5, atol=1e-3), (outs[0] - outs[1]).abs().max()
 
 
+@pytest.mark.parametrize("M,N,K", [(256, 256, 256), (512, 768, 1024), (1024, 512, 4096), (768, 1280, 2304)])
+def test_fp8_gemm_v4_kernel_matches_reference(M, N, K, monkeypatch):
+    """The 16x16x128-MFMA kernel (v4: two 64 KiB LDS slots, BK 128) with the scaled (variant 6) and the unscaled
+    (variant 7) MFMA opcode, on the hand-written path: exact small integers (bit-exact vs fp32 matmul, pins the operand
+    layout and swizzle), then random scaled e4m3 x e5m2 operands with bias / fp32 and bf16 outputs / accumulate
+    against the fp32 reference of the dequantised operands."""
+    from accelerate_hpc_test_amd.ops import fp8
+    from accelerate_hpc_test_amd.ops._ext import ext
+
+    monkeypatch.setattr(fp8, "_FP8_GEMM_BACKEND", "hip")
+    torch.manual_seed(0)
+    one = torch.ones(1, device=DEV)
+    ai = torch.randint(-3, 4, (M, K), device=DEV).to(torch.bfloat16)
+    bi = torch.randint(-3, 4, (N, K), device=DEV).to(torch.bfloat16)
+    a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    b = torch.randn(N, K, device=DEV, dtype=torch.bfloat16)
+    bias = torch.randn(N, device=DEV, dtype=torch.bfloat16)
+    sa, sb = fp8.Scale(fp8.amax(a), fp8.E4M3_MAX), fp8.Scale(fp8.amax(b), fp8.E5M2_MAX)
+    a8, b8 = fp8.cast(a, sa), fp8.cast(b, sb, e5m2=True)
+    ref = (a8.float() * sa.inv()) @ (b8.float() * sb.inv()).t() + bias.float()
+    base = torch.randn(M, N, device=DEV)
+    exact_ref = ai.float() @ bi.float().t()
+    try:
+        for v in (6, 7):
+            ext().fp8_gemm_select(v)
+            exact = fp8.gemm(fp8.cast(ai, one), fp8.cast(bi, one), one, one, out_dtype=torch.float32)
+            assert torch.equal(exact, exact_ref), (v, (exact - exact_ref).abs().max())
+            o32 = fp8.gemm(a8, b8, sa, sb, bias, torch.float32)
+            assert torch.allclose(o32, ref, rtol=1e-4, atol=1e-3 * ref.abs().max().item()), (v, (o32 - ref).abs().max())
+            o16 = fp8.gemm(a8, b8, sa, sb, bias, torch.bfloat16)
+            assert _rel(o16.float(), ref) < 1e-2, (v, _rel(o16.float(), ref))
+            acc = base.clone()
+            fp8.gemm(a8, b8, sa, sb, bias, out=acc, accumulate=True)
+            assert torch.allclose(acc, base + ref, rtol=1e-4, atol=1e-3 * ref.abs().max().item()), v
+    finally:
+        ext().fp8_gemm_select(0)
+
+
 @pytest.mark.parametrize("M,N,K", [(256, 256, 256), (512, 768, 1024), (1024, 512, 4096), (256, 1280, 768)])
 def test_fp8_gemm_v3_ring_kernel_matches_reference(M, N, K):
     """The 4-deep-ring kernel (v3: buffer_load...lds, counted vmcnt, one barrier per K-tile) on exact small integers
