@@ -23,7 +23,7 @@ import os
 import torch
 
 
-GLOBAL_BATCH = 4
+GLOBAL_BATCH = 8  # divisible by every rehearsed world size (1 / 2 / 4 / 8)
 SEQ = 256
 
 
@@ -34,7 +34,7 @@ def _batches(steps, vocab):
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--mode", choices=["fsdp", "fsdp_fp8", "ddp", "cp_allgather", "cp_alltoall"], required=True)
+    p.add_argument("--mode", choices=["fsdp", "fsdp_fp8", "ddp", "hsdp", "cp_allgather", "cp_alltoall"], required=True)
     p.add_argument("--seq", type=int, default=16384)
     p.add_argument("--heads", default="8,2", help="cp modes: query,kv heads")
     p.add_argument("--no-ref", action="store_true", help="cp modes: skip the fp32 reference (long sequences)")
@@ -65,8 +65,13 @@ def main():
         if args.mode == "fsdp_fp8":
             handlers.append(AORecipeKwargs(enable_fsdp_float8_all_gather=True))
         handlers.append(RcclKwargs())
+        pc = None
+        if args.mode == "hsdp" and W > 1:  # 2 replicas x W/2 shards: reduce-scatter in the shard group + replica all-reduce
+            from accelerate_hpc_test_amd import ParallelismConfig
+
+            pc = ParallelismConfig(dp_replicate_size=2, dp_shard_size=W // 2)
         acc = Accelerator(mixed_precision="fp8" if args.mode == "fsdp_fp8" else "bf16", fsdp_plugin=plugin,
-                          kwargs_handlers=handlers, cpu=args.cpu)
+                          kwargs_handlers=handlers, cpu=args.cpu, parallelism_config=pc)
         with torch.device("meta"):
             model = LlamaForCausalLM(cfg)
     r = acc.process_index
@@ -80,6 +85,7 @@ def main():
         # parameters cut by a shard boundary (the case the forced one-GPU mode never has)
         facts["split_params"] = sum(1 for u in eng.units for i in u.infos if 0 < i.local_hi - i.local_lo < i.numel)
         facts["fp8_units"] = len(eng.f8_units)
+        facts["replicated"] = eng.replicate_group is not None
     else:
         facts["ddp_buckets"] = len(getattr(model, "buckets", []))
     if W > 1:

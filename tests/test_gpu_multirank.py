@@ -54,14 +54,16 @@ def _reference(mode, outdir):
     return _REF[mode]
 
 
-@pytest.mark.parametrize("world", [2, 4])
-@pytest.mark.parametrize("mode", ["fsdp", "fsdp_fp8", "ddp"])
+@pytest.mark.parametrize("mode,world", [(m, w) for m in ("fsdp", "fsdp_fp8", "ddp") for w in (2, 4)]
+                         + [("fsdp", 8), ("ddp", 8), ("hsdp", 4), ("hsdp", 8)])
 def test_ranks_sharing_one_gpu_match_single_process(mode, world, outdir):
-    ref, ref_params = _reference(mode, outdir)
+    """W = 8 is the driver's scaling node's rank count; HSDP = 2 replicas x W/2 shards (dp_replicate x dp_shard)."""
+    ref, ref_params = _reference("fsdp" if mode == "hsdp" else mode, outdir)
     res, params = _run(mode, world, outdir)
     assert res["world"] == world and res["ipc_allreduce"], res  # clip-norm / amax / reduce over the IPC kernel
     if mode != "ddp":
         assert res["sharded"] and res["split_params"] > 0, res  # real partial-parameter shards
+        assert res["replicated"] == (mode == "hsdp"), res
         if mode == "fsdp_fp8":
             assert res["fp8_units"] > 0
     if mode == "fsdp":
