@@ -205,6 +205,143 @@ bool blaslt_wgrad_f32(torch::Tensor dy, torch::Tensor x, torch::Tensor out, bool
                                out.data_ptr(), plan->lc, out.data_ptr(), plan->lc, &plan->algo, ws, kWorkspace, stream));
 }
 
+// ------------------------------------------------------------------------------------------------ bf16 dgrad, NN layout
+// dx[T, K] = dy[T, N] . W[N, K] with both operands row-major as the autograd graph holds them (no transposed weight
+// copy). Column-major view: D (K x T, ld K) = A (W: K x N, ld K, op N) . B (dy: N x T, ld N, op N). torch's matmul
+// reaches hipBLASLt's first heuristic choice for this NN class only; here the candidates are timed once per
+// (power-of-two T bucket, N, K) as for the weight gradient above, and other token counts of a bucket reuse the winner
+// (or the heuristic's first choice where it does not apply) without a search.
+namespace {
+
+struct DgState {
+  std::map<std::tuple<int64_t, int64_t, int64_t, int>, Plan> plans;
+};
+
+DgState& dgstate() {
+  static DgState s;
+  return s;
+}
+
+bool dg_layouts(int64_t T, int64_t N, int64_t K, hipblasLtMatrixLayout_t* la, hipblasLtMatrixLayout_t* lb,
+                hipblasLtMatrixLayout_t* lc) {
+  return check(hipblasLtMatrixLayoutCreate(la, HIP_R_16BF, K, N, K)) && check(hipblasLtMatrixLayoutCreate(lb, HIP_R_16BF, N, T, N)) &&
+         check(hipblasLtMatrixLayoutCreate(lc, HIP_R_16BF, K, T, K));
+}
+
+bool build_dg_plan(State& s, Plan& p, int64_t T, int64_t N, int64_t K, hipStream_t stream, const torch::Tensor& like) {
+  const hipblasOperation_t op = HIPBLAS_OP_N;
+  if (!check(hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F))) return false;
+  if (!check(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &op, sizeof(op)))) return false;
+  if (!check(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &op, sizeof(op)))) return false;
+  if (!dg_layouts(T, N, K, &p.la, &p.lb, &p.lc)) return false;
+  hipblasLtMatmulPreference_t pref;
+  if (!check(hipblasLtMatmulPreferenceCreate(&pref))) return false;
+  uint64_t ws = kWorkspace;
+  hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &ws, sizeof(ws));
+  std::vector<hipblasLtMatmulHeuristicResult_t> res(32);
+  int got = 0;
+  const bool okh = check(hipblasLtMatmulAlgoGetHeuristic(s.handle, p.desc, p.la, p.lb, p.lc, p.lc, pref, (int)res.size(),
+                                                         res.data(), &got));
+  hipblasLtMatmulPreferenceDestroy(pref);
+  if (!okh || got <= 0) return false;
+  p.candidates = got;
+  auto w = torch::empty({N, K}, like.options().dtype(torch::kBFloat16)).normal_();
+  auto dy = torch::empty({T, N}, like.options().dtype(torch::kBFloat16)).normal_();
+  auto d = torch::empty({T, K}, like.options().dtype(torch::kBFloat16));
+  const float one = 1.f, zero = 0.f;
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  float best = 1e30f;
+  for (int i = 0; i < got; ++i) {
+    if (res[i].state != HIPBLAS_STATUS_SUCCESS || res[i].workspaceSize > kWorkspace) continue;
+    auto run = [&]() {
+      return hipblasLtMatmul(s.handle, p.desc, &one, w.data_ptr(), p.la, dy.data_ptr(), p.lb, &zero, d.data_ptr(), p.lc,
+                             d.data_ptr(), p.lc, &res[i].algo, workspace_for(s, stream, like), kWorkspace, stream);
+    };
+    if (!check(run())) continue;
+    hipEventRecord(e0, stream);
+    for (int r = 0; r < 3; ++r) run();
+    hipEventRecord(e1, stream);
+    hipEventSynchronize(e1);
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, e0, e1);
+    if (ms < best) {
+      best = ms;
+      p.algo = res[i].algo;
+      p.ok = true;
+    }
+  }
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  p.ms = best / 3.f;
+  p.T = T;
+  return p.ok;
+}
+
+}  // namespace
+
+// Returns false (nothing launched) when hipBLASLt offers no algorithm: the caller falls back to torch.
+bool blaslt_dgrad_bf16(torch::Tensor dy, torch::Tensor w, torch::Tensor out) {
+  TORCH_CHECK(dy.is_cuda() && w.is_cuda() && out.is_cuda() && dy.scalar_type() == at::kBFloat16 &&
+                  w.scalar_type() == at::kBFloat16 && out.scalar_type() == at::kBFloat16,
+              "blaslt_dgrad_bf16: bf16 HIP tensors expected");
+  TORCH_CHECK(dy.dim() == 2 && w.dim() == 2 && out.dim() == 2 && dy.is_contiguous() && w.is_contiguous() && out.is_contiguous(),
+              "blaslt_dgrad_bf16: 2-D contiguous tensors expected");
+  const int64_t T = dy.size(0), N = dy.size(1), K = w.size(1);
+  TORCH_CHECK(w.size(0) == N && out.size(0) == T && out.size(1) == K, "blaslt_dgrad_bf16: shape mismatch");
+  State& s = state();
+  hipStream_t stream = at::hip::getCurrentHIPStream();
+  std::lock_guard<std::mutex> lk(s.mu);
+  if (s.handle == nullptr) {
+    if (!check(hipblasLtCreate(&s.handle))) return false;
+    s.workspace = torch::empty({(int64_t)kWorkspace}, out.options().dtype(torch::kUInt8));
+  }
+  auto key = std::make_tuple(dim_bucket(T), N, K, (int)out.get_device());
+  auto& plans = dgstate().plans;
+  auto it = plans.find(key);
+  if (it == plans.end()) {
+    Plan p;
+    build_dg_plan(s, p, T, N, K, stream, out);
+    it = plans.emplace(key, p).first;
+  }
+  Plan& plan = it->second;
+  if (!plan.ok) return false;
+  void* ws = workspace_for(s, stream, out);
+  const float one = 1.f, zero = 0.f;
+  if (plan.T == T)
+    return check(hipblasLtMatmul(s.handle, plan.desc, &one, w.data_ptr(), plan.la, dy.data_ptr(), plan.lb, &zero,
+                                 out.data_ptr(), plan.lc, out.data_ptr(), plan.lc, &plan.algo, ws, kWorkspace, stream));
+  hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, lc = nullptr;
+  bool ok = dg_layouts(T, N, K, &la, &lb, &lc);
+  hipblasLtMatmulAlgo_t algo = plan.algo;
+  if (ok) {
+    size_t wsz = 0;
+    if (hipblaslt_ext::matmulIsAlgoSupported(s.handle, plan.desc, (void*)&one, la, lb, (void*)&zero, lc, lc, algo, wsz) !=
+            HIPBLAS_STATUS_SUCCESS || wsz > kWorkspace) {
+      hipblasLtMatmulPreference_t pref;
+      ok = check(hipblasLtMatmulPreferenceCreate(&pref));
+      if (ok) {
+        uint64_t wsl = kWorkspace;
+        hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsl, sizeof(wsl));
+        hipblasLtMatmulHeuristicResult_t r;
+        int got = 0;
+        ok = check(hipblasLtMatmulAlgoGetHeuristic(s.handle, plan.desc, la, lb, lc, lc, pref, 1, &r, &got)) && got > 0 &&
+             r.state == HIPBLAS_STATUS_SUCCESS;
+        if (ok) algo = r.algo;
+        hipblasLtMatmulPreferenceDestroy(pref);
+      }
+    }
+  }
+  if (ok)
+    ok = check(hipblasLtMatmul(s.handle, plan.desc, &one, w.data_ptr(), la, dy.data_ptr(), lb, &zero, out.data_ptr(), lc,
+                               out.data_ptr(), lc, &algo, ws, kWorkspace, stream));
+  if (la) hipblasLtMatrixLayoutDestroy(la);
+  if (lb) hipblasLtMatrixLayoutDestroy(lb);
+  if (lc) hipblasLtMatrixLayoutDestroy(lc);
+  return ok;
+}
+
 // ------------------------------------------------------------------------------------------------ fp8, per-tensor
 // C[M, N] (=|+=) alpha * sa * sb * (A[M, K] . B[N, K]^T)   A, B: row-major (K-contiguous) e4m3 / e5m2; sa, sb: device
 // fp32 [1] scale factors read by the kernel (Fp8Linear passes each operand's amax and folds 1 / (qmax_a * qmax_b)

@@ -17,6 +17,9 @@ from ._ext import ext, use_native
 _DGRAD_WT = os.environ.get("ACCELERATE_DGRAD_WT", "1") != "0"
 # fp32-output weight-gradient GEMMs through the searched hipBLASLt runner (csrc/runtime/blaslt_gemm.cpp)
 _BLASLT_WGRAD = os.environ.get("ACCELERATE_BLASLT_WGRAD", "1") != "0"
+# dgrad dx = dy . W in its natural NN layout on the searched hipBLASLt runner (opt-in until measured faster than the
+# transposed-weight path below, tools/bench_dgrad.py)
+_DGRAD_BLASLT = os.environ.get("ACCELERATE_DGRAD_BLASLT", "0") == "1"
 
 
 # ----------------------------------------------------------------------------------------------------------
@@ -343,6 +346,12 @@ def linear_dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     tools/bench_transpose.py; 436 MB of weights per Llama-3-8B layer ≈ 0.15 ms) and dx = linear(dy2, Wᵀ) runs in the
     forward's layout: 1.1-1.5 % faster end to end on one MI355X (gpu_steps.sh bench8b vs bench8b_dgradwt, two
     boxes). The copy is transient (freed as soon as the GEMM is enqueued)."""
+    if _DGRAD_BLASLT and dy2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and w.is_contiguous() \
+            and dy2.is_contiguous() and use_native(dy2):
+        # the NN product on a searched hipBLASLt algorithm (csrc/runtime/blaslt_gemm.cpp): no transposed weight copy
+        out = torch.empty((dy2.shape[0], w.shape[1]), dtype=dy2.dtype, device=dy2.device)
+        if ext().blaslt_dgrad_bf16(dy2, w, out):
+            return out
     if (_DGRAD_WT and dy2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and w.is_contiguous()
             and w.shape[0] % 64 == 0 and w.shape[1] % 64 == 0 and use_native(dy2)):
         return torch.nn.functional.linear(dy2, ext().transpose_bf16(w))

@@ -74,6 +74,9 @@ for step in "$@"; do
     attn_long) run attn_long 300 python tools/bench_attn.py --S 32768 --iters 3 ;;
     pmc_attn) run pmc_attn 200 bash tools/pmc_attn.sh ;;
     gemm) run gemm 300 python tools/bench_gemm.py ;;
+    dgrad) run dgrad 300 python tools/bench_dgrad.py ;;
+    bench8b_dgradbl) ACCELERATE_DGRAD_BLASLT=1 run bench8b_dgradbl 600 python bench.py --steps 5 --warmup 2 $BENCH_ARGS ;;
+    probe) run probe 60 bash -c 'df -h . /tmp /dev/shm; free -g; nproc; mount | grep -E " /tmp | /dev/shm | / " || true' ;;
     gemm_v4) run ktest_v4 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "fp8_gemm_v4 or fp8_gemm_v3 or fp8_gemm_exact" && \
              run gemm_v4 400 python tools/bench_gemm.py --variants ${GEMM_VARIANTS:-bl,4,6,7} --no-bf16 --no-scaled-mm --rounds 3 ;;
     gen_gptj) run gen_gptj 600 python tools/bench_generate.py --model gpt-j-6b ;;
