@@ -630,7 +630,7 @@ __device__ __forceinline__ void v3_wait() {
 
 // MX: the per-32-element e8m0 block scales of A [M, K/32] and B [N, K/32] (mx_quant's grouped layout, see below)
 // feed the MFMA's own scale operands instead of unit scales; the per-tensor sa / sb are then unused.
-template <int FA, int FB, bool OUT_F32, int NW, bool MX = false>
+template <int FA, int FB, bool OUT_F32, int NW, bool MX = false, bool UNSCALED = false>
 __device__ __forceinline__ void fp8_gemm_v3_body(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
                                                  const float* __restrict__ sa, const float* __restrict__ sb, float smul,
                                                  const bf16_t* __restrict__ bias, void* __restrict__ C, int M, int N,
@@ -752,9 +752,10 @@ __device__ __forceinline__ void fp8_gemm_v3_body(const uint8_t* __restrict__ A, 
         if constexpr (MX)  // op_sel picks byte Q of the scale dword in the MFMA itself (no VALU byte shifts)
           acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fb[j], fa[i], acc[i][j], FB, FA, Q, (int)scb[j], Q,
                                                                       (int)sca[i]);
-        else
-          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fb[j], fa[i], acc[i][j], FB, FA, 0, 0x7f7f7f7f, 0,
-                                                                      0x7f7f7f7f);
+        else  // unit block scales; UNSCALED: scale operands 0 -> the plain v_mfma_f32_32x32x64_f8f6f4 (no ld_scale)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fb[j], fa[i], acc[i][j], FB, FA, 0,
+                                                                      UNSCALED ? 0 : 0x7f7f7f7f, 0,
+                                                                      UNSCALED ? 0 : 0x7f7f7f7f);
       }
   };
 
@@ -877,12 +878,12 @@ __device__ __forceinline__ void fp8_gemm_v3_body(const uint8_t* __restrict__ A, 
   }
 }
 
-template <int FA, int FB, bool OUT_F32>
+template <int FA, int FB, bool OUT_F32, bool UNSCALED = false>
 __global__ __launch_bounds__(256, 1) void fp8_gemm_v3_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
                                                              const float* __restrict__ sa, const float* __restrict__ sb, float smul,
                                                              const bf16_t* __restrict__ bias, void* __restrict__ C, int M, int N,
                                                              int K, int accum, int group_m) {
-  fp8_gemm_v3_body<FA, FB, OUT_F32, 4>(A, B, sa, sb, smul, bias, C, M, N, K, accum, group_m);
+  fp8_gemm_v3_body<FA, FB, OUT_F32, 4, false, UNSCALED>(A, B, sa, sb, smul, bias, C, M, N, K, accum, group_m);
 }
 
 // MXFP8 GEMM: v3 4-wave body with per-block e8m0 scales (xa: [M, K/32], xb: [N, K/32], grouped layout)
@@ -894,12 +895,12 @@ __global__ __launch_bounds__(256, 1) void mx_gemm_kernel(const uint8_t* __restri
   fp8_gemm_v3_body<FA, FB, OUT_F32, 4, true>(A, B, nullptr, nullptr, smul, bias, C, M, N, K, accum, group_m, xa, xb);
 }
 
-template <int FA, int FB, bool OUT_F32>
+template <int FA, int FB, bool OUT_F32, bool UNSCALED = false>
 __global__ __launch_bounds__(512, 1) void fp8_gemm_v3_w8_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
                                                                 const float* __restrict__ sa, const float* __restrict__ sb,
                                                                 float smul, const bf16_t* __restrict__ bias, void* __restrict__ C,
                                                                 int M, int N, int K, int accum, int group_m) {
-  fp8_gemm_v3_body<FA, FB, OUT_F32, 8>(A, B, sa, sb, smul, bias, C, M, N, K, accum, group_m);
+  fp8_gemm_v3_body<FA, FB, OUT_F32, 8, false, UNSCALED>(A, B, sa, sb, smul, bias, C, M, N, K, accum, group_m);
 }
 
 // ------------------------------------------------------------------------------------------------ GEMM v4
@@ -1254,13 +1255,14 @@ void fp8_cast_into(torch::Tensor x, torch::Tensor t, double qmax, bool from_amax
 }
 
 // Kernel choice of fp8_gemm: 0 = default, 1 = v1 (128x128), 2 = v2 4 waves, 3 = v2 8 waves, 4 = v3 (4-deep ring),
-// 5 = v3 8 waves, 6 = v4 (16x16x128 MFMA, BK 128, two slots), 7 = v4 with the unscaled MFMA opcode.
+// 5 = v3 8 waves, 6 = v4 (16x16x128 MFMA, BK 128, two slots), 7 = v4 with the unscaled MFMA opcode, 8 / 9 = v3 4 / 8
+// waves with the unscaled MFMA opcode.
 // Shapes a variant cannot tile fall back to the next one that can (v3 -> v2 -> v1).
 constexpr int kFp8GemmDefault = 4;
 static int g_fp8_gemm_variant = 0;
 static int g_fp8_gemm_group_m = 4;  // v3 tile-row grouping (1 = plain row-major tile order)
 void fp8_gemm_select(int64_t variant, int64_t group_m) {
-  TORCH_CHECK(variant >= 0 && variant <= 7, "fp8_gemm_select: variant 0..7");
+  TORCH_CHECK(variant >= 0 && variant <= 9, "fp8_gemm_select: variant 0..9");
   TORCH_CHECK(group_m >= 0 && group_m <= 64, "fp8_gemm_select: group_m 0..64");
   g_fp8_gemm_variant = (int)variant;
   if (group_m > 0) g_fp8_gemm_group_m = (int)group_m;
@@ -1328,6 +1330,8 @@ torch::Tensor fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor a_scale_i
     return out;
   }
   if (variant == 6 || variant == 7) variant = 4;  // shapes v4 cannot tile
+  const bool v3_unscaled = variant == 8 || variant == 9;
+  if (v3_unscaled) variant -= 4;
   const bool v3 = variant == 4 || variant == 5;
   if (v3 && !(M % V3_BM == 0 && N % V3_BN == 0 && K % (4 * V3_BK) == 0)) variant = 2;
   if (v3 && (reinterpret_cast<uintptr_t>(bp) & 7) != 0) variant = 2;  // v3 reads the bias 4 at a time
@@ -1338,9 +1342,15 @@ torch::Tensor fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor a_scale_i
     const bool w8_3 = variant == 5;
 #define GEMM3_LAUNCH(FA, FB, OF)                                                                                        \
   do {                                                                                                                  \
-    if (w8_3)                                                                                                           \
+    if (w8_3 && v3_unscaled)                                                                                            \
+      hipLaunchKernelGGL((fp8_gemm_v3_w8_kernel<FA, FB, OF, true>), dim3(nwg3), dim3(512), 0, stream, ap, bptr, sap, sbp, \
+                         (float)smul, bp, cp, M, N, K, accum, g_fp8_gemm_group_m);                                       \
+    else if (w8_3)                                                                                                      \
       hipLaunchKernelGGL((fp8_gemm_v3_w8_kernel<FA, FB, OF>), dim3(nwg3), dim3(512), 0, stream, ap, bptr, sap, sbp, (float)smul, bp, \
                          cp, M, N, K, accum, g_fp8_gemm_group_m);                                                        \
+    else if (v3_unscaled)                                                                                               \
+      hipLaunchKernelGGL((fp8_gemm_v3_kernel<FA, FB, OF, true>), dim3(nwg3), dim3(256), 0, stream, ap, bptr, sap, sbp,    \
+                         (float)smul, bp, cp, M, N, K, accum, g_fp8_gemm_group_m);                                       \
     else                                                                                                                \
       hipLaunchKernelGGL((fp8_gemm_v3_kernel<FA, FB, OF>), dim3(nwg3), dim3(256), 0, stream, ap, bptr, sap, sbp, (float)smul, bp, \
                          cp, M, N, K, accum, g_fp8_gemm_group_m);                                                        \

@@ -277,7 +277,7 @@ def test_fp8_gemm_v2_matches_v1_random():
 
 
 @pytest.mark.parametrize("M,N,K", [(256, 256, 256), (512, 768, 1024), (1024, 512, 4096), (768, 1280, 2304)])
-def test_fp8_gemm_v4_kernel_matches_reference(M, N, K, monkeypatch):
+def test_fp8_gemm_v4_and_unscaled_kernels_match_reference(M, N, K, monkeypatch):
     """The 16x16x128-MFMA kernel (v4: two 64 KiB LDS slots, BK 128) with the scaled (variant 6) and the unscaled
     (variant 7) MFMA opcode, on the hand-written path: exact small integers (bit-exact vs fp32 matmul, pins the operand
     layout and swizzle), then random scaled e4m3 x e5m2 operands with bias / fp32 and bf16 outputs / accumulate
@@ -299,7 +299,7 @@ def test_fp8_gemm_v4_kernel_matches_reference(M, N, K, monkeypatch):
     base = torch.randn(M, N, device=DEV)
     exact_ref = ai.float() @ bi.float().t()
     try:
-        for v in (6, 7):
+        for v in (6, 7, 8, 9):
             ext().fp8_gemm_select(v)
             exact = fp8.gemm(fp8.cast(ai, one), fp8.cast(bi, one), one, one, out_dtype=torch.float32)
             assert torch.equal(exact, exact_ref), (v, (exact - exact_ref).abs().max())

@@ -168,6 +168,9 @@ def main():
             toks.append(out.shape[1] - n)
             checksum = (checksum * 1000003 + int(out[0, n:].long().sum().item())) % (1 << 61)
     per_tok = [t / k for t, k in zip(times, toks)]
+    total_bytes = sum(per_device.values())
+    host_bytes = sum(v for k, v in per_device.items() if k in ("cpu", "disk"))
+    gen_s = sum(times[1:])
     rec = {
         "metric": "big-model load s / generation s per token (reference benchmarks/big_model_inference)",
         "model": args.model,
@@ -180,6 +183,10 @@ def main():
         "generated_checksum": checksum,  # greedy decoding: equal across placements of the same checkpoint
         "params_b": round(sum(v for k, v in sizes.items() if k == "") / (torch.finfo(dtype).bits // 8) / 1e9, 2),
         "placement_gib": {k: round(v / 2**30, 1) for k, v in per_device.items()},
+        # load: checkpoint bytes / load time (page-cache safetensors -> pinned staging -> HBM, or -> host offload store)
+        "load_gbs": round(total_bytes / t_load / 1e9, 1),
+        # generation with offload: the offloaded blocks stream back once per forward (one forward per new token)
+        "offload_stream_gbs": round(host_bytes * sum(toks[1:]) / gen_s / 1e9, 1) if host_bytes and gen_s > 0 else None,
         "n_gpus": n_gpu,
         "checkpoint_write_s": round(t_write, 1),
         "data": "synthetic checkpoint (random-init weights, reference architecture), random prompt ids of the "

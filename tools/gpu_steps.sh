@@ -74,6 +74,7 @@ for step in "$@"; do
     attn_long) run attn_long 300 python tools/bench_attn.py --S 32768 --iters 3 ;;
     pmc_attn) run pmc_attn 200 bash tools/pmc_attn.sh ;;
     gemm) run gemm 300 python tools/bench_gemm.py ;;
+    pmc_gemm) run pmc_gemm 400 bash tools/pmc_gemm.sh --variants ${GEMM_VARIANTS:-bl,4,8,7} --shapes o,down --iters 2 --rounds 1 --no-bf16 --no-scaled-mm ;;
     dgrad) run dgrad 300 python tools/bench_dgrad.py ;;
     bench8b_dgradbl) ACCELERATE_DGRAD_BLASLT=1 run bench8b_dgradbl 600 python bench.py --steps 5 --warmup 2 $BENCH_ARGS ;;
     probe) run probe 60 bash -c 'df -h . /tmp /dev/shm; free -g; nproc; mount | grep -E " /tmp | /dev/shm | / " || true' ;;
@@ -85,6 +86,9 @@ for step in "$@"; do
     gen_opt30b_offload) run gen_opt30b_offload 900 python tools/bench_generate.py --model opt-30b --gpu-mem 46GiB ;;
     gen_neox_disk) run gen_neox_disk 900 python tools/bench_generate.py --model gpt-neox-20b --gpu-mem 14GiB --cpu-mem 10GiB --disk-offload ;;
     gen_llama70b) run gen_llama70b 900 python tools/bench_generate.py --model llama3-70b --dtype bf16 ;;
+    gen70_disk) CK=/dev/shm/acc_ckpt_llama3_70b_bf16; trap 'rm -rf /dev/shm/acc_ckpt_llama3_70b_bf16' EXIT
+                run gen70_resident 900 python tools/bench_generate.py --model llama3-70b --dtype bf16 --ckpt-dir $CK && \
+                run gen70_offload 900 python tools/bench_generate.py --model llama3-70b --dtype bf16 --ckpt-dir $CK --gpu-mem 100GiB ;;
     big70b) run big70b 900 python tools/bench_big_model.py --model llama3-70b --tokens 2048 --iters 3 ;;
     big70b_offload) run big70b_offload 900 python tools/bench_big_model.py --model llama3-70b --gpu-mem 100GiB --tokens 2048 --iters 3 ;;
     *) echo "unknown step $step"; exit 2 ;;
