@@ -903,6 +903,185 @@ __global__ __launch_bounds__(512, 1) void fp8_gemm_v3_w8_kernel(const uint8_t* _
   fp8_gemm_v3_body<FA, FB, OUT_F32, 8, false, UNSCALED>(A, B, sa, sb, smul, bias, C, M, N, K, accum, group_m);
 }
 
+// ------------------------------------------------------------------------------------------------ GEMM v6
+// v3's tiling and 4-slot LDS ring (256x256, 4 waves of 128x128, 32x32x64 MFMA, BK 64) with the LDS-DMA issue spread
+// over the whole K-tile. A buffer_load ... lds piece costs 60-185 issue cycles beside the MFMAs (MI355X constants), and
+// v3 issued all 8 pieces of tile t+4 in the second half of tile t together with the 16 fragment reads of t+1: that half
+// is issue-bound (8 x ~100 + 16 reads against 8 x 64 MFMA cycles) and the matrix pipe idles (PMC: 57 % MFMA busy vs
+// hipBLASLt's 74 % at the same clock). Here tile t issues the pieces of tile t+3 into the slot tile t-1 left (free since
+// the barrier of t-1): 4 with the first half's MFMAs, 4 with the second's. Two tiles stay in flight across each barrier.
+template <int FA, int FB, bool OUT_F32, bool UNSCALED>
+__global__ __launch_bounds__(256, 1) void fp8_gemm_v6_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
+                                                             const float* __restrict__ sa, const float* __restrict__ sb,
+                                                             float smul, const bf16_t* __restrict__ bias, void* __restrict__ C,
+                                                             int M, int N, int K, int accum, int group_m) {
+  __shared__ __attribute__((aligned(1024))) uint8_t ring0[V3_TILE];
+  __shared__ __attribute__((aligned(1024))) uint8_t ring1[V3_TILE];
+  __shared__ __attribute__((aligned(1024))) uint8_t ring2[V3_TILE];
+  __shared__ __attribute__((aligned(1024))) uint8_t ring3[V3_TILE];
+  constexpr int TI = 4, TJ = 4, DPW = 4;
+  const int tiles_n = N / V3_BN, tiles_m = M / V3_BM;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  int tile_m, tile_n;
+  if (group_m > 1) {
+    const int per_group = group_m * tiles_n;
+    const int g = bid / per_group, first = g * group_m, rows = min(tiles_m - first, group_m), in = bid % per_group;
+    tile_m = first + in % rows;
+    tile_n = in / rows;
+  } else {
+    tile_m = bid / tiles_n;
+    tile_n = bid % tiles_n;
+  }
+  const int tm = tile_m * V3_BM, tn = tile_n * V3_BN;
+  ACC_CHECK_OR_RETURN(tm + V3_BM <= M && tn + V3_BN <= N && K % 256 == 0 && bid < nwg, kChkGemmTile);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hf = lane >> 5;
+  const int wm = (wave >> 1) * 128, wn = (wave & 1) * 128;
+  constexpr int SC = UNSCALED ? 0 : 0x7f7f7f7f;
+
+  f32x16 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  unsigned voff[DPW];
+#pragma unroll
+  for (int t = 0; t < DPW; ++t) {
+    const int row = (wv * DPW + t) * 16 + (lane >> 2);
+    voff[t] = (unsigned)(row * K + v3_swz(row, lane & 3) * 16);
+  }
+  const auto a_rs = __builtin_amdgcn_make_buffer_rsrc((void*)(A + (long)tm * K), (short)0, V3_BM * K, 0x00020000);
+  const auto b_rs = __builtin_amdgcn_make_buffer_rsrc((void*)(B + (long)tn * K), (short)0, V3_BN * K, 0x00020000);
+  const int nk = K / V3_BK;
+  // half h of tile kt's pieces: A and B blocks 2h, 2h + 1 of this wave (zero-fill past the end, one count per wait)
+  auto stage_half = [&](int kt, uint8_t* base, int h) {
+    const int so = kt < nk ? kt * V3_BK : 0x40000000;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int t = 2 * h + u, blk = wv * DPW + t;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rs, base + blk * 1024, 16, voff[t], so, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rs, base + V3_BOFF + blk * 1024, 16, voff[t], so, 0, 0);
+    }
+  };
+  const int sw = (r >> 2) & 3;
+  const int lo0 = (hf ^ sw) * 16, lo1 = ((2 + hf) ^ sw) * 16;
+  const int arow = (wm + r) * V3_BK, brow = V3_BOFF + (wn + r) * V3_BK;
+  auto frag = [&](const uint8_t* p) -> v8i {
+    const uint4 lo = *reinterpret_cast<const uint4*>(p + lo0);
+    const uint4 hi = *reinterpret_cast<const uint4*>(p + lo1);
+    v8i v;
+    v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w; v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+    return v;
+  };
+  auto load = [&](const uint8_t* img, v8i (&fa)[TI], v8i (&fb)[TJ]) {
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) fb[j] = frag(img + brow + j * 32 * V3_BK);
+#pragma unroll
+    for (int i = 0; i < TI; ++i) fa[i] = frag(img + arow + i * 32 * V3_BK);
+  };
+  auto mfma_rows = [&](const v8i (&fa)[TI], const v8i (&fb)[TJ], int i0) {
+#pragma unroll
+    for (int i = i0; i < i0 + 2; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fb[j], fa[i], acc[i][j], FB, FA, 0, SC, 0, SC);
+  };
+
+  // prologue: tiles 0..2 in flight, tile 0 landed, its fragments in registers
+  stage_half(0, ring0, 0); stage_half(0, ring0, 1);
+  stage_half(1, ring1, 0); stage_half(1, ring1, 1);
+  stage_half(2, ring2, 0); stage_half(2, ring2, 1);
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  v8i xa[TI], xb[TJ], ya[TI], yb[TJ];
+  load(ring0, xa, xb);
+
+  // tile t: `cur` fragments -> MFMAs; pieces of t+3 into `fill` (tile t-1's slot); fragments of t+1 from `nslot`
+  auto step = [&](int t, const uint8_t* nslot, uint8_t* fill, v8i (&ca)[TI], v8i (&cb)[TJ], v8i (&na)[TI], v8i (&nb)[TJ]) {
+    stage_half(t + 3, fill, 0);
+    mfma_rows(ca, cb, 0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // one piece per two MFMAs
+      __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x8, 2, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory");  // t+1 landed; t+2 and half of t+3 in flight
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    stage_half(t + 3, fill, 1);
+    load(nslot, na, nb);
+    mfma_rows(ca, cb, 2);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // per two MFMAs: one piece and four fragment reads
+      __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+      __builtin_amdgcn_sched_group_barrier(0x8, 2, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  for (int t = 0; t < nk; t += 4) {  // nk % 4 == 0 (host check)
+    step(t, ring1, ring3, xa, xb, ya, yb);
+    step(t + 1, ring2, ring0, ya, yb, xa, xb);
+    step(t + 2, ring3, ring1, xa, xb, ya, yb);
+    step(t + 3, ring0, ring2, ya, yb, xa, xb);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  const float s = sa[0] * sb[0] * smul;
+  auto epilogue = [&](auto has_bias, auto acc_in) {
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int m = tm + wm + i * 32 + r;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int n = tn + wn + j * 32 + 8 * g + 4 * hf;
+          float v[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) v[u] = acc[i][j][4 * g + u] * s;
+          if constexpr (decltype(has_bias)::value) {
+            const bf16x4 b4 = *reinterpret_cast<const bf16x4*>(bias + n);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] += bf2f(b4.v[u]);
+          }
+          if constexpr (OUT_F32) {
+            float4* cp4 = reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + (long)m * N + n);
+            if constexpr (decltype(acc_in)::value) {
+              const float4 o = *cp4;
+              v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+            }
+            *cp4 = make_float4(v[0], v[1], v[2], v[3]);
+          } else {
+            bf16x4* cp4 = reinterpret_cast<bf16x4*>(reinterpret_cast<bf16_t*>(C) + (long)m * N + n);
+            if constexpr (decltype(acc_in)::value) {
+              const bf16x4 o = *cp4;
+#pragma unroll
+              for (int u = 0; u < 4; ++u) v[u] += bf2f(o.v[u]);
+            }
+            bf16x4 w;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) w.v[u] = f2bf(v[u]);
+            *cp4 = w;
+          }
+        }
+      }
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  if (bias != nullptr) {
+    if (accum) epilogue(T_{}, T_{}); else epilogue(T_{}, F_{});
+  } else {
+    if (accum) epilogue(F_{}, T_{}); else epilogue(F_{}, F_{});
+  }
+}
+
 // ------------------------------------------------------------------------------------------------ GEMM v4
 // 256x256 output tile, 4 waves (2 x 2, one per SIMD, 128x128 per wave), v_mfma 16x16x128 f8f6f4: 8 x 8 accumulator
 // blocks of 4 registers (256 AGPR/VGPR). The 16x16 shape holds a higher clock under load than 32x32 at equal
@@ -1048,6 +1227,156 @@ __global__ __launch_bounds__(256, 1) void fp8_gemm_v4_kernel(const uint8_t* __re
     step(t + 1, slot1, slot0, by, bx, a0y, a0x);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the zero-fill DMAs past the end retire before the exit
+
+  const float s = sa[0] * sb[0] * smul;
+  auto epilogue = [&](auto has_bias, auto acc_in) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int m = tm + wm + i * 16 + r16;
+        const int n = tn + wn + j * 16 + 4 * q;
+        float v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = acc[i][j][u] * s;
+        if constexpr (decltype(has_bias)::value) {
+          const bf16x4 b4 = *reinterpret_cast<const bf16x4*>(bias + n);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) v[u] += bf2f(b4.v[u]);
+        }
+        if constexpr (OUT_F32) {
+          float4* cp4 = reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + (long)m * N + n);
+          if constexpr (decltype(acc_in)::value) {
+            const float4 o = *cp4;
+            v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+          }
+          *cp4 = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+          bf16x4* cp4 = reinterpret_cast<bf16x4*>(reinterpret_cast<bf16_t*>(C) + (long)m * N + n);
+          if constexpr (decltype(acc_in)::value) {
+            const bf16x4 o = *cp4;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] += bf2f(o.v[u]);
+          }
+          bf16x4 w;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) w.v[u] = f2bf(v[u]);
+          *cp4 = w;
+        }
+      }
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  if (bias != nullptr) {
+    if (accum) epilogue(T_{}, T_{}); else epilogue(T_{}, F_{});
+  } else {
+    if (accum) epilogue(F_{}, T_{}); else epilogue(F_{}, F_{});
+  }
+}
+
+// ------------------------------------------------------------------------------------------------ GEMM v5
+// v4's tiling (256x256, 4 waves of 128x128, 16x16x128 MFMA, BK 128, two 64 KiB slots) with ONE barrier per K-step and
+// no register double buffer of the B fragments (v4's two B sets + prefetched A pushed hipcc into ~600 AGPR<->VGPR
+// moves per loop trip). Per K-step t (slot s = t % 2):
+//   DMA of t+1 into slot s^1 (free: every wave passed the barrier that ended t-1), interleaved with the first rows'
+//     MFMAs;
+//   B fragments of t (8 x 2 ds_read_b128) read at the step's start, A fragments streamed one row ahead;
+//   vmcnt(0) + barrier at the end: t+1 landed for every wave, every wave is done reading slot s.
+template <int FA, int FB, bool OUT_F32, bool UNSCALED>
+__global__ __launch_bounds__(256, 1) void fp8_gemm_v5_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
+                                                             const float* __restrict__ sa, const float* __restrict__ sb,
+                                                             float smul, const bf16_t* __restrict__ bias, void* __restrict__ C,
+                                                             int M, int N, int K, int accum, int group_m) {
+  __shared__ __attribute__((aligned(1024))) uint8_t slot0[V4_SLOT];
+  __shared__ __attribute__((aligned(1024))) uint8_t slot1[V4_SLOT];
+  const int tiles_n = N / V4_BN, tiles_m = M / V4_BM;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  int tile_m, tile_n;
+  if (group_m > 1) {
+    const int per_group = group_m * tiles_n;
+    const int g = bid / per_group, first = g * group_m, rows = min(tiles_m - first, group_m), in = bid % per_group;
+    tile_m = first + in % rows;
+    tile_n = in / rows;
+  } else {
+    tile_m = bid / tiles_n;
+    tile_n = bid % tiles_n;
+  }
+  const int tm = tile_m * V4_BM, tn = tile_n * V4_BN;
+  ACC_CHECK_OR_RETURN(tm + V4_BM <= M && tn + V4_BN <= N && K % 256 == 0 && bid < nwg, kChkGemmTile);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r16 = lane & 15, q = lane >> 4;
+  const int wm = (wave >> 1) * 128, wn = (wave & 1) * 128;
+  constexpr int SC = UNSCALED ? 0 : 0x7f7f7f7f;
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  unsigned voff[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int row = (wv * 8 + t) * 8 + (lane >> 3);
+    voff[t] = (unsigned)(row * K + v4_swz(row, lane & 7) * 16);
+  }
+  const auto a_rs = __builtin_amdgcn_make_buffer_rsrc((void*)(A + (long)tm * K), (short)0, V4_BM * K, 0x00020000);
+  const auto b_rs = __builtin_amdgcn_make_buffer_rsrc((void*)(B + (long)tn * K), (short)0, V4_BN * K, 0x00020000);
+  const int nk = K / V4_BK;
+  auto stage = [&](int kt, uint8_t* base) {
+    const int so = kt < nk ? kt * V4_BK : 0x40000000;  // past the end: zero-fill, one count for every wait
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rs, base + (wv * 8 + t) * 1024, 16, voff[t], so, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rs, base + V4_BOFF + (wv * 8 + t) * 1024, 16, voff[t], so, 0, 0);
+    }
+  };
+  const int f = (r16 >> 1) & 7;
+  const int lo = (q ^ f) * 16, hi = ((q + 4) ^ f) * 16;
+  const int arow = (wm + r16) * V4_BK, brow = V4_BOFF + (wn + r16) * V4_BK;
+  auto frag = [&](const uint8_t* p) -> v8i {
+    const uint4 a = *reinterpret_cast<const uint4*>(p + lo);
+    const uint4 b = *reinterpret_cast<const uint4*>(p + hi);
+    v8i v;
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    return v;
+  };
+
+  stage(0, slot0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+
+  auto step = [&](int t, const uint8_t* cur, uint8_t* nxt) {
+    stage(t + 1, nxt);
+    v8i bf[8], ar[2];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bf[j] = frag(cur + brow + j * 16 * V4_BK);
+    ar[0] = frag(cur + arow);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (i < 7) ar[(i + 1) & 1] = frag(cur + arow + (i + 1) * 16 * V4_BK);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)  // swapped operands: acc holds C^T blocks (lane <-> m, registers <-> 4 n)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bf[j], ar[i & 1], acc[i][j], FB, FA, 0, SC, 0, SC);
+    }
+    // issue order: the B / first A fragment reads first, then one DMA of t+1 per MFMA of rows 0-1
+    __builtin_amdgcn_sched_group_barrier(0x100, 18, 0);  // DS read
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);  // VMEM read (buffer_load ... lds)
+      __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);   // MFMA
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // t+1 landed (this wave), slot reads retired
+    __builtin_amdgcn_s_barrier();                               // ... every wave's
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  for (int t = 0; t < nk; t += 2) {  // nk even (host check: K % 256 == 0)
+    step(t, slot0, slot1);
+    step(t + 1, slot1, slot0);
+  }
 
   const float s = sa[0] * sb[0] * smul;
   auto epilogue = [&](auto has_bias, auto acc_in) {
@@ -1256,13 +1585,14 @@ void fp8_cast_into(torch::Tensor x, torch::Tensor t, double qmax, bool from_amax
 
 // Kernel choice of fp8_gemm: 0 = default, 1 = v1 (128x128), 2 = v2 4 waves, 3 = v2 8 waves, 4 = v3 (4-deep ring),
 // 5 = v3 8 waves, 6 = v4 (16x16x128 MFMA, BK 128, two slots), 7 = v4 with the unscaled MFMA opcode, 8 / 9 = v3 4 / 8
-// waves with the unscaled MFMA opcode.
+// waves with the unscaled MFMA opcode, 10 / 11 = v5 (v4 tiling, one barrier per K-step) scaled / unscaled, 12 / 13 =
+// v6 (v3 with the LDS-DMA issue spread over the whole K-tile) scaled / unscaled.
 // Shapes a variant cannot tile fall back to the next one that can (v3 -> v2 -> v1).
 constexpr int kFp8GemmDefault = 4;
 static int g_fp8_gemm_variant = 0;
 static int g_fp8_gemm_group_m = 4;  // v3 tile-row grouping (1 = plain row-major tile order)
 void fp8_gemm_select(int64_t variant, int64_t group_m) {
-  TORCH_CHECK(variant >= 0 && variant <= 9, "fp8_gemm_select: variant 0..9");
+  TORCH_CHECK(variant >= 0 && variant <= 13, "fp8_gemm_select: variant 0..13");
   TORCH_CHECK(group_m >= 0 && group_m <= 64, "fp8_gemm_select: group_m 0..64");
   g_fp8_gemm_variant = (int)variant;
   if (group_m > 0) g_fp8_gemm_group_m = (int)group_m;
@@ -1309,6 +1639,48 @@ torch::Tensor fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor a_scale_i
   }();
   int variant = g_fp8_gemm_variant;
   if (variant == 0) variant = force_v1 ? 1 : (env_w8 ? 3 : kFp8GemmDefault);
+  if ((variant == 10 || variant == 11) && M % V4_BM == 0 && N % V4_BN == 0 && K % 256 == 0 &&
+      (long)V4_BM * K < (1L << 30) && (reinterpret_cast<uintptr_t>(bp) & 7) == 0) {
+    const int nwg5 = (M / V4_BM) * (N / V4_BN);
+    const bool un = variant == 11;
+#define GEMM5_LAUNCH(FA, FB, OF)                                                                                        \
+  do {                                                                                                                  \
+    if (un)                                                                                                             \
+      hipLaunchKernelGGL((fp8_gemm_v5_kernel<FA, FB, OF, true>), dim3(nwg5), dim3(256), 0, stream, ap, bptr, sap, sbp,   \
+                         (float)smul, bp, cp, M, N, K, accum, g_fp8_gemm_group_m);                                       \
+    else                                                                                                                \
+      hipLaunchKernelGGL((fp8_gemm_v5_kernel<FA, FB, OF, false>), dim3(nwg5), dim3(256), 0, stream, ap, bptr, sap, sbp,  \
+                         (float)smul, bp, cp, M, N, K, accum, g_fp8_gemm_group_m);                                       \
+  } while (0)
+    if (!a_e5m2 && !b_e5m2) { if (out_fp32) GEMM5_LAUNCH(0, 0, true); else GEMM5_LAUNCH(0, 0, false); }
+    else if (!a_e5m2 && b_e5m2) { if (out_fp32) GEMM5_LAUNCH(0, 1, true); else GEMM5_LAUNCH(0, 1, false); }
+    else if (a_e5m2 && !b_e5m2) { if (out_fp32) GEMM5_LAUNCH(1, 0, true); else GEMM5_LAUNCH(1, 0, false); }
+    else { if (out_fp32) GEMM5_LAUNCH(1, 1, true); else GEMM5_LAUNCH(1, 1, false); }
+#undef GEMM5_LAUNCH
+    return out;
+  }
+  if (variant == 10 || variant == 11) variant = 4;
+  if ((variant == 12 || variant == 13) && M % V3_BM == 0 && N % V3_BN == 0 && K % 256 == 0 &&
+      (long)V3_BM * K < (1L << 30) && (reinterpret_cast<uintptr_t>(bp) & 7) == 0) {
+    const int nwg6 = (M / V3_BM) * (N / V3_BN);
+    const bool un = variant == 13;
+#define GEMM6_LAUNCH(FA, FB, OF)                                                                                        \
+  do {                                                                                                                  \
+    if (un)                                                                                                             \
+      hipLaunchKernelGGL((fp8_gemm_v6_kernel<FA, FB, OF, true>), dim3(nwg6), dim3(256), 0, stream, ap, bptr, sap, sbp,   \
+                         (float)smul, bp, cp, M, N, K, accum, g_fp8_gemm_group_m);                                       \
+    else                                                                                                                \
+      hipLaunchKernelGGL((fp8_gemm_v6_kernel<FA, FB, OF, false>), dim3(nwg6), dim3(256), 0, stream, ap, bptr, sap, sbp,  \
+                         (float)smul, bp, cp, M, N, K, accum, g_fp8_gemm_group_m);                                       \
+  } while (0)
+    if (!a_e5m2 && !b_e5m2) { if (out_fp32) GEMM6_LAUNCH(0, 0, true); else GEMM6_LAUNCH(0, 0, false); }
+    else if (!a_e5m2 && b_e5m2) { if (out_fp32) GEMM6_LAUNCH(0, 1, true); else GEMM6_LAUNCH(0, 1, false); }
+    else if (a_e5m2 && !b_e5m2) { if (out_fp32) GEMM6_LAUNCH(1, 0, true); else GEMM6_LAUNCH(1, 0, false); }
+    else { if (out_fp32) GEMM6_LAUNCH(1, 1, true); else GEMM6_LAUNCH(1, 1, false); }
+#undef GEMM6_LAUNCH
+    return out;
+  }
+  if (variant == 12 || variant == 13) variant = 4;
   if ((variant == 6 || variant == 7) && M % V4_BM == 0 && N % V4_BN == 0 && K % 256 == 0 && (long)V4_BM * K < (1L << 30) &&
       (reinterpret_cast<uintptr_t>(bp) & 7) == 0) {
     const int nwg4 = (M / V4_BM) * (N / V4_BN);

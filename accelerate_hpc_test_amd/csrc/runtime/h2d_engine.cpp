@@ -1,5 +1,10 @@
 // Host runtime: asynchronous host->device copy engine with a pinned staging ring.
 //
+// Sources: a host tensor (pageable pieces are memcpy'd into the ring, pinned ones DMA'd directly), or a byte range
+// of a FILE (`copy_file`: the checkpoint loader's path for safetensors shards — the workers pread() straight into the
+// pinned slots, several in parallel, so the bytes are copied once on the host instead of mmap -> pageable tensor ->
+// pinned, and no page-table entries are created for a 140 GB checkpoint).
+//
 // Used by big-model inference (offloaded weights are uploaded block by block ahead of use), checkpoint loading
 // (safetensors mmap -> HBM) and FSDP CPU offload. A pageable source (e.g. an mmap'd checkpoint) cannot be
 // DMA'd directly; the engine splits it into slot-sized pieces, worker threads memcpy each piece into one of
@@ -12,8 +17,13 @@
 #include <ATen/hip/HIPContext.h>
 #include <hip/hip_runtime.h>
 
+#include <fcntl.h>
+#include <unistd.h>
+
 #include <atomic>
 #include <condition_variable>
+#include <map>
+#include <string>
 #include <cstring>
 #include <deque>
 #include <functional>
@@ -54,6 +64,7 @@ class H2DEngine {
     }
     cv_.notify_all();
     for (auto& w : workers_) w.join();
+    for (auto& kv : fds_) ::close(kv.second);
     hipSetDevice(device_);
     hipStreamSynchronize(stream_);
     for (auto& f : inflight_) hipEventDestroy(f.ev);
@@ -91,12 +102,46 @@ class H2DEngine {
       std::lock_guard<std::mutex> g(mu_);
       for (int64_t off = 0; off < n; off += slot_bytes_) {
         const int64_t len = std::min<int64_t>(slot_bytes_, n - off);
-        tasks_.push_back({s + off, d + off, len});
+        tasks_.push_back({s + off, d + off, len, -1, 0});
         ++pending_;
       }
       staged_.push_back(src);  // pageable: read by the workers' memcpy into the pinned ring, released at drain
     }
     cv_.notify_all();
+  }
+
+  // Enqueue a copy of bytes [offset, offset + dst.nbytes()) of the file at `path` into a contiguous device tensor.
+  void copy_file(const std::string& path, int64_t offset, torch::Tensor dst) {
+    TORCH_CHECK(dst.is_cuda() && dst.is_contiguous(), "H2DEngine.copy_file: dst must be a contiguous HIP tensor");
+    TORCH_CHECK(offset >= 0, "H2DEngine.copy_file: negative offset");
+    char* d = static_cast<char*>(dst.data_ptr());
+    const int64_t n = dst.nbytes();
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      int fd;
+      auto it = fds_.find(path);
+      if (it == fds_.end()) {
+        fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
+        TORCH_CHECK(fd >= 0, "H2DEngine.copy_file: cannot open ", path);
+        fds_[path] = fd;
+      } else {
+        fd = it->second;
+      }
+      for (int64_t off = 0; off < n; off += slot_bytes_) {
+        const int64_t len = std::min<int64_t>(slot_bytes_, n - off);
+        tasks_.push_back({nullptr, d + off, len, fd, offset + off});
+        ++pending_;
+      }
+    }
+    cv_.notify_all();
+  }
+
+  // Close the files opened by copy_file (after every piece has been read).
+  void close_files() {
+    drain_issue();
+    std::lock_guard<std::mutex> g(mu_);
+    for (auto& kv : fds_) ::close(kv.second);
+    fds_.clear();
   }
 
   // Block the host until every enqueued piece has been staged and its DMA issued, then make the caller's
@@ -136,9 +181,11 @@ class H2DEngine {
     bool busy;
   };
   struct Task {
-    const char* src;
+    const char* src;  // host source, or nullptr for a file range
     char* dst;
     int64_t len;
+    int fd = -1;
+    int64_t file_off = 0;
   };
 
   // caller holds mu_
@@ -189,7 +236,21 @@ class H2DEngine {
       }
       // a recycled slot's previous DMA must be complete before overwriting it
       HIP_OK(hipEventSynchronize(slots_[slot].ev));
-      std::memcpy(slots_[slot].ptr, t.src, t.len);
+      if (t.fd >= 0) {
+        char* p = static_cast<char*>(slots_[slot].ptr);
+        int64_t done = 0;
+        while (done < t.len) {
+          const ssize_t got = ::pread(t.fd, p + done, (size_t)(t.len - done), (off_t)(t.file_off + done));
+          if (got <= 0) {  // short file / IO error: leave the bytes zero rather than hang; the loader validated sizes
+            std::memset(p + done, 0, (size_t)(t.len - done));
+            read_errors_.fetch_add(1);
+            break;
+          }
+          done += got;
+        }
+      } else {
+        std::memcpy(slots_[slot].ptr, t.src, t.len);
+      }
       {
         std::lock_guard<std::mutex> g(mu_);
         HIP_OK(hipMemcpyAsync(t.dst, slots_[slot].ptr, t.len, hipMemcpyHostToDevice, stream_));
@@ -218,6 +279,11 @@ class H2DEngine {
   std::condition_variable cv_, idle_cv_;
   int64_t pending_ = 0;
   bool stop_ = false;
+  std::map<std::string, int> fds_;
+  std::atomic<int64_t> read_errors_{0};
+
+ public:
+  int64_t read_errors() const { return read_errors_.load(); }
 };
 
 
@@ -230,6 +296,10 @@ void register_runtime(pybind11::module& m) {
       .def(pybind11::init<int, int64_t, int64_t, int64_t>(), pybind11::arg("device"), pybind11::arg("num_slots") = 4,
            pybind11::arg("slot_bytes") = 64 << 20, pybind11::arg("num_threads") = 4)
       .def("copy", &H2DEngine::copy, pybind11::call_guard<pybind11::gil_scoped_release>())
+      .def("copy_file", &H2DEngine::copy_file, pybind11::arg("path"), pybind11::arg("offset"), pybind11::arg("dst"),
+           pybind11::call_guard<pybind11::gil_scoped_release>())
+      .def("close_files", &H2DEngine::close_files, pybind11::call_guard<pybind11::gil_scoped_release>())
+      .def("read_errors", &H2DEngine::read_errors)
       .def("wait_on_current_stream", &H2DEngine::wait_on_current_stream, pybind11::call_guard<pybind11::gil_scoped_release>())
       .def("synchronize", &H2DEngine::synchronize, pybind11::call_guard<pybind11::gil_scoped_release>())
       .def("inflight", &H2DEngine::inflight)

@@ -68,6 +68,11 @@ def checkpoint_files(checkpoint: Union[str, os.PathLike]) -> list:
     )
 
 
+_ST_DTYPES = {"F64": torch.float64, "F32": torch.float32, "F16": torch.float16, "BF16": torch.bfloat16,
+              "I64": torch.int64, "I32": torch.int32, "I16": torch.int16, "I8": torch.int8, "U8": torch.uint8,
+              "BOOL": torch.bool, "F8_E4M3": torch.float8_e4m3fn, "F8_E5M2": torch.float8_e5m2}
+
+
 class SafetensorsShard(Mapping):
     """Lazy name -> CPU tensor view of one safetensors file (one `get_tensor` per access)."""
 
@@ -85,6 +90,26 @@ class SafetensorsShard(Mapping):
         if key not in self._keys:
             raise KeyError(key)
         return self._f.get_tensor(key)
+
+    def layout(self) -> dict:
+        """name -> (torch dtype, shape, absolute byte offset, byte length) of every tensor, from the file's own header
+        (8-byte little-endian header length, JSON header, data section): what lets the native engine pread a tensor's
+        bytes straight into its pinned ring (`H2DEngine.copy_file`) without materialising a host tensor."""
+        if getattr(self, "_layout", None) is None:
+            with open(self.path, "rb") as fh:
+                n = int.from_bytes(fh.read(8), "little")
+                header = json.loads(fh.read(n))
+            base = 8 + n
+            out = {}
+            for name, info in header.items():
+                if name == "__metadata__":
+                    continue
+                dt = _ST_DTYPES.get(info["dtype"])
+                lo, hi = info["data_offsets"]
+                if dt is not None:
+                    out[name] = (dt, tuple(info["shape"]), base + lo, hi - lo)
+            self._layout = out
+        return self._layout
 
     def __iter__(self):
         return iter(self._keys)
@@ -121,7 +146,8 @@ def h2d_engine(device_index: int):
     if not _ext.available():
         return None
     if device_index not in _ENGINES:
-        _ENGINES[device_index] = _ext.ext().H2DEngine(device_index, 4, 64 << 20, 4)
+        # 8 x 64 MB pinned slots, 8 worker threads: parallel pread / memcpy into the ring keeps PCIe Gen5 busy
+        _ENGINES[device_index] = _ext.ext().H2DEngine(device_index, 8, 64 << 20, 8)
     return _ENGINES[device_index]
 
 
@@ -142,6 +168,9 @@ class _Installer:
         self.keys = set(model.state_dict().keys())
         self.unexpected = set()
         self.engines = set()
+        # file-range uploads (safetensors -> pinned ring by pread -> HBM); ACCELERATE_LOAD_DIRECT=0 reads through
+        # safetensors' own get_tensor instead
+        self.direct = os.environ.get("ACCELERATE_LOAD_DIRECT", "1") != "0"
 
     def target_dtype(self, name, t):
         if self.dtype is None or not torch.is_floating_point(t):
@@ -151,6 +180,32 @@ class _Installer:
         ):
             return torch.float32
         return self.dtype
+
+    def put_from_file(self, name, path: str, dtype, shape, offset: int, nbytes: int) -> bool:
+        """A GPU-bound tensor stored in the checkpoint with the dtype it keeps: the engine preads its bytes from the
+        shard straight into the pinned ring and DMAs them (no host tensor). False when this path does not apply."""
+        if name not in self.keys or not self.direct:
+            return False
+        dest = _device_of(name, self.device_map)
+        if isinstance(dest, int):
+            dev = torch.device("cuda", dest)
+        elif isinstance(dest, (str, torch.device)) and str(dest).startswith("cuda"):
+            dev = torch.device(dest)
+        else:
+            return False  # host / disk placements keep the tensor path
+        old = recursive_getattr(self.model, name)
+        want = self.target_dtype(name, torch.empty(0, dtype=dtype)) or (old.dtype if dtype.is_floating_point else dtype)
+        if want != dtype or tuple(old.shape) != tuple(shape) or nbytes != torch.Size(shape).numel() * dtype.itemsize:
+            return False
+        eng = h2d_engine(dev.index if dev.index is not None else torch.cuda.current_device())
+        if eng is None or not hasattr(eng, "copy_file"):
+            return False
+        dst = torch.empty(shape, dtype=dtype, device=dev)
+        if nbytes:
+            eng.copy_file(path, offset, dst)
+        self.engines.add(eng)
+        set_module_tensor_to_device(self.model, name, dev, value=dst, clear_cache=False)
+        return True
 
     def put(self, name, t):
         if name not in self.keys:
@@ -185,6 +240,10 @@ class _Installer:
     def finish(self):
         for eng in self.engines:
             eng.wait_on_current_stream()
+            if hasattr(eng, "close_files"):
+                eng.close_files()
+                if eng.read_errors():
+                    raise OSError(f"checkpoint loading: {eng.read_errors()} short read(s) from the shard files")
         if self.disk is not None:
             self.disk.flush_index()
         if self.host_spill is not None:
@@ -282,7 +341,11 @@ def load_checkpoint_in_model(
         inst = _Installer(model, device_map, dtype, keep_in_fp32_modules, offload_folder, offload_state_dict, offload_buffers, strict)
         for path in files:
             shard = load_state_dict(path, device_map=device_map)
+            layout = shard.layout() if isinstance(shard, SafetensorsShard) else {}
             for name in list(shard.keys()):
+                lay = layout.get(name)
+                if lay is not None and inst.put_from_file(name, path, *lay):
+                    continue
                 inst.put(name, shard[name])  # one tensor resident at a time for safetensors shards
             del shard
             gc.collect()

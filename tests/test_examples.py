@@ -96,6 +96,9 @@ def test_config_templates_load_and_launch(tmp_path):
 
 @pytest.mark.parametrize("script,expect", [
     ("examples/inference/pippy/llama.py", "max |staged - unsplit| = 0.00e+00"),
+    ("examples/inference/pippy/bert.py", "BertForMaskedLM: stages=2"),
+    ("examples/inference/pippy/gpt2.py", "GPT2ForSequenceClassification: stages=2"),
+    ("examples/inference/pippy/t5.py", "T5ForConditionalGeneration: stages=2"),
     ("examples/inference/distributed/llama_generation.py", "generated 10 completions on 2 process(es)"),
     ("examples/alst_ulysses_sequence_parallelism/sp_ulysses.py", "local tokens 32 of 64"),
 ])

@@ -299,7 +299,7 @@ def test_fp8_gemm_v4_and_unscaled_kernels_match_reference(M, N, K, monkeypatch):
     base = torch.randn(M, N, device=DEV)
     exact_ref = ai.float() @ bi.float().t()
     try:
-        for v in (6, 7, 8, 9):
+        for v in (6, 7, 8, 9, 10, 11, 12, 13):
             ext().fp8_gemm_select(v)
             exact = fp8.gemm(fp8.cast(ai, one), fp8.cast(bi, one), one, one, out_dtype=torch.float32)
             assert torch.equal(exact, exact_ref), (v, (exact - exact_ref).abs().max())
@@ -1347,3 +1347,52 @@ def test_blaslt_mx_gemm_matches_dequantised_product():
     assert ext().blaslt_mx_gemm(qa, qb, fp8.mx_scales_natural(sa).contiguous(), fp8.mx_scales_natural(sb).contiguous(),
                                 out, False)
     assert _rel(out, ref) < 1e-2, _rel(out, ref)
+
+
+def test_checkpoint_direct_file_upload(tmp_path, monkeypatch):
+    """load_checkpoint_in_model onto the GPU reads safetensors byte ranges straight into the H2D engine's pinned ring
+    (H2DEngine.copy_file: pread by the workers, no host tensor): every tensor equals the file's; a dtype conversion and
+    host placements keep the tensor path, and ACCELERATE_LOAD_DIRECT=0 gives the same result through it."""
+    from safetensors.torch import save_file
+
+    from accelerate_hpc_test_amd.utils import checkpoint_io
+
+    torch.manual_seed(0)
+
+    def make():
+        holder = torch.nn.Module()
+        holder.register_buffer("big", torch.zeros(3001, 1111))  # odd byte length, odd offset, > one 1 MB test slot
+        return torch.nn.Sequential(torch.nn.Linear(256, 512), torch.nn.LayerNorm(512), torch.nn.Linear(512, 77, bias=False),
+                                   holder)
+
+    sd = {k: torch.randn(v.shape).to(torch.bfloat16) for k, v in make().state_dict().items()}
+    path = str(tmp_path / "model.safetensors")
+    save_file(sd, path, metadata={"format": "pt"})
+    counts = {"put": 0, "file": 0}
+    real_put, real_file = checkpoint_io._Installer.put, checkpoint_io._Installer.put_from_file
+
+    def put(self, name, t):
+        counts["put"] += 1
+        return real_put(self, name, t)
+
+    def put_file(self, *a):
+        ok = real_file(self, *a)
+        counts["file"] += int(ok)
+        return ok
+
+    monkeypatch.setattr(checkpoint_io._Installer, "put", put)
+    monkeypatch.setattr(checkpoint_io._Installer, "put_from_file", put_file)
+    for direct, dtype, want in (("1", None, (5, 1)), ("0", None, (0, 6)), ("1", torch.float16, (0, 6))):
+        monkeypatch.setenv("ACCELERATE_LOAD_DIRECT", direct)
+        counts.update(put=0, file=0)
+        with torch.device("meta"):
+            m = make().to(torch.bfloat16)
+        checkpoint_io.load_checkpoint_in_model(m, path, device_map={"0": 0, "1": 0, "2": "cpu", "3": 0}, dtype=dtype)
+        torch.cuda.synchronize()
+        got_sd = m.state_dict()
+        for k, v in sd.items():
+            got = got_sd[k]
+            assert got.device.type == ("cpu" if k.startswith("2.") else "cuda"), k
+            ref = v.to(dtype) if dtype is not None else v
+            assert torch.equal(got.cpu(), ref), (k, direct, dtype)
+        assert (counts["file"], counts["put"]) == want, (direct, dtype, counts)

@@ -27,8 +27,9 @@ def test_nd_parallel_single_process():
 
 @pytest.mark.parametrize(
     "dims",
-    [["--dp-shard-size", "2"], ["--tp-size", "2"], ["--cp-size", "2"], ["--dp-replicate-size", "2"]],
-    ids=["fsdp", "tp", "cp", "hsdp_replicate"],
+    [["--dp-shard-size", "2"], ["--tp-size", "2"], ["--cp-size", "2"], ["--dp-replicate-size", "2"],
+     ["--tp-size", "2", "--hf"]],
+    ids=["fsdp", "tp", "cp", "hsdp_replicate", "tp_hf_tp_plan"],
 )
 def test_nd_parallel_two_ranks(dims):
     debug_launcher(_run, args=(BASE + dims,), num_processes=2)
