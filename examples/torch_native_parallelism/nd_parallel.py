@@ -37,6 +37,8 @@ def parse_args(argv=None):
     p.add_argument("--num-steps", type=int, default=20)
     p.add_argument("--cpu", action="store_true")
     p.add_argument("--tiny", action="store_true", help="2-layer toy Llama (CPU smoke runs / tests)")
+    p.add_argument("--hf", action="store_true",
+                   help="a transformers LlamaForCausalLM (as the reference example loads), TP-sharded by its own tp_plan")
     return p.parse_args(argv)
 
 
@@ -53,13 +55,22 @@ def main(argv=None):
     set_seed(42)
     cfg = TINY if args.tiny else LLAMA_PRESETS[args.model]
     seq = min(args.sequence_length, cfg.max_position_embeddings) if args.tiny else args.sequence_length
-    if args.cpu:
+    if args.hf:
+        import transformers as tf
+
+        hcfg = tf.LlamaConfig(vocab_size=cfg.vocab_size, hidden_size=cfg.hidden_size, intermediate_size=cfg.intermediate_size,
+                              num_hidden_layers=cfg.num_hidden_layers, num_attention_heads=cfg.num_attention_heads,
+                              num_key_value_heads=cfg.num_key_value_heads, max_position_embeddings=cfg.max_position_embeddings)
+        model = tf.LlamaForCausalLM(hcfg)
+        if args.dp_shard_size * args.cp_size > 1 or args.dp_replicate_size > 1:
+            plugin.transformer_cls_names_to_wrap = ["LlamaDecoderLayer"]
+    elif args.cpu:
         model = LlamaForCausalLM(cfg)
         model.init_weights()
     else:
         with torch.device("meta"):
             model = LlamaForCausalLM(cfg)
-    opt = torch.optim.AdamW(model.parameters(), lr=1e-4 if args.tiny else 1e-5)
+    opt = torch.optim.AdamW(model.parameters(), lr=(1e-3 if args.hf else 1e-4) if args.tiny else 1e-5)
     model, opt = acc.prepare(model, opt)
     # every rank of one data-parallel replica sees the same batch; TP / CP ranks split the work inside it
     dp_rank = acc.process_index // (args.tp_size * args.cp_size)
@@ -67,6 +78,8 @@ def main(argv=None):
     tracker = ThroughputTracker(warmup_steps=min(5, max(1, args.num_steps - 1)))
     losses = []
     for step in range(args.num_steps):
+        if args.tiny and step % 2 == 0:  # tiny runs revisit two batches so a falling loss shows learning
+            g.manual_seed(1000 + dp_rank)
         ids = torch.randint(0, cfg.vocab_size, (1, seq), generator=g).to(acc.device)
         labels = ids.clone()
         if args.cp_size > 1:
@@ -74,7 +87,7 @@ def main(argv=None):
                 loss = model(ids, shift_labels=labels).loss
                 acc.backward(loss)
         else:
-            loss = model(ids, labels=labels).loss
+            loss = model(input_ids=ids, labels=labels).loss
             acc.backward(loss)
         opt.step()
         opt.zero_grad()
