@@ -194,7 +194,9 @@ class _Installer:
         else:
             return False  # host / disk placements keep the tensor path
         old = recursive_getattr(self.model, name)
-        want = self.target_dtype(name, torch.empty(0, dtype=dtype)) or (old.dtype if dtype.is_floating_point else dtype)
+        # the installed tensor must come out of the DMA in its final dtype: a cast inside set_module_tensor_to_device
+        # would read `dst` on the current stream before the engine's copy has landed
+        want = self.target_dtype(name, torch.empty(0, dtype=dtype)) or old.dtype
         if want != dtype or tuple(old.shape) != tuple(shape) or nbytes != torch.Size(shape).numel() * dtype.itemsize:
             return False
         eng = h2d_engine(dev.index if dev.index is not None else torch.cuda.current_device())
@@ -204,7 +206,7 @@ class _Installer:
         if nbytes:
             eng.copy_file(path, offset, dst)
         self.engines.add(eng)
-        set_module_tensor_to_device(self.model, name, dev, value=dst, clear_cache=False)
+        set_module_tensor_to_device(self.model, name, dev, value=dst, dtype=want, clear_cache=False)
         return True
 
     def put(self, name, t):
@@ -229,11 +231,14 @@ class _Installer:
             eng = h2d_engine(dev.index if dev.index is not None else torch.cuda.current_device())
             if eng is not None:
                 old = recursive_getattr(self.model, name)
-                src = t.to(dt) if dt is not None else (t.to(old.dtype) if torch.is_floating_point(t) else t)
-                dst = torch.empty(src.shape, dtype=src.dtype, device=dev)
+                # convert on the host so `dst` needs no cast after the (asynchronous) DMA: a cast here would read
+                # it on the current stream before the engine's copy has landed
+                final = dt if dt is not None else old.dtype
+                src = t.to(final)
+                dst = torch.empty(src.shape, dtype=final, device=dev)
                 eng.copy(src.contiguous(), dst)
                 self.engines.add(eng)
-                set_module_tensor_to_device(self.model, name, dev, value=dst, clear_cache=False)
+                set_module_tensor_to_device(self.model, name, dev, value=dst, dtype=final, clear_cache=False)
                 return
         set_module_tensor_to_device(self.model, name, dest, value=t, dtype=dt, clear_cache=False)
 

@@ -77,6 +77,7 @@ for step in "$@"; do
     pmc_gemm) run pmc_gemm 400 bash tools/pmc_gemm.sh --variants ${GEMM_VARIANTS:-bl,4,8,7} --shapes o,down --iters 2 --rounds 1 --no-bf16 --no-scaled-mm ;;
     dgrad) run dgrad 300 python tools/bench_dgrad.py ;;
     bench8b_dgradbl) ACCELERATE_DGRAD_BLASLT=1 run bench8b_dgradbl 600 python bench.py --steps 5 --warmup 2 $BENCH_ARGS ;;
+    mfma_peak) run mfma_peak 60 tools/microbench/mfma_peak ;;
     probe) run probe 60 bash -c 'df -h . /tmp /dev/shm; free -g; nproc; mount | grep -E " /tmp | /dev/shm | / " || true' ;;
     gemm_v4) run ktest_v4 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "fp8_gemm_v4 or fp8_gemm_v3 or fp8_gemm_exact" && \
              run gemm_v4 400 python tools/bench_gemm.py --variants ${GEMM_VARIANTS:-bl,4,6,7} --no-bf16 --no-scaled-mm --rounds 3 ;;

@@ -103,14 +103,16 @@ int main() {
   srand(1);
   for (int i = 0; i < 4096; ++i) host[i] = rand() & 0x7f7f7f7f;  // random finite e4m3 bytes (no NaN pattern)
   hipMemcpy(in, host, sizeof(host), hipMemcpyHostToDevice);
-  // per wave per trip: 16 MFMAs of 32x32x64 (2*32*32*64 FLOP) = 64 of 16x16x128 (2*16*16*128)
-  const double flop = (double)grid * 4 * iters * 16 * 2.0 * 32 * 32 * 64;
+  // per wave per trip: k32 = 16 MFMAs of 32x32x64 (2*32*32*64 FLOP each), k16 = 64 of 16x16x128 (2*16*16*128 each),
+  // i.e. k16 does twice the work of k32 per trip
+  const double flop32 = (double)grid * 4 * iters * 16 * 2.0 * 32 * 32 * 64;
+  const double flop16 = (double)grid * 4 * iters * 64 * 2.0 * 16 * 16 * 128;
   const float t32s = timeit(k32<0x7f7f7f7f>, in, out, iters, grid);
   const float t32u = timeit(k32<0>, in, out, iters, grid);
   const float t16s = timeit(k16<0x7f7f7f7f>, in, out, iters, grid);
   const float t16u = timeit(k16<0>, in, out, iters, grid);
   printf("{\"mfma_32x32x64_scaled_tflops\": %.1f, \"mfma_32x32x64_unscaled_tflops\": %.1f, "
          "\"mfma_16x16x128_scaled_tflops\": %.1f, \"mfma_16x16x128_unscaled_tflops\": %.1f}\n",
-         flop / t32s / 1e9, flop / t32u / 1e9, flop / t16s / 1e9, flop / t16u / 1e9);
+         flop32 / t32s / 1e9, flop32 / t32u / 1e9, flop16 / t16s / 1e9, flop16 / t16u / 1e9);
   return 0;
 }
