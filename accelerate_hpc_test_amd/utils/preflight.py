@@ -57,9 +57,12 @@ def _limited(fn, timeout_s: float, on_timeout):
 
 
 def communicator_preflight(groups: dict, device: torch.device, big_bytes: int = 436 << 20, timeout_s: float = 10.0,
-                           iters: int = 3, hard_exit: bool = True, check_ipc: bool = True) -> dict:
+                           iters: int = 3, hard_exit: bool = True, check_ipc: bool = True,
+                           init_timeout_s: float = 180.0) -> dict:
     """Self-test `groups` ({name: process group or None for the world}); returns {name: {...bandwidths}} plus
-    `ipc_allreduce` and `seconds`. Collective over every rank of every group (call it on all ranks, same order)."""
+    `ipc_allreduce` and `seconds`. Collective over every rank of every group (call it on all ranks, same order).
+    The first call on each group may create its RCCL communicator (topology discovery, connection setup: seconds on a
+    cold node), so it gets `init_timeout_s`; every later call gets `timeout_s`."""
     t_all = time.perf_counter()
     report: dict = {}
     for name, group in groups.items():
@@ -67,14 +70,18 @@ def communicator_preflight(groups: dict, device: torch.device, big_bytes: int = 
         entry = {"world": W}
         report[name] = entry
 
-        def run(op, fn, _name=name):
+        def run(op, fn, _name=name, limit=None):
+            limit = timeout_s if limit is None else limit
+
             def timed_out():
-                _fail({"preflight": report}, _name, op, f"no completion within {timeout_s:.0f}s", True)
-            return _limited(lambda: (fn(), _sync(device))[0], timeout_s, timed_out)
+                _fail({"preflight": report}, _name, op, f"no completion within {limit:.0f}s", True)
+            return _limited(lambda: (fn(), _sync(device))[0], limit, timed_out)
 
         # known values (small): all-reduce, all-gather, reduce-scatter
         x = torch.full((W * 4,), float(r + 1), device=device)
-        run("all_reduce", lambda: dist.all_reduce(x, group=group))
+        t0 = time.perf_counter()
+        run("all_reduce", lambda: dist.all_reduce(x, group=group), limit=init_timeout_s)
+        entry["first_call_s"] = round(time.perf_counter() - t0, 3)
         if not bool((x == W * (W + 1) / 2).all()):
             _fail({"preflight": report}, name, "all_reduce", f"expected {W * (W + 1) / 2}, got {x[:4].tolist()}",
                   hard_exit)
@@ -96,7 +103,7 @@ def communicator_preflight(groups: dict, device: torch.device, big_bytes: int = 
         shard = torch.ones(n // W, dtype=torch.bfloat16, device=device)
         for op, fn in (("all_gather_big", lambda: dist.all_gather_into_tensor(full, shard, group=group)),
                        ("reduce_scatter_big", lambda: dist.reduce_scatter_tensor(shard, full, group=group))):
-            run(op, fn)  # warm-up (first use of a size sets up channels / buffers)
+            run(op, fn, limit=max(timeout_s, init_timeout_s / 4))  # warm-up: first use of a size sets up buffers
             t0 = time.perf_counter()
             for _ in range(iters):
                 run(op, fn)
@@ -123,22 +130,33 @@ def communicator_preflight(groups: dict, device: torch.device, big_bytes: int = 
     return report
 
 
-def engine_groups(model) -> dict:
+def engine_groups(model) -> tuple:
     """The named process groups a prepared model's engine communicates on: the world, the FSDP engine's all-gather /
-    reduce-scatter communicators, the DDP reducer's."""
+    reduce-scatter communicators, the DDP reducer's. Returns ({name: group}, {name: "world"}): the second dict names
+    the engine communicators that ARE the world group (gloo engines use it directly), tested once under "world"."""
     groups: dict = {"world": None}
+    aliases: dict = {}
     eng = getattr(model, "engine", None)
     if eng is not None:
         for attr, name in (("ag_group", "fsdp_all_gather"), ("rs_group", "fsdp_reduce_scatter"),
                            ("replicate_group", "fsdp_replicate")):
-            g = getattr(eng, attr, None)
-            if g is not None and name not in groups and dist.get_world_size(g) > 1:
+            if not hasattr(eng, attr):
+                continue
+            g = getattr(eng, attr)
+            if g is None or g is dist.group.WORLD:
+                if attr != "replicate_group":  # no replicate group = no replication, not the world group
+                    aliases[name] = "world"
+            elif name not in groups and dist.get_world_size(g) > 1:
                 groups[name] = g
-    if hasattr(model, "comm_group") and getattr(model, "comm_group", None) is not None:
+    if getattr(model, "comm_group", None) is not None:
         groups["ddp"] = model.comm_group
-    return groups
+    return groups, aliases
 
 
 def preflight_model(model, device: Optional[torch.device] = None, **kw) -> dict:
     device = device or (torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
-    return communicator_preflight(engine_groups(model), device, **kw)
+    groups, aliases = engine_groups(model)
+    report = communicator_preflight(groups, device, **kw)
+    for name, target in aliases.items():
+        report[name] = {"alias_of": target, "ok": report[target]["ok"]}
+    return report
