@@ -408,7 +408,7 @@ try:
     acc.gather(t)
 except DistributedOperationException as e:
     # one write per line: the two ranks share the launcher's stdout
-    sys.stdout.write(f"MISMATCH CAUGHT {acc.process_index} {'Process 1: [3]' in str(e)}\n")
+    sys.stdout.write(f"MISMATCH CAUGHT {acc.process_index} {'Process 1: [3]' in str(e)}\\n")
     sys.stdout.flush()
 else:
     print("NO CHECK", acc.process_index)
