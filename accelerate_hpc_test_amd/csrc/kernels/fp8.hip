@@ -1602,6 +1602,198 @@ __global__ __launch_bounds__(256, 1) void fp8_gemm_v7_kernel(const uint8_t* __re
   }
 }
 
+// ------------------------------------------------------------------------------------------------ GEMM v8
+// v7's tile, slots and register-staged copy with 8 waves in two groups of 4 (one wave of each group per SIMD) that
+// run a barrier-staggered ping-pong (the 8-phase structure of cdna_hip_programming.md §5): group g = wave / 4 owns
+// output rows 128 g .. +127, wave w % 4 of it columns 64 (w % 4) .. +63 (8 x 4 blocks of 16x16 = 128 accumulator
+// registers). Each K-step is two phases per wave, each a MEMORY half (fragment reads, the staged chunks of tile t+1
+// written into the other slot, loads of tile t+2 into the freed registers, lgkmcnt(0)) and a COMPUTE half (16 MFMAs
+// under s_setprio 1), separated by s_barrier. Group 1 passes one extra barrier first, so between two barriers one group
+// computes while the other does its memory half: each group's LDS latency and waits hide under the other's MFMAs.
+// Ordering (regions between consecutive barriers; group 1 lags group 0 by one region): the slot a memory half writes
+// (tile t+1) was last read for tile t-1 at least one barrier earlier by both groups, and the slot it reads (tile t)
+// was completed, lgkmcnt(0) included, by both groups' memory halves of step t-1 before the barrier that precedes it.
+template <int FA, int FB, bool OUT_F32, bool UNSCALED>
+__global__ __launch_bounds__(512, 1) void fp8_gemm_v8_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
+                                                             const float* __restrict__ sa, const float* __restrict__ sb,
+                                                             float smul, const bf16_t* __restrict__ bias, void* __restrict__ C,
+                                                             int M, int N, int K, int accum, int group_m) {
+  __shared__ __attribute__((aligned(1024))) uint8_t slot0[V4_SLOT];
+  __shared__ __attribute__((aligned(1024))) uint8_t slot1[V4_SLOT];
+  const int tiles_n = N / V4_BN, tiles_m = M / V4_BM;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  int tile_m, tile_n;
+  if (group_m > 1) {
+    const int per_group = group_m * tiles_n;
+    const int g = bid / per_group, first = g * group_m, rows = min(tiles_m - first, group_m), in = bid % per_group;
+    tile_m = first + in % rows;
+    tile_n = in / rows;
+  } else {
+    tile_m = bid / tiles_n;
+    tile_n = bid % tiles_n;
+  }
+  const int tm = tile_m * V4_BM, tn = tile_n * V4_BN;
+  ACC_CHECK_OR_RETURN(tm + V4_BM <= M && tn + V4_BN <= N && K % V4_BK == 0 && bid < nwg, kChkGemmTile);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r16 = lane & 15, q = lane >> 4;
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const int grp = wv >> 2;  // wave-uniform and provably so: the stagger barrier below is a scalar branch
+  const int wm = grp * 128, wn = (wv & 3) * 64;
+  constexpr int SC = UNSCALED ? 0 : 0x7f7f7f7f;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // copy: 32 A and 32 B blocks of 8 rows x 128 B per K-tile; wave w moves A blocks 4w .. 4w + 3 and B blocks 4w ..
+  // 4w + 3 (the v4 image: lane l of a block reads logical chunk (l % 8) ^ ((row >> 1) & 7) of row 8b + l / 8 and
+  // writes it at l * 16)
+  unsigned voff[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int row = (wv * 4 + c) * 8 + (lane >> 3);
+    voff[c] = (unsigned)(row * K + v4_swz(row, lane & 7) * 16);
+  }
+  const int woff = wv * 4 * 1024 + lane * 16;
+  const auto a_rs = __builtin_amdgcn_make_buffer_rsrc((void*)(A + (long)tm * K), (short)0, V4_BM * K, 0x00020000);
+  const auto b_rs = __builtin_amdgcn_make_buffer_rsrc((void*)(B + (long)tn * K), (short)0, V4_BN * K, 0x00020000);
+  const int nk = K / V4_BK;
+  auto soff = [&](int kt) { return kt < nk ? kt * V4_BK : 0x40000000; };
+  u32x4 stA[4], stB[4];
+
+  const int f = (r16 >> 1) & 7;
+  const int lo = (q ^ f) * 16, hi = ((q + 4) ^ f) * 16;
+  const int arow = (wm + r16) * V4_BK, brow = V4_BOFF + (wn + r16) * V4_BK;
+  auto frag = [&](const uint8_t* p) -> v8i {
+    const uint4 x = *reinterpret_cast<const uint4*>(p + lo);
+    const uint4 y = *reinterpret_cast<const uint4*>(p + hi);
+    v8i v;
+    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w; v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+    return v;
+  };
+
+  // prologue: tile 0 -> slot 0 through the registers, tile 1 -> registers
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    stA[c] = __builtin_amdgcn_raw_buffer_load_b128(a_rs, voff[c], soff(0), 0);
+    stB[c] = __builtin_amdgcn_raw_buffer_load_b128(b_rs, voff[c], soff(0), 0);
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    *reinterpret_cast<u32x4*>(slot0 + woff + c * 1024) = stA[c];
+    *reinterpret_cast<u32x4*>(slot0 + V4_BOFF + woff + c * 1024) = stB[c];
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    stA[c] = __builtin_amdgcn_raw_buffer_load_b128(a_rs, voff[c], soff(1), 0);
+    stB[c] = __builtin_amdgcn_raw_buffer_load_b128(b_rs, voff[c], soff(1), 0);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  if (grp == 1) __builtin_amdgcn_s_barrier();  // the stagger
+  __builtin_amdgcn_sched_barrier(0);
+
+  auto sync = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto step = [&](int t, const uint8_t* __restrict__ cur, uint8_t* __restrict__ nxt) {
+    const int so2 = soff(t + 2);
+    v8i bf[4], af[4];
+    // memory half 0: B fragments + A rows 0-3 of tile t; A chunks of tile t+1 -> nxt; A chunks of t+2 -> registers
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bf[j] = frag(cur + brow + j * 16 * V4_BK);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = frag(cur + arow + i * 16 * V4_BK);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) *reinterpret_cast<u32x4*>(nxt + woff + c * 1024) = stA[c];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) stA[c] = __builtin_amdgcn_raw_buffer_load_b128(a_rs, voff[c], so2, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    sync();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)  // swapped operands: acc holds C^T blocks (lane <-> m, registers <-> 4 n)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bf[j], af[i], acc[i][j], FB, FA, 0, SC, 0, SC);
+    __builtin_amdgcn_s_setprio(0);
+    sync();
+    // memory half 1: A rows 4-7; B chunks of t+1 -> nxt; B chunks of t+2 -> registers
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = frag(cur + arow + (i + 4) * 16 * V4_BK);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) *reinterpret_cast<u32x4*>(nxt + V4_BOFF + woff + c * 1024) = stB[c];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) stB[c] = __builtin_amdgcn_raw_buffer_load_b128(b_rs, voff[c], so2, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    sync();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i + 4][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bf[j], af[i], acc[i + 4][j], FB, FA, 0, SC, 0, SC);
+    __builtin_amdgcn_s_setprio(0);
+    sync();
+  };
+  for (int t = 0; t < nk; ++t) {
+    const bool odd = t & 1;
+    step(t, odd ? slot1 : slot0, odd ? slot0 : slot1);
+  }
+  if (grp == 0) __builtin_amdgcn_s_barrier();  // equal barrier counts for both groups
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the zero-filled loads past the end retire before the exit
+
+  const float s = sa[0] * sb[0] * smul;
+  auto epilogue = [&](auto has_bias, auto acc_in) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = tm + wm + i * 16 + r16;
+        const int n = tn + wn + j * 16 + 4 * q;
+        float v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = acc[i][j][u] * s;
+        if constexpr (decltype(has_bias)::value) {
+          const bf16x4 b4 = *reinterpret_cast<const bf16x4*>(bias + n);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) v[u] += bf2f(b4.v[u]);
+        }
+        if constexpr (OUT_F32) {
+          float4* cp4 = reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + (long)m * N + n);
+          if constexpr (decltype(acc_in)::value) {
+            const float4 o = *cp4;
+            v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+          }
+          *cp4 = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+          bf16x4* cp4 = reinterpret_cast<bf16x4*>(reinterpret_cast<bf16_t*>(C) + (long)m * N + n);
+          if constexpr (decltype(acc_in)::value) {
+            const bf16x4 o = *cp4;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] += bf2f(o.v[u]);
+          }
+          bf16x4 w;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) w.v[u] = f2bf(v[u]);
+          *cp4 = w;
+        }
+      }
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  if (bias != nullptr) {
+    if (accum) epilogue(T_{}, T_{}); else epilogue(T_{}, F_{});
+  } else {
+    if (accum) epilogue(F_{}, T_{}); else epilogue(F_{}, F_{});
+  }
+}
+
 }  // namespace
 
 ACC_DEBUG_TAKE_FN(acc_dbg_take_fp8)
@@ -1765,13 +1957,14 @@ void fp8_cast_into(torch::Tensor x, torch::Tensor t, double qmax, bool from_amax
 // 5 = v3 8 waves, 6 = v4 (16x16x128 MFMA, BK 128, two slots), 7 = v4 with the unscaled MFMA opcode, 8 / 9 = v3 4 / 8
 // waves with the unscaled MFMA opcode, 10 / 11 = v5 (v4 tiling, one barrier per K-step) scaled / unscaled, 12 / 13 =
 // v6 (v3 with the LDS-DMA issue spread over the whole K-tile) scaled / unscaled, 14 / 15 = v7 (v5 tiling, copy staged
-// through registers instead of LDS-DMA) scaled / unscaled.
+// through registers instead of LDS-DMA) scaled / unscaled, 16 / 17 = v8 (v7 with 8 waves in a barrier-staggered
+// ping-pong) scaled / unscaled.
 // Shapes a variant cannot tile fall back to the next one that can (v3 -> v2 -> v1).
 constexpr int kFp8GemmDefault = 13;  // v6 unscaled: +1-6 % over v3 (profiles/r4_gemm_fp8.md)
 static int g_fp8_gemm_variant = 0;
 static int g_fp8_gemm_group_m = 4;  // v3 tile-row grouping (1 = plain row-major tile order)
 void fp8_gemm_select(int64_t variant, int64_t group_m) {
-  TORCH_CHECK(variant >= 0 && variant <= 15, "fp8_gemm_select: variant 0..15");
+  TORCH_CHECK(variant >= 0 && variant <= 17, "fp8_gemm_select: variant 0..17");
   TORCH_CHECK(group_m >= 0 && group_m <= 64, "fp8_gemm_select: group_m 0..64");
   g_fp8_gemm_variant = (int)variant;
   if (group_m > 0) g_fp8_gemm_group_m = (int)group_m;
@@ -1881,6 +2074,27 @@ torch::Tensor fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor a_scale_i
     return out;
   }
   if (variant == 14 || variant == 15) variant = 4;
+  if ((variant == 16 || variant == 17) && M % V4_BM == 0 && N % V4_BN == 0 && K % V4_BK == 0 &&
+      (long)V4_BM * K < (1L << 30) && (reinterpret_cast<uintptr_t>(bp) & 7) == 0) {
+    const int nwg8 = (M / V4_BM) * (N / V4_BN);
+    const bool un = variant == 17;
+#define GEMM8_LAUNCH(FA, FB, OF)                                                                                        \
+  do {                                                                                                                  \
+    if (un)                                                                                                             \
+      hipLaunchKernelGGL((fp8_gemm_v8_kernel<FA, FB, OF, true>), dim3(nwg8), dim3(512), 0, stream, ap, bptr, sap, sbp,   \
+                         (float)smul, bp, cp, M, N, K, accum, g_fp8_gemm_group_m);                                       \
+    else                                                                                                                \
+      hipLaunchKernelGGL((fp8_gemm_v8_kernel<FA, FB, OF, false>), dim3(nwg8), dim3(512), 0, stream, ap, bptr, sap, sbp,  \
+                         (float)smul, bp, cp, M, N, K, accum, g_fp8_gemm_group_m);                                       \
+  } while (0)
+    if (!a_e5m2 && !b_e5m2) { if (out_fp32) GEMM8_LAUNCH(0, 0, true); else GEMM8_LAUNCH(0, 0, false); }
+    else if (!a_e5m2 && b_e5m2) { if (out_fp32) GEMM8_LAUNCH(0, 1, true); else GEMM8_LAUNCH(0, 1, false); }
+    else if (a_e5m2 && !b_e5m2) { if (out_fp32) GEMM8_LAUNCH(1, 0, true); else GEMM8_LAUNCH(1, 0, false); }
+    else { if (out_fp32) GEMM8_LAUNCH(1, 1, true); else GEMM8_LAUNCH(1, 1, false); }
+#undef GEMM8_LAUNCH
+    return out;
+  }
+  if (variant == 16 || variant == 17) variant = 4;
   if ((variant == 6 || variant == 7) && M % V4_BM == 0 && N % V4_BN == 0 && K % 256 == 0 && (long)V4_BM * K < (1L << 30) &&
       (reinterpret_cast<uintptr_t>(bp) & 7) == 0) {
     const int nwg4 = (M / V4_BM) * (N / V4_BN);
