@@ -1960,7 +1960,7 @@ void fp8_cast_into(torch::Tensor x, torch::Tensor t, double qmax, bool from_amax
 // through registers instead of LDS-DMA) scaled / unscaled, 16 / 17 = v8 (v7 with 8 waves in a barrier-staggered
 // ping-pong) scaled / unscaled.
 // Shapes a variant cannot tile fall back to the next one that can (v3 -> v2 -> v1).
-constexpr int kFp8GemmDefault = 13;  // v6 unscaled: +1-6 % over v3 (profiles/r4_gemm_fp8.md)
+constexpr int kFp8GemmDefault = 17;  // v8 unscaled: the fastest HIP variant at all 12 shapes (profiles/r4_gemm_fp8.md)
 static int g_fp8_gemm_variant = 0;
 static int g_fp8_gemm_group_m = 4;  // v3 tile-row grouping (1 = plain row-major tile order)
 void fp8_gemm_select(int64_t variant, int64_t group_m) {

@@ -336,6 +336,8 @@ void adam_multi_tensor(torch::Tensor meta, torch::Tensor block_prefix, int64_t n
   else if (pdtype == 0 && gdtype == 1 && sdtype == 0) ADAM_LAUNCH(float, bf16_t, float);
   else if (pdtype == 1 && gdtype == 1 && sdtype == 1) ADAM_LAUNCH(bf16_t, bf16_t, bf16_t);
   else if (pdtype == 1 && gdtype == 1 && sdtype == 0) ADAM_LAUNCH(bf16_t, bf16_t, float);
+  else if (pdtype == 0 && gdtype == 0 && sdtype == 1) ADAM_LAUNCH(float, float, bf16_t);  // fp32 master, bf16 m / v
+  else if (pdtype == 0 && gdtype == 1 && sdtype == 1) ADAM_LAUNCH(float, bf16_t, bf16_t);
   else TORCH_CHECK(false, "adam_multi_tensor: unsupported dtype combination");
 #undef ADAM_LAUNCH
 }

@@ -3,7 +3,10 @@
 
 Reference workload: `examples/torch_native_parallelism/fsdp2_fp8.py` — Llama-3.1-8B, seq 8192,
 micro-batch 1 per device, AdamW(lr=1e-5), FSDP2 transformer-wrap of LlamaDecoderLayer, bf16 mixed precision,
-forward / backward / optimizer.step / zero_grad each step. Same here, on this framework's stack:
+forward / backward / optimizer.step / zero_grad each step. The reference builds the model with torch_dtype=bfloat16
+(`fsdp2_fp8.py:88-97`), so its AdamW holds bf16 params and bf16 moments; here the params stay fp32 masters (bf16
+shadows feed the all-gather) and the moments are bf16 (`--adam-states fp32` for fp32 moments). Same here, on this
+framework's stack:
 `Accelerator(fsdp_plugin=FSDP2, mixed_precision="bf16")` → native FSDP engine (RCCL all-gather / reduce-scatter per
 decoder layer on side streams), HIP kernels (flash attention, RMSNorm, RoPE, SwiGLU, cross-entropy, fused AdamW),
 hipBLASLt GEMMs. Synthetic token data (random ids) and random-init weights (no network access).
@@ -31,6 +34,10 @@ def parse():
     p.add_argument("--model", default="llama3-8b")
     p.add_argument("--seq", type=int, default=8192)
     p.add_argument("--mbs", type=int, default=1)
+    p.add_argument("--adam-states", default="bf16", choices=["fp32", "bf16"],
+                   help="dtype of the AdamW moments beside the fp32 master weights (ACCELERATE_ADAM_STATE_DTYPE). The "
+                        "reference's config builds the model in bf16, so its AdamW keeps bf16 params AND bf16 moments; "
+                        "bf16 moments + fp32 master stays at or above that precision in every state")
     p.add_argument("--precision", default="bf16", choices=["bf16", "fp8", "mxfp8"],
                    help="fp8: dynamic per-tensor scaling (torchao recipe); mxfp8: TE MXFP8BlockScaling (e8m0 scale per "
                         "32 elements, applied inside the MFMA)")
@@ -110,6 +117,8 @@ def _spawn_ranks(n: int) -> int:
 
 def main():
     args = parse()
+    if args.adam_states == "bf16":
+        os.environ["ACCELERATE_ADAM_STATE_DTYPE"] = "bf16"
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     launched_world = os.environ.get("WORLD_SIZE")
     if launched_world is None and args.gpus > 1:
@@ -270,7 +279,8 @@ def main():
                 "seq_len": args.seq,
                 "parallelism": f"{args.parallel}{world}" + ("-forced-sharded" if force else "")
                 + ("-forced-reducer" if force_ddp else ""),
-                "optimizer": "AdamW(lr=1e-5), fp32 master" + (", per-unit update overlapped with backward" if overlap else "")
+                "optimizer": "AdamW(lr=1e-5), fp32 master" + (", bf16 moments" if args.adam_states == "bf16" else "")
+                + (", per-unit update overlapped with backward" if overlap else "")
                 + (", CPU-offloaded (host AdamW)" if args.fsdp_cpu_offload else ""),
                 "activation_checkpointing": args.activation_checkpointing,
             },

@@ -201,6 +201,38 @@ def test_fused_adamw_matches_torch():
         assert torch.allclose(a, b, atol=1e-5, rtol=1e-4)
 
 
+def test_fused_adamw_bf16_moments_match_fp32_reference(monkeypatch):
+    """ACCELERATE_ADAM_STATE_DTYPE=bf16: fp32 master weights and grads with bf16 exp_avg / exp_avg_sq.
+    Against torch AdamW with fp32 moments over 20 steps: the moments are the torch moments rounded to bf16 each step,
+    so the parameters agree to the bf16 rounding of the update (rel. 2^-8 of lr per step), far below the update size."""
+    from accelerate_hpc_test_amd.ops.multi_tensor import FusedAdamStep
+
+    monkeypatch.setenv("ACCELERATE_ADAM_STATE_DTYPE", "bf16")
+    torch.manual_seed(0)
+    shapes = [(1000,), (64, 33), (8193,), (3,)]
+    p1 = [torch.randn(s, device=DEV, requires_grad=True) for s in shapes]
+    p2 = [p.detach().clone().requires_grad_() for p in p1]
+    lr = 1e-2
+    o1 = torch.optim.AdamW(p1, lr=lr, weight_decay=0.1)
+    o2 = torch.optim.AdamW(p2, lr=lr, weight_decay=0.1)
+    fused_step = FusedAdamStep(o2)
+    start = [p.detach().clone() for p in p1]
+    for _ in range(20):
+        for a, b in zip(p1, p2):
+            g = torch.randn_like(a)
+            a.grad = g.clone()
+            b.grad = g.clone()
+        o1.step()
+        fused_step.step()
+    for a, b, a0 in zip(p1, p2, start):
+        st = o2.state[b]
+        assert st["exp_avg"].dtype == torch.bfloat16 and st["exp_avg_sq"].dtype == torch.bfloat16 and b.dtype == torch.float32
+        moved = (a - a0).abs().max().item()
+        err = (a - b).abs().max().item()
+        assert moved > lr and err < 0.02 * moved, (err, moved)
+        assert torch.allclose(o1.state[a]["exp_avg_sq"], st["exp_avg_sq"].float(), rtol=2e-2, atol=1e-6)
+
+
 def test_grad_norm_and_clip():
     from accelerate_hpc_test_amd.ops.multi_tensor import clip_grads_by_total_sq, grad_sq_norm
 

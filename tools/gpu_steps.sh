@@ -30,6 +30,8 @@ for step in "$@"; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench20) run bench20 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench20_fp8) run bench20_fp8 600 python bench.py --gpus 1 --steps 20 --warmup 5 --precision fp8 ;;
+    bench20_adambf16) run bench20_adambf16 600 python bench.py --gpus 1 --steps 20 --warmup 5 --adam-states bf16 ;;
+    bench20_fp8hip) ACCELERATE_FP8_GEMM=hip run bench20_fp8hip 600 python bench.py --gpus 1 --steps 20 --warmup 5 --precision fp8 ;;
     bench8b) run bench8b 600 python bench.py --steps 5 --warmup 2 $BENCH_ARGS ;;
     bench8b_nodgradwt) ACCELERATE_DGRAD_WT=0 run bench8b_nodgradwt 600 python bench.py --steps 5 --warmup 2 $BENCH_ARGS ;;
     transpose) run transpose 300 python tools/bench_transpose.py && ACCELERATE_TRANSPOSE128=0 run transpose_old 300 python tools/bench_transpose.py ;;
