@@ -30,8 +30,12 @@ def duplicate_group(group=None):
     """A new process group over exactly the ranks of `group`, i.e. a separate RCCL communicator.
 
     Each purpose that issues collectives from its own HIP stream (FSDP all-gather, FSDP reduce-scatter, DDP bucket
-    all-reduce) gets one: a synchronous collective runs on the issuing stream, and one communicator must not be driven
-    from two streams at once, so separate communicators are what lets those streams really overlap. `new_group` has to
+    all-reduce) gets one. ProcessGroupNCCL (RCCL here) runs every collective of a process group on that group's own
+    internal stream (high priority, `_high_priority_options`), fenced by events: the internal stream first waits for the
+    issuing stream's earlier work, and the issuing stream then waits for the collective. Collectives of ONE group
+    therefore serialise on its single internal stream whichever stream issued them; separate groups are what let the
+    all-gather of one unit and the reduce-scatter of another run at the same time (`profiles/r4_fsdp_forced_sharded.md`:
+    the nranks=1 stand-ins of both overlap 76 % with compute). `new_group` has to
     be entered by every rank of the world for every group created, so the member lists of all ranks are exchanged
     first and each distinct list is created, in the same order everywhere (HSDP / mesh sub-groups included)."""
     ranks = tuple(dist.get_process_group_ranks(group if group is not None else dist.group.WORLD))

@@ -238,9 +238,9 @@ class FSDPEngine:
             self.rs_stream = torch.cuda.Stream(device=device, priority=-1)
         else:
             self.ag_stream = self.rs_stream = None
-        # All-gather and reduce-scatter get communicators of their own (same ranks as `group`): a synchronous RCCL
-        # collective runs on the stream that issues it, and two streams must not drive one communicator
-        # concurrently, so only separate communicators let the backward prefetch AG(i-1) overlap RS(i+1).
+        # All-gather and reduce-scatter get communicators of their own (same ranks as `group`): ProcessGroupNCCL runs
+        # all collectives of one group on that group's single internal stream (event-fenced against the issuing
+        # stream), so only separate groups let the backward prefetch AG(i-1) overlap RS(i+1) (comm.duplicate_group).
         self.ag_group = self.rs_group = process_group
         if self.sharded and self.is_cuda and dist.get_backend(process_group) != "gloo":
             from .comm import duplicate_group
