@@ -1305,6 +1305,62 @@ def check_fsdp_split_root_units(steps: int = 2):
         assert torch.equal(full[n], back[n]), n
 
 
+def check_fsdp_bert_accuracy_lower_bound(version: int, strategy: str = "FULL_SHARD", wrap: str = "transformer_based_wrap",
+                                        steps: int = 60, bound: float = 0.82):
+    """The reference's FSDP `test_performance` (tests/fsdp/test_fsdp.py:484-566: BERT trained under FSDP1 / FSDP2 x
+    sharding strategy x wrap policy must reach accuracy >= 0.82) without the Hub: a tiny random-init transformers
+    BertForSequenceClassification learns a synthetic pair task (label 1 iff the marker token 4 occurs in the sequence,
+    the evaluation set held out) on 2 gloo ranks; evaluation goes through gather_for_metrics."""
+    import transformers as tf
+
+    plugin = FullyShardedDataParallelPlugin(fsdp_version=version, sharding_strategy=strategy if version == 1 else None,
+                                            reshard_after_forward=(strategy == "FULL_SHARD") if version == 2 else None,
+                                            auto_wrap_policy=wrap, transformer_cls_names_to_wrap=["BertLayer"],
+                                            min_num_params=2000 if wrap == "size_based_wrap" else None)
+    acc = Accelerator(cpu=True, fsdp_plugin=plugin)
+    W, r = acc.num_processes, acc.process_index
+    set_seed(0)
+    cfg = tf.BertConfig(vocab_size=64, hidden_size=64, num_hidden_layers=2, num_attention_heads=4, intermediate_size=128,
+                        max_position_embeddings=64, num_labels=2, hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    model = tf.BertForSequenceClassification(cfg)
+
+    def make(n, seed):
+        g = torch.Generator().manual_seed(seed)
+        ids = torch.randint(5, 64, (n, 24), generator=g)
+        ids[:, 0] = 2  # [CLS]-like
+        y = (torch.rand(n, generator=g) < 0.5).long()
+        pos = torch.randint(1, 24, (n,), generator=g)
+        ids[y == 1, pos[y == 1]] = 4
+        return ids, y
+
+    xtr, ytr = make(steps * 16 * W, 1)
+    xev, yev = make(256, 2)
+    opt = torch.optim.AdamW(model.parameters(), lr=2e-3)
+    model, opt = acc.prepare(model, opt)
+    model.train()
+    bs = 16
+    for i in range(steps):
+        lo = (i * W + r) * bs
+        out = model(input_ids=xtr[lo : lo + bs], labels=ytr[lo : lo + bs])
+        acc.backward(out.loss)
+        opt.step()
+        opt.zero_grad()
+    model.eval()
+    correct = total = 0
+    per = len(xev) // W
+    with torch.no_grad():
+        for lo in range(r * per, (r + 1) * per, 32):
+            hi = min(lo + 32, (r + 1) * per)
+            pred = model(input_ids=xev[lo:hi]).logits.argmax(-1)
+            pred, ref = acc.gather_for_metrics((pred, yev[lo:hi]))
+            correct += int((pred == ref).sum())
+            total += len(ref)
+    accuracy = correct / total
+    assert total == len(xev), total
+    assert accuracy >= bound, (version, strategy, wrap, accuracy)
+    return accuracy
+
+
 def _tiny_hf_model(kind: str):
     """Tiny random-init transformers models of the families the reference's pippy examples run
     (`/root/reference/examples/inference/pippy/{llama,bert,gpt2,t5}.py`), and example inputs."""

@@ -210,3 +210,13 @@ def test_tp_hf_models_match_single_process(kind, world):
     """ParallelismConfig(tp_size) on transformers models, sharded by their own tp_plan (colwise / rowwise /
     colwise_gather_output / replicated_with_grad_allreduce / packed_colwise / moe_tp_experts)."""
     debug_launcher(td.check_tp_hf, args=(kind,), num_processes=world)
+
+
+@pytest.mark.parametrize("version,strategy,wrap", [(2, "FULL_SHARD", "transformer_based_wrap"),
+                                                   (1, "SHARD_GRAD_OP", "transformer_based_wrap"),
+                                                   (1, "FULL_SHARD", "size_based_wrap")])
+def test_fsdp_bert_accuracy_lower_bound(version, strategy, wrap):
+    """Reference tests/fsdp/test_fsdp.py::test_performance: FSDP1 / FSDP2 x sharding x wrap policy reach the 0.82
+    accuracy bound (tiny random-init BERT on a learnable synthetic pair task; no Hub access)."""
+    debug_launcher(td.check_fsdp_bert_accuracy_lower_bound, args=(version, strategy, wrap), num_processes=2)
+
