@@ -114,6 +114,11 @@ class FusedAdamStep:
                     st["step"] = torch.tensor(0.0, dtype=torch.float32)
                     st["exp_avg"] = torch.zeros_like(p, dtype=sdt, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, dtype=sdt, memory_format=torch.preserve_format)
+                elif st["exp_avg"].dtype != adam_state_dtype(p) and st["exp_avg"].dtype == torch.float32:
+                    # bf16 moments requested but the state came back fp32 (torch's load_state_dict casts optimizer state
+                    # to the param dtype): narrow it once
+                    st["exp_avg"] = st["exp_avg"].to(torch.bfloat16)
+                    st["exp_avg_sq"] = st["exp_avg_sq"].to(torch.bfloat16)
                 st["step"] += 1
                 s = float(st["step"]) if step_val is None else step_val
                 step_val = s

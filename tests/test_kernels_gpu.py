@@ -231,6 +231,16 @@ def test_fused_adamw_bf16_moments_match_fp32_reference(monkeypatch):
         err = (a - b).abs().max().item()
         assert moved > lr and err < 0.02 * moved, (err, moved)
         assert torch.allclose(o1.state[a]["exp_avg_sq"], st["exp_avg_sq"].float(), rtol=2e-2, atol=1e-6)
+    # a checkpoint round trip through torch's load_state_dict widens the moments to the param dtype; the next fused
+    # step narrows them back to bf16 and carries on from the same values
+    sd = o2.state_dict()
+    o3 = torch.optim.AdamW(p2, lr=lr, weight_decay=0.1)
+    o3.load_state_dict(sd)
+    assert o3.state[p2[0]]["exp_avg"].dtype == torch.float32
+    for b in p2:
+        b.grad = torch.zeros_like(b)
+    FusedAdamStep(o3).step()
+    assert all(o3.state[b]["exp_avg"].dtype == torch.bfloat16 for b in p2)
 
 
 def test_grad_norm_and_clip():
