@@ -61,9 +61,20 @@ __device__ __forceinline__ v8bf row_frag(const char* img, int row, int chunk) {
   return *reinterpret_cast<const v8bf*>(img + img_off(row, chunk));
 }
 
+// Row-read-only image (layout (a) of cdna_hip_programming.md T10: 8-row x 32-column subtiles of 512 B, 16-B chunks
+// XOR-swizzled within each 64-B row segment). For a lane's fixed row the 8 row reads of a 32x32x16 operand (chunks
+// 2s + hf) sit at base_even / base_odd + 512 (s >> 1): two address registers and immediate offsets, where the 256-B
+// row image needs one register per read. Used for the dK / dV kernel's K and V tiles, which live above 64 KB of LDS
+// (the 16-bit offset field cannot hold their base, so every read there needs its own address register anyway).
+__device__ __forceinline__ int img_off_a(int row, int ch) {
+  return 2048 * (row >> 3) + 512 * (ch >> 2) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3));
+}
+
+// The LDS pointer is address-space-cast (not round-tripped through an integer): it keeps its provenance, so hipcc's
+// alias analysis still sees which __shared__ object a transposed read touches and does not make it wait (vmcnt(0))
+// for an LDS-DMA in flight into a different object.
 __device__ __forceinline__ v4bf tr_read(const char* p) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-      (__attribute__((address_space(3))) v4bf*)(reinterpret_cast<uintptr_t>(p)));
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) v4bf*)(p));
 }
 
 // A-operand fragment of X^T, X a [rows][128] tile in the dual image: rows rb..rb+15 form the MFMA k dimension in
@@ -83,6 +94,37 @@ __device__ __forceinline__ v8bf tr_frag(const char* img, int rb, int db, int lan
 }
 
 __device__ __forceinline__ int acc_row(int i, int hf) { return (i & 3) + 8 * (i >> 2) + 4 * hf; }
+
+// Lane offsets of the reads of a layout-(a) image (img_off_a), computed once per kernel: two registers serve every
+// row read of a 32x32x16 operand and two every transposed read, the rest is the instruction's immediate offset.
+struct ImgA {
+  int row_e, row_o;  // row reads, chunk parity even / odd: row r0 + (lane & 31), chunk 2s + (lane >> 5)
+  int tr_lo, tr_hi;  // transposed reads (tr_frag's lane map), rows +0 / +8 of the 16-row block
+  __device__ __forceinline__ void init(int lane) {
+    const int r = lane & 31, hf = lane >> 5;
+    row_e = 2048 * (r >> 3) + 64 * (r & 7) + 16 * (hf ^ ((r >> 2) & 3));
+    row_o = row_e ^ 32;  // chunk (2 + hf) ^ w = (hf ^ w) ^ 2
+    const int g = lane >> 4, i = lane & 15;
+    const int row0 = 4 * (g >> 1) + (i >> 2);        // 0 .. 7
+    const int ch0 = 2 * (g & 1) + ((i & 3) >> 1);    // 0 .. 3
+    const int sub = 8 * (i & 1);
+    tr_lo = 64 * row0 + 16 * (ch0 ^ (row0 >> 2)) + sub;
+    tr_hi = 2048 + 64 * row0 + 16 * (ch0 ^ ((row0 >> 2) + 2)) + sub;
+  }
+  // row read: rows rb + (lane & 31) (rb a multiple of 8 with (rb >> 2) & 3 == 0, i.e. of 16), chunk 2s + hf
+  __device__ __forceinline__ v8bf row(const char* img, int rb, int s) const {
+    return *reinterpret_cast<const v8bf*>(img + ((s & 1) ? row_o : row_e) + 256 * rb + 512 * (s >> 1));
+  }
+  // tr_frag of a layout-(a) image: rows rb .. rb + 15 (rb a multiple of 16), columns db * 32 .. + 31
+  __device__ __forceinline__ v8bf tr(const char* img, int rb, int db) const {
+    const v4bf lo = tr_read(img + tr_lo + 256 * rb + 512 * db);
+    const v4bf hi = tr_read(img + tr_hi + 256 * rb + 512 * db);
+    v8bf x;
+    x[0] = lo[0]; x[1] = lo[1]; x[2] = lo[2]; x[3] = lo[3];
+    x[4] = hi[0]; x[5] = hi[1]; x[6] = hi[2]; x[7] = hi[3];
+    return x;
+  }
+};
 
 // Query head of workgroup x in a (Hq, S/128, B) grid. Workgroups are dealt round-robin over the 8 XCDs and the
 // linear id is x + Hq * (y + ...), so with Hq % 8 == 0 workgroup x runs on XCD x % 8. Mapping x to head
@@ -121,6 +163,13 @@ struct Stage {
       *reinterpret_cast<v8bf*>(img + img_off(row, ch)) = r[t];
     }
   }
+  __device__ __forceinline__ void store_a(char* img, int tid) const {  // layout (a), img_off_a
+#pragma unroll
+    for (int t = 0; t < kPer; ++t) {
+      const int c = tid + t * NT, row = c >> 4, ch = c & 15;
+      *reinterpret_cast<v8bf*>(img + img_off_a(row, ch)) = r[t];
+    }
+  }
 };
 
 // LDS-DMA staging of a ROWS x 128 bf16 tile of a token-strided [S, ..., 128] tensor into the dual image: buffer_load
@@ -141,6 +190,18 @@ struct TileDMA {
     for (int t = 0; t < kPer; ++t) {
       const int row = 4 * (first + t) + (lane >> 4), pc = lane & 15;
       voff[t] = (unsigned)(row * ts_bytes + ((pc ^ img_swz(row)) << 4));
+    }
+  }
+  // the same pieces filling a layout-(a) image (img_off_a): LDS byte o = 1024 p + 16 l holds row 8 (o >> 11) +
+  // ((o >> 6) & 7), logical chunk 4 ((o >> 9) & 3) + (((o >> 4) & 3) ^ ((row >> 2) & 3))
+  __device__ __forceinline__ void init_a(int wave, int lane, int ts_bytes) {
+    first = __builtin_amdgcn_readfirstlane(wave) * kPer;
+#pragma unroll
+    for (int t = 0; t < kPer; ++t) {
+      const int o = 1024 * (first + t) + 16 * lane;
+      const int row = 8 * (o >> 11) + ((o >> 6) & 7);
+      const int ch = 4 * ((o >> 9) & 3) + (((o >> 4) & 3) ^ ((row >> 2) & 3));
+      voff[t] = (unsigned)(row * ts_bytes + ch * 16);
     }
   }
   __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, int row0, int ts_bytes, char* img) const {
@@ -235,8 +296,10 @@ __global__ __launch_bounds__(256 * NH, 2 / NH) void attn_fwd_kernel(FwdParams p)
 
   TileDMA<64, 4 * NH> dk, dv_;
   const int kts = (int)(p.k_ts * 2), vts = (int)(p.v_ts * 2);
-  dk.init(wave_id, lane, kts);
-  dv_.init(wave_id, lane, vts);
+  dk.init_a(wave_id, lane, kts);  // K / V tiles in layout (a): ImgA reads
+  dv_.init_a(wave_id, lane, vts);
+  ImgA ia;
+  ia.init(lane);
   const auto krs = head_rsrc(kb_, p.Sk, p.k_ts), vrs = head_rsrc(vb_, p.Sk, p.v_ts);
   dk.issue(krs, 0, kts, k0s);
   dv_.issue(vrs, 0, vts, v0s);
@@ -259,7 +322,7 @@ __global__ __launch_bounds__(256 * NH, 2 / NH) void attn_fwd_kernel(FwdParams p)
       for (int kb = 0; kb < 2; ++kb) {
         zero(sc[kb]);
 #pragma unroll
-        for (int s = 0; s < 8; ++s) sc[kb] = mfma(row_frag(k_img, kb * 32 + r, 2 * s + hf), qf[s], sc[kb]);
+        for (int s = 0; s < 8; ++s) sc[kb] = mfma(ia.row(k_img, kb * 32, s), qf[s], sc[kb]);
       }
       // Only tiles that reach past the wave's first query need the mask (wave-uniform branch)
       if (MASKED && k0 + 63 > qw0 + off) {
@@ -308,7 +371,7 @@ __global__ __launch_bounds__(256 * NH, 2 / NH) void attn_fwd_kernel(FwdParams p)
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) o[d] = mfma(tr_frag(v_img, kb * 32 + 16 * s2, d, lane), pb[kb][s2], o[d]);
+          for (int s2 = 0; s2 < 2; ++s2) o[d] = mfma(ia.tr(v_img, kb * 32 + 16 * s2, d), pb[kb][s2], o[d]);
     }
     wait_dma_and_sync();
   };
@@ -342,9 +405,12 @@ __global__ __launch_bounds__(256 * NH, 2 / NH) void attn_fwd_kernel(FwdParams p)
   wave_trace(p.trace, t_start, wave_id, (unsigned)qt | ((unsigned)h << 16));
 }
 
-// delta[b, h, s] = sum_d dO * O (fp32), one wave per (b, s, h).
+// The dK / dV kernel's row constants, both pre-negated so they seed its S and dP accumulators as loaded (no VALU):
+// ndelta[b, h, s] = -sum_d dO * O (fp32) and nlse[b, h, s] = -lse / scale. One wave per (b, s, h). (The dQ kernel
+// writes the same two buffers itself on the normal path; this kernel serves the diagnostic variants.)
 __global__ void attn_delta_kernel(const bf16_t* __restrict__ o, long o_ts, long o_bs, const bf16_t* __restrict__ dout,
-                                  long do_ts, long do_bs, float* __restrict__ delta, int S, int Hq, int B) {
+                                  long do_ts, long do_bs, float* __restrict__ delta, const float* __restrict__ lse,
+                                  float* __restrict__ nlse, float inv_scale, int S, int Hq, int B) {
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= (long)B * S * Hq) return;
@@ -355,13 +421,17 @@ __global__ void attn_delta_kernel(const bf16_t* __restrict__ o, long o_ts, long 
   const bf16_t* dp = dout + b * do_bs + (long)s * do_ts + (long)h * kD + lane * 2;
   float acc = bf2f(op[0]) * bf2f(dp[0]) + bf2f(op[1]) * bf2f(dp[1]);
   acc = wave_sum(acc);
-  if (lane == 0) delta[((long)b * Hq + h) * S + s] = acc;
+  const long st = ((long)b * Hq + h) * S + s;
+  if (lane == 0) {
+    delta[st] = -acc;
+    nlse[st] = -lse[st] * inv_scale;
+  }
 }
 
 struct BwdParams {
   const bf16_t *q, *k, *v, *dout;
   long q_ts, k_ts, v_ts, do_ts, q_bs, k_bs, v_bs, do_bs;
-  const float *lse, *delta;
+  const float *lse, *delta;  // delta holds -rowsum(dO * O) (see attn_delta_kernel)
   bf16_t *dq, *dk, *dv;
   long dq_ts, dq_bs, dk_ts, dk_bs, dv_ts, dv_bs;
   int S, Hq, Hkv;
@@ -372,6 +442,7 @@ struct BwdParams {
   const bf16_t* o;
   long o_ts, o_bs;
   float* delta_out;
+  float* nlse;  // -lse / scale, written next to delta (dQ kernel or attn_delta_kernel), read by the dK / dV kernel
   int Sk, off;  // key count and causal offset Sk - S (see the header)
   unsigned long long* trace;  // optional per-wave timeline (attn_trace), see wave_trace
 };
@@ -416,9 +487,12 @@ __global__ __launch_bounds__(256 * NH, 2 / NH) void attn_bwd_dq_kernel(BwdParams
       for (int j = 0; j < 8; ++j) acc = fmaf(static_cast<float>(df[s][j]), static_cast<float>(of[j]), acc);
     }
     dlt = acc + __shfl_xor(acc, 32, 64);
-    if (hf == 0) p.delta_out[st] = dlt;
+    if (hf == 0) {
+      p.delta_out[st] = -dlt;
+      p.nlse[st] = -p.lse[st] * p.inv_scale;
+    }
   } else {
-    dlt = p.delta[st];
+    dlt = -p.delta[st];
   }
   f32x16 dq[4];
 #pragma unroll
@@ -428,8 +502,10 @@ __global__ __launch_bounds__(256 * NH, 2 / NH) void attn_bwd_dq_kernel(BwdParams
 
   TileDMA<64, 4 * NH> dk, dv_;
   const int kts = (int)(p.k_ts * 2), vts = (int)(p.v_ts * 2);
-  dk.init(wave_id, lane, kts);
-  dv_.init(wave_id, lane, vts);
+  dk.init_a(wave_id, lane, kts);  // K / V tiles in layout (a): ImgA reads
+  dv_.init_a(wave_id, lane, vts);
+  ImgA ia;
+  ia.init(lane);
   const auto krs = head_rsrc(kb_, p.Sk, p.k_ts), vrs = head_rsrc(vb_, p.Sk, p.v_ts);
   dk.issue(krs, 0, kts, k0s);
   dv_.issue(vrs, 0, vts, v0s);
@@ -454,8 +530,8 @@ __global__ __launch_bounds__(256 * NH, 2 / NH) void attn_bwd_dq_kernel(BwdParams
         zero(dp);
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
-          sc = mfma(row_frag(k_img, kb * 32 + r, 2 * s + hf), qf[s], sc);
-          dp = mfma(row_frag(v_img, kb * 32 + r, 2 * s + hf), df[s], dp);
+          sc = mfma(ia.row(k_img, kb * 32, s), qf[s], sc);
+          dp = mfma(ia.row(v_img, kb * 32, s), df[s], dp);
         }
         // causal: query qw0 + r sees keys k0 + 32kb + 4hf + acc_row(i, 0) up to itself (diagonal tiles only)
         const int lim = qw0 + r + off - (k0 + kb * 32 + 4 * hf);
@@ -474,7 +550,7 @@ __global__ __launch_bounds__(256 * NH, 2 / NH) void attn_bwd_dq_kernel(BwdParams
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) dq[d] = mfma(tr_frag(k_img, kb * 32 + 16 * s2, d, ln), dsb[kb][s2], dq[d]);
+          for (int s2 = 0; s2 < 2; ++s2) dq[d] = mfma(ia.tr(k_img, kb * 32 + 16 * s2, d), dsb[kb][s2], dq[d]);
     }
     wait_dma_and_sync();
   };
@@ -516,8 +592,10 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_kernel(BwdParams p) {
   constexpr int kSlice = 64;
   constexpr int kImg = kSlice * kRow;  // 16 KB: one 64-row Q or dO image
   constexpr int kKV = 128 * kRow;      // 32 KB: the key tile's K (or V) image
-  // K | V of the key tile (one object: the epilogue reuses it as one 64 KB reduction buffer), and two slice buffers
-  // (Q image, dO image, lse[64] | delta[64]) filled by LDS-DMA, one static object each (see TileDMA)
+  // K | V of the key tile (one object, layout (a): img_off_a; the epilogue reuses it as one 64 KB reduction buffer),
+  // and two slice buffers (Q image, dO image, -lse/scale[64] | -delta[64]) filled by LDS-DMA, one static object each
+  // (see TileDMA). hipcc places the largest object first: K | V at LDS offset 0, where the parity base registers of
+  // the K / V row reads take every other offset as an immediate.
   __shared__ __attribute__((aligned(1024))) char smem[2 * kKV];
   __shared__ __attribute__((aligned(1024))) char qs0[kImg], ds0[kImg], qs1[kImg], ds1[kImg];
   __shared__ __attribute__((aligned(16))) float ls0[2 * kSlice], ls1[2 * kSlice];
@@ -531,14 +609,12 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_kernel(BwdParams p) {
   const int kr = (wave & 3) * 32, qh = (wave >> 2) * 32;
   const int kw0 = kt * 128 + kr;
   ACC_CHECK_OR_RETURN(kt * 128 + 128 <= p.Sk && kh < p.Hkv && p.Hq % p.Hkv == 0, kChkAttnTile);
-  char* k_img = smem;
-  char* v_img = smem + kKV;
   {
     Stage<128, 512> sk, sv;
     sk.load(p.k + b * p.k_bs + (long)kh * kD, p.k_ts, kt * 128, tid);
     sv.load(p.v + b * p.v_bs + (long)kh * kD, p.v_ts, kt * 128, tid);
-    sk.store(k_img, tid);
-    sv.store(v_img, tid);
+    sk.store_a(smem, tid);
+    sv.store_a(smem + kKV, tid);
   }
   f32x16 dk[4], dv[4];
 #pragma unroll
@@ -560,7 +636,7 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_kernel(BwdParams p) {
   dmd.init(wave, lane, dts);
   const long rc_bytes = (long)gridDim.y * p.Hq * p.S * 4;
   const int rc = (int)(rc_bytes > 0x7fffffffL ? 0x7fffffffL : rc_bytes);
-  const auto lrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.lse, (short)0, rc, 0x00020000);
+  const auto lrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.nlse, (short)0, rc, 0x00020000);
   const auto drs = __builtin_amdgcn_make_buffer_rsrc((void*)p.delta, (short)0, rc, 0x00020000);
   const int wv = __builtin_amdgcn_readfirstlane(wave);
   auto issue = [&](int it, char* qi, char* di, float* ld) {
@@ -592,19 +668,26 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_kernel(BwdParams p) {
     const int q0 = (qs0_ + it % per) * kSlice;
     if (CAUSAL ? q0 + qh + 31 + off >= kw0 : lv >= 0) {  // non-causal: an opaque always-true test keeps the block shape
       const int r = lv & 31, hf = lv >> 5;
+      const int krow = kr + r, kw = (krow >> 2) & 3;
+      const int kv_e = 2048 * (krow >> 3) + 64 * (krow & 7) + 16 * (hf ^ kw);
+      const int kv_o = kv_e ^ 32;  // chunk (2 + hf) ^ kw = (hf ^ kw) ^ 2
       f32x16 sc, dp;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {  // rows qh + 8g + 4hf .. +3 of the slice: one 16-B LDS read per constant
+        // -lse / scale and -delta, negated and scaled by their producer: the reads land in the accumulators as is
         const float4 l4 = *reinterpret_cast<const float4*>(lse_s + qh + 8 * g + 4 * hf);
         const float4 d4 = *reinterpret_cast<const float4*>(dlt_s + qh + 8 * g + 4 * hf);
-        const float ni = -p.inv_scale;
-        sc[4 * g] = l4.x * ni; sc[4 * g + 1] = l4.y * ni; sc[4 * g + 2] = l4.z * ni; sc[4 * g + 3] = l4.w * ni;
-        dp[4 * g] = -d4.x; dp[4 * g + 1] = -d4.y; dp[4 * g + 2] = -d4.z; dp[4 * g + 3] = -d4.w;
+        sc[4 * g] = l4.x; sc[4 * g + 1] = l4.y; sc[4 * g + 2] = l4.z; sc[4 * g + 3] = l4.w;
+        dp[4 * g] = d4.x; dp[4 * g + 1] = d4.y; dp[4 * g + 2] = d4.z; dp[4 * g + 3] = d4.w;
       }
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
-        sc = mfma(row_frag(q_img, qh + r, 2 * s + hf), row_frag(k_img, kr + r, 2 * s + hf), sc);
-        dp = mfma(row_frag(d_img, qh + r, 2 * s + hf), row_frag(v_img, kr + r, 2 * s + hf), dp);
+        // img_off_a(krow, 2s + hf) = (s odd ? kv_o : kv_e) + 512 (s >> 1): one register per operand and parity
+        const int o = ((s & 1) ? kv_o : kv_e) + 512 * (s >> 1);
+        const v8bf kf = *reinterpret_cast<const v8bf*>(smem + o);
+        const v8bf vf = *reinterpret_cast<const v8bf*>(smem + kKV + o);
+        sc = mfma(row_frag(q_img, qh + r, 2 * s + hf), kf, sc);
+        dp = mfma(row_frag(d_img, qh + r, 2 * s + hf), vf, dp);
       }
       // causal: key kw0 + r is masked for query rows q0 + qh + 4hf + acc_row(i, 0) below it (diagonal tiles only)
       const int lim = kw0 + r - (q0 + off + qh + 4 * hf);
@@ -643,10 +726,11 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_kernel(BwdParams p) {
 
   // Waves 4-7 hand their query-half partials to waves 0-3 through LDS (64 KB per pass: dK, then dV); the sum is
   // scaled and written as bf16 into the strided [B, S, Hkv, D] output.
-  float* red = reinterpret_cast<float*>(smem);
+  // reduction buffer of query-half partner pair i (16 KB = 4096 floats): the four K / V objects, free after the loop
+  auto red = [&](int i) { return reinterpret_cast<float*>(smem) + i * 4096; };
   auto finish = [&](f32x16(&acc)[4], bf16_t* dst, long ts, long bs, float scale) {
     if (wave >= 4) {
-      float* w = red + (wave - 4) * 4096;
+      float* w = red(wave - 4);
 #pragma unroll
       for (int d = 0; d < 4; ++d)
 #pragma unroll
@@ -654,7 +738,7 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_kernel(BwdParams p) {
     }
     __syncthreads();
     if (wave < 4) {
-      const float* w = red + wave * 4096;
+      const float* w = red(wave);
       bf16_t* out = dst + b * bs + (long)(kw0 + r) * ts + (long)kh * kD;
 #pragma unroll
       for (int d = 0; d < 4; ++d)
@@ -777,13 +861,15 @@ void flash_attn_bwd(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch:
               o.size(1) == S, "flash_attn: q / k / v / gradient sequence lengths");
   auto stream = at::hip::getCurrentHIPStream();
   auto delta = torch::empty({B, Hq, S}, q.options().dtype(torch::kFloat32));
+  auto nlse = torch::empty({B, Hq, S}, q.options().dtype(torch::kFloat32));
   const bool fused_delta = g_attn_dbg == 0 || !causal;  // the diagnostic variants may skip the dQ kernel
   if (!fused_delta) {
     const long rows = (long)B * S * Hq;
     hipLaunchKernelGGL(attn_delta_kernel, dim3((rows + 3) / 4), dim3(256), 0, stream,
                        reinterpret_cast<const bf16_t*>(o.data_ptr()), o.stride(1), o.stride(0),
                        reinterpret_cast<const bf16_t*>(dout.data_ptr()), dout.stride(1), dout.stride(0),
-                       delta.data_ptr<float>(), S, Hq, B);
+                       delta.data_ptr<float>(), lse.data_ptr<float>(), nlse.data_ptr<float>(),
+                       (float)(1.0 / softmax_scale), S, Hq, B);
   }
   TORCH_CHECK(Hq % Hkv == 0 && dk.size(2) == Hkv && dv.size(2) == Hkv && dq.size(2) == Hq, "flash_attn: head counts");
   BwdParams p{reinterpret_cast<const bf16_t*>(q.data_ptr()), reinterpret_cast<const bf16_t*>(k.data_ptr()),
@@ -794,7 +880,7 @@ void flash_attn_bwd(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch:
               dq.stride(0), dk.stride(1), dk.stride(0), dv.stride(1), dv.stride(0), S, Hq, Hkv,
               (float)(softmax_scale * kLog2e), (float)softmax_scale, (float)(1.0 / softmax_scale),
               reinterpret_cast<const bf16_t*>(o.data_ptr()), o.stride(1), o.stride(0),
-              fused_delta ? delta.data_ptr<float>() : nullptr, Sk, Sk - S, nullptr};
+              fused_delta ? delta.data_ptr<float>() : nullptr, nlse.data_ptr<float>(), Sk, Sk - S, nullptr};
   static const int dq_heads = [] { const char* e = std::getenv("ACCELERATE_ATTN_DQ_HEADS"); return e ? std::atoi(e) : 2; }();
   const int nh = (dq_heads == 2 && (Hq / Hkv) % 2 == 0) ? 2 : 1;  // query heads per dQ workgroup (see the kernel)
   const dim3 dq_grid(Hq / nh, S / 128, B), kv_grid(Hkv * (Sk / 128), B);
