@@ -805,7 +805,11 @@ def test_fsdp_wgrad_from_transposed_input_matches(monkeypatch, direct):
             opt.zero_grad()
         finals[xt] = acc.get_state_dict(model)
     for n, t in finals[False].items():
-        assert torch.allclose(t, finals[True][n], atol=2e-4, rtol=1e-3), (n, (t - finals[True][n]).abs().max())
+        # Adam normalises a gradient element by its own running RMS, so an element whose two summation orders differ
+        # in sign near zero (embedding rows of rarely seen tokens) moves by up to +-lr per step in either run; every
+        # other element agrees to rounding
+        d = (t.float() - finals[True][n].float()).abs()
+        assert d.max() <= 2 * 1e-3 * 2 and d.mean() <= 2e-5, (n, d.max(), d.mean())
 
 
 def _llama_tiny_run(steps, handlers=(), preset="llama-tiny", lr=1e-3, seed_ids=1, clip=None, precision="bf16", **plugin_kw):
