@@ -61,6 +61,17 @@ State& state() {
 
 bool check(hipblasStatus_t st) { return st == HIPBLAS_STATUS_SUCCESS; }
 
+// How many of hipBLASLt's heuristic candidates a searched plan times (ACCELERATE_BLASLT_CANDIDATES, default 32): the
+// search runs once per problem (bucket), at its first call.
+int search_width() {
+  static const int n = [] {
+    const char* e = std::getenv("ACCELERATE_BLASLT_CANDIDATES");
+    const int v = e ? std::atoi(e) : 32;
+    return v < 1 ? 1 : (v > 512 ? 512 : v);
+  }();
+  return n;
+}
+
 // Workspace of `stream` (call with s.mu held).
 void* workspace_for(State& s, hipStream_t stream, const torch::Tensor& like) {
   auto it = s.stream_ws.find(stream);
@@ -87,7 +98,7 @@ bool build_plan(State& s, Plan& p, int64_t T, int64_t N, int64_t K, bool x_t, hi
   if (!check(hipblasLtMatmulPreferenceCreate(&pref))) return false;
   uint64_t ws = kWorkspace;
   hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &ws, sizeof(ws));
-  std::vector<hipblasLtMatmulHeuristicResult_t> res(32);
+  std::vector<hipblasLtMatmulHeuristicResult_t> res(search_width());
   int got = 0;
   const bool okh = check(hipblasLtMatmulAlgoGetHeuristic(s.handle, p.desc, p.la, p.lb, p.lc, p.lc, pref, (int)res.size(),
                                                          res.data(), &got));
@@ -238,7 +249,7 @@ bool build_dg_plan(State& s, Plan& p, int64_t T, int64_t N, int64_t K, hipStream
   if (!check(hipblasLtMatmulPreferenceCreate(&pref))) return false;
   uint64_t ws = kWorkspace;
   hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &ws, sizeof(ws));
-  std::vector<hipblasLtMatmulHeuristicResult_t> res(32);
+  std::vector<hipblasLtMatmulHeuristicResult_t> res(search_width());
   int got = 0;
   const bool okh = check(hipblasLtMatmulAlgoGetHeuristic(s.handle, p.desc, p.la, p.lb, p.lc, p.lc, pref, (int)res.size(),
                                                          res.data(), &got));
@@ -404,7 +415,7 @@ bool build_f8_plan(State& s, F8Plan& p, int64_t M, int64_t N, int64_t K, int64_t
   if (!check(hipblasLtMatmulPreferenceCreate(&pref))) return false;
   uint64_t ws = kWorkspace;
   hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &ws, sizeof(ws));
-  std::vector<hipblasLtMatmulHeuristicResult_t> res(32);
+  std::vector<hipblasLtMatmulHeuristicResult_t> res(search_width());
   int got = 0;
   const bool okh = check(hipblasLtMatmulAlgoGetHeuristic(s.handle, p.desc, p.la, p.lb, p.lc, p.lc, pref, (int)res.size(),
                                                          res.data(), &got));

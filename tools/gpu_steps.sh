@@ -43,6 +43,8 @@ for step in "$@"; do
                run bench_tuned 600 python bench.py --steps 5 --warmup 2 --gemm-table gpurun_out/tunableop_merged.csv && \
                run bench_untuned 600 python bench.py --steps 5 --warmup 2 ;;
     wgrad_layout) run wgrad_layout 300 python tools/bench_wgrad_layout.py ;;
+    wgrad_wide) ACCELERATE_BLASLT_CANDIDATES=${CANDIDATES:-256} run wgrad_wide 300 python tools/bench_wgrad_layout.py ;;
+    bench20_wide) ACCELERATE_BLASLT_CANDIDATES=${CANDIDATES:-256} run bench20_wide 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench8b_noblaslt) ACCELERATE_BLASLT_WGRAD=0 run bench8b_noblaslt 600 python bench.py --steps 5 --warmup 2 $BENCH_ARGS ;;
     bench8b_blaslt) ACCELERATE_BLASLT_WGRAD=1 run bench8b_blaslt 600 python bench.py --steps 5 --warmup 2 $BENCH_ARGS ;;
     bench8b_nooverlap) run bench8b_nooverlap 600 python bench.py --steps 5 --warmup 2 --optimizer-overlap off $BENCH_ARGS ;;
