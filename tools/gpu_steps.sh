@@ -75,6 +75,12 @@ for step in "$@"; do
     prof_mixtral_bf16) prof prof_mixtral_bf16 600 bench.py --model mixtral-8x7b-4l --steps 2 --warmup 1 ;;
     moetests) run moetests 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "grouped or moe or transpose" ;;
     attn) run attn 300 python tools/bench_attn.py --no-sdpa ;;
+    attn_k128) ACCELERATE_ATTN_FWD_KEYS=128 run attn_k128 300 python tools/bench_attn.py --no-sdpa ;;
+    ktest_k128) ACCELERATE_ATTN_FWD_KEYS=128 run ktest_k128 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "flash or attention or context_parallel" ;;
+    ktest_dq128) ACCELERATE_ATTN_DQ_KEYS=128 run ktest_dq128 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "flash or attention or context_parallel" ;;
+    attn_dq128) ACCELERATE_ATTN_DQ_KEYS=128 run attn_dq128 300 python tools/bench_attn.py --no-sdpa ;;
+    bench20_dq128) ACCELERATE_ATTN_DQ_KEYS=128 run bench20_dq128 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    bench20_k128) ACCELERATE_ATTN_FWD_KEYS=128 run bench20_k128 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     attn_long) run attn_long 300 python tools/bench_attn.py --S 32768 --iters 3 ;;
     pmc_attn) run pmc_attn 200 bash tools/pmc_attn.sh ;;
     gemm) run gemm 300 python tools/bench_gemm.py ;;
