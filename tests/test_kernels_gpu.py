@@ -105,8 +105,11 @@ def _attn_ref(q, k, v, causal, scale):
 
 
 @pytest.mark.parametrize("causal", [True, False])
-@pytest.mark.parametrize("B,S,Hq,Hkv", [(1, 256, 4, 2), (2, 512, 8, 2), (1, 384, 2, 2), (1, 1024, 8, 2), (1, 2048, 32, 8)])
+@pytest.mark.parametrize("B,S,Hq,Hkv", [(1, 256, 4, 2), (2, 512, 8, 2), (1, 384, 2, 2), (1, 384, 4, 2), (1, 1024, 8, 2),
+                                         (1, 2048, 32, 8)])
 def test_flash_attention(causal, B, S, Hq, Hkv):
+    """Forward and backward against fp32. (1, 384, 4, 2): three 128-key tiles in the two-head forward (odd count: the
+    last plain tile outside the buffer pairs); the kv-prefix test's 640-key cases do the same with an offset."""
     torch.manual_seed(0)
     D = 128
     qkv = torch.randn(B, S, Hq + 2 * Hkv, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
@@ -145,7 +148,7 @@ def _prefix_attn_ref(q, k, v, causal, scale):
 
 
 @pytest.mark.parametrize("causal", [True, False])
-@pytest.mark.parametrize("Sq,Sk", [(1024, 1024), (1024, 2048), (512, 3072), (128, 1024)])
+@pytest.mark.parametrize("Sq,Sk", [(1024, 1024), (1024, 2048), (512, 3072), (128, 1024), (384, 640), (256, 640)])
 def test_flash_attention_kv_prefix(causal, Sq, Sk):
     """More keys than queries (the context-parallel call: a query chunk against its whole causal K/V prefix): forward
     O / LSE and the dQ / dK / dV backward against fp32, bottom-right-aligned causal mask."""
