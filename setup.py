@@ -8,10 +8,39 @@ loads). `__graft_entry__.build()` runs the same thing.
 
 import glob
 import os
+import re
 
 from setuptools import find_packages, setup
 
 os.environ.setdefault("PYTORCH_ROCM_ARCH", "gfx950")
+
+
+def _touch_if_includes_changed(sources, include_dirs):
+    """The ninja build recompiles a .hip source only when that file changes, not when a file it #includes does (no
+    depfiles for hipcc here): the csrc/debug shims are one-line includes of the kernel sources, and every kernel
+    includes kernels/common.h. Give each source the newest mtime of its quoted-include closure so ninja sees it."""
+    pat = re.compile(r'^\s*#\s*include\s+"([^"]+)"', re.M)
+
+    def closure(path, seen):
+        if path in seen or not os.path.isfile(path):
+            return
+        seen.add(path)
+        with open(path, encoding="utf-8", errors="replace") as f:
+            text = f.read()
+        for inc in pat.findall(text):
+            for d in [os.path.dirname(path)] + list(include_dirs):
+                cand = os.path.normpath(os.path.join(d, inc))
+                if os.path.isfile(cand):
+                    closure(cand, seen)
+                    break
+
+    for src in sources:
+        deps = set()
+        closure(src, deps)
+        newest = max(os.path.getmtime(p) for p in deps)
+        if newest > os.path.getmtime(src):
+            os.utime(src, (newest, newest))
+
 
 ext_modules = []
 cmdclass = {}
@@ -24,6 +53,7 @@ if os.environ.get("ACCELERATE_SKIP_NATIVE_BUILD", "0") != "1":
         + sorted(g for g in glob.glob(os.path.join(root, "kernels", "*.hip")) if not g.endswith("_hip.hip"))
         + sorted(glob.glob(os.path.join(root, "runtime", "*.cpp")))
     )
+    _touch_if_includes_changed(sources, [os.path.join(root, "kernels")])
     sources = [os.path.relpath(s, os.path.dirname(os.path.abspath(__file__))) for s in sources]
     ext_modules.append(
         CUDAExtension(
@@ -43,6 +73,7 @@ if os.environ.get("ACCELERATE_SKIP_NATIVE_BUILD", "0") != "1":
     # ACCELERATE_BUILD_DEBUG_KERNELS=0 skips it.
     if os.environ.get("ACCELERATE_BUILD_DEBUG_KERNELS", "1") != "0":
         dbg = sorted(glob.glob(os.path.join(root, "debug", "*.hip"))) + sorted(glob.glob(os.path.join(root, "debug", "*.cpp")))
+        _touch_if_includes_changed(dbg, [os.path.join(root, "kernels")])
         ext_modules.append(
             CUDAExtension(
                 name="accelerate_hpc_test_amd._C_debug",
