@@ -86,8 +86,11 @@ __global__ __launch_bounds__(kXentThreads) void xent_bwd_kernel(const bf16_t* lo
 // ------------------------------------------------------------------------------------------------
 // Multi-tensor apply
 // ------------------------------------------------------------------------------------------------
+// amax (Adam only, optional): an fp32 slot receiving max |bf16(updated p)| over the tensor by atomicMax on its bits (the
+// caller zeroes it first). The FSDP engine points it at a weight's fp8 all-gather amax, so the per-step re-quantisation
+// needs no second read of the bf16 shards (parallel/fsdp.py refresh_fp8).
 struct TensorMeta {
-  int64_t p, g, m, v, shadow, n;
+  int64_t p, g, m, v, shadow, n, amax;
 };
 
 constexpr int kMTThreads = 256;
@@ -158,6 +161,8 @@ __global__ __launch_bounds__(kMTThreads) void adam_mt_kernel(const TensorMeta* _
   S* m = reinterpret_cast<S*>(tm.m);
   S* v = reinterpret_cast<S*>(tm.v);
   bf16_t* sh = reinterpret_cast<bf16_t*>(tm.shadow);
+  unsigned int* amax = reinterpret_cast<unsigned int*>(tm.amax);  // block-uniform
+  float am = 0.f;
   const float gs = grad_scale != nullptr ? grad_scale[0] : 1.f;
   const bool aligned = (tm.p % Vec4<P>::kAlign == 0) && (tm.g % Vec4<G>::kAlign == 0) &&
                        (tm.m % Vec4<S>::kAlign == 0) && (tm.v % Vec4<S>::kAlign == 0) && (tm.shadow % 8 == 0);
@@ -175,12 +180,17 @@ __global__ __launch_bounds__(kMTThreads) void adam_mt_kernel(const TensorMeta* _
       Vec4<S>::store(m + i, mf);
       Vec4<S>::store(v + i, vf);
       if (sh != nullptr) Vec4<bf16_t>::store(sh + i, pf);
+      if (amax != nullptr) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) am = fmaxf(am, fabsf(bf2f(f2bf(pf[j]))));
+      }
     }
     for (int64_t i = vend + threadIdx.x; i < end; i += kMTThreads) {
       float pf = to_f<P>(p[i]), mf = to_f<S>(m[i]), vf = to_f<S>(v[i]);
       adam_elem(pf, to_f<G>(g[i]) * gs, mf, vf, h);
       p[i] = from_f<P>(pf); m[i] = from_f<S>(mf); v[i] = from_f<S>(vf);
       if (sh != nullptr) sh[i] = f2bf(pf);
+      if (amax != nullptr) am = fmaxf(am, fabsf(bf2f(f2bf(pf))));
     }
   } else {
     for (int64_t i = start + threadIdx.x; i < end; i += kMTThreads) {
@@ -188,7 +198,13 @@ __global__ __launch_bounds__(kMTThreads) void adam_mt_kernel(const TensorMeta* _
       adam_elem(pf, to_f<G>(g[i]) * gs, mf, vf, h);
       p[i] = from_f<P>(pf); m[i] = from_f<S>(mf); v[i] = from_f<S>(vf);
       if (sh != nullptr) sh[i] = f2bf(pf);
+      if (amax != nullptr) am = fmaxf(am, fabsf(bf2f(f2bf(pf))));
     }
+  }
+  if (amax != nullptr) {  // block-uniform: every thread reaches the barriers
+    __shared__ float scratch[16];
+    am = block_max(am, scratch);
+    if (threadIdx.x == 0) atomicMax(amax, __float_as_uint(am));  // non-negative floats order like their bits
   }
 }
 
@@ -323,6 +339,7 @@ void xent_bwd(torch::Tensor logits, torch::Tensor labels, torch::Tensor lse, tor
 void adam_multi_tensor(torch::Tensor meta, torch::Tensor block_prefix, int64_t nblocks, int64_t pdtype, int64_t gdtype,
                        int64_t sdtype, double lr, double beta1, double beta2, double eps, double wd, double bc1,
                        double bc2_sqrt, bool adamw, c10::optional<torch::Tensor> grad_scale) {
+  TORCH_CHECK(meta.dim() == 2 && meta.size(1) == sizeof(TensorMeta) / 8, "multi_tensor: meta must be [n, 7] int64");
   const int nt = meta.size(0);
   if (nt == 0 || nblocks == 0) return;
   auto stream = at::hip::getCurrentHIPStream();
@@ -348,6 +365,7 @@ int64_t multi_tensor_chunk() { return kChunk; }
 // or accumulated when `accumulate`).
 void sqnorm_multi_tensor(torch::Tensor meta, torch::Tensor block_prefix, int64_t nblocks, int64_t gdtype, torch::Tensor out,
                          bool accumulate) {
+  TORCH_CHECK(meta.dim() == 2 && meta.size(1) == sizeof(TensorMeta) / 8, "multi_tensor: meta must be [n, 7] int64");
   const int nt = meta.size(0);
   auto stream = at::hip::getCurrentHIPStream();
   if (nt == 0 || nblocks == 0) {
@@ -367,6 +385,7 @@ void sqnorm_multi_tensor(torch::Tensor meta, torch::Tensor block_prefix, int64_t
 
 void clip_multi_tensor(torch::Tensor meta, torch::Tensor block_prefix, int64_t nblocks, int64_t gdtype, torch::Tensor total_sq,
                        double max_norm) {
+  TORCH_CHECK(meta.dim() == 2 && meta.size(1) == sizeof(TensorMeta) / 8, "multi_tensor: meta must be [n, 7] int64");
   const int nt = meta.size(0);
   if (nt == 0 || nblocks == 0) return;
   auto stream = at::hip::getCurrentHIPStream();
@@ -381,6 +400,7 @@ void clip_multi_tensor(torch::Tensor meta, torch::Tensor block_prefix, int64_t n
 // grads *= inv_scale[0]; found_inf[0] = 1 if any result is inf / NaN (found_inf is NOT cleared here: torch semantics).
 void unscale_multi_tensor(torch::Tensor meta, torch::Tensor block_prefix, int64_t nblocks, int64_t gdtype, torch::Tensor inv_scale,
                           torch::Tensor found_inf) {
+  TORCH_CHECK(meta.dim() == 2 && meta.size(1) == sizeof(TensorMeta) / 8, "multi_tensor: meta must be [n, 7] int64");
   const int nt = meta.size(0);
   if (nt == 0 || nblocks == 0) return;
   TORCH_CHECK(inv_scale.scalar_type() == at::kFloat && found_inf.scalar_type() == at::kFloat, "unscale: fp32 scale / flag");

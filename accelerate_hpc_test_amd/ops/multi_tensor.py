@@ -20,6 +20,10 @@ import torch
 from ._ext import ext, use_native
 
 _DT = {torch.float32: 0, torch.bfloat16: 1}
+# The fused AdamW also reduces max |bf16(p)| of FSDP fp8-gathered weights into their amax slots (their per-step
+# re-quantisation then skips its amax pass over the bf16 shards); ACCELERATE_FP8_AMAX_IN_ADAM=0 turns that off.
+_AMAX_IN_ADAM = os.environ.get("ACCELERATE_FP8_AMAX_IN_ADAM", "1") != "0"
+_META_COLS = 7  # TensorMeta: p, g, m, v, shadow, n, amax
 
 
 class _MetaCache:
@@ -32,7 +36,8 @@ class _MetaCache:
         if hit is not None:
             return hit
         chunk = ext().multi_tensor_chunk()
-        meta = torch.tensor(rows, dtype=torch.int64) if rows else torch.zeros((0, 6), dtype=torch.int64)
+        rows = [tuple(r) + (0,) * (_META_COLS - len(r)) for r in rows]  # absent trailing fields (amax) are 0
+        meta = torch.tensor(rows, dtype=torch.int64) if rows else torch.zeros((0, _META_COLS), dtype=torch.int64)
         nblocks = [(r[5] + chunk - 1) // chunk for r in rows]
         prefix = [0]
         for n in nblocks:
@@ -53,14 +58,15 @@ _CACHE = _MetaCache()
 
 def _merge_contiguous(rows):
     """Merge rows whose p/g/m/v/shadow ranges are adjacent in memory (per-parameter views of one flat FSDP shard
-    become a single range → aligned vector access, fewer chunk boundaries)."""
+    become a single range → aligned vector access, fewer chunk boundaries). Rows are (p, g, m, v, shadow, n, p / g / m
+    element sizes, amax); a row with an amax slot stays on its own (the slot covers exactly that tensor)."""
     if not rows:
         return rows
     out = [list(rows[0])]
     for r in rows[1:]:
         prev = out[-1]
         n = prev[5]
-        ok = True
+        ok = prev[9] == 0 and r[9] == 0
         for idx, esz in ((0, r[6]), (1, r[7]), (2, r[8]), (3, r[8])):
             if prev[idx] + n * esz != r[idx]:
                 ok = False
@@ -69,7 +75,7 @@ def _merge_contiguous(rows):
             prev[5] += r[5]
         else:
             out.append(list(r))
-    return [tuple(x[:6]) for x in out]
+    return [tuple(x[:6]) + (x[9],) for x in out]
 
 
 def adam_state_dtype(param: torch.Tensor) -> torch.dtype:
@@ -94,6 +100,7 @@ class FusedAdamStep:
         updates of `fsdp_optimizer_overlap`, and the remainder at `optimizer.step()`)."""
         opt = self.optimizer
         e = ext()
+        amax_units = {}  # FSDP units whose fp8 amax slots this call fills: id -> (engine, unit, ids of updated params)
         for group in opt.param_groups:
             lr = group["lr"]
             if isinstance(lr, torch.Tensor):
@@ -135,6 +142,15 @@ class FusedAdamStep:
                     self._launch(e, rows, dtypes, lr, beta1, beta2, eps, wd, step_val, grad_scale, p.device)
                     rows, dtypes = [], dt
                 shadow = getattr(p, "_acc_bf16_shadow", None)
+                amax_ptr = 0
+                amax_ref = getattr(p, "_acc_fp8_amax", None) if (_AMAX_IN_ADAM and shadow is not None) else None
+                if amax_ref is not None:
+                    eng, unit, slot = amax_ref
+                    if id(unit) not in amax_units:
+                        unit.f8_amax.zero_()  # stream-ordered before the launch that max-reduces into it
+                        amax_units[id(unit)] = (eng, unit, set())
+                    amax_units[id(unit)][2].add(id(p))
+                    amax_ptr = slot.data_ptr()
                 rows.append(
                     (
                         p.data_ptr(),
@@ -146,10 +162,13 @@ class FusedAdamStep:
                         p.element_size(),
                         g.element_size(),
                         m.element_size(),
+                        amax_ptr,
                     )
                 )
             if rows:
                 self._launch(e, rows, dtypes, lr, beta1, beta2, eps, wd, step_val, grad_scale, group["params"][0].device)
+        for eng, unit, seen in amax_units.values():
+            eng.fp8_amax_from_optimizer(unit, seen)
 
     def _launch(self, e, rows, dtypes, lr, beta1, beta2, eps, wd, step, grad_scale, device):
         if not rows:

@@ -389,6 +389,12 @@ class FSDPEngine:
         for u in self.f8_units:
             first = u.f8_seg[3]
             u.f8_amax = self.f8_amax_all[first : first + len(u.f8_infos)]
+            # the fused AdamW writes these weights' bf16 shards and can max-reduce them into the amax slots on the way
+            # (ops/multi_tensor.py FusedAdamStep); refresh_fp8 then skips its own amax pass for the unit
+            u.f8_amax_fresh = False
+            u.f8_param_ids = {id(info.shard_param) for info in u.f8_infos}
+            for k, info in enumerate(u.f8_infos):
+                info.shard_param._acc_fp8_amax = (self, u, u.f8_amax[k : k + 1])
         # World size 1 (no all-gather), opt-in with ACCELERATE_FP8_PRETRANSPOSE=1: the e4m3 weights are persistent, so
         # their K-major copies for the dgrad GEMM can be kept too and written by the same per-step cast (one read of the
         # bf16 weight writes both layouts) instead of a byte transpose of every weight in every backward. Measured on
@@ -403,8 +409,13 @@ class FSDPEngine:
                              if self.f8_pretransposed else None)
         self.refresh_fp8()
 
+    def fp8_amax_from_optimizer(self, unit: FlatUnit, updated_ids: set):
+        """Called by the fused AdamW after it max-reduced |bf16(update)| into `unit.f8_amax` (zeroed first): the amax is
+        current only if every fp8 weight of the unit was updated by that launch."""
+        unit.f8_amax_fresh = updated_ids >= unit.f8_param_ids
+
     @torch.no_grad()
-    def refresh_fp8(self):
+    def refresh_fp8(self, optimizer_amax: bool = False):
         """Re-quantise the fp8-gathered weights from the bf16 shards: per-weight amax of the local pieces, ONE
         all-reduce(MAX) over the shard group for every weight of the model (torchao's
         `precompute_float8_dynamic_scale_for_fsdp`, reference accelerator.py:2061-2066), then the per-weight scaled
@@ -414,6 +425,9 @@ class FSDPEngine:
         from ..ops._ext import use_native
 
         for u in self.f8_units:
+            fresh, u.f8_amax_fresh = u.f8_amax_fresh, False
+            if optimizer_amax and fresh:
+                continue  # the fused AdamW already reduced this unit's amax from the values it wrote
             lo, hi, max_len, _ = u.f8_seg
             src = u.shard_lp[: u.f8.shard_len]
             if use_native(src):
@@ -1152,7 +1166,8 @@ class FSDPEngine:
         elif self.param_dtype != torch.float32 and not fused_wrote_shadow:
             for unit in self.units:
                 unit.shard_lp.copy_(unit.master)
-        self.refresh_fp8()  # the bf16 shards are current: re-quantise the fp8 all-gather sources
+        # the bf16 shards are current: re-quantise the fp8 all-gather sources (amax from the fused AdamW when it wrote them)
+        self.refresh_fp8(optimizer_amax=fused_wrote_shadow and not self.offload)
         if self.sharded:
             for unit in self.units:
                 if unit.state == "unsharding" and unit.ag_event is not None and self.is_cuda:

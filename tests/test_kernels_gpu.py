@@ -1191,6 +1191,41 @@ def test_fsdp_fp8_all_gather_matches_bf16_all_gather(one_rank_rccl, monkeypatch,
         assert torch.equal(t, res[True][2][n]), n
 
 
+@pytest.mark.parametrize("force", [False, True])
+def test_fsdp_fp8_amax_from_fused_adamw(one_rank_rccl, monkeypatch, force):
+    """The fused AdamW max-reduces |bf16(update)| of the fp8-gathered weights into their amax slots while it writes the
+    bf16 shards, and the per-step re-quantisation (refresh_fp8) skips its own amax pass over the shards: the same
+    amaxes, losses and weights bit for bit as with the separate segment-amax kernel, with fewer of its launches."""
+    from accelerate_hpc_test_amd.ops import multi_tensor
+    from accelerate_hpc_test_amd.ops._ext import ext
+    from accelerate_hpc_test_amd.utils import AORecipeKwargs, RcclKwargs
+
+    e = ext()
+    real = e.fp8_segment_amax
+    res = {}
+    for fused in (False, True):
+        calls = [0]
+
+        def counting(*a, _real=real, _calls=calls):
+            _calls[0] += 1
+            return _real(*a)
+
+        monkeypatch.setattr(multi_tensor, "_AMAX_IN_ADAM", fused)
+        monkeypatch.setattr(e, "fp8_segment_amax", counting)
+        acc, model, losses, _ = _llama_tiny_run(3, [RcclKwargs(fsdp_force_sharded=force),
+                                                    AORecipeKwargs(enable_fsdp_float8_all_gather=True)], precision="fp8")
+        eng = model.engine
+        assert eng.f8_units
+        res[fused] = (losses, eng.f8_amax_all.clone(), acc.get_state_dict(model), calls[0])
+    monkeypatch.setattr(e, "fp8_segment_amax", real)
+    assert res[False][0] == res[True][0], (res[False][0], res[True][0])
+    assert torch.equal(res[False][1], res[True][1])
+    for n, t in res[False][2].items():
+        assert torch.equal(t, res[True][2][n]), n
+    # off: one amax launch per fp8 unit at set-up and after each of the 3 steps; on: the set-up ones only
+    assert res[True][3] < res[False][3], (res[True][3], res[False][3])
+
+
 def test_fp8_segment_kernels_and_byte_transpose():
     from accelerate_hpc_test_amd.ops._ext import ext
 
