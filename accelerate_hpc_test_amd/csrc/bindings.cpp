@@ -59,6 +59,7 @@ torch::Tensor fp8_amax(torch::Tensor x, c10::optional<torch::Tensor> out);
 std::vector<torch::Tensor> fp8_cast(torch::Tensor x, torch::Tensor t, double qmax, bool from_amax, bool e5m2, bool transpose);
 void fp8_cast_into(torch::Tensor x, torch::Tensor t, double qmax, bool from_amax, bool e5m2, torch::Tensor y,
                    c10::optional<torch::Tensor> yt);
+void fp8_cast_batched_into(torch::Tensor x, torch::Tensor amax, double qmax, torch::Tensor y, torch::Tensor yt);
 torch::Tensor fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor a_scale_inv, torch::Tensor b_scale_inv,
                        double smul, bool a_e5m2, bool b_e5m2, c10::optional<torch::Tensor> bias, bool out_fp32,
                        c10::optional<torch::Tensor> out, bool accumulate);
@@ -123,6 +124,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fp8_amax", &fp8_amax);
   m.def("fp8_cast", &fp8_cast);
   m.def("fp8_cast_into", &fp8_cast_into);
+  m.def("fp8_cast_batched_into", &fp8_cast_batched_into);
   m.def("fp8_gemm", &fp8_gemm, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("a_scale_inv"), pybind11::arg("b_scale_inv"),
         pybind11::arg("smul"), pybind11::arg("a_e5m2"), pybind11::arg("b_e5m2"), pybind11::arg("bias"), pybind11::arg("out_fp32"),
         pybind11::arg("out") = pybind11::none(), pybind11::arg("accumulate") = false);

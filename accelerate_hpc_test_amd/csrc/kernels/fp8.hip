@@ -91,6 +91,13 @@ __global__ __launch_bounds__(256) void cast_kernel(const bf16_t* __restrict__ x,
                                                    int from_amax, uint8_t* __restrict__ y, uint8_t* __restrict__ yt, int M,
                                                    int N) {
   __shared__ __attribute__((aligned(16))) uint8_t tile[kCT * kCTP];
+  {  // batched [E, M, N] stacks (grid.z = E): matrix z and its own scale / amax slot; grid.z = 1 otherwise
+    const long zo = (long)blockIdx.z * M * N;
+    x += zo;
+    y += zo;
+    if (TRANS) yt += zo;
+    st += blockIdx.z;
+  }
   const int tm = blockIdx.y * kCT, tn = blockIdx.x * kCT;
   const float s = cast_scale(st, qmax, from_amax != 0);
   const int tid = threadIdx.x;
@@ -1951,6 +1958,26 @@ void fp8_cast_into(torch::Tensor x, torch::Tensor t, double qmax, bool from_amax
     if (tr) hipLaunchKernelGGL((cast_kernel<false, true>), grid, dim3(256), 0, stream, xp, tp, q, fa, yp, ytp, M, N);
     else hipLaunchKernelGGL((cast_kernel<false, false>), grid, dim3(256), 0, stream, xp, tp, q, fa, yp, ytp, M, N);
   }
+}
+
+// Per-matrix e4m3 cast of a [E, M, N] bf16 stack with one amax per matrix (scale 448 / amax[e], the conversion of
+// seg_cast_kernel) into y [E, M, N] and its per-matrix transpose yt [E, N, M], one launch: the MoE expert weights'
+// e4m3 copies and their K-major dgrad operands in one pass (no separate byte transpose re-reading y).
+void fp8_cast_batched_into(torch::Tensor x, torch::Tensor amax, double qmax, torch::Tensor y, torch::Tensor yt) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.dim() == 3,
+              "fp8_cast_batched_into: x must be a 3-D contiguous bf16 stack");
+  const int E = x.size(0), M = x.size(1), N = x.size(2);
+  TORCH_CHECK(amax.is_cuda() && amax.scalar_type() == at::kFloat && amax.is_contiguous() && amax.numel() == E,
+              "fp8_cast_batched_into: amax must be fp32 [E]");
+  TORCH_CHECK(y.is_cuda() && y.element_size() == 1 && y.is_contiguous() && y.numel() == (long)E * M * N &&
+                  yt.is_cuda() && yt.element_size() == 1 && yt.is_contiguous() && yt.numel() == (long)E * M * N,
+              "fp8_cast_batched_into: bad y / yt");
+  if (E == 0 || M == 0 || N == 0) return;
+  TORCH_CHECK(E <= 65535, "fp8_cast_batched_into: too many matrices");
+  dim3 grid((N + kCT - 1) / kCT, (M + kCT - 1) / kCT, E);
+  hipLaunchKernelGGL((cast_kernel<false, true>), grid, dim3(256), 0, at::hip::getCurrentHIPStream(),
+                     reinterpret_cast<const bf16_t*>(x.data_ptr()), amax.data_ptr<float>(), (float)qmax, 1,
+                     reinterpret_cast<uint8_t*>(y.data_ptr()), reinterpret_cast<uint8_t*>(yt.data_ptr()), M, N);
 }
 
 // Kernel choice of fp8_gemm: 0 = default, 1 = v1 (128x128), 2 = v2 4 waves, 3 = v2 8 waves, 4 = v3 (4-deep ring),

@@ -295,8 +295,18 @@ def _expert_weight_fp8(w, recipe, key):
     flat = w.contiguous().view(-1)
     n = flat.numel() // E
     lo = torch.arange(E, device=w.device, dtype=torch.long) * n
-    amax = torch.empty(E, dtype=torch.float32, device=w.device)
-    ext().fp8_segment_amax(flat, lo, lo + n, amax, n)
+    held = getattr(w, "_acc_fp8_expert_amax", None)  # FSDP world size 1: reduced by the fused AdamW that wrote w
+    if held is not None and held.fresh and held.amax.numel() == E:
+        amax = held.amax
+    else:
+        amax = torch.empty(E, dtype=torch.float32, device=w.device)
+        ext().fp8_segment_amax(flat, lo, lo + n, amax, n)
+    if os.environ.get("ACCELERATE_MOE_FP8_CAST_T", "1") != "0":
+        # one pass writes both layouts (per-expert scale): no byte transpose re-reading the e4m3 stack
+        w8 = torch.empty(w.shape, dtype=torch.float8_e4m3fn, device=w.device)
+        w8t = torch.empty((E, w.shape[2], w.shape[1]), dtype=torch.float8_e4m3fn, device=w.device)
+        ext().fp8_cast_batched_into(flat.view(w.shape), amax, E4M3_MAX, w8, w8t)
+        return w8, w8t, amax
     w8 = torch.empty(flat.numel(), dtype=torch.float8_e4m3fn, device=w.device)
     ext().fp8_segment_cast(flat, lo, lo + n, amax, E4M3_MAX, w8, n)
     w8 = w8.view(w.shape)

@@ -101,6 +101,7 @@ class FusedAdamStep:
         opt = self.optimizer
         e = ext()
         amax_units = {}  # FSDP units whose fp8 amax slots this call fills: id -> (engine, unit, ids of updated params)
+        expert_amax = []  # MoE expert-stack amax holders this call fills (one kernel row per expert)
         for group in opt.param_groups:
             lr = group["lr"]
             if isinstance(lr, torch.Tensor):
@@ -142,6 +143,17 @@ class FusedAdamStep:
                     self._launch(e, rows, dtypes, lr, beta1, beta2, eps, wd, step_val, grad_scale, p.device)
                     rows, dtypes = [], dt
                 shadow = getattr(p, "_acc_bf16_shadow", None)
+                segs = getattr(p, "_acc_fp8_amax_segs", None) if (_AMAX_IN_ADAM and shadow is not None) else None
+                if segs is not None and segs.seg * segs.amax.numel() == p.numel():
+                    segs.amax.zero_()  # stream-ordered before the launch that max-reduces into it
+                    expert_amax.append(segs)
+                    es = (p.element_size(), g.element_size(), m.element_size())
+                    for k in range(segs.amax.numel()):
+                        o = k * segs.seg
+                        rows.append((p.data_ptr() + o * es[0], g.data_ptr() + o * es[1], m.data_ptr() + o * es[2],
+                                     v.data_ptr() + o * es[2], shadow.data_ptr() + o * 2, segs.seg, *es,
+                                     segs.amax.data_ptr() + 4 * k))
+                    continue
                 amax_ptr = 0
                 amax_ref = getattr(p, "_acc_fp8_amax", None) if (_AMAX_IN_ADAM and shadow is not None) else None
                 if amax_ref is not None:
@@ -169,6 +181,8 @@ class FusedAdamStep:
                 self._launch(e, rows, dtypes, lr, beta1, beta2, eps, wd, step_val, grad_scale, group["params"][0].device)
         for eng, unit, seen in amax_units.values():
             eng.fp8_amax_from_optimizer(unit, seen)
+        for h in expert_amax:
+            h.fresh = True
 
     def _launch(self, e, rows, dtypes, lr, beta1, beta2, eps, wd, step, grad_scale, device):
         if not rows:

@@ -305,6 +305,7 @@ class FSDPEngine:
             self.units.append(unit)
         self.root = self.units[0]
         self._init_fp8_all_gather()
+        self._init_expert_amax()
         # parameters the engine does not own (ignored modules, expert-parallel experts): kept as plain device
         # tensors; they still take part in the global grad-norm (see clip_grad_norm_)
         self.extra_names = [n for n, p in self.model.named_parameters() if id(p) in ignored]
@@ -409,6 +410,28 @@ class FSDPEngine:
                              if self.f8_pretransposed else None)
         self.refresh_fp8()
 
+    def _init_expert_amax(self):
+        """World size 1 (the shard is the whole stack): give every fp8 MoE expert stack [E, N, K] a per-expert amax
+        that the fused AdamW max-reduces from the bf16 values it writes (one kernel row per expert), so the expert
+        forward (models/moe.py `_expert_weight_fp8`) skips its amax pass over the stack."""
+        self.expert_amax = []
+        if self.sharded or self.offload or self.param_dtype != torch.bfloat16:
+            return
+        from ..models.moe import MoEExperts  # lazy: models import parallel.comm
+
+        for unit in self.units:
+            for info in unit.infos:
+                m, sp = info.module, info.shard_param
+                rec = getattr(m, "fp8_recipe", None)
+                if (not isinstance(m, MoEExperts) or rec is None or getattr(rec, "mx", False) or len(info.shape) != 3
+                        or sp is None or sp.numel() != info.numel or getattr(sp, "_acc_bf16_shadow", None) is None):
+                    continue
+                holder = _ExpertAmax(torch.zeros(info.shape[0], dtype=torch.float32, device=self.device),
+                                     info.numel // info.shape[0])
+                info.param._acc_fp8_expert_amax = holder
+                sp._acc_fp8_amax_segs = holder
+                self.expert_amax.append(holder)
+
     def fp8_amax_from_optimizer(self, unit: FlatUnit, updated_ids: set):
         """Called by the fused AdamW after it max-reduced |bf16(update)| into `unit.f8_amax` (zeroed first): the amax is
         current only if every fp8 weight of the unit was updated by that launch."""
@@ -420,6 +443,9 @@ class FSDPEngine:
         all-reduce(MAX) over the shard group for every weight of the model (torchao's
         `precompute_float8_dynamic_scale_for_fsdp`, reference accelerator.py:2061-2066), then the per-weight scaled
         cast of each shard into its e4m3 all-gather source. Runs after every optimizer step."""
+        if not optimizer_amax:
+            for h in getattr(self, "expert_amax", ()):
+                h.fresh = False  # weights changed by something other than the fused AdamW: recompute in forward
         if not self.f8_units:
             return
         from ..ops._ext import use_native
@@ -1428,6 +1454,16 @@ class FullyShardedModule(nn.Module):
             return super().__getattr__(name)
         except AttributeError:
             return getattr(self.module, name)
+
+
+class _ExpertAmax:
+    """Per-expert amax [E] of an fp8 MoE weight stack, written by the fused AdamW (ops/multi_tensor.py); `fresh` while
+    the stack holds the values that launch wrote."""
+
+    __slots__ = ("amax", "seg", "fresh")
+
+    def __init__(self, amax: torch.Tensor, seg: int):
+        self.amax, self.seg, self.fresh = amax, seg, False
 
 
 class _WgradSlot:

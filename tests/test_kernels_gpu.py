@@ -1226,6 +1226,78 @@ def test_fsdp_fp8_amax_from_fused_adamw(one_rank_rccl, monkeypatch, force):
     assert res[True][3] < res[False][3], (res[True][3], res[False][3])
 
 
+@pytest.mark.parametrize("E,M,N", [(8, 512, 384), (3, 200, 136)])
+def test_fp8_cast_batched_into_matches_segment_cast_and_transpose(E, M, N):
+    """The MoE expert-weight quantiser: one launch casting each [M, N] matrix of a stack with its own amax and writing
+    its transpose too, bit-identical to the segment cast + batched byte transpose it replaces (edge tiles included)."""
+    from accelerate_hpc_test_amd.ops._ext import ext
+
+    torch.manual_seed(0)
+    w = torch.randn(E, M, N, device=DEV, dtype=torch.bfloat16) * torch.arange(1, E + 1, device=DEV).view(E, 1, 1)
+    flat = w.view(-1)
+    lo = torch.arange(E, device=DEV, dtype=torch.long) * (M * N)
+    amax = torch.empty(E, device=DEV)
+    ext().fp8_segment_amax(flat, lo, lo + M * N, amax, M * N)
+    ref = torch.empty(E * M * N, device=DEV, dtype=torch.float8_e4m3fn)
+    ext().fp8_segment_cast(flat, lo, lo + M * N, amax, 448.0, ref, M * N)
+    ref = ref.view(E, M, N)
+    y = torch.empty(E, M, N, device=DEV, dtype=torch.float8_e4m3fn)
+    yt = torch.empty(E, N, M, device=DEV, dtype=torch.float8_e4m3fn)
+    ext().fp8_cast_batched_into(w, amax, 448.0, y, yt)
+    assert torch.equal(y.view(torch.uint8), ref.view(torch.uint8))
+    assert torch.equal(yt.view(torch.uint8), ref.view(torch.uint8).transpose(1, 2).contiguous())
+
+
+def test_moe_fp8_expert_amax_from_fused_adamw(one_rank_rccl, monkeypatch):
+    """FSDP world size 1, fp8 MoE experts: the fused AdamW max-reduces every expert matrix of the stacks it updates
+    into a per-expert amax (one kernel row per expert) and the expert forward uses it instead of its own amax pass:
+    identical losses and weights to the amax-pass path, with fewer amax launches."""
+    from accelerate_hpc_test_amd import Accelerator, FullyShardedDataParallelPlugin
+    from accelerate_hpc_test_amd.models.mixtral import MIXTRAL_PRESETS, build_mixtral
+    from accelerate_hpc_test_amd.ops import multi_tensor
+    from accelerate_hpc_test_amd.ops._ext import ext
+    from accelerate_hpc_test_amd.state import AcceleratorState, GradientState
+
+    e = ext()
+    real = e.fp8_segment_amax
+    res = {}
+    for fused in (False, True):
+        calls = [0]
+
+        def counting(*a, _real=real, _calls=calls):
+            _calls[0] += 1
+            return _real(*a)
+
+        monkeypatch.setattr(multi_tensor, "_AMAX_IN_ADAM", fused)
+        monkeypatch.setattr(e, "fp8_segment_amax", counting)
+        AcceleratorState._reset_state(True)
+        GradientState._reset_state()
+        plugin = FullyShardedDataParallelPlugin(fsdp_version=2, auto_wrap_policy="transformer_based_wrap",
+                                                transformer_cls_names_to_wrap=["MixtralDecoderLayer"])
+        acc = Accelerator(mixed_precision="fp8", fsdp_plugin=plugin)
+        model = build_mixtral("mixtral-tiny", meta=True)
+        opt = torch.optim.AdamW(model.parameters(), lr=1e-3)
+        model, opt = acc.prepare(model, opt)
+        holders = model.engine.expert_amax
+        assert len(holders) == 2 * MIXTRAL_PRESETS["mixtral-tiny"].num_hidden_layers
+        ids = torch.randint(0, 512, (2, 512), generator=torch.Generator().manual_seed(3)).to(DEV)
+        losses = []
+        for _ in range(3):
+            out = model(ids, labels=ids)
+            acc.backward(out.loss)
+            opt.step()
+            opt.zero_grad()
+            losses.append(out.loss.item())
+        torch.cuda.synchronize()
+        assert all(h.fresh == fused for h in holders)
+        res[fused] = (losses, acc.get_state_dict(model), calls[0])
+    monkeypatch.setattr(e, "fp8_segment_amax", real)
+    assert res[False][0] == res[True][0], (res[False][0], res[True][0])
+    for n, t in res[False][1].items():
+        assert torch.equal(t, res[True][1][n]), n
+    assert res[True][2] < res[False][2], (res[True][2], res[False][2])
+
+
 def test_fp8_segment_kernels_and_byte_transpose():
     from accelerate_hpc_test_amd.ops._ext import ext
 
