@@ -85,6 +85,7 @@ for step in "$@"; do
     bench20_ovl) run bench20_ovl 600 python bench.py --gpus 1 --steps 20 --warmup 5 --optimizer-overlap on ;;
     bench20_fp8_ovl) run bench20_fp8_ovl 600 python bench.py --gpus 1 --steps 20 --warmup 5 --precision fp8 --optimizer-overlap on ;;
     bench20_fp8_amaxoff) ACCELERATE_FP8_AMAX_IN_ADAM=0 run bench20_fp8_amaxoff 600 python bench.py --gpus 1 --steps 20 --warmup 5 --precision fp8 ;;
+    bench20_fp8_pret) ACCELERATE_FP8_PRETRANSPOSE=1 run bench20_fp8_pret 600 python bench.py --gpus 1 --steps 20 --warmup 5 --precision fp8 ;;
     bench20_dgradbl) ACCELERATE_DGRAD_BLASLT=1 run bench20_dgradbl 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench20_k128) ACCELERATE_ATTN_FWD_KEYS=128 run bench20_k128 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     attn_long) run attn_long 300 python tools/bench_attn.py --S 32768 --iters 3 ;;
