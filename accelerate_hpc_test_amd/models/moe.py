@@ -210,6 +210,31 @@ def _t(x):
     return x.t().contiguous()
 
 
+# bf16 expert dgrad on the per-expert library path straight from the stored stack (NN layout) instead of through a
+# transposed copy of both stacks per backward: an expert sees ~1/E of the tokens, so re-laying out its whole weight
+# costs more than the layout gains (ACCELERATE_MOE_DGRAD_NN=0: the transposed copy, as the grouped kernel needs).
+_MOE_DGRAD_NN = os.environ.get("ACCELERATE_MOE_DGRAD_NN", "1") != "0"
+
+
+def _dgrad_mm(a, w, seg, out):
+    """out[r] = a[r] . w[e] for the rows r of expert e's segment (w [E, N, K] as stored: the dgrad of a mode-1
+    product). The per-expert hipBLASLt path (host segment bounds attached) runs it on w itself; otherwise the grouped
+    kernel takes the K-contiguous copy `_bt(w)`."""
+    bounds = getattr(seg, "_acc_bounds", None)
+    if (_MOE_DGRAD_NN and bounds is not None and _MOE_GEMM == "blaslt" and a.is_cuda and use_native(a)
+            and a.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and out.dtype == torch.bfloat16
+            and a.is_contiguous() and w.is_contiguous() and out.is_contiguous()):
+        E = len(bounds) - 1
+        for e in range(E):
+            lo, hi = bounds[e], bounds[e + 1]
+            if hi > lo:
+                torch.mm(a[lo:hi], w[e], out=out[lo:hi])
+        if bounds[E] < out.shape[0]:
+            out[bounds[E] :].zero_()  # rows past the last segment are defined (zero), as in grouped_mm
+        return out
+    return grouped_mm(a, _bt(w), seg, 1, out)
+
+
 def _bt(w):
     """[E, N, K] -> [E, K, N] (expert weight stacks; bf16 or fp8)."""
     if w.is_cuda and use_native(w) and (w.element_size() == 1 or (w.shape[1] % 64 == 0 and w.shape[2] % 64 == 0)):
@@ -270,11 +295,11 @@ class _GroupedExpertsFn(torch.autograd.Function):
             R, H = x.shape
             I = w_down.shape[2]
             a = _swiglu_fwd(h)
-            da = grouped_mm(dy, _bt(w_down), seg, 1, x.new_empty(R, I))
+            da = _dgrad_mm(dy, w_down, seg, x.new_empty(R, I))
             grouped_mm(_t(dy), _t(a), seg, 2, g_d, accumulate=acc_d)
             dh = _swiglu_bwd(h, da)
             grouped_mm(_t(dh), _t(x), seg, 2, g_gu, accumulate=acc_gu)
-            dx = grouped_mm(dh, _bt(w_gu), seg, 1, x.new_empty(R, H))
+            dx = _dgrad_mm(dh, w_gu, seg, x.new_empty(R, H))
         ctx.st = None
         grads = []
         for dest, _, slot in dsts:
