@@ -10,13 +10,15 @@ int64_t acc_dbg_take_norm_act();
 int64_t acc_dbg_take_xent_optim();
 int64_t acc_dbg_take_small_allreduce();
 int64_t acc_dbg_take_comm_pack();
+int64_t acc_dbg_take_moe_route();
 bool debug_selftest(torch::Tensor out, int64_t overshoot);
 
 // (check id << 32 | source line) of the first failed device check since the last call, 0 if none; clears it.
 static int64_t debug_status() {
   int64_t first = 0;
   for (auto fn : {acc_dbg_take_flash_attn, acc_dbg_take_fp8, acc_dbg_take_grouped_gemm, acc_dbg_take_norm_act,
-                  acc_dbg_take_xent_optim, acc_dbg_take_small_allreduce, acc_dbg_take_comm_pack}) {
+                  acc_dbg_take_xent_optim, acc_dbg_take_small_allreduce, acc_dbg_take_comm_pack,
+                  acc_dbg_take_moe_route}) {
     const int64_t w = fn();
     if (first == 0) first = w;
   }
@@ -60,6 +62,9 @@ std::vector<torch::Tensor> fp8_cast(torch::Tensor x, torch::Tensor t, double qma
 void fp8_cast_into(torch::Tensor x, torch::Tensor t, double qmax, bool from_amax, bool e5m2, torch::Tensor y,
                    c10::optional<torch::Tensor> yt);
 void fp8_cast_batched_into(torch::Tensor x, torch::Tensor amax, double qmax, torch::Tensor y, torch::Tensor yt);
+void moe_scatter_rows(torch::Tensor src, torch::Tensor pos, c10::optional<torch::Tensor> w, torch::Tensor dst,
+                      c10::optional<torch::Tensor> y, c10::optional<torch::Tensor> dotw, int64_t K);
+torch::Tensor moe_gather_rows(torch::Tensor src, torch::Tensor pos, c10::optional<torch::Tensor> w, int64_t T, int64_t K);
 torch::Tensor fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor a_scale_inv, torch::Tensor b_scale_inv,
                        double smul, bool a_e5m2, bool b_e5m2, c10::optional<torch::Tensor> bias, bool out_fp32,
                        c10::optional<torch::Tensor> out, bool accumulate);
@@ -125,6 +130,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fp8_cast", &fp8_cast);
   m.def("fp8_cast_into", &fp8_cast_into);
   m.def("fp8_cast_batched_into", &fp8_cast_batched_into);
+  m.def("moe_scatter_rows", &moe_scatter_rows);
+  m.def("moe_gather_rows", &moe_gather_rows);
   m.def("fp8_gemm", &fp8_gemm, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("a_scale_inv"), pybind11::arg("b_scale_inv"),
         pybind11::arg("smul"), pybind11::arg("a_e5m2"), pybind11::arg("b_e5m2"), pybind11::arg("bias"), pybind11::arg("out_fp32"),
         pybind11::arg("out") = pybind11::none(), pybind11::arg("accumulate") = false);

@@ -242,6 +242,57 @@ def _bt(w):
     return w.transpose(1, 2).contiguous()
 
 
+# Token dispatch / combine through the HIP row kernels (csrc/kernels/moe_route.hip) instead of torch index_copy /
+# index_select / bf16 index_add (ACCELERATE_MOE_ROUTE_HIP=0 restores those).
+_MOE_ROUTE_HIP = os.environ.get("ACCELERATE_MOE_ROUTE_HIP", "1") != "0"
+
+
+def _route_native_ok(t: torch.Tensor, K: int) -> bool:
+    return (_MOE_ROUTE_HIP and t.is_cuda and use_native(t) and t.dtype == torch.bfloat16 and t.dim() == 2
+            and t.shape[1] % 8 == 0 and 1 <= K <= 8)
+
+
+class _RouteDispatch(torch.autograd.Function):
+    """x_routed [R, H]: row pos[t*K + k] = token t, pad rows zero (each slot owns a unique row). Backward: the token
+    gradient is the sum of its K rows (a gather, no atomics)."""
+
+    @staticmethod
+    def forward(ctx, t, pos, R, K):
+        out = t.new_zeros(R, t.shape[1])
+        ext().moe_scatter_rows(t.contiguous(), pos, None, out, None, None, K)
+        ctx.save_for_backward(pos)
+        ctx.T, ctx.K = t.shape[0], K
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (pos,) = ctx.saved_tensors
+        return ext().moe_gather_rows(g.contiguous(), pos, None, ctx.T, ctx.K), None, None, None
+
+
+class _RouteCombine(torch.autograd.Function):
+    """out[t] = sum_k w[t*K + k] * y[pos[t*K + k]] (fp32 accumulation). Backward: dy rows = w * dout (pad rows zero) and
+    dw = <dout[t], y[pos]>, one kernel."""
+
+    @staticmethod
+    def forward(ctx, y, pos, w, K):
+        y = y.contiguous()
+        wf = w.float().contiguous()
+        T = pos.numel() // K
+        out = ext().moe_gather_rows(y, pos, wf, T, K)
+        ctx.save_for_backward(y, pos, wf)
+        ctx.K, ctx.w_dtype = K, w.dtype
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        y, pos, wf = ctx.saved_tensors
+        dy = torch.zeros_like(y)
+        dw = torch.empty_like(wf)
+        ext().moe_scatter_rows(g.contiguous(), pos, wf, dy, y, dw, ctx.K)
+        return dy, None, dw.to(ctx.w_dtype), None
+
+
 class _GroupedExpertsFn(torch.autograd.Function):
     """y = down_e(swiglu(gate_up_e(x))) for the rows of each expert segment of the routed buffer `x` [R, H].
 
@@ -458,6 +509,12 @@ class MoELayer(nn.Module):
         if self.ep_group is None or comm.group_size(self.ep_group) == 1:
             order, dest, seg, R = expert_layout(flat_e, self.num_experts)
             _attach_bounds(seg)
+            if _route_native_ok(t, self.top_k):
+                pos = torch.empty_like(dest)
+                pos[order] = dest  # routed row of slot t*K + k
+                x_routed = _RouteDispatch.apply(t, pos, R, self.top_k)
+                out = _RouteCombine.apply(self.experts(x_routed, seg), pos, w.reshape(-1), self.top_k)
+                return out.view(shape)
             src_tok = order // self.top_k
             w_sorted = w.reshape(-1)[order]
             x_routed = t.new_zeros(R, t.shape[1]).index_copy(0, dest, t.index_select(0, src_tok))

@@ -64,6 +64,7 @@ for step in "$@"; do
     mix8_bf16) run mix8_bf16 600 python bench.py --model mixtral-8x7b-8l --steps 5 --warmup 2 --verbose $BENCH_ARGS ;;
     mix8_fp8) run mix8_fp8 600 python bench.py --model mixtral-8x7b-8l --steps 5 --warmup 2 --precision fp8 --verbose $BENCH_ARGS ;;
     mix8_bf16_nonn) ACCELERATE_MOE_DGRAD_NN=0 run mix8_bf16_nonn 600 python bench.py --model mixtral-8x7b-8l --steps 5 --warmup 2 --verbose $BENCH_ARGS ;;
+    mix8_fp8_noroute) ACCELERATE_MOE_ROUTE_HIP=0 run mix8_fp8_noroute 600 python bench.py --model mixtral-8x7b-8l --steps 5 --warmup 2 --precision fp8 --verbose $BENCH_ARGS ;;
     mix8_fp8_nocastt) ACCELERATE_MOE_FP8_CAST_T=0 run mix8_fp8_nocastt 600 python bench.py --model mixtral-8x7b-8l --steps 5 --warmup 2 --precision fp8 --verbose $BENCH_ARGS ;;
     mix8_fp8_blaslt) ACCELERATE_MOE_FP8_BLASLT=1 run mix8_fp8_blaslt 600 python bench.py --model mixtral-8x7b-8l --steps 5 --warmup 2 --precision fp8 --verbose $BENCH_ARGS ;;
     moegemm) run moegemm 300 python tools/bench_moe_gemm.py ;;
