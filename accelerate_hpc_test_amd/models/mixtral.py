@@ -79,7 +79,9 @@ class MixtralDecoderLayer(nn.Module):
     def forward(self, hidden, residual, cos, sin, position_ids=None):
         x, residual = self.input_layernorm(hidden, residual)
         hidden = self.self_attn(x, cos, sin, position_ids)
-        x, residual = self.post_attention_layernorm(hidden, residual)
+        rec = self.block_sparse_moe.experts.fp8_recipe
+        # per-tensor fp8 experts: the norm also produces the abs-max of the routed tokens (no amax pass over them)
+        x, residual = self.post_attention_layernorm(hidden, residual, amax=rec is not None and not rec.mx)
         return self.block_sparse_moe(x), residual
 
 

@@ -389,18 +389,29 @@ def _expert_weight_fp8(w, recipe, key):
     return w8, _bt(w8), amax
 
 
+def _swiglu_amax(h, da=None):
+    """SwiGLU forward (da None) or backward with the abs-max of its output from the same kernel (the amax a consuming
+    fp8 cast needs), or (output, None) off the HIP path."""
+    if use_native(h) and h.dtype == torch.bfloat16 and (h.shape[-1] // 2) % 8 == 0:
+        am = torch.empty(1, dtype=torch.float32, device=h.device)
+        if da is None:
+            return ext().swiglu_fwd(h.contiguous(), am), am
+        return ext().swiglu_bwd(h.contiguous(), da.contiguous(), am), am
+    return (_swiglu_fwd(h) if da is None else _swiglu_bwd(h, da)), None
+
+
 def _fp8_fwd(x, w_gu, w_down, seg, recipe):
-    from ..ops.fp8 import E4M3_MAX, cast
+    from ..ops.fp8 import E4M3_MAX, cast, producer_amax
 
     R, H = x.shape
-    sx = recipe.scale("x", x, E4M3_MAX)
+    sx = recipe.scale("x", x, E4M3_MAX, producer_amax(x))  # tagged by the dispatch when the norm produced it
     x8, x8t = cast(x, sx, False, transpose=True)
     gu8, gu8t, a_gu = _expert_weight_fp8(w_gu, recipe, "wgu")
     d8, d8t, a_d = _expert_weight_fp8(w_down, recipe, "wd")
     q2 = 1.0 / (E4M3_MAX * sx.qmax)
     h = grouped_mm(x8, gu8, seg, 1, x.new_empty(R, w_gu.shape[1]), sx.amax, a_gu, q2)
-    a = _swiglu_fwd(h)
-    sa = recipe.scale("a", a, E4M3_MAX)
+    a, am_a = _swiglu_amax(h)
+    sa = recipe.scale("a", a, E4M3_MAX, am_a)
     a8, a8t = cast(a, sa, False, transpose=True)
     y = grouped_mm(a8, d8, seg, 1, x.new_empty(R, H), sa.amax, a_d, 1.0 / (E4M3_MAX * sa.qmax))
     return y, (h, x8t, a8t, gu8t, d8t, sx, sa, a_gu, a_d)
@@ -419,8 +430,8 @@ def _fp8_bwd(dy, x, w_gu, w_down, seg, st, recipe, gu_out, d_out):
     dy8, dy8t = cast(dy, sg, e5, transpose=True)
     da = grouped_mm(dy8, d8t, seg, 1, x.new_empty(R, I), sg.amax, a_d, 1.0 / (sg.qmax * E4M3_MAX))
     grouped_mm(dy8t, a8t, seg, 2, d_out[0], sg.amax, sa.amax, 1.0 / (sg.qmax * sa.qmax), accumulate=d_out[1])
-    dh = _swiglu_bwd(h, da)
-    sh = recipe.scale("gh", dh, gmax)
+    dh, am_dh = _swiglu_amax(h, da)
+    sh = recipe.scale("gh", dh, gmax, am_dh)
     dh8, dh8t = cast(dh, sh, e5, transpose=True)
     grouped_mm(dh8t, x8t, seg, 2, gu_out[0], sh.amax, sx.amax, 1.0 / (sh.qmax * sx.qmax), accumulate=gu_out[1])
     return grouped_mm(dh8, gu8t, seg, 1, x.new_empty(R, H), sh.amax, a_gu, 1.0 / (sh.qmax * E4M3_MAX))
@@ -510,9 +521,14 @@ class MoELayer(nn.Module):
             order, dest, seg, R = expert_layout(flat_e, self.num_experts)
             _attach_bounds(seg)
             if _route_native_ok(t, self.top_k):
+                from ..ops.fp8 import producer_amax, tag_amax
+
                 pos = torch.empty_like(dest)
                 pos[order] = dest  # routed row of slot t*K + k
                 x_routed = _RouteDispatch.apply(t, pos, R, self.top_k)
+                am = producer_amax(x)
+                if am is not None:  # every token lands in the routed buffer, the pad rows are zero: same abs-max
+                    tag_amax(x_routed, am)
                 out = _RouteCombine.apply(self.experts(x_routed, seg), pos, w.reshape(-1), self.top_k)
                 return out.view(shape)
             src_tok = order // self.top_k

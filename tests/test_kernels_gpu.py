@@ -467,6 +467,41 @@ def test_grouped_gemm_kernel_both_modes(dt):
             assert _rel(dw[e], r) < 1e-3, (e, _rel(dw[e], r))
 
 
+def test_moe_fp8_producer_amax_is_bit_exact(monkeypatch):
+    """fp8 MoE layer: the routed tokens' abs-max taken from the RMSNorm that produced them (tag carried through the
+    dispatch), the SwiGLU output's and its input gradient's from the SwiGLU kernels, against separate amax passes:
+    bit-identical output and gradients."""
+    from accelerate_hpc_test_amd.models import moe
+    from accelerate_hpc_test_amd.ops import fp8
+    from accelerate_hpc_test_amd.ops.fused import rms_norm
+
+    torch.manual_seed(0)
+    layer = moe.MoELayer(256, 512, 4, 2).to(DEV, torch.bfloat16)
+    with torch.no_grad():
+        layer.gate.weight.normal_(0, 0.2)
+        layer.experts.w_gate_up.normal_(0, 0.05)
+        layer.experts.w_down.normal_(0, 0.05)
+    layer.experts.fp8_recipe = fp8.Fp8Recipe()
+    nw = torch.ones(256, device=DEV, dtype=torch.bfloat16)
+    h0 = torch.randn(2, 512, 256, device=DEV, dtype=torch.bfloat16)
+    g = torch.randn(2, 512, 256, device=DEV, dtype=torch.bfloat16)
+    real_swiglu_amax = moe._swiglu_amax
+    res = {}
+    for hints in (True, False):
+        if not hints:
+            monkeypatch.setattr(fp8, "producer_amax", lambda t: None)
+            monkeypatch.setattr(moe, "_swiglu_amax", lambda h, da=None: (real_swiglu_amax(h, da)[0], None))
+        layer.zero_grad(set_to_none=True)
+        hin = h0.clone().requires_grad_(True)
+        x, _ = rms_norm(hin, nw, 1e-5, amax=True)
+        assert (fp8.producer_amax(x) is not None) == hints
+        y = layer(x)
+        y.backward(g)
+        res[hints] = [y.detach(), hin.grad, layer.experts.w_gate_up.grad, layer.experts.w_down.grad, layer.gate.weight.grad]
+    for name, a, b in zip(("y", "dx", "dw_gu", "dw_down", "dgate"), res[True], res[False]):
+        assert torch.equal(a, b), name
+
+
 @pytest.mark.parametrize("top_k,norm", [(1, False), (2, True), (2, False)])
 def test_moe_route_kernels_match_torch_index_ops(top_k, norm, monkeypatch):
     """MoELayer token dispatch / combine through the HIP row kernels (csrc/kernels/moe_route.hip: unique-row scatter,
