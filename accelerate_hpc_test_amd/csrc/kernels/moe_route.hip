@@ -9,6 +9,7 @@
 // fp32 accumulation, one bf16 rounding per output. One wave per row (scatter) / token (gather), 16-B accesses.
 // Replaces torch index_copy / index_select / bf16 index_add (an atomic bf16 read-modify-write per element, ~0.6 TB/s
 // on the Mixtral combine) in the non-expert-parallel path.
+#include <hip/hip_runtime.h>
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 
