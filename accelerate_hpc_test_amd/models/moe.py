@@ -537,6 +537,13 @@ class MoELayer(nn.Module):
             y_sorted = self.experts(x_routed, seg).index_select(0, dest)
         else:
             order = torch.argsort(flat_e, stable=True)
+            if _route_native_ok(t, self.top_k):
+                # expert-sorted rows, one per slot: the same atomic-free dispatch / combine with R = T * K (no pads)
+                pos = torch.empty_like(order)
+                pos[order] = torch.arange(order.numel(), device=order.device)
+                x_sorted = _RouteDispatch.apply(t, pos, order.numel(), self.top_k)
+                y_sorted = self._ep_experts(x_sorted, flat_e[order])
+                return _RouteCombine.apply(y_sorted, pos, w.reshape(-1), self.top_k).view(shape)
             src_tok = order // self.top_k
             w_sorted = w.reshape(-1)[order]
             y_sorted = self._ep_experts(t.index_select(0, src_tok), flat_e[order])

@@ -34,7 +34,7 @@ def _batches(steps, vocab):
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--mode", choices=["fsdp", "fsdp_fp8", "ddp", "hsdp", "cp_allgather", "cp_alltoall"], required=True)
+    p.add_argument("--mode", choices=["fsdp", "fsdp_fp8", "ddp", "hsdp", "cp_allgather", "cp_alltoall", "ep"], required=True)
     p.add_argument("--seq", type=int, default=16384)
     p.add_argument("--heads", default="8,2", help="cp modes: query,kv heads")
     p.add_argument("--no-ref", action="store_true", help="cp modes: skip the fp32 reference (long sequences)")
@@ -46,6 +46,8 @@ def main():
 
     if args.mode.startswith("cp_"):
         return run_context_parallel(args)
+    if args.mode == "ep":
+        return run_expert_parallel(args)
     from accelerate_hpc_test_amd import Accelerator, FullyShardedDataParallelPlugin
     from accelerate_hpc_test_amd.models.llama import LLAMA_PRESETS, LlamaForCausalLM
     from accelerate_hpc_test_amd.parallel import small_allreduce
@@ -218,6 +220,74 @@ def run_context_parallel(args):
         res = {"world": W, "mode": args.mode, "seq": S, "rel_err": rel, "peak_transient_bytes": peaks}
         os.makedirs(args.out, exist_ok=True)
         with open(os.path.join(args.out, f"result_{args.mode}_W{W}.json"), "w") as f:
+            json.dump(res, f)
+        print(json.dumps(res), flush=True)
+    if W > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def run_expert_parallel(args):
+    """Expert parallelism (models/moe.py `shard_experts`): W ranks each route their own token slice through an 8-expert
+    top-2 MoELayer whose experts are split W ways (variable all-to-all dispatch / combine, local grouped expert GEMMs
+    on the HIP kernels); rank 0 compares the gathered output, the summed router gradient and every expert's gradient
+    (x W: the EP hook averages expert grads over the group) with ONE process running the unsharded layer on all the
+    tokens."""
+    import torch.distributed as dist
+
+    from accelerate_hpc_test_amd.models.moe import MoELayer
+
+    W = int(os.environ.get("WORLD_SIZE", "1"))
+    torch.cuda.set_device(0)
+    if W > 1:
+        dist.init_process_group("gloo")
+    r = dist.get_rank() if W > 1 else 0
+    E, H, I, T = 8, 256, 512, 512  # T tokens per rank
+    torch.manual_seed(0)
+    ref = MoELayer(H, I, E, 2).to("cuda", torch.bfloat16)
+    with torch.no_grad():
+        ref.gate.weight.normal_(0, 0.2)
+        ref.experts.w_gate_up.normal_(0, 0.05)
+        ref.experts.w_down.normal_(0, 0.05)
+    g = torch.Generator().manual_seed(5)
+    X = torch.randn(W * T, H, generator=g).to("cuda", torch.bfloat16)
+    DY = torch.randn(W * T, H, generator=g).to("cuda", torch.bfloat16)
+    layer = MoELayer(H, I, E, 2).to("cuda", torch.bfloat16)
+    layer.load_state_dict(ref.state_dict())
+    if W > 1:
+        layer.shard_experts(dist.group.WORLD)
+    x = X[r * T : (r + 1) * T].clone().requires_grad_(True)
+    y = layer(x)
+    y.backward(DY[r * T : (r + 1) * T])
+    torch.cuda.synchronize()
+
+    def gather_rows(t):
+        if W == 1:
+            return t.detach()
+        parts = [torch.empty_like(t) for _ in range(W)]
+        dist.all_gather(parts, t.detach().contiguous())
+        return torch.cat(parts)
+
+    ys, dxs = gather_rows(y), gather_rows(x.grad)
+    dgate = layer.gate.weight.grad.float().clone()
+    if W > 1:
+        dist.all_reduce(dgate)
+    # expert grads: this rank holds experts [r E / W, (r + 1) E / W), averaged 1 / W by the EP hook
+    ex = {n: gather_rows(getattr(layer.experts, n).grad.float() * W) for n in ("w_gate_up", "w_down")}
+    if r == 0:
+        xr = X.clone().requires_grad_(True)
+        yr = ref(xr)
+        yr.backward(DY)
+
+        def rel(a, b):
+            return ((a.float() - b.float()).norm() / b.float().norm()).item()
+
+        res = {"world": W, "mode": "ep", "rel_err": {
+            "y": rel(ys, yr), "dx": rel(dxs, xr.grad), "dgate": rel(dgate, ref.gate.weight.grad),
+            "dw_gate_up": rel(ex["w_gate_up"], ref.experts.w_gate_up.grad),
+            "dw_down": rel(ex["w_down"], ref.experts.w_down.grad)}}
+        os.makedirs(args.out, exist_ok=True)
+        with open(os.path.join(args.out, f"result_ep_W{W}.json"), "w") as f:
             json.dump(res, f)
         print(json.dumps(res), flush=True)
     if W > 1:

@@ -112,3 +112,24 @@ def test_context_parallel_ring_attention_matches_full(strategy, world, outdir):
     assert res["rel_err"]["o"] < 2e-2, res
     for n in ("dq", "dk", "dv"):
         assert res["rel_err"][n] < 3e-2, res
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_expert_parallel_moe_matches_single_process(world, outdir):
+    """Expert parallelism with HIP tensors: W processes sharing cuda:0 over gloo, experts split W ways (variable
+    all-to-all dispatch / combine, grouped expert GEMMs), against one process running the whole batch unsharded:
+    output, dx, router and expert gradients (test_utils/scripts/test_gpu_ranks.py `run_expert_parallel`)."""
+    from accelerate_hpc_test_amd.utils.other import get_free_port
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(PYTHONPATH=REPO, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(get_free_port()), SCRIPT, "--mode", "ep", "--out",
+           str(outdir)]
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-5000:]
+    with open(os.path.join(outdir, f"result_ep_W{world}.json")) as f:
+        res = json.load(f)
+    print(f"[ep W={world}] rel err {res['rel_err']}")
+    for n, e in res["rel_err"].items():
+        assert e < 2e-2, (n, res)
