@@ -1017,6 +1017,9 @@ class Accelerator:
                 return m.clip_grad_norm_(max_norm, norm_type)
         self.unscale_gradients()
         grads_params = [p for p in parameters if p.grad is not None]
+        tp_sharded = [p for p in grads_params if getattr(getattr(p, "_tp_spec", None), "size", 1) > 1]
+        if tp_sharded and float(norm_type) == 2.0:
+            return self._clip_grad_norm_tp(grads_params, tp_sharded, float(max_norm))
         if grads_params and grads_params[0].grad.is_cuda and float(norm_type) == 2.0:
             from .ops.multi_tensor import clip_grads_by_total_sq, grad_sq_norm
 
@@ -1024,6 +1027,41 @@ class Accelerator:
             clip_grads_by_total_sq(grads_params, total, float(max_norm))
             return total.sqrt().reshape(())
         return torch.nn.utils.clip_grad_norm_(parameters, max_norm, norm_type=norm_type)
+
+    @staticmethod
+    def _clip_grad_norm_tp(grads_params, sharded, max_norm):
+        """Tensor parallel: each rank holds 1/tp of a sharded parameter's gradient, so those squares are summed over
+        the tp group, while replicated parameters (norms, biases of rowwise layers, ...) hold the whole gradient on
+        every rank and count once. (The plain local norm under-counts the sharded part by 1/tp.)"""
+        import torch.distributed as dist
+
+        group = sharded[0]._tp_spec.group
+        ids = {id(p) for p in sharded}
+        rest = [p for p in grads_params if id(p) not in ids]
+        dev = grads_params[0].grad.device
+        native = grads_params[0].grad.is_cuda
+
+        def sq(ps):
+            if not ps:
+                return torch.zeros(1, dtype=torch.float32, device=dev)
+            if native:
+                from .ops.multi_tensor import grad_sq_norm
+
+                return grad_sq_norm(ps)
+            return sum(p.grad.detach().float().pow(2).sum() for p in ps).reshape(1)
+
+        total = sq(sharded)
+        dist.all_reduce(total, group=group)
+        total = total + sq(rest)
+        if native:
+            from .ops.multi_tensor import clip_grads_by_total_sq
+
+            clip_grads_by_total_sq(grads_params, total, max_norm)
+        else:
+            coef = (max_norm / (total.sqrt() + 1e-6)).clamp(max=1.0)
+            for p in grads_params:
+                p.grad.mul_(coef.to(p.grad.dtype))
+        return total.sqrt().reshape(())
 
     def clip_grad_value_(self, parameters, clip_value):
         if self.distributed_type in (DistributedType.FSDP,):

@@ -292,10 +292,15 @@ def check_tp_matches_single(sequence_parallel: bool = False, dp_shard: int = 1, 
         local = ids[dp_rank * bs : (dp_rank + 1) * bs]
         out = model(local, labels=local)
         acc.backward(out.loss)
+        # the global gradient norm: tp-sharded squares summed over the group, replicated ones counted once
+        gn = acc.clip_grad_norm_(model.parameters(), 1e9)
         opt.step()
         opt.zero_grad()
         ref = base(ids, labels=ids)
         ref.loss.backward()
+        if dp_shard == 1:
+            gn_ref = torch.nn.utils.clip_grad_norm_(base.parameters(), 1e9)
+            assert torch.allclose(gn.float(), gn_ref.float(), rtol=1e-4), (gn, gn_ref)
         base_opt.step()
         base_opt.zero_grad()
         lg = acc.reduce(out.loss.detach().reshape(1), reduction="mean")

@@ -34,7 +34,7 @@ def _batches(steps, vocab):
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--mode", choices=["fsdp", "fsdp_fp8", "ddp", "hsdp", "cp_allgather", "cp_alltoall", "ep"], required=True)
+    p.add_argument("--mode", choices=["fsdp", "fsdp_fp8", "ddp", "hsdp", "tp", "cp_allgather", "cp_alltoall", "ep"], required=True)
     p.add_argument("--seq", type=int, default=16384)
     p.add_argument("--heads", default="8,2", help="cp modes: query,kv heads")
     p.add_argument("--no-ref", action="store_true", help="cp modes: skip the fp32 reference (long sequences)")
@@ -61,6 +61,13 @@ def main():
         acc = Accelerator(mixed_precision="bf16", kwargs_handlers=handlers, cpu=args.cpu)
         torch.manual_seed(0)
         model = LlamaForCausalLM(cfg).to(acc.device)
+    elif args.mode == "tp":  # Megatron column / row parallel over W ranks, every rank on the whole batch
+        from accelerate_hpc_test_amd import ParallelismConfig
+
+        acc = Accelerator(mixed_precision="bf16", kwargs_handlers=handlers, cpu=args.cpu,
+                          parallelism_config=ParallelismConfig(tp_size=W) if W > 1 else None)
+        torch.manual_seed(0)
+        model = LlamaForCausalLM(cfg).to(acc.device)
     else:
         plugin = FullyShardedDataParallelPlugin(fsdp_version=2, auto_wrap_policy="transformer_based_wrap",
                                                 transformer_cls_names_to_wrap=["LlamaDecoderLayer"])
@@ -81,7 +88,9 @@ def main():
     opt = torch.optim.AdamW(model.parameters(), lr=lr, weight_decay=0.01)
     model, opt = acc.prepare(model, opt)
     facts = {"world": W, "mode": args.mode}
-    if args.mode != "ddp":
+    if args.mode == "tp":
+        facts["tp_sharded"] = sum(1 for q in model.parameters() if getattr(q, "_tp_spec", None) is not None)
+    elif args.mode != "ddp":
         eng = model.engine
         facts["sharded"] = bool(eng.sharded)
         # parameters cut by a shard boundary (the case the forced one-GPU mode never has)
@@ -92,10 +101,10 @@ def main():
         facts["ddp_buckets"] = len(getattr(model, "buckets", []))
     if W > 1:
         facts["ipc_allreduce"] = small_allreduce.get(None) is not None
-    bs = GLOBAL_BATCH // W
+    bs = GLOBAL_BATCH if args.mode == "tp" else GLOBAL_BATCH // W
     losses, norms = [], []
     for ids in _batches(args.steps, cfg.vocab_size):
-        local = ids[r * bs : (r + 1) * bs].to(acc.device)
+        local = (ids if args.mode == "tp" else ids[r * bs : (r + 1) * bs]).to(acc.device)
         out = model(local, labels=local)
         acc.backward(out.loss)
         norms.append(float(acc.clip_grad_norm_(model.parameters(), 1e9)))
