@@ -34,7 +34,7 @@ def _batches(steps, vocab):
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--mode", choices=["fsdp", "fsdp_fp8", "ddp", "hsdp", "tp", "cp_allgather", "cp_alltoall", "ep"], required=True)
+    p.add_argument("--mode", choices=["fsdp", "fsdp_fp8", "ddp", "hsdp", "tp", "cp_allgather", "cp_alltoall", "ep", "ulysses"], required=True)
     p.add_argument("--seq", type=int, default=16384)
     p.add_argument("--heads", default="8,2", help="cp modes: query,kv heads")
     p.add_argument("--no-ref", action="store_true", help="cp modes: skip the fp32 reference (long sequences)")
@@ -48,6 +48,8 @@ def main():
         return run_context_parallel(args)
     if args.mode == "ep":
         return run_expert_parallel(args)
+    if args.mode == "ulysses":
+        return run_ulysses(args)
     from accelerate_hpc_test_amd import Accelerator, FullyShardedDataParallelPlugin
     from accelerate_hpc_test_amd.models.llama import LLAMA_PRESETS, LlamaForCausalLM
     from accelerate_hpc_test_amd.parallel import small_allreduce
@@ -297,6 +299,65 @@ def run_expert_parallel(args):
             "dw_down": rel(ex["w_down"], ref.experts.w_down.grad)}}
         os.makedirs(args.out, exist_ok=True)
         with open(os.path.join(args.out, f"result_ep_W{W}.json"), "w") as f:
+            json.dump(res, f)
+        print(json.dumps(res), flush=True)
+    if W > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def run_ulysses(args):
+    """Ulysses sequence parallelism (parallel/ulysses.py): W ranks hold contiguous sequence slices of q / k / v; the
+    all-to-all regroups them by heads, the HIP flash kernels attend over the whole sequence, and the inverse all-to-all
+    returns sequence slices. Rank 0 compares the gathered O / dQ / dK / dV with fp32 causal attention."""
+    import math
+
+    import torch.distributed as dist
+
+    from accelerate_hpc_test_amd.parallel.ulysses import ulysses_attention
+
+    W = int(os.environ.get("WORLD_SIZE", "1"))
+    torch.cuda.set_device(0)
+    if W > 1:
+        dist.init_process_group("gloo")
+    r = dist.get_rank() if W > 1 else 0
+    S, Hq, Hkv, D = 4096, 16, 4, 128
+    g = torch.Generator().manual_seed(13)
+    full = {n: torch.randn(1, S, h, D, generator=g).to(torch.bfloat16).cuda() for n, h in
+            (("q", Hq), ("k", Hkv), ("v", Hkv), ("do", Hq))}
+    L = S // W
+    local = {n: t[:, r * L : (r + 1) * L].clone().requires_grad_(n != "do") for n, t in full.items()}
+    o = ulysses_attention(local["q"], local["k"], local["v"], dist.group.WORLD if W > 1 else None)
+    o.backward(local["do"])
+    torch.cuda.synchronize()
+
+    def gather(t):
+        if W == 1:
+            return t.detach()
+        parts = [torch.empty_like(t) for _ in range(W)]
+        dist.all_gather(parts, t.detach().contiguous())
+        return torch.cat(parts, 1)
+
+    outs = {"o": gather(o), "dq": gather(local["q"].grad), "dk": gather(local["k"].grad), "dv": gather(local["v"].grad)}
+    if r == 0:
+        scale, rep = 1 / math.sqrt(D), Hq // Hkv
+        ref = {"o": torch.zeros(1, S, Hq, D, device="cuda"), "dq": torch.zeros(1, S, Hq, D, device="cuda"),
+               "dk": torch.zeros(1, S, Hkv, D, device="cuda"), "dv": torch.zeros(1, S, Hkv, D, device="cuda")}
+        mask = torch.ones(S, S, device="cuda", dtype=torch.bool).triu(1)
+        for h in range(Hq):  # fp32 reference, one head at a time
+            qh = full["q"][0, :, h].float().requires_grad_()
+            kh = full["k"][0, :, h // rep].float().requires_grad_()
+            vh = full["v"][0, :, h // rep].float().requires_grad_()
+            oh = torch.softmax((qh @ kh.t() * scale).masked_fill(mask, float("-inf")), -1) @ vh
+            oh.backward(full["do"][0, :, h].float())
+            ref["o"][0, :, h] = oh.detach()
+            ref["dq"][0, :, h] = qh.grad
+            ref["dk"][0, :, h // rep] += kh.grad
+            ref["dv"][0, :, h // rep] += vh.grad
+        rel = {n: ((outs[n].float() - ref[n]).norm() / ref[n].norm()).item() for n in outs}
+        res = {"world": W, "mode": "ulysses", "seq": S, "rel_err": rel}
+        os.makedirs(args.out, exist_ok=True)
+        with open(os.path.join(args.out, f"result_ulysses_W{W}.json"), "w") as f:
             json.dump(res, f)
         print(json.dumps(res), flush=True)
     if W > 1:

@@ -137,3 +137,25 @@ def test_expert_parallel_moe_matches_single_process(world, outdir):
     print(f"[ep W={world}] rel err {res['rel_err']}")
     for n, e in res["rel_err"].items():
         assert e < 2e-2, (n, res)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_ulysses_attention_matches_full(world, outdir):
+    """Ulysses sequence parallelism with HIP tensors: W processes sharing cuda:0 over gloo, each with a contiguous
+    4096 / W-token slice, 16 q / 4 kv heads; the head all-to-all, the HIP flash kernels over the whole sequence and the
+    inverse all-to-all against fp32 causal attention (test_utils/scripts/test_gpu_ranks.py `run_ulysses`)."""
+    from accelerate_hpc_test_amd.utils.other import get_free_port
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(PYTHONPATH=REPO, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(get_free_port()), SCRIPT, "--mode", "ulysses", "--out",
+           str(outdir)]
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-5000:]
+    with open(os.path.join(outdir, f"result_ulysses_W{world}.json")) as f:
+        res = json.load(f)
+    print(f"[ulysses W={world}] rel err {res['rel_err']}")
+    assert res["rel_err"]["o"] < 2e-2, res
+    for n in ("dq", "dk", "dv"):
+        assert res["rel_err"][n] < 3e-2, res
