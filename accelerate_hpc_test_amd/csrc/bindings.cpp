@@ -5,6 +5,7 @@
 // device-side check words of the debug build (one per kernel file; release builds return 0), see kernels/common.h
 int64_t acc_dbg_take_flash_attn();
 int64_t acc_dbg_take_fp8();
+int64_t acc_dbg_take_fp8_asm();
 int64_t acc_dbg_take_grouped_gemm();
 int64_t acc_dbg_take_norm_act();
 int64_t acc_dbg_take_xent_optim();
@@ -16,7 +17,7 @@ bool debug_selftest(torch::Tensor out, int64_t overshoot);
 // (check id << 32 | source line) of the first failed device check since the last call, 0 if none; clears it.
 static int64_t debug_status() {
   int64_t first = 0;
-  for (auto fn : {acc_dbg_take_flash_attn, acc_dbg_take_fp8, acc_dbg_take_grouped_gemm, acc_dbg_take_norm_act,
+  for (auto fn : {acc_dbg_take_flash_attn, acc_dbg_take_fp8, acc_dbg_take_fp8_asm, acc_dbg_take_grouped_gemm, acc_dbg_take_norm_act,
                   acc_dbg_take_xent_optim, acc_dbg_take_small_allreduce, acc_dbg_take_comm_pack,
                   acc_dbg_take_moe_route}) {
     const int64_t w = fn();

@@ -1988,10 +1988,14 @@ void fp8_cast_batched_into(torch::Tensor x, torch::Tensor amax, double qmax, tor
 // ping-pong) scaled / unscaled.
 // Shapes a variant cannot tile fall back to the next one that can (v3 -> v2 -> v1).
 constexpr int kFp8GemmDefault = 17;  // v8 unscaled: the fastest HIP variant at all 12 shapes (profiles/r4_gemm_fp8.md)
+// variant 18: the hand-scheduled asm main loop (fp8_gemm_asm.hip)
+bool fp8_gemm_asm_launch(const uint8_t* a, const uint8_t* b, const float* sa, const float* sb, float smul,
+                         const bf16_t* bias, void* c, int M, int N, int K, bool a_e5m2, bool b_e5m2, bool out_f32,
+                         bool accum, int group_m, hipStream_t stream);
 static int g_fp8_gemm_variant = 0;
 static int g_fp8_gemm_group_m = 4;  // v3 tile-row grouping (1 = plain row-major tile order)
 void fp8_gemm_select(int64_t variant, int64_t group_m) {
-  TORCH_CHECK(variant >= 0 && variant <= 17, "fp8_gemm_select: variant 0..17");
+  TORCH_CHECK(variant >= 0 && variant <= 18, "fp8_gemm_select: variant 0..18");
   TORCH_CHECK(group_m >= 0 && group_m <= 64, "fp8_gemm_select: group_m 0..64");
   g_fp8_gemm_variant = (int)variant;
   if (group_m > 0) g_fp8_gemm_group_m = (int)group_m;
@@ -2038,6 +2042,12 @@ torch::Tensor fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor a_scale_i
   }();
   int variant = g_fp8_gemm_variant;
   if (variant == 0) variant = force_v1 ? 1 : (env_w8 ? 3 : kFp8GemmDefault);
+  if (variant == 18) {
+    if (fp8_gemm_asm_launch(ap, bptr, sap, sbp, (float)smul, bp, cp, M, N, K, a_e5m2, b_e5m2, out_fp32, accumulate,
+                            g_fp8_gemm_group_m, stream))
+      return out;
+    variant = 17;
+  }
   if ((variant == 10 || variant == 11) && M % V4_BM == 0 && N % V4_BN == 0 && K % 256 == 0 &&
       (long)V4_BM * K < (1L << 30) && (reinterpret_cast<uintptr_t>(bp) & 7) == 0) {
     const int nwg5 = (M / V4_BM) * (N / V4_BN);

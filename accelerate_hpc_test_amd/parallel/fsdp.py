@@ -1223,18 +1223,57 @@ class FSDPEngine:
                 holder = _GradHolder(unit.grad_shard)
                 flat_params.append(holder)
         total = torch.zeros(1, dtype=torch.float32, device=self.device)
-        if flat_params:
+        tp_group, tp = self._tp_group()
+        if tp > 1:
+            # 2-D FSDP x TP: a TP-sharded parameter's shard holds a disjoint 1/tp of its gradient on each tp rank (its
+            # squares are summed over tp as well as dp_shard), a TP-replicated one the same values on every tp rank
+            # (pre-divided by tp so the tp all-reduce counts it once). Reference: DTensor-aware clip_grad_norm_ over
+            # the whole mesh, /root/reference/src/accelerate/accelerator.py:2943-2953.
+            shard_pieces, rep_pieces = [], []
+            for unit in self.units:
+                if not unit.grad_valid:
+                    continue
+                for info in unit.infos:
+                    if info.local_hi <= info.local_lo:
+                        continue
+                    piece = _GradHolder(unit.grad_shard[info.local_lo : info.local_hi])
+                    spec = getattr(info.param, "_tp_spec", None)
+                    (shard_pieces if spec is not None and spec.size > 1 else rep_pieces).append(piece)
+            if shard_pieces:
+                grad_sq_norm(shard_pieces, out=total)
+            if rep_pieces:
+                rep = grad_sq_norm(rep_pieces).to(total.device)
+                total += rep / tp
+        elif flat_params:
             grad_sq_norm(flat_params, out=total)
         # non-engine params: expert-parallel shards are disjoint across the group (summed by the all-reduce);
-        # replicated ones are pre-divided by W so the all-reduce counts them once
+        # replicated ones are pre-divided by W (and by tp under a tp all-reduce) so the all-reduces count them once
         extra = [p for p in getattr(self, "extra_params", []) if p.grad is not None]
         for p in extra:
             sq = p.grad.detach().float().pow(2).sum()
-            total += sq if getattr(p, "_ep_spec", None) is not None else sq / self.world_size
+            if getattr(getattr(p, "_tp_spec", None), "size", 1) > 1:
+                total += sq / self.world_size
+            else:
+                total += (sq if getattr(p, "_ep_spec", None) is not None else sq / self.world_size) / tp
         if self.sharded:
             small_allreduce.all_reduce_(total, group=self.group)  # 4 bytes: IPC one-shot kernel, not an RCCL ring
+        if tp > 1:
+            torch.distributed.all_reduce(total, group=tp_group)
         clip_grads_by_total_sq(flat_params + extra, total, max_norm)
         return total.sqrt().reshape(())
+
+    def _tp_group(self):
+        """(tp process group, tp size) of the tensor-parallel parameters this engine shards; (None, 1) without TP."""
+        if not hasattr(self, "_tp_cache"):
+            self._tp_cache = (None, 1)
+            params = [info.param for unit in self.units for info in unit.infos]
+            params += list(getattr(self, "extra_params", []))
+            for p in params:
+                spec = getattr(p, "_tp_spec", None)
+                if spec is not None and spec.size > 1:
+                    self._tp_cache = (spec.group, spec.size)
+                    break
+        return self._tp_cache
 
     # --- state dicts --------------------------------------------------------------------------------------
     @torch.no_grad()

@@ -85,7 +85,19 @@ def test_tensor_parallel_matches_single_process(sequence_parallel):
 
 
 def test_tensor_parallel_x_fsdp_2d():
+    """dp_shard 2 x tp 2: loss, global grad norm and weights == one process (the norm sums tp-sharded squares over
+    tp as well as dp_shard)."""
     debug_launcher(td.check_tp_matches_single, args=(False, 2), num_processes=4)
+
+
+def test_tensor_parallel_x_hsdp_3d():
+    """dp_replicate 2 x dp_shard 2 x tp 2 (8 gloo ranks) == one process."""
+    debug_launcher(td.check_tp_matches_single, args=(False, 2, 2, 2), num_processes=8)
+
+
+def test_context_parallel_x_fsdp_2d():
+    """dp_shard 2 x cp 2: ring attention inside FSDP over the flattened dp_shard x cp mesh == one process."""
+    debug_launcher(td.check_cp_llama_matches_single, args=("allgather", 2, 2), num_processes=4)
 
 
 @pytest.mark.parametrize("strategy", ["allgather", "alltoall"])

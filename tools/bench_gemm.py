@@ -45,6 +45,7 @@ def main():
     p.add_argument("--shapes", default="qkv,o,gate_up,down")
     p.add_argument("--no-bf16", action="store_true")
     p.add_argument("--no-scaled-mm", action="store_true")
+    p.add_argument("--check", action="store_true", help="compare every hand-written variant's output with hipBLASLt's")
     args = p.parse_args()
     from accelerate_hpc_test_amd.ops import fp8, gemm_tuning
     from accelerate_hpc_test_amd.ops._ext import ext
@@ -98,8 +99,24 @@ def main():
                         fp8._FP8_GEMM_BACKEND = "hip"
                         times[v].append(timeit(lambda: fp8.gemm(a8, b8, one, one), args.iters))
                         fp8._FP8_GEMM_BACKEND = "blaslt"
+            errs = {}
+            if args.check:  # max |x - ref| / max |ref| against the hipBLASLt runner on the same fp8 operands
+                ref = torch.empty(m, n, device="cuda", dtype=torch.bfloat16)
+                ext().blaslt_fp8_gemm(a8, b8, one, one, 1.0, ref, False)
+                scale = ref.float().abs().max().item()
+                for v in variants:
+                    if v in ("bl", "mx"):
+                        continue
+                    select(v)
+                    fp8._FP8_GEMM_BACKEND = "hip"
+                    o = fp8.gemm(a8, b8, one, one)
+                    fp8._FP8_GEMM_BACKEND = "blaslt"
+                    errs[v] = (o.float() - ref.float()).abs().max().item() / scale
+                del ref
             ext().fp8_gemm_select(0, 4)
             row = {"gemm": f"{name}.{kind}", "M": m, "N": n, "K": k}
+            for v, e_ in errs.items():
+                row[f"v{v}_err"] = float(f"{e_:.3g}")
             if bf:
                 ms = statistics.median(bf)
                 row.update(bf16_ms=round(ms, 3), bf16_tflops=round(flops / ms / 1e9, 1))

@@ -1,0 +1,218 @@
+#!/usr/bin/env python3
+"""Generate the hand-scheduled main loop of the per-tensor fp8 GEMM (csrc/kernels/fp8_gemm_asm.hip).
+
+Writes `accelerate_hpc_test_amd/csrc/kernels/fp8_asm_loop.inc`: one C string macro, `FP8ASM_MAIN_LOOP`, that is
+the body of a single `asm volatile` statement in `fp8_gemm_asm_kernel`. The output file is checked in; rerun this
+script after editing the schedule below (`python tools/gen_fp8_asm.py`).
+
+Why a generated asm loop (profiles/r4_gemm_fp8.md, "16x16x128 in HIP is register-allocation bound"): the 256x256
+tile at 16x16x128 keeps 8x8 accumulator blocks = 256 fp32 per lane. hipcc splits them between VGPRs and AGPRs and
+shuffles them with v_accvgpr_mov inside the K-loop; here the accumulators live in a[0:255] for the whole loop and
+the 16 operand fragments of one K-tile (A 0..7, B 0..7, 8 VGPRs each) in v[128:255], so the loop is nothing but
+MFMAs, ds_reads, LDS-DMA issues and a few scalar ops.
+
+Schedule (one K-tile = 128 fp8 bytes of K = one MFMA K; 4 waves, wave (wm, wn) owns a 128x128 output block;
+fragment i of a wave = rows 8r + i, r = 0..15, so each lane ends up with 8 consecutive output columns per row):
+
+  registers at the top of tile t:  A0..A3 and B0..B3 of tile t (read during tile t-1)
+  phase 1  MFMA A0-3 x B0-3  | ds_read B4-7 of t | lgkmcnt(0) + barrier (every wave done with B of t)
+                             | DMA 5/8 of B(t+2) into the same buffer | ds_read A4-7 of t
+  phase 2  MFMA A0-3 x B4-7  | DMA 3/8 of B(t+2) | lgkmcnt(0) + barrier (every wave done with A of t)
+                             | DMA 2/8 of A(t+2)
+  phase 3  MFMA A4-7 x B0-3  | DMA 5/8 of A(t+2) | vmcnt(15) + barrier (tile t+1 landed for every wave)
+  phase 4  MFMA A4-7 x B4-7  | ds_read A0-3, B0-3 of t+1 from the other buffer | DMA 1/8 of A(t+2) | lgkmcnt(0)
+
+Two LDS buffers (one K-tile of A and B each, 2 x 2 x 33 KiB): a tile's buffer is refilled with tile t+2 as soon as
+every wave holds tile t in registers, so two tiles are in flight with only two buffers. LDS image of one operand:
+32 chunks of 8 rows x 128 B (one wave-wide buffer_load_dwordx4 ... lds each) at a 1056-B stride (32 B pad); the
+fragment reads (lane (r, g): row 8r + i, bytes 16g and 64 + 16g) are then conflict-free for all four ds_read_b128
+lane groups.
+
+The tail runs the same body twice without DMA (tile nk-2 waits vmcnt(0) for nk-1; tile nk-1 reads nothing).
+"""
+
+from __future__ import annotations
+
+import os
+import sys
+
+# register map (must match fp8_gemm_asm.hip)
+A_BASE = 128  # A fragment i = v[128 + 8i : 135 + 8i]
+B_BASE = 192  # B fragment j = v[192 + 8j : 199 + 8j]
+SRD_A = 40    # s[40:43]
+SRD_B = 44    # s[44:47]
+SOFF = 48     # s48..s54 = j * 32 * K, j = 1..7
+M0_A = 56     # LDS-DMA destination of this wave's first A chunk in the current buffer
+M0_B = 57
+M0_X = 58     # xor toggling both destinations between buffer 0 and 1
+CNT = 59      # main-loop trips left
+M0_KEEP = 60  # caller's m0
+CHUNK_STEP = 4 * 1056  # m0 advance per DMA instruction (4 waves x one 1056-B chunk)
+
+
+def A(i):
+    return f"v[{A_BASE + 8 * i}:{A_BASE + 8 * i + 7}]"
+
+
+def B(j):
+    return f"v[{B_BASE + 8 * j}:{B_BASE + 8 * j + 7}]"
+
+
+def acc(i, j):
+    b = (i * 8 + j) * 4
+    return f"a[{b}:{b + 3}]"
+
+
+def mfma(i, j):
+    return f"v_mfma_f32_16x16x128_f8f6f4 {acc(i, j)}, {A(i)}, {B(j)}, {acc(i, j)} cbsz:%c[fa] blgp:%c[fb]"
+
+
+def ds_frag(dst_base, f, addr):
+    """two ds_read_b128 of fragment slot f (0..7) into v[dst : dst+7] from lane address `addr`"""
+    d = dst_base + 8 * f
+    return [f"ds_read_b128 v[{d}:{d + 3}], {addr} offset:{128 * f}",
+            f"ds_read_b128 v[{d + 4}:{d + 7}], {addr} offset:{128 * f + 64}"]
+
+
+def dma(op, n):
+    """n-th (0..7) DMA instruction of operand op ('A'|'B'); m0 must hold this instruction's destination"""
+    srd = SRD_A if op == "A" else SRD_B
+    so = "0" if n == 0 else f"s{SOFF + n - 1}"
+    out = [f"buffer_load_dwordx4 %[voff], s[{srd}:{srd + 3}], {so} offen lds"]
+    if n < 7:
+        out.append(f"s_add_u32 m0, m0, {CHUNK_STEP}")
+    return out
+
+
+def advance_srd(op):
+    srd = SRD_A if op == "A" else SRD_B
+    return [f"s_add_u32 s{srd}, s{srd}, 128", f"s_addc_u32 s{srd + 1}, s{srd + 1}, 0"]
+
+
+def body(dma_on: bool, wait_next: bool, read_next: bool):
+    """one K-tile; returns a list of instruction lines. Extra work is attached after MFMA #k via `slots[k]`."""
+    slots = {k: [] for k in range(64)}
+    order = ([(i, j) for i in range(4) for j in range(4)] + [(i, j) for i in range(4) for j in range(4, 8)]
+             + [(i, j) for i in range(4, 8) for j in range(4)] + [(i, j) for i in range(4, 8) for j in range(4, 8)])
+    # phase 1: B4-7 of t, then (after the barrier) B DMA 0..4 and A4-7 of t
+    for f in range(4):
+        slots[f] += ds_frag(B_BASE, 4 + f, "%[vb]")
+    if dma_on:
+        slots[5] += [f"s_mov_b32 m0, s{M0_B}"]
+    slots[5] += ["s_waitcnt lgkmcnt(0)"]
+    slots[6] += ["s_barrier"]
+    if dma_on:
+        for n in range(5):
+            slots[8 + n] += dma("B", n)
+    for f in range(3):
+        slots[13 + f] += ds_frag(A_BASE, 4 + f, "%[va]")
+    # phase 2
+    slots[16] += ds_frag(A_BASE, 7, "%[va]")
+    slots[20] += ["s_waitcnt lgkmcnt(0)"]
+    slots[21] += ["s_barrier"]
+    if dma_on:
+        for n in range(5, 8):
+            slots[22 + n - 5] += dma("B", n)
+        slots[24] += [f"s_mov_b32 m0, s{M0_A}"]
+        slots[28] += advance_srd("B")  # the SRD bases always point at the next K-tile to load
+        for n in range(2):
+            slots[25 + n] += dma("A", n)
+        # phase 3
+        for n in range(2, 7):
+            slots[38 + n - 2] += dma("A", n)
+    if wait_next:
+        slots[45] += ["s_waitcnt vmcnt(15)" if dma_on else "s_waitcnt vmcnt(0)"]
+        slots[46] += ["s_barrier"]
+    # phase 4: lo fragments of t+1 from the other buffer
+    if read_next:
+        slots[47] += ["v_xor_b32 %[va], %[vax], %[va]", "v_xor_b32 %[vb], %[vbx], %[vb]"]
+        for f in range(4):
+            slots[48 + f] += ds_frag(B_BASE, f, "%[vb]")
+        for f in range(4):
+            slots[52 + f + (1 if f >= 1 else 0)] += ds_frag(A_BASE, f, "%[va]")
+    if dma_on:
+        slots[53] += dma("A", 7)
+        slots[55] += advance_srd("A")
+        slots[57] += [f"s_xor_b32 s{M0_A}, s{M0_A}, s{M0_X}", f"s_xor_b32 s{M0_B}, s{M0_B}, s{M0_X}"]
+    if read_next:
+        slots[61] += ["s_waitcnt lgkmcnt(0)"]
+    lines = []
+    for k, (i, j) in enumerate(order):
+        lines.append(mfma(i, j))
+        lines += slots[k]
+    return lines
+
+
+def prologue():
+    L = []
+    L += [f"s_mov_b32 s{M0_KEEP}, m0",
+          f"s_mov_b64 s[{SRD_A}:{SRD_A + 1}], %[pa]", f"s_mov_b32 s{SRD_A + 2}, -1", f"s_mov_b32 s{SRD_A + 3}, 0x20000",
+          f"s_mov_b64 s[{SRD_B}:{SRD_B + 1}], %[pb]", f"s_mov_b32 s{SRD_B + 2}, -1", f"s_mov_b32 s{SRD_B + 3}, 0x20000",
+          f"s_mov_b32 s{SOFF}, %[stride]"]
+    for n in range(1, 7):
+        L.append(f"s_add_u32 s{SOFF + n}, s{SOFF + n - 1}, %[stride]")
+    L += [f"s_mov_b32 s{M0_A}, %[m0a]", f"s_add_u32 s{M0_B}, %[m0a], 33792",
+          f"s_add_u32 s{M0_X}, %[m0a], 67584", f"s_xor_b32 s{M0_X}, s{M0_X}, %[m0a]",
+          f"s_mov_b32 s{CNT}, %[cnt]"]
+    # tile 0 -> buffer 0, tile 1 -> buffer 1
+    for tile in range(2):
+        L.append(f"s_mov_b32 m0, s{M0_B}")
+        L.append("s_nop 0")
+        for n in range(8):
+            L += dma("B", n)
+        L.append(f"s_mov_b32 m0, s{M0_A}")
+        L.append("s_nop 0")
+        for n in range(8):
+            L += dma("A", n)
+        L += advance_srd("A") + advance_srd("B")
+        L += [f"s_xor_b32 s{M0_A}, s{M0_A}, s{M0_X}", f"s_xor_b32 s{M0_B}, s{M0_B}, s{M0_X}"]
+    for a in range(256):
+        L.append(f"v_accvgpr_write_b32 a{a}, 0")
+    L += ["s_waitcnt vmcnt(16)", "s_barrier"]
+    for f in range(4):
+        L += ds_frag(B_BASE, f, "%[vb]")
+    for f in range(4):
+        L += ds_frag(A_BASE, f, "%[va]")
+    L += ["s_waitcnt lgkmcnt(0)"]
+    return L
+
+
+def generate() -> str:
+    L = prologue()
+    L += [f"s_cmp_eq_u32 s{CNT}, 0", "s_cbranch_scc1 2f", "1:"]
+    L += body(dma_on=True, wait_next=True, read_next=True)
+    L += [f"s_sub_u32 s{CNT}, s{CNT}, 1", f"s_cmp_eq_u32 s{CNT}, 0", "s_cbranch_scc0 1b", "2:"]
+    L += body(dma_on=False, wait_next=True, read_next=True)
+    L += body(dma_on=False, wait_next=False, read_next=False)
+    L += ["s_nop 7", "s_nop 7", f"s_mov_b32 m0, s{M0_KEEP}"]
+    n_mfma = sum(1 for x in L if x.startswith("v_mfma"))
+    assert n_mfma == 3 * 64, n_mfma
+    out = ["// GENERATED by tools/gen_fp8_asm.py -- do not edit by hand; edit the generator and rerun it.",
+           "// Main loop of fp8_gemm_asm_kernel (csrc/kernels/fp8_gemm_asm.hip): see the generator's docstring.",
+           f"// {len(L)} lines, {n_mfma} MFMAs (loop body 64).",
+           "#pragma once",
+           "#define FP8ASM_MAIN_LOOP \\"]
+    for x in L:
+        out.append(f'  "{x}\\n" \\')
+    out.append('  ""')
+    out.append("")
+    out.append(f"#define FP8ASM_SGPR_CLOBBERS " + ", ".join(f'"s{s}"' for s in range(SRD_A, M0_KEEP + 1)))
+    out.append("")
+    return "\n".join(out)
+
+
+def main(argv):
+    here = os.path.dirname(os.path.abspath(__file__))
+    path = os.path.join(here, "..", "accelerate_hpc_test_amd", "csrc", "kernels", "fp8_asm_loop.inc")
+    text = generate()
+    if len(argv) > 1 and argv[1] == "--check":
+        with open(path) as f:
+            return 0 if f.read() == text else 1
+    with open(path, "w") as f:
+        f.write(text)
+    print(f"wrote {os.path.normpath(path)}")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main(sys.argv))

@@ -93,6 +93,9 @@ for step in "$@"; do
     attn_long) run attn_long 300 python tools/bench_attn.py --S 32768 --iters 3 ;;
     pmc_attn) run pmc_attn 200 bash tools/pmc_attn.sh ;;
     gemm) run gemm 300 python tools/bench_gemm.py ;;
+    mr_tp) run mr_tp 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_multirank.py -k "tp" ;;
+    gemm_asm) run ktest_asm 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "fp8_gemm_v4" && \
+              run gemm_asm 400 python tools/bench_gemm.py --variants ${GEMM_VARIANTS:-bl,18,17} --no-bf16 --no-scaled-mm --rounds 3 --check ;;
     pmc_gemm) run pmc_gemm 400 bash tools/pmc_gemm.sh --variants ${GEMM_VARIANTS:-bl,4,8,7} --shapes o,down --iters 2 --rounds 1 --no-bf16 --no-scaled-mm ;;
     dgrad) run dgrad 300 python tools/bench_dgrad.py ;;
     bench8b_dgradbl) ACCELERATE_DGRAD_BLASLT=1 run bench8b_dgradbl 600 python bench.py --steps 5 --warmup 2 $BENCH_ARGS ;;
