@@ -1360,6 +1360,55 @@ class FSDPEngine:
         return missing
 
     @torch.no_grad()
+    def broadcast_full(self, full: torch.Tensor):
+        """Broadcast a full-layout unit buffer from global rank 0: over the shard group, then from replica 0 over the
+        replicate group (HSDP), as `_materialize` does for cpu_ram_efficient_loading."""
+        if self.world_size > 1:
+            dist.broadcast(full, src=dist.get_global_rank(self.group, 0) if self.group is not None else 0, group=self.group)
+        if self.replicate_size > 1:
+            dist.broadcast(full, src=dist.get_global_rank(self.replicate_group, 0), group=self.replicate_group)
+
+    @torch.no_grad()
+    def load_full_state_dict_broadcast(self, sd: Optional[dict]):
+        """FULL_STATE_DICT load where only global rank 0 holds `sd` (None elsewhere): one broadcast of each unit's
+        flat fp32 buffer, every rank keeps its slice (reference fsdp2_load_full_state_dict,
+        /root/reference/src/accelerate/utils/fsdp_utils.py:467-554). Host memory: rank 0 maps the file, the others
+        hold nothing."""
+        from ..utils.fsdp_utils import IO_STATS
+
+        missing = []
+        for unit in self.units:
+            full = torch.zeros(unit.padded, dtype=torch.float32, device=self.device)
+            if sd is not None:
+                for info in unit.infos:
+                    t = sd.get(info.fqn)
+                    if t is None:
+                        missing.append(info.fqn)
+                        continue
+                    IO_STATS["bytes_read"] += t.numel() * t.element_size()
+                    full[info.offset : info.offset + info.numel].copy_(t.reshape(-1).to(self.device, torch.float32))
+            self.broadcast_full(full)
+            unit.master.copy_(unit.local_of_full(full).to(unit.master.device))
+            if unit.shard_lp is not unit.master:
+                unit.shard_lp.copy_(unit.master.to(unit.shard_lp.device))
+            del full
+        self.refresh_fp8()
+        for name, p in self._extras():
+            spec = getattr(p, "_ep_spec", None)
+            shape = ((spec[1] * p.shape[0],) + tuple(p.shape[1:])) if spec is not None else tuple(p.shape)
+            full = torch.zeros(shape, dtype=torch.float32, device=p.device)
+            if sd is not None and name in sd:
+                full.copy_(sd[name].to(p.device, torch.float32))
+            if dist.is_available() and dist.is_initialized():
+                dist.broadcast(full, src=0)
+            self._load_extra(name, full)
+        if missing:
+            import logging
+
+            logging.getLogger(__name__).warning(f"FULL_STATE_DICT load: {len(missing)} keys missing from the checkpoint, e.g. {missing[:3]}")
+        return missing
+
+    @torch.no_grad()
     def load_sharded_pieces(self, pieces: list[tuple[dict, dict]]):
         """Load from any number of saved shards (resharding): each piece is (tensors, meta) of one saved rank."""
         for unit in self.units:

@@ -172,6 +172,69 @@ def check_fsdp_matches_single(reshard: bool = True, state_dict_type: str = "SHAR
         assert torch.allclose(full3[n], q, atol=1e-5), (n, (full3[n] - q).abs().max())
 
 
+def check_fsdp_checkpoint_io(phase: str, ckpt_dir: str, state_dict_type: str = "SHARDED_STATE_DICT"):
+    """Per-rank-bounded checkpoint IO (reference: DCP planned reads / rank-0 broadcast,
+    /root/reference/src/accelerate/utils/fsdp_utils.py:161-230,281-335,467-554).
+
+    phase "save": tiny Llama, 2 AdamW steps, `save_state`; rank 0 also writes the full model + optimizer state as the
+    oracle. phase "load" (any world size): fresh model, `load_state`, then every rank's bytes of tensor data read from
+    the checkpoint must be <= 1/W of it plus boundary pieces (SHARDED), or zero off rank 0 (FULL); the full model and
+    optimizer state must equal the oracle."""
+    from accelerate_hpc_test_amd.models.llama import LlamaForCausalLM
+    from accelerate_hpc_test_amd.utils import fsdp_utils
+
+    plugin = FullyShardedDataParallelPlugin(fsdp_version=2, auto_wrap_policy="transformer_based_wrap",
+                                            transformer_cls_names_to_wrap=["LlamaDecoderLayer"], state_dict_type=state_dict_type)
+    acc = Accelerator(cpu=True, fsdp_plugin=plugin)
+    W, r = acc.num_processes, acc.process_index
+    set_seed(0 if phase == "save" else 1)
+    cfg = _tiny_llama_cfg()
+    model = LlamaForCausalLM(cfg)
+    model.init_weights()
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-2, weight_decay=0.01)
+    model, opt = acc.prepare(model, opt)
+    eng = model.engine
+    if phase == "save":
+        g = torch.Generator().manual_seed(3)
+        for _ in range(2):
+            ids = torch.randint(0, cfg.vocab_size, (2 * W, 16), generator=g)[2 * r : 2 * r + 2]
+            acc.backward(model(ids, labels=ids).loss)
+            opt.step()
+            opt.zero_grad()
+        acc.save_state(ckpt_dir)
+        full = acc.get_state_dict(model)
+        optim = fsdp_utils._optim_full_state(eng, opt)
+        if r == 0:
+            torch.save({"model": full, "optim": optim["state"]}, os.path.join(ckpt_dir, "oracle.pt"))
+        acc.wait_for_everyone()
+        return
+    fsdp_utils.IO_STATS["bytes_read"] = 0
+    acc.load_state(ckpt_dir)
+    mine = fsdp_utils.IO_STATS["bytes_read"]
+    reads = gather_object([mine])
+    oracle = torch.load(os.path.join(ckpt_dir, "oracle.pt"), weights_only=True)
+    total = sum(t.numel() * 4 for t in oracle["model"].values())
+    total += sum(t.numel() * 4 for st in oracle["optim"].values() for t in st.values())
+    if r == 0:
+        print(f"[checkpoint io] {state_dict_type} W={W}: bytes read per rank {reads}, checkpoint tensors {total}", flush=True)
+    if state_dict_type == "SHARDED_STATE_DICT":
+        # a rank's slice of every unit (padding included) + the pieces of parameters cut by a saved-rank boundary
+        bound = total / W * 1.05 + 64 * 1024
+        assert max(reads) <= bound, (reads, total, W)
+        assert sum(reads) >= total * 0.99, (reads, total)  # and together the ranks read everything once
+    else:
+        assert all(b == 0 for b in reads[1:]) and reads[0] >= total * 0.99, (reads, total)
+    full = acc.get_state_dict(model)
+    for n, t in oracle["model"].items():
+        assert torch.equal(full[n].float(), t.float()), n
+    optim = fsdp_utils._optim_full_state(eng, opt)
+    if r == 0:
+        for fqn, st in oracle["optim"].items():
+            for k, t in st.items():
+                assert torch.equal(optim["state"][fqn][k], t), (fqn, k)
+    acc.wait_for_everyone()
+
+
 def check_fsdp_optimizer_overlap(grad_accum: int = 1):
     """`RcclKwargs(fsdp_optimizer_overlap=True)`: the per-unit updates applied during backward must give exactly the
     single-process AdamW trajectory (with a LR schedule and gradient accumulation), and clipping must refuse."""

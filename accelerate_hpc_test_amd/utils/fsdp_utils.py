@@ -47,11 +47,33 @@ def _barrier():
         PartialState().wait_for_everyone()
 
 
+# bytes of tensor data this process read from checkpoint files (sharded / full loads): the per-rank IO bound test
+# (tests/test_multiprocess_cpu.py::test_fsdp_checkpoint_io_is_per_rank_bounded) reads and resets it
+IO_STATS = {"bytes_read": 0}
+
+
+def _count(t: torch.Tensor) -> torch.Tensor:
+    IO_STATS["bytes_read"] += t.numel() * t.element_size()
+    return t
+
+
+def _tp_info(eng):
+    group, size = eng._tp_group() if hasattr(eng, "_tp_group") else (None, 1)
+    return (dist.get_rank(group) if size > 1 else 0), size
+
+
+def _shard_stem(eng):
+    """File stem of this rank's shard: `shard_{dp_shard rank}`, plus `_tp{t}` when tensor parallel ranks hold
+    different slices of the same FSDP shard position."""
+    t, tp = _tp_info(eng)
+    return f"shard_{eng.rank}" + (f"_tp{t}" if tp > 1 else "")
+
+
 def save_fsdp_model(fsdp_plugin, accelerator, model, output_dir, model_index=0, adapter_only=False):
     os.makedirs(output_dir, exist_ok=True)
     eng = _engine(model)
     if fsdp_plugin.state_dict_type == "FULL_STATE_DICT":
-        sd = eng.full_state_dict(rank0_only=True)
+        sd = eng.full_state_dict(rank0_only=True)  # gathered unit by unit; only rank 0 keeps host copies
         if _rank() == 0:
             name = f"{FSDP_MODEL_NAME}.bin" if model_index == 0 else f"{FSDP_MODEL_NAME}_{model_index}.bin"
             path = os.path.join(output_dir, name)
@@ -63,28 +85,121 @@ def save_fsdp_model(fsdp_plugin, accelerator, model, output_dir, model_index=0, 
         shard = eng.sharded_state_dict()
         from safetensors.torch import save_file
 
-        r = eng.rank
         if getattr(eng, "replicate_rank", 0) != 0:  # HSDP / NO_SHARD replicas hold identical shards: replica 0 writes
             _barrier()
             return
-        save_file({k: v.contiguous() for k, v in shard["tensors"].items()}, os.path.join(ckpt_dir, f"shard_{r}.safetensors"))
-        with open(os.path.join(ckpt_dir, f"meta_{r}.json"), "w") as f:
+        t, tp = _tp_info(eng)
+        shard["meta"].update(tp_rank=t, tp_size=tp)
+        stem = _shard_stem(eng)
+        save_file({k: v.contiguous() for k, v in shard["tensors"].items()}, os.path.join(ckpt_dir, f"{stem}.safetensors"))
+        with open(os.path.join(ckpt_dir, stem.replace("shard_", "meta_") + ".json"), "w") as f:
             json.dump(shard["meta"], f)
         logger.info(f"Model shard saved to {ckpt_dir}")
     _barrier()
 
 
-def _read_sharded_dir(ckpt_dir):
-    from safetensors.torch import load_file
-
-    pieces = []
+def _saved_metas(ckpt_dir, tp_rank=None):
+    """[(shard file, meta)] of a sharded model dir, from the small JSON files only (no tensor data read). With
+    `tp_rank`, only the shards written by that tensor-parallel rank."""
+    out = []
     for meta_path in sorted(glob.glob(os.path.join(ckpt_dir, "meta_*.json"))):
-        r = int(os.path.basename(meta_path)[5:-5])
         with open(meta_path) as f:
             meta = json.load(f)
-        tensors = load_file(os.path.join(ckpt_dir, f"shard_{r}.safetensors"))
-        pieces.append((tensors, meta))
-    return pieces
+        if tp_rank is not None and meta.get("tp_size", 1) > 1 and meta.get("tp_rank", 0) != tp_rank:
+            continue
+        stem = os.path.basename(meta_path)[len("meta_") : -len(".json")]
+        out.append((os.path.join(ckpt_dir, f"shard_{stem}.safetensors"), meta))
+    return out
+
+
+def _read_sharded_dir(ckpt_dir):
+    """Every saved shard in full: (tensors, meta) per saved rank (the merge tool; loads use `_load_sharded_model`)."""
+    from safetensors.torch import load_file
+
+    return [(load_file(path), meta) for path, meta in _saved_metas(ckpt_dir)]
+
+
+class _ShardReader:
+    """Lazily opened safetensors shards; `read(path, key, a, b)` returns elements [a, b) of a 1-D tensor through the
+    file's mmap, so only the overlapping byte range is read."""
+
+    def __init__(self):
+        self.handles = {}
+
+    def read(self, path, key, a=None, b=None):
+        from safetensors import safe_open
+
+        h = self.handles.get(path)
+        if h is None:
+            h = self.handles[path] = safe_open(path, framework="pt")
+        sl = h.get_slice(key)
+        return _count(sl[a:b] if a is not None else sl[:])
+
+    def shape(self, path, key):
+        from safetensors import safe_open
+
+        h = self.handles.get(path)
+        if h is None:
+            h = self.handles[path] = safe_open(path, framework="pt")
+        return tuple(h.get_slice(key).get_shape())
+
+
+@torch.no_grad()
+def _load_sharded_model(eng, ckpt_dir):
+    """SHARDED_STATE_DICT load that reads only the saved pieces overlapping this rank's flat slice (reference: DCP's
+    planned per-rank reads, /root/reference/src/accelerate/utils/fsdp_utils.py:221-225). Same world size: one file
+    per rank; any other world size: the few files whose [param_lo, param_lo + numel) ranges intersect."""
+    t, _ = _tp_info(eng)
+    metas = _saved_metas(ckpt_dir, tp_rank=t)
+    if not metas:
+        raise FileNotFoundError(f"No model shards in {ckpt_dir}")
+    rd = _ShardReader()
+    for unit in eng.units:
+        for info in unit.infos:
+            lo_need, hi_need = info.param_lo, info.param_lo + (info.local_hi - info.local_lo)
+            if hi_need <= lo_need:
+                continue
+            for path, meta in metas:
+                pm = meta["params"].get(info.fqn)
+                if pm is None or pm["numel"] <= 0:
+                    continue
+                s_lo = pm["param_lo"]
+                a, b = max(lo_need, s_lo), min(hi_need, s_lo + pm["numel"])
+                if b > a:
+                    src = rd.read(path, info.fqn, a - s_lo, b - s_lo)
+                    unit.master[info.local_lo + (a - lo_need) : info.local_lo + (b - lo_need)].copy_(src.to(unit.master.device))
+        if unit.shard_lp is not unit.master:
+            unit.shard_lp.copy_(unit.master.to(unit.shard_lp.device))
+    eng.refresh_fp8()
+    for name, p in eng._extras():
+        found = [(path, m["extra"][name]) for path, m in metas if name in m.get("extra", {})]
+        if not found:
+            continue
+        if not found[0][1]["ep"]:
+            p.copy_(rd.read(found[0][0], name).to(p.device, p.dtype))
+            continue
+        # expert-parallel stack: this rank's rows [r n, (r + 1) n) of the saved ranks' stacks in rank order
+        group, W = p._ep_spec
+        n = p.shape[0]
+        lo = dist.get_rank(group) * n
+        pos = 0
+        for path, em in sorted(found, key=lambda x: x[1]["rank"]):
+            rows = rd.shape(path, name)[0]
+            a, b = max(lo, pos), min(lo + n, pos + rows)
+            if b > a:
+                p[a - lo : b - lo].copy_(rd.read(path, name, a - pos, b - pos).to(p.device, p.dtype))
+            pos += rows
+
+
+@torch.no_grad()
+def _load_full_model_rank0(eng, path):
+    """FULL_STATE_DICT load: global rank 0 reads the file (memory-mapped), every unit reaches the other ranks as one
+    broadcast of its flat fp32 buffer (reference fsdp2_load_full_state_dict: rank 0 reads, broadcasts,
+    /root/reference/src/accelerate/utils/fsdp_utils.py:467-554)."""
+    sd = None
+    if _rank() == 0:
+        sd = torch.load(path, map_location="cpu", weights_only=True, mmap=True)
+    eng.load_full_state_dict_broadcast(sd)
 
 
 def load_fsdp_model(fsdp_plugin, accelerator, model, input_dir, model_index=0, adapter_only=False):
@@ -93,19 +208,23 @@ def load_fsdp_model(fsdp_plugin, accelerator, model, input_dir, model_index=0, a
     if fsdp_plugin.state_dict_type == "FULL_STATE_DICT":
         name = f"{FSDP_MODEL_NAME}.bin" if model_index == 0 else f"{FSDP_MODEL_NAME}_{model_index}.bin"
         path = os.path.join(input_dir, name)
-        # every rank reads the full file (host RAM is plentiful on MI355X nodes) and keeps its slice
-        sd = torch.load(path, map_location="cpu", weights_only=True)
-        eng.load_full_state_dict(sd)
+        if _tp_info(eng)[1] > 1 or not (dist.is_available() and dist.is_initialized()):
+            sd = torch.load(path, map_location="cpu", weights_only=True, mmap=True)  # tp slices: every rank keeps its own
+            eng.load_full_state_dict(sd)
+        else:
+            _load_full_model_rank0(eng, path)
     else:
         ckpt_dir = input_dir if os.path.basename(os.path.normpath(input_dir)).startswith(FSDP_MODEL_NAME) else os.path.join(input_dir, f"{FSDP_MODEL_NAME}_{model_index}")
-        eng.load_sharded_pieces(_read_sharded_dir(ckpt_dir))
+        _load_sharded_model(eng, ckpt_dir)
     _barrier()
 
 
 # ---------------------------------------------------------------------------------------------- optimizer
 def _optim_full_state(eng, optimizer):
-    """Gather optimizer state into {fqn: {key: full tensor}} (one all-gather per unit per state key)."""
+    """Gather optimizer state into {fqn: {key: full tensor}} (one all-gather per unit per state key); only global rank
+    0 keeps host copies."""
     opt = getattr(optimizer, "optimizer", optimizer)
+    keep = _rank() == 0
     out, step_val = OrderedDict(), None
     for unit in eng.units:
         keys = set()
@@ -114,15 +233,18 @@ def _optim_full_state(eng, optimizer):
             st = opt.state.get(info.shard_param, {})
             if "step" in st:
                 step_val = st["step"]
-        for key in sorted(keys):
+        keys = _agree_keys(keys)
+        for key in keys:
             local = torch.zeros(unit.shard_numel, dtype=torch.float32, device=eng.device)
             for info in unit.infos:
                 t = opt.state.get(info.shard_param, {}).get(key)
                 if t is not None and info.local_hi > info.local_lo:
                     local[info.local_lo : info.local_hi].copy_(t.reshape(-1).float())
             full = eng.gather_full(unit, local)
-            for info in unit.infos:
-                out.setdefault(info.fqn, {})[key] = full[info.offset : info.offset + info.numel].view(info.shape).cpu().clone()
+            if keep:
+                for info in unit.infos:
+                    out.setdefault(info.fqn, {})[key] = full[info.offset : info.offset + info.numel].view(info.shape).cpu().clone()
+            del full, local
     groups = []
     fqn_of = {id(info.shard_param): info.fqn for unit in eng.units for info in unit.infos}
     for g in opt.param_groups:
@@ -130,6 +252,16 @@ def _optim_full_state(eng, optimizer):
         gg["params"] = [fqn_of.get(id(p)) for p in g["params"]]
         groups.append(gg)
     return {"state": out, "param_groups": groups, "step": step_val}
+
+
+def _agree_keys(keys):
+    """The sorted union of state keys over all ranks (a rank whose shard of a unit is empty has none)."""
+    keys = sorted(keys)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        allk = [None] * dist.get_world_size()
+        dist.all_gather_object(allk, keys)
+        keys = sorted(set().union(*[set(k) for k in allk]))
+    return keys
 
 
 def _optim_load_full(eng, optimizer, sd):
@@ -146,10 +278,67 @@ def _optim_load_full(eng, optimizer, sd):
         if sd.get("step") is not None:
             new["step"] = torch.as_tensor(sd["step"], dtype=torch.float32).clone()
         opt.state[info.shard_param] = new
-    for g, gs in zip(opt.param_groups, sd.get("param_groups", [])):
+    _apply_groups(opt, sd.get("param_groups", []))
+
+
+def _apply_groups(opt, saved_groups):
+    for g, gs in zip(opt.param_groups, saved_groups):
         for k, v in gs.items():
             if k != "params":
                 g[k] = v
+
+
+@torch.no_grad()
+def _optim_load_full_rank0(eng, optimizer, path):
+    """FULL optimizer load: rank 0 reads the file, each unit's state key is broadcast as one flat fp32 buffer."""
+    opt = getattr(optimizer, "optimizer", optimizer)
+    sd = torch.load(path, map_location="cpu", weights_only=True, mmap=True) if _rank() == 0 else None
+    head = [None]
+    if _rank() == 0:
+        keys = {fqn: sorted(k for k, v in st.items() if torch.is_tensor(v) and v.dim() > 0) for fqn, st in sd["state"].items()}
+        head = [{"keys": keys, "step": sd.get("step"), "param_groups": sd.get("param_groups", [])}]
+    dist.broadcast_object_list(head, src=0)
+    head = head[0]
+    step = head["step"]
+    for unit in eng.units:
+        ukeys = sorted({k for info in unit.infos for k in head["keys"].get(info.fqn, [])})
+        for key in ukeys:
+            full = torch.zeros(unit.padded, dtype=torch.float32, device=eng.device)
+            if _rank() == 0:
+                for info in unit.infos:
+                    v = sd["state"].get(info.fqn, {}).get(key)
+                    if v is not None:
+                        full[info.offset : info.offset + info.numel].copy_(_count(v.reshape(-1)).to(eng.device, torch.float32))
+            eng.broadcast_full(full)
+            for info in unit.infos:
+                if key not in head["keys"].get(info.fqn, []):
+                    continue
+                st = opt.state.setdefault(info.shard_param, {})
+                st[key] = full[info.offset + info.param_lo : info.offset + info.param_lo + (info.local_hi - info.local_lo)].clone()
+                if step is not None:
+                    st["step"] = torch.as_tensor(step, dtype=torch.float32).clone()
+            del full
+    _apply_groups(opt, head["param_groups"])
+
+
+def _jsonable(v):
+    if torch.is_tensor(v):
+        return {"__tensor__": v.item(), "dtype": str(v.dtype).replace("torch.", "")}
+    if isinstance(v, tuple):
+        return {"__tuple__": [_jsonable(x) for x in v]}
+    if isinstance(v, list):
+        return [_jsonable(x) for x in v]
+    return v
+
+
+def _unjson(v):
+    if isinstance(v, dict) and "__tensor__" in v:
+        return torch.tensor(v["__tensor__"], dtype=getattr(torch, v["dtype"]))
+    if isinstance(v, dict) and "__tuple__" in v:
+        return tuple(_unjson(x) for x in v["__tuple__"])
+    if isinstance(v, list):
+        return [_unjson(x) for x in v]
+    return v
 
 
 def save_fsdp_optimizer(fsdp_plugin, accelerator, optimizer, model, output_dir, optimizer_index=0):
@@ -161,21 +350,61 @@ def save_fsdp_optimizer(fsdp_plugin, accelerator, optimizer, model, output_dir, 
             name = f"{OPTIMIZER_NAME}.bin" if optimizer_index == 0 else f"{OPTIMIZER_NAME}_{optimizer_index}.bin"
             torch.save(sd, os.path.join(output_dir, name))
     else:
+        # one safetensors file of this rank's 1-D state pieces ("{fqn}|{key}") + a JSON of their ranges, the scalar
+        # states and the param groups: loads read only the overlapping byte ranges, like the model shards
         d = os.path.join(output_dir, f"{OPTIMIZER_NAME}_{optimizer_index}")
         os.makedirs(d, exist_ok=True)
         opt = getattr(optimizer, "optimizer", optimizer)
-        local = {}
+        tensors, meta, scalars = {}, {}, {}
         for unit in eng.units:
             for info in unit.infos:
-                st = opt.state.get(info.shard_param)
-                if st:
-                    local[info.fqn] = {k: (v.cpu() if torch.is_tensor(v) else v) for k, v in st.items()}
+                st = opt.state.get(info.shard_param) or {}
+                keys = []
+                for k, v in st.items():
+                    if torch.is_tensor(v) and v.dim() > 0:
+                        tensors[f"{info.fqn}|{k}"] = v.detach().reshape(-1).float().cpu().contiguous()
+                        keys.append(k)
+                    else:
+                        scalars.setdefault(info.fqn, {})[k] = _jsonable(v)
+                meta[info.fqn] = {"param_lo": info.param_lo, "numel": info.local_hi - info.local_lo, "keys": keys}
         fqn_of = {id(info.shard_param): info.fqn for unit in eng.units for info in unit.infos}
-        groups = [{**{k: v for k, v in g.items() if k != "params"}, "params": [fqn_of.get(id(p)) for p in g["params"]]} for g in opt.param_groups]
-        meta = {info.fqn: {"param_lo": info.param_lo, "numel": info.local_hi - info.local_lo} for unit in eng.units for info in unit.infos}
+        groups = [{**{k: _jsonable(v) for k, v in g.items() if k != "params"}, "params": [fqn_of.get(id(p)) for p in g["params"]]}
+                  for g in opt.param_groups]
         if getattr(eng, "replicate_rank", 0) == 0:  # replicas hold identical optimizer shards
-            torch.save({"state": local, "param_groups": groups, "meta": meta}, os.path.join(d, f"shard_{eng.rank}.pt"))
+            from safetensors.torch import save_file
+
+            t, tp = _tp_info(eng)
+            stem = _shard_stem(eng)
+            save_file(tensors, os.path.join(d, f"{stem}.safetensors"))
+            with open(os.path.join(d, stem.replace("shard_", "meta_") + ".json"), "w") as f:
+                json.dump({"meta": meta, "scalars": scalars, "param_groups": groups, "tp_rank": t, "tp_size": tp}, f)
     _barrier()
+
+
+@torch.no_grad()
+def _load_sharded_optimizer(eng, opt, d):
+    t, _ = _tp_info(eng)
+    metas = _saved_metas(d, tp_rank=t)
+    rd = _ShardReader()
+    for unit in eng.units:
+        for info in unit.infos:
+            lo_need, hi_need = info.param_lo, info.param_lo + (info.local_hi - info.local_lo)
+            new = {}
+            for path, m in metas:
+                pm = m["meta"].get(info.fqn)
+                if pm is None:
+                    continue
+                for k, v in m["scalars"].get(info.fqn, {}).items():
+                    new.setdefault(k, _unjson(v))
+                a, b = max(lo_need, pm["param_lo"]), min(hi_need, pm["param_lo"] + pm["numel"])
+                for k in pm["keys"]:
+                    dst = new.setdefault(k, torch.zeros(hi_need - lo_need, dtype=torch.float32))
+                    if b > a:
+                        dst[a - lo_need : b - lo_need].copy_(rd.read(path, f"{info.fqn}|{k}", a - pm["param_lo"], b - pm["param_lo"]))
+            if new:
+                opt.state[info.shard_param] = {k: (v.to(eng.device) if torch.is_tensor(v) and v.dim() > 0 else v) for k, v in new.items()}
+    if metas:
+        _apply_groups(opt, [{k: _unjson(v) for k, v in g.items()} for g in metas[0][1]["param_groups"]])
 
 
 def load_fsdp_optimizer(fsdp_plugin, accelerator, optimizer, model, input_dir, optimizer_index=0, adapter_only=False):
@@ -184,36 +413,44 @@ def load_fsdp_optimizer(fsdp_plugin, accelerator, optimizer, model, input_dir, o
     opt = getattr(optimizer, "optimizer", optimizer)
     if fsdp_plugin.state_dict_type == "FULL_STATE_DICT":
         name = f"{OPTIMIZER_NAME}.bin" if optimizer_index == 0 else f"{OPTIMIZER_NAME}_{optimizer_index}.bin"
-        sd = torch.load(os.path.join(input_dir, name), map_location="cpu", weights_only=True)
-        _optim_load_full(eng, optimizer, sd)
+        path = os.path.join(input_dir, name)
+        if _tp_info(eng)[1] > 1 or not (dist.is_available() and dist.is_initialized()):
+            _optim_load_full(eng, optimizer, torch.load(path, map_location="cpu", weights_only=True, mmap=True))
+        else:
+            _optim_load_full_rank0(eng, optimizer, path)
     else:
         d = input_dir if os.path.basename(os.path.normpath(input_dir)).startswith(OPTIMIZER_NAME) else os.path.join(input_dir, f"{OPTIMIZER_NAME}_{optimizer_index}")
-        files = sorted(glob.glob(os.path.join(d, "shard_*.pt")))
-        saved = [torch.load(f, map_location="cpu", weights_only=True) for f in files]
-        for unit in eng.units:
-            for info in unit.infos:
-                lo_need, hi_need = info.param_lo, info.param_lo + (info.local_hi - info.local_lo)
-                new = {}
-                for s in saved:
-                    st, m = s["state"].get(info.fqn), s["meta"].get(info.fqn)
-                    if st is None or m is None:
-                        continue
-                    a, b = max(lo_need, m["param_lo"]), min(hi_need, m["param_lo"] + m["numel"])
-                    for k, v in st.items():
-                        if torch.is_tensor(v) and v.dim() > 0:
-                            dst = new.setdefault(k, torch.zeros(hi_need - lo_need, dtype=torch.float32))
-                            if b > a:
-                                dst[a - lo_need : b - lo_need].copy_(v[a - m["param_lo"] : b - m["param_lo"]])
-                        else:
-                            new[k] = v.clone() if torch.is_tensor(v) else v
-                if new:
-                    opt.state[info.shard_param] = {k: (v.to(eng.device) if torch.is_tensor(v) and v.dim() > 0 else v) for k, v in new.items()}
-        if saved:
-            for g, gs in zip(opt.param_groups, saved[0]["param_groups"]):
-                for k, v in gs.items():
-                    if k != "params":
-                        g[k] = v
+        if glob.glob(os.path.join(d, "meta_*.json")):
+            _load_sharded_optimizer(eng, opt, d)
+        else:
+            _load_sharded_optimizer_v1(eng, opt, d)
     _barrier()
+
+
+def _load_sharded_optimizer_v1(eng, opt, d):
+    """Round-4 layout (`shard_{rank}.pt` holding every piece): read in full."""
+    files = sorted(glob.glob(os.path.join(d, "shard_*.pt")))
+    saved = [torch.load(f, map_location="cpu", weights_only=True) for f in files]
+    for unit in eng.units:
+        for info in unit.infos:
+            lo_need, hi_need = info.param_lo, info.param_lo + (info.local_hi - info.local_lo)
+            new = {}
+            for s in saved:
+                st, m = s["state"].get(info.fqn), s["meta"].get(info.fqn)
+                if st is None or m is None:
+                    continue
+                a, b = max(lo_need, m["param_lo"]), min(hi_need, m["param_lo"] + m["numel"])
+                for k, v in st.items():
+                    if torch.is_tensor(v) and v.dim() > 0:
+                        dst = new.setdefault(k, torch.zeros(hi_need - lo_need, dtype=torch.float32))
+                        if b > a:
+                            dst[a - lo_need : b - lo_need].copy_(v[a - m["param_lo"] : b - m["param_lo"]])
+                    else:
+                        new[k] = v.clone() if torch.is_tensor(v) else v
+            if new:
+                opt.state[info.shard_param] = {k: (v.to(eng.device) if torch.is_tensor(v) and v.dim() > 0 else v) for k, v in new.items()}
+    if saved:
+        _apply_groups(opt, saved[0]["param_groups"])
 
 
 def merge_fsdp_weights(checkpoint_dir: str, output_path: str, safe_serialization: bool = True, remove_checkpoint_dir: bool = False):

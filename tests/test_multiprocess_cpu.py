@@ -160,6 +160,16 @@ def test_local_sgd(chunk_bytes):
     debug_launcher(td.check_local_sgd, args=(2, 4, chunk_bytes), num_processes=2)
 
 
+@pytest.mark.parametrize("sd_type", ["SHARDED_STATE_DICT", "FULL_STATE_DICT"])
+@pytest.mark.parametrize("load_world", [4, 2])
+def test_fsdp_checkpoint_io_is_per_rank_bounded(sd_type, load_world, tmp_path):
+    """Saved on 4 ranks, loaded on 4 (one file per rank) or 2 (resharded): each rank reads <= 1/W of a SHARDED
+    checkpoint (+ boundary pieces); a FULL one is read by rank 0 only and broadcast unit by unit."""
+    d = str(tmp_path / "ckpt")
+    debug_launcher(td.check_fsdp_checkpoint_io, args=("save", d, sd_type), num_processes=4)
+    debug_launcher(td.check_fsdp_checkpoint_io, args=("load", d, sd_type), num_processes=load_world)
+
+
 def test_fsdp_three_ranks():
     debug_launcher(td.check_fsdp_matches_single, args=(True, "SHARDED_STATE_DICT"), num_processes=3)
 
