@@ -180,6 +180,14 @@ def _only_tensors(data) -> bool:
         return False
     return True
 
+def _any_dtensor(params) -> bool:
+    try:
+        from torch.distributed.tensor import DTensor
+    except ImportError:  # pragma: no cover
+        return False
+    return any(isinstance(p, DTensor) or isinstance(p.grad, DTensor) for p in params)
+
+
 class Accelerator:
     def __init__(
         self,
@@ -1017,9 +1025,11 @@ class Accelerator:
                 return m.clip_grad_norm_(max_norm, norm_type)
         self.unscale_gradients()
         grads_params = [p for p in parameters if p.grad is not None]
+        if _any_dtensor(grads_params):
+            return self._clip_grad_norm_dtensor(grads_params, float(max_norm), float(norm_type))
         tp_sharded = [p for p in grads_params if getattr(getattr(p, "_tp_spec", None), "size", 1) > 1]
-        if tp_sharded and float(norm_type) == 2.0:
-            return self._clip_grad_norm_tp(grads_params, tp_sharded, float(max_norm))
+        if tp_sharded:
+            return self._clip_grad_norm_tp(grads_params, tp_sharded, float(max_norm), float(norm_type))
         if grads_params and grads_params[0].grad.is_cuda and float(norm_type) == 2.0:
             from .ops.multi_tensor import clip_grads_by_total_sq, grad_sq_norm
 
@@ -1029,10 +1039,11 @@ class Accelerator:
         return torch.nn.utils.clip_grad_norm_(parameters, max_norm, norm_type=norm_type)
 
     @staticmethod
-    def _clip_grad_norm_tp(grads_params, sharded, max_norm):
+    def _clip_grad_norm_tp(grads_params, sharded, max_norm, norm_type=2.0):
         """Tensor parallel: each rank holds 1/tp of a sharded parameter's gradient, so those squares are summed over
         the tp group, while replicated parameters (norms, biases of rowwise layers, ...) hold the whole gradient on
-        every rank and count once. (The plain local norm under-counts the sharded part by 1/tp.)"""
+        every rank and count once. (The plain local norm under-counts the sharded part by 1/tp.) norm_type inf: the
+        sharded part's max is MAX-reduced over tp; other finite orders are not supported here."""
         import torch.distributed as dist
 
         group = sharded[0]._tp_spec.group
@@ -1040,6 +1051,19 @@ class Accelerator:
         rest = [p for p in grads_params if id(p) not in ids]
         dev = grads_params[0].grad.device
         native = grads_params[0].grad.is_cuda
+        if norm_type == float("inf"):
+            def amax(ps):
+                return torch.stack([p.grad.detach().abs().max().float() for p in ps]).max().reshape(1) if ps else torch.zeros(1, device=dev)
+
+            total = amax(sharded)
+            dist.all_reduce(total, op=dist.ReduceOp.MAX, group=group)
+            total = torch.maximum(total, amax(rest))
+            coef = (max_norm / (total + 1e-6)).clamp(max=1.0)
+            for p in grads_params:
+                p.grad.mul_(coef.to(p.grad.dtype))
+            return total.reshape(())
+        if norm_type != 2.0:
+            raise NotImplementedError(f"clip_grad_norm_ with tensor-parallel parameters supports norm_type 2 and inf, not {norm_type}")
 
         def sq(ps):
             if not ps:
@@ -1062,6 +1086,51 @@ class Accelerator:
             for p in grads_params:
                 p.grad.mul_(coef.to(p.grad.dtype))
         return total.sqrt().reshape(())
+
+    @staticmethod
+    @torch.no_grad()
+    def _clip_grad_norm_dtensor(grads_params, max_norm, norm_type=2.0):
+        """Parameters already sharded as DTensors (transformers `tp_plan="auto"` / torch `parallelize_module`): the
+        reference clips with DTensor-aware `torch.nn.utils.clip_grad_norm_` (accelerator.py:2943-2953). Here the
+        squares (or maxima) of Shard-placed gradients are reduced over their mesh, Replicate-placed and plain ones
+        count once, Partial ones are first reduced to Replicate; the scale is applied to the local shards."""
+        import torch.distributed as dist
+        from torch.distributed.tensor import DTensor, Replicate
+
+        inf = norm_type == float("inf")
+        if not inf and norm_type != 2.0:
+            raise NotImplementedError(f"clip_grad_norm_ on DTensor parameters supports norm_type 2 and inf, not {norm_type}")
+        dev = grads_params[0].grad.device
+        shard_part = torch.zeros(1, dtype=torch.float32, device=dev)
+        rest_part = torch.zeros(1, dtype=torch.float32, device=dev)
+        groups = []
+        for p in grads_params:
+            g = p.grad
+            if isinstance(g, DTensor):
+                if any(pl.is_partial() for pl in g.placements):
+                    g = p.grad = g.redistribute(placements=[Replicate() if pl.is_partial() else pl for pl in g.placements])
+                local = g.to_local().detach().float()
+                v = local.abs().max().reshape(1) if inf and local.numel() else local.pow(2).sum().reshape(1)
+                if any(pl.is_shard() for pl in g.placements):
+                    shard_part = torch.maximum(shard_part, v) if inf else shard_part + v
+                    for d, pl in enumerate(g.placements):
+                        if pl.is_shard():
+                            grp = g.device_mesh.get_group(d)
+                            if grp not in groups:
+                                groups.append(grp)
+                    continue
+            else:
+                local = g.detach().float()
+                v = local.abs().max().reshape(1) if inf and local.numel() else local.pow(2).sum().reshape(1)
+            rest_part = torch.maximum(rest_part, v) if inf else rest_part + v
+        for grp in groups:
+            dist.all_reduce(shard_part, op=dist.ReduceOp.MAX if inf else dist.ReduceOp.SUM, group=grp)
+        total = torch.maximum(shard_part, rest_part) if inf else (shard_part + rest_part).sqrt()
+        coef = (max_norm / (total + 1e-6)).clamp(max=1.0)
+        for p in grads_params:
+            g = p.grad.to_local() if isinstance(p.grad, DTensor) else p.grad
+            g.mul_(coef.to(g.dtype))
+        return total.reshape(())
 
     def clip_grad_value_(self, parameters, clip_value):
         if self.distributed_type in (DistributedType.FSDP,):

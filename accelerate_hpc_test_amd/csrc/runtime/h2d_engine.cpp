@@ -136,12 +136,15 @@ class H2DEngine {
     cv_.notify_all();
   }
 
-  // Close the files opened by copy_file (after every piece has been read).
-  void close_files() {
+  // Close the files opened by copy_file (after every piece has been read) and return the number of short reads
+  // since the last call, resetting it: the engine is cached per device for the process lifetime, so one failed
+  // load must not poison the next one.
+  int64_t close_files() {
     drain_issue();
     std::lock_guard<std::mutex> g(mu_);
     for (auto& kv : fds_) ::close(kv.second);
     fds_.clear();
+    return read_errors_.exchange(0);
   }
 
   // Block the host until every enqueued piece has been staged and its DMA issued, then make the caller's

@@ -59,7 +59,11 @@ class LocalSGD:
         gloo = dist.get_backend(group) == "gloo"
 
         def average(buf):
-            if gloo or not buf.dtype.is_floating_point:
+            if not buf.dtype.is_floating_point:  # integer / bool parameters: sum then floor-divide (stays integral)
+                dist.all_reduce(buf, group=group)
+                if buf.dtype != torch.bool:
+                    buf.div_(world, rounding_mode="floor")
+            elif gloo:
                 dist.all_reduce(buf, group=group)
                 buf.div_(world)
             else:
@@ -78,9 +82,8 @@ class LocalSGD:
                 off += n
 
         by_dtype: dict = {}
-        for p in model.parameters():
-            if p.dtype.is_floating_point:
-                by_dtype.setdefault((p.dtype, p.device), []).append(p)
+        for p in model.parameters():  # every dtype in its own buckets, like the reference's per-parameter reduce
+            by_dtype.setdefault((p.dtype, p.device), []).append(p)
         for params in by_dtype.values():
             batch, nbytes = [], 0
             for p in params:

@@ -59,11 +59,21 @@ def _record_inner_steps(optimizer):
             optimizer.step = own
 
 
+def _has_dtensor(optimizer) -> bool:
+    try:
+        from torch.distributed.tensor import DTensor
+    except ImportError:  # pragma: no cover
+        return False
+    return any(isinstance(p, DTensor) for g in optimizer.param_groups for p in g["params"])
+
+
 def _fused_adam_eligible(optimizer):
     """"gpu" (HIP multi-tensor kernel), "cpu" (native OpenMP kernel over CPU-offloaded fp32 shards) or None."""
     if os.environ.get("ACCELERATE_FUSED_ADAMW", "1") == "0" or os.environ.get("ACCELERATE_NATIVE_KERNELS", "1") == "0":
         return None
     if type(optimizer) not in (torch.optim.AdamW, torch.optim.Adam):
+        return None
+    if _has_dtensor(optimizer):  # DTensor wrappers own no storage: torch's DTensor-aware step
         return None
     devs = set()
     for g in optimizer.param_groups:

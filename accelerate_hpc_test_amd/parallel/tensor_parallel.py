@@ -398,9 +398,6 @@ def parallelize_module(model: nn.Module, group, plan: Optional[dict] = None, seq
     After sharding, modules exposing `shard_heads(tp_size)` (attention) adapt their local head counts. With
     `sequence_parallel`, gradients of replicated parameters are all-reduced across tp (they see different
     sequence shards)."""
-    plan = plan if plan is not None else get_tp_plan(model, sequence_parallel)
-    if plan is None:
-        raise ValueError("No tensor-parallel plan: pass `plan=` or give the model a `tp_plan()` / transformers `_tp_plan`.")
     W = comm.group_size(group)
     if W == 1:
         return model
@@ -409,10 +406,16 @@ def parallelize_module(model: nn.Module, group, plan: Optional[dict] = None, seq
     except ImportError:  # pragma: no cover
         DTensor = ()
     if any(isinstance(p, DTensor) for p in model.parameters()):
-        # already sharded by transformers (`from_pretrained(tp_plan="auto", device_mesh=...)`, the reference's flow):
-        # keep its DTensor layout
+        # already sharded by transformers (`from_pretrained(tp_plan="auto", device_mesh=...)`, the reference's flow) or
+        # torch's `parallelize_module`: keep its DTensor layout. The optimizer then runs torch's DTensor-aware AdamW
+        # (the fused HIP kernel needs plain storage, optimizer._fused_adam_eligible) and the gradient norm sums the
+        # sharded placements over their mesh (Accelerator._clip_grad_norm_dtensor).
         model._tp_group, model._tp_size, model._tp_sequence_parallel = group, W, False
+        model._tp_dtensor = True
         return model
+    plan = plan if plan is not None else get_tp_plan(model, sequence_parallel)
+    if plan is None:
+        raise ValueError("No tensor-parallel plan: pass `plan=` or give the model a `tp_plan()` / transformers `_tp_plan`.")
     _PARAM_MAP.clear()
     matched = set()
     for name, module in list(model.named_modules()):

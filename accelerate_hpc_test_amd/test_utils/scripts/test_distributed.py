@@ -324,7 +324,8 @@ def _tiny_llama_cfg():
                        num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=64)
 
 
-def check_tp_matches_single(sequence_parallel: bool = False, dp_shard: int = 1, steps: int = 2, dp_replicate: int = 1):
+def check_tp_matches_single(sequence_parallel: bool = False, dp_shard: int = 1, steps: int = 2, dp_replicate: int = 1,
+                            norm_type: float = 2.0):
     """TP (optionally sequence-parallel, optionally x FSDP over dp_shard, optionally x HSDP replicas) must train
     exactly like one process on the global batch: same loss, same global gradient norm, same full weights after
     `steps` steps. The norm is the reference's DTensor-aware `clip_grad_norm_` over the whole mesh
@@ -361,12 +362,12 @@ def check_tp_matches_single(sequence_parallel: bool = False, dp_shard: int = 1, 
         out = model(local, labels=local)
         acc.backward(out.loss)
         # the global gradient norm: tp-sharded squares summed over the group, replicated ones counted once
-        gn = acc.clip_grad_norm_(model.parameters(), 1e9)
+        gn = acc.clip_grad_norm_(model.parameters(), 1e9, norm_type=norm_type)
         opt.step()
         opt.zero_grad()
         ref = base(ids, labels=ids)
         ref.loss.backward()
-        gn_ref = torch.nn.utils.clip_grad_norm_(base.parameters(), 1e9)
+        gn_ref = torch.nn.utils.clip_grad_norm_(base.parameters(), 1e9, norm_type=norm_type)
         assert torch.allclose(gn.float(), gn_ref.float(), rtol=1e-4), (gn, gn_ref)
         base_opt.step()
         base_opt.zero_grad()
@@ -376,6 +377,50 @@ def check_tp_matches_single(sequence_parallel: bool = False, dp_shard: int = 1, 
     for n, q in base.state_dict().items():
         assert full[n].shape == q.shape, (n, full[n].shape, q.shape)
         assert torch.allclose(full[n].float(), q.float(), atol=2e-5), (n, (full[n] - q).abs().max())
+
+
+def check_tp_dtensor_model(steps: int = 3, norm_type: float = 2.0):
+    """A model already sharded as DTensors (torch `parallelize_module`, the layout transformers' `tp_plan="auto"`
+    produces in the reference's nd-parallel flow) goes through `prepare` unchanged; AdamW runs torch's DTensor-aware
+    step (not the fused HIP kernel) and `clip_grad_norm_` reduces the sharded placements over the mesh: losses, norms
+    and full weights == one process."""
+    from torch.distributed.device_mesh import init_device_mesh
+    from torch.distributed.tensor import DTensor
+    from torch.distributed.tensor.parallel import ColwiseParallel, RowwiseParallel
+    from torch.distributed.tensor.parallel import parallelize_module as torch_parallelize
+
+    from accelerate_hpc_test_amd import ParallelismConfig
+
+    W = int(os.environ["WORLD_SIZE"])
+    acc = Accelerator(cpu=True, parallelism_config=ParallelismConfig(tp_size=W))
+    torch.manual_seed(0)
+    base = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 4))
+    model = copy.deepcopy(base)
+    mesh = init_device_mesh("cpu", (W,))
+    torch_parallelize(model, mesh, {"0": ColwiseParallel(), "2": RowwiseParallel()})
+    assert any(isinstance(p, DTensor) for p in model.parameters())
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-2)
+    base_opt = torch.optim.AdamW(base.parameters(), lr=1e-2)
+    model, opt = acc.prepare(model, opt)
+    assert opt._maybe_fused() is False, "DTensor parameters must not take the fused HIP AdamW"
+    g = torch.Generator().manual_seed(1)
+    for _ in range(steps):
+        x, y = torch.randn(6, 8, generator=g), torch.randn(6, 4, generator=g)
+        loss = F.mse_loss(model(x), y)
+        acc.backward(loss)
+        gn = acc.clip_grad_norm_(model.parameters(), 0.05, norm_type=norm_type)
+        opt.step()
+        opt.zero_grad()
+        ref = F.mse_loss(base(x), y)
+        ref.backward()
+        gn_ref = torch.nn.utils.clip_grad_norm_(base.parameters(), 0.05, norm_type=norm_type)
+        base_opt.step()
+        base_opt.zero_grad()
+        assert torch.allclose(loss.detach(), ref.detach(), atol=1e-6), (loss, ref)
+        assert torch.allclose(gn.float(), gn_ref.float(), rtol=1e-5), (gn, gn_ref)
+    for (n, p), q in zip(model.named_parameters(), base.parameters()):
+        full = p.full_tensor() if isinstance(p, DTensor) else p
+        assert torch.allclose(full.detach(), q.detach(), atol=1e-6), (n, (full - q).abs().max())
 
 
 def check_ring_attention(strategy: str = "allgather"):
@@ -559,6 +604,26 @@ def check_local_sgd(k: int = 2, steps: int = 4, chunk_bytes: int = 256 << 20):
     inner = acc.unwrap_model(model)
     for (n, p), q in zip(inner.named_parameters(), sims[0].parameters()):
         assert torch.allclose(p, q, atol=1e-6), (n, (p - q).abs().max())
+
+
+def check_local_sgd_integer_params():
+    """Non-float parameters (e.g. an integer step counter registered as a frozen Parameter) are averaged too, in
+    their own buckets (sum, then floor division), as the reference's per-parameter `reduce(param, "mean")` does."""
+    from accelerate_hpc_test_amd.local_sgd import LocalSGD
+
+    acc = Accelerator(cpu=True)
+    W, r = acc.num_processes, acc.process_index
+    set_seed(0)
+    model = TinyMLP()
+    model.counter = torch.nn.Parameter(torch.zeros(2, dtype=torch.int64), requires_grad=False)
+    opt = torch.optim.SGD([p for p in model.parameters() if p.is_floating_point()], lr=0.1)
+    model, opt = acc.prepare(model, opt)
+    acc.unwrap_model(model).counter.data.copy_(torch.tensor([10 * (r + 1), 3 * r]))  # diverged after DDP's broadcast
+    with LocalSGD(acc, model, local_sgd_steps=1) as local_sgd:
+        local_sgd.step()
+    inner = acc.unwrap_model(model)
+    want = torch.tensor([sum(10 * (j + 1) for j in range(W)) // W, sum(3 * j for j in range(W)) // W])
+    assert inner.counter.dtype == torch.int64 and torch.equal(inner.counter.data, want), (inner.counter, want)
 
 
 def _local_sgd_loop(acc, model, opt, sims, sim_opts, batches, W, r, bs, k, chunk_bytes):

@@ -535,28 +535,36 @@ for _name, _check in (
         _available_trackers.append(_name)
 
 
+def _resolve_tracker(entry, logging_dir):
+    """One `log_with` entry -> a GeneralTracker instance, a usable LoggerType, or None (package not installed)."""
+    if isinstance(entry, GeneralTracker):
+        return entry
+    try:
+        kind = LoggerType(entry)
+    except ValueError:
+        raise ValueError(f"Unsupported logging capability: {entry}. Choose between {LoggerType.list()}") from None
+    name = str(kind)
+    if name not in get_available_trackers():
+        logger.debug(f"Tracker `{name}` requested but its package is not installed; skipping it.")
+        return None
+    if LOGGER_TYPE_TO_CLASS[name].requires_logging_directory and logging_dir is None:
+        raise ValueError(f"Logging with `{name}` requires a `logging_dir` to be passed in.")
+    return kind
+
+
 def filter_trackers(log_with: Optional[list[Union[str, LoggerType, GeneralTracker]]] = None, logging_dir: Union[str, os.PathLike] = None):
-    """Resolve `log_with` to the list of usable trackers (`"all"` = every installed one)."""
-    loggers = []
-    if log_with is not None:
-        if not isinstance(log_with, (list, tuple)):
-            log_with = [log_with]
-        if "all" in log_with or LoggerType.ALL in log_with:
-            loggers = [o for o in log_with if issubclass(type(o), GeneralTracker)] + get_available_trackers()
-        else:
-            for log_type in log_with:
-                if log_type not in LoggerType and not issubclass(type(log_type), GeneralTracker):
-                    raise ValueError(f"Unsupported logging capability: {log_type}. Choose between {LoggerType.list()}")
-                if issubclass(type(log_type), GeneralTracker):
-                    loggers.append(log_type)
-                else:
-                    log_type = LoggerType(log_type)
-                    if log_type not in loggers:
-                        if str(log_type) in get_available_trackers():
-                            tracker_init = LOGGER_TYPE_TO_CLASS[str(log_type)]
-                            if tracker_init.requires_logging_directory and logging_dir is None:
-                                raise ValueError(f"Logging with `{log_type}` requires a `logging_dir` to be passed in.")
-                            loggers.append(log_type)
-                        else:
-                            logger.debug(f"Tried adding logger {log_type}, but package is unavailable in the system.")
-    return loggers
+    """Resolve `log_with` to the list of usable trackers: custom tracker objects pass through, names / LoggerTypes
+    are kept when their package is installed (checking the logging-directory requirement), "all" expands to every
+    installed tracker. Behaviour: reference tracking.py:1262-1317."""
+    if log_with is None:
+        return []
+    entries = list(log_with) if isinstance(log_with, (list, tuple)) else [log_with]
+    custom = [e for e in entries if isinstance(e, GeneralTracker)]
+    if any(e == "all" or e == LoggerType.ALL for e in entries if not isinstance(e, GeneralTracker)):
+        return custom + get_available_trackers()
+    resolved = []
+    for entry in entries:
+        t = _resolve_tracker(entry, logging_dir)
+        if t is not None and (isinstance(t, GeneralTracker) or t not in resolved):
+            resolved.append(t)
+    return resolved

@@ -242,13 +242,25 @@ class _Installer:
                 return
         set_module_tensor_to_device(self.model, name, dest, value=t, dtype=dt, clear_cache=False)
 
+    def release(self):
+        """Close every shard file the engines opened and return the short-read count (reset in the engine); safe to
+        call on an error path (the `finally` of `load_checkpoint_in_model`)."""
+        errors = 0
+        for eng in self.engines:
+            if hasattr(eng, "close_files"):
+                try:
+                    eng.wait_on_current_stream()
+                finally:
+                    errors += int(eng.close_files() or 0)
+        return errors
+
     def finish(self):
         for eng in self.engines:
             eng.wait_on_current_stream()
-            if hasattr(eng, "close_files"):
-                eng.close_files()
-                if eng.read_errors():
-                    raise OSError(f"checkpoint loading: {eng.read_errors()} short read(s) from the shard files")
+        errors = self.release()
+        self.engines = set()
+        if errors:
+            raise OSError(f"checkpoint loading: {errors} short read(s) from the shard files")
         if self.disk is not None:
             self.disk.flush_index()
         if self.host_spill is not None:
@@ -344,17 +356,20 @@ def load_checkpoint_in_model(
     else:
         files = checkpoint_files(checkpoint)
         inst = _Installer(model, device_map, dtype, keep_in_fp32_modules, offload_folder, offload_state_dict, offload_buffers, strict)
-        for path in files:
-            shard = load_state_dict(path, device_map=device_map)
-            layout = shard.layout() if isinstance(shard, SafetensorsShard) else {}
-            for name in list(shard.keys()):
-                lay = layout.get(name)
-                if lay is not None and inst.put_from_file(name, path, *lay):
-                    continue
-                inst.put(name, shard[name])  # one tensor resident at a time for safetensors shards
-            del shard
-            gc.collect()
-        inst.finish()
+        try:
+            for path in files:
+                shard = load_state_dict(path, device_map=device_map)
+                layout = shard.layout() if isinstance(shard, SafetensorsShard) else {}
+                for name in list(shard.keys()):
+                    lay = layout.get(name)
+                    if lay is not None and inst.put_from_file(name, path, *lay):
+                        continue
+                    inst.put(name, shard[name])  # one tensor resident at a time for safetensors shards
+                del shard
+                gc.collect()
+            inst.finish()
+        finally:
+            inst.release()  # no-op after finish(); on an error path closes the shard files and clears the error count
         unexpected = inst.unexpected
     if unexpected:
         logger.warning(

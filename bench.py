@@ -277,7 +277,8 @@ def main():
                 "moe": {"experts": cfg.num_local_experts, "top_k": cfg.num_experts_per_tok} if is_moe else None,
                 "global_batch": args.mbs * world,
                 "seq_len": args.seq,
-                "parallelism": f"{args.parallel}{world}" + ("-forced-sharded" if force else "")
+                # "-w1": one rank, the engine's no-collective path; "-forced-sharded": one rank running the multi-rank code
+                "parallelism": f"{args.parallel}-w{world}" + ("-forced-sharded" if force else "")
                 + ("-forced-reducer" if force_ddp else ""),
                 "optimizer": "AdamW(lr=1e-5), fp32 master" + (", bf16 moments" if args.adam_states == "bf16" else "")
                 + (", per-unit update overlapped with backward" if overlap else "")

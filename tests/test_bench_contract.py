@@ -27,7 +27,7 @@ def test_bench_two_ranks_prints_one_json_line(tmp_path):
         assert k in rec, k
     assert rec["n_gpus"] == 2 and rec["steps"] == 2 and rec["warmup"] == 1 and rec["scaling"] == "weak"
     assert rec["config"]["global_batch"] == 2 and rec["config"]["seq_len"] == 256 and rec["config"]["model"] == "llama-tiny"
-    assert rec["config"]["parallelism"] == "fsdp2" and rec["vs_baseline"] is None  # not the headline model
+    assert rec["config"]["parallelism"] == "fsdp-w2" and rec["vs_baseline"] is None  # not the headline model
     pf = rec["preflight"]  # every communicator checked before training (utils/preflight.py)
     assert pf["world"]["ok"] and pf["fsdp_all_gather"]["ok"] and pf["fsdp_reduce_scatter"]["ok"], pf
     # value is the whole-job rate: all ranks' tokens over the slowest rank's timed window
@@ -47,7 +47,7 @@ def test_bench_spawns_its_own_ranks(tmp_path):
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
     rec = json.loads(lines[0])
-    assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "fsdp2" and rec["config"]["global_batch"] == 2
+    assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "fsdp-w2" and rec["config"]["global_batch"] == 2
 
 
 def test_rccl_bench_tool_gloo_plumbing():

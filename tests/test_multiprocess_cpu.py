@@ -84,6 +84,11 @@ def test_tensor_parallel_matches_single_process(sequence_parallel):
     debug_launcher(td.check_tp_matches_single, args=(sequence_parallel,), num_processes=2)
 
 
+def test_tensor_parallel_inf_norm():
+    """norm_type=inf under TP: the sharded parameters' max is MAX-reduced over the tp group."""
+    debug_launcher(td.check_tp_matches_single, args=(False, 1, 2, 1, float("inf")), num_processes=2)
+
+
 def test_tensor_parallel_x_fsdp_2d():
     """dp_shard 2 x tp 2: loss, global grad norm and weights == one process (the norm sums tp-sharded squares over
     tp as well as dp_shard)."""
@@ -98,6 +103,11 @@ def test_tensor_parallel_x_hsdp_3d():
 def test_context_parallel_x_fsdp_2d():
     """dp_shard 2 x cp 2: ring attention inside FSDP over the flattened dp_shard x cp mesh == one process."""
     debug_launcher(td.check_cp_llama_matches_single, args=("allgather", 2, 2), num_processes=4)
+
+
+@pytest.mark.parametrize("norm_type", [2.0, float("inf")])
+def test_tensor_parallel_dtensor_model_trains_like_single_process(norm_type):
+    debug_launcher(td.check_tp_dtensor_model, args=(3, norm_type), num_processes=2)
 
 
 @pytest.mark.parametrize("strategy", ["allgather", "alltoall"])
@@ -168,6 +178,10 @@ def test_fsdp_checkpoint_io_is_per_rank_bounded(sd_type, load_world, tmp_path):
     d = str(tmp_path / "ckpt")
     debug_launcher(td.check_fsdp_checkpoint_io, args=("save", d, sd_type), num_processes=4)
     debug_launcher(td.check_fsdp_checkpoint_io, args=("load", d, sd_type), num_processes=load_world)
+
+
+def test_local_sgd_averages_integer_params():
+    debug_launcher(td.check_local_sgd_integer_params, num_processes=2)
 
 
 def test_fsdp_three_ranks():

@@ -97,7 +97,12 @@ def _split_parity_worker():
 
     from accelerate_hpc_test_amd.state import PartialState
 
+    # upstream's PartialState is a Borg too: a forked rank inherits whatever single-process state an earlier test in the
+    # same pytest worker left in the parent (seen as an intermittent failure under `pytest -n 8`), so start clean
+    accelerate.state.AcceleratorState._reset_state(True)
+    accelerate.state.PartialState._reset_state()
     ours_state, up_state = PartialState(cpu=True), accelerate.PartialState(cpu=True)
+    assert up_state.num_processes == ours_state.num_processes > 1, (up_state.num_processes, ours_state.num_processes)
     for inputs, pad in _split_cases():
         with ours_state.split_between_processes(copy.deepcopy(inputs), apply_padding=pad) as a:
             with up_state.split_between_processes(copy.deepcopy(inputs), apply_padding=pad) as b:
@@ -129,7 +134,11 @@ def _split_parity_worker():
 def test_split_between_processes_matches_upstream(world):
     """Our `split_between_processes` (own implementation, no padding collective) against the upstream accelerate in
     the image on 2 and 3 gloo ranks, for lists, tuples, 1-D / 2-D tensors (with and without padding) and dicts."""
+    # import upstream accelerate (and what it pulls in) in the parent: the forked ranks then share the loaded modules
+    # instead of each importing the package concurrently while `pytest -n 8` saturates the CPUs
     pytest.importorskip("accelerate")
+    import accelerate.state  # noqa: F401
+
     from accelerate_hpc_test_amd import debug_launcher
 
     debug_launcher(_split_parity_worker, num_processes=world)
