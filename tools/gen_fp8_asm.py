@@ -143,18 +143,26 @@ def body(dma_on: bool, wait_next: bool, read_next: bool):
     return lines
 
 
-def prologue():
-    L = []
-    L += [f"s_mov_b32 s{M0_KEEP}, m0",
-          f"s_mov_b64 s[{SRD_A}:{SRD_A + 1}], %[pa]", f"s_mov_b32 s{SRD_A + 2}, -1", f"s_mov_b32 s{SRD_A + 3}, 0x20000",
-          f"s_mov_b64 s[{SRD_B}:{SRD_B + 1}], %[pb]", f"s_mov_b32 s{SRD_B + 2}, -1", f"s_mov_b32 s{SRD_B + 3}, 0x20000",
-          f"s_mov_b32 s{SOFF}, %[stride]"]
+def setup(k_tiles_skipped: int):
+    """SRDs at K-tile `k_tiles_skipped` of this tile's A / B rows, soffsets, DMA destinations of buffer 0."""
+    L = [f"s_mov_b32 s{M0_KEEP}, m0",
+         f"s_mov_b64 s[{SRD_A}:{SRD_A + 1}], %[pa]", f"s_mov_b32 s{SRD_A + 2}, -1", f"s_mov_b32 s{SRD_A + 3}, 0x20000",
+         f"s_mov_b64 s[{SRD_B}:{SRD_B + 1}], %[pb]", f"s_mov_b32 s{SRD_B + 2}, -1", f"s_mov_b32 s{SRD_B + 3}, 0x20000",
+         f"s_mov_b32 s{SOFF}, %[stride]"]
     for n in range(1, 7):
         L.append(f"s_add_u32 s{SOFF + n}, s{SOFF + n - 1}, %[stride]")
+    for _ in range(k_tiles_skipped):
+        L += advance_srd("A") + advance_srd("B")
     L += [f"s_mov_b32 s{M0_A}, %[m0a]", f"s_add_u32 s{M0_B}, %[m0a], 33792",
-          f"s_add_u32 s{M0_X}, %[m0a], 67584", f"s_xor_b32 s{M0_X}, s{M0_X}, %[m0a]",
-          f"s_mov_b32 s{CNT}, %[cnt]"]
-    # tile 0 -> buffer 0, tile 1 -> buffer 1
+          f"s_add_u32 s{M0_X}, %[m0a], 67584", f"s_xor_b32 s{M0_X}, s{M0_X}, %[m0a]"]
+    return L
+
+
+def issue():
+    """DMA of K-tiles 0 and 1 of a tile into LDS buffers 0 and 1. Issued for the NEXT tile of a persistent
+    workgroup before the current tile's epilogue (every wave passed the last body's final barrier after its last
+    ds_read, so both buffers are free), which hides the first loads' latency under the epilogue."""
+    L = setup(0)
     for tile in range(2):
         L.append(f"s_mov_b32 m0, s{M0_B}")
         L.append("s_nop 0")
@@ -164,8 +172,19 @@ def prologue():
         L.append("s_nop 0")
         for n in range(8):
             L += dma("A", n)
-        L += advance_srd("A") + advance_srd("B")
-        L += [f"s_xor_b32 s{M0_A}, s{M0_A}, s{M0_X}", f"s_xor_b32 s{M0_B}, s{M0_B}, s{M0_X}"]
+        if tile == 0:
+            L += advance_srd("A") + advance_srd("B")
+            L += [f"s_xor_b32 s{M0_A}, s{M0_A}, s{M0_X}", f"s_xor_b32 s{M0_B}, s{M0_B}, s{M0_X}"]
+    L.append(f"s_mov_b32 m0, s{M0_KEEP}")
+    return L
+
+
+def main_loop():
+    """Everything after `issue()`: zero the accumulators, K-tile 0's fragments, the loop and the 2-tile tail.
+    vmcnt(16) at the start: the 32 DMAs of `issue()` plus whatever epilogue stores the previous tile issued after
+    them (vmcnt counts in order) -> at most the 16 newest may still be in flight, so K-tile 0 has landed."""
+    L = setup(2)
+    L.append(f"s_mov_b32 s{CNT}, %[cnt]")
     for a in range(256):
         L.append(f"v_accvgpr_write_b32 a{a}, 0")
     L += ["s_waitcnt vmcnt(16)", "s_barrier"]
@@ -174,28 +193,29 @@ def prologue():
     for f in range(4):
         L += ds_frag(A_BASE, f, "%[va]")
     L += ["s_waitcnt lgkmcnt(0)"]
-    return L
-
-
-def generate() -> str:
-    L = prologue()
     L += [f"s_cmp_eq_u32 s{CNT}, 0", "s_cbranch_scc1 2f", "1:"]
     L += body(dma_on=True, wait_next=True, read_next=True)
     L += [f"s_sub_u32 s{CNT}, s{CNT}, 1", f"s_cmp_eq_u32 s{CNT}, 0", "s_cbranch_scc0 1b", "2:"]
     L += body(dma_on=False, wait_next=True, read_next=True)
     L += body(dma_on=False, wait_next=False, read_next=False)
-    L += ["s_nop 7", "s_nop 7", f"s_mov_b32 m0, s{M0_KEEP}"]
+    L += ["s_nop 7", "s_nop 7", "s_nop 7", f"s_mov_b32 m0, s{M0_KEEP}"]
+    return L
+
+
+def generate() -> str:
+    I, L = issue(), main_loop()
     n_mfma = sum(1 for x in L if x.startswith("v_mfma"))
     assert n_mfma == 3 * 64, n_mfma
     out = ["// GENERATED by tools/gen_fp8_asm.py -- do not edit by hand; edit the generator and rerun it.",
-           "// Main loop of fp8_gemm_asm_kernel (csrc/kernels/fp8_gemm_asm.hip): see the generator's docstring.",
-           f"// {len(L)} lines, {n_mfma} MFMAs (loop body 64).",
-           "#pragma once",
-           "#define FP8ASM_MAIN_LOOP \\"]
-    for x in L:
-        out.append(f'  "{x}\\n" \\')
-    out.append('  ""')
-    out.append("")
+           "// K-loop of fp8_gemm_asm_kernel (csrc/kernels/fp8_gemm_asm.hip): see the generator's docstring.",
+           f"// FP8ASM_ISSUE {len(I)} lines; FP8ASM_MAIN_LOOP {len(L)} lines, {n_mfma} MFMAs (loop body 64).",
+           "#pragma once"]
+    for name, lines in (("FP8ASM_ISSUE", I), ("FP8ASM_MAIN_LOOP", L)):
+        out.append(f"#define {name} \\")
+        for x in lines:
+            out.append(f'  "{x}\\n" \\')
+        out.append('  ""')
+        out.append("")
     out.append(f"#define FP8ASM_SGPR_CLOBBERS " + ", ".join(f'"s{s}"' for s in range(SRD_A, M0_KEEP + 1)))
     out.append("")
     return "\n".join(out)
