@@ -77,6 +77,7 @@ std::vector<torch::Tensor> mx_quant(torch::Tensor x, bool e5m2, bool colwise);
 torch::Tensor mx_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor sa, torch::Tensor sb, double smul,
                       c10::optional<torch::Tensor> bias, bool out_fp32, c10::optional<torch::Tensor> out_opt, bool accumulate);
 void fp8_gemm_select(int64_t variant, int64_t group_m);
+torch::Tensor fp8asm_dma_probe(torch::Tensor a, torch::Tensor b);
 // grouped_gemm.hip
 void grouped_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor out, torch::Tensor seg, int64_t mode, torch::Tensor sa,
                   torch::Tensor sb, double smul, bool accumulate);
@@ -155,6 +156,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sar_status", &sar_status);
   m.def("sar_allreduce_local_group", &sar_allreduce_local_group);
   m.def("sar_destroy", &sar_destroy);
+  m.def("fp8asm_dma_probe", &fp8asm_dma_probe, "debug: LDS image after the asm GEMM's first-tile DMA");
   m.def("fp8_gemm_select", &fp8_gemm_select, pybind11::arg("variant"), pybind11::arg("group_m") = 0);
   register_runtime(m);
   m.def("blaslt_dgrad_bf16", &blaslt_dgrad_bf16, pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("out"),

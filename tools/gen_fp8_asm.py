@@ -44,7 +44,8 @@ SRD_B = 44    # s[44:47]
 SOFF = 48     # s48..s54 = j * 32 * K, j = 1..7
 M0_A = 56     # LDS-DMA destination of this wave's first A chunk in the current buffer
 M0_B = 57
-M0_X = 58     # xor toggling both destinations between buffer 0 and 1
+M0_X = 58     # xor toggling the A destination between buffer 0 and 1
+M0_XB = 55    # the same for B (an xor mask toggles only the base it was computed from)
 CNT = 59      # main-loop trips left
 M0_KEEP = 60  # caller's m0
 CHUNK_STEP = 4 * 1056  # m0 advance per DMA instruction (4 waves x one 1056-B chunk)
@@ -133,7 +134,7 @@ def body(dma_on: bool, wait_next: bool, read_next: bool):
     if dma_on:
         slots[53] += dma("A", 7)
         slots[55] += advance_srd("A")
-        slots[57] += [f"s_xor_b32 s{M0_A}, s{M0_A}, s{M0_X}", f"s_xor_b32 s{M0_B}, s{M0_B}, s{M0_X}"]
+        slots[57] += [f"s_xor_b32 s{M0_A}, s{M0_A}, s{M0_X}", f"s_xor_b32 s{M0_B}, s{M0_B}, s{M0_XB}"]
     if read_next:
         slots[61] += ["s_waitcnt lgkmcnt(0)"]
     lines = []
@@ -154,7 +155,8 @@ def setup(k_tiles_skipped: int):
     for _ in range(k_tiles_skipped):
         L += advance_srd("A") + advance_srd("B")
     L += [f"s_mov_b32 s{M0_A}, %[m0a]", f"s_add_u32 s{M0_B}, %[m0a], 33792",
-          f"s_add_u32 s{M0_X}, %[m0a], 67584", f"s_xor_b32 s{M0_X}, s{M0_X}, %[m0a]"]
+          f"s_add_u32 s{M0_X}, %[m0a], 67584", f"s_xor_b32 s{M0_X}, s{M0_X}, %[m0a]",
+          f"s_add_u32 s{M0_XB}, s{M0_B}, 67584", f"s_xor_b32 s{M0_XB}, s{M0_XB}, s{M0_B}"]
     return L
 
 
@@ -174,7 +176,7 @@ def issue():
             L += dma("A", n)
         if tile == 0:
             L += advance_srd("A") + advance_srd("B")
-            L += [f"s_xor_b32 s{M0_A}, s{M0_A}, s{M0_X}", f"s_xor_b32 s{M0_B}, s{M0_B}, s{M0_X}"]
+            L += [f"s_xor_b32 s{M0_A}, s{M0_A}, s{M0_X}", f"s_xor_b32 s{M0_B}, s{M0_B}, s{M0_XB}"]
     L.append(f"s_mov_b32 m0, s{M0_KEEP}")
     return L
 

@@ -93,6 +93,8 @@ for step in "$@"; do
     attn_long) run attn_long 300 python tools/bench_attn.py --S 32768 --iters 3 ;;
     pmc_attn) run pmc_attn 200 bash tools/pmc_attn.sh ;;
     gemm) run gemm 300 python tools/bench_gemm.py ;;
+    asmdiag) run asmdiag 120 python tools/debug/fp8asm_diag.py ;;
+    asmprobe) run asmprobe 120 python tools/debug/fp8asm_probe.py ;;
     mr_tp) run mr_tp 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_multirank.py -k "tp" ;;
     gemm_asm) run ktest_asm 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "fp8_gemm_v4" && \
               run gemm_asm 400 python tools/bench_gemm.py --variants ${GEMM_VARIANTS:-bl,18,17} --no-bf16 --no-scaled-mm --rounds 3 --check ;;
