@@ -1987,18 +1987,20 @@ void fp8_cast_batched_into(torch::Tensor x, torch::Tensor amax, double qmax, tor
 // through registers instead of LDS-DMA) scaled / unscaled, 16 / 17 = v8 (v7 with 8 waves in a barrier-staggered
 // ping-pong) scaled / unscaled.
 // Shapes a variant cannot tile fall back to the next one that can (v3 -> v2 -> v1).
-constexpr int kFp8GemmDefault = 17;  // v8 unscaled: the fastest HIP variant at all 12 shapes (profiles/r4_gemm_fp8.md)
+constexpr int kFp8GemmDefault = 18;  // the asm-scheduled kernel (fp8_gemm_asm.hip; profiles/r5_gemm_fp8_asm.md); v8 for other shapes
 // variant 18: the hand-scheduled asm main loop (fp8_gemm_asm.hip)
 bool fp8_gemm_asm_launch(const uint8_t* a, const uint8_t* b, const float* sa, const float* sb, float smul,
                          const bf16_t* bias, void* c, int M, int N, int K, bool a_e5m2, bool b_e5m2, bool out_f32,
                          bool accum, int group_m, hipStream_t stream);
 static int g_fp8_gemm_variant = 0;
 static int g_fp8_gemm_group_m = 4;  // v3 tile-row grouping (1 = plain row-major tile order)
+static int g_fp8_asm_group_m = 0;   // variant 18's grouping; 0 = by shape (fp8_gemm_asm_launch)
 void fp8_gemm_select(int64_t variant, int64_t group_m) {
   TORCH_CHECK(variant >= 0 && variant <= 18, "fp8_gemm_select: variant 0..18");
   TORCH_CHECK(group_m >= 0 && group_m <= 64, "fp8_gemm_select: group_m 0..64");
   g_fp8_gemm_variant = (int)variant;
   if (group_m > 0) g_fp8_gemm_group_m = (int)group_m;
+  g_fp8_asm_group_m = (int)group_m;
 }
 
 // C = (a . b^T) * sa[0] * sb[0] * smul (+ bias): sa / sb are inverse scales, or amax buffers with smul = 1/(qa*qb).
@@ -2044,7 +2046,7 @@ torch::Tensor fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor a_scale_i
   if (variant == 0) variant = force_v1 ? 1 : (env_w8 ? 3 : kFp8GemmDefault);
   if (variant == 18) {
     if (fp8_gemm_asm_launch(ap, bptr, sap, sbp, (float)smul, bp, cp, M, N, K, a_e5m2, b_e5m2, out_fp32, accumulate,
-                            g_fp8_gemm_group_m, stream))
+                            g_fp8_asm_group_m, stream))
       return out;
     variant = 17;
   }

@@ -33,10 +33,17 @@ from ._ext import ext, use_native
 
 E4M3_MAX = 448.0
 E5M2_MAX = 57344.0
-# Per-tensor-scaled fp8 GEMM backend: "blaslt" = hipBLASLt's fp8 kernels through our runner (csrc/runtime/blaslt_gemm.cpp;
-# 2.7-3.4 PF/s on the Llama-3-8B shapes vs 2.1-2.7 PF/s for the hand-written MX-MFMA kernel, profiles/r3_gemm_fp8_library.md),
-# "hip" = the hand-written kernel (csrc/kernels/fp8.hip), which also takes every problem hipBLASLt declines (bias epilogue).
-_FP8_GEMM_BACKEND = os.environ.get("ACCELERATE_FP8_GEMM", "blaslt")
+# Per-tensor-scaled fp8 GEMM backend. "hip" (default) = the hand-written kernels: the asm-scheduled 256x256 kernel
+# (csrc/kernels/fp8_gemm_asm.hip, 0.95-1.04x hipBLASLt on the Llama-3-8B shapes, profiles/r5_gemm_fp8_asm.md) for
+# every M, N multiple of 256 and K multiple of 128, the HIP-only variants of csrc/kernels/fp8.hip for a bias epilogue;
+# other shapes take hipBLASLt when it accepts them. "blaslt" = hipBLASLt's fp8 kernels through our runner
+# (csrc/runtime/blaslt_gemm.cpp) whenever there is no bias.
+_FP8_GEMM_BACKEND = os.environ.get("ACCELERATE_FP8_GEMM", "hip")
+
+
+def _asm_tileable(m: int, n: int, k: int) -> bool:
+    """Shapes the asm-scheduled kernel tiles (fp8_gemm_asm_launch's host check)."""
+    return m % 256 == 0 and n % 256 == 0 and k % 128 == 0 and k >= 256 and 256 * k < 2**31
 
 
 def amax(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -125,7 +132,9 @@ def gemm(a8: torch.Tensor, b8: torch.Tensor, a_scale_inv, b_scale_inv, bias=None
         e5b = b8.dtype == torch.float8_e5m2
         ta, ma = _inv_parts(a_scale_inv)
         tb, mb = _inv_parts(b_scale_inv)
-        if bias is None and _FP8_GEMM_BACKEND == "blaslt":
+        m, k = a8.shape
+        n = b8.shape[0]
+        if bias is None and (_FP8_GEMM_BACKEND == "blaslt" or not _asm_tileable(m, n, k)):
             dst = out if out is not None else torch.empty((a8.shape[0], b8.shape[0]), dtype=out_dtype, device=a8.device)
             if ext().blaslt_fp8_gemm(a8, b8, ta, tb, ma * mb, dst, accumulate):
                 return dst
