@@ -78,6 +78,7 @@ torch::Tensor mx_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor sa, torch:
                       c10::optional<torch::Tensor> bias, bool out_fp32, c10::optional<torch::Tensor> out_opt, bool accumulate);
 void fp8_gemm_select(int64_t variant, int64_t group_m);
 torch::Tensor fp8asm_dma_probe(torch::Tensor a, torch::Tensor b);
+bool bf16_gemm_asm(torch::Tensor a, torch::Tensor b, c10::optional<torch::Tensor> bias, torch::Tensor out, bool accumulate);
 // grouped_gemm.hip
 void grouped_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor out, torch::Tensor seg, int64_t mode, torch::Tensor sa,
                   torch::Tensor sb, double smul, bool accumulate);
@@ -156,6 +157,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sar_status", &sar_status);
   m.def("sar_allreduce_local_group", &sar_allreduce_local_group);
   m.def("sar_destroy", &sar_destroy);
+  m.def("bf16_gemm_asm", &bf16_gemm_asm, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("bias"), pybind11::arg("out"),
+        pybind11::arg("accumulate") = false, "bf16 out (=|+=) a . b^T (+ bias) on the asm-scheduled GEMM; false = shape not tiled");
   m.def("fp8asm_dma_probe", &fp8asm_dma_probe, "debug: LDS image after the asm GEMM's first-tile DMA");
   m.def("fp8_gemm_select", &fp8_gemm_select, pybind11::arg("variant"), pybind11::arg("group_m") = 0);
   register_runtime(m);

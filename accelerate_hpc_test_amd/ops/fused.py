@@ -20,6 +20,40 @@ _BLASLT_WGRAD = os.environ.get("ACCELERATE_BLASLT_WGRAD", "1") != "0"
 # dgrad dx = dy . W in its natural NN layout on the searched hipBLASLt runner (opt-in until measured faster than the
 # transposed-weight path below, tools/bench_dgrad.py)
 _DGRAD_BLASLT = os.environ.get("ACCELERATE_DGRAD_BLASLT", "0") == "1"
+# bf16 Linear GEMMs (forward, dgrad, wgrad) on the asm-scheduled 256x256 MFMA kernel (csrc/kernels/fp8_gemm_asm.hip,
+# the fp8 kernel's schedule with two v_mfma_f32_16x16x32_bf16 per block) when the shape tiles. Opt-in
+# (ACCELERATE_ASM_BF16_GEMM=1): it runs at 0.93-1.04x hipBLASLt's bf16 kernels on the Llama-3-8B shapes (both ~1.45
+# PF/s, the bf16 loop is clock-bound like the fp8 one) and its wgrad needs a transposed dy, so the step is 3 % slower
+# with it (profiles/r5_gemm_fp8_asm.md, "bf16 on the same kernel").
+_ASM_BF16 = os.environ.get("ACCELERATE_ASM_BF16_GEMM", "0") == "1"
+
+
+def asm_gemm_bf16(a: torch.Tensor, b: torch.Tensor, bias=None, out=None, accumulate: bool = False):
+    """out (=|+=) a . bᵀ (+ bias) for bf16 a [M, K], b [N, K] (both contraction-contiguous) on the asm kernel, or None
+    when it does not apply (switched off, not native, CPU, shape not a multiple of its 256x256x64 tile)."""
+    if not (_ASM_BF16 and a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.dim() == 2
+            and b.dim() == 2 and a.is_contiguous() and b.is_contiguous() and use_native(a)):
+        return None
+    m, k = a.shape
+    n = b.shape[0]
+    if m % 256 or n % 256 or k % 64 or k < 128:
+        return None
+    if out is None:
+        if accumulate:
+            return None
+        out = torch.empty((m, n), dtype=torch.bfloat16, device=a.device)
+    if bias is not None and (bias.dtype != torch.bfloat16 or not bias.is_contiguous()):
+        return None
+    return out if ext().bf16_gemm_asm(a, b, bias, out, accumulate) else None
+
+
+def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias=None) -> torch.Tensor:
+    """y = x · Wᵀ (+ b) for a bf16 Linear: the asm kernel when the token count and both widths tile, else torch."""
+    if x.dim() >= 2 and x.is_contiguous():
+        y = asm_gemm_bf16(x.reshape(-1, x.shape[-1]), w, bias)
+        if y is not None:
+            return y.view(*x.shape[:-1], w.shape[0])
+    return torch.nn.functional.linear(x, w, bias)
 
 
 # ----------------------------------------------------------------------------------------------------------
@@ -354,7 +388,9 @@ def linear_dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
             return out
     if (_DGRAD_WT and dy2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and w.is_contiguous()
             and w.shape[0] % 64 == 0 and w.shape[1] % 64 == 0 and use_native(dy2)):
-        return torch.nn.functional.linear(dy2, ext().transpose_bf16(w))
+        wt = ext().transpose_bf16(w)
+        dx = asm_gemm_bf16(dy2, wt) if dy2.is_contiguous() else None
+        return dx if dx is not None else torch.nn.functional.linear(dy2, wt)
     return dy2 @ w
 
 
@@ -366,6 +402,12 @@ def wgrad_into(dest: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, accumula
     a, b = dy2.t(), x2
     if b.dtype != a.dtype:
         b = b.to(a.dtype)
+    # asm kernel: both operands token-contiguous -- x2 is the transposed view of the saved xᵀ, dy2 is transposed here
+    if (_ASM_BF16 and dest.is_cuda and dest.is_contiguous() and a.dtype == torch.bfloat16 and b.t().is_contiguous()
+            and dy2.is_contiguous() and dy2.shape[0] % 256 == 0 and dy2.shape[1] % 256 == 0 and b.shape[1] % 256 == 0
+            and dest.dtype in (torch.float32, torch.bfloat16) and use_native(dy2)):
+        if asm_gemm_bf16(ext().transpose_bf16(dy2), b.t(), None, dest, accumulate) is not None:
+            return
     if dest.dtype == a.dtype:
         dest.addmm_(a, b) if accumulate else torch.mm(a, b, out=dest)
     elif dest.is_cuda and dest.dtype == torch.float32:

@@ -51,7 +51,7 @@ from ..utils.fault_tolerance import record_collective
 from ..utils.tracing import trace_range
 from ..ops._ext import ext, native_enabled
 from ..ops.fp8 import Fp8Linear
-from ..ops.fused import linear_dgrad, wgrad_into
+from ..ops.fused import linear_dgrad, linear_fwd, wgrad_into
 from . import small_allreduce
 
 _ALIGN = 64  # elements; keeps every rank's shard 128-B aligned for bf16 / 256-B for fp32
@@ -1582,7 +1582,7 @@ class _FusedWgradLinearFn(torch.autograd.Function):
         ctx.save_for_backward(ext().transpose_bf16(x2) if ctx.x_transposed else x, weight)
         ctx.slot = slot
         ctx.has_bias = bias is not None
-        return nn.functional.linear(x, weight, bias)
+        return linear_fwd(x, weight, bias)
 
     @staticmethod
     def backward(ctx, dy):

@@ -321,6 +321,36 @@ def test_fp8_gemm_v2_matches_v1_random():
     assert torch.allclose(outs[0], outs[1], rtol=1e-5, atol=1e-3), (outs[0] - outs[1]).abs().max()
 
 
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 1024), (1024, 512, 4096), (768, 1280, 2240)])
+def test_bf16_asm_gemm_matches_fp32_reference(M, N, K):
+    """The asm-scheduled GEMM with bf16 MFMAs (ext().bf16_gemm_asm): exact small integers (bit-exact vs the fp32
+    matmul), then random operands with bias / bf16 and fp32 outputs / accumulate against the fp32 reference."""
+    from accelerate_hpc_test_amd.ops._ext import ext
+
+    torch.manual_seed(0)
+    ai = torch.randint(-3, 4, (M, K), device=DEV).to(torch.bfloat16)
+    bi = torch.randint(-3, 4, (N, K), device=DEV).to(torch.bfloat16)
+    out = torch.empty(M, N, device=DEV)
+    assert ext().bf16_gemm_asm(ai, bi, None, out, False)
+    assert torch.equal(out, ai.float() @ bi.float().t()), (out - ai.float() @ bi.float().t()).abs().max()
+    a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    b = torch.randn(N, K, device=DEV, dtype=torch.bfloat16)
+    bias = torch.randn(N, device=DEV, dtype=torch.bfloat16)
+    ref = a.float() @ b.float().t() + bias.float()
+    o32 = torch.empty(M, N, device=DEV)
+    assert ext().bf16_gemm_asm(a, b, bias, o32, False)
+    assert torch.allclose(o32, ref, rtol=1e-4, atol=1e-3 * ref.abs().max().item()), (o32 - ref).abs().max()
+    o16 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    assert ext().bf16_gemm_asm(a, b, bias, o16, False)
+    assert _rel(o16.float(), ref) < 1e-2
+    base = torch.randn(M, N, device=DEV)
+    acc = base.clone()
+    assert ext().bf16_gemm_asm(a, b, None, acc, True)
+    assert torch.allclose(acc, base + ref - bias.float(), rtol=1e-4, atol=1e-3 * ref.abs().max().item())
+    assert not ext().bf16_gemm_asm(a[:, : K - 32].contiguous(), b[:, : K - 32].contiguous(), None, o32[:, :], False) \
+        or (K - 32) % 64 == 0  # K not a multiple of 64: declined, nothing launched
+
+
 @pytest.mark.parametrize("M,N,K", [(256, 256, 256), (512, 768, 1024), (1024, 512, 4096), (768, 1280, 2304)])
 def test_fp8_gemm_v4_and_unscaled_kernels_match_reference(M, N, K, monkeypatch):
     """The 16x16x128-MFMA kernel (v4: two 64 KiB LDS slots, BK 128) with the scaled (variant 6) and the unscaled

@@ -68,6 +68,13 @@ def mfma(i, j):
     return f"v_mfma_f32_16x16x128_f8f6f4 {acc(i, j)}, {A(i)}, {B(j)}, {acc(i, j)} cbsz:%c[fa] blgp:%c[fb]"
 
 
+def mfma_bf16(i, j, half):
+    """bf16: a 128-byte K-tile is 64 elements = two v_mfma_f32_16x16x32_bf16 per accumulator block; lane (r, g)'s
+    fragment registers 0-3 hold elements 8g..8g+7 of the first 32 (bytes 16g..), registers 4-7 those of the second."""
+    a0, b0 = A_BASE + 8 * i + 4 * half, B_BASE + 8 * j + 4 * half
+    return f"v_mfma_f32_16x16x32_bf16 {acc(i, j)}, v[{a0}:{a0 + 3}], v[{b0}:{b0 + 3}], {acc(i, j)}"
+
+
 def ds_frag(dst_base, f, addr):
     """two ds_read_b128 of fragment slot f (0..7) into v[dst : dst+7] from lane address `addr`"""
     d = dst_base + 8 * f
@@ -90,8 +97,10 @@ def advance_srd(op):
     return [f"s_add_u32 s{srd}, s{srd}, 128", f"s_addc_u32 s{srd + 1}, s{srd + 1}, 0"]
 
 
-def body(dma_on: bool, wait_next: bool, read_next: bool):
-    """one K-tile; returns a list of instruction lines. Extra work is attached after MFMA #k via `slots[k]`."""
+def body(dma_on: bool, wait_next: bool, read_next: bool, bf16: bool = False):
+    """one K-tile; returns a list of instruction lines. Extra work is attached after MFMA #k via `slots[k]`. bf16:
+    each accumulator block takes two MFMAs; in every run of four blocks (same A fragment) the four first halves are
+    issued, each followed by its slot's work, then the four second halves (4 MFMAs between dependent ones)."""
     slots = {k: [] for k in range(64)}
     order = ([(i, j) for i in range(4) for j in range(4)] + [(i, j) for i in range(4) for j in range(4, 8)]
              + [(i, j) for i in range(4, 8) for j in range(4)] + [(i, j) for i in range(4, 8) for j in range(4, 8)])
@@ -138,9 +147,17 @@ def body(dma_on: bool, wait_next: bool, read_next: bool):
     if read_next:
         slots[61] += ["s_waitcnt lgkmcnt(0)"]
     lines = []
-    for k, (i, j) in enumerate(order):
-        lines.append(mfma(i, j))
-        lines += slots[k]
+    if not bf16:
+        for k, (i, j) in enumerate(order):
+            lines.append(mfma(i, j))
+            lines += slots[k]
+        return lines
+    for c in range(0, 64, 4):
+        for k in range(c, c + 4):
+            lines.append(mfma_bf16(*order[k], 0))
+            lines += slots[k]
+        for k in range(c, c + 4):
+            lines.append(mfma_bf16(*order[k], 1))
     return lines
 
 
@@ -181,7 +198,7 @@ def issue():
     return L
 
 
-def main_loop():
+def main_loop(bf16: bool = False):
     """Everything after `issue()`: zero the accumulators, K-tile 0's fragments, the loop and the 2-tile tail.
     vmcnt(16) at the start: the 32 DMAs of `issue()` plus whatever epilogue stores the previous tile issued after
     them (vmcnt counts in order) -> at most the 16 newest may still be in flight, so K-tile 0 has landed."""
@@ -196,23 +213,25 @@ def main_loop():
         L += ds_frag(A_BASE, f, "%[va]")
     L += ["s_waitcnt lgkmcnt(0)"]
     L += [f"s_cmp_eq_u32 s{CNT}, 0", "s_cbranch_scc1 2f", "1:"]
-    L += body(dma_on=True, wait_next=True, read_next=True)
+    L += body(dma_on=True, wait_next=True, read_next=True, bf16=bf16)
     L += [f"s_sub_u32 s{CNT}, s{CNT}, 1", f"s_cmp_eq_u32 s{CNT}, 0", "s_cbranch_scc0 1b", "2:"]
-    L += body(dma_on=False, wait_next=True, read_next=True)
-    L += body(dma_on=False, wait_next=False, read_next=False)
+    L += body(dma_on=False, wait_next=True, read_next=True, bf16=bf16)
+    L += body(dma_on=False, wait_next=False, read_next=False, bf16=bf16)
     L += ["s_nop 7", "s_nop 7", "s_nop 7", f"s_mov_b32 m0, s{M0_KEEP}"]
     return L
 
 
 def generate() -> str:
-    I, L = issue(), main_loop()
+    I, L, LB = issue(), main_loop(), main_loop(bf16=True)
     n_mfma = sum(1 for x in L if x.startswith("v_mfma"))
     assert n_mfma == 3 * 64, n_mfma
+    assert sum(1 for x in LB if x.startswith("v_mfma")) == 3 * 128
     out = ["// GENERATED by tools/gen_fp8_asm.py -- do not edit by hand; edit the generator and rerun it.",
            "// K-loop of fp8_gemm_asm_kernel (csrc/kernels/fp8_gemm_asm.hip): see the generator's docstring.",
-           f"// FP8ASM_ISSUE {len(I)} lines; FP8ASM_MAIN_LOOP {len(L)} lines, {n_mfma} MFMAs (loop body 64).",
+           f"// FP8ASM_ISSUE {len(I)} lines; FP8ASM_MAIN_LOOP {len(L)} lines, {n_mfma} MFMAs (loop body 64);",
+           f"// BF16ASM_MAIN_LOOP {len(LB)} lines (loop body 128 MFMAs).",
            "#pragma once"]
-    for name, lines in (("FP8ASM_ISSUE", I), ("FP8ASM_MAIN_LOOP", L)):
+    for name, lines in (("FP8ASM_ISSUE", I), ("FP8ASM_MAIN_LOOP", L), ("BF16ASM_MAIN_LOOP", LB)):
         out.append(f"#define {name} \\")
         for x in lines:
             out.append(f'  "{x}\\n" \\')

@@ -31,6 +31,7 @@ for step in "$@"; do
     bench20) run bench20 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench20_fp8) run bench20_fp8 600 python bench.py --gpus 1 --steps 20 --warmup 5 --precision fp8 ;;
     bench20_adambf16) run bench20_adambf16 600 python bench.py --gpus 1 --steps 20 --warmup 5 --adam-states bf16 ;;
+    bench20_asm) ACCELERATE_ASM_BF16_GEMM=1 run bench20_asm 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench20_fp8bl) ACCELERATE_FP8_GEMM=blaslt run bench20_fp8bl 600 python bench.py --gpus 1 --steps 20 --warmup 5 --precision fp8 ;;
     bench20_fp8hip) ACCELERATE_FP8_GEMM=hip run bench20_fp8hip 600 python bench.py --gpus 1 --steps 20 --warmup 5 --precision fp8 ;;
     bench8b) run bench8b 600 python bench.py --steps 5 --warmup 2 $BENCH_ARGS ;;
@@ -96,6 +97,8 @@ for step in "$@"; do
     gemm) run gemm 300 python tools/bench_gemm.py ;;
     asmdiag) run asmdiag 120 python tools/debug/fp8asm_diag.py ;;
     gemm_grp) run gemm_grp 400 python tools/bench_gemm.py --variants ${GEMM_VARIANTS:-bl,18,18g1,18g2,18g8,18g16} --no-bf16 --no-scaled-mm --rounds 3 ;;
+    gemm_bf16) run ktest_bf16asm 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "bf16_asm" && \
+               run gemm_bf16 400 python tools/bench_gemm_bf16.py ;;
     asmprobe) run asmprobe 120 python tools/debug/fp8asm_probe.py ;;
     mr_tp) run mr_tp 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_multirank.py -k "tp" ;;
     gemm_asm) run ktest_asm 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "fp8_gemm_v4" && \
