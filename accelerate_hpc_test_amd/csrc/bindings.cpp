@@ -79,6 +79,8 @@ torch::Tensor mx_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor sa, torch:
 void fp8_gemm_select(int64_t variant, int64_t group_m);
 torch::Tensor fp8asm_dma_probe(torch::Tensor a, torch::Tensor b);
 bool bf16_gemm_asm(torch::Tensor a, torch::Tensor b, c10::optional<torch::Tensor> bias, torch::Tensor out, bool accumulate);
+bool grouped_gemm_asm(torch::Tensor a, torch::Tensor b, torch::Tensor out, std::vector<int64_t> bounds, int64_t mode,
+                      c10::optional<torch::Tensor> sa, c10::optional<torch::Tensor> sb, double smul, bool accumulate);
 // grouped_gemm.hip
 void grouped_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor out, torch::Tensor seg, int64_t mode, torch::Tensor sa,
                   torch::Tensor sb, double smul, bool accumulate);
@@ -159,6 +161,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sar_destroy", &sar_destroy);
   m.def("bf16_gemm_asm", &bf16_gemm_asm, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("bias"), pybind11::arg("out"),
         pybind11::arg("accumulate") = false, "bf16 out (=|+=) a . b^T (+ bias) on the asm-scheduled GEMM; false = shape not tiled");
+  m.def("grouped_gemm_asm", &grouped_gemm_asm, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("out"),
+        pybind11::arg("bounds"), pybind11::arg("mode"), pybind11::arg("sa") = pybind11::none(),
+        pybind11::arg("sb") = pybind11::none(), pybind11::arg("smul") = 1.0, pybind11::arg("accumulate") = false,
+        "MoE grouped GEMM on the asm kernel with a host segment table; false = not tiled (nothing launched)");
   m.def("fp8asm_dma_probe", &fp8asm_dma_probe, "debug: LDS image after the asm GEMM's first-tile DMA");
   m.def("fp8_gemm_select", &fp8_gemm_select, pybind11::arg("variant"), pybind11::arg("group_m") = 0);
   register_runtime(m);

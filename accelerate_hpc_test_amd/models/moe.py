@@ -56,7 +56,9 @@ def _swiglu_bwd(h, da):
     return torch.cat([dg, du], -1).to(h.dtype)
 
 
-SEG_ALIGN = 64  # every expert's segment of the routed-token buffer starts at a multiple of 64 rows
+# every expert's segment of the routed-token buffer starts at a multiple of 128 rows: the asm grouped GEMM's 128-byte
+# K-tiles then never straddle two experts in the fp8 weight-gradient product (mode 2 reduces over tokens)
+SEG_ALIGN = 128
 
 
 def _round_up(x: int, m: int) -> int:
@@ -67,7 +69,8 @@ def expert_layout(flat_e: torch.Tensor, num_experts: int, align: int = SEG_ALIGN
     """Device-side routing layout (no host synchronisation): for the (token, slot) entries sorted stably by expert,
     `dest[j]` is entry j's row in a buffer where expert e owns rows [seg[e], seg[e + 1]) — its token count rounded
     up to `align` (the pad rows stay zero). `R`, the buffer's row count, is a host-side bound that does not depend on
-    the routing: N + (align - 1) * E, rounded up to 256."""
+    the routing: N + (align - 1) * E, rounded up to 256, plus 256 rows of slack so that a 256-row tile of the last
+    expert's segment stays inside the buffer (the asm grouped GEMM reads whole tiles, rows past a segment unused)."""
     N = flat_e.numel()
     counts = torch.bincount(flat_e, minlength=num_experts)
     padded = (counts + align - 1) // align * align
@@ -77,7 +80,7 @@ def expert_layout(flat_e: torch.Tensor, num_experts: int, align: int = SEG_ALIGN
     e_sorted = flat_e[order]
     start = torch.cumsum(counts, 0) - counts
     dest = seg[:-1].long()[e_sorted] + (torch.arange(N, device=flat_e.device) - start[e_sorted])
-    R = _round_up(N + (align - 1) * num_experts, 256)
+    R = _round_up(N + (align - 1) * num_experts, 256) + 256
     return order, dest, seg, R
 
 
@@ -118,6 +121,36 @@ _MOE_GEMM = os.environ.get("ACCELERATE_MOE_GEMM", "blaslt")
 # 14.3k to 34.4k tok/s on Mixtral-8x7B-8l, still under the grouped kernel's 36.2k: a ~2k-row expert GEMM fills half
 # the chip (profiles/r3_moe_gemm.md).
 _MOE_FP8_BLASLT = os.environ.get("ACCELERATE_MOE_FP8_BLASLT", "0") == "1"
+# fp8 expert GEMMs on the asm-scheduled grouped kernel (csrc/kernels/fp8_gemm_asm.hip modes 1 / 2: 256x256 tiles of
+# 16x16x128 MFMAs, persistent over (expert, tile) items from the host segment table) when the table is on the host.
+_MOE_ASM = os.environ.get("ACCELERATE_MOE_ASM_GEMM", "1") != "0"
+
+
+def _asm_grouped_mm(a, b, bounds, mode, out, sa, sb, smul, accumulate) -> bool:
+    """grouped_mm on the asm kernel (fp8 operands, host `bounds`); False when it does not apply. Mode-2 experts with
+    fewer than 256 bytes of K (the kernel's two-K-tile minimum) are finished here: zero, or one small product."""
+    if not (_MOE_ASM and a.is_cuda and use_native(a) and a.dtype in (torch.float8_e4m3fn, torch.float8_e5m2)
+            and b.dtype in (torch.float8_e4m3fn, torch.float8_e5m2)):
+        return False
+    if not ext().grouped_gemm_asm(a, b, out, list(bounds), mode, sa, sb, float(smul), bool(accumulate)):
+        return False
+    if mode == 2:
+        es = a.element_size()
+        for e in range(len(bounds) - 1):
+            lo, hi = bounds[e], bounds[e + 1]
+            if (hi - lo) * es >= 256:
+                continue
+            o = out[e]
+            if hi == lo:
+                if not accumulate:
+                    o.zero_()
+                continue
+            res = a[:, lo:hi].float() @ b[:, lo:hi].float().t()
+            if sa is not None:
+                res = res * (sa.reshape(-1)[0] * sb.reshape(-1)[0])
+            res = res * smul
+            o.add_(res.to(o.dtype)) if accumulate else o.copy_(res)
+    return True
 
 
 def _per_expert_mm(a, b, bounds, mode, out, sa, sb, smul, accumulate) -> bool:
@@ -175,6 +208,8 @@ def grouped_mm(a, b, seg, mode, out, sa=None, sb=None, smul=1.0, accumulate=Fals
     shapes the kernel does not tile) the same product runs in PyTorch from a host copy of `seg`."""
     E = seg.numel() - 1
     bounds = getattr(seg, "_acc_bounds", None)
+    if bounds is not None and _asm_grouped_mm(a, b, bounds, mode, out, sa, sb, smul, accumulate):
+        return out
     if (bounds is not None and _MOE_GEMM == "blaslt" and a.is_cuda and use_native(a)
             and _per_expert_mm(a, b, bounds, mode, out, sa, sb, smul, accumulate)):
         return out
@@ -597,7 +632,7 @@ class MoELayer(nn.Module):
 
 def _attach_bounds(seg):
     """Host copy of the segment table for the per-expert library GEMMs (one device -> host copy per MoE layer)."""
-    if seg.is_cuda and _MOE_GEMM == "blaslt" and use_native(seg):
+    if seg.is_cuda and (_MOE_GEMM == "blaslt" or _MOE_ASM) and use_native(seg):
         seg._acc_bounds = seg.tolist()
     return seg
 
