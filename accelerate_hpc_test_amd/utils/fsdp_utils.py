@@ -361,8 +361,8 @@ def save_fsdp_optimizer(fsdp_plugin, accelerator, optimizer, model, output_dir, 
                 st = opt.state.get(info.shard_param) or {}
                 keys = []
                 for k, v in st.items():
-                    if torch.is_tensor(v) and v.dim() > 0:
-                        tensors[f"{info.fqn}|{k}"] = v.detach().reshape(-1).float().cpu().contiguous()
+                    if torch.is_tensor(v) and v.dim() > 0:  # stored in its own dtype (bf16 moments stay bf16)
+                        tensors[f"{info.fqn}|{k}"] = v.detach().reshape(-1).cpu().contiguous()
                         keys.append(k)
                     else:
                         scalars.setdefault(info.fqn, {})[k] = _jsonable(v)
@@ -389,18 +389,23 @@ def _load_sharded_optimizer(eng, opt, d):
     for unit in eng.units:
         for info in unit.infos:
             lo_need, hi_need = info.param_lo, info.param_lo + (info.local_hi - info.local_lo)
-            new = {}
+            new, keys = {}, set()
             for path, m in metas:
                 pm = m["meta"].get(info.fqn)
                 if pm is None:
                     continue
+                keys.update(pm["keys"])
                 for k, v in m["scalars"].get(info.fqn, {}).items():
                     new.setdefault(k, _unjson(v))
                 a, b = max(lo_need, pm["param_lo"]), min(hi_need, pm["param_lo"] + pm["numel"])
                 for k in pm["keys"]:
-                    dst = new.setdefault(k, torch.zeros(hi_need - lo_need, dtype=torch.float32))
-                    if b > a:
-                        dst[a - lo_need : b - lo_need].copy_(rd.read(path, f"{info.fqn}|{k}", a - pm["param_lo"], b - pm["param_lo"]))
+                    if b <= a:
+                        continue
+                    src = rd.read(path, f"{info.fqn}|{k}", a - pm["param_lo"], b - pm["param_lo"])
+                    dst = new.setdefault(k, torch.zeros(hi_need - lo_need, dtype=src.dtype))
+                    dst[a - lo_need : b - lo_need].copy_(src)
+            for k in keys - set(new):  # an empty local piece: nothing to read
+                new[k] = torch.zeros(hi_need - lo_need, dtype=torch.float32)
             if new:
                 opt.state[info.shard_param] = {k: (v.to(eng.device) if torch.is_tensor(v) and v.dim() > 0 else v) for k, v in new.items()}
     if metas:

@@ -100,6 +100,7 @@ for step in "$@"; do
     gemm_bf16) run ktest_bf16asm 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "bf16_asm" && \
                run gemm_bf16 400 python tools/bench_gemm_bf16.py ;;
     ktest_moe_asm) run ktest_moe_asm 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "grouped or moe or expert" ;;
+    ckpt8b) run ckpt8b 900 python tools/ckpt_roundtrip.py ;;
     asmprobe) run asmprobe 120 python tools/debug/fp8asm_probe.py ;;
     mr_tp) run mr_tp 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_multirank.py -k "tp" ;;
     gemm_asm) run ktest_asm 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "fp8_gemm_v4" && \
