@@ -618,9 +618,9 @@ class MoELayer(nn.Module):
 
     @staticmethod
     def _exchange_counts(send_e, W, group):
-        """All-to-all of equal El-sized slices of the per-expert count vector (gloo: via all_gather)."""
+        """All-to-all of equal El-sized slices of the per-expert count vector (HIP tensors on gloo: via all_gather)."""
         El = send_e.numel() // W
-        if dist.get_backend(group) == "gloo":
+        if not comm.tensor_forms(group, send_e):
             gathered = [torch.empty_like(send_e) for _ in range(W)]
             dist.all_gather(gathered, send_e, group=group)
             me = comm.group_rank(group)

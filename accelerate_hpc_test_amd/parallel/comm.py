@@ -2,8 +2,11 @@
 
 On MI355X these are single RCCL calls over xGMI (`all_gather_into_tensor`, `reduce_scatter_tensor`,
 `all_to_all_single`) on contiguous buffers laid out so the exchanged dimension is outermost (one collective, no
-per-chunk launches). The gloo back-end (CPU fake cluster used by the test-suite) lacks some of them; the
-fallbacks below reproduce the same semantics with the primitives gloo has.
+per-chunk launches). The CPU fake cluster of the test-suite (gloo, host tensors) runs the SAME tensor collectives
+(torch's gloo has `all_gather_into_tensor` / `reduce_scatter_tensor` / `all_to_all_single` for host tensors), so the
+multi-process CPU tests exercise the exact calls, buffers and shard offsets an RCCL job issues. Only HIP tensors on a
+gloo group (several ranks sharing one GPU in the one-GPU rehearsal, `tests/test_gpu_multirank.py`) fall back to the
+list / all-reduce forms below.
 """
 
 from __future__ import annotations
@@ -24,6 +27,12 @@ def group_rank(group) -> int:
 
 def _is_gloo(group) -> bool:
     return dist.get_backend(group) == "gloo"
+
+
+def tensor_forms(group, t: torch.Tensor) -> bool:
+    """Whether `t` goes through the packed tensor collectives on `group`: always on RCCL, and on gloo for host tensors;
+    HIP tensors on a gloo group take the list forms (gloo's tensor collectives are host-only)."""
+    return not (t.is_cuda and _is_gloo(group))
 
 
 def duplicate_group(group=None):
@@ -83,7 +92,7 @@ def all_gather_dim(t: torch.Tensor, dim: int, group=None) -> torch.Tensor:
     dim = dim % t.dim()
     src = t.movedim(dim, 0).contiguous()
     out = torch.empty((W * src.shape[0],) + tuple(src.shape[1:]), dtype=t.dtype, device=t.device)
-    if _is_gloo(group):
+    if not tensor_forms(group, src):
         dist.all_gather(list(out.chunk(W)), src, group=group)
     else:
         dist.all_gather_into_tensor(out, src, group=group)
@@ -99,7 +108,7 @@ def reduce_scatter_dim(t: torch.Tensor, dim: int, group=None) -> torch.Tensor:
     src = t.movedim(dim, 0).contiguous()
     if src.shape[0] % W:
         raise ValueError(f"reduce_scatter along dim {dim}: size {src.shape[0]} not divisible by {W}")
-    if _is_gloo(group):
+    if not tensor_forms(group, src):
         tmp = src.clone()
         dist.all_reduce(tmp, group=group)
         out = tmp.chunk(W)[group_rank(group)].contiguous()
@@ -132,8 +141,8 @@ def all_to_all_dims(t: torch.Tensor, scatter_dim: int, gather_dim: int, group=No
     chunks = t.chunk(W, dim=scatter_dim)
     send = torch.stack([c.contiguous() for c in chunks], 0)
     recv = torch.empty_like(send)
-    if _is_gloo(group):
-        # gloo has all_to_all only in recent builds and only for CPU tensors; do it with all_gather
+    if not tensor_forms(group, send):
+        # HIP tensors on a gloo group: all_to_all through all_gather
         gathered = [torch.empty_like(send) for _ in range(W)]
         dist.all_gather(gathered, send, group=group)
         me = group_rank(group)
@@ -149,9 +158,9 @@ def all_to_all_varlen(t: torch.Tensor, send_counts: list, recv_counts: list, gro
     if W == 1:
         return t
     out = torch.empty((sum(recv_counts),) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-    if _is_gloo(group):
+    if not tensor_forms(group, t):
         me = group_rank(group)
-        # exchange via all_gather of padded blocks (test path)
+        # HIP tensors on a gloo group: exchange via all_gather of padded blocks
         mx = max(max(send_counts), 1)
         pad = torch.zeros((W, mx) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         o = 0

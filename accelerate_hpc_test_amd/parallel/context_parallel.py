@@ -129,7 +129,7 @@ class _KVGather:
         second = kv[:, :, L:].movedim(2, 0).contiguous()
         self.h1 = torch.empty((W * L,) + tuple(first.shape[1:]), dtype=k.dtype, device=k.device)
         self.h2 = torch.empty_like(self.h1)
-        self.async_ok = W > 1 and dist.get_backend(group) != "gloo"
+        self.async_ok = W > 1 and comm.tensor_forms(group, first)
         if W == 1:
             self.h1.copy_(first)
             self.h2.copy_(second)

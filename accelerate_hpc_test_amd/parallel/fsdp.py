@@ -226,10 +226,11 @@ class FSDPEngine:
             self.bwd_prefetch = "BACKWARD_PRE"
         self.requires_grad_sync = True
         self.is_cuda = device.type == "cuda"
-        # gloo lacks all_gather_into_tensor / reduce_scatter_tensor (CPU tensors, and HIP tensors when several ranks
-        # share one GPU over a gloo group): the list / all-reduce forms below are chosen by the group's backend
-        self._uses_gloo = (not self.is_cuda) or (dist.is_available() and dist.is_initialized()
-                                                 and dist.get_backend(process_group) == "gloo")
+        # host ranks on gloo run the same all_gather_into_tensor / reduce_scatter_tensor calls as RCCL ranks (the CPU
+        # tests then cover the exact shard offsets and buffers); only HIP tensors on a gloo group (several ranks
+        # sharing one GPU in the one-GPU rehearsal) need the list / all-reduce forms, gloo's tensor forms being host-only
+        self._uses_gloo = self.is_cuda and (dist.is_available() and dist.is_initialized()
+                                            and dist.get_backend(process_group) == "gloo")
         self.offload = plugin.cpu_offload not in (None, False)
         self._pin = self.offload and torch.cuda.is_available() and getattr(plugin.cpu_offload, "pin_memory", True)
         self._d2h_pending = []
@@ -1087,7 +1088,7 @@ class FSDPEngine:
         self._d2h_pending.clear()
 
     def _gloo_rs(self, out, src):
-        # gloo has no reduce_scatter: all-reduce then slice (CPU test path only).
+        # HIP tensors on a gloo group (one-GPU rehearsal): all-reduce then slice
         tmp = src.clone()
         dist.all_reduce(tmp, group=self.group)
         out.copy_(tmp[self.rank * out.numel() : (self.rank + 1) * out.numel()])
@@ -1319,7 +1320,7 @@ class FSDPEngine:
         group, W = p._ep_spec
         t = p.detach().float().contiguous()
         out = torch.empty((W * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-        if dist.get_backend(group) == "gloo":
+        if t.is_cuda and dist.get_backend(group) == "gloo":
             dist.all_gather(list(out.chunk(W)), t, group=group)
         else:
             dist.all_gather_into_tensor(out, t, group=group)

@@ -250,7 +250,7 @@ def _gpu_gather_one(tensor: torch.Tensor) -> torch.Tensor:
         tensor = tensor.clone()[None]
     if not tensor.is_contiguous():
         tensor = tensor.contiguous()
-    if state.backend is not None and state.backend.startswith("gloo"):
+    if tensor.is_cuda and state.backend is not None and state.backend.startswith("gloo"):  # gloo: host-only tensor forms
         outs = [torch.empty_like(tensor) for _ in range(state.num_processes)]
         record_collective("all_gather", tensor)
         torch.distributed.all_gather(outs, tensor)
