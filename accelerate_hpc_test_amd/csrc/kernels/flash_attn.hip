@@ -95,6 +95,62 @@ __device__ __forceinline__ v8bf tr_frag(const char* img, int rb, int db, int lan
 
 __device__ __forceinline__ int acc_row(int i, int hf) { return (i & 3) + 8 * (i >> 2) + 4 * hf; }
 
+// S / dP MFMA of the one-wave-per-SIMD dK / dV kernel with the accumulator in VGPRs and the K / V operand in AGPRs
+// (inline asm: hipcc puts every MFMA accumulator of a 512-register kernel in AGPRs, so each S / dP element then costs a
+// v_accvgpr_read before its softmax VALU). Wait states the compiler does not pad inside asm: FIRST opens a chain whose
+// seed a VALU may just have written (2 states), LAST closes a pair of chains whose results the softmax VALU reads next
+// (an MFMA result read by anything but the next accumulating MFMA: 16 states). A chain in between needs none
+// (accumulation into the same registers by the same opcode is interlocked).
+template <int WS>
+__device__ __forceinline__ void mfma_vacc(f32x16& c, const v8bf& a, const v8bf& b) {
+  if constexpr (WS == 1)
+    asm("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "a"(b));
+  else if constexpr (WS == 2)
+    asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0\n\ts_nop 7\n\ts_nop 7" : "+v"(c) : "v"(a), "a"(b));
+  else if constexpr (WS == 3)  // a chain's first MFMA with C = 0 (no seed registers, nothing to wait for)
+    asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(a), "a"(b));
+  else
+    asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "a"(b));
+}
+
+// Lane offsets of one wave's reads of a dual image (img_off): row reads of rows 32c + (lane & 31), chunk 2s + hf
+// (8 registers; the 32-row block c is an immediate) and transposed reads (tr_frag's lane map) of column block db,
+// rows +0 / +8 (8 registers; the 16-row block is an immediate) — the swizzle depends on row & 15 only. Made opaque
+// once, so hipcc keeps exactly these 16 VGPRs instead of re-deriving or hoisting an address per read and buffer.
+struct DualOff {
+  int row[8];
+  int tr[4][2];
+  __device__ __forceinline__ void init(int lane) {
+    const int r = lane & 31, hf = lane >> 5;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) row[s] = img_off(r, 2 * s + hf);
+    const int g = lane >> 4, i = lane & 15;
+    const int row0 = 4 * (g >> 1) + (i >> 2), ch0 = 2 * (g & 1) + ((i & 3) >> 1), sub = 8 * (i & 1);
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      tr[db][0] = img_off(row0, db * 4 + ch0) + sub;
+      tr[db][1] = img_off(row0 + 8, db * 4 + ch0) + sub;
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s) asm volatile("" : "+v"(row[s]));
+#pragma unroll
+    for (int db = 0; db < 4; ++db) asm volatile("" : "+v"(tr[db][0]), "+v"(tr[db][1]));
+  }
+  // row_frag(img, 32 c + (lane & 31), 2 s + hf)
+  __device__ __forceinline__ v8bf rowf(const char* img, int c, int s) const {
+    return *reinterpret_cast<const v8bf*>(img + 8192 * c + row[s]);
+  }
+  // tr_frag(img, rb, db, lane), rb a multiple of 16
+  __device__ __forceinline__ v8bf trf(const char* img, int rb, int db) const {
+    const v4bf lo = tr_read(img + 256 * rb + tr[db][0]);
+    const v4bf hi = tr_read(img + 256 * rb + tr[db][1]);
+    v8bf x;
+    x[0] = lo[0]; x[1] = lo[1]; x[2] = lo[2]; x[3] = lo[3];
+    x[4] = hi[0]; x[5] = hi[1]; x[6] = hi[2]; x[7] = hi[3];
+    return x;
+  }
+};
+
 // Lane offsets of the reads of a layout-(a) image (img_off_a), computed once per kernel: two registers serve every
 // row read of a 32x32x16 operand and two every transposed read, the rest is the instruction's immediate offset.
 struct ImgA {
@@ -209,6 +265,9 @@ struct TileDMA {
 #pragma unroll
     for (int t = 0; t < kPer; ++t)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, img + (first + t) * 1024, 16, voff[t], so, 0, 0);
+  }
+  __device__ __forceinline__ void issue_piece(__amdgpu_buffer_rsrc_t rs, int row0, int ts_bytes, char* img, int t) const {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, img + (first + t) * 1024, 16, voff[t], row0 * ts_bytes, 0, 0);
   }
 };
 
@@ -827,6 +886,462 @@ __global__ __launch_bounds__(512) void attn_bwd_dkdv_kernel(BwdParams p) {
   wave_trace(p.trace, t_start, wave, (unsigned)kt | ((unsigned)kh << 16));
 }
 
+// dQ, one wave per SIMD (the default; ACCELERATE_ATTN_DQ_W4=0 selects the 8-wave kernel). Workgroup = 128 queries of
+// one query head (grid (Hq, S / 128, B), heavy causal tiles first, a GQA group's heads on one XCD as in the 8-wave
+// kernel); 4 waves, wave w owns queries 32w .. 32w + 31. Its Q and dO fragments sit in AGPRs as the B operands of
+// S^T = K Q^T and dP^T = V dO^T (mfma_vacc: S / dP accumulate in VGPRs, no v_accvgpr_read before the softmax);
+// dQ^T accumulates in 64 more AGPRs.
+// Software pipeline over 32-key units u = (tile, key block kb): the phase of unit u runs S / dP of u (16 MFMAs), the
+// softmax VALU of u - 1 and dQ += dS K of u - 2 (8 MFMAs), so MFMAs and VALU interleave evenly instead of a unit's
+// VALU waiting on its own S / dP with nothing to overlap (one wave per SIMD: no partner wave to lend issue slots).
+// dQ of u - 2 reads the previous K tile, so K and V tiles rotate through three LDS buffers (96 KB). A phase is 6
+// steps of 4 MFMAs (S S Q S S Q), each step's fragments read one step ahead (sched_barrier between steps), the next
+// tile's LDS-DMA one piece per step.
+template <bool CAUSAL>
+__global__ __launch_bounds__(256, 1) void attn_bwd_dq_w4_kernel(BwdParams p) {
+  constexpr int kKeys = 64;
+  constexpr int kTile = kKeys * kRow;  // 16 KB
+  __shared__ __attribute__((aligned(1024))) char k0s[kTile], k1s[kTile], k2s[kTile], v0s[kTile], v1s[kTile], v2s[kTile];
+  const long long t_start = wall_clock64();
+  const int nqt = p.S / 128;
+  const int qt = CAUSAL ? (nqt - 1 - (int)blockIdx.y) : (int)blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hf = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = xcd_head(blockIdx.x, p.Hq), b = blockIdx.z;
+  const int kh = h / (p.Hq / p.Hkv);
+  const int qw0 = qt * 128 + wave * 32;
+  ACC_CHECK_OR_RETURN(qt * 128 + 128 <= p.S && h < p.Hq && kh < p.Hkv && (!CAUSAL || (qt + 1) * 128 + p.off <= p.Sk),
+                      kChkAttnTile);
+  v8bf qf[8], df[8];
+  const bf16_t* qb = p.q + b * p.q_bs + (long)h * kD + (long)(qw0 + r) * p.q_ts + 8 * hf;
+  const bf16_t* dob = p.dout + b * p.do_bs + (long)h * kD + (long)(qw0 + r) * p.do_ts + 8 * hf;
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    qf[s] = *reinterpret_cast<const v8bf*>(qb + 16 * s);
+    df[s] = *reinterpret_cast<const v8bf*>(dob + 16 * s);
+  }
+  const long st = ((long)b * p.Hq + h) * p.S + qw0 + r;
+  const float lse2 = p.lse[st] * kLog2e;
+  float dlt;
+  if (p.delta_out != nullptr) {  // delta = rowsum(dO * O) from the dO fragments held, stored for the dK / dV kernel
+    const bf16_t* ob = p.o + b * p.o_bs + (long)h * kD + (long)(qw0 + r) * p.o_ts + 8 * hf;
+    float acc = 0.f;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const v8bf of = *reinterpret_cast<const v8bf*>(ob + 16 * s);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc = fmaf(static_cast<float>(df[s][j]), static_cast<float>(of[j]), acc);
+    }
+    dlt = acc + __shfl_xor(acc, 32, 64);
+    if (hf == 0) {
+      p.delta_out[st] = -dlt;
+      p.nlse[st] = -p.lse[st] * p.inv_scale;
+    }
+  } else {
+    dlt = -p.delta[st];
+  }
+  f32x16 dq[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) zero(dq[d]);
+  const int off = p.off;
+  const int n_kt = CAUSAL ? ((qt + 1) * 128 + off) / kKeys : p.Sk / kKeys;
+  const int n_full = CAUSAL ? n_kt - 2 : n_kt;  // the causal workgroup's last 128 keys are its diagonal
+
+  TileDMA<kKeys, 4> dmk, dmv;
+  const int kts = (int)(p.k_ts * 2), vts = (int)(p.v_ts * 2);
+  dmk.init_a(wave, lane, kts);  // K / V tiles in layout (a): ImgA reads
+  dmv.init_a(wave, lane, vts);
+  ImgA ia;
+  ia.init(lane);
+  const auto krs = head_rsrc(p.k + b * p.k_bs + (long)kh * kD, p.Sk, p.k_ts);
+  const auto vrs = head_rsrc(p.v + b * p.v_bs + (long)kh * kD, p.Sk, p.v_ts);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    dmk.issue_piece(krs, 0, kts, k0s, t);
+    dmv.issue_piece(vrs, 0, vts, v0s, t);
+  }
+  wait_dma_and_sync();
+
+  // carried between tiles: S / dP of the previous tile's key block 1 (softmax pending) and the dS of its block 0
+  f32x16 scb, dpb;
+  v8bf ds0[2], ds1[2];  // dS^T packs (k halves) of key block 0 / 1
+  // One tile: T's S / dP (HC), T - 1's block-1 softmax and dQ of both its blocks (HP); k_prev = T - 1's K buffer.
+  auto tile = [&](auto has_prev, auto mask_prev, auto has_cur, auto mask_cur, int T, const char* k_img,
+                  const char* v_img, const char* k_prev, char* nk, char* nv) {
+    constexpr bool HP = decltype(has_prev)::value;
+    constexpr bool HC = decltype(has_cur)::value;
+    const int nrow = (T + 1 < n_kt ? T + 1 : T) * kKeys;  // past the last tile: refetch it (nobody reads the copy)
+    f32x16 sca, dpa;
+    // softmax of key block kb of tile tt, elements i0 .. i1 - 1: dS = P (dP - delta) in place, packed after 7 / 15
+    auto softmax = [&](auto masked, int tt, int kb, f32x16& sc, const f32x16& dp, v8bf (&dst)[2], int i0, int i1) {
+      constexpr bool M = decltype(masked)::value;
+      const int lim = qw0 + r + off - (tt * kKeys + kb * 32 + 4 * hf);  // key row acc_row(i, 0) hidden above lim
+#pragma unroll
+      for (int i = i0; i < i1; ++i) {
+        float pv = fast_exp2(fmaf(sc[i], p.scale_log2, -lse2));
+        if (M && acc_row(i, 0) > lim) pv = 0.f;
+        sc[i] = pv * (dp[i] - dlt);
+      }
+      if (i0 <= 7 && 7 < i1) dst[0] = pack8(sc, 0);
+      if (i1 == 16) dst[1] = pack8(sc, 1);
+    };
+    // step j (0..5) of phase ph (= key block): S-steps j = 0, 1, 3, 4 (s = 2m, 2m + 1 for m = 0, 1, 2, 3), Q-steps
+    // j = 2, 5 (d = 0, 1 and d = 2, 3)
+    auto load_ops = [&](int ph, int j, v8bf (&o)[4]) {
+      if (j == 2 || j == 5) {
+        if (HP) {
+          const int d0 = j == 2 ? 0 : 2;
+          o[0] = ia.tr(k_prev, ph * 32, d0);
+          o[1] = ia.tr(k_prev, ph * 32 + 16, d0);
+          o[2] = ia.tr(k_prev, ph * 32, d0 + 1);
+          o[3] = ia.tr(k_prev, ph * 32 + 16, d0 + 1);
+        }
+      } else if (HC) {
+        const int m = j < 2 ? j : j - 1;
+        o[0] = ia.row(k_img, ph * 32, 2 * m);
+        o[1] = ia.row(v_img, ph * 32, 2 * m);
+        o[2] = ia.row(k_img, ph * 32, 2 * m + 1);
+        o[3] = ia.row(v_img, ph * 32, 2 * m + 1);
+      }
+    };
+    auto mfma_step = [&](int ph, int j, const v8bf (&o)[4]) {
+      f32x16& sc = ph == 0 ? sca : scb;
+      f32x16& dp = ph == 0 ? dpa : dpb;
+      if (j == 2 || j == 5) {
+        if (HP) {
+          const v8bf (&dsx)[2] = ph == 0 ? ds0 : ds1;
+          const int d0 = j == 2 ? 0 : 2;
+          dq[d0] = mfma(o[0], dsx[0], dq[d0]);
+          dq[d0] = mfma(o[1], dsx[1], dq[d0]);
+          dq[d0 + 1] = mfma(o[2], dsx[0], dq[d0 + 1]);
+          dq[d0 + 1] = mfma(o[3], dsx[1], dq[d0 + 1]);
+        }
+      } else if (HC) {
+        const int m = j < 2 ? j : j - 1;
+        if (m == 0) {
+          mfma_vacc<3>(sc, o[0], qf[0]);
+          mfma_vacc<3>(dp, o[1], df[0]);
+        } else {
+          mfma_vacc<0>(sc, o[0], qf[2 * m]);
+          mfma_vacc<0>(dp, o[1], df[2 * m]);
+        }
+        mfma_vacc<0>(sc, o[2], qf[2 * m + 1]);
+        if (m == 3) mfma_vacc<2>(dp, o[3], df[2 * m + 1]);  // results read by the next phase's softmax VALU
+        else mfma_vacc<0>(dp, o[3], df[2 * m + 1]);
+      }
+    };
+    v8bf ops[2][4];
+    load_ops(0, 0, ops[0]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int g = 0; g < 12; ++g) {
+      const int ph = g / 6, j = g % 6;
+      if (g + 1 < 12) load_ops((g + 1) / 6, (g + 1) % 6, ops[(g + 1) & 1]);
+      if (HC && g < 8) {  // the next tile's K / V pieces (none in the drain: nothing may land after the last wait)
+        if (g < 4) dmk.issue_piece(krs, nrow, kts, nk, g);
+        else dmv.issue_piece(vrs, nrow, vts, nv, g - 4);
+      }
+      mfma_step(ph, j, ops[g & 1]);
+      // softmax: phase 0 finishes T - 1's block 1 (its dS feeds phase 1's dQ), phase 1 runs T's block 0 (its dS
+      // feeds the next tile's phase 0); 16 elements over the phase's 6 steps
+      constexpr int kSplit[7] = {0, 3, 6, 8, 11, 14, 16};
+      if (ph == 0 && HP) softmax(mask_prev, T - 1, 1, scb, dpb, ds1, kSplit[j], kSplit[j + 1]);
+      if (ph == 1 && HC) softmax(mask_cur, T, 0, sca, dpa, ds0, kSplit[j], kSplit[j + 1]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (HC) wait_dma_and_sync();
+  };
+  using F = std::false_type;
+  using Tr = std::true_type;
+  using MC = std::integral_constant<bool, CAUSAL>;
+  // tile 0 (no previous tile), the plain tiles in a 3-buffer rotation entered at tile 1, then the causal diagonal and
+  // the drain (HAS_CUR = false) with run-time buffers (they run once per workgroup)
+  if (n_full > 0) tile(F{}, F{}, Tr{}, F{}, 0, k0s, v0s, k2s, k1s, v1s);
+  else tile(F{}, F{}, Tr{}, MC{}, 0, k0s, v0s, k2s, k1s, v1s);
+  int T = 1;
+  for (;;) {
+    if (T >= n_full) break;
+    tile(Tr{}, F{}, Tr{}, F{}, T, k1s, v1s, k0s, k2s, v2s);
+    ++T;
+    if (T >= n_full) break;
+    tile(Tr{}, F{}, Tr{}, F{}, T, k2s, v2s, k1s, k0s, v0s);
+    ++T;
+    if (T >= n_full) break;
+    tile(Tr{}, F{}, Tr{}, F{}, T, k0s, v0s, k2s, k1s, v1s);
+    ++T;
+  }
+  auto kbuf = [&](int i) -> char* { return i == 0 ? k0s : (i == 1 ? k1s : k2s); };
+  auto vbuf = [&](int i) -> char* { return i == 0 ? v0s : (i == 1 ? v1s : v2s); };
+  if (CAUSAL) {
+    for (; T < n_kt; ++T) {  // the diagonal: T = n_full (its previous tile plain unless n_full == 0), n_full + 1
+      if (T == n_full && T > 0)
+        tile(Tr{}, F{}, Tr{}, Tr{}, T, kbuf(T % 3), vbuf(T % 3), kbuf((T + 2) % 3), kbuf((T + 1) % 3), vbuf((T + 1) % 3));
+      else if (T > 0)
+        tile(Tr{}, Tr{}, Tr{}, Tr{}, T, kbuf(T % 3), vbuf(T % 3), kbuf((T + 2) % 3), kbuf((T + 1) % 3), vbuf((T + 1) % 3));
+    }
+    tile(Tr{}, Tr{}, F{}, F{}, T, kbuf(T % 3), vbuf(T % 3), kbuf((T + 2) % 3), kbuf((T + 1) % 3), vbuf((T + 1) % 3));
+  } else {
+    tile(Tr{}, F{}, F{}, F{}, T, kbuf(T % 3), vbuf(T % 3), kbuf((T + 2) % 3), kbuf((T + 1) % 3), vbuf((T + 1) % 3));
+  }
+  bf16_t* out = p.dq + b * p.dq_bs + (long)h * kD + (long)(qw0 + r) * p.dq_ts;
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      bf16x4 w;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) w.v[t] = f2bf(dq[d][4 * g + t] * p.scale);
+      *reinterpret_cast<bf16x4*>(out + d * 32 + 8 * g + 4 * hf) = w;
+    }
+  wave_trace(p.trace, t_start, wave, (unsigned)qt | ((unsigned)h << 16));
+}
+
+// dK / dV, one wave per SIMD (the default; ACCELERATE_ATTN_DKDV=8 selects the 8-wave kernel above). Same workgroup
+// (batch, kv head, 128-key tile), same sweep and row constants, but 4 waves that each own the whole 512-entry register
+// file: wave w owns keys 32w .. 32w + 31 of the tile and BOTH 32-query halves of every 64-query slice. Its K and V
+// fragments (the B operands of S = Q K^T and dP = dO V^T, key on the lane) are read from HBM once into 64 VGPRs and
+// stay there for the whole sweep, so per slice only Q and dO cross LDS (half the LDS bytes per MFMA of the 8-wave
+// kernel, where every slice re-read K and V from LDS), and dK^T / dV^T of the wave's keys sum over every query of the
+// group in its own accumulators: no cross-wave reduction at the end. The two query halves are independent chains: the
+// softmax VALU of one hides under the other's MFMAs inside the wave (no SIMD partner to lend its issue slots).
+// SCHED = 1: inside each step the next step's reads are issued first and the MFMAs alternate with the VALU
+// (sched_group_barrier), instead of leaving the order inside a step to hipcc (SCHED = 0); ACCELERATE_ATTN_DKDV_SCHED.
+template <bool CAUSAL, int SCHED>
+__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_w4_kernel(BwdParams p) {
+  constexpr int kSlice = 64;
+  constexpr int kImg = kSlice * kRow;  // 16 KB: one 64-row Q or dO image (dual image: row and transposed reads)
+  __shared__ __attribute__((aligned(1024))) char qs0[kImg], ds0[kImg], qs1[kImg], ds1[kImg];
+  __shared__ __attribute__((aligned(16))) float ls0[2 * kSlice], ls1[2 * kSlice];
+  const long long t_start = wall_clock64();
+  const int kh = blockIdx.x % p.Hkv, kt = blockIdx.x / p.Hkv, b = blockIdx.y;  // grid and order as the 8-wave kernel
+  const int grp = p.Hq / p.Hkv;
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hf = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: the slice tests below stay uniform branches
+  const int kw0 = kt * 128 + wave * 32;
+  ACC_CHECK_OR_RETURN(kt * 128 + 128 <= p.Sk && kh < p.Hkv && p.Hq % p.Hkv == 0, kChkAttnTile);
+  v8bf kf[8], vf[8];  // key kw0 + r, columns 16 s + 8 hf .. + 7
+  {
+    const bf16_t* kp = p.k + b * p.k_bs + (long)kh * kD + (long)(kw0 + r) * p.k_ts + 8 * hf;
+    const bf16_t* vp = p.v + b * p.v_bs + (long)kh * kD + (long)(kw0 + r) * p.v_ts + 8 * hf;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      kf[s] = *reinterpret_cast<const v8bf*>(kp + 16 * s);
+      vf[s] = *reinterpret_cast<const v8bf*>(vp + 16 * s);
+    }
+  }
+  f32x16 dk[4], dv[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) { zero(dk[d]); zero(dv[d]); }
+
+  const int off = p.off;
+  const int qs0_ = CAUSAL ? max(0, (kt * 128 - off) / kSlice) : 0;
+  const int per = p.S / kSlice - qs0_;
+  const int n_it = grp * per;
+  TileDMA<kSlice, 4> dmq, dmd;  // 4 pieces per wave per operand
+  const int qts = (int)(p.q_ts * 2), dts = (int)(p.do_ts * 2);
+  dmq.init(wave, lane, qts);
+  dmd.init(wave, lane, dts);
+  const long rc_bytes = (long)gridDim.y * p.Hq * p.S * 4;
+  const int rc = (int)(rc_bytes > 0x7fffffffL ? 0x7fffffffL : rc_bytes);
+  const auto lrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.nlse, (short)0, rc, 0x00020000);
+  const auto drs = __builtin_amdgcn_make_buffer_rsrc((void*)p.delta, (short)0, rc, 0x00020000);
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  // Sweep order, lockstep: slices descending from the last one, the group's query heads innermost. Every workgroup of
+  // the kv head (all on one XCD, see the grid) then streams the same Q / dO slice at about the same time and the XCD's
+  // L2 serves it to all of them (the head-major order left the causal kernel at a 57 % L2 hit rate; at one wave per
+  // SIMD the fetch latency is not hidden by a partner wave). A causal tile's diagonal slices come last.
+  auto coords = [&](int it, int& h, int& q0) {
+    h = kh * grp + it % grp;
+    q0 = (qs0_ + per - 1 - it / grp) * kSlice;
+  };
+  // The next slice's LDS-DMA in 9 pieces (4 Q, 4 dO, then lse | delta from waves 0 | 1), one per MFMA step, so each
+  // piece's issue cost (60-185 cycles) hides beside the MFMAs instead of stalling the slice's start.
+  // Past the last slice the pieces still go out (no branch per piece): they fetch an in-range slice (or nothing: the
+  // descriptor's range check) into the buffer nobody reads any more, and the final vmcnt(0) drains them.
+  struct Next {
+    __amdgpu_buffer_rsrc_t qr, dr;
+    int q0, row;
+    char *qi, *di;
+    float* ld;
+  };
+  auto next_of = [&](int it, char* qi, char* di, float* ld) {
+    Next n;
+    int h, q0;
+    coords(it < n_it ? it : n_it - 1, h, q0);
+    n.qr = head_rsrc(p.q + b * p.q_bs + (long)h * kD, p.S, p.q_ts);
+    n.dr = head_rsrc(p.dout + b * p.do_bs + (long)h * kD, p.S, p.do_ts);
+    n.q0 = q0;
+    n.row = (int)((((long)b * p.Hq + h) * p.S + q0) * 4);
+    n.qi = qi; n.di = di; n.ld = ld;
+    return n;
+  };
+  auto dma_piece = [&](const Next& n, int t) {
+    if (t < 4) dmq.issue_piece(n.qr, n.q0, qts, n.qi, t);
+    else if (t < 8) dmd.issue_piece(n.dr, n.q0, dts, n.di, t - 4);
+    else if (t == 8) {
+      if (wv == 0) __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, n.ld, 4, lane * 4, n.row, 0, 0);
+      else if (wv == 1) __builtin_amdgcn_raw_ptr_buffer_load_lds(drs, n.ld + kSlice, 4, lane * 4, n.row, 0, 0);
+    }
+  };
+  DualOff lo_;
+  lo_.init(lane);
+  {
+    const Next n0 = next_of(0, qs0, ds0, ls0);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) dma_piece(n0, t);
+  }
+  wait_dma_and_sync();
+
+  // One slice as 16 steps of 4 MFMAs, each step's operand fragments read one step ahead (a sched_barrier(0) between
+  // steps pins the order: hipcc otherwise issues each fragment read right before its MFMA and waits for it, which at
+  // one wave per SIMD exposes the LDS latency at every MFMA):
+  //   steps 0-3: S and dP of query half c = 0 (s = 2t, 2t + 1)     steps 4-7: the same for c = 1
+  //   steps 8-11: dV^T / dK^T from half 0, j-major (8: dV j=0, 9: dK j=0, 10: dV j=1, 11: dK j=1, d = 0..3 each)
+  //   steps 12-15: the same from half 1
+  // The softmax VALU of half 0 (exp, mask, dS, bf16 packs) runs in steps 4-9 beside the MFMAs, half 1's in steps 10-13,
+  // two elements at a time, each pack just before the step that consumes it.
+  // MASKED = the slice reaches the wave's diagonal (causal only): per-element mask; every other slice runs the plain body.
+  auto body = [&](auto masked, int q0, const char* q_img, const char* d_img, const float* lse_s, int lane,
+                  const Next& nx) {
+    constexpr bool MASKED = decltype(masked)::value;
+    const int r = lane & 31, hf = lane >> 5;
+    const float* dlt_s = lse_s + kSlice;
+    f32x16 sc[2], dp[2];
+    v8bf pb[2][2], dsb[2][2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {  // seeds: -lse / scale and -delta of rows 32c + 8g + 4hf .. + 3
+        const float4 l4 = *reinterpret_cast<const float4*>(lse_s + 32 * c + 8 * g + 4 * hf);
+        const float4 d4 = *reinterpret_cast<const float4*>(dlt_s + 32 * c + 8 * g + 4 * hf);
+        sc[c][4 * g] = l4.x; sc[c][4 * g + 1] = l4.y; sc[c][4 * g + 2] = l4.z; sc[c][4 * g + 3] = l4.w;
+        dp[c][4 * g] = d4.x; dp[c][4 * g + 1] = d4.y; dp[c][4 * g + 2] = d4.z; dp[c][4 * g + 3] = d4.w;
+      }
+    auto load_ops = [&](int t, v8bf(&o)[4]) {
+      if (t < 8) {
+        const int c = t >> 2, s0 = 2 * (t & 3);
+        o[0] = lo_.rowf(q_img, c, s0);
+        o[1] = lo_.rowf(d_img, c, s0);
+        o[2] = lo_.rowf(q_img, c, s0 + 1);
+        o[3] = lo_.rowf(d_img, c, s0 + 1);
+      } else {
+        const int c = (t - 8) >> 2, j = ((t - 8) >> 1) & 1;
+        const char* img = (t & 1) ? q_img : d_img;  // even steps dV (dO^T), odd steps dK (Q^T)
+#pragma unroll
+        for (int d = 0; d < 4; ++d) o[d] = lo_.trf(img, 32 * c + 16 * j, d);
+      }
+    };
+    auto mfma_step = [&](int t, const v8bf(&o)[4]) {
+      if (t < 8 && (SCHED & 2)) {
+        const int c = t >> 2, s0 = 2 * (t & 3);
+        if (s0 == 0) {
+          mfma_vacc<1>(sc[c], o[0], kf[s0]);
+          mfma_vacc<1>(dp[c], o[1], vf[s0]);
+        } else {
+          mfma_vacc<0>(sc[c], o[0], kf[s0]);
+          mfma_vacc<0>(dp[c], o[1], vf[s0]);
+        }
+        mfma_vacc<0>(sc[c], o[2], kf[s0 + 1]);
+        if (s0 == 6) mfma_vacc<2>(dp[c], o[3], vf[s0 + 1]);
+        else mfma_vacc<0>(dp[c], o[3], vf[s0 + 1]);
+      } else if (t < 8) {
+        const int c = t >> 2, s0 = 2 * (t & 3);
+        sc[c] = mfma(o[0], kf[s0], sc[c]);
+        dp[c] = mfma(o[1], vf[s0], dp[c]);
+        sc[c] = mfma(o[2], kf[s0 + 1], sc[c]);
+        dp[c] = mfma(o[3], vf[s0 + 1], dp[c]);
+      } else {
+        const int c = (t - 8) >> 2, j = ((t - 8) >> 1) & 1;
+        if (t & 1) {
+#pragma unroll
+          for (int d = 0; d < 4; ++d) dk[d] = mfma(o[d], dsb[c][j], dk[d]);
+        } else {
+#pragma unroll
+          for (int d = 0; d < 4; ++d) dv[d] = mfma(o[d], pb[c][j], dv[d]);
+        }
+      }
+    };
+    // elements 2e, 2e + 1 of half c: P = exp2(S' scale_log2) (masked), dS = P (dP - delta); packs after e = 3 and 7
+    auto softmax2 = [&](int c, int e) {
+      const int lim = kw0 + r - (q0 + off + 32 * c + 4 * hf);  // causal: key kw0 + r hidden from rows below it
+      const bool diag = MASKED && q0 + 32 * c + off < kw0 + 31;
+#pragma unroll
+      for (int i = 2 * e; i < 2 * e + 2; ++i) {
+        float pv = fast_exp2(sc[c][i] * p.scale_log2);
+        if (MASKED && diag && acc_row(i, 0) < lim) pv = 0.f;
+        sc[c][i] = pv;
+        dp[c][i] = pv * dp[c][i];
+      }
+      if (e == 3) { pb[c][0] = pack8(sc[c], 0); dsb[c][0] = pack8(dp[c], 0); }
+      if (e == 7) { pb[c][1] = pack8(sc[c], 1); dsb[c][1] = pack8(dp[c], 1); }
+    };
+    v8bf ops[2][4];
+    load_ops(0, ops[0]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      if (t + 1 < 16) load_ops(t + 1, ops[(t + 1) & 1]);
+      if (t < 9) dma_piece(nx, t);
+      mfma_step(t, ops[t & 1]);
+      if (t >= 4 && t < 8) softmax2(0, t - 4);                  // half 0, elements 0-7 (pack 0 before step 8)
+      if (t == 8 || t == 9) { softmax2(0, 2 * t - 12); softmax2(0, 2 * t - 11); }  // elements 8-15 (pack 1 before 10)
+      if (t == 10 || t == 11) { softmax2(1, 2 * t - 20); softmax2(1, 2 * t - 19); }  // half 1, 0-7 (before 12)
+      if (t == 12 || t == 13) { softmax2(1, 2 * t - 20); softmax2(1, 2 * t - 19); }  // half 1, 8-15 (before 14)
+      if (SCHED & 1) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);  // DS reads (the next step's fragments) first
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);  // then MFMA, VALU, MFMA, VALU ...
+          __builtin_amdgcn_sched_group_barrier(0x2, 7, 0);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  auto slice = [&](auto masked, int it, const char* q_img, const char* d_img, const float* lse_s, char* nq, char* nd,
+                   float* nl) {
+    int h, q0;
+    coords(it, h, q0);
+    body(masked, q0, q_img, d_img, lse_s, lane, next_of(it + 1, nq, nd, nl));  // the body streams slice it + 1 in
+    wait_dma_and_sync();
+  };
+  // plain slices, then (causal, when the sweep reaches the diagonal: the last two slices q0 = kt * 128 - off, + 64 of
+  // every head) the masked ones; one body per loop keeps the loop-carried dK / dV in the same registers (a per-slice
+  // choice between bodies made hipcc copy them between AGPR and VGPR copies at every join). A wave whose keys no query
+  // of a diagonal slice sees runs it fully masked (zero contribution). Both counts are even (per, off, the slice origin
+  // are multiples of 128), so the two static buffers alternate in pairs.
+  const int n_diag = (CAUSAL && kt * 128 >= off) ? 2 : 0;
+  const int n_plain = (per - n_diag) * grp;
+  int it = 0;
+  for (; it < n_plain; it += 2) {
+    slice(std::false_type{}, it, qs0, ds0, ls0, qs1, ds1, ls1);
+    __builtin_amdgcn_sched_barrier(0);
+    slice(std::false_type{}, it + 1, qs1, ds1, ls1, qs0, ds0, ls0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  for (; it < n_it; it += 2) {
+    slice(std::true_type{}, it, qs0, ds0, ls0, qs1, ds1, ls1);
+    __builtin_amdgcn_sched_barrier(0);
+    slice(std::true_type{}, it + 1, qs1, ds1, ls1, qs0, ds0, ls0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  auto store = [&](const f32x16(&acc)[4], bf16_t* dst, long ts, long bs, float scale) {
+    bf16_t* out = dst + b * bs + (long)(kw0 + r) * ts + (long)kh * kD;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 o;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) o.v[t] = f2bf(acc[d][4 * g + t] * scale);
+        *reinterpret_cast<bf16x4*>(out + d * 32 + 8 * g + 4 * hf) = o;
+      }
+  };
+  store(dk, p.dk, p.dk_ts, p.dk_bs, p.scale);
+  store(dv, p.dv, p.dv_ts, p.dv_bs, 1.f);
+  wave_trace(p.trace, t_start, wave, (unsigned)kt | ((unsigned)kh << 16));
+}
+
 void check_qkv(const torch::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16, name, " must be a bf16 HIP tensor");
   TORCH_CHECK(t.dim() == 4 && t.size(3) == kD && t.stride(3) == 1 && t.stride(2) == kD,
@@ -854,6 +1369,16 @@ template __global__ void attn_bwd_dkdv_kernel<true, 1>(BwdParams);
 template __global__ void attn_bwd_dkdv_kernel<true, 2>(BwdParams);
 template __global__ void attn_bwd_dkdv_kernel<true, 3>(BwdParams);
 template __global__ void attn_bwd_dkdv_kernel<false, 0>(BwdParams);
+template __global__ void attn_bwd_dq_w4_kernel<true>(BwdParams);
+template __global__ void attn_bwd_dq_w4_kernel<false>(BwdParams);
+template __global__ void attn_bwd_dkdv_w4_kernel<true, 0>(BwdParams);
+template __global__ void attn_bwd_dkdv_w4_kernel<false, 0>(BwdParams);
+template __global__ void attn_bwd_dkdv_w4_kernel<true, 1>(BwdParams);
+template __global__ void attn_bwd_dkdv_w4_kernel<false, 1>(BwdParams);
+template __global__ void attn_bwd_dkdv_w4_kernel<true, 2>(BwdParams);
+template __global__ void attn_bwd_dkdv_w4_kernel<false, 2>(BwdParams);
+template __global__ void attn_bwd_dkdv_w4_kernel<true, 3>(BwdParams);
+template __global__ void attn_bwd_dkdv_w4_kernel<false, 3>(BwdParams);
 
 }  // namespace
 
@@ -863,6 +1388,21 @@ ACC_DEBUG_TAKE_FN(acc_dbg_take_flash_attn)
 // normal dK/dV kernel, bits 0-1 = run a dK/dV DBG variant instead. 0 = normal operation.
 static int g_attn_dbg = 0;
 void attn_debug_mode(int64_t mode) { g_attn_dbg = (int)mode; }
+
+// dK / dV kernel choice: waves 4 = one wave per SIMD (attn_bwd_dkdv_w4_kernel, its SCHED variant `sched`), 8 = the
+// 8-wave kernel. Initial values from ACCELERATE_ATTN_DKDV / ACCELERATE_ATTN_DKDV_SCHED; tools/bench_attn.py
+// --dkdv-variants switches them between timed runs in one process.
+static int env_int(const char* name, int dflt) { const char* e = std::getenv(name); return e ? std::atoi(e) : dflt; }
+static int g_dkdv_waves = env_int("ACCELERATE_ATTN_DKDV", 4);
+static int g_dkdv_sched = env_int("ACCELERATE_ATTN_DKDV_SCHED", 0);
+static int g_dq_waves = env_int("ACCELERATE_ATTN_DQ_W4", 0) ? 4 : 8;  // dQ: 4 = attn_bwd_dq_w4_kernel, 8 = 8-wave
+void attn_dkdv_config(int64_t waves, int64_t sched, int64_t dq_waves) {
+  TORCH_CHECK((waves == 4 && sched >= 0 && sched <= 3) || waves == 8, "attn_dkdv_config: waves 4 (sched 0-3) or 8");
+  TORCH_CHECK(dq_waves == 4 || dq_waves == 8, "attn_dkdv_config: dQ waves 4 or 8");
+  g_dkdv_waves = (int)waves;
+  g_dkdv_sched = (int)sched;
+  g_dq_waves = (int)dq_waves;
+}
 
 // Timeline buffer for the next launches (tools/attn_timeline.py): an int64 HIP tensor with 32 entries per workgroup
 // of the largest grid launched, or an empty tensor to switch tracing off. The caller keeps the tensor alive.
@@ -967,6 +1507,13 @@ void flash_attn_bwd(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch:
   // key-tile width of the two-head dQ kernel (ACCELERATE_ATTN_DQ_KEYS=64 | 128)
   static const int dq_keys = [] { const char* e = std::getenv("ACCELERATE_ATTN_DQ_KEYS"); return e ? std::atoi(e) : 64; }();
   auto launch_dq = [&](bool c) {
+    if (g_dq_waves == 4) {
+      const dim3 g4(Hq, S / 128, B);
+      p.trace = g_attn_trace == nullptr ? nullptr : trace_for(g4);
+      if (c) hipLaunchKernelGGL((attn_bwd_dq_w4_kernel<true>), g4, dim3(256), 0, stream, p);
+      else hipLaunchKernelGGL((attn_bwd_dq_w4_kernel<false>), g4, dim3(256), 0, stream, p);
+      return;
+    }
     if (nh == 2 && dq_keys == 128) {
       if (c) hipLaunchKernelGGL((attn_bwd_dq_kernel<true, 2, 4>), dq_grid, dim3(512), 0, stream, p);
       else hipLaunchKernelGGL((attn_bwd_dq_kernel<false, 2, 4>), dq_grid, dim3(512), 0, stream, p);
@@ -983,20 +1530,39 @@ void flash_attn_bwd(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch:
   pk.trace = g_attn_trace == nullptr ? nullptr : trace_for(kv_grid) + (long)dq_grid.x * dq_grid.y * dq_grid.z * 32;
   TORCH_CHECK(g_attn_trace == nullptr || (long)(dq_grid.x * dq_grid.y * dq_grid.z + kv_grid.x * kv_grid.y) * 32 <= g_attn_trace_len,
               "attn_trace: buffer too small for the dQ + dK/dV grids");
+  const int dkdv_waves = g_dkdv_waves, dkdv_sched = g_dkdv_sched;
+  auto launch_w4 = [&](bool c) {
+    if (dkdv_sched == 1) {
+      if (c) hipLaunchKernelGGL((attn_bwd_dkdv_w4_kernel<true, 1>), kv_grid, dim3(256), 0, stream, pk);
+      else hipLaunchKernelGGL((attn_bwd_dkdv_w4_kernel<false, 1>), kv_grid, dim3(256), 0, stream, pk);
+    } else if (dkdv_sched == 2) {
+      if (c) hipLaunchKernelGGL((attn_bwd_dkdv_w4_kernel<true, 2>), kv_grid, dim3(256), 0, stream, pk);
+      else hipLaunchKernelGGL((attn_bwd_dkdv_w4_kernel<false, 2>), kv_grid, dim3(256), 0, stream, pk);
+    } else if (dkdv_sched == 3) {
+      if (c) hipLaunchKernelGGL((attn_bwd_dkdv_w4_kernel<true, 3>), kv_grid, dim3(256), 0, stream, pk);
+      else hipLaunchKernelGGL((attn_bwd_dkdv_w4_kernel<false, 3>), kv_grid, dim3(256), 0, stream, pk);
+    } else {
+      if (c) hipLaunchKernelGGL((attn_bwd_dkdv_w4_kernel<true, 0>), kv_grid, dim3(256), 0, stream, pk);
+      else hipLaunchKernelGGL((attn_bwd_dkdv_w4_kernel<false, 0>), kv_grid, dim3(256), 0, stream, pk);
+    }
+  };
   if (causal && g_attn_dbg != 0) {  // diagnostic timing variants (tools/bench_attn.py --dbg)
     if (g_attn_dbg & 8) launch_dq(true);
     const int m = g_attn_dbg & 3;
     if (m == 1) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<true, 1>), kv_grid, dim3(512), 0, stream, pk);
     else if (m == 2) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<true, 2>), kv_grid, dim3(512), 0, stream, pk);
     else if (m == 3) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<true, 3>), kv_grid, dim3(512), 0, stream, pk);
-    else if (g_attn_dbg & 4) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<true, 0>), kv_grid, dim3(512), 0, stream, pk);
+    else if (g_attn_dbg & 4) {
+      if (dkdv_waves == 4) launch_w4(true);
+      else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<true, 0>), kv_grid, dim3(512), 0, stream, pk);
+    }
     return;
   }
-  if (causal) {
-    launch_dq(true);
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<true, 0>), kv_grid, dim3(512), 0, stream, pk);
+  launch_dq(causal);
+  if (dkdv_waves == 4) {
+    launch_w4(causal);
   } else {
-    launch_dq(false);
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<false, 0>), kv_grid, dim3(512), 0, stream, pk);
+    if (causal) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<true, 0>), kv_grid, dim3(512), 0, stream, pk);
+    else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<false, 0>), kv_grid, dim3(512), 0, stream, pk);
   }
 }

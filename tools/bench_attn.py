@@ -18,6 +18,10 @@ p.add_argument("--no-sdpa", action="store_true")
 p.add_argument("--isolated", action="store_true", help="also time single launches after a 50 ms idle gap")
 p.add_argument("--dbg", action="store_true", help="also time the causal backward's kernels separately and the dK/dV "
                "diagnostic variants (cache-hot fetch / no LDS commit); timing only")
+p.add_argument("--dkdv-variants", default="", help="comma list of dq_waves:dkdv_waves:sched backward kernel choices "
+               "(e.g. 8:8:0,4:4:2) timed in interleaved rounds in this process: causal / full backward and the causal "
+               "dK/dV and dQ kernels alone")
+p.add_argument("--rounds", type=int, default=3)
 a = p.parse_args()
 e = _ext.ext()
 D = 128
@@ -58,6 +62,40 @@ if a.dbg:
         dbg[name + "_ms"] = round((time.perf_counter() - t) / a.iters * 1e3, 3)
     e.attn_debug_mode(0)
     res["causal_bwd_parts"] = dbg
+if a.dkdv_variants:
+    variants = [tuple(int(x) for x in v.split(":")) for v in a.dkdv_variants.split(",")]
+    e.attn_debug_mode(0)
+    data = {}
+    for causal in (True, False):
+        o, lse = e.flash_attn_fwd(q, k, v, scale, causal)
+        do = torch.randn_like(o)
+        data[causal] = (o, lse, do)
+
+    def timed(fn, n):
+        fn(); torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(n): fn()
+        e1.record(); e1.synchronize()
+        return e0.elapsed_time(e1) / n
+    best = {}
+    for _ in range(a.rounds):
+        for qw, w, sch in variants:
+            e.attn_dkdv_config(w, sch, qw)
+            row = best.setdefault(f"{qw}:{w}:{sch}", {})
+            for causal in (True, False):
+                o, lse, do = data[causal]
+                t = timed(lambda: e.flash_attn_bwd(do, q, k, v, o, lse, dq, dk, dv, scale, causal), a.iters)
+                key = "causal_bwd_ms" if causal else "full_bwd_ms"
+                row[key] = round(min(row.get(key, 1e9), t), 4)
+            o, lse, do = data[True]
+            for name, mode in (("causal_dkdv_only_ms", 4), ("causal_dq_only_ms", 8)):  # + the delta pass
+                e.attn_debug_mode(mode)
+                t = timed(lambda: e.flash_attn_bwd(do, q, k, v, o, lse, dq, dk, dv, scale, True), a.iters)
+                e.attn_debug_mode(0)
+                row[name] = round(min(row.get(name, 1e9), t), 4)
+    e.attn_dkdv_config(4, 0, 4)
+    res["dkdv_variants"] = best
 if a.isolated:
     # one kernel at a time after an idle gap (clock recovered), timed by events around the single launch: against the
     # back-to-back loop above this separates sustained-power clock effects from the kernels' own cost
