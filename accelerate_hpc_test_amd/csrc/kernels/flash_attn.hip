@@ -920,6 +920,11 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_w4_kernel(BwdParams p) {
     qf[s] = *reinterpret_cast<const v8bf*>(qb + 16 * s);
     df[s] = *reinterpret_cast<const v8bf*>(dob + 16 * s);
   }
+  // pin the Q / dO fragments in AGPRs here, away from their MFMA readers: a v_accvgpr_write right in front of an asm
+  // MFMA that reads it is a hazard hipcc does not pad (tools/check_mfma_asm_hazards.py checks the build)
+#pragma unroll
+  for (int s = 0; s < 8; ++s) asm volatile("" : "+a"(qf[s]), "+a"(df[s]));
+  asm volatile("s_nop 2");
   const long st = ((long)b * p.Hq + h) * p.S + qw0 + r;
   const float lse2 = p.lse[st] * kLog2e;
   float dlt;
@@ -1128,6 +1133,11 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_w4_kernel(BwdParams p) {
       kf[s] = *reinterpret_cast<const v8bf*>(kp + 16 * s);
       vf[s] = *reinterpret_cast<const v8bf*>(vp + 16 * s);
     }
+  }
+  if (SCHED & 2) {  // the asm S / dP MFMAs read K / V from AGPRs: pin them there now, away from those readers
+#pragma unroll
+    for (int s = 0; s < 8; ++s) asm volatile("" : "+a"(kf[s]), "+a"(vf[s]));
+    asm volatile("s_nop 2");
   }
   f32x16 dk[4], dv[4];
 #pragma unroll
@@ -1394,7 +1404,7 @@ void attn_debug_mode(int64_t mode) { g_attn_dbg = (int)mode; }
 // --dkdv-variants switches them between timed runs in one process.
 static int env_int(const char* name, int dflt) { const char* e = std::getenv(name); return e ? std::atoi(e) : dflt; }
 static int g_dkdv_waves = env_int("ACCELERATE_ATTN_DKDV", 4);
-static int g_dkdv_sched = env_int("ACCELERATE_ATTN_DKDV_SCHED", 0);
+static int g_dkdv_sched = env_int("ACCELERATE_ATTN_DKDV_SCHED", 2);
 static int g_dq_waves = env_int("ACCELERATE_ATTN_DQ_W4", 0) ? 4 : 8;  // dQ: 4 = attn_bwd_dq_w4_kernel, 8 = 8-wave
 void attn_dkdv_config(int64_t waves, int64_t sched, int64_t dq_waves) {
   TORCH_CHECK((waves == 4 && sched >= 0 && sched <= 3) || waves == 8, "attn_dkdv_config: waves 4 (sched 0-3) or 8");

@@ -84,7 +84,7 @@ for step in "$@"; do
              run attn_w4 300 python tools/bench_attn.py --no-sdpa && ACCELERATE_ATTN_DKDV=8 run attn_w8 300 python tools/bench_attn.py --no-sdpa && \
              ACCELERATE_ATTN_DKDV_SCHED=1 run attn_w4s1 300 python tools/bench_attn.py --no-sdpa ;;
     attn_dkdv) run ktest_attn 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "flash or attention or context_parallel" && \
-               ACCELERATE_ATTN_DKDV_SCHED=2 run ktest_attn_s2 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "flash or attention or context_parallel" && \
+               ACCELERATE_ATTN_DQ_W4=1 ACCELERATE_ATTN_DKDV_SCHED=2 run ktest_attn_s2 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "flash or attention or context_parallel" && \
                run attn_dkdv 300 python tools/bench_attn.py --no-sdpa --dkdv-variants ${DKDV_VARIANTS:-8:8:0,8:4:0,8:4:2,8:4:3,4:4:0,4:4:2} ;;
     attn_var) for v in ${ATTN_VARIANTS:-0 2 3}; do ACCELERATE_ATTN_DKDV_SCHED=$v run ktest_attn_s$v 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "flash or attention or context_parallel" && \
               ACCELERATE_ATTN_DKDV_SCHED=$v run attn_s$v 300 python tools/bench_attn.py --no-sdpa || exit 1; done ;;
