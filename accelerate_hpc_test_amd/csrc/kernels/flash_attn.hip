@@ -266,6 +266,9 @@ struct TileDMA {
     for (int t = 0; t < kPer; ++t)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, img + (first + t) * 1024, 16, voff[t], so, 0, 0);
   }
+  __device__ __forceinline__ void issue_piece_at(__amdgpu_buffer_rsrc_t rs, int soff, char* img, int t) const {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, img + (first + t) * 1024, 16, voff[t], soff, 0, 0);
+  }
   __device__ __forceinline__ void issue_piece(__amdgpu_buffer_rsrc_t rs, int row0, int ts_bytes, char* img, int t) const {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, img + (first + t) * 1024, 16, voff[t], row0 * ts_bytes, 0, 0);
   }
@@ -1160,34 +1163,49 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_w4_kernel(BwdParams p) {
   // the kv head (all on one XCD, see the grid) then streams the same Q / dO slice at about the same time and the XCD's
   // L2 serves it to all of them (the head-major order left the causal kernel at a 57 % L2 hit rate; at one wave per
   // SIMD the fetch latency is not hidden by a partner wave). A causal tile's diagonal slices come last.
-  auto coords = [&](int it, int& h, int& q0) {
-    h = kh * grp + it % grp;
-    q0 = (qs0_ + per - 1 - it / grp) * kSlice;
+  // Slice coordinates advance incrementally (heads innermost, slices descending): (h, q0) of the current slice and of
+  // the one being fetched, all scalar; the Q / dO descriptors cover every head of the batch row, the head rides in
+  // soffset with the first query row (no per-slice descriptor or division).
+  struct Pos {
+    int h, q0;
   };
-  // The next slice's LDS-DMA in 9 pieces (4 Q, 4 dO, then lse | delta from waves 0 | 1), one per MFMA step, so each
-  // piece's issue cost (60-185 cycles) hides beside the MFMAs instead of stalling the slice's start.
-  // Past the last slice the pieces still go out (no branch per piece): they fetch an in-range slice (or nothing: the
-  // descriptor's range check) into the buffer nobody reads any more, and the final vmcnt(0) drains them.
+  const int h_lo = kh * grp, q_last = (qs0_ + per - 1) * kSlice;
+  auto advance = [&](Pos x) {
+    if (++x.h == h_lo + grp) {
+      x.h = h_lo;
+      x.q0 -= kSlice;
+    }
+    return x;
+  };
+  auto all_rsrc = [&](const bf16_t* base, long ts) {
+    const long bytes = (long)p.S * ts * 2;
+    const unsigned long long a = reinterpret_cast<unsigned long long>(base);
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a), hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+    const int n = __builtin_amdgcn_readfirstlane((int)(bytes > 0x7fffffffL ? 0x7fffffffL : bytes));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((unsigned long long)hi << 32) | lo), (short)0, n,
+                                             0x00020000);
+  };
+  const auto qrs = all_rsrc(p.q + b * p.q_bs, p.q_ts), dors = all_rsrc(p.dout + b * p.do_bs, p.do_ts);
+  const int lrow0 = b * p.Hq * p.S * 4;
+  // The next slice's LDS-DMA in 9 pieces (4 Q, 4 dO, then lse | delta from waves 0 | 1), spread over the MFMA steps
+  // so each piece's issue cost (60-185 cycles) hides beside the MFMAs instead of stalling the slice's start. After the
+  // last slice the pieces refetch it into the buffer nobody reads any more; the final vmcnt(0) drains them.
   struct Next {
-    __amdgpu_buffer_rsrc_t qr, dr;
-    int q0, row;
+    int qoff, doff, row;
     char *qi, *di;
     float* ld;
   };
-  auto next_of = [&](int it, char* qi, char* di, float* ld) {
+  auto next_of = [&](Pos x, char* qi, char* di, float* ld) {
     Next n;
-    int h, q0;
-    coords(it < n_it ? it : n_it - 1, h, q0);
-    n.qr = head_rsrc(p.q + b * p.q_bs + (long)h * kD, p.S, p.q_ts);
-    n.dr = head_rsrc(p.dout + b * p.do_bs + (long)h * kD, p.S, p.do_ts);
-    n.q0 = q0;
-    n.row = (int)((((long)b * p.Hq + h) * p.S + q0) * 4);
+    n.qoff = x.q0 * qts + x.h * (kD * 2);
+    n.doff = x.q0 * dts + x.h * (kD * 2);
+    n.row = lrow0 + (x.h * p.S + x.q0) * 4;
     n.qi = qi; n.di = di; n.ld = ld;
     return n;
   };
   auto dma_piece = [&](const Next& n, int t) {
-    if (t < 4) dmq.issue_piece(n.qr, n.q0, qts, n.qi, t);
-    else if (t < 8) dmd.issue_piece(n.dr, n.q0, dts, n.di, t - 4);
+    if (t < 4) dmq.issue_piece_at(qrs, n.qoff, n.qi, t);
+    else if (t < 8) dmd.issue_piece_at(dors, n.doff, n.di, t - 4);
     else if (t == 8) {
       if (wv == 0) __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, n.ld, 4, lane * 4, n.row, 0, 0);
       else if (wv == 1) __builtin_amdgcn_raw_ptr_buffer_load_lds(drs, n.ld + kSlice, 4, lane * 4, n.row, 0, 0);
@@ -1195,8 +1213,9 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_w4_kernel(BwdParams p) {
   };
   DualOff lo_;
   lo_.init(lane);
+  Pos cur{h_lo, q_last};
   {
-    const Next n0 = next_of(0, qs0, ds0, ls0);
+    const Next n0 = next_of(cur, qs0, ds0, ls0);
 #pragma unroll
     for (int t = 0; t < 9; ++t) dma_piece(n0, t);
   }
@@ -1310,9 +1329,9 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_w4_kernel(BwdParams p) {
   };
   auto slice = [&](auto masked, int it, const char* q_img, const char* d_img, const float* lse_s, char* nq, char* nd,
                    float* nl) {
-    int h, q0;
-    coords(it, h, q0);
-    body(masked, q0, q_img, d_img, lse_s, lane, next_of(it + 1, nq, nd, nl));  // the body streams slice it + 1 in
+    const Pos nxt = it + 1 < n_it ? advance(cur) : cur;
+    body(masked, cur.q0, q_img, d_img, lse_s, lane, next_of(nxt, nq, nd, nl));  // the body streams slice it + 1 in
+    cur = nxt;
     wait_dma_and_sync();
   };
   // plain slices, then (causal, when the sweep reaches the diagonal: the last two slices q0 = kt * 128 - off, + 64 of
