@@ -26,3 +26,22 @@ def test_attention_asm_mfma_wait_states(tmp_path):
         out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "check_mfma_asm_hazards.py"), asm, kernel],
                              capture_output=True, text=True)
         assert out.returncode == 0, out.stdout[-3000:]
+
+
+def _lint(tmp_path, body):
+    asm = tmp_path / "k.s"
+    asm.write_text("_Z6kernelv:\n" + body + ".Lfunc_end0:\n")
+    return subprocess.run([sys.executable, os.path.join(ROOT, "tools", "check_mfma_asm_hazards.py"), str(asm), "kernel"],
+                          capture_output=True, text=True)
+
+
+def test_lint_flags_each_hazard_kind(tmp_path):
+    """The lint itself on synthetic streams: a fresh AGPR operand, an early reader of the result, and the clean forms
+    (the next MFMA of the same accumulation chain, a padded reader) that must pass."""
+    mfma = "\t;;#ASMSTART\n\tv_mfma_f32_32x32x16_bf16 v[0:15], v[16:19], a[0:3], v[0:15]\n\t;;#ASMEND\n"
+    fresh = _lint(tmp_path, "\tv_accvgpr_write_b32 a1, v40\n" + mfma)
+    assert fresh.returncode == 1 and "source read" in fresh.stdout
+    early = _lint(tmp_path, mfma + "\tv_mul_f32_e32 v20, v3, v3\n")
+    assert early.returncode == 1 and "result" in early.stdout
+    chain = _lint(tmp_path, "\ts_nop 1\n" + mfma + mfma + "\ts_nop 7\n\ts_nop 7\n\tv_mul_f32_e32 v20, v3, v3\n")
+    assert chain.returncode == 0, chain.stdout
