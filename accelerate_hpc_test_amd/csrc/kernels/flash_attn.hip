@@ -45,6 +45,7 @@ constexpr int kD = 128;
 constexpr int kRow = 256;  // bytes per image row (128 bf16)
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
+constexpr float kRescaleLog2 = 8.f;  // forward: deferred-rescale threshold (P <= 2^8 between rescales)
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }  // v_exp_f32, exp2(-inf)=0
 
@@ -400,33 +401,46 @@ __global__ __launch_bounds__(256 * NH, 2 / NH) void attn_fwd_kernel(FwdParams p)
       }
       // Max over the RAW scores (the positive scale commutes with max), then one fma per element feeds exp2:
       // p = exp2(s * scale_log2 - m).
-      float mx = -INFINITY;
+      // max and (below) row sums as trees of independent partials: a single running fmaxf / += over all KB x 16
+      // elements is a serial dependency chain of 32 v_max3 / 64 v_add per tile
+      float mxp[KB];
 #pragma unroll
-      for (int kb = 0; kb < KB; ++kb)
+      for (int kb = 0; kb < KB; ++kb) {
+        mxp[kb] = sc[kb][0];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sc[kb][i]);
+        for (int i = 1; i < 16; ++i) mxp[kb] = fmaxf(mxp[kb], sc[kb][i]);
+      }
+      float mx = mxp[0];
+#pragma unroll
+      for (int kb = 1; kb < KB; ++kb) mx = fmaxf(mx, mxp[kb]);
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float m_new = fmaxf(m, mx * p.scale_log2);
-      // Lazy rescale: once the running maxima settle, most tiles raise no lane's max and skip the O rescale.
-      if (__any(m_new > m)) {
+      // Deferred rescale: the reference max m (log2 units) moves only when some lane's tile max exceeds it by more
+      // than kRescaleLog2; below that P = exp2(s c - m) stays under 2^8 and the fp32 O / l sums carry the factor
+      // exactly, so most tiles skip the O rescale (and its wait on the previous tile's P V MFMAs). The first tile
+      // always moves m off -inf (key 0 is visible to every query).
+      const float m_cand = mx * p.scale_log2;
+      if (__any(m_cand > m + kRescaleLog2)) {
+        const float m_new = fmaxf(m, m_cand);
         const float alpha = fast_exp2(m - m_new);
         l *= alpha;
 #pragma unroll
         for (int d = 0; d < 4; ++d)
 #pragma unroll
           for (int i = 0; i < 16; ++i) o[d][i] *= alpha;
+        m = m_new;
       }
-      m = m_new;
       const float neg_m = -m;
       if constexpr (KB == 4) {  // block by block: exp, pack, P V (8 bf16 pairs live instead of 32)
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb) {
+          float lp[2] = {0.f, 0.f};
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
             const float pv = fast_exp2(fmaf(sc[kb][i], p.scale_log2, neg_m));
             sc[kb][i] = pv;
-            l += pv;
+            lp[i & 1] += pv;
           }
+          l += lp[0] + lp[1];
           const v8bf p0 = pack8(sc[kb], 0), p1 = pack8(sc[kb], 1);
 #pragma unroll
           for (int d = 0; d < 4; ++d) {
@@ -438,13 +452,16 @@ __global__ __launch_bounds__(256 * NH, 2 / NH) void attn_fwd_kernel(FwdParams p)
         return;
       }
 #pragma unroll
-      for (int kb = 0; kb < KB; ++kb)
+      for (int kb = 0; kb < KB; ++kb) {
+        float lp[2] = {0.f, 0.f};
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const float pv = fast_exp2(fmaf(sc[kb][i], p.scale_log2, neg_m));
           sc[kb][i] = pv;
-          l += pv;
+          lp[i & 1] += pv;
         }
+        l += lp[0] + lp[1];
+      }
       v8bf pb[KB][2];
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) {

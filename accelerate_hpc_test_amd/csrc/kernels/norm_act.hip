@@ -81,7 +81,7 @@ __global__ __launch_bounds__(kNormThreads) void rmsnorm_bwd_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
     const float* __restrict__ rstd, const bf16_t* __restrict__ dres, bf16_t* __restrict__ dx,
     float* __restrict__ dw_part, int T, int H, float* __restrict__ amax_part) {
-  __shared__ float scratch[16];
+  __shared__ float scratch[2][kNormThreads / 64];  // wave partials, alternating per row (one barrier per row)
   float m = 0.f;
   const int nvec = H >> 3;
   float wv[VPT][8], dwacc[VPT][8];
@@ -97,7 +97,8 @@ __global__ __launch_bounds__(kNormThreads) void rmsnorm_bwd_kernel(
       for (int j = 0; j < 8; ++j) wv[i][j] = bf2f(ww.v[j]);
     }
   }
-  for (int row = blockIdx.x; row < T; row += gridDim.x) {
+  int parity = 0;
+  for (int row = blockIdx.x; row < T; row += gridDim.x, parity ^= 1) {
     const float r = rstd[row];
     float xh[VPT][8], g[VPT][8];
     float dot = 0.f;
@@ -117,7 +118,15 @@ __global__ __launch_bounds__(kNormThreads) void rmsnorm_bwd_kernel(
         }
       }
     }
-    dot = block_sum(dot, scratch) / (float)H;
+    {  // block sum in one barrier: the row after next writes this parity's slots only after the next row's barrier
+      dot = wave_sum(dot);
+      if ((threadIdx.x & 63) == 0) scratch[parity][threadIdx.x >> 6] = dot;
+      __syncthreads();
+      float t = 0.f;
+#pragma unroll
+      for (int k = 0; k < kNormThreads / 64; ++k) t += scratch[parity][k];
+      dot = t / (float)H;
+    }
 #pragma unroll
     for (int i = 0; i < VPT; ++i) {
       const int c = threadIdx.x + i * kNormThreads;
@@ -146,7 +155,7 @@ __global__ __launch_bounds__(kNormThreads) void rmsnorm_bwd_kernel(
     }
   }
   if (amax_part != nullptr) {
-    m = block_max(m, scratch);
+    m = block_max(m, &scratch[0][0]);
     if (threadIdx.x == 0) amax_part[blockIdx.x] = m;
   }
 }
