@@ -1326,6 +1326,10 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_w4_kernel(BwdParams p) {
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int t = 0; t < 16; ++t) {
+      if (SCHED & 4) {  // one wait per step for the fragments read during the previous one (hipcc: one per MFMA)
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), vmcnt / expcnt untouched
+        __builtin_amdgcn_sched_barrier(0);
+      }
       if (t + 1 < 16) load_ops(t + 1, ops[(t + 1) & 1]);
       if (t < 9) dma_piece(nx, t);
       mfma_step(t, ops[t & 1]);
@@ -1425,6 +1429,8 @@ template __global__ void attn_bwd_dkdv_w4_kernel<true, 2>(BwdParams);
 template __global__ void attn_bwd_dkdv_w4_kernel<false, 2>(BwdParams);
 template __global__ void attn_bwd_dkdv_w4_kernel<true, 3>(BwdParams);
 template __global__ void attn_bwd_dkdv_w4_kernel<false, 3>(BwdParams);
+template __global__ void attn_bwd_dkdv_w4_kernel<true, 6>(BwdParams);
+template __global__ void attn_bwd_dkdv_w4_kernel<false, 6>(BwdParams);
 
 }  // namespace
 
@@ -1440,10 +1446,11 @@ void attn_debug_mode(int64_t mode) { g_attn_dbg = (int)mode; }
 // --dkdv-variants switches them between timed runs in one process.
 static int env_int(const char* name, int dflt) { const char* e = std::getenv(name); return e ? std::atoi(e) : dflt; }
 static int g_dkdv_waves = env_int("ACCELERATE_ATTN_DKDV", 4);
-static int g_dkdv_sched = env_int("ACCELERATE_ATTN_DKDV_SCHED", 2);
+static int g_dkdv_sched = env_int("ACCELERATE_ATTN_DKDV_SCHED", 6);
 static int g_dq_waves = env_int("ACCELERATE_ATTN_DQ_W4", 0) ? 4 : 8;  // dQ: 4 = attn_bwd_dq_w4_kernel, 8 = 8-wave
 void attn_dkdv_config(int64_t waves, int64_t sched, int64_t dq_waves) {
-  TORCH_CHECK((waves == 4 && sched >= 0 && sched <= 3) || waves == 8, "attn_dkdv_config: waves 4 (sched 0-3) or 8");
+  TORCH_CHECK((waves == 4 && ((sched >= 0 && sched <= 3) || sched == 6)) || waves == 8,
+              "attn_dkdv_config: waves 4 (sched 0-3, 6) or 8");
   TORCH_CHECK(dq_waves == 4 || dq_waves == 8, "attn_dkdv_config: dQ waves 4 or 8");
   g_dkdv_waves = (int)waves;
   g_dkdv_sched = (int)sched;
@@ -1578,20 +1585,18 @@ void flash_attn_bwd(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch:
               "attn_trace: buffer too small for the dQ + dK/dV grids");
   const int dkdv_waves = g_dkdv_waves, dkdv_sched = g_dkdv_sched;
   auto launch_w4 = [&](bool c) {
-    if (dkdv_sched == 1) {
-      if (c) hipLaunchKernelGGL((attn_bwd_dkdv_w4_kernel<true, 1>), kv_grid, dim3(256), 0, stream, pk);
-      else hipLaunchKernelGGL((attn_bwd_dkdv_w4_kernel<false, 1>), kv_grid, dim3(256), 0, stream, pk);
-    } else if (dkdv_sched == 2) {
-      if (c) hipLaunchKernelGGL((attn_bwd_dkdv_w4_kernel<true, 2>), kv_grid, dim3(256), 0, stream, pk);
-      else hipLaunchKernelGGL((attn_bwd_dkdv_w4_kernel<false, 2>), kv_grid, dim3(256), 0, stream, pk);
-    } else if (dkdv_sched == 3) {
-      if (c) hipLaunchKernelGGL((attn_bwd_dkdv_w4_kernel<true, 3>), kv_grid, dim3(256), 0, stream, pk);
-      else hipLaunchKernelGGL((attn_bwd_dkdv_w4_kernel<false, 3>), kv_grid, dim3(256), 0, stream, pk);
-    } else {
-      if (c) hipLaunchKernelGGL((attn_bwd_dkdv_w4_kernel<true, 0>), kv_grid, dim3(256), 0, stream, pk);
-      else hipLaunchKernelGGL((attn_bwd_dkdv_w4_kernel<false, 0>), kv_grid, dim3(256), 0, stream, pk);
+#define ACC_DKDV_W4(S_)                                                                                 \
+  case S_:                                                                                              \
+    if (c) hipLaunchKernelGGL((attn_bwd_dkdv_w4_kernel<true, S_>), kv_grid, dim3(256), 0, stream, pk);  \
+    else hipLaunchKernelGGL((attn_bwd_dkdv_w4_kernel<false, S_>), kv_grid, dim3(256), 0, stream, pk);   \
+    break;
+    switch (dkdv_sched) {
+      ACC_DKDV_W4(0) ACC_DKDV_W4(1) ACC_DKDV_W4(2) ACC_DKDV_W4(3) ACC_DKDV_W4(6)
+      default: TORCH_CHECK(false, "dK/dV w4 variant ", dkdv_sched, " not built");
     }
+#undef ACC_DKDV_W4
   };
+
   if (causal && g_attn_dbg != 0) {  // diagnostic timing variants (tools/bench_attn.py --dbg)
     if (g_attn_dbg & 8) launch_dq(true);
     const int m = g_attn_dbg & 3;

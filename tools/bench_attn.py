@@ -94,7 +94,7 @@ if a.dkdv_variants:
                 t = timed(lambda: e.flash_attn_bwd(do, q, k, v, o, lse, dq, dk, dv, scale, True), a.iters)
                 e.attn_debug_mode(0)
                 row[name] = round(min(row.get(name, 1e9), t), 4)
-    e.attn_dkdv_config(4, 2, 8)
+    e.attn_dkdv_config(4, 6, 8)
     res["dkdv_variants"] = best
 if a.isolated:
     # one kernel at a time after an idle gap (clock recovered), timed by events around the single launch: against the

@@ -84,7 +84,7 @@ for step in "$@"; do
              run attn_w4 300 python tools/bench_attn.py --no-sdpa && ACCELERATE_ATTN_DKDV=8 run attn_w8 300 python tools/bench_attn.py --no-sdpa && \
              ACCELERATE_ATTN_DKDV_SCHED=1 run attn_w4s1 300 python tools/bench_attn.py --no-sdpa ;;
     attn_dkdv) run ktest_attn 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "flash or attention or context_parallel" && \
-               ACCELERATE_ATTN_DQ_W4=1 ACCELERATE_ATTN_DKDV_SCHED=2 run ktest_attn_s2 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "flash or attention or context_parallel" && \
+               ACCELERATE_ATTN_DQ_W4=1 ACCELERATE_ATTN_DKDV_SCHED=${KTEST_SCHED:-2} run ktest_attn_s2 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "flash or attention or context_parallel" && \
                run attn_dkdv 300 python tools/bench_attn.py --no-sdpa --dkdv-variants ${DKDV_VARIANTS:-8:8:0,8:4:0,8:4:2,8:4:3,4:4:0,4:4:2} ;;
     attn_var) for v in ${ATTN_VARIANTS:-0 2 3}; do ACCELERATE_ATTN_DKDV_SCHED=$v run ktest_attn_s$v 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "flash or attention or context_parallel" && \
               ACCELERATE_ATTN_DKDV_SCHED=$v run attn_s$v 300 python tools/bench_attn.py --no-sdpa || exit 1; done ;;
@@ -104,6 +104,7 @@ for step in "$@"; do
     bench20_k128) ACCELERATE_ATTN_FWD_KEYS=128 run bench20_k128 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     attn_long) run attn_long 300 python tools/bench_attn.py --S 32768 --iters 3 ;;
     pmc_attn) run pmc_attn 200 bash tools/pmc_attn.sh ;;
+    pmc_attn_var) run pmc_attn_var 200 bash tools/pmc_attn.sh --no-sdpa --dkdv-variants 8:4:2,4:4:2 --rounds 1 ;;
     gemm) run gemm 300 python tools/bench_gemm.py ;;
     asmdiag) run asmdiag 120 python tools/debug/fp8asm_diag.py ;;
     gemm_grp) run gemm_grp 400 python tools/bench_gemm.py --variants ${GEMM_VARIANTS:-bl,18,18g1,18g2,18g8,18g16} --no-bf16 --no-scaled-mm --rounds 3 ;;
