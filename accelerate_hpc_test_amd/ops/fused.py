@@ -25,13 +25,18 @@ _DGRAD_BLASLT = os.environ.get("ACCELERATE_DGRAD_BLASLT", "0") == "1"
 # (ACCELERATE_ASM_BF16_GEMM=1): it runs at 0.93-1.04x hipBLASLt's bf16 kernels on the Llama-3-8B shapes (both ~1.45
 # PF/s, the bf16 loop is clock-bound like the fp8 one) and its wgrad needs a transposed dy, so the step is 3 % slower
 # with it (profiles/r5_gemm_fp8_asm.md, "bf16 on the same kernel").
-_ASM_BF16 = os.environ.get("ACCELERATE_ASM_BF16_GEMM", "0") == "1"
+# The value is "1" / "all" or a comma list of the products to move: fwd, dgrad, wgrad.
+_ASM_BF16_ENV = os.environ.get("ACCELERATE_ASM_BF16_GEMM", "0").strip().lower()
+_ASM_BF16_KINDS = ({"fwd", "dgrad", "wgrad"} if _ASM_BF16_ENV in ("1", "all")
+                   else {k.strip() for k in _ASM_BF16_ENV.split(",") if k.strip() in ("fwd", "dgrad", "wgrad")})
+_ASM_BF16 = bool(_ASM_BF16_KINDS)
 
 
-def asm_gemm_bf16(a: torch.Tensor, b: torch.Tensor, bias=None, out=None, accumulate: bool = False):
+def asm_gemm_bf16(a: torch.Tensor, b: torch.Tensor, bias=None, out=None, accumulate: bool = False, kind: str = "fwd"):
     """out (=|+=) a . bᵀ (+ bias) for bf16 a [M, K], b [N, K] (both contraction-contiguous) on the asm kernel, or None
-    when it does not apply (switched off, not native, CPU, shape not a multiple of its 256x256x64 tile)."""
-    if not (_ASM_BF16 and a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.dim() == 2
+    when it does not apply (this product kind not switched on, not native, CPU, shape not a multiple of its 256x256x64
+    tile)."""
+    if not (kind in _ASM_BF16_KINDS and a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.dim() == 2
             and b.dim() == 2 and a.is_contiguous() and b.is_contiguous() and use_native(a)):
         return None
     m, k = a.shape
@@ -389,7 +394,7 @@ def linear_dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     if (_DGRAD_WT and dy2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and w.is_contiguous()
             and w.shape[0] % 64 == 0 and w.shape[1] % 64 == 0 and use_native(dy2)):
         wt = ext().transpose_bf16(w)
-        dx = asm_gemm_bf16(dy2, wt) if dy2.is_contiguous() else None
+        dx = asm_gemm_bf16(dy2, wt, kind="dgrad") if dy2.is_contiguous() else None
         return dx if dx is not None else torch.nn.functional.linear(dy2, wt)
     return dy2 @ w
 
@@ -403,10 +408,11 @@ def wgrad_into(dest: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, accumula
     if b.dtype != a.dtype:
         b = b.to(a.dtype)
     # asm kernel: both operands token-contiguous -- x2 is the transposed view of the saved xᵀ, dy2 is transposed here
-    if (_ASM_BF16 and dest.is_cuda and dest.is_contiguous() and a.dtype == torch.bfloat16 and b.t().is_contiguous()
+    if ("wgrad" in _ASM_BF16_KINDS and dest.is_cuda and dest.is_contiguous() and a.dtype == torch.bfloat16
+            and b.t().is_contiguous()
             and dy2.is_contiguous() and dy2.shape[0] % 256 == 0 and dy2.shape[1] % 256 == 0 and b.shape[1] % 256 == 0
             and dest.dtype in (torch.float32, torch.bfloat16) and use_native(dy2)):
-        if asm_gemm_bf16(ext().transpose_bf16(dy2), b.t(), None, dest, accumulate) is not None:
+        if asm_gemm_bf16(ext().transpose_bf16(dy2), b.t(), None, dest, accumulate, kind="wgrad") is not None:
             return
     if dest.dtype == a.dtype:
         dest.addmm_(a, b) if accumulate else torch.mm(a, b, out=dest)

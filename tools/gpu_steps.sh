@@ -32,6 +32,8 @@ for step in "$@"; do
     bench20_fp8) run bench20_fp8 600 python bench.py --gpus 1 --steps 20 --warmup 5 --precision fp8 ;;
     bench20_adambf16) run bench20_adambf16 600 python bench.py --gpus 1 --steps 20 --warmup 5 --adam-states bf16 ;;
     bench20_asm) ACCELERATE_ASM_BF16_GEMM=1 run bench20_asm 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    bench20_asmw) ACCELERATE_ASM_BF16_GEMM=wgrad run bench20_asmw 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    prof8b_asmw) ACCELERATE_ASM_BF16_GEMM=wgrad prof prof8b_asmw 600 bench.py --steps 3 --warmup 2 $BENCH_ARGS ;;
     bench20_fp8bl) ACCELERATE_FP8_GEMM=blaslt run bench20_fp8bl 600 python bench.py --gpus 1 --steps 20 --warmup 5 --precision fp8 ;;
     bench20_fp8hip) ACCELERATE_FP8_GEMM=hip run bench20_fp8hip 600 python bench.py --gpus 1 --steps 20 --warmup 5 --precision fp8 ;;
     bench8b) run bench8b 600 python bench.py --steps 5 --warmup 2 $BENCH_ARGS ;;
