@@ -103,7 +103,7 @@ void grad_shard_update(torch::Tensor dst, torch::Tensor src, double scale, bool 
 void register_runtime(pybind11::module& m);
 void cpu_adam_step(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, c10::optional<torch::Tensor> shadow,
                    double lr, double beta1, double beta2, double eps, double wd, double bc1, double bc2_sqrt, bool adamw);
-bool blaslt_wgrad_f32(torch::Tensor dy, torch::Tensor x, torch::Tensor out, bool accumulate, bool x_t);
+bool blaslt_wgrad_f32(torch::Tensor dy, torch::Tensor x, torch::Tensor out, bool accumulate, bool x_t, bool dy_t);
 bool blaslt_dgrad_bf16(torch::Tensor dy, torch::Tensor w, torch::Tensor out);
 std::vector<std::tuple<int64_t, int64_t, int64_t, int64_t, double>> blaslt_wgrad_plans();
 bool blaslt_fp8_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor sa, torch::Tensor sb, double alpha, torch::Tensor out,
@@ -173,7 +173,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("blaslt_dgrad_bf16", &blaslt_dgrad_bf16, pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("out"),
         "dx = dy . W (bf16, both row-major: the NN layout) on a searched hipBLASLt algorithm; False if none");
   m.def("blaslt_wgrad_f32", &blaslt_wgrad_f32, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("out"), pybind11::arg("accumulate"),
-        pybind11::arg("x_t") = false);
+        pybind11::arg("x_t") = false, pybind11::arg("dy_t") = false);
   m.def("cpu_adam_step", &cpu_adam_step);
   m.def("blaslt_wgrad_plans", &blaslt_wgrad_plans);
   m.def("blaslt_fp8_gemm", &blaslt_fp8_gemm, "per-tensor-scaled fp8 GEMM on hipBLASLt (C = alpha sa sb A B^T)",

@@ -51,7 +51,7 @@ struct State {
   // one workspace per HIP stream: GEMMs enqueued on different streams (MoE experts spread over side streams) run
   // concurrently, and a shared workspace would be written by both
   std::map<hipStream_t, torch::Tensor> stream_ws;
-  std::map<std::tuple<int64_t, int64_t, int64_t, int, bool>, Plan> plans;
+  std::map<std::tuple<int64_t, int64_t, int64_t, int, int>, Plan> plans;  // (T bucket, N, K, device, x_t | dy_t << 1)
   std::mutex mu;
 };
 
@@ -127,15 +127,18 @@ int search_best(const std::vector<hipblasLtMatmulHeuristicResult_t>& res, int go
   return best;
 }
 
-bool build_plan(State& s, Plan& p, int64_t T, int64_t N, int64_t K, bool x_t, hipStream_t stream,
+// dy_t: dy arrives transposed ([N, T], token-contiguous), so both operands are contraction-contiguous (the TN class of
+// the forward GEMMs) instead of dy being read across its rows.
+bool build_plan(State& s, Plan& p, int64_t T, int64_t N, int64_t K, bool x_t, bool dy_t, hipStream_t stream,
                 const torch::Tensor& like) {
-  const hipblasOperation_t ta = x_t ? HIPBLAS_OP_T : HIPBLAS_OP_N, tb = HIPBLAS_OP_T;
+  const hipblasOperation_t ta = x_t ? HIPBLAS_OP_T : HIPBLAS_OP_N, tb = dy_t ? HIPBLAS_OP_N : HIPBLAS_OP_T;
   if (!check(hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F))) return false;
   if (!check(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta)))) return false;
   if (!check(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb)))) return false;
   if (!check(x_t ? hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16BF, T, K, T)
                  : hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16BF, K, T, K))) return false;
-  if (!check(hipblasLtMatrixLayoutCreate(&p.lb, HIP_R_16BF, N, T, N))) return false;
+  if (!check(dy_t ? hipblasLtMatrixLayoutCreate(&p.lb, HIP_R_16BF, T, N, T)
+                  : hipblasLtMatrixLayoutCreate(&p.lb, HIP_R_16BF, N, T, N))) return false;
   if (!check(hipblasLtMatrixLayoutCreate(&p.lc, HIP_R_32F, K, N, K))) return false;
   hipblasLtMatmulPreference_t pref;
   if (!check(hipblasLtMatmulPreferenceCreate(&pref))) return false;
@@ -170,11 +173,12 @@ bool build_plan(State& s, Plan& p, int64_t T, int64_t N, int64_t K, bool x_t, hi
 
 // Token count T of a bucket whose plan was searched on another T: per-call layouts (host objects), the bucket's algorithm
 // when hipBLASLt supports it for this problem, else the heuristic's first choice — no timing, no synchronisation.
-bool run_wgrad_other_t(State& s, Plan& plan, int64_t T, int64_t N, int64_t K, bool x_t, const void* x, const void* dy,
-                       void* out, float beta, void* ws, hipStream_t stream) {
+bool run_wgrad_other_t(State& s, Plan& plan, int64_t T, int64_t N, int64_t K, bool x_t, bool dy_t, const void* x,
+                       const void* dy, void* out, float beta, void* ws, hipStream_t stream) {
   hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, lc = nullptr;
   bool ok = check(x_t ? hipblasLtMatrixLayoutCreate(&la, HIP_R_16BF, T, K, T) : hipblasLtMatrixLayoutCreate(&la, HIP_R_16BF, K, T, K)) &&
-            check(hipblasLtMatrixLayoutCreate(&lb, HIP_R_16BF, N, T, N)) && check(hipblasLtMatrixLayoutCreate(&lc, HIP_R_32F, K, N, K));
+            check(dy_t ? hipblasLtMatrixLayoutCreate(&lb, HIP_R_16BF, T, N, T) : hipblasLtMatrixLayoutCreate(&lb, HIP_R_16BF, N, T, N)) &&
+            check(hipblasLtMatrixLayoutCreate(&lc, HIP_R_32F, K, N, K));
   const float one = 1.f;
   hipblasLtMatmulAlgo_t algo = plan.algo;
   if (ok) {
@@ -206,13 +210,13 @@ bool run_wgrad_other_t(State& s, Plan& plan, int64_t T, int64_t N, int64_t K, bo
 }  // namespace
 
 // Returns false (and does nothing) when hipBLASLt offers no working algorithm: the caller falls back to torch.
-bool blaslt_wgrad_f32(torch::Tensor dy, torch::Tensor x, torch::Tensor out, bool accumulate, bool x_t) {
+bool blaslt_wgrad_f32(torch::Tensor dy, torch::Tensor x, torch::Tensor out, bool accumulate, bool x_t, bool dy_t) {
   TORCH_CHECK(dy.is_cuda() && x.is_cuda() && out.is_cuda(), "blaslt_wgrad_f32: HIP tensors expected");
   TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16 && out.scalar_type() == at::kFloat,
               "blaslt_wgrad_f32: bf16 operands and an fp32 output expected");
   TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && out.dim() == 2 && dy.is_contiguous() && x.is_contiguous() && out.is_contiguous(),
               "blaslt_wgrad_f32: 2-D contiguous tensors expected");
-  const int64_t T = dy.size(0), N = dy.size(1), K = x_t ? x.size(0) : x.size(1);
+  const int64_t T = dy_t ? dy.size(1) : dy.size(0), N = dy_t ? dy.size(0) : dy.size(1), K = x_t ? x.size(0) : x.size(1);
   TORCH_CHECK((x_t ? x.size(1) : x.size(0)) == T && out.size(0) == N && out.size(1) == K, "blaslt_wgrad_f32: shape mismatch");
   State& s = state();
   hipStream_t stream = at::hip::getCurrentHIPStream();
@@ -225,17 +229,17 @@ bool blaslt_wgrad_f32(torch::Tensor dy, torch::Tensor x, torch::Tensor out, bool
       s.workspace = torch::empty({(int64_t)kWorkspace}, out.options().dtype(torch::kUInt8));
     }
     const int dev = out.get_device();
-    auto key = std::make_tuple(dim_bucket(T), N, K, dev, x_t);
+    auto key = std::make_tuple(dim_bucket(T), N, K, dev, (int)x_t | ((int)dy_t << 1));
     auto it = s.plans.find(key);
     if (it == s.plans.end()) {
       Plan p;
-      build_plan(s, p, T, N, K, x_t, stream, out);
+      build_plan(s, p, T, N, K, x_t, dy_t, stream, out);
       it = s.plans.emplace(key, p).first;
     }
     plan = &it->second;
     ws = workspace_for(s, stream, out);
     if (plan->ok && plan->T != T)
-      return run_wgrad_other_t(s, *plan, T, N, K, x_t, x.data_ptr(), dy.data_ptr(), out.data_ptr(), accumulate ? 1.f : 0.f,
+      return run_wgrad_other_t(s, *plan, T, N, K, x_t, dy_t, x.data_ptr(), dy.data_ptr(), out.data_ptr(), accumulate ? 1.f : 0.f,
                                ws, stream);
   }
   if (!plan->ok) return false;

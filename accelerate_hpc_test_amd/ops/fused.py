@@ -30,6 +30,9 @@ _ASM_BF16_ENV = os.environ.get("ACCELERATE_ASM_BF16_GEMM", "0").strip().lower()
 _ASM_BF16_KINDS = ({"fwd", "dgrad", "wgrad"} if _ASM_BF16_ENV in ("1", "all")
                    else {k.strip() for k in _ASM_BF16_ENV.split(",") if k.strip() in ("fwd", "dgrad", "wgrad")})
 _ASM_BF16 = bool(_ASM_BF16_KINDS)
+# fp32 weight gradients with dy transposed first (ACCELERATE_WGRAD_DYT=1): both hipBLASLt operands token-contiguous,
+# the TN class the forward GEMMs run in, for the price of one dy transpose per Linear
+_WGRAD_DYT = os.environ.get("ACCELERATE_WGRAD_DYT", "0") == "1"
 
 
 def asm_gemm_bf16(a: torch.Tensor, b: torch.Tensor, bias=None, out=None, accumulate: bool = False, kind: str = "fwd"):
@@ -418,6 +421,9 @@ def wgrad_into(dest: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, accumula
         dest.addmm_(a, b) if accumulate else torch.mm(a, b, out=dest)
     elif dest.is_cuda and dest.dtype == torch.float32:
         if _BLASLT_WGRAD and a.dtype == torch.bfloat16 and dy2.is_contiguous():
+            if (_WGRAD_DYT and b.t().is_contiguous() and dy2.shape[0] % 64 == 0 and dy2.shape[1] % 64 == 0
+                    and ext().blaslt_wgrad_f32(ext().transpose_bf16(dy2), b.t(), dest, accumulate, True, True)):
+                return
             if b.is_contiguous() and ext().blaslt_wgrad_f32(dy2, b, dest, accumulate, False):
                 return
             if b.t().is_contiguous() and ext().blaslt_wgrad_f32(dy2, b.t(), dest, accumulate, True):

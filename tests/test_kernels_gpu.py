@@ -895,6 +895,12 @@ def test_blaslt_wgrad_f32_matches_torch(T, N, K):
     assert _rel(out, ref) < 1e-3, _rel(out, ref)
     assert ext().blaslt_wgrad_f32(dy, xt, out, True, True)
     assert _rel(out, 2 * ref) < 1e-3
+    # dy transposed too ([N, T]): both operands token-contiguous
+    dyt = dy.t().contiguous()
+    assert ext().blaslt_wgrad_f32(dyt, xt, out, False, True, True)
+    assert _rel(out, ref) < 1e-3, _rel(out, ref)
+    assert ext().blaslt_wgrad_f32(dyt, xt, out, True, True, True)
+    assert _rel(out, 2 * ref) < 1e-3
 
 
 @pytest.mark.parametrize("precision", ["bf16", "fp8"])

@@ -33,6 +33,8 @@ for step in "$@"; do
     bench20_adambf16) run bench20_adambf16 600 python bench.py --gpus 1 --steps 20 --warmup 5 --adam-states bf16 ;;
     bench20_asm) ACCELERATE_ASM_BF16_GEMM=1 run bench20_asm 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench20_asmw) ACCELERATE_ASM_BF16_GEMM=wgrad run bench20_asmw 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    bench20_dyt) ACCELERATE_WGRAD_DYT=1 run bench20_dyt 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    prof8b_dyt) ACCELERATE_WGRAD_DYT=1 prof prof8b_dyt 600 bench.py --steps 3 --warmup 2 $BENCH_ARGS ;;
     prof8b_asmw) ACCELERATE_ASM_BF16_GEMM=wgrad prof prof8b_asmw 600 bench.py --steps 3 --warmup 2 $BENCH_ARGS ;;
     bench20_fp8bl) ACCELERATE_FP8_GEMM=blaslt run bench20_fp8bl 600 python bench.py --gpus 1 --steps 20 --warmup 5 --precision fp8 ;;
     bench20_fp8hip) ACCELERATE_FP8_GEMM=hip run bench20_fp8hip 600 python bench.py --gpus 1 --steps 20 --warmup 5 --precision fp8 ;;
@@ -88,6 +90,8 @@ for step in "$@"; do
     attn_dkdv) run ktest_attn 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "flash or attention or context_parallel" && \
                ACCELERATE_ATTN_DQ_W4=1 ACCELERATE_ATTN_DKDV_SCHED=${KTEST_SCHED:-2} run ktest_attn_s2 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "flash or attention or context_parallel" && \
                run attn_dkdv 300 python tools/bench_attn.py --no-sdpa --dkdv-variants ${DKDV_VARIANTS:-8:8:0,8:4:0,8:4:2,8:4:3,4:4:0,4:4:2} ;;
+    attn_dq128) run attn_dq64 300 python tools/bench_attn.py --no-sdpa --dkdv-variants 8:8:0,8:4:6 && \
+                ACCELERATE_ATTN_DQ_KEYS=128 run attn_dq128 300 python tools/bench_attn.py --no-sdpa --dkdv-variants 8:8:0,8:4:6 ;;
     attn_var) for v in ${ATTN_VARIANTS:-0 2 3}; do ACCELERATE_ATTN_DKDV_SCHED=$v run ktest_attn_s$v 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "flash or attention or context_parallel" && \
               ACCELERATE_ATTN_DKDV_SCHED=$v run attn_s$v 300 python tools/bench_attn.py --no-sdpa || exit 1; done ;;
     prof_attn) prof prof_attn 300 tools/bench_attn.py --no-sdpa --iters 5 && \
