@@ -51,14 +51,18 @@ def main(argv=None):
             ids = torch.tensor([prompt], device=state.device)
             done.append((idx, greedy(model, ids, args.new_tokens)[0, len(prompt):].tolist()))
     results = gather_object(done)
+    by_idx = None
     if state.is_main_process:
         by_idx = dict(results)  # padding duplicates collapse onto their index
         assert sorted(by_idx) == list(range(args.n_prompts)), sorted(by_idx)
         for i in range(min(3, args.n_prompts)):
             print(f"prompt {i}: {prompts[i]} -> {by_idx[i]}")
         print(f"generated {args.n_prompts} completions on {state.num_processes} process(es)")
-        return by_idx
-    return None
+    # tear the group down on every rank together: a rank that exits while its peer is still inside a gloo call
+    # can abort in the transport's destructor
+    state.wait_for_everyone()
+    state.destroy_process_group()
+    return by_idx
 
 
 if __name__ == "__main__":
