@@ -102,6 +102,7 @@ for step in "$@"; do
     attn_dq128) ACCELERATE_ATTN_DQ_KEYS=128 run attn_dq128 300 python tools/bench_attn.py --no-sdpa ;;
     bench20_dq128) ACCELERATE_ATTN_DQ_KEYS=128 run bench20_dq128 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench20_sharded) run bench20_sharded 600 python bench.py --gpus 1 --steps 20 --warmup 5 --fsdp-force-sharded ;;
+    bench20_sharded_nors) run bench20_sharded_nors 600 python bench.py --gpus 1 --steps 20 --warmup 5 --fsdp-force-sharded --reshard-after-forward off ;;
     bench20_ovl) run bench20_ovl 600 python bench.py --gpus 1 --steps 20 --warmup 5 --optimizer-overlap on ;;
     bench20_fp8_ovl) run bench20_fp8_ovl 600 python bench.py --gpus 1 --steps 20 --warmup 5 --precision fp8 --optimizer-overlap on ;;
     bench20_fp8_amaxoff) ACCELERATE_FP8_AMAX_IN_ADAM=0 run bench20_fp8_amaxoff 600 python bench.py --gpus 1 --steps 20 --warmup 5 --precision fp8 ;;
