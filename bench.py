@@ -282,7 +282,8 @@ def main():
                 "seq_len": args.seq,
                 # "-w1": one rank, the engine's no-collective path; "-forced-sharded": one rank running the multi-rank code
                 "parallelism": f"{args.parallel}-w{world}" + ("-forced-sharded" if force else "")
-                + ("-forced-reducer" if force_ddp else ""),
+                + ("-forced-reducer" if force_ddp else "")
+                + ("-shard-grad-op" if args.parallel == "fsdp" and args.reshard_after_forward == "off" else ""),
                 "optimizer": "AdamW(lr=1e-5), fp32 master" + (", bf16 moments" if args.adam_states == "bf16" else "")
                 + (", per-unit update overlapped with backward" if overlap else "")
                 + (", CPU-offloaded (host AdamW)" if args.fsdp_cpu_offload else ""),
