@@ -30,6 +30,7 @@ for step in "$@"; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench20) run bench20 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench20_fp8) run bench20_fp8 600 python bench.py --gpus 1 --steps 20 --warmup 5 --precision fp8 ;;
+    bench20_mxfp8) run bench20_mxfp8 600 python bench.py --gpus 1 --steps 20 --warmup 5 --precision mxfp8 ;;
     bench20_adambf16) run bench20_adambf16 600 python bench.py --gpus 1 --steps 20 --warmup 5 --adam-states bf16 ;;
     bench20_asm) ACCELERATE_ASM_BF16_GEMM=1 run bench20_asm 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench20_asmw) ACCELERATE_ASM_BF16_GEMM=wgrad run bench20_asmw 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
