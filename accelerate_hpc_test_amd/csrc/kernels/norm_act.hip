@@ -97,17 +97,58 @@ __global__ __launch_bounds__(kNormThreads) void rmsnorm_bwd_kernel(
       for (int j = 0; j < 8; ++j) wv[i][j] = bf2f(ww.v[j]);
     }
   }
+  // The next row's x / dy / dres / rstd are loaded while this row is reduced and written: one block walks T / grid
+  // rows in sequence, and without the prefetch every row paid a full HBM latency after the previous row's barrier.
+  // Only up to VPT = 2 (H <= 4096): wider rows would lose the second resident block per CU to the extra registers.
+  constexpr bool kPrefetch = VPT <= 2;
+  bf16x8 xa[VPT] = {}, xd[VPT] = {}, xr[VPT] = {};
+  float rn = 0.f;
+  auto load_row = [&](int rw) {
+    rn = rstd[rw];
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int c = threadIdx.x + i * kNormThreads;
+      if (c < nvec) {
+        xa[i] = reinterpret_cast<const bf16x8*>(x + (size_t)rw * H)[c];
+        xd[i] = reinterpret_cast<const bf16x8*>(dy + (size_t)rw * H)[c];
+        if (dres != nullptr) xr[i] = reinterpret_cast<const bf16x8*>(dres + (size_t)rw * H)[c];
+      }
+    }
+  };
+  if (kPrefetch && (int)blockIdx.x < T) load_row(blockIdx.x);
   int parity = 0;
   for (int row = blockIdx.x; row < T; row += gridDim.x, parity ^= 1) {
-    const float r = rstd[row];
+    float r;
+    bf16x8 ca[VPT], cd[VPT], cr[VPT];
+    if constexpr (kPrefetch) {
+      r = rn;
+#pragma unroll
+      for (int i = 0; i < VPT; ++i) {
+        ca[i] = xa[i];
+        cd[i] = xd[i];
+        cr[i] = xr[i];
+      }
+      if (row + (int)gridDim.x < T) load_row(row + gridDim.x);
+    } else {
+      r = rstd[row];
+#pragma unroll
+      for (int i = 0; i < VPT; ++i) {
+        const int c = threadIdx.x + i * kNormThreads;
+        if (c < nvec) {
+          ca[i] = reinterpret_cast<const bf16x8*>(x + (size_t)row * H)[c];
+          cd[i] = reinterpret_cast<const bf16x8*>(dy + (size_t)row * H)[c];
+          if (dres != nullptr) cr[i] = reinterpret_cast<const bf16x8*>(dres + (size_t)row * H)[c];
+        }
+      }
+    }
     float xh[VPT][8], g[VPT][8];
     float dot = 0.f;
 #pragma unroll
     for (int i = 0; i < VPT; ++i) {
       const int c = threadIdx.x + i * kNormThreads;
       if (c < nvec) {
-        bf16x8 a = reinterpret_cast<const bf16x8*>(x + (size_t)row * H)[c];
-        bf16x8 d = reinterpret_cast<const bf16x8*>(dy + (size_t)row * H)[c];
+        const bf16x8 a = ca[i];
+        const bf16x8 d = cd[i];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           xh[i][j] = bf2f(a.v[j]) * r;
@@ -132,8 +173,7 @@ __global__ __launch_bounds__(kNormThreads) void rmsnorm_bwd_kernel(
       const int c = threadIdx.x + i * kNormThreads;
       if (c < nvec) {
         bf16x8 o;
-        bf16x8 rr;
-        if (dres != nullptr) rr = reinterpret_cast<const bf16x8*>(dres + (size_t)row * H)[c];
+        const bf16x8 rr = cr[i];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           float val = r * (g[i][j] - xh[i][j] * dot);

@@ -25,7 +25,7 @@ def test_extension_loaded():
     assert _ext.available(), "native extension must be importable on the GPU box"
 
 
-@pytest.mark.parametrize("T,H", [(64, 256), (300, 4096), (17, 1024)])
+@pytest.mark.parametrize("T,H", [(64, 256), (300, 4096), (17, 1024), (1500, 2048), (2048, 4096), (1100, 8192)])
 @pytest.mark.parametrize("with_res", [False, True])
 def test_rmsnorm(T, H, with_res):
     torch.manual_seed(0)
