@@ -207,9 +207,18 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ p
   __shared__ float red[8][33];
   const int c = threadIdx.x & 31, rg = threadIdx.x >> 5;
   const int col = blockIdx.x * 32 + c;
-  float s = 0.f;
-  if (col < H)
-    for (int p = rg; p < P; p += 8) s += part[(size_t)p * H + col];
+  // eight independent partial sums: eight loads in flight per lane (one dependent chain left the kernel latency-bound,
+  // 18 us for 8 MB of partials)
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (col < H) {
+    int p = rg;
+    for (; p + 56 < P; p += 64) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc[u] += part[(size_t)(p + 8 * u) * H + col];
+    }
+    for (; p < P; p += 8) acc[0] += part[(size_t)p * H + col];
+  }
+  const float s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   red[rg][c] = s;
   __syncthreads();
   if (rg == 0 && col < H) {
@@ -287,11 +296,14 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const bf16_t* __restric
 // (inverse rotation of the incoming gradient). Out of place (src != dst: one read + one write of the whole row, V
 // copied) or in place (src == dst, heads_iter = n_rot_heads: V never touched).
 // ---------------------------------------------------------------------------------------------------
+// W pairs per thread step (W bf16 = 8 or 16 B of each half): 16-B accesses whenever D / 2 is a multiple of 8.
+template <int W>
 __global__ void rope_kernel(const bf16_t* __restrict__ src, bf16_t* __restrict__ dst, const float* __restrict__ cosb,
                             const float* __restrict__ sinb, const int64_t* __restrict__ pos, long T, int S,
                             int n_rot_heads, int heads_iter, int n_heads_total, int D, float sign) {
+  using vec = typename std::conditional<W == 8, bf16x8, bf16x4>::type;
   const int half = D >> 1;
-  const int nvec = half >> 2;  // 4 pairs per thread step (8 B of each half)
+  const int nvec = half / W;
   const long per_row = (long)heads_iter * nvec;
   const long total = T * per_row;
   for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
@@ -299,26 +311,30 @@ __global__ void rope_kernel(const bf16_t* __restrict__ src, bf16_t* __restrict__
     const int rem = (int)(idx - t * per_row);
     const int h = rem / nvec, c = rem - h * nvec;
     const long off = (t * n_heads_total + h) * (long)D;
-    const bf16x4 a = reinterpret_cast<const bf16x4*>(src + off)[c];
-    const bf16x4 b = reinterpret_cast<const bf16x4*>(src + off + half)[c];
-    bf16x4 oa = a, ob = b;
+    const vec a = reinterpret_cast<const vec*>(src + off)[c];
+    const vec b = reinterpret_cast<const vec*>(src + off + half)[c];
+    vec oa = a, ob = b;
     if (h < n_rot_heads) {
       const long p = pos != nullptr ? pos[t] : (t % S);
       ACC_CHECK(p >= 0 && p < S, kChkRopePos);  // debug build: a position past the cos / sin table
       if (ACC_DEBUG_BUILD && (p < 0 || p >= S)) continue;
-      const float4 cs = reinterpret_cast<const float4*>(cosb + p * half)[c];
-      const float4 sn = reinterpret_cast<const float4*>(sinb + p * half)[c];
-      const float cc[4] = {cs.x, cs.y, cs.z, cs.w};
-      const float ss[4] = {sn.x * sign, sn.y * sign, sn.z * sign, sn.w * sign};
+      float cc[W], ss[W];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int q = 0; q < W / 4; ++q) {
+        const float4 cs = reinterpret_cast<const float4*>(cosb + p * half)[c * (W / 4) + q];
+        const float4 sn = reinterpret_cast<const float4*>(sinb + p * half)[c * (W / 4) + q];
+        cc[4 * q] = cs.x; cc[4 * q + 1] = cs.y; cc[4 * q + 2] = cs.z; cc[4 * q + 3] = cs.w;
+        ss[4 * q] = sn.x * sign; ss[4 * q + 1] = sn.y * sign; ss[4 * q + 2] = sn.z * sign; ss[4 * q + 3] = sn.w * sign;
+      }
+#pragma unroll
+      for (int j = 0; j < W; ++j) {
         const float x1 = bf2f(a.v[j]), x2 = bf2f(b.v[j]);
         oa.v[j] = f2bf(x1 * cc[j] - x2 * ss[j]);
         ob.v[j] = f2bf(x2 * cc[j] + x1 * ss[j]);
       }
     }
-    reinterpret_cast<bf16x4*>(dst + off)[c] = oa;
-    reinterpret_cast<bf16x4*>(dst + off + half)[c] = ob;
+    reinterpret_cast<vec*>(dst + off)[c] = oa;
+    reinterpret_cast<vec*>(dst + off + half)[c] = ob;
   }
 }
 
@@ -509,12 +525,17 @@ static void rope_launch(const torch::Tensor& src, torch::Tensor& dst, const torc
   }
   const bool inplace = src.data_ptr() == dst.data_ptr();
   const int heads_iter = (int)(inplace ? n_rot_heads : n_heads_total);
-  const long work = T * heads_iter * (head_dim / 8);
+  const bool wide = (head_dim / 2) % 8 == 0;
+  const long work = T * heads_iter * (head_dim / (wide ? 16 : 8));
   if (work == 0) return;
-  hipLaunchKernelGGL(rope_kernel, dim3(grid_for(work, 256)), dim3(256), 0, at::hip::getCurrentHIPStream(),
-                     reinterpret_cast<const bf16_t*>(src.data_ptr()), reinterpret_cast<bf16_t*>(dst.data_ptr()),
-                     cos.data_ptr<float>(), sin.data_ptr<float>(), posp, T, S, (int)n_rot_heads, heads_iter,
-                     (int)n_heads_total, (int)head_dim, (float)sign);
+#define ROPE_GO(W_)                                                                                                  \
+  hipLaunchKernelGGL(rope_kernel<W_>, dim3(grid_for(work, 256)), dim3(256), 0, at::hip::getCurrentHIPStream(),      \
+                     reinterpret_cast<const bf16_t*>(src.data_ptr()), reinterpret_cast<bf16_t*>(dst.data_ptr()),   \
+                     cos.data_ptr<float>(), sin.data_ptr<float>(), posp, T, S, (int)n_rot_heads, heads_iter,       \
+                     (int)n_heads_total, (int)head_dim, (float)sign)
+  if (wide) ROPE_GO(8);
+  else ROPE_GO(4);
+#undef ROPE_GO
 }
 
 void rope_inplace(torch::Tensor qkv, torch::Tensor cos, torch::Tensor sin, c10::optional<torch::Tensor> pos,
