@@ -30,7 +30,8 @@ static int64_t debug_status() {
 std::vector<torch::Tensor> rmsnorm_fwd(torch::Tensor x, c10::optional<torch::Tensor> residual, torch::Tensor w, double eps,
                                        c10::optional<torch::Tensor> amax);
 std::vector<torch::Tensor> rmsnorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor w, torch::Tensor rstd,
-                                       c10::optional<torch::Tensor> dres, c10::optional<torch::Tensor> amax);
+                                       c10::optional<torch::Tensor> dres, c10::optional<torch::Tensor> amax,
+                                       c10::optional<torch::Tensor> dw_out, bool accumulate);
 torch::Tensor swiglu_fwd(torch::Tensor gu, c10::optional<torch::Tensor> amax);
 torch::Tensor transpose_bf16(torch::Tensor x);
 torch::Tensor swiglu_bwd(torch::Tensor gu, torch::Tensor dh, c10::optional<torch::Tensor> amax);
@@ -117,7 +118,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rmsnorm_fwd", &rmsnorm_fwd, pybind11::arg("x"), pybind11::arg("residual"), pybind11::arg("w"), pybind11::arg("eps"),
         pybind11::arg("amax") = pybind11::none());
   m.def("rmsnorm_bwd", &rmsnorm_bwd, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("rstd"),
-        pybind11::arg("dres"), pybind11::arg("amax") = pybind11::none());
+        pybind11::arg("dres"), pybind11::arg("amax") = pybind11::none(), pybind11::arg("dw_out") = pybind11::none(),
+        pybind11::arg("accumulate") = false);
   m.def("swiglu_fwd", &swiglu_fwd, pybind11::arg("gu"), pybind11::arg("amax") = pybind11::none());
   m.def("transpose_bf16", &transpose_bf16);
   m.def("swiglu_bwd", &swiglu_bwd, pybind11::arg("gu"), pybind11::arg("dh"), pybind11::arg("amax") = pybind11::none());

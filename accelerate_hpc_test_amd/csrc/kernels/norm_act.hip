@@ -202,7 +202,12 @@ __global__ __launch_bounds__(kNormThreads) void rmsnorm_bwd_kernel(
 
 // Column sum of the [P, H] fp32 partials → dweight (bf16 or fp32 output). 256 threads = 32 columns x 8 row
 // groups; each row group strides over the partial rows, then the 8 partial sums are combined through LDS.
-template <typename OutT>
+__device__ __forceinline__ float as_float(float v) { return v; }
+__device__ __forceinline__ float as_float(bf16_t v) { return bf2f(v); }
+
+// ACC: add into `out` (a weight-gradient slot that already holds earlier micro-batches' gradient) instead of
+// overwriting it.
+template <typename OutT, bool ACC = false>
 __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part, OutT* __restrict__ out, int P, int H) {
   __shared__ float red[8][33];
   const int c = threadIdx.x & 31, rg = threadIdx.x >> 5;
@@ -225,6 +230,7 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ p
     float t = 0.f;
 #pragma unroll
     for (int g = 0; g < 8; ++g) t += red[g][c];
+    if (ACC) t += as_float(out[col]);
     out[col] = from_f<OutT>(t);
   }
 }
@@ -425,8 +431,11 @@ std::vector<torch::Tensor> rmsnorm_fwd(torch::Tensor x, c10::optional<torch::Ten
   return {y, rstd, res_out};
 }
 
+// dw_out: write dweight straight into this [H] fp32 / bf16 tensor (an FSDP weight-gradient slot; `accumulate` adds to
+// it) instead of a new bf16 tensor that autograd would then add into the slot.
 std::vector<torch::Tensor> rmsnorm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor w, torch::Tensor rstd,
-                                       c10::optional<torch::Tensor> dres, c10::optional<torch::Tensor> amax) {
+                                       c10::optional<torch::Tensor> dres, c10::optional<torch::Tensor> amax,
+                                       c10::optional<torch::Tensor> dw_out, bool accumulate) {
   check_bf16_cuda(dy, "dy");
   check_bf16_cuda(x, "x");
   check_bf16_cuda(w, "weight");
@@ -435,7 +444,16 @@ std::vector<torch::Tensor> rmsnorm_bwd(torch::Tensor dy, torch::Tensor x, torch:
   auto dx = torch::empty_like(x);
   const int P = (int)std::min<long>(T > 0 ? T : 1, 512);
   auto part = torch::empty({P, H}, x.options().dtype(torch::kFloat32));
-  auto dw = torch::empty({H}, w.options());
+  torch::Tensor dw;
+  if (dw_out.has_value()) {
+    dw = *dw_out;
+    TORCH_CHECK(dw.is_cuda() && dw.is_contiguous() && dw.numel() == H &&
+                    (dw.scalar_type() == at::kFloat || dw.scalar_type() == at::kBFloat16),
+                "rmsnorm_bwd: dw_out must be a contiguous fp32 / bf16 HIP tensor of H elements");
+  } else {
+    dw = torch::empty({H}, w.options());
+    accumulate = false;
+  }
   auto stream = at::hip::getCurrentHIPStream();
   const bf16_t* dresp = nullptr;
   if (dres.has_value()) {
@@ -444,7 +462,7 @@ std::vector<torch::Tensor> rmsnorm_bwd(torch::Tensor dy, torch::Tensor x, torch:
   }
   const AmaxOut am(amax, P, x);
   if (T == 0) {
-    dw.zero_();
+    if (!accumulate) dw.zero_();
     am.finalize(0);
     return {dx, dw};
   }
@@ -459,8 +477,15 @@ std::vector<torch::Tensor> rmsnorm_bwd(torch::Tensor dy, torch::Tensor x, torch:
   else if (vpt <= 4) LAUNCH_BWD(4);
   else LAUNCH_BWD(8);
 #undef LAUNCH_BWD
-  hipLaunchKernelGGL(colsum_kernel<bf16_t>, dim3((H + 31) / 32), dim3(256), 0, stream, part.data_ptr<float>(),
-                     reinterpret_cast<bf16_t*>(dw.data_ptr()), P, H);
+  const dim3 cgrid((H + 31) / 32);
+  if (dw.scalar_type() == at::kFloat) {
+    if (accumulate) hipLaunchKernelGGL((colsum_kernel<float, true>), cgrid, dim3(256), 0, stream, part.data_ptr<float>(), dw.data_ptr<float>(), P, H);
+    else hipLaunchKernelGGL((colsum_kernel<float, false>), cgrid, dim3(256), 0, stream, part.data_ptr<float>(), dw.data_ptr<float>(), P, H);
+  } else {
+    bf16_t* o = reinterpret_cast<bf16_t*>(dw.data_ptr());
+    if (accumulate) hipLaunchKernelGGL((colsum_kernel<bf16_t, true>), cgrid, dim3(256), 0, stream, part.data_ptr<float>(), o, P, H);
+    else hipLaunchKernelGGL((colsum_kernel<bf16_t, false>), cgrid, dim3(256), 0, stream, part.data_ptr<float>(), o, P, H);
+  }
   am.finalize(P);
   return {dx, dw};
 }

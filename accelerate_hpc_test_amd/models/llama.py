@@ -93,7 +93,9 @@ class RMSNorm(nn.Module):
     def forward(self, x, residual=None, amax: bool = False, grad_amax: bool = False):
         # fp32 weights under autocast (DDP mixed precision): the fused kernel runs in the activation dtype.
         w = self.weight if self.weight.dtype == x.dtype else self.weight.to(x.dtype)
-        return rms_norm(x, w, self.eps, residual, amax=amax, grad_amax=grad_amax)
+        # FSDP: the backward writes dweight straight into the weight's gradient slot (parallel/fsdp.py)
+        slot = getattr(self.weight, "_acc_wgrad_slot", None) if w is self.weight else None
+        return rms_norm(x, w, self.eps, residual, amax=amax, grad_amax=grad_amax, slot=slot)
 
 
 class LlamaAttention(nn.Module):

@@ -81,10 +81,13 @@ def _amax_buf(like: torch.Tensor, want: bool):
 
 class _RMSNormFn(torch.autograd.Function):
     """`amax` / `grad_amax`: also produce max|y| (forward) / max|dx| (backward) for a consuming fp8 linear (its input /
-    its output gradient), tagged on the tensor (ops/fp8.py `tag_amax`) instead of re-read by a separate amax pass."""
+    its output gradient), tagged on the tensor (ops/fp8.py `tag_amax`) instead of re-read by a separate amax pass.
+    `slot`: the weight's FSDP gradient slot (parallel/fsdp.py `_WgradSlot`): the backward's column sum writes dweight
+    into it (fp32 grad shard at world size 1, flat bf16 grad buffer otherwise) and reports it ready, instead of a new
+    tensor that a zero fill, an add and an fp32 copy then move into place (four launches per norm per step)."""
 
     @staticmethod
-    def forward(ctx, x, weight, eps, residual, amax=False, grad_amax=False):
+    def forward(ctx, x, weight, eps, residual, amax=False, grad_amax=False, slot=None):
         e = ext()
         shape = x.shape
         x2 = x.reshape(-1, shape[-1]).contiguous()
@@ -96,6 +99,7 @@ class _RMSNormFn(torch.autograd.Function):
         ctx.has_res = residual is not None
         ctx.shape = shape
         ctx.grad_amax = grad_amax
+        ctx.slot = slot
         if am is None:
             am = torch.empty(0, device=x.device)
         ctx.mark_non_differentiable(am)
@@ -113,22 +117,35 @@ class _RMSNormFn(torch.autograd.Function):
             dy = torch.zeros(ctx.shape, dtype=x.dtype, device=x.device)
         d2 = dres.reshape(-1, H).contiguous() if (dres is not None and ctx.has_res) else None
         am = _amax_buf(x, ctx.grad_amax)
-        dx, dw = e.rmsnorm_bwd(dy.reshape(-1, H).contiguous(), x, w.contiguous(), rstd, d2, am)
+        slot = ctx.slot
+        if slot is not None:
+            dest, acc = slot.engine._fused_slot_dest(slot)
+            dx, _ = e.rmsnorm_bwd(dy.reshape(-1, H).contiguous(), x, w.contiguous(), rstd, d2, am, dest.view(-1), acc)
+            slot.engine._fused_slot_done(slot)
+            dw = None
+        else:
+            dx, dw = e.rmsnorm_bwd(dy.reshape(-1, H).contiguous(), x, w.contiguous(), rstd, d2, am)
         dx = dx.view(ctx.shape)
         if am is not None:
             from .fp8 import tag_amax
 
             tag_amax(dx, am)
         # d(x + residual) flows to both summands.
-        return dx, dw, None, (dx if ctx.has_res else None), None, None
+        return dx, dw, None, (dx if ctx.has_res else None), None, None, None
 
 
 def rms_norm(x: torch.Tensor, weight: torch.Tensor, eps: float = 1e-6, residual: Optional[torch.Tensor] = None,
-             amax: bool = False, grad_amax: bool = False):
+             amax: bool = False, grad_amax: bool = False, slot=None):
     """y = RMSNorm(x [+ residual]) * weight. Returns (y, residual_out) where residual_out = x + residual (or x).
-    `amax` / `grad_amax`: tag y / the input gradient with their abs-max for a consuming fp8 linear (HIP path only)."""
+    `amax` / `grad_amax`: tag y / the input gradient with their abs-max for a consuming fp8 linear (HIP path only).
+    `slot`: the weight's FSDP gradient slot (see `_RMSNormFn`); every other path leaves the gradient to autograd."""
     if use_native(x) and x.dtype == torch.bfloat16 and x.shape[-1] % 8 == 0:
-        y, r, am = _RMSNormFn.apply(x, weight, eps, residual, amax, grad_amax)
+        if slot is not None and not (torch.is_grad_enabled() and weight.requires_grad and weight.dtype == x.dtype
+                                     and weight.is_contiguous()):
+            slot = None
+        if slot is not None and torch._C._current_graph_task_id() == -1:
+            slot.uses += 1  # a forward whose backward is pending (recomputation inside backward is not counted)
+        y, r, am = _RMSNormFn.apply(x, weight, eps, residual, amax, grad_amax, slot)
         if amax:
             from .fp8 import tag_amax
 

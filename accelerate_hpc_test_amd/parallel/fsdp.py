@@ -491,9 +491,10 @@ class FSDPEngine:
 
     def _install_fused_wgrad(self):
         """Route the weight gradient of every plain `nn.Linear` whose weight this engine owns (and that no other module
-        shares) through `_FusedWgradLinearFn`; Fp8Linear weights and MoE expert stacks get a slot their own backward
-        writes into."""
-        from ..models.moe import MoEExperts  # lazy: models import parallel.comm
+        shares) through `_FusedWgradLinearFn`; Fp8Linear weights, MoE expert stacks and RMSNorm weights get a slot their
+        own backward writes into."""
+        from ..models.llama import RMSNorm  # lazy: models import parallel.comm
+        from ..models.moe import MoEExperts
         refs = {}
         for m in self.model.modules():
             for p in m._parameters.values():
@@ -504,12 +505,14 @@ class FSDPEngine:
                 m = info.module
                 plain = type(m) is nn.Linear
                 experts = isinstance(m, MoEExperts) and info.attr in ("w_gate_up", "w_down")
-                if (((plain or isinstance(m, Fp8Linear)) and info.attr == "weight") or experts) and info.param.requires_grad \
+                norm = type(m) is RMSNorm and info.attr == "weight"
+                if (((plain or isinstance(m, Fp8Linear) or norm) and info.attr == "weight") or experts) and info.param.requires_grad \
                         and refs.get(id(info.param), 0) == 1 and getattr(info.param, "_tp_spec", None) is None:
                     info.fused = True
                     info.param._acc_wgrad_slot = _WgradSlot(self, unit, info)
                     # Fp8Linear routes its fp8 weight-gradient GEMM to the slot itself (ops/fp8.py), MoEExperts its
-                    # grouped weight-gradient GEMMs (models/moe.py)
+                    # grouped weight-gradient GEMMs (models/moe.py), RMSNorm its dweight column sum (ops/fused.py; on a
+                    # path without the HIP kernel the plain autograd gradient is absorbed into the slot instead)
                     if plain:
                         m.__class__ = _FusedWgradLinear
 
