@@ -506,7 +506,11 @@ class FSDPEngine:
                 plain = type(m) is nn.Linear
                 experts = isinstance(m, MoEExperts) and info.attr in ("w_gate_up", "w_down")
                 norm = type(m) is RMSNorm and info.attr == "weight"
-                if (((plain or isinstance(m, Fp8Linear) or norm) and info.attr == "weight") or experts) and info.param.requires_grad \
+                # embeddings only where the slot is the fp32 grad shard (world size 1): the backward scatters the token
+                # rows into it instead of a dense bf16 [V, H] gradient that is then added and converted
+                emb = (type(m) is nn.Embedding and info.attr == "weight" and self._direct_grads() and m.padding_idx is None
+                       and m.max_norm is None and not m.scale_grad_by_freq and not m.sparse)
+                if (((plain or isinstance(m, Fp8Linear) or norm or emb) and info.attr == "weight") or experts) and info.param.requires_grad \
                         and refs.get(id(info.param), 0) == 1 and getattr(info.param, "_tp_spec", None) is None:
                     info.fused = True
                     info.param._acc_wgrad_slot = _WgradSlot(self, unit, info)
@@ -515,6 +519,8 @@ class FSDPEngine:
                     # path without the HIP kernel the plain autograd gradient is absorbed into the slot instead)
                     if plain:
                         m.__class__ = _FusedWgradLinear
+                    elif emb:
+                        m.__class__ = _FusedSlotEmbedding
 
     def _replace_param(self, info: _ParamInfo, new: nn.Parameter):
         """Swap a (meta) Parameter object for `new` in every module that registers it (tied weights included)."""
@@ -1614,6 +1620,41 @@ class _FusedWgradLinear(nn.Linear):
         if torch._C._current_graph_task_id() == -1:
             slot.uses += 1
         return _FusedWgradLinearFn.apply(x, self.weight, self.bias, slot)
+
+
+class _FusedSlotEmbeddingFn(torch.autograd.Function):
+    """Embedding lookup whose weight gradient is scattered straight into the fp32 grad shard (world size 1): rows of
+    dy added at their token ids (`index_put_(accumulate=True)`: sorted, deterministic), untouched rows zero."""
+
+    @staticmethod
+    def forward(ctx, ids, weight, slot):
+        ctx.save_for_backward(ids)
+        ctx.slot = slot
+        return nn.functional.embedding(ids, weight)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (ids,) = ctx.saved_tensors
+        slot = ctx.slot
+        dest, acc = slot.engine._fused_slot_dest(slot)
+        if not acc:
+            dest.zero_()
+        dest.index_put_((ids.reshape(-1),), dy.reshape(-1, dy.shape[-1]).to(dest.dtype), accumulate=True)
+        slot.engine._fused_slot_done(slot)
+        return None, None, None
+
+
+class _FusedSlotEmbedding(nn.Embedding):
+    """`nn.Embedding` owned by an FSDP unit at world size 1: same parameters and forward; the weight gradient goes to
+    the engine's slot (`_FusedSlotEmbeddingFn`)."""
+
+    def forward(self, ids):
+        slot = getattr(self.weight, "_acc_wgrad_slot", None)
+        if slot is None or not torch.is_grad_enabled() or not self.weight.requires_grad:
+            return super().forward(ids)
+        if torch._C._current_graph_task_id() == -1:
+            slot.uses += 1
+        return _FusedSlotEmbeddingFn.apply(ids, self.weight, slot)
 
 
 def _cast_floats(x, dtype):
