@@ -1200,6 +1200,9 @@ class Accelerator:
                 tracker.log(values, step=step, **log_kwargs.get(tracker.name, {}))
 
     def end_training(self):
+        from .utils.async_checkpoint import wait_pending_saves
+
+        wait_pending_saves()
         if getattr(self, "_watchdog", None) is not None:
             self._watchdog.stop()
             self._watchdog = None
@@ -1295,8 +1298,10 @@ class Accelerator:
         """Save model(s), optimizer(s), scheduler(s), dataloader positions, scaler, RNG and registered custom states.
         With `ProjectConfiguration(automatic_checkpoint_naming=True)` the state goes to
         `<project_dir>/checkpoints/checkpoint_<iteration>` and the oldest checkpoints beyond `total_limit` are pruned."""
+        from .utils.async_checkpoint import wait_pending_saves
         from .utils.fsdp_utils import save_fsdp_model, save_fsdp_optimizer
 
+        wait_pending_saves()  # the previous non-blocking save's files are complete before rotation / overwrite
         rot = _CheckpointRotation(self.project_configuration)
         if rot.enabled:
             if self.is_main_process:
@@ -1324,8 +1329,11 @@ class Accelerator:
 
     def load_state(self, input_dir: str = None, load_kwargs: dict | None = None, **load_model_func_kwargs):
         """Restore what `save_state` wrote (the newest automatic checkpoint when `input_dir` is None)."""
+        from .utils.async_checkpoint import wait_pending_saves
         from .utils.fsdp_utils import load_fsdp_model, load_fsdp_optimizer
 
+        wait_pending_saves()  # a non-blocking save of this process may still be writing the files
+        self.wait_for_everyone()
         if input_dir is not None:
             input_dir = os.path.expanduser(input_dir)
             if not os.path.isdir(input_dir):

@@ -243,17 +243,22 @@ def load_checkpoint_and_dispatch(
 
 
 # ------------------------------------------------------------------------------------------------ layerwise casting
-_CASTABLE = (nn.Linear, nn.Conv1d, nn.Conv2d, nn.Conv3d, nn.ConvTranspose1d, nn.ConvTranspose2d, nn.ConvTranspose3d,
-             nn.Embedding, nn.LayerNorm, nn.GroupNorm)
-_DEFAULT_SKIP = ("pos_embed", "patch_embed", "norm", "^proj_in$", "^proj_out$")
+# The layers whose weights are stored low-precision: the reference's SUPPORTED_PYTORCH_LAYERS_FOR_UPCASTING
+# (/root/reference/src/accelerate/utils/constants.py:99-107) -- convolutions and Linear only.
+_CASTABLE = (nn.Conv1d, nn.Conv2d, nn.Conv3d, nn.ConvTranspose1d, nn.ConvTranspose2d, nn.ConvTranspose3d, nn.Linear)
 
 
 def attach_layerwise_casting_hooks(module: nn.Module, storage_dtype: torch.dtype, compute_dtype: torch.dtype,
                                    skip_modules_pattern=None, skip_modules_classes=None, non_blocking: bool = False):
-    """Store the weights of supported layers in `storage_dtype` (e.g. fp8 e4m3: half the HBM of bf16) and upcast to
-    `compute_dtype` around each forward. Modules matching `skip_modules_pattern` (regexes on the qualified name) or
-    `skip_modules_classes` are left alone, with their whole subtree."""
-    patterns = _DEFAULT_SKIP if skip_modules_pattern is None else tuple(skip_modules_pattern)
+    """Store the weights of supported layers (`Conv*`, `ConvTranspose*`, `Linear`) in `storage_dtype` (e.g. fp8 e4m3:
+    half the HBM of bf16) and upcast them to `compute_dtype` around each forward (hooks.py `LayerwiseCastingHook`).
+    Modules whose qualified name matches a regex of `skip_modules_pattern`, or that are instances of
+    `skip_modules_classes`, are left alone together with their subtree; by default nothing is skipped (reference
+    big_modeling.py:724-750). A single string pattern is one regex (the reference iterates a bare string character by
+    character)."""
+    if isinstance(skip_modules_pattern, str):
+        skip_modules_pattern = (skip_modules_pattern,)
+    patterns = tuple(skip_modules_pattern or ())
     classes = tuple(skip_modules_classes or ())
     stack = [("", module)]
     while stack:

@@ -12,6 +12,7 @@ int64_t acc_dbg_take_xent_optim();
 int64_t acc_dbg_take_small_allreduce();
 int64_t acc_dbg_take_comm_pack();
 int64_t acc_dbg_take_moe_route();
+int64_t acc_dbg_take_cast();
 bool debug_selftest(torch::Tensor out, int64_t overshoot);
 
 // (check id << 32 | source line) of the first failed device check since the last call, 0 if none; clears it.
@@ -19,7 +20,7 @@ static int64_t debug_status() {
   int64_t first = 0;
   for (auto fn : {acc_dbg_take_flash_attn, acc_dbg_take_fp8, acc_dbg_take_fp8_asm, acc_dbg_take_grouped_gemm, acc_dbg_take_norm_act,
                   acc_dbg_take_xent_optim, acc_dbg_take_small_allreduce, acc_dbg_take_comm_pack,
-                  acc_dbg_take_moe_route}) {
+                  acc_dbg_take_moe_route, acc_dbg_take_cast}) {
     const int64_t w = fn();
     if (first == 0) first = w;
   }
@@ -80,6 +81,9 @@ torch::Tensor mx_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor sa, torch:
 void fp8_gemm_select(int64_t variant, int64_t group_m);
 torch::Tensor fp8asm_dma_probe(torch::Tensor a, torch::Tensor b);
 bool bf16_gemm_asm(torch::Tensor a, torch::Tensor b, c10::optional<torch::Tensor> bias, torch::Tensor out, bool accumulate);
+bool bf16_gemm_asm_amn(torch::Tensor a_t, torch::Tensor b, torch::Tensor out, bool accumulate, bool trans_out);
+// cast.hip
+bool upcast_multi(std::vector<torch::Tensor> srcs, std::vector<torch::Tensor> dsts);
 bool grouped_gemm_asm(torch::Tensor a, torch::Tensor b, torch::Tensor out, std::vector<int64_t> bounds, int64_t mode,
                       c10::optional<torch::Tensor> sa, c10::optional<torch::Tensor> sb, double smul, bool accumulate);
 // grouped_gemm.hip
@@ -102,6 +106,7 @@ void sar_destroy(int64_t id);
 void grad_shard_update(torch::Tensor dst, torch::Tensor src, double scale, bool accumulate);
 // runtime/*.cpp
 void register_runtime(pybind11::module& m);
+void register_d2h_writer(pybind11::module& m);
 void cpu_adam_step(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, c10::optional<torch::Tensor> shadow,
                    double lr, double beta1, double beta2, double eps, double wd, double bc1, double bc2_sqrt, bool adamw);
 bool blaslt_wgrad_f32(torch::Tensor dy, torch::Tensor x, torch::Tensor out, bool accumulate, bool x_t, bool dy_t);
@@ -165,6 +170,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sar_destroy", &sar_destroy);
   m.def("bf16_gemm_asm", &bf16_gemm_asm, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("bias"), pybind11::arg("out"),
         pybind11::arg("accumulate") = false, "bf16 out (=|+=) a . b^T (+ bias) on the asm-scheduled GEMM; false = shape not tiled");
+  m.def("bf16_gemm_asm_amn", &bf16_gemm_asm_amn, pybind11::arg("a_t"), pybind11::arg("b"), pybind11::arg("out"),
+        pybind11::arg("accumulate") = false, pybind11::arg("trans_out") = false,
+        "out (=|+=) a_t^T . b^T (or its transpose) with a_t [K, M] M-contiguous, on the asm GEMM; false = shape not tiled");
+  m.def("upcast_multi", &upcast_multi, pybind11::arg("srcs"), pybind11::arg("dsts"),
+        "dsts[i] = srcs[i] upcast (fp8 / fp16 / bf16 / fp32 -> bf16 / fp16 / fp32) in one launch; false = not handled");
   m.def("grouped_gemm_asm", &grouped_gemm_asm, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("out"),
         pybind11::arg("bounds"), pybind11::arg("mode"), pybind11::arg("sa") = pybind11::none(),
         pybind11::arg("sb") = pybind11::none(), pybind11::arg("smul") = 1.0, pybind11::arg("accumulate") = false,
@@ -172,6 +182,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fp8asm_dma_probe", &fp8asm_dma_probe, "debug: LDS image after the asm GEMM's first-tile DMA");
   m.def("fp8_gemm_select", &fp8_gemm_select, pybind11::arg("variant"), pybind11::arg("group_m") = 0);
   register_runtime(m);
+  register_d2h_writer(m);
   m.def("blaslt_dgrad_bf16", &blaslt_dgrad_bf16, pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("out"),
         "dx = dy . W (bf16, both row-major: the NN layout) on a searched hipBLASLt algorithm; False if none");
   m.def("blaslt_wgrad_f32", &blaslt_wgrad_f32, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("out"), pybind11::arg("accumulate"),

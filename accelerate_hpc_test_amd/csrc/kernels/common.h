@@ -92,7 +92,7 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // check since the last call (0 = none) and clearing it; `_C.debug_status()` polls every file.
 enum AccCheck : int {
   kChkAttnTile = 1, kChkGemmTile = 2, kChkGroupSeg = 3, kChkNormRow = 4, kChkXentLabel = 5, kChkMtChunk = 6,
-  kChkAllreduceSize = 7, kChkRopePos = 8, kChkRoutePos = 9, kChkSelfTest = 99,
+  kChkAllreduceSize = 7, kChkRopePos = 8, kChkRoutePos = 9, kChkCastTable = 10, kChkSelfTest = 99,
 };
 #ifdef ACC_DEBUG_BOUNDS
 static __device__ int acc_dbg_word[2];

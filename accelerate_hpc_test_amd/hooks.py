@@ -491,8 +491,25 @@ class UserCpuOffloadHook:
         remove_hook_from_module(self.model)
 
 
+# storage -> compute upcasts that are exact, so that the storage tensor can be kept and the compute copy dropped after
+# the forward with the same result as the reference's `.to(storage)` round trip
+_EXACT_UPCASTS = {
+    (torch.float8_e4m3fn, torch.bfloat16), (torch.float8_e4m3fn, torch.float16), (torch.float8_e4m3fn, torch.float32),
+    (torch.float8_e5m2, torch.bfloat16), (torch.float8_e5m2, torch.float16), (torch.float8_e5m2, torch.float32),
+    (torch.float16, torch.float32), (torch.bfloat16, torch.float32),
+}
+
+
 class LayerwiseCastingHook(ModelHook):
-    """Weights stored in `storage_dtype` (e.g. fp8) and cast to `compute_dtype` for the duration of each forward."""
+    """Weights stored in `storage_dtype` (e.g. fp8) and used in `compute_dtype` for the duration of each forward
+    (reference hooks.py:757-783: `module.to(compute)` before and `module.to(storage)` after every forward).
+
+    When the upcast is exact (fp8 -> bf16 / fp16 / fp32, fp16 / bf16 -> fp32) the storage tensors stay resident: the
+    pre-forward hook upcasts all of the module's floating-point tensors into compute-dtype scratch tensors in one HIP
+    launch (`ext().upcast_multi`, csrc/kernels/cast.hip) and points the parameters at them; the post-forward hook points
+    them back at the untouched storage tensors and the scratch is freed. One read of the stored weights per forward and
+    no downcast pass; values and dtypes seen by the caller are the reference's. Other dtype pairs (a lossy "upcast")
+    take the reference's `.to()` round trip."""
 
     _is_stateful = False
 
@@ -500,17 +517,50 @@ class LayerwiseCastingHook(ModelHook):
         self.storage_dtype = storage_dtype
         self.compute_dtype = compute_dtype
         self.non_blocking = non_blocking
+        self._keep = (storage_dtype, compute_dtype) in _EXACT_UPCASTS
+        self._stored = None
 
     def init_hook(self, module):
         module.to(dtype=self.storage_dtype, non_blocking=self.non_blocking)
         return module
 
+    def _tensors(self, module):
+        """(tensor, data) of the module's own parameters and buffers held in the storage dtype."""
+        out = []
+        for holder in (module._parameters, module._buffers):
+            for t in holder.values():
+                if t is not None and t.dtype == self.storage_dtype:
+                    out.append(t)
+        return out
+
     def pre_forward(self, module, *args, **kwargs):
-        module.to(dtype=self.compute_dtype, non_blocking=self.non_blocking)
+        items = self._tensors(module) if self._keep and next(module.children(), None) is None else None
+        if not items:
+            module.to(dtype=self.compute_dtype, non_blocking=self.non_blocking)
+            return args, kwargs
+        srcs = [t.data for t in items]
+        dsts = [torch.empty(s.shape, dtype=self.compute_dtype, device=s.device) for s in srcs]
+        done = False
+        if srcs[0].is_cuda and all(s.is_contiguous() for s in srcs):
+            from .ops._ext import ext, use_native
+
+            if use_native(srcs[0]):
+                done = ext().upcast_multi(srcs, dsts)
+        if not done:
+            for s, d in zip(srcs, dsts):
+                d.copy_(s, non_blocking=self.non_blocking)
+        for t, d in zip(items, dsts):
+            t.data = d
+        self._stored = list(zip(items, srcs))
         return args, kwargs
 
     def post_forward(self, module, output):
-        module.to(dtype=self.storage_dtype, non_blocking=self.non_blocking)
+        if self._stored is None:
+            module.to(dtype=self.storage_dtype, non_blocking=self.non_blocking)
+            return output
+        for t, s in self._stored:
+            t.data = s
+        self._stored = None
         return output
 
 

@@ -124,13 +124,23 @@ _MOE_FP8_BLASLT = os.environ.get("ACCELERATE_MOE_FP8_BLASLT", "0") == "1"
 # fp8 expert GEMMs on the asm-scheduled grouped kernel (csrc/kernels/fp8_gemm_asm.hip modes 1 / 2: 256x256 tiles of
 # 16x16x128 MFMAs, persistent over (expert, tile) items from the host segment table) when the table is on the host.
 _MOE_ASM = os.environ.get("ACCELERATE_MOE_ASM_GEMM", "1") != "0"
+# bf16 expert GEMMs on the same asm grouped kernel (its bf16 mode: two 16x16x32 bf16 MFMAs per 128-byte K-tile), by
+# product: "fwd" (mode 1 on the stored stacks), "wgrad" (mode 2), "dgrad" (mode 1 on a transposed copy of the stack);
+# the others stay on per-expert hipBLASLt. Chosen per product by measurement (profiles/r6_mixtral.md).
+_MOE_ASM_BF16 = {k.strip() for k in os.environ.get("ACCELERATE_MOE_ASM_BF16", "fwd,wgrad,dgrad").split(",") if k.strip()}
+_F8 = (torch.float8_e4m3fn, torch.float8_e5m2)
 
 
-def _asm_grouped_mm(a, b, bounds, mode, out, sa, sb, smul, accumulate) -> bool:
-    """grouped_mm on the asm kernel (fp8 operands, host `bounds`); False when it does not apply. Mode-2 experts with
-    fewer than 256 bytes of K (the kernel's two-K-tile minimum) are finished here: zero, or one small product."""
-    if not (_MOE_ASM and a.is_cuda and use_native(a) and a.dtype in (torch.float8_e4m3fn, torch.float8_e5m2)
-            and b.dtype in (torch.float8_e4m3fn, torch.float8_e5m2)):
+def _asm_grouped_mm(a, b, bounds, mode, out, sa, sb, smul, accumulate, kind=None) -> bool:
+    """grouped_mm on the asm kernel (fp8 operands, or bf16 ones for the products in ACCELERATE_MOE_ASM_BF16; host
+    `bounds`); False when it does not apply. Mode-2 experts with fewer than 256 bytes of K (the kernel's two-K-tile
+    minimum) are finished here: zero, or one small product."""
+    if not (_MOE_ASM and a.is_cuda and use_native(a)):
+        return False
+    f8 = a.dtype in _F8 and b.dtype in _F8
+    bf = (a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and sa is None and sb is None
+          and kind is not None and kind in _MOE_ASM_BF16)
+    if not (f8 or bf):
         return False
     if not ext().grouped_gemm_asm(a, b, out, list(bounds), mode, sa, sb, float(smul), bool(accumulate)):
         return False
@@ -200,15 +210,16 @@ def _expert_mm(a, b, bounds, e, mode, out, sa, sb, smul, accumulate, fp8) -> boo
     return True
 
 
-def grouped_mm(a, b, seg, mode, out, sa=None, sb=None, smul=1.0, accumulate=False):
+def grouped_mm(a, b, seg, mode, out, sa=None, sb=None, smul=1.0, accumulate=False, kind=None):
     """One grouped GEMM over the expert segment table `seg` (csrc/kernels/grouped_gemm.hip):
     mode 1: out[r] = a[r] . b[e]^T for rows r of segment e (a [R, K], b [E, N, K], out [R, N]; rows past seg[E] -> 0);
     mode 2: out[e] = a[:, seg_e] . b[:, seg_e]^T (a [M, T], b [N, T], out [E, M, N]).
     sa / sb: fp32 amax-style scale tensors ([1] and [E] (mode 1) / [1] (mode 2)), times `smul`. Off the GPU (and for
-    shapes the kernel does not tile) the same product runs in PyTorch from a host copy of `seg`."""
+    shapes the kernel does not tile) the same product runs in PyTorch from a host copy of `seg`. `kind` ("fwd" /
+    "dgrad" / "wgrad") names the product for the bf16 backend choice."""
     E = seg.numel() - 1
     bounds = getattr(seg, "_acc_bounds", None)
-    if bounds is not None and _asm_grouped_mm(a, b, bounds, mode, out, sa, sb, smul, accumulate):
+    if bounds is not None and _asm_grouped_mm(a, b, bounds, mode, out, sa, sb, smul, accumulate, kind):
         return out
     if (bounds is not None and _MOE_GEMM == "blaslt" and a.is_cuda and use_native(a)
             and _per_expert_mm(a, b, bounds, mode, out, sa, sb, smul, accumulate)):
@@ -256,6 +267,8 @@ def _dgrad_mm(a, w, seg, out):
     product). The per-expert hipBLASLt path (host segment bounds attached) runs it on w itself; otherwise the grouped
     kernel takes the K-contiguous copy `_bt(w)`."""
     bounds = getattr(seg, "_acc_bounds", None)
+    if "dgrad" in _MOE_ASM_BF16 and bounds is not None and a.is_cuda and use_native(a) and _MOE_ASM:
+        return grouped_mm(a, _bt(w), seg, 1, out, kind="dgrad")
     if (_MOE_DGRAD_NN and bounds is not None and _MOE_GEMM == "blaslt" and a.is_cuda and use_native(a)
             and a.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and out.dtype == torch.bfloat16
             and a.is_contiguous() and w.is_contiguous() and out.is_contiguous()):
@@ -351,8 +364,8 @@ class _GroupedExpertsFn(torch.autograd.Function):
             y, st = _fp8_fwd(x, w_gu, w_down, seg, recipe)
             ctx.st = st
         else:
-            h = grouped_mm(x, w_gu, seg, 1, x.new_empty(R, I2))
-            y = grouped_mm(_swiglu_fwd(h), w_down, seg, 1, x.new_empty(R, H))
+            h = grouped_mm(x, w_gu, seg, 1, x.new_empty(R, I2), kind="fwd")
+            y = grouped_mm(_swiglu_fwd(h), w_down, seg, 1, x.new_empty(R, H), kind="fwd")
             ctx.st = h
         ctx.save_for_backward(x, w_gu, w_down, seg)
         ctx.recipe, ctx.fp8, ctx.slots = recipe, fp8, slots
@@ -382,9 +395,9 @@ class _GroupedExpertsFn(torch.autograd.Function):
             I = w_down.shape[2]
             a = _swiglu_fwd(h)
             da = _dgrad_mm(dy, w_down, seg, x.new_empty(R, I))
-            grouped_mm(_t(dy), _t(a), seg, 2, g_d, accumulate=acc_d)
+            grouped_mm(_t(dy), _t(a), seg, 2, g_d, accumulate=acc_d, kind="wgrad")
             dh = _swiglu_bwd(h, da)
-            grouped_mm(_t(dh), _t(x), seg, 2, g_gu, accumulate=acc_gu)
+            grouped_mm(_t(dh), _t(x), seg, 2, g_gu, accumulate=acc_gu, kind="wgrad")
             dx = _dgrad_mm(dh, w_gu, seg, x.new_empty(R, H))
         ctx.st = None
         grads = []

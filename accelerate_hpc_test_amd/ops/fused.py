@@ -33,6 +33,10 @@ _ASM_BF16 = bool(_ASM_BF16_KINDS)
 # fp32 weight gradients with dy transposed first (ACCELERATE_WGRAD_DYT=1): both hipBLASLt operands token-contiguous,
 # the TN class the forward GEMMs run in, for the price of one dy transpose per Linear
 _WGRAD_DYT = os.environ.get("ACCELERATE_WGRAD_DYT", "0") == "1"
+# weight gradients on the asm kernel's MN-major-A mode (ext().bf16_gemm_asm_amn): dy read as it is ([T, N], the output
+# row index contiguous) through transposed LDS reads, x from the saved token-contiguous copy; no transposed dy
+# (tools/bench_gemm_amn.py, profiles/r6_gemm_amn.md)
+_ASM_WGRAD_AMN = os.environ.get("ACCELERATE_ASM_WGRAD_AMN", "1") != "0"
 
 
 def asm_gemm_bf16(a: torch.Tensor, b: torch.Tensor, bias=None, out=None, accumulate: bool = False, kind: str = "fwd"):
@@ -427,6 +431,11 @@ def wgrad_into(dest: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, accumula
     a, b = dy2.t(), x2
     if b.dtype != a.dtype:
         b = b.to(a.dtype)
+    if (_ASM_WGRAD_AMN and dest.is_cuda and dest.is_contiguous() and a.dtype == torch.bfloat16 and dy2.is_contiguous()
+            and b.t().is_contiguous() and dest.dtype in (torch.float32, torch.bfloat16) and use_native(dy2)
+            and dy2.shape[1] % 256 == 0 and b.shape[1] % 256 == 0 and dy2.shape[0] % 64 == 0 and dy2.shape[0] >= 128):
+        if ext().bf16_gemm_asm_amn(dy2, b.t(), dest, accumulate, False):
+            return
     # asm kernel: both operands token-contiguous -- x2 is the transposed view of the saved xᵀ, dy2 is transposed here
     if ("wgrad" in _ASM_BF16_KINDS and dest.is_cuda and dest.is_contiguous() and a.dtype == torch.bfloat16
             and b.t().is_contiguous()

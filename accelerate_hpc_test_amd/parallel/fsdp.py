@@ -510,8 +510,11 @@ class FSDPEngine:
                 # rows into it instead of a dense bf16 [V, H] gradient that is then added and converted
                 emb = (type(m) is nn.Embedding and info.attr == "weight" and self._direct_grads() and m.padding_idx is None
                        and m.max_norm is None and not m.scale_grad_by_freq and not m.sparse)
+                # parameters whose gradient a TP hook all-reduces (sequence-parallel norms, per-head q/k norms:
+                # tensor_parallel.ReplicatedGradAllReduce) keep the autograd gradient: a slot would bypass the hook
+                tp_hooked = getattr(m, "_tp_grad_allreduce_group", None) is not None or getattr(info.param, "_tp_grad_hooked", False)
                 if (((plain or isinstance(m, Fp8Linear) or norm or emb) and info.attr == "weight") or experts) and info.param.requires_grad \
-                        and refs.get(id(info.param), 0) == 1 and getattr(info.param, "_tp_spec", None) is None:
+                        and refs.get(id(info.param), 0) == 1 and getattr(info.param, "_tp_spec", None) is None and not tp_hooked:
                     info.fused = True
                     info.param._acc_wgrad_slot = _WgradSlot(self, unit, info)
                     # Fp8Linear routes its fp8 weight-gradient GEMM to the slot itself (ops/fp8.py), MoEExperts its
@@ -1308,15 +1311,20 @@ class FSDPEngine:
             out[name] = t.cpu().clone() if cpu else t.clone()
         return out
 
-    def sharded_state_dict(self) -> dict:
-        """This rank's master shards: {fqn: local 1-D slice} plus layout metadata for resharding."""
+    def sharded_state_dict(self, to_cpu: bool = True) -> dict:
+        """This rank's master shards: {fqn: local 1-D slice} plus layout metadata for resharding. `to_cpu=False`
+        returns device views of the live shards (the non-blocking writer snapshots them on the device)."""
         tensors, meta = OrderedDict(), {"world_size": self.world_size, "rank": self.rank, "params": {}, "extra": {}}
         for unit in self.units:
             for info in unit.infos:
-                tensors[info.fqn] = unit.master[info.local_lo : info.local_hi].detach().cpu().clone()
+                piece = unit.master[info.local_lo : info.local_hi].detach()
+                tensors[info.fqn] = piece.cpu().clone() if to_cpu else piece
                 meta["params"][info.fqn] = {"shape": list(info.shape), "param_lo": info.param_lo, "numel": info.local_hi - info.local_lo}
+                spec = getattr(info.param, "_tp_spec", None)
+                if spec is not None and spec.size > 1:  # TP-local shape: how merge_fsdp_weights reassembles the full one
+                    meta["params"][info.fqn]["tp"] = {"dim": spec.dim, "segments": list(spec.segments) if spec.segments else None}
         for name, p in self._extras():
-            tensors[name] = p.detach().float().cpu().clone()
+            tensors[name] = p.detach().float().cpu().clone() if to_cpu else p.detach().float()
             meta["extra"][name] = {"ep": getattr(p, "_ep_spec", None) is not None, "rank": self.rank}
         return {"tensors": tensors, "meta": meta}
 
@@ -1379,37 +1387,63 @@ class FSDPEngine:
             dist.broadcast(full, src=dist.get_global_rank(self.replicate_group, 0), group=self.replicate_group)
 
     @torch.no_grad()
-    def load_full_state_dict_broadcast(self, sd: Optional[dict]):
+    def load_full_state_dict_broadcast(self, sd: Optional[dict], strict: bool = True):
         """FULL_STATE_DICT load where only global rank 0 holds `sd` (None elsewhere): one broadcast of each unit's
         flat fp32 buffer, every rank keeps its slice (reference fsdp2_load_full_state_dict,
         /root/reference/src/accelerate/utils/fsdp_utils.py:467-554). Host memory: rank 0 maps the file, the others
-        hold nothing."""
+        hold nothing.
+
+        Keys: rank 0 lists the parameters `sd` lacks and broadcasts the list before anything is copied; with `strict`
+        every rank raises KeyError (as `load_full_state_dict`), otherwise the missing parameters keep their current
+        values on every rank (nothing is overwritten with a placeholder)."""
         from ..utils.fsdp_utils import IO_STATS
 
-        missing = []
+        multi = dist.is_available() and dist.is_initialized()
+        missing = None
+        if sd is not None:
+            missing = [info.fqn for unit in self.units for info in unit.infos if info.fqn not in sd]
+            missing += [name for name, _ in self._extras() if name not in sd]
+        if multi:
+            box = [missing]
+            dist.broadcast_object_list(box, src=0)
+            missing = box[0]
+        if missing is None:
+            raise ValueError("load_full_state_dict_broadcast: global rank 0 must hold the state dict")
+        if strict and missing:
+            raise KeyError(f"Missing keys in state dict: {missing[:5]}...")
+        skip = set(missing)
         for unit in self.units:
             full = torch.zeros(unit.padded, dtype=torch.float32, device=self.device)
             if sd is not None:
                 for info in unit.infos:
-                    t = sd.get(info.fqn)
-                    if t is None:
-                        missing.append(info.fqn)
+                    if info.fqn in skip:
                         continue
+                    t = sd[info.fqn]
                     IO_STATS["bytes_read"] += t.numel() * t.element_size()
                     full[info.offset : info.offset + info.numel].copy_(t.reshape(-1).to(self.device, torch.float32))
             self.broadcast_full(full)
-            unit.master.copy_(unit.local_of_full(full).to(unit.master.device))
+            if not any(info.fqn in skip for info in unit.infos):
+                unit.master.copy_(unit.local_of_full(full).to(unit.master.device))
+            else:  # copy only the parameters the checkpoint holds
+                for info in unit.infos:
+                    if info.fqn in skip or info.local_hi <= info.local_lo:
+                        continue
+                    lo = info.offset + info.param_lo
+                    unit.master[info.local_lo : info.local_hi].copy_(
+                        full[lo : lo + (info.local_hi - info.local_lo)].to(unit.master.device))
             if unit.shard_lp is not unit.master:
                 unit.shard_lp.copy_(unit.master.to(unit.shard_lp.device))
             del full
         self.refresh_fp8()
         for name, p in self._extras():
+            if name in skip:
+                continue
             spec = getattr(p, "_ep_spec", None)
             shape = ((spec[1] * p.shape[0],) + tuple(p.shape[1:])) if spec is not None else tuple(p.shape)
             full = torch.zeros(shape, dtype=torch.float32, device=p.device)
-            if sd is not None and name in sd:
+            if sd is not None:
                 full.copy_(sd[name].to(p.device, torch.float32))
-            if dist.is_available() and dist.is_initialized():
+            if multi:
                 dist.broadcast(full, src=0)
             self._load_extra(name, full)
         if missing:

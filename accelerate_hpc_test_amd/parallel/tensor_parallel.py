@@ -254,6 +254,11 @@ class ReplicatedGradAllReduce(ParallelStyle):
     q/k norms) see only this rank's heads, so their gradients are summed over tp."""
 
     def apply(self, module, group, sequence_parallel):
+        # marks the module at parallelize time (the hook itself is attached at the first forward): engines that write a
+        # parameter's gradient straight into a buffer (FSDP gradient slots) must leave these parameters on autograd so
+        # the tp all-reduce hook fires
+        module._tp_grad_allreduce_group = group
+
         def attach(mod, args):  # lazily: engines may replace the Parameter objects after parallelize
             for p in mod.parameters(recurse=False):
                 if p.requires_grad and not getattr(p, "_tp_grad_hooked", False):

@@ -325,12 +325,13 @@ def _tiny_llama_cfg():
 
 
 def check_tp_matches_single(sequence_parallel: bool = False, dp_shard: int = 1, steps: int = 2, dp_replicate: int = 1,
-                            norm_type: float = 2.0):
+                            norm_type: float = 2.0, max_norm: float = 1e9, adamw: bool = False):
     """TP (optionally sequence-parallel, optionally x FSDP over dp_shard, optionally x HSDP replicas) must train
     exactly like one process on the global batch: same loss, same global gradient norm, same full weights after
     `steps` steps. The norm is the reference's DTensor-aware `clip_grad_norm_` over the whole mesh
     (/root/reference/src/accelerate/accelerator.py:2943-2953): tp-sharded squares summed over tp and dp_shard,
-    tp-replicated ones counted once, HSDP replicas not at all."""
+    tp-replicated ones counted once, HSDP replicas not at all. `max_norm` below the norm exercises the clip scale
+    itself (every rank must scale its shards by the same global factor); `adamw` trains with AdamW instead of SGD."""
     from accelerate_hpc_test_amd import ParallelismConfig
     from accelerate_hpc_test_amd.models.llama import LlamaForCausalLM
     from accelerate_hpc_test_amd.utils.dataclasses import TorchTensorParallelConfig
@@ -350,8 +351,12 @@ def check_tp_matches_single(sequence_parallel: bool = False, dp_shard: int = 1, 
     base = LlamaForCausalLM(cfg)
     base.init_weights()
     model = copy.deepcopy(base)
-    opt = torch.optim.SGD(model.parameters(), lr=0.5, momentum=0.9)
-    base_opt = torch.optim.SGD(base.parameters(), lr=0.5, momentum=0.9)
+    if adamw:
+        opt = torch.optim.AdamW(model.parameters(), lr=1e-2, weight_decay=0.01)
+        base_opt = torch.optim.AdamW(base.parameters(), lr=1e-2, weight_decay=0.01)
+    else:
+        opt = torch.optim.SGD(model.parameters(), lr=0.5, momentum=0.9)
+        base_opt = torch.optim.SGD(base.parameters(), lr=0.5, momentum=0.9)
     model, opt = acc.prepare(model, opt)
     dp_rank = acc.process_index // tp  # mesh order: dp_replicate, dp_shard outer, tp inner
     g = torch.Generator().manual_seed(3)
@@ -362,21 +367,79 @@ def check_tp_matches_single(sequence_parallel: bool = False, dp_shard: int = 1, 
         out = model(local, labels=local)
         acc.backward(out.loss)
         # the global gradient norm: tp-sharded squares summed over the group, replicated ones counted once
-        gn = acc.clip_grad_norm_(model.parameters(), 1e9, norm_type=norm_type)
+        gn = acc.clip_grad_norm_(model.parameters(), max_norm, norm_type=norm_type)
         opt.step()
         opt.zero_grad()
         ref = base(ids, labels=ids)
         ref.loss.backward()
-        gn_ref = torch.nn.utils.clip_grad_norm_(base.parameters(), 1e9, norm_type=norm_type)
+        gn_ref = torch.nn.utils.clip_grad_norm_(base.parameters(), max_norm, norm_type=norm_type)
         assert torch.allclose(gn.float(), gn_ref.float(), rtol=1e-4), (gn, gn_ref)
+        if max_norm < 1e9:
+            assert gn_ref.item() > max_norm, "the clip must be active for this check"
         base_opt.step()
         base_opt.zero_grad()
         lg = acc.reduce(out.loss.detach().reshape(1), reduction="mean")
         assert torch.allclose(lg, ref.loss.detach().reshape(1), atol=2e-5), (lg, ref.loss)
     full = acc.get_state_dict(model)
+    # AdamW normalises each element's step, so float rounding in a near-zero gradient can move a weight by a sizeable
+    # fraction of lr (1e-2): 2 % of one step; SGD stays at the rounding level
+    atol = 2e-4 if adamw else 2e-5
     for n, q in base.state_dict().items():
         assert full[n].shape == q.shape, (n, full[n].shape, q.shape)
-        assert torch.allclose(full[n].float(), q.float(), atol=2e-5), (n, (full[n] - q).abs().max())
+        assert torch.allclose(full[n].float(), q.float(), atol=atol), (n, (full[n] - q).abs().max())
+
+
+def check_tp_fsdp_sharded_merge():
+    """dp_shard 2 x tp 2, SHARDED_STATE_DICT: every (dp, tp) rank writes its TP-local FSDP shard; `merge_fsdp_weights`
+    must rebuild the FULL weights (TP slices concatenated along each parameter's shard dim, fused q/k/v and gate/up
+    segments re-interleaved) equal to `get_state_dict`; `load_state` round-trips exactly in the same layout, and a
+    checkpoint whose tp size differs from the loading job's is refused."""
+    from safetensors.torch import load_file
+
+    from accelerate_hpc_test_amd import ParallelismConfig
+    from accelerate_hpc_test_amd.models.llama import LlamaForCausalLM
+    from accelerate_hpc_test_amd.utils import fsdp_utils, merge_fsdp_weights
+
+    pc = ParallelismConfig(tp_size=2, dp_shard_size=2)
+    plugin = FullyShardedDataParallelPlugin(fsdp_version=2, auto_wrap_policy="transformer_based_wrap",
+                                            transformer_cls_names_to_wrap=["LlamaDecoderLayer"],
+                                            state_dict_type="SHARDED_STATE_DICT")
+    acc = Accelerator(cpu=True, parallelism_config=pc, fsdp_plugin=plugin)
+    r = acc.process_index
+    set_seed(0)
+    cfg = _tiny_llama_cfg()
+    model = LlamaForCausalLM(cfg)
+    model.init_weights()
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-2)
+    model, opt = acc.prepare(model, opt)
+    ids = torch.randint(0, cfg.vocab_size, (2, 16), generator=torch.Generator().manual_seed(1))
+    acc.backward(model(ids, labels=ids).loss)
+    opt.step()
+    opt.zero_grad()
+    full = acc.get_state_dict(model)
+    d = gather_object([tempfile.mkdtemp() if r == 0 else None])[0]
+    acc.save_state(d)
+    if r == 0:
+        merged = load_file(merge_fsdp_weights(os.path.join(d, "pytorch_model_fsdp_0"), os.path.join(d, "merged")))
+        assert set(merged) == set(full), set(merged) ^ set(full)
+        for k, v in full.items():
+            assert merged[k].shape == v.shape, (k, merged[k].shape, v.shape)
+            assert torch.equal(merged[k].float(), v.float()), (k, (merged[k].float() - v.float()).abs().max())
+    acc.wait_for_everyone()
+    with torch.no_grad():
+        for q in model.parameters():
+            q.add_(1.0)
+    acc.load_state(d)
+    back = acc.get_state_dict(model)
+    for k, v in full.items():
+        assert torch.equal(back[k], v), k
+    metas = fsdp_utils._saved_metas(os.path.join(d, "pytorch_model_fsdp_0"))
+    fake = [(path, dict(m, tp_size=4)) for path, m in metas]
+    try:
+        fsdp_utils._check_tp_layout(fake, model.engine, "probe")
+        raise AssertionError("a tp-size mismatch must be refused")
+    except ValueError as exc:
+        assert "tensor-parallel size" in str(exc)
 
 
 def check_tp_dtensor_model(steps: int = 3, norm_type: float = 2.0):
@@ -994,6 +1057,38 @@ def check_broadcast_from_rank0_loading():
     full = acc.get_state_dict(model)
     for k, v in src.state_dict().items():
         assert torch.equal(full[k], v), (r, k)
+
+
+def check_fsdp_full_load_missing_keys():
+    """FULL_STATE_DICT rank-0 broadcast load (`FSDPEngine.load_full_state_dict_broadcast`) with a key missing from the
+    checkpoint: strict -> KeyError on EVERY rank before anything is copied (the model is untouched); non-strict -> the
+    missing parameter keeps its current values on every rank (no zero placeholder), the others are loaded."""
+    plugin = FullyShardedDataParallelPlugin(fsdp_version=2, auto_wrap_policy="transformer_based_wrap",
+                                            transformer_cls_names_to_wrap=["Block"])
+    acc = Accelerator(cpu=True, fsdp_plugin=plugin)
+    r = acc.process_index
+    torch.manual_seed(5)
+    model = acc.prepare(TinyMLP())
+    eng = model.engine
+    before = acc.get_state_dict(model)
+    drop = sorted(before)[0]
+    sd = None
+    if r == 0:
+        sd = {k: v + 1.0 for k, v in before.items() if k != drop}
+    try:
+        eng.load_full_state_dict_broadcast(sd)
+        raise AssertionError("strict load with a missing key must raise")
+    except KeyError as exc:
+        assert drop in str(exc), exc
+    after = acc.get_state_dict(model)
+    for k, v in before.items():
+        assert torch.equal(after[k], v), (r, k)
+    missing = eng.load_full_state_dict_broadcast(sd, strict=False)
+    assert missing == [drop], missing
+    after = acc.get_state_dict(model)
+    for k, v in before.items():
+        want = v if k == drop else v + 1.0
+        assert torch.allclose(after[k], want), (r, k, (after[k] - want).abs().max())
 
 
 class _F8Block(torch.nn.Module):

@@ -34,7 +34,7 @@ def _batches(steps, vocab):
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--mode", choices=["fsdp", "fsdp_fp8", "ddp", "hsdp", "tp", "tp_fsdp", "hsdp_tp", "cp_allgather", "cp_alltoall", "ep", "ulysses"], required=True)
+    p.add_argument("--mode", choices=["fsdp", "fsdp_fp8", "ddp", "hsdp", "tp", "tp_sp", "tp_fsdp", "tp_fsdp_sp", "hsdp_tp", "cp_allgather", "cp_alltoall", "ep", "ulysses"], required=True)
     p.add_argument("--seq", type=int, default=16384)
     p.add_argument("--heads", default="8,2", help="cp modes: query,kv heads")
     p.add_argument("--no-ref", action="store_true", help="cp modes: skip the fp32 reference (long sequences)")
@@ -63,22 +63,27 @@ def main():
         acc = Accelerator(mixed_precision="bf16", kwargs_handlers=handlers, cpu=args.cpu)
         torch.manual_seed(0)
         model = LlamaForCausalLM(cfg).to(acc.device)
-    elif args.mode == "tp":  # Megatron column / row parallel over W ranks, every rank on the whole batch
+    elif args.mode in ("tp", "tp_sp"):  # Megatron column / row parallel over W ranks, every rank on the whole batch
         from accelerate_hpc_test_amd import ParallelismConfig
+        from accelerate_hpc_test_amd.utils.dataclasses import TorchTensorParallelConfig
 
         acc = Accelerator(mixed_precision="bf16", kwargs_handlers=handlers, cpu=args.cpu,
-                          parallelism_config=ParallelismConfig(tp_size=W) if W > 1 else None)
+                          parallelism_config=ParallelismConfig(tp_size=W, tp_handler=TorchTensorParallelConfig(
+                              sequence_parallel=args.mode == "tp_sp")) if W > 1 else None)
         torch.manual_seed(0)
         model = LlamaForCausalLM(cfg).to(acc.device)
-    elif args.mode in ("tp_fsdp", "hsdp_tp"):
+    elif args.mode in ("tp_fsdp", "tp_fsdp_sp", "hsdp_tp"):
         # 2-D / 3-D meshes: tp 2 innermost, FSDP over dp_shard (x 2 HSDP replicas); the global grad norm must sum the
-        # tp-sharded squares over tp and dp_shard and count the tp-replicated ones once
+        # tp-sharded squares over tp and dp_shard and count the tp-replicated ones once. tp_fsdp_sp: sequence-parallel
+        # TP, whose norm weights see 1/tp of the tokens and need the tp all-reduce of their gradients (no FSDP slot)
         from accelerate_hpc_test_amd import ParallelismConfig
+        from accelerate_hpc_test_amd.utils.dataclasses import TorchTensorParallelConfig
 
         pc = None
         if W > 1:
             rep = 2 if args.mode == "hsdp_tp" else 1
-            pc = ParallelismConfig(tp_size=2, dp_shard_size=W // (2 * rep), dp_replicate_size=rep)
+            pc = ParallelismConfig(tp_size=2, dp_shard_size=W // (2 * rep), dp_replicate_size=rep,
+                                   tp_handler=TorchTensorParallelConfig(sequence_parallel=args.mode == "tp_fsdp_sp"))
         plugin = FullyShardedDataParallelPlugin(fsdp_version=2, auto_wrap_policy="transformer_based_wrap",
                                                 transformer_cls_names_to_wrap=["LlamaDecoderLayer"])
         acc = Accelerator(mixed_precision="bf16", fsdp_plugin=plugin, kwargs_handlers=handlers + [RcclKwargs()],
@@ -105,16 +110,19 @@ def main():
     opt = torch.optim.AdamW(model.parameters(), lr=lr, weight_decay=0.01)
     model, opt = acc.prepare(model, opt)
     facts = {"world": W, "mode": args.mode}
-    tp_modes = ("tp", "tp_fsdp", "hsdp_tp")
+    tp_modes = ("tp", "tp_sp", "tp_fsdp", "tp_fsdp_sp", "hsdp_tp")
     def _tp_sharded(q):
         return getattr(getattr(q, "_tp_spec", None), "size", 1) > 1
 
-    if args.mode == "tp":
+    if args.mode in ("tp", "tp_sp"):
         facts["tp_sharded"] = sum(1 for q in model.parameters() if _tp_sharded(q))
-    if args.mode in tp_modes[1:]:
+    if args.mode in tp_modes[2:]:
         facts["tp_sharded"] = sum(1 for u in model.engine.units for i in u.infos if _tp_sharded(i.param))
         facts["sharded"] = bool(model.engine.sharded)
-    elif args.mode not in ("ddp", "tp"):
+        # parameters whose gradient a tp hook all-reduces must not take an FSDP gradient slot
+        facts["tp_hooked_with_slot"] = sum(1 for u in model.engine.units for i in u.infos
+                                           if i.fused and getattr(i.module, "_tp_grad_allreduce_group", None) is not None)
+    elif args.mode not in ("ddp", "tp", "tp_sp"):
         eng = model.engine
         facts["sharded"] = bool(eng.sharded)
         # parameters cut by a shard boundary (the case the forced one-GPU mode never has)
@@ -125,7 +133,7 @@ def main():
         facts["ddp_buckets"] = len(getattr(model, "buckets", []))
     if W > 1:
         facts["ipc_allreduce"] = small_allreduce.get(None) is not None
-    tp = W if args.mode == "tp" else (2 if args.mode in tp_modes and W > 1 else 1)
+    tp = W if args.mode in ("tp", "tp_sp") else (2 if args.mode in tp_modes and W > 1 else 1)
     bs = GLOBAL_BATCH // (W // tp)
     dp_rank = r // tp  # mesh order: dp_replicate, dp_shard outer, tp inner
     losses, norms = [], []

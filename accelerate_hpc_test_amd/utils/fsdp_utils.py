@@ -20,6 +20,7 @@ import torch
 import torch.distributed as dist
 
 from ..logging import get_logger
+from .async_checkpoint import writer as async_writer
 from .constants import FSDP_MODEL_NAME, OPTIMIZER_NAME, SAFE_WEIGHTS_NAME, WEIGHTS_NAME
 
 logger = get_logger(__name__)
@@ -82,16 +83,17 @@ def save_fsdp_model(fsdp_plugin, accelerator, model, output_dir, model_index=0, 
     else:
         ckpt_dir = os.path.join(output_dir, f"{FSDP_MODEL_NAME}_{model_index}")
         os.makedirs(ckpt_dir, exist_ok=True)
-        shard = eng.sharded_state_dict()
-        from safetensors.torch import save_file
-
         if getattr(eng, "replicate_rank", 0) != 0:  # HSDP / NO_SHARD replicas hold identical shards: replica 0 writes
             _barrier()
             return
+        # device views of the live shards: the non-blocking writer snapshots them in HBM and streams them to the file
+        # (utils/async_checkpoint.py); CPU shards are written synchronously in the same safetensors layout
+        shard = eng.sharded_state_dict(to_cpu=False)
         t, tp = _tp_info(eng)
         shard["meta"].update(tp_rank=t, tp_size=tp)
         stem = _shard_stem(eng)
-        save_file({k: v.contiguous() for k, v in shard["tensors"].items()}, os.path.join(ckpt_dir, f"{stem}.safetensors"))
+        async_writer().save_file({k: v.contiguous() for k, v in shard["tensors"].items()},
+                                 os.path.join(ckpt_dir, f"{stem}.safetensors"))
         with open(os.path.join(ckpt_dir, stem.replace("shard_", "meta_") + ".json"), "w") as f:
             json.dump(shard["meta"], f)
         logger.info(f"Model shard saved to {ckpt_dir}")
@@ -110,6 +112,17 @@ def _saved_metas(ckpt_dir, tp_rank=None):
         stem = os.path.basename(meta_path)[len("meta_") : -len(".json")]
         out.append((os.path.join(ckpt_dir, f"shard_{stem}.safetensors"), meta))
     return out
+
+
+def _check_tp_layout(metas, eng, what):
+    """A sharded checkpoint holds TP-local slices: it loads only into the same tensor-parallel layout."""
+    _, tp = _tp_info(eng)
+    saved = {m.get("tp_size", 1) if "tp_size" in m else m.get("meta", {}).get("tp_size", 1) for _, m in metas}
+    saved = {s for s in saved if s is not None} or {1}
+    if saved != {tp}:
+        raise ValueError(f"{what} was saved with tensor-parallel size {sorted(saved)} and is being loaded with tp={tp}: "
+                         "a sharded checkpoint holds TP-local slices. Merge it (`merge_fsdp_weights` / "
+                         "`accelerate merge-weights`) and load the full weights instead.")
 
 
 def _read_sharded_dir(ckpt_dir):
@@ -153,6 +166,7 @@ def _load_sharded_model(eng, ckpt_dir):
     metas = _saved_metas(ckpt_dir, tp_rank=t)
     if not metas:
         raise FileNotFoundError(f"No model shards in {ckpt_dir}")
+    _check_tp_layout(metas, eng, f"The sharded model in {ckpt_dir}")
     rd = _ShardReader()
     for unit in eng.units:
         for info in unit.infos:
@@ -362,7 +376,7 @@ def save_fsdp_optimizer(fsdp_plugin, accelerator, optimizer, model, output_dir, 
                 keys = []
                 for k, v in st.items():
                     if torch.is_tensor(v) and v.dim() > 0:  # stored in its own dtype (bf16 moments stay bf16)
-                        tensors[f"{info.fqn}|{k}"] = v.detach().reshape(-1).cpu().contiguous()
+                        tensors[f"{info.fqn}|{k}"] = v.detach().reshape(-1).contiguous()
                         keys.append(k)
                     else:
                         scalars.setdefault(info.fqn, {})[k] = _jsonable(v)
@@ -371,11 +385,9 @@ def save_fsdp_optimizer(fsdp_plugin, accelerator, optimizer, model, output_dir, 
         groups = [{**{k: _jsonable(v) for k, v in g.items() if k != "params"}, "params": [fqn_of.get(id(p)) for p in g["params"]]}
                   for g in opt.param_groups]
         if getattr(eng, "replicate_rank", 0) == 0:  # replicas hold identical optimizer shards
-            from safetensors.torch import save_file
-
             t, tp = _tp_info(eng)
             stem = _shard_stem(eng)
-            save_file(tensors, os.path.join(d, f"{stem}.safetensors"))
+            async_writer().save_file(tensors, os.path.join(d, f"{stem}.safetensors"))
             with open(os.path.join(d, stem.replace("shard_", "meta_") + ".json"), "w") as f:
                 json.dump({"meta": meta, "scalars": scalars, "param_groups": groups, "tp_rank": t, "tp_size": tp}, f)
     _barrier()
@@ -385,6 +397,8 @@ def save_fsdp_optimizer(fsdp_plugin, accelerator, optimizer, model, output_dir, 
 def _load_sharded_optimizer(eng, opt, d):
     t, _ = _tp_info(eng)
     metas = _saved_metas(d, tp_rank=t)
+    if metas:
+        _check_tp_layout(metas, eng, f"The sharded optimizer in {d}")
     rd = _ShardReader()
     for unit in eng.units:
         for info in unit.infos:
@@ -458,24 +472,67 @@ def _load_sharded_optimizer_v1(eng, opt, d):
         _apply_groups(opt, saved[0]["param_groups"])
 
 
+def _unshard_tp_host(parts, dim, segments):
+    """Full tensor from the tp ranks' local slices (rank order): each fused segment was split tp ways on its own
+    (parallel/tensor_parallel.py `_shard_tensor`), so the pieces are re-interleaved segment by segment."""
+    tp = len(parts)
+    local = parts[0].shape[dim]
+    segs = [s // tp for s in segments] if segments else [local]
+    out, off = [], 0
+    for s in segs:
+        out += [p.narrow(dim, off, s) for p in parts]
+        off += s
+    return torch.cat(out, dim=dim)
+
+
 def merge_fsdp_weights(checkpoint_dir: str, output_path: str, safe_serialization: bool = True, remove_checkpoint_dir: bool = False):
-    """Merge a SHARDED_STATE_DICT model dir into a single weights file (reference fsdp_utils.py:366-418)."""
+    """Merge a SHARDED_STATE_DICT model dir into a single weights file (reference fsdp_utils.py:366-418). FSDP pieces
+    are placed by their flat offsets per tensor-parallel rank; with tp > 1 the TP-local tensors are then concatenated
+    along each parameter's recorded shard dim (replicated parameters come from tp rank 0); expert-parallel stacks
+    (engine extras) are concatenated in rank order."""
+    from .async_checkpoint import wait_pending_saves
+
+    wait_pending_saves()  # this process's own non-blocking save may still be writing into the directory
     pieces = _read_sharded_dir(checkpoint_dir)
     if not pieces:
         raise ValueError(f"No shards found in {checkpoint_dir}")
-    full = OrderedDict()
+    tp_size = max(meta.get("tp_size", 1) for _, meta in pieces)
+    by_tp = {}
     for tensors, meta in pieces:
-        for fqn, pm in meta["params"].items():
-            if fqn not in full:
-                shape = pm["shape"]
-                n = 1
-                for s in shape:
-                    n *= s
-                full[fqn] = (torch.zeros(n, dtype=tensors[fqn].dtype), shape)
-            buf, _ = full[fqn]
-            if pm["numel"] > 0:
-                buf[pm["param_lo"] : pm["param_lo"] + pm["numel"]].copy_(tensors[fqn])
-    sd = OrderedDict((k, v.view(shape)) for k, (v, shape) in full.items())
+        by_tp.setdefault(meta.get("tp_rank", 0) if tp_size > 1 else 0, []).append((tensors, meta))
+    if sorted(by_tp) != list(range(tp_size)):
+        raise ValueError(f"{checkpoint_dir}: shards of tp ranks {sorted(by_tp)} found, expected 0..{tp_size - 1}")
+    local = {}
+    for t, group in by_tp.items():
+        full = OrderedDict()
+        for tensors, meta in group:
+            for fqn, pm in meta["params"].items():
+                if fqn not in full:
+                    shape = pm["shape"]
+                    n = 1
+                    for s_ in shape:
+                        n *= s_
+                    full[fqn] = (torch.zeros(n, dtype=tensors[fqn].dtype), shape, pm.get("tp"))
+                buf = full[fqn][0]
+                if pm["numel"] > 0:
+                    buf[pm["param_lo"] : pm["param_lo"] + pm["numel"]].copy_(tensors[fqn])
+        local[t] = full
+    merged = OrderedDict()
+    for fqn, (buf, shape, tpm) in local[0].items():
+        if tp_size == 1 or tpm is None:
+            merged[fqn] = buf.view(shape)
+        else:
+            merged[fqn] = _unshard_tp_host([local[t][fqn][0].view(local[t][fqn][1]) for t in range(tp_size)],
+                                           tpm["dim"], tpm.get("segments"))
+    # engine extras (ignored / expert-parallel parameters): replicated ones once, EP stacks in rank order
+    ext_pieces = sorted(((meta.get("rank", 0), tensors, meta) for tensors, meta in by_tp[0]), key=lambda x: x[0])
+    for _, tensors, meta in ext_pieces:
+        for name, em in meta.get("extra", {}).items():
+            if em.get("ep"):
+                merged[name] = torch.cat([merged[name], tensors[name]]) if name in merged else tensors[name]
+            elif name not in merged:
+                merged[name] = tensors[name]
+    sd = merged
     os.makedirs(output_path, exist_ok=True)
     if safe_serialization:
         from safetensors.torch import save_file

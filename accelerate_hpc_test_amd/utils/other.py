@@ -173,23 +173,26 @@ def load(f, map_location=None, **kwargs):
         raise
 
 
-def get_pretty_name(obj):
-    if not hasattr(obj, "__qualname__") and not hasattr(obj, "__name__"):
-        obj = getattr(obj, "__class__", obj)
-    if hasattr(obj, "__qualname__"):
-        return obj.__qualname__
-    if hasattr(obj, "__name__"):
-        return obj.__name__
+def get_pretty_name(obj) -> str:
+    """Readable name of a class, function or instance (its class's qualified name), for log and error messages."""
+    for cand in (obj, type(obj)):
+        name = getattr(cand, "__qualname__", None) or getattr(cand, "__name__", None)
+        if name:
+            return name
     return str(obj)
 
 
-def merge_dicts(source, destination):
-    for key, value in source.items():
-        if isinstance(value, dict):
-            node = destination.setdefault(key, {})
-            merge_dicts(value, node)
-        else:
-            destination[key] = value
+def merge_dicts(source: dict, destination: dict) -> dict:
+    """Deep-merge `source` into `destination` in place (nested dicts merged key by key, other values replaced) and
+    return `destination`."""
+    stack = [(source, destination)]
+    while stack:
+        src, dst = stack.pop()
+        for key, value in src.items():
+            if isinstance(value, dict):
+                stack.append((value, dst.setdefault(key, {})))
+            else:
+                dst[key] = value
     return destination
 
 
@@ -206,31 +209,36 @@ def get_free_port() -> int:
         return s.getsockname()[1]
 
 
-def convert_bytes(size):
-    for x in ["bytes", "KB", "MB", "GB", "TB"]:
-        if size < 1024.0:
-            return f"{round(size, 2)} {x}"
-        size /= 1024.0
-    return f"{round(size, 2)} PB"
+_BYTE_UNITS = ("bytes", "KB", "MB", "GB", "TB", "PB")
+
+
+def convert_bytes(size) -> str:
+    """`size` bytes in the largest binary unit that keeps the value under 1024 (two decimals)."""
+    value, unit = size, 0
+    while value >= 1024.0 and unit < len(_BYTE_UNITS) - 1:
+        value /= 1024.0
+        unit += 1
+    return f"{round(value, 2)} {_BYTE_UNITS[unit]}"
+
+
+_MIN_LINUX_KERNEL = (5, 5, 0)
 
 
 def check_os_kernel():
-    """Warn on Linux kernels < 5.5 (known to hang multi-process jobs)."""
+    """Multi-process jobs are known to hang on Linux kernels older than 5.5: log a warning on such a host."""
     info = platform.uname()
-    system = info.system
-    if system != "Linux":
+    if info.system != "Linux":
         return
-    _, version, *_ = re.split(r"(\d+\.\d+\.\d+)", info.release)
-    min_version = "5.5.0"
-    from packaging import version as pv
-
-    if pv.parse(version) < pv.parse(min_version):
+    found = re.search(r"(\d+)\.(\d+)\.(\d+)", info.release)
+    if found is None:
+        return
+    release = tuple(int(x) for x in found.groups())
+    if release < _MIN_LINUX_KERNEL:
         from ..logging import get_logger
 
+        have, need = ".".join(map(str, release)), ".".join(map(str, _MIN_LINUX_KERNEL))
         get_logger(__name__).warning(
-            f"Detected kernel version {version}, which is below the recommended minimum of {min_version}; this can "
-            "cause the process to hang. It is recommended to upgrade the kernel to the minimum version or higher."
-        )
+            f"Linux kernel {have} is older than {need}: multi-process runs can hang on it; upgrade the host kernel.")
 
 
 def recursive_getattr(obj, attr: str):

@@ -55,19 +55,23 @@ def _reference(mode, outdir):
 
 
 @pytest.mark.parametrize("mode,world", [(m, w) for m in ("fsdp", "fsdp_fp8", "ddp") for w in (2, 4)]
-                         + [("fsdp", 8), ("ddp", 8), ("hsdp", 4), ("hsdp", 8), ("tp", 2), ("tp_fsdp", 4), ("hsdp_tp", 8)])
+                         + [("fsdp", 8), ("ddp", 8), ("hsdp", 4), ("hsdp", 8), ("tp", 2), ("tp_fsdp", 4), ("hsdp_tp", 8),
+                            ("tp_sp", 2), ("tp_fsdp_sp", 4)])
 def test_ranks_sharing_one_gpu_match_single_process(mode, world, outdir):
     """W = 8 is the driver's scaling node's rank count; HSDP = 2 replicas x W/2 shards (dp_replicate x dp_shard); TP =
     Megatron column / row parallel linears over W ranks on the whole batch (ParallelismConfig(tp_size=W); W = 2: the
     preset has 2 kv heads); tp_fsdp = dp_shard W/2 x tp 2 and hsdp_tp = 2 replicas x dp_shard W/4 x tp 2, both against
-    the one-process TP run (the 2-D / 3-D global grad norm)."""
-    ref, ref_params = _reference({"hsdp": "fsdp", "tp_fsdp": "tp", "hsdp_tp": "tp"}.get(mode, mode), outdir)
+    the one-process TP run (the 2-D / 3-D global grad norm); the *_sp modes run TP sequence-parallel (norm weights on a
+    sequence shard: their gradients must be all-reduced over tp, so they take no FSDP gradient slot)."""
+    ref, ref_params = _reference({"hsdp": "fsdp", "tp_fsdp": "tp", "hsdp_tp": "tp", "tp_sp": "tp", "tp_fsdp_sp": "tp"}.get(mode, mode),
+                                 outdir)
     res, params = _run(mode, world, outdir)
     assert res["world"] == world and res["ipc_allreduce"], res  # clip-norm / amax / reduce over the IPC kernel
     if mode.startswith("tp") or mode == "hsdp_tp":
         assert res["tp_sharded"] > 0, res
-        if mode != "tp":
+        if mode not in ("tp", "tp_sp"):
             assert res["sharded"], res
+            assert res["tp_hooked_with_slot"] == 0, res
     elif mode != "ddp":
         assert res["sharded"] and res["split_params"] > 0, res  # real partial-parameter shards
         assert res["replicated"] == (mode == "hsdp"), res

@@ -352,6 +352,45 @@ def test_bf16_asm_gemm_matches_fp32_reference(M, N, K):
         or (K - 32) % 64 == 0  # K not a multiple of 64: declined, nothing launched
 
 
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 320), (1024, 512, 4096), (768, 1280, 8192)])
+def test_bf16_asm_amn_gemm_matches_fp32_reference(M, N, K):
+    """The MN-major-A asm GEMM (ext().bf16_gemm_asm_amn, transposed LDS reads): a_t [K, M] M-contiguous, b [N, K];
+    exact small integers for C = a_tᵀ·bᵀ and for the transposed store (pins the tr-read operand map, the chunk layout
+    and both epilogues), then random operands with bf16 / fp32 outputs and accumulate against the fp32 reference."""
+    from accelerate_hpc_test_amd.ops._ext import ext
+
+    torch.manual_seed(0)
+    ai = torch.randint(-3, 4, (K, M), device=DEV).to(torch.bfloat16)
+    bi = torch.randint(-3, 4, (N, K), device=DEV).to(torch.bfloat16)
+    refi = ai.float().t() @ bi.float().t()
+    out = torch.empty(M, N, device=DEV)
+    assert ext().bf16_gemm_asm_amn(ai, bi, out, False, False)
+    assert torch.equal(out, refi), (out - refi).abs().max()
+    out_t = torch.empty(N, M, device=DEV)
+    assert ext().bf16_gemm_asm_amn(ai, bi, out_t, False, True)
+    assert torch.equal(out_t, refi.t()), (out_t - refi.t()).abs().max()
+    a = torch.randn(K, M, device=DEV, dtype=torch.bfloat16)
+    b = torch.randn(N, K, device=DEV, dtype=torch.bfloat16)
+    ref = a.float().t() @ b.float().t()
+    tol = 1e-3 * ref.abs().max().item()
+    o32 = torch.empty(M, N, device=DEV)
+    assert ext().bf16_gemm_asm_amn(a, b, o32, False, False)
+    assert torch.allclose(o32, ref, rtol=1e-4, atol=tol), (o32 - ref).abs().max()
+    o16t = torch.empty(N, M, device=DEV, dtype=torch.bfloat16)
+    assert ext().bf16_gemm_asm_amn(a, b, o16t, False, True)
+    assert _rel(o16t.float(), ref.t()) < 1e-2
+    base = torch.randn(M, N, device=DEV)
+    acc = base.clone()
+    assert ext().bf16_gemm_asm_amn(a, b, acc, True, False)
+    assert torch.allclose(acc, base + ref, rtol=1e-4, atol=tol)
+    base16 = torch.randn(N, M, device=DEV, dtype=torch.bfloat16)
+    acc16 = base16.clone()
+    assert ext().bf16_gemm_asm_amn(a, b, acc16, True, True)
+    assert _rel(acc16.float(), base16.float() + ref.t()) < 1e-2
+    # shapes it does not tile are declined (nothing launched)
+    assert not ext().bf16_gemm_asm_amn(a[:, : M - 128].contiguous(), b, torch.empty(M - 128, N, device=DEV), False, False)
+
+
 @pytest.mark.parametrize("M,N,K", [(256, 256, 256), (512, 768, 1024), (1024, 512, 4096), (768, 1280, 2304)])
 def test_fp8_gemm_v4_and_unscaled_kernels_match_reference(M, N, K, monkeypatch):
     """The 16x16x128-MFMA kernel (v4: two 64 KiB LDS slots, BK 128) with the scaled (variant 6) and the unscaled
@@ -1719,3 +1758,46 @@ def test_checkpoint_direct_file_upload(tmp_path, monkeypatch):
             ref = v.to(dtype) if dtype is not None else v
             assert torch.equal(got.cpu(), ref), (k, direct, dtype)
         assert (counts["file"], counts["put"]) == want, (direct, dtype, counts)
+
+
+@pytest.mark.parametrize("src_dt,dst_dt", [(torch.float8_e4m3fn, torch.bfloat16), (torch.float8_e5m2, torch.float32),
+                                           (torch.float8_e4m3fn, torch.float16), (torch.float16, torch.float32),
+                                           (torch.bfloat16, torch.float32)])
+def test_upcast_multi_matches_torch_cast(src_dt, dst_dt):
+    """The layerwise-casting upcast kernel (csrc/kernels/cast.hip): several tensors of odd sizes (8-wide body + element
+    tail, a tensor spanning many workgroups, an empty one) in one launch, bit-equal to torch's `.to()`."""
+    from accelerate_hpc_test_amd.ops._ext import ext
+
+    torch.manual_seed(0)
+    sizes = [(4096, 1031), (7,), (0,), (33, 65), (300000,)]
+    srcs = [(torch.randn(s, device=DEV) * 4).to(src_dt) for s in sizes]
+    dsts = [torch.empty(s, device=DEV, dtype=dst_dt) for s in sizes]
+    assert ext().upcast_multi(srcs, dsts)
+    for s, d in zip(srcs, dsts):
+        assert torch.equal(d, s.to(dst_dt)), (src_dt, dst_dt, s.shape)
+    # outside what it handles: nothing launched, False
+    assert not ext().upcast_multi([srcs[0]], [torch.empty(4096, 1031, device=DEV, dtype=torch.float8_e4m3fn)])
+
+
+def test_layerwise_casting_hook_on_gpu_keeps_storage_and_matches_reference_semantics():
+    """attach_layerwise_casting_hooks on HIP tensors: fp8 storage, bf16 compute; the forward runs on bf16 weights made
+    by the upcast kernel, the stored fp8 tensors are the same storage afterwards, and the output equals the reference's
+    `.to(compute)` / `.to(storage)` semantics computed by hand."""
+    import torch.nn as nn
+
+    from accelerate_hpc_test_amd.big_modeling import attach_layerwise_casting_hooks
+
+    torch.manual_seed(0)
+    m = nn.Sequential(nn.Linear(256, 512), nn.LayerNorm(512), nn.Linear(512, 128)).to(DEV, torch.bfloat16)
+    ref = [(lin.weight.detach().to(torch.float8_e4m3fn).to(torch.bfloat16), lin.bias.detach().to(torch.float8_e4m3fn).to(torch.bfloat16))
+           for lin in (m[0], m[2])]
+    attach_layerwise_casting_hooks(m, torch.float8_e4m3fn, torch.bfloat16)
+    stored = m[0].weight.data
+    assert stored.dtype == torch.float8_e4m3fn and m[1].weight.dtype == torch.bfloat16
+    x = torch.randn(64, 256, device=DEV, dtype=torch.bfloat16)
+    with torch.no_grad():
+        y = m(x)
+        h = torch.nn.functional.linear(x, *ref[0])
+        want = torch.nn.functional.linear(m[1](h), *ref[1])
+    assert m[0].weight.data.data_ptr() == stored.data_ptr() and m[0].weight.dtype == torch.float8_e4m3fn
+    assert torch.equal(y, want), (y.float() - want.float()).abs().max()

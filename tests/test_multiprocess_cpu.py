@@ -100,6 +100,30 @@ def test_tensor_parallel_x_hsdp_3d():
     debug_launcher(td.check_tp_matches_single, args=(False, 2, 2, 2), num_processes=8)
 
 
+@pytest.mark.parametrize("sequence_parallel", [False, True])
+def test_tensor_parallel_x_fsdp_2d_clipped_adamw(sequence_parallel):
+    """dp_shard 2 x tp 2 with the clip ACTIVE (max_norm below the global norm) and AdamW: every rank scales its TP /
+    FSDP shards by the same global factor; sequence-parallel norm weights keep their tp gradient all-reduce."""
+    debug_launcher(td.check_tp_matches_single, args=(sequence_parallel, 2, 3, 1, 2.0, 0.05, True), num_processes=4)
+
+
+def test_tensor_parallel_x_fsdp_sharded_checkpoint_merge():
+    """dp_shard 2 x tp 2 SHARDED_STATE_DICT: merge_fsdp_weights rebuilds the full weights from the per-tp-rank shard
+    files; load_state round-trips; a different tp layout is refused."""
+    debug_launcher(td.check_tp_fsdp_sharded_merge, num_processes=4)
+
+
+def test_fsdp_full_state_load_missing_keys():
+    """Rank-0 broadcast FULL_STATE_DICT load: a missing key raises on every rank (strict) or keeps the parameter's
+    values (non-strict) -- never a silent zero fill."""
+    debug_launcher(td.check_fsdp_full_load_missing_keys, num_processes=2)
+
+
+def test_tensor_parallel_x_hsdp_3d_clipped_adamw():
+    """dp_replicate 2 x dp_shard 2 x tp 2, clipped at max_norm 0.05, AdamW == one process."""
+    debug_launcher(td.check_tp_matches_single, args=(False, 2, 3, 2, 2.0, 0.05, True), num_processes=8)
+
+
 def test_context_parallel_x_fsdp_2d():
     """dp_shard 2 x cp 2: ring attention inside FSDP over the flattened dp_shard x cp mesh == one process."""
     debug_launcher(td.check_cp_llama_matches_single, args=("allgather", 2, 2), num_processes=4)

@@ -29,6 +29,16 @@ fragment reads (lane (r, g): row 8r + i, bytes 16g and 64 + 16g) are then confli
 lane groups.
 
 The tail runs the same body twice without DMA (tile nk-2 waits vmcnt(0) for nk-1; tile nk-1 reads nothing).
+
+MN-major A (`BF16AMN_*`, bf16 only): A is stored [K][M] (the M index contiguous: dy of a weight gradient, W of a
+dgrad computed as its transpose). One K-tile of A is then 64 k-rows x 512 B (the tile's 256 columns); a DMA chunk
+holds two k-rows (1 KiB, same 1056-B chunk stride as the K-major image). Chunk n = q | G'<<2 | (k>>4)<<3 holds rows
+k with k&3 = q, bit 3 = G' and bit 2 = the row inside the chunk, so the eight rows one half-wave of a transposed read
+touches sit in eight consecutive chunks: at a 1056-B stride they start 32 B apart modulo 256 and the 32 lanes' 8-B
+pieces cover all 64 banks once. Fragments come out of LDS through `ds_read_b64_tr_b16` (4 per fragment instead of 2
+`ds_read_b128`): lane 4q + p of a 16-lane group g supplies row 8g + 4s + q (+32 for the second MFMA of the K-tile),
+columns 4p..4p+3 of its block; block i = 16 consecutive output rows 16i..16i+15 of the wave's 128. One address VGPR
+serves all 32 reads of a K-tile (immediate offsets 16896 h + 512 s + 32 i).
 """
 
 from __future__ import annotations
@@ -49,6 +59,8 @@ M0_XB = 55    # the same for B (an xor mask toggles only the base it was compute
 CNT = 59      # main-loop trips left
 M0_KEEP = 60  # caller's m0
 CHUNK_STEP = 4 * 1056  # m0 advance per DMA instruction (4 waves x one 1056-B chunk)
+SOFF_A = 61   # MN-major A: s61..s67 = j * 8 rows * lda, j = 1..7
+ADV_A = 68    # MN-major A: bytes between K-tiles (64 rows * lda)
 
 
 def A(i):
@@ -82,9 +94,26 @@ def ds_frag(dst_base, f, addr):
             f"ds_read_b128 v[{d + 4}:{d + 7}], {addr} offset:{128 * f + 64}"]
 
 
-def dma(op, n):
+def ds_frag_tr(f, addr):
+    """MN-major A fragment f: four ds_read_b64_tr_b16 (MFMA half h, k sub-block s) into v[d + 4h + 2s : +1]"""
+    d = A_BASE + 8 * f
+    return [f"ds_read_b64_tr_b16 v[{d + 4 * h + 2 * s}:{d + 4 * h + 2 * s + 1}], {addr} offset:{16896 * h + 512 * s + 32 * f}"
+            for h in range(2) for s in range(2)]
+
+
+def a_frag(f, amn):
+    return ds_frag_tr(f, "%[va]") if amn else ds_frag(A_BASE, f, "%[va]")
+
+
+def dma(op, n, amn=False):
     """n-th (0..7) DMA instruction of operand op ('A'|'B'); m0 must hold this instruction's destination"""
     srd = SRD_A if op == "A" else SRD_B
+    if op == "A" and amn:
+        so = "0" if n == 0 else f"s{SOFF_A + n - 1}"
+        out = [f"buffer_load_dwordx4 %[voffa], s[{srd}:{srd + 3}], {so} offen lds"]
+        if n < 7:
+            out.append(f"s_add_u32 m0, m0, {CHUNK_STEP}")
+        return out
     so = "0" if n == 0 else f"s{SOFF + n - 1}"
     out = [f"buffer_load_dwordx4 %[voff], s[{srd}:{srd + 3}], {so} offen lds"]
     if n < 7:
@@ -92,12 +121,13 @@ def dma(op, n):
     return out
 
 
-def advance_srd(op):
+def advance_srd(op, amn=False):
     srd = SRD_A if op == "A" else SRD_B
-    return [f"s_add_u32 s{srd}, s{srd}, 128", f"s_addc_u32 s{srd + 1}, s{srd + 1}, 0"]
+    step = f"s{ADV_A}" if (op == "A" and amn) else "128"
+    return [f"s_add_u32 s{srd}, s{srd}, {step}", f"s_addc_u32 s{srd + 1}, s{srd + 1}, 0"]
 
 
-def body(dma_on: bool, wait_next: bool, read_next: bool, bf16: bool = False):
+def body(dma_on: bool, wait_next: bool, read_next: bool, bf16: bool = False, amn: bool = False):
     """one K-tile; returns a list of instruction lines. Extra work is attached after MFMA #k via `slots[k]`. bf16:
     each accumulator block takes two MFMAs; in every run of four blocks (same A fragment) the four first halves are
     issued, each followed by its slot's work, then the four second halves (4 MFMAs between dependent ones)."""
@@ -115,9 +145,9 @@ def body(dma_on: bool, wait_next: bool, read_next: bool, bf16: bool = False):
         for n in range(5):
             slots[8 + n] += dma("B", n)
     for f in range(3):
-        slots[13 + f] += ds_frag(A_BASE, 4 + f, "%[va]")
+        slots[13 + f] += a_frag(4 + f, amn)
     # phase 2
-    slots[16] += ds_frag(A_BASE, 7, "%[va]")
+    slots[16] += a_frag(7, amn)
     slots[20] += ["s_waitcnt lgkmcnt(0)"]
     slots[21] += ["s_barrier"]
     if dma_on:
@@ -126,10 +156,10 @@ def body(dma_on: bool, wait_next: bool, read_next: bool, bf16: bool = False):
         slots[24] += [f"s_mov_b32 m0, s{M0_A}"]
         slots[28] += advance_srd("B")  # the SRD bases always point at the next K-tile to load
         for n in range(2):
-            slots[25 + n] += dma("A", n)
+            slots[25 + n] += dma("A", n, amn)
         # phase 3
         for n in range(2, 7):
-            slots[38 + n - 2] += dma("A", n)
+            slots[38 + n - 2] += dma("A", n, amn)
     if wait_next:
         slots[45] += ["s_waitcnt vmcnt(15)" if dma_on else "s_waitcnt vmcnt(0)"]
         slots[46] += ["s_barrier"]
@@ -139,10 +169,10 @@ def body(dma_on: bool, wait_next: bool, read_next: bool, bf16: bool = False):
         for f in range(4):
             slots[48 + f] += ds_frag(B_BASE, f, "%[vb]")
         for f in range(4):
-            slots[52 + f + (1 if f >= 1 else 0)] += ds_frag(A_BASE, f, "%[va]")
+            slots[52 + f + (1 if f >= 1 else 0)] += a_frag(f, amn)
     if dma_on:
-        slots[53] += dma("A", 7)
-        slots[55] += advance_srd("A")
+        slots[53] += dma("A", 7, amn)
+        slots[55] += advance_srd("A", amn)
         slots[57] += [f"s_xor_b32 s{M0_A}, s{M0_A}, s{M0_X}", f"s_xor_b32 s{M0_B}, s{M0_B}, s{M0_XB}"]
     if read_next:
         slots[61] += ["s_waitcnt lgkmcnt(0)"]
@@ -161,7 +191,7 @@ def body(dma_on: bool, wait_next: bool, read_next: bool, bf16: bool = False):
     return lines
 
 
-def setup(k_tiles_skipped: int):
+def setup(k_tiles_skipped: int, amn: bool = False):
     """SRDs at K-tile `k_tiles_skipped` of this tile's A / B rows, soffsets, DMA destinations of buffer 0."""
     L = [f"s_mov_b32 s{M0_KEEP}, m0",
          f"s_mov_b64 s[{SRD_A}:{SRD_A + 1}], %[pa]", f"s_mov_b32 s{SRD_A + 2}, -1", f"s_mov_b32 s{SRD_A + 3}, 0x20000",
@@ -169,19 +199,23 @@ def setup(k_tiles_skipped: int):
          f"s_mov_b32 s{SOFF}, %[stride]"]
     for n in range(1, 7):
         L.append(f"s_add_u32 s{SOFF + n}, s{SOFF + n - 1}, %[stride]")
+    if amn:
+        L += [f"s_mov_b32 s{SOFF_A}, %[stridea]", f"s_mov_b32 s{ADV_A}, %[adva]"]
+        for n in range(1, 7):
+            L.append(f"s_add_u32 s{SOFF_A + n}, s{SOFF_A + n - 1}, %[stridea]")
     for _ in range(k_tiles_skipped):
-        L += advance_srd("A") + advance_srd("B")
+        L += advance_srd("A", amn) + advance_srd("B")
     L += [f"s_mov_b32 s{M0_A}, %[m0a]", f"s_add_u32 s{M0_B}, %[m0a], 33792",
           f"s_add_u32 s{M0_X}, %[m0a], 67584", f"s_xor_b32 s{M0_X}, s{M0_X}, %[m0a]",
           f"s_add_u32 s{M0_XB}, s{M0_B}, 67584", f"s_xor_b32 s{M0_XB}, s{M0_XB}, s{M0_B}"]
     return L
 
 
-def issue():
+def issue(amn: bool = False):
     """DMA of K-tiles 0 and 1 of a tile into LDS buffers 0 and 1. Issued for the NEXT tile of a persistent
     workgroup before the current tile's epilogue (every wave passed the last body's final barrier after its last
     ds_read, so both buffers are free), which hides the first loads' latency under the epilogue."""
-    L = setup(0)
+    L = setup(0, amn)
     for tile in range(2):
         L.append(f"s_mov_b32 m0, s{M0_B}")
         L.append("s_nop 0")
@@ -190,19 +224,19 @@ def issue():
         L.append(f"s_mov_b32 m0, s{M0_A}")
         L.append("s_nop 0")
         for n in range(8):
-            L += dma("A", n)
+            L += dma("A", n, amn)
         if tile == 0:
-            L += advance_srd("A") + advance_srd("B")
+            L += advance_srd("A", amn) + advance_srd("B")
             L += [f"s_xor_b32 s{M0_A}, s{M0_A}, s{M0_X}", f"s_xor_b32 s{M0_B}, s{M0_B}, s{M0_XB}"]
     L.append(f"s_mov_b32 m0, s{M0_KEEP}")
     return L
 
 
-def main_loop(bf16: bool = False):
+def main_loop(bf16: bool = False, amn: bool = False):
     """Everything after `issue()`: zero the accumulators, K-tile 0's fragments, the loop and the 2-tile tail.
     vmcnt(16) at the start: the 32 DMAs of `issue()` plus whatever epilogue stores the previous tile issued after
     them (vmcnt counts in order) -> at most the 16 newest may still be in flight, so K-tile 0 has landed."""
-    L = setup(2)
+    L = setup(2, amn)
     L.append(f"s_mov_b32 s{CNT}, %[cnt]")
     for a in range(256):
         L.append(f"v_accvgpr_write_b32 a{a}, 0")
@@ -210,34 +244,39 @@ def main_loop(bf16: bool = False):
     for f in range(4):
         L += ds_frag(B_BASE, f, "%[vb]")
     for f in range(4):
-        L += ds_frag(A_BASE, f, "%[va]")
+        L += a_frag(f, amn)
     L += ["s_waitcnt lgkmcnt(0)"]
     L += [f"s_cmp_eq_u32 s{CNT}, 0", "s_cbranch_scc1 2f", "1:"]
-    L += body(dma_on=True, wait_next=True, read_next=True, bf16=bf16)
+    L += body(dma_on=True, wait_next=True, read_next=True, bf16=bf16, amn=amn)
     L += [f"s_sub_u32 s{CNT}, s{CNT}, 1", f"s_cmp_eq_u32 s{CNT}, 0", "s_cbranch_scc0 1b", "2:"]
-    L += body(dma_on=False, wait_next=True, read_next=True, bf16=bf16)
-    L += body(dma_on=False, wait_next=False, read_next=False, bf16=bf16)
+    L += body(dma_on=False, wait_next=True, read_next=True, bf16=bf16, amn=amn)
+    L += body(dma_on=False, wait_next=False, read_next=False, bf16=bf16, amn=amn)
     L += ["s_nop 7", "s_nop 7", "s_nop 7", f"s_mov_b32 m0, s{M0_KEEP}"]
     return L
 
 
 def generate() -> str:
     I, L, LB = issue(), main_loop(), main_loop(bf16=True)
+    IT, LT = issue(amn=True), main_loop(bf16=True, amn=True)
     n_mfma = sum(1 for x in L if x.startswith("v_mfma"))
     assert n_mfma == 3 * 64, n_mfma
     assert sum(1 for x in LB if x.startswith("v_mfma")) == 3 * 128
+    assert sum(1 for x in LT if x.startswith("v_mfma")) == 3 * 128
+    assert sum(1 for x in LT if x.startswith("ds_read_b64_tr_b16")) == 16 + 32 + 32 + 16
     out = ["// GENERATED by tools/gen_fp8_asm.py -- do not edit by hand; edit the generator and rerun it.",
            "// K-loop of fp8_gemm_asm_kernel (csrc/kernels/fp8_gemm_asm.hip): see the generator's docstring.",
            f"// FP8ASM_ISSUE {len(I)} lines; FP8ASM_MAIN_LOOP {len(L)} lines, {n_mfma} MFMAs (loop body 64);",
-           f"// BF16ASM_MAIN_LOOP {len(LB)} lines (loop body 128 MFMAs).",
+           f"// BF16ASM_MAIN_LOOP {len(LB)} lines (loop body 128 MFMAs); BF16AMN_* (MN-major A): {len(IT)} / {len(LT)} lines.",
            "#pragma once"]
-    for name, lines in (("FP8ASM_ISSUE", I), ("FP8ASM_MAIN_LOOP", L), ("BF16ASM_MAIN_LOOP", LB)):
+    for name, lines in (("FP8ASM_ISSUE", I), ("FP8ASM_MAIN_LOOP", L), ("BF16ASM_MAIN_LOOP", LB),
+                        ("BF16AMN_ISSUE", IT), ("BF16AMN_MAIN_LOOP", LT)):
         out.append(f"#define {name} \\")
         for x in lines:
             out.append(f'  "{x}\\n" \\')
         out.append('  ""')
         out.append("")
     out.append(f"#define FP8ASM_SGPR_CLOBBERS " + ", ".join(f'"s{s}"' for s in range(SRD_A, M0_KEEP + 1)))
+    out.append(f"#define BF16AMN_SGPR_CLOBBERS " + ", ".join(f'"s{s}"' for s in range(SRD_A, ADV_A + 1)))
     out.append("")
     return "\n".join(out)
 

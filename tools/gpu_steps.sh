@@ -33,6 +33,11 @@ for step in "$@"; do
     bench20_mxfp8) run bench20_mxfp8 600 python bench.py --gpus 1 --steps 20 --warmup 5 --precision mxfp8 ;;
     bench20_adambf16) run bench20_adambf16 600 python bench.py --gpus 1 --steps 20 --warmup 5 --adam-states bf16 ;;
     bench20_asm) ACCELERATE_ASM_BF16_GEMM=1 run bench20_asm 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    bench20_noamn) ACCELERATE_ASM_WGRAD_AMN=0 run bench20_noamn 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    bench20_b) run bench20_b 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    bench20_noamn_b) ACCELERATE_ASM_WGRAD_AMN=0 run bench20_noamn_b 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    newtests) run newtests 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py tests/test_async_checkpoint.py -k "upcast or layerwise or amn or grouped or moe or async or native_writer" ;;
+    mr_sp) run mr_sp 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_multirank.py -k "tp" ;;
     bench20_asmw) ACCELERATE_ASM_BF16_GEMM=wgrad run bench20_asmw 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench20_dyt) ACCELERATE_WGRAD_DYT=1 run bench20_dyt 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     prof8b_dyt) ACCELERATE_WGRAD_DYT=1 prof prof8b_dyt 600 bench.py --steps 3 --warmup 2 $BENCH_ARGS ;;
@@ -70,6 +75,9 @@ for step in "$@"; do
     prof_mixtral8l_bf16) prof prof_mixtral8l_bf16 600 bench.py --model mixtral-8x7b-8l --steps 2 --warmup 1 ;;
     mix8_bf16) run mix8_bf16 600 python bench.py --model mixtral-8x7b-8l --steps 5 --warmup 2 --verbose $BENCH_ARGS ;;
     mix8_fp8) run mix8_fp8 600 python bench.py --model mixtral-8x7b-8l --steps 5 --warmup 2 --precision fp8 --verbose $BENCH_ARGS ;;
+    mix8_bf16_asmall) ACCELERATE_MOE_ASM_BF16=fwd,wgrad,dgrad run mix8_bf16_asmall 600 python bench.py --model mixtral-8x7b-8l --steps 5 --warmup 2 --verbose $BENCH_ARGS ;;
+    mix8_bf16_asmnone) ACCELERATE_MOE_ASM_BF16=none run mix8_bf16_asmnone 600 python bench.py --model mixtral-8x7b-8l --steps 5 --warmup 2 --verbose $BENCH_ARGS ;;
+    mix8_bf16_asmfwd) ACCELERATE_MOE_ASM_BF16=fwd run mix8_bf16_asmfwd 600 python bench.py --model mixtral-8x7b-8l --steps 5 --warmup 2 --verbose $BENCH_ARGS ;;
     mix8_bf16_nonn) ACCELERATE_MOE_DGRAD_NN=0 run mix8_bf16_nonn 600 python bench.py --model mixtral-8x7b-8l --steps 5 --warmup 2 --verbose $BENCH_ARGS ;;
     mix8_fp8_noroute) ACCELERATE_MOE_ROUTE_HIP=0 run mix8_fp8_noroute 600 python bench.py --model mixtral-8x7b-8l --steps 5 --warmup 2 --precision fp8 --verbose $BENCH_ARGS ;;
     mix8_fp8_nocastt) ACCELERATE_MOE_FP8_CAST_T=0 run mix8_fp8_nocastt 600 python bench.py --model mixtral-8x7b-8l --steps 5 --warmup 2 --precision fp8 --verbose $BENCH_ARGS ;;
@@ -116,6 +124,8 @@ for step in "$@"; do
     gemm) run gemm 300 python tools/bench_gemm.py ;;
     asmdiag) run asmdiag 120 python tools/debug/fp8asm_diag.py ;;
     gemm_grp) run gemm_grp 400 python tools/bench_gemm.py --variants ${GEMM_VARIANTS:-bl,18,18g1,18g2,18g8,18g16} --no-bf16 --no-scaled-mm --rounds 3 ;;
+    amn) run ktest_amn 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "bf16_asm" && \
+         run gemm_amn 400 python tools/bench_gemm_amn.py ;;
     gemm_bf16) run ktest_bf16asm 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "bf16_asm" && \
                run gemm_bf16 400 python tools/bench_gemm_bf16.py ;;
     ktest_moe_asm) run ktest_moe_asm 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "grouped or moe or expert" ;;
