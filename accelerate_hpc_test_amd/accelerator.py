@@ -1101,9 +1101,11 @@ class Accelerator:
         if not inf and norm_type != 2.0:
             raise NotImplementedError(f"clip_grad_norm_ on DTensor parameters supports norm_type 2 and inf, not {norm_type}")
         dev = grads_params[0].grad.device
-        shard_part = torch.zeros(1, dtype=torch.float32, device=dev)
         rest_part = torch.zeros(1, dtype=torch.float32, device=dev)
-        groups = []
+        # one partial per (mesh, set of sharded mesh dims): a gradient sharded on dims {0, 1} of a 2-D mesh is summed
+        # over both groups, one sharded on dim 1 only over that group (summing it over dim 0 too would count it once
+        # per dim-0 replica)
+        partials = {}
         for p in grads_params:
             g = p.grad
             if isinstance(g, DTensor):
@@ -1111,21 +1113,25 @@ class Accelerator:
                     g = p.grad = g.redistribute(placements=[Replicate() if pl.is_partial() else pl for pl in g.placements])
                 local = g.to_local().detach().float()
                 v = local.abs().max().reshape(1) if inf and local.numel() else local.pow(2).sum().reshape(1)
-                if any(pl.is_shard() for pl in g.placements):
-                    shard_part = torch.maximum(shard_part, v) if inf else shard_part + v
-                    for d, pl in enumerate(g.placements):
-                        if pl.is_shard():
-                            grp = g.device_mesh.get_group(d)
-                            if grp not in groups:
-                                groups.append(grp)
+                dims = tuple(d for d, pl in enumerate(g.placements) if pl.is_shard())
+                if dims:
+                    key = (id(g.device_mesh), dims)
+                    if key not in partials:
+                        partials[key] = [g.device_mesh, dims, torch.zeros(1, dtype=torch.float32, device=dev)]
+                    acc = partials[key]
+                    acc[2] = torch.maximum(acc[2], v) if inf else acc[2] + v
                     continue
             else:
                 local = g.detach().float()
                 v = local.abs().max().reshape(1) if inf and local.numel() else local.pow(2).sum().reshape(1)
             rest_part = torch.maximum(rest_part, v) if inf else rest_part + v
-        for grp in groups:
-            dist.all_reduce(shard_part, op=dist.ReduceOp.MAX if inf else dist.ReduceOp.SUM, group=grp)
-        total = torch.maximum(shard_part, rest_part) if inf else (shard_part + rest_part).sqrt()
+        total = rest_part
+        for mesh, dims, part in partials.values():
+            for d in dims:
+                dist.all_reduce(part, op=dist.ReduceOp.MAX if inf else dist.ReduceOp.SUM, group=mesh.get_group(d))
+            total = torch.maximum(total, part) if inf else total + part
+        if not inf:
+            total = total.sqrt()
         coef = (max_norm / (total + 1e-6)).clamp(max=1.0)
         for p in grads_params:
             g = p.grad.to_local() if isinstance(p.grad, DTensor) else p.grad

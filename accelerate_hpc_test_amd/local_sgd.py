@@ -59,10 +59,16 @@ class LocalSGD:
         gloo = dist.get_backend(group) == "gloo"
 
         def average(buf):
-            if not buf.dtype.is_floating_point:  # integer / bool parameters: sum then floor-divide (stays integral)
+            if buf.dtype == torch.bool:
+                # bool parameters: a majority vote over the ranks (RCCL would reduce bool as uint8; a SUM is neither a
+                # mean nor guaranteed to stay 0 / 1), computed in int32 so every rank ends with the same flags; ties
+                # keep True
+                votes = buf.to(torch.int32)
+                dist.all_reduce(votes, group=group)
+                buf.copy_(votes * 2 >= world)
+            elif not buf.dtype.is_floating_point:  # integer parameters: sum then floor-divide (stays integral)
                 dist.all_reduce(buf, group=group)
-                if buf.dtype != torch.bool:
-                    buf.div_(world, rounding_mode="floor")
+                buf.div_(world, rounding_mode="floor")
             elif gloo:
                 dist.all_reduce(buf, group=group)
                 buf.div_(world)

@@ -442,6 +442,38 @@ def check_tp_fsdp_sharded_merge():
         assert "tensor-parallel size" in str(exc)
 
 
+def check_dtensor_clip_norm_2d_mesh(norm_type: float = 2.0):
+    """DTensor gradients on a 2 x 2 mesh sharded on dim 0 only, dim 1 only, both dims, or replicated: the global norm
+    of `Accelerator._clip_grad_norm_dtensor` equals the norm of the full gradients (each partial is reduced over its
+    own sharded dims only), and the clip scales every local shard by the same factor."""
+    import torch.distributed as dist
+    from torch.distributed.device_mesh import init_device_mesh
+    from torch.distributed.tensor import Replicate, Shard, distribute_tensor
+
+    acc = Accelerator(cpu=True)
+    assert acc.num_processes == 4
+    mesh = init_device_mesh("cpu", (2, 2))
+    g = torch.Generator().manual_seed(0)
+    fulls = [torch.randn(8, 6, generator=g) for _ in range(4)]
+    grads = [torch.randn(8, 6, generator=g) for _ in range(4)]
+    layouts = [[Shard(0), Replicate()], [Replicate(), Shard(1)], [Shard(0), Shard(1)], [Replicate(), Replicate()]]
+    params = []
+    for w, gr, pl in zip(fulls, grads, layouts):
+        p = torch.nn.Parameter(distribute_tensor(w.clone(), mesh, pl))
+        p.grad = distribute_tensor(gr.clone(), mesh, pl)
+        params.append(p)
+    want = torch.stack([x.abs().max() for x in grads]).max() if norm_type == float("inf") else \
+        torch.sqrt(sum((x ** 2).sum() for x in grads))
+    total = Accelerator._clip_grad_norm_dtensor(params, 1e9, norm_type)
+    assert torch.allclose(total, want, rtol=1e-5), (total, want)
+    clip = float(want) / 4
+    total = Accelerator._clip_grad_norm_dtensor(params, clip, norm_type)
+    for p, gr in zip(params, grads):
+        got = p.grad.full_tensor()
+        assert torch.allclose(got, gr * (clip / (float(want) + 1e-6)), rtol=1e-4, atol=1e-6)
+    dist.barrier()
+
+
 def check_tp_dtensor_model(steps: int = 3, norm_type: float = 2.0):
     """A model already sharded as DTensors (torch `parallelize_module`, the layout transformers' `tp_plan="auto"`
     produces in the reference's nd-parallel flow) goes through `prepare` unchanged; AdamW runs torch's DTensor-aware
@@ -671,7 +703,8 @@ def check_local_sgd(k: int = 2, steps: int = 4, chunk_bytes: int = 256 << 20):
 
 def check_local_sgd_integer_params():
     """Non-float parameters (e.g. an integer step counter registered as a frozen Parameter) are averaged too, in
-    their own buckets (sum, then floor division), as the reference's per-parameter `reduce(param, "mean")` does."""
+    their own buckets: integers as sum then floor division (the reference's per-parameter `reduce(param, "mean")`
+    cannot divide an integer tensor in place), bool flags by majority vote (ties True), identical on every rank."""
     from accelerate_hpc_test_amd.local_sgd import LocalSGD
 
     acc = Accelerator(cpu=True)
@@ -679,14 +712,24 @@ def check_local_sgd_integer_params():
     set_seed(0)
     model = TinyMLP()
     model.counter = torch.nn.Parameter(torch.zeros(2, dtype=torch.int64), requires_grad=False)
+    model.small = torch.nn.Parameter(torch.zeros(3, dtype=torch.int8), requires_grad=False)
+    model.flags = torch.nn.Parameter(torch.zeros(4, dtype=torch.bool), requires_grad=False)
     opt = torch.optim.SGD([p for p in model.parameters() if p.is_floating_point()], lr=0.1)
     model, opt = acc.prepare(model, opt)
-    acc.unwrap_model(model).counter.data.copy_(torch.tensor([10 * (r + 1), 3 * r]))  # diverged after DDP's broadcast
+    inner = acc.unwrap_model(model)
+    inner.counter.data.copy_(torch.tensor([10 * (r + 1), 3 * r]))  # diverged after DDP's broadcast
+    inner.small.data.copy_(torch.tensor([r, -r, 7], dtype=torch.int8))
+    # flag 0 set on every rank, flag 1 on rank 0 only, flag 2 on ranks < W / 2 (a tie at even W), flag 3 on none
+    inner.flags.data.copy_(torch.tensor([True, r == 0, r < W / 2, False]))
     with LocalSGD(acc, model, local_sgd_steps=1) as local_sgd:
         local_sgd.step()
-    inner = acc.unwrap_model(model)
     want = torch.tensor([sum(10 * (j + 1) for j in range(W)) // W, sum(3 * j for j in range(W)) // W])
     assert inner.counter.dtype == torch.int64 and torch.equal(inner.counter.data, want), (inner.counter, want)
+    want8 = torch.tensor([sum(range(W)) // W, -sum(range(W)) // W, 7], dtype=torch.int8)
+    assert inner.small.dtype == torch.int8 and torch.equal(inner.small.data, want8), (inner.small, want8)
+    votes = [W, 1, sum(1 for j in range(W) if j < W / 2), 0]
+    want_b = torch.tensor([2 * v >= W for v in votes])
+    assert inner.flags.dtype == torch.bool and torch.equal(inner.flags.data, want_b), (inner.flags, want_b)
 
 
 def _local_sgd_loop(acc, model, opt, sims, sim_opts, batches, W, r, bs, k, chunk_bytes):

@@ -113,6 +113,12 @@ def test_tensor_parallel_x_fsdp_sharded_checkpoint_merge():
     debug_launcher(td.check_tp_fsdp_sharded_merge, num_processes=4)
 
 
+@pytest.mark.parametrize("norm_type", [2.0, float("inf")])
+def test_dtensor_clip_norm_2d_mesh(norm_type):
+    """DTensor grads sharded on different dims of a 2 x 2 mesh: global norm == full-tensor norm (no over-counting)."""
+    debug_launcher(td.check_dtensor_clip_norm_2d_mesh, args=(norm_type,), num_processes=4)
+
+
 def test_fsdp_full_state_load_missing_keys():
     """Rank-0 broadcast FULL_STATE_DICT load: a missing key raises on every rank (strict) or keeps the parameter's
     values (non-strict) -- never a silent zero fill."""
@@ -204,8 +210,9 @@ def test_fsdp_checkpoint_io_is_per_rank_bounded(sd_type, load_world, tmp_path):
     debug_launcher(td.check_fsdp_checkpoint_io, args=("load", d, sd_type), num_processes=load_world)
 
 
-def test_local_sgd_averages_integer_params():
-    debug_launcher(td.check_local_sgd_integer_params, num_processes=2)
+@pytest.mark.parametrize("world", [2, 3])
+def test_local_sgd_averages_integer_and_bool_params(world):
+    debug_launcher(td.check_local_sgd_integer_params, num_processes=world)
 
 
 def test_fsdp_three_ranks():
