@@ -1,7 +1,9 @@
 """Sharded checkpoint round trip of Llama-3-8B on the FSDP engine's multi-rank code path at one rank (forced sharded,
-one-rank RCCL group): one AdamW step, `save_state` (SHARDED_STATE_DICT: model shard as safetensors + JSON, optimizer
-shard as safetensors + JSON), perturb, `load_state`, compare. Prints wall times, checkpoint bytes, the process's
-peak host RSS and the RSS growth across the load, as one JSON line.
+one-rank RCCL group): a few AdamW steps (timed), `save_state` (SHARDED_STATE_DICT: model shard as safetensors + JSON,
+optimizer shard as safetensors + JSON) through the non-blocking writer (utils/async_checkpoint.py: device snapshot,
+native D2H file writer), training steps while the files are written (timed against the steps before), the wait for
+the writer, perturb, `load_state`, compare with the state at save time. Prints wall times, checkpoint bytes, the
+process's peak host RSS and the RSS growth across save and load, as one JSON line.
 
     python tools/ckpt_roundtrip.py [--model llama3-8b] [--dir /tmp/ckpt8b] [--seq 2048]"""
 import argparse
@@ -60,11 +62,16 @@ def main():
     model, opt = acc.prepare(model, opt)
     assert model.engine.sharded
     ids = torch.randint(0, cfg.vocab_size, (1, args.seq), device=acc.device)
-    acc.backward(model(ids, labels=ids).loss)
-    opt.step()
-    opt.zero_grad()
-    torch.cuda.synchronize()
 
+    def step():
+        t0 = time.time()
+        acc.backward(model(ids, labels=ids).loss)
+        opt.step()
+        opt.zero_grad()
+        torch.cuda.synchronize()
+        return time.time() - t0
+
+    normal = [step() for _ in range(4)][1:]
     def snapshot():
         eng = model.engine
         m = torch.stack([u.master.double().sum() for u in eng.units]).cpu()
@@ -75,10 +82,17 @@ def main():
     before = snapshot()
     rss0 = rss_gib()
     shutil.rmtree(ckpt, ignore_errors=True)
+    from accelerate_hpc_test_amd.utils.async_checkpoint import wait_pending_saves, writer
+
     t = time.time()
     acc.save_state(ckpt)
     torch.cuda.synchronize()
-    t_save = time.time() - t
+    t_save = time.time() - t  # what the training loop is blocked for
+    during = [step() for _ in range(3)]  # the writer streams the snapshot to disk meanwhile
+    t = time.time()
+    wait_pending_saves()
+    t_wait = time.time() - t
+    t_total = t_save + sum(during) + t_wait
     nbytes = dir_bytes(ckpt)
     rss_after_save = rss_gib()
     with torch.no_grad():
@@ -93,8 +107,10 @@ def main():
     after = snapshot()
     ok = bool(torch.equal(before[0], after[0]) and torch.equal(before[1], after[1]))
     res = {"model": args.model, "world": 1, "path": "fsdp-forced-sharded", "ckpt_gib": round(nbytes / 2**30, 2),
-           "save_s": round(t_save, 1), "load_s": round(t_load, 1),
-           "save_gbps": round(nbytes / t_save / 1e9, 2), "load_gbps": round(nbytes / t_load / 1e9, 2),
+           "save_blocking_s": round(t_save, 3), "async_snapshot_gib": round(writer().last_snapshot_bytes / 2**30, 2),
+           "step_s_before_save": [round(x, 3) for x in normal], "step_s_while_writing": [round(x, 3) for x in during],
+           "wait_after_steps_s": round(t_wait, 2), "save_to_disk_s": round(t_total, 1), "load_s": round(t_load, 1),
+           "save_gbps_end_to_end": round(nbytes / t_total / 1e9, 2), "load_gbps": round(nbytes / t_load / 1e9, 2),
            "tensor_bytes_read_gib": round(fsdp_utils.IO_STATS["bytes_read"] / 2**30, 2),
            "rss_gib": {"before_save": round(rss0, 1), "after_save": round(rss_after_save, 1),
                        "before_load": round(rss_before_load, 1), "after_load": round(rss_gib(), 1),
