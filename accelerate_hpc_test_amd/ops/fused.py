@@ -37,6 +37,11 @@ _WGRAD_DYT = os.environ.get("ACCELERATE_WGRAD_DYT", "0") == "1"
 # row index contiguous) through transposed LDS reads, x from the saved token-contiguous copy; no transposed dy
 # (tools/bench_gemm_amn.py, profiles/r6_gemm_amn.md)
 _ASM_WGRAD_AMN = os.environ.get("ACCELERATE_ASM_WGRAD_AMN", "1") != "0"
+# weight gradients with BOTH operands read as the step has them (dy [T, N] and the layer input x [T, K], token-major):
+# the asm kernel's MN-major-A/B mode computes xᵀ·dy and stores its transpose, so the engines keep x itself instead of
+# a token-contiguous copy (no transpose in the forward, 2 GiB less for Llama-3-8B at 8k tokens): 387.4 / 387.8 vs
+# 390.9 / 391.1 ms per step on one box (profiles/r6_gemm_amn.md). ACCELERATE_ASM_WGRAD_ABMN=0: the x^T copy + MN-A mode.
+ASM_WGRAD_ABMN = os.environ.get("ACCELERATE_ASM_WGRAD_ABMN", "1") != "0"
 
 
 def asm_gemm_bf16(a: torch.Tensor, b: torch.Tensor, bias=None, out=None, accumulate: bool = False, kind: str = "fwd"):
@@ -431,10 +436,12 @@ def wgrad_into(dest: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, accumula
     a, b = dy2.t(), x2
     if b.dtype != a.dtype:
         b = b.to(a.dtype)
-    if (_ASM_WGRAD_AMN and dest.is_cuda and dest.is_contiguous() and a.dtype == torch.bfloat16 and dy2.is_contiguous()
-            and b.t().is_contiguous() and dest.dtype in (torch.float32, torch.bfloat16) and use_native(dy2)
+    if (dest.is_cuda and dest.is_contiguous() and a.dtype == torch.bfloat16 and dy2.is_contiguous()
+            and dest.dtype in (torch.float32, torch.bfloat16) and use_native(dy2)
             and dy2.shape[1] % 256 == 0 and b.shape[1] % 256 == 0 and dy2.shape[0] % 64 == 0 and dy2.shape[0] >= 128):
-        if ext().bf16_gemm_asm_amn(dy2, b.t(), dest, accumulate, False):
+        if _ASM_WGRAD_AMN and b.t().is_contiguous() and ext().bf16_gemm_asm_amn(dy2, b.t(), dest, accumulate, False):
+            return
+        if ASM_WGRAD_ABMN and b.is_contiguous() and ext().bf16_gemm_asm_amn(b, dy2, dest, accumulate, True, True):
             return
     # asm kernel: both operands token-contiguous -- x2 is the transposed view of the saved xᵀ, dy2 is transposed here
     if ("wgrad" in _ASM_BF16_KINDS and dest.is_cuda and dest.is_contiguous() and a.dtype == torch.bfloat16

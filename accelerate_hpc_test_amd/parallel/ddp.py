@@ -34,6 +34,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..ops._ext import ext, use_native
+from ..ops import fused as fused_ops
 from ..ops.fused import linear_dgrad, wgrad_into
 from ..utils.dataclasses import DDPCommunicationHookType
 from ..utils.fault_tolerance import record_collective
@@ -93,7 +94,7 @@ class _DDPFusedLinearFn(torch.autograd.Function):
         # token-contiguous copy xᵀ for the weight-gradient GEMM (as the FSDP engine does, parallel/fsdp.py
         # _FusedWgradLinearFn): hipBLASLt's fp32-output kernels run that layout with a depth-64 tile instead of a
         # depth-32 one (measured on Llama-3-8B under the reducer: 1.21 ms -> ~0.91 ms per call)
-        ctx.x_t = (x2.is_cuda and x2.dtype == torch.bfloat16 and x2.is_contiguous() and x2.shape[0] % 64 == 0
+        ctx.x_t = (not fused_ops.ASM_WGRAD_ABMN and x2.is_cuda and x2.dtype == torch.bfloat16 and x2.is_contiguous() and x2.shape[0] % 64 == 0
                    and x2.shape[1] % 64 == 0 and use_native(x2))
         ctx.save_for_backward(ext().transpose_bf16(x2) if ctx.x_t else x2, wc)
         ctx.slot, ctx.xdtype, ctx.xshape = slot, x.dtype, x.shape

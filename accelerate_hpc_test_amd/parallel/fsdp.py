@@ -51,6 +51,7 @@ from ..utils.fault_tolerance import record_collective
 from ..utils.tracing import trace_range
 from ..ops._ext import ext, native_enabled
 from ..ops.fp8 import Fp8Linear
+from ..ops import fused as fused_ops
 from ..ops.fused import linear_dgrad, linear_fwd, wgrad_into
 from . import small_allreduce
 
@@ -1621,7 +1622,7 @@ class _FusedWgradLinearFn(torch.autograd.Function):
         # so there the copy is extra: T x 4096 bf16 = 64 MiB per layer, 2 GiB for Llama-3-8B at 8k tokens (peak
         # 175 of 288 GiB; kept for the faster layout). ACCELERATE_FSDP_WGRAD_XT=0 disables it. The opt-in hipBLASLt
         # wgrad runner (ACCELERATE_BLASLT_WGRAD=1) takes either layout (ops/fused.py wgrad_into).
-        ctx.x_transposed = (_WGRAD_XT and x2.is_cuda and x2.dtype == torch.bfloat16 and x2.is_contiguous() and native_enabled()
+        ctx.x_transposed = (_WGRAD_XT and not fused_ops.ASM_WGRAD_ABMN and x2.is_cuda and x2.dtype == torch.bfloat16 and x2.is_contiguous() and native_enabled()
                             and x2.shape[0] % 64 == 0 and x2.shape[1] % 64 == 0)
         ctx.save_for_backward(ext().transpose_bf16(x2) if ctx.x_transposed else x, weight)
         ctx.slot = slot

@@ -387,6 +387,18 @@ def test_bf16_asm_amn_gemm_matches_fp32_reference(M, N, K):
     acc16 = base16.clone()
     assert ext().bf16_gemm_asm_amn(a, b, acc16, True, True)
     assert _rel(acc16.float(), base16.float() + ref.t()) < 1e-2
+    # MN-major B too (b given as [K, N]), transposed store: exact integers, fp32 oracle, accumulate
+    out_tb = torch.empty(N, M, device=DEV)
+    assert ext().bf16_gemm_asm_amn(ai, bi.t().contiguous(), out_tb, False, True, True)
+    assert torch.equal(out_tb, refi.t()), (out_tb - refi.t()).abs().max()
+    bt = b.t().contiguous()
+    o32t = torch.empty(N, M, device=DEV)
+    assert ext().bf16_gemm_asm_amn(a, bt, o32t, False, True, True)
+    assert torch.allclose(o32t, ref.t(), rtol=1e-4, atol=tol), (o32t - ref.t()).abs().max()
+    acct = base.t().contiguous()
+    assert ext().bf16_gemm_asm_amn(a, bt, acct, True, True, True)
+    assert torch.allclose(acct, base.t() + ref.t(), rtol=1e-4, atol=tol)
+    assert not ext().bf16_gemm_asm_amn(a, bt, torch.empty(M, N, device=DEV), False, False, True)  # needs trans_out
     # shapes it does not tile are declined (nothing launched)
     assert not ext().bf16_gemm_asm_amn(a[:, : M - 128].contiguous(), b, torch.empty(M - 128, N, device=DEV), False, False)
 

@@ -84,19 +84,30 @@ def main():
         ref = dy.float().t() @ xt.float().t()
         err_w = ((dw - ref).norm() / ref.norm()).item()
         del ref
-        tb, ta = [], []
+        x = xt.t().contiguous()  # [T, K]: the layer input as the forward has it (no saved transposed copy)
+        dw3 = torch.empty(N, K, device="cuda", dtype=torch.float32)
+        assert ext().bf16_gemm_asm_amn(x, dy, dw3, False, True, True)
+        err_w2 = ((dw3 - dw).norm() / dw.norm()).item()
+        tb, ta, tab, tx = [], [], [], []
         for _ in range(args.rounds):
             if ok_bl:
                 tb.append(timeit(lambda: ext().blaslt_wgrad_f32(dy, xt, dw2, False, True), args.iters))
             else:
                 tb.append(timeit(lambda: torch.mm(dy.t(), xt.t(), out_dtype=torch.float32, out=dw2), args.iters))
             ta.append(timeit(lambda: ext().bf16_gemm_asm_amn(dy, xt, dw, False, False), args.iters))
-        m_b, m_a = statistics.median(tb), statistics.median(ta)
+            tab.append(timeit(lambda: ext().bf16_gemm_asm_amn(x, dy, dw3, False, True, True), args.iters))
+            tx.append(timeit(lambda: ext().transpose_bf16(x), args.iters))
+        m_b, m_a, m_ab, m_x = statistics.median(tb), statistics.median(ta), statistics.median(tab), statistics.median(tx)
         tot["wgrad_today"] += m_b
         tot["wgrad_asm"] += m_a
+        tot["wgrad_asm_abmn"] = tot.get("wgrad_asm_abmn", 0.0) + m_ab
+        tot["x_transpose"] = tot.get("x_transpose", 0.0) + m_x
         print(json.dumps({"gemm": f"{name}.wgrad", "M": N, "N": K, "K": T, "blaslt_runner": bool(ok_bl),
                           "blaslt_tflops": round(flops / m_b / 1e9, 1), "asm_amn_tflops": round(flops / m_a / 1e9, 1),
-                          "asm_vs_blaslt": round(m_b / m_a, 3), "asm_rel_err": float(f"{err_w:.3g}")}), flush=True)
+                          "asm_abmn_tflops": round(flops / m_ab / 1e9, 1), "x_transpose_ms": round(m_x, 3),
+                          "asm_vs_blaslt": round(m_b / m_a, 3), "abmn_plus_no_transpose_vs_amn": round((m_a + m_x) / m_ab, 3),
+                          "asm_rel_err": float(f"{err_w:.3g}"), "abmn_vs_amn_rel": float(f"{err_w2:.3g}")}), flush=True)
+        del x, dw3
         del dy, w, xt, dw, dw2
         torch.cuda.empty_cache()
     print(json.dumps({"totals_ms_one_layer_each": {k: round(v, 3) for k, v in tot.items()}}), flush=True)

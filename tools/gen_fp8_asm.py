@@ -39,6 +39,10 @@ pieces cover all 64 banks once. Fragments come out of LDS through `ds_read_b64_t
 `ds_read_b128`): lane 4q + p of a 16-lane group g supplies row 8g + 4s + q (+32 for the second MFMA of the K-tile),
 columns 4p..4p+3 of its block; block i = 16 consecutive output rows 16i..16i+15 of the wave's 128. One address VGPR
 serves all 32 reads of a K-tile (immediate offsets 16896 h + 512 s + 32 i).
+
+MN-major A and B (`BF16ABMN_*`): B takes the same image and transposed reads (block j = 16 consecutive output columns);
+the kernel then stores C^T (the accumulator's registers run along A's rows), so the 16-column blocks never have to be
+re-packed for 16-byte stores. B's K-tile step is s69; its soffsets reuse s48..s54 (the host passes 8 rows x ldb).
 """
 
 from __future__ import annotations
@@ -61,6 +65,7 @@ M0_KEEP = 60  # caller's m0
 CHUNK_STEP = 4 * 1056  # m0 advance per DMA instruction (4 waves x one 1056-B chunk)
 SOFF_A = 61   # MN-major A: s61..s67 = j * 8 rows * lda, j = 1..7
 ADV_A = 68    # MN-major A: bytes between K-tiles (64 rows * lda)
+ADV_B = 69    # MN-major B: bytes between K-tiles (64 rows * ldb); its soffsets reuse s48..s54 (= j * 8 rows * ldb)
 
 
 def A(i):
@@ -94,15 +99,19 @@ def ds_frag(dst_base, f, addr):
             f"ds_read_b128 v[{d + 4}:{d + 7}], {addr} offset:{128 * f + 64}"]
 
 
-def ds_frag_tr(f, addr):
-    """MN-major A fragment f: four ds_read_b64_tr_b16 (MFMA half h, k sub-block s) into v[d + 4h + 2s : +1]"""
-    d = A_BASE + 8 * f
+def ds_frag_tr(f, addr, base=A_BASE):
+    """MN-major fragment f: four ds_read_b64_tr_b16 (MFMA half h, k sub-block s) into v[d + 4h + 2s : +1]"""
+    d = base + 8 * f
     return [f"ds_read_b64_tr_b16 v[{d + 4 * h + 2 * s}:{d + 4 * h + 2 * s + 1}], {addr} offset:{16896 * h + 512 * s + 32 * f}"
             for h in range(2) for s in range(2)]
 
 
 def a_frag(f, amn):
     return ds_frag_tr(f, "%[va]") if amn else ds_frag(A_BASE, f, "%[va]")
+
+
+def b_frag(f, bmn):
+    return ds_frag_tr(f, "%[vb]", B_BASE) if bmn else ds_frag(B_BASE, f, "%[vb]")
 
 
 def dma(op, n, amn=False):
@@ -122,12 +131,13 @@ def dma(op, n, amn=False):
 
 
 def advance_srd(op, amn=False):
+    """`amn`: this operand is MN-major (its K-tile step is a whole row block, held in an SGPR)"""
     srd = SRD_A if op == "A" else SRD_B
-    step = f"s{ADV_A}" if (op == "A" and amn) else "128"
+    step = (f"s{ADV_A}" if op == "A" else f"s{ADV_B}") if amn else "128"
     return [f"s_add_u32 s{srd}, s{srd}, {step}", f"s_addc_u32 s{srd + 1}, s{srd + 1}, 0"]
 
 
-def body(dma_on: bool, wait_next: bool, read_next: bool, bf16: bool = False, amn: bool = False):
+def body(dma_on: bool, wait_next: bool, read_next: bool, bf16: bool = False, amn: bool = False, bmn: bool = False):
     """one K-tile; returns a list of instruction lines. Extra work is attached after MFMA #k via `slots[k]`. bf16:
     each accumulator block takes two MFMAs; in every run of four blocks (same A fragment) the four first halves are
     issued, each followed by its slot's work, then the four second halves (4 MFMAs between dependent ones)."""
@@ -136,7 +146,7 @@ def body(dma_on: bool, wait_next: bool, read_next: bool, bf16: bool = False, amn
              + [(i, j) for i in range(4, 8) for j in range(4)] + [(i, j) for i in range(4, 8) for j in range(4, 8)])
     # phase 1: B4-7 of t, then (after the barrier) B DMA 0..4 and A4-7 of t
     for f in range(4):
-        slots[f] += ds_frag(B_BASE, 4 + f, "%[vb]")
+        slots[f] += b_frag(4 + f, bmn)
     if dma_on:
         slots[5] += [f"s_mov_b32 m0, s{M0_B}"]
     slots[5] += ["s_waitcnt lgkmcnt(0)"]
@@ -154,7 +164,7 @@ def body(dma_on: bool, wait_next: bool, read_next: bool, bf16: bool = False, amn
         for n in range(5, 8):
             slots[22 + n - 5] += dma("B", n)
         slots[24] += [f"s_mov_b32 m0, s{M0_A}"]
-        slots[28] += advance_srd("B")  # the SRD bases always point at the next K-tile to load
+        slots[28] += advance_srd("B", bmn)  # the SRD bases always point at the next K-tile to load
         for n in range(2):
             slots[25 + n] += dma("A", n, amn)
         # phase 3
@@ -167,7 +177,7 @@ def body(dma_on: bool, wait_next: bool, read_next: bool, bf16: bool = False, amn
     if read_next:
         slots[47] += ["v_xor_b32 %[va], %[vax], %[va]", "v_xor_b32 %[vb], %[vbx], %[vb]"]
         for f in range(4):
-            slots[48 + f] += ds_frag(B_BASE, f, "%[vb]")
+            slots[48 + f] += b_frag(f, bmn)
         for f in range(4):
             slots[52 + f + (1 if f >= 1 else 0)] += a_frag(f, amn)
     if dma_on:
@@ -191,7 +201,7 @@ def body(dma_on: bool, wait_next: bool, read_next: bool, bf16: bool = False, amn
     return lines
 
 
-def setup(k_tiles_skipped: int, amn: bool = False):
+def setup(k_tiles_skipped: int, amn: bool = False, bmn: bool = False):
     """SRDs at K-tile `k_tiles_skipped` of this tile's A / B rows, soffsets, DMA destinations of buffer 0."""
     L = [f"s_mov_b32 s{M0_KEEP}, m0",
          f"s_mov_b64 s[{SRD_A}:{SRD_A + 1}], %[pa]", f"s_mov_b32 s{SRD_A + 2}, -1", f"s_mov_b32 s{SRD_A + 3}, 0x20000",
@@ -203,19 +213,21 @@ def setup(k_tiles_skipped: int, amn: bool = False):
         L += [f"s_mov_b32 s{SOFF_A}, %[stridea]", f"s_mov_b32 s{ADV_A}, %[adva]"]
         for n in range(1, 7):
             L.append(f"s_add_u32 s{SOFF_A + n}, s{SOFF_A + n - 1}, %[stridea]")
+    if bmn:
+        L += [f"s_mov_b32 s{ADV_B}, %[advb]"]
     for _ in range(k_tiles_skipped):
-        L += advance_srd("A", amn) + advance_srd("B")
+        L += advance_srd("A", amn) + advance_srd("B", bmn)
     L += [f"s_mov_b32 s{M0_A}, %[m0a]", f"s_add_u32 s{M0_B}, %[m0a], 33792",
           f"s_add_u32 s{M0_X}, %[m0a], 67584", f"s_xor_b32 s{M0_X}, s{M0_X}, %[m0a]",
           f"s_add_u32 s{M0_XB}, s{M0_B}, 67584", f"s_xor_b32 s{M0_XB}, s{M0_XB}, s{M0_B}"]
     return L
 
 
-def issue(amn: bool = False):
+def issue(amn: bool = False, bmn: bool = False):
     """DMA of K-tiles 0 and 1 of a tile into LDS buffers 0 and 1. Issued for the NEXT tile of a persistent
     workgroup before the current tile's epilogue (every wave passed the last body's final barrier after its last
     ds_read, so both buffers are free), which hides the first loads' latency under the epilogue."""
-    L = setup(0, amn)
+    L = setup(0, amn, bmn)
     for tile in range(2):
         L.append(f"s_mov_b32 m0, s{M0_B}")
         L.append("s_nop 0")
@@ -226,31 +238,31 @@ def issue(amn: bool = False):
         for n in range(8):
             L += dma("A", n, amn)
         if tile == 0:
-            L += advance_srd("A", amn) + advance_srd("B")
+            L += advance_srd("A", amn) + advance_srd("B", bmn)
             L += [f"s_xor_b32 s{M0_A}, s{M0_A}, s{M0_X}", f"s_xor_b32 s{M0_B}, s{M0_B}, s{M0_XB}"]
     L.append(f"s_mov_b32 m0, s{M0_KEEP}")
     return L
 
 
-def main_loop(bf16: bool = False, amn: bool = False):
+def main_loop(bf16: bool = False, amn: bool = False, bmn: bool = False):
     """Everything after `issue()`: zero the accumulators, K-tile 0's fragments, the loop and the 2-tile tail.
     vmcnt(16) at the start: the 32 DMAs of `issue()` plus whatever epilogue stores the previous tile issued after
     them (vmcnt counts in order) -> at most the 16 newest may still be in flight, so K-tile 0 has landed."""
-    L = setup(2, amn)
+    L = setup(2, amn, bmn)
     L.append(f"s_mov_b32 s{CNT}, %[cnt]")
     for a in range(256):
         L.append(f"v_accvgpr_write_b32 a{a}, 0")
     L += ["s_waitcnt vmcnt(16)", "s_barrier"]
     for f in range(4):
-        L += ds_frag(B_BASE, f, "%[vb]")
+        L += b_frag(f, bmn)
     for f in range(4):
         L += a_frag(f, amn)
     L += ["s_waitcnt lgkmcnt(0)"]
     L += [f"s_cmp_eq_u32 s{CNT}, 0", "s_cbranch_scc1 2f", "1:"]
-    L += body(dma_on=True, wait_next=True, read_next=True, bf16=bf16, amn=amn)
+    L += body(dma_on=True, wait_next=True, read_next=True, bf16=bf16, amn=amn, bmn=bmn)
     L += [f"s_sub_u32 s{CNT}, s{CNT}, 1", f"s_cmp_eq_u32 s{CNT}, 0", "s_cbranch_scc0 1b", "2:"]
-    L += body(dma_on=False, wait_next=True, read_next=True, bf16=bf16, amn=amn)
-    L += body(dma_on=False, wait_next=False, read_next=False, bf16=bf16, amn=amn)
+    L += body(dma_on=False, wait_next=True, read_next=True, bf16=bf16, amn=amn, bmn=bmn)
+    L += body(dma_on=False, wait_next=False, read_next=False, bf16=bf16, amn=amn, bmn=bmn)
     L += ["s_nop 7", "s_nop 7", "s_nop 7", f"s_mov_b32 m0, s{M0_KEEP}"]
     return L
 
@@ -258,6 +270,8 @@ def main_loop(bf16: bool = False, amn: bool = False):
 def generate() -> str:
     I, L, LB = issue(), main_loop(), main_loop(bf16=True)
     IT, LT = issue(amn=True), main_loop(bf16=True, amn=True)
+    IBT, LBT = issue(amn=True, bmn=True), main_loop(bf16=True, amn=True, bmn=True)
+    assert sum(1 for x in LBT if x.startswith("ds_read_b64_tr_b16")) == 2 * (16 + 32 + 32 + 16)
     n_mfma = sum(1 for x in L if x.startswith("v_mfma"))
     assert n_mfma == 3 * 64, n_mfma
     assert sum(1 for x in LB if x.startswith("v_mfma")) == 3 * 128
@@ -269,7 +283,8 @@ def generate() -> str:
            f"// BF16ASM_MAIN_LOOP {len(LB)} lines (loop body 128 MFMAs); BF16AMN_* (MN-major A): {len(IT)} / {len(LT)} lines.",
            "#pragma once"]
     for name, lines in (("FP8ASM_ISSUE", I), ("FP8ASM_MAIN_LOOP", L), ("BF16ASM_MAIN_LOOP", LB),
-                        ("BF16AMN_ISSUE", IT), ("BF16AMN_MAIN_LOOP", LT)):
+                        ("BF16AMN_ISSUE", IT), ("BF16AMN_MAIN_LOOP", LT),
+                        ("BF16ABMN_ISSUE", IBT), ("BF16ABMN_MAIN_LOOP", LBT)):
         out.append(f"#define {name} \\")
         for x in lines:
             out.append(f'  "{x}\\n" \\')
@@ -277,6 +292,7 @@ def generate() -> str:
         out.append("")
     out.append(f"#define FP8ASM_SGPR_CLOBBERS " + ", ".join(f'"s{s}"' for s in range(SRD_A, M0_KEEP + 1)))
     out.append(f"#define BF16AMN_SGPR_CLOBBERS " + ", ".join(f'"s{s}"' for s in range(SRD_A, ADV_A + 1)))
+    out.append(f"#define BF16ABMN_SGPR_CLOBBERS " + ", ".join(f'"s{s}"' for s in range(SRD_A, ADV_B + 1)))
     out.append("")
     return "\n".join(out)
 

@@ -33,6 +33,8 @@ for step in "$@"; do
     bench20_mxfp8) run bench20_mxfp8 600 python bench.py --gpus 1 --steps 20 --warmup 5 --precision mxfp8 ;;
     bench20_adambf16) run bench20_adambf16 600 python bench.py --gpus 1 --steps 20 --warmup 5 --adam-states bf16 ;;
     bench20_asm) ACCELERATE_ASM_BF16_GEMM=1 run bench20_asm 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    bench20_abmn) ACCELERATE_ASM_WGRAD_ABMN=1 run bench20_abmn 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    bench20_abmn_b) ACCELERATE_ASM_WGRAD_ABMN=1 run bench20_abmn_b 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench20_noamn) ACCELERATE_ASM_WGRAD_AMN=0 run bench20_noamn 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench20_b) run bench20_b 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench20_noamn_b) ACCELERATE_ASM_WGRAD_AMN=0 run bench20_noamn_b 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
