@@ -106,27 +106,48 @@ def ds_frag_tr(f, addr, base=A_BASE):
             for h in range(2) for s in range(2)]
 
 
-def a_frag(f, amn):
-    return ds_frag_tr(f, "%[va]") if amn else ds_frag(A_BASE, f, "%[va]")
+# fp8 MN-major image (`mn8`): a 1 KiB chunk = 4 k-rows x 256 B, chunk stride 1040 B (16 B pad: rows in consecutive
+# chunks start 16 B apart modulo 256). Row k of a K-tile sits in chunk (k & 7) | ((k >> 4) & 1) << 3 | (k >> 6) << 4 at
+# row ((k >> 3) & 1) | ((k >> 5) & 1) << 1, so the 16 k-rows one half-wave of a ds_read_b64_tr_b8 touches (8 rows of
+# two 16-lane groups) fall in 16 consecutive chunks and their 16-B pieces cover the 64 banks once. Fragment registers
+# 2s, 2s + 1 hold the k-run s of lane group g: k = 16 g + (0, 8, 64, 72)[s] .. +7 (the 16x16x128 f8 operand's bytes
+# 16 g .. 16 g + 15 and 64 + 16 g .. 64 + 16 g + 15), read at immediate offsets (0, 256, 16640, 16896)[s] + 16 i.
+MN8_CHUNK = 1040
+MN8_RUN_OFF = (0, 256, 16 * MN8_CHUNK, 16 * MN8_CHUNK + 256)
+MN8_ROW_OFF = (4, 16, 20, 64, 68, 80, 84)  # k-row of DMA instruction j (j = 1..7) of wave 0, lane 0: soffset = row * ld
 
 
-def b_frag(f, bmn):
-    return ds_frag_tr(f, "%[vb]", B_BASE) if bmn else ds_frag(B_BASE, f, "%[vb]")
+def ds_frag_tr8(f, addr, base=A_BASE):
+    """fp8 MN-major fragment f: four ds_read_b64_tr_b8 (k-run s) into v[d + 2s : +1]"""
+    d = base + 8 * f
+    return [f"ds_read_b64_tr_b8 v[{d + 2 * s}:{d + 2 * s + 1}], {addr} offset:{MN8_RUN_OFF[s] + 16 * f}" for s in range(4)]
 
 
-def dma(op, n, amn=False):
-    """n-th (0..7) DMA instruction of operand op ('A'|'B'); m0 must hold this instruction's destination"""
+def a_frag(f, amn, mn8=False):
+    if amn:
+        return ds_frag_tr8(f, "%[va]") if mn8 else ds_frag_tr(f, "%[va]")
+    return ds_frag(A_BASE, f, "%[va]")
+
+
+def b_frag(f, bmn, mn8=False):
+    if bmn:
+        return ds_frag_tr8(f, "%[vb]", B_BASE) if mn8 else ds_frag_tr(f, "%[vb]", B_BASE)
+    return ds_frag(B_BASE, f, "%[vb]")
+
+
+def dma(op, n, amn=False, mn8=False):
+    """n-th (0..7) DMA instruction of operand op ('A'|'B'); m0 must hold this instruction's destination. `amn`: this
+    operand is MN-major; `mn8`: in the fp8 MN image (1040-B chunks)."""
     srd = SRD_A if op == "A" else SRD_B
+    step = 4 * MN8_CHUNK if (amn and mn8) else CHUNK_STEP
     if op == "A" and amn:
         so = "0" if n == 0 else f"s{SOFF_A + n - 1}"
         out = [f"buffer_load_dwordx4 %[voffa], s[{srd}:{srd + 3}], {so} offen lds"]
-        if n < 7:
-            out.append(f"s_add_u32 m0, m0, {CHUNK_STEP}")
-        return out
-    so = "0" if n == 0 else f"s{SOFF + n - 1}"
-    out = [f"buffer_load_dwordx4 %[voff], s[{srd}:{srd + 3}], {so} offen lds"]
+    else:
+        so = "0" if n == 0 else f"s{SOFF + n - 1}"
+        out = [f"buffer_load_dwordx4 %[voff], s[{srd}:{srd + 3}], {so} offen lds"]
     if n < 7:
-        out.append(f"s_add_u32 m0, m0, {CHUNK_STEP}")
+        out.append(f"s_add_u32 m0, m0, {step}")
     return out
 
 
@@ -137,7 +158,8 @@ def advance_srd(op, amn=False):
     return [f"s_add_u32 s{srd}, s{srd}, {step}", f"s_addc_u32 s{srd + 1}, s{srd + 1}, 0"]
 
 
-def body(dma_on: bool, wait_next: bool, read_next: bool, bf16: bool = False, amn: bool = False, bmn: bool = False):
+def body(dma_on: bool, wait_next: bool, read_next: bool, bf16: bool = False, amn: bool = False, bmn: bool = False,
+         reads_on: bool = True, mn8: bool = False):
     """one K-tile; returns a list of instruction lines. Extra work is attached after MFMA #k via `slots[k]`. bf16:
     each accumulator block takes two MFMAs; in every run of four blocks (same A fragment) the four first halves are
     issued, each followed by its slot's work, then the four second halves (4 MFMAs between dependent ones)."""
@@ -145,43 +167,44 @@ def body(dma_on: bool, wait_next: bool, read_next: bool, bf16: bool = False, amn
     order = ([(i, j) for i in range(4) for j in range(4)] + [(i, j) for i in range(4) for j in range(4, 8)]
              + [(i, j) for i in range(4, 8) for j in range(4)] + [(i, j) for i in range(4, 8) for j in range(4, 8)])
     # phase 1: B4-7 of t, then (after the barrier) B DMA 0..4 and A4-7 of t
-    for f in range(4):
-        slots[f] += b_frag(4 + f, bmn)
+    for f in range(4 if reads_on else 0):
+        slots[f] += b_frag(4 + f, bmn, mn8)
     if dma_on:
         slots[5] += [f"s_mov_b32 m0, s{M0_B}"]
     slots[5] += ["s_waitcnt lgkmcnt(0)"]
     slots[6] += ["s_barrier"]
     if dma_on:
         for n in range(5):
-            slots[8 + n] += dma("B", n)
-    for f in range(3):
-        slots[13 + f] += a_frag(4 + f, amn)
+            slots[8 + n] += dma("B", n, bmn, mn8)
+    for f in range(3 if reads_on else 0):
+        slots[13 + f] += a_frag(4 + f, amn, mn8)
     # phase 2
-    slots[16] += a_frag(7, amn)
+    if reads_on:
+        slots[16] += a_frag(7, amn, mn8)
     slots[20] += ["s_waitcnt lgkmcnt(0)"]
     slots[21] += ["s_barrier"]
     if dma_on:
         for n in range(5, 8):
-            slots[22 + n - 5] += dma("B", n)
+            slots[22 + n - 5] += dma("B", n, bmn, mn8)
         slots[24] += [f"s_mov_b32 m0, s{M0_A}"]
         slots[28] += advance_srd("B", bmn)  # the SRD bases always point at the next K-tile to load
         for n in range(2):
-            slots[25 + n] += dma("A", n, amn)
+            slots[25 + n] += dma("A", n, amn, mn8)
         # phase 3
         for n in range(2, 7):
-            slots[38 + n - 2] += dma("A", n, amn)
+            slots[38 + n - 2] += dma("A", n, amn, mn8)
     if wait_next:
         slots[45] += ["s_waitcnt vmcnt(15)" if dma_on else "s_waitcnt vmcnt(0)"]
         slots[46] += ["s_barrier"]
     # phase 4: lo fragments of t+1 from the other buffer
     if read_next:
         slots[47] += ["v_xor_b32 %[va], %[vax], %[va]", "v_xor_b32 %[vb], %[vbx], %[vb]"]
-        for f in range(4):
-            slots[48 + f] += b_frag(f, bmn)
-        for f in range(4):
-            slots[52 + f + (1 if f >= 1 else 0)] += a_frag(f, amn)
+        for f in range(4 if reads_on else 0):
+            slots[48 + f] += b_frag(f, bmn, mn8)
+        for f in range(4 if reads_on else 0):
+            slots[52 + f + (1 if f >= 1 else 0)] += a_frag(f, amn, mn8)
     if dma_on:
-        slots[53] += dma("A", 7, amn)
+        slots[53] += dma("A", 7, amn, mn8)
         slots[55] += advance_srd("A", amn)
         slots[57] += [f"s_xor_b32 s{M0_A}, s{M0_A}, s{M0_X}", f"s_xor_b32 s{M0_B}, s{M0_B}, s{M0_XB}"]
     if read_next:
@@ -201,15 +224,23 @@ def body(dma_on: bool, wait_next: bool, read_next: bool, bf16: bool = False, amn
     return lines
 
 
-def setup(k_tiles_skipped: int, amn: bool = False, bmn: bool = False):
-    """SRDs at K-tile `k_tiles_skipped` of this tile's A / B rows, soffsets, DMA destinations of buffer 0."""
+def setup(k_tiles_skipped: int, amn: bool = False, bmn: bool = False, mn8: bool = False):
+    """SRDs at K-tile `k_tiles_skipped` of this tile's A / B rows, soffsets, DMA destinations of buffer 0. fp8 MN-major
+    operands (`mn8`): %[stride] / %[stridea] are the row strides in bytes, the soffsets MN8_ROW_OFF[j] rows, and B's DMA
+    base comes in as %[m0b] (the two images have different chunk strides)."""
     L = [f"s_mov_b32 s{M0_KEEP}, m0",
          f"s_mov_b64 s[{SRD_A}:{SRD_A + 1}], %[pa]", f"s_mov_b32 s{SRD_A + 2}, -1", f"s_mov_b32 s{SRD_A + 3}, 0x20000",
-         f"s_mov_b64 s[{SRD_B}:{SRD_B + 1}], %[pb]", f"s_mov_b32 s{SRD_B + 2}, -1", f"s_mov_b32 s{SRD_B + 3}, 0x20000",
-         f"s_mov_b32 s{SOFF}, %[stride]"]
-    for n in range(1, 7):
-        L.append(f"s_add_u32 s{SOFF + n}, s{SOFF + n - 1}, %[stride]")
-    if amn:
+         f"s_mov_b64 s[{SRD_B}:{SRD_B + 1}], %[pb]", f"s_mov_b32 s{SRD_B + 2}, -1", f"s_mov_b32 s{SRD_B + 3}, 0x20000"]
+    if bmn and mn8:
+        L += [f"s_mul_i32 s{SOFF + n - 1}, %[stride], {MN8_ROW_OFF[n - 1]}" for n in range(1, 8)]
+    else:
+        L.append(f"s_mov_b32 s{SOFF}, %[stride]")
+        for n in range(1, 7):
+            L.append(f"s_add_u32 s{SOFF + n}, s{SOFF + n - 1}, %[stride]")
+    if amn and mn8:
+        L += [f"s_mov_b32 s{ADV_A}, %[adva]"]
+        L += [f"s_mul_i32 s{SOFF_A + n - 1}, %[stridea], {MN8_ROW_OFF[n - 1]}" for n in range(1, 8)]
+    elif amn:
         L += [f"s_mov_b32 s{SOFF_A}, %[stridea]", f"s_mov_b32 s{ADV_A}, %[adva]"]
         for n in range(1, 7):
             L.append(f"s_add_u32 s{SOFF_A + n}, s{SOFF_A + n - 1}, %[stridea]")
@@ -217,26 +248,26 @@ def setup(k_tiles_skipped: int, amn: bool = False, bmn: bool = False):
         L += [f"s_mov_b32 s{ADV_B}, %[advb]"]
     for _ in range(k_tiles_skipped):
         L += advance_srd("A", amn) + advance_srd("B", bmn)
-    L += [f"s_mov_b32 s{M0_A}, %[m0a]", f"s_add_u32 s{M0_B}, %[m0a], 33792",
+    L += [f"s_mov_b32 s{M0_A}, %[m0a]", f"s_mov_b32 s{M0_B}, %[m0b]" if mn8 else f"s_add_u32 s{M0_B}, %[m0a], 33792",
           f"s_add_u32 s{M0_X}, %[m0a], 67584", f"s_xor_b32 s{M0_X}, s{M0_X}, %[m0a]",
           f"s_add_u32 s{M0_XB}, s{M0_B}, 67584", f"s_xor_b32 s{M0_XB}, s{M0_XB}, s{M0_B}"]
     return L
 
 
-def issue(amn: bool = False, bmn: bool = False):
+def issue(amn: bool = False, bmn: bool = False, mn8: bool = False):
     """DMA of K-tiles 0 and 1 of a tile into LDS buffers 0 and 1. Issued for the NEXT tile of a persistent
     workgroup before the current tile's epilogue (every wave passed the last body's final barrier after its last
     ds_read, so both buffers are free), which hides the first loads' latency under the epilogue."""
-    L = setup(0, amn, bmn)
+    L = setup(0, amn, bmn, mn8)
     for tile in range(2):
         L.append(f"s_mov_b32 m0, s{M0_B}")
         L.append("s_nop 0")
         for n in range(8):
-            L += dma("B", n)
+            L += dma("B", n, bmn, mn8)
         L.append(f"s_mov_b32 m0, s{M0_A}")
         L.append("s_nop 0")
         for n in range(8):
-            L += dma("A", n, amn)
+            L += dma("A", n, amn, mn8)
         if tile == 0:
             L += advance_srd("A", amn) + advance_srd("B", bmn)
             L += [f"s_xor_b32 s{M0_A}, s{M0_A}, s{M0_X}", f"s_xor_b32 s{M0_B}, s{M0_B}, s{M0_XB}"]
@@ -244,25 +275,28 @@ def issue(amn: bool = False, bmn: bool = False):
     return L
 
 
-def main_loop(bf16: bool = False, amn: bool = False, bmn: bool = False):
+def main_loop(bf16: bool = False, amn: bool = False, bmn: bool = False, probe: str = "", mn8: bool = False):
     """Everything after `issue()`: zero the accumulators, K-tile 0's fragments, the loop and the 2-tile tail.
     vmcnt(16) at the start: the 32 DMAs of `issue()` plus whatever epilogue stores the previous tile issued after
     them (vmcnt counts in order) -> at most the 16 newest may still be in flight, so K-tile 0 has landed."""
-    L = setup(2, amn, bmn)
+    L = setup(2, amn, bmn, mn8)
     L.append(f"s_mov_b32 s{CNT}, %[cnt]")
     for a in range(256):
         L.append(f"v_accvgpr_write_b32 a{a}, 0")
     L += ["s_waitcnt vmcnt(16)", "s_barrier"]
     for f in range(4):
-        L += b_frag(f, bmn)
+        L += b_frag(f, bmn, mn8)
     for f in range(4):
-        L += a_frag(f, amn)
+        L += a_frag(f, amn, mn8)
     L += ["s_waitcnt lgkmcnt(0)"]
     L += [f"s_cmp_eq_u32 s{CNT}, 0", "s_cbranch_scc1 2f", "1:"]
-    L += body(dma_on=True, wait_next=True, read_next=True, bf16=bf16, amn=amn, bmn=bmn)
+    # probe loops (timing diagnostics only, wrong results): "nodma" issues no LDS-DMA inside the loop, "noread" no
+    # fragment reads, "mfma" neither
+    L += body(dma_on=probe not in ("nodma", "mfma"), wait_next=True, read_next=True, bf16=bf16, amn=amn, bmn=bmn,
+              reads_on=probe not in ("noread", "mfma"), mn8=mn8)
     L += [f"s_sub_u32 s{CNT}, s{CNT}, 1", f"s_cmp_eq_u32 s{CNT}, 0", "s_cbranch_scc0 1b", "2:"]
-    L += body(dma_on=False, wait_next=True, read_next=True, bf16=bf16, amn=amn, bmn=bmn)
-    L += body(dma_on=False, wait_next=False, read_next=False, bf16=bf16, amn=amn, bmn=bmn)
+    L += body(dma_on=False, wait_next=True, read_next=True, bf16=bf16, amn=amn, bmn=bmn, mn8=mn8)
+    L += body(dma_on=False, wait_next=False, read_next=False, bf16=bf16, amn=amn, bmn=bmn, mn8=mn8)
     L += ["s_nop 7", "s_nop 7", "s_nop 7", f"s_mov_b32 m0, s{M0_KEEP}"]
     return L
 
@@ -271,6 +305,11 @@ def generate() -> str:
     I, L, LB = issue(), main_loop(), main_loop(bf16=True)
     IT, LT = issue(amn=True), main_loop(bf16=True, amn=True)
     IBT, LBT = issue(amn=True, bmn=True), main_loop(bf16=True, amn=True, bmn=True)
+    probes = [(f"BF16ASM_PROBE_{k.upper()}_LOOP", main_loop(bf16=True, probe=k)) for k in ("nodma", "noread", "mfma")]
+    f8mn = [("FP8AMN_ISSUE", issue(amn=True, mn8=True)), ("FP8AMN_MAIN_LOOP", main_loop(amn=True, mn8=True)),
+            ("FP8ABMN_ISSUE", issue(amn=True, bmn=True, mn8=True)),
+            ("FP8ABMN_MAIN_LOOP", main_loop(amn=True, bmn=True, mn8=True))]
+    assert sum(1 for x in f8mn[3][1] if x.startswith("ds_read_b64_tr_b8")) == 2 * (16 + 32 + 32 + 16)
     assert sum(1 for x in LBT if x.startswith("ds_read_b64_tr_b16")) == 2 * (16 + 32 + 32 + 16)
     n_mfma = sum(1 for x in L if x.startswith("v_mfma"))
     assert n_mfma == 3 * 64, n_mfma
@@ -284,7 +323,7 @@ def generate() -> str:
            "#pragma once"]
     for name, lines in (("FP8ASM_ISSUE", I), ("FP8ASM_MAIN_LOOP", L), ("BF16ASM_MAIN_LOOP", LB),
                         ("BF16AMN_ISSUE", IT), ("BF16AMN_MAIN_LOOP", LT),
-                        ("BF16ABMN_ISSUE", IBT), ("BF16ABMN_MAIN_LOOP", LBT)):
+                        ("BF16ABMN_ISSUE", IBT), ("BF16ABMN_MAIN_LOOP", LBT)) + tuple(probes) + tuple(f8mn):
         out.append(f"#define {name} \\")
         for x in lines:
             out.append(f'  "{x}\\n" \\')

@@ -126,6 +126,8 @@ for step in "$@"; do
     gemm) run gemm 300 python tools/bench_gemm.py ;;
     asmdiag) run asmdiag 120 python tools/debug/fp8asm_diag.py ;;
     gemm_grp) run gemm_grp 400 python tools/bench_gemm.py --variants ${GEMM_VARIANTS:-bl,18,18g1,18g2,18g8,18g16} --no-bf16 --no-scaled-mm --rounds 3 ;;
+    gprobe) run gprobe 300 python tools/bench_gemm_probe.py ;;
+    trprobe) run trprobe 60 tools/microbench/tr_probe ;;
     amn) run ktest_amn 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "bf16_asm" && \
          run gemm_amn 400 python tools/bench_gemm_amn.py ;;
     gemm_bf16) run ktest_bf16asm 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "bf16_asm" && \
