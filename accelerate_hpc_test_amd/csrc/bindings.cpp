@@ -83,6 +83,8 @@ torch::Tensor fp8asm_dma_probe(torch::Tensor a, torch::Tensor b);
 bool bf16_gemm_asm(torch::Tensor a, torch::Tensor b, c10::optional<torch::Tensor> bias, torch::Tensor out, bool accumulate);
 bool bf16_gemm_asm_amn(torch::Tensor a_t, torch::Tensor b, torch::Tensor out, bool accumulate, bool trans_out, bool b_mn);
 bool bf16_gemm_asm_probe(torch::Tensor a, torch::Tensor b, torch::Tensor out, int64_t probe);
+bool fp8_gemm_asm_amn(torch::Tensor a_t, torch::Tensor b, c10::optional<torch::Tensor> sa, c10::optional<torch::Tensor> sb,
+                      double smul, torch::Tensor out, bool accumulate, bool b_mn);
 // cast.hip
 bool upcast_multi(std::vector<torch::Tensor> srcs, std::vector<torch::Tensor> dsts);
 bool grouped_gemm_asm(torch::Tensor a, torch::Tensor b, torch::Tensor out, std::vector<int64_t> bounds, int64_t mode,
@@ -175,6 +177,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("accumulate") = false, pybind11::arg("trans_out") = false, pybind11::arg("b_mn") = false,
         "out (=|+=) a_t^T . b^T (or its transpose) with a_t [K, M] M-contiguous (b_mn: b [K, N] N-contiguous, "
         "transposed store), on the asm GEMM; false = shape not tiled");
+  m.def("fp8_gemm_asm_amn", &fp8_gemm_asm_amn, pybind11::arg("a_t"), pybind11::arg("b"), pybind11::arg("sa"),
+        pybind11::arg("sb"), pybind11::arg("smul") = 1.0, pybind11::arg("out"), pybind11::arg("accumulate") = false,
+        pybind11::arg("b_mn") = false,
+        "out (=|+=) (a_t^T . b^T)^T * sa * sb * smul, fp8 a_t [K, M] M-contiguous (b_mn: b [K, N]); false = not tiled");
   m.def("bf16_gemm_asm_probe", &bf16_gemm_asm_probe, "timing probe of the bf16 asm loop (1 no DMA, 2 no reads, 3 MFMA only)");
   m.def("upcast_multi", &upcast_multi, pybind11::arg("srcs"), pybind11::arg("dsts"),
         "dsts[i] = srcs[i] upcast (fp8 / fp16 / bf16 / fp32 -> bf16 / fp16 / fp32) in one launch; false = not handled");

@@ -39,6 +39,11 @@ E5M2_MAX = 57344.0
 # other shapes take hipBLASLt when it accepts them. "blaslt" = hipBLASLt's fp8 kernels through our runner
 # (csrc/runtime/blaslt_gemm.cpp) whenever there is no bias.
 _FP8_GEMM_BACKEND = os.environ.get("ACCELERATE_FP8_GEMM", "hip")
+# The backward GEMMs on the asm kernel's MN-major modes (csrc/kernels/fp8_gemm_asm.hip `fp8_gemm_amn_kernel`,
+# ds_read_b64_tr_b8): dx^T = w8^T . dy8^T reads the e4m3 weight as it is, dW = (x8^T . dy8)^T reads x8 and dy8 as they
+# are, so every cast writes one layout (no transposed copies of x, dy or the weight). ACCELERATE_FP8_MN=0: the
+# transposing casts + K-major GEMMs.
+_FP8_MN = os.environ.get("ACCELERATE_FP8_MN", "1") != "0"
 
 
 def _asm_tileable(m: int, n: int, k: int) -> bool:
@@ -151,6 +156,21 @@ def gemm(a8: torch.Tensor, b8: torch.Tensor, a_scale_inv, b_scale_inv, bias=None
     else:
         out.copy_(res)
     return out
+
+
+def _mn_ok(T: int, N: int, K: int) -> bool:
+    """The three products of an fp8 linear (x [T, K], w [N, K]) all tile on the MN-major / K-major asm kernels."""
+    return (_FP8_MN and _FP8_GEMM_BACKEND == "hip" and T % 256 == 0 and N % 256 == 0 and K % 256 == 0
+            and T >= 256 and _asm_tileable(T, N, K))
+
+
+def gemm_t(a_t8: torch.Tensor, b8: torch.Tensor, a_scale_inv, b_scale_inv, out: torch.Tensor, b_mn: bool = False,
+           accumulate: bool = False):
+    """out (=|+=) ((a_t8ᵀ · b8ᵀ)ᵀ) · a_scale_inv · b_scale_inv on the MN-major asm kernel: a_t8 [K, M] (M contiguous),
+    b8 [N, K] or (b_mn) [K, N]; out [N, M]. Returns False when the kernel does not take the shape."""
+    ta, ma = _inv_parts(a_scale_inv)
+    tb, mb = _inv_parts(b_scale_inv)
+    return ext().fp8_gemm_asm_amn(a_t8, b8, ta, tb, ma * mb, out, accumulate, b_mn)
 
 
 def transpose_fp8(w8: torch.Tensor) -> torch.Tensor:
@@ -323,6 +343,21 @@ class _Fp8LinearFn(torch.autograd.Function):
         N = w.shape[0]
         fwd_max = E5M2_MAX if recipe.fwd_e5m2() else E4M3_MAX
         sx = recipe.scale("x", x2, fwd_max, producer_amax(x))
+        ctx.mn = x2.is_cuda and use_native(x2) and _mn_ok(x2.shape[0], N, x2.shape[1])
+        if ctx.mn:  # one layout of everything: the backward reads x8 and the weight as they are (MN-major kernels)
+            x8 = cast(x2, sx, recipe.fwd_e5m2())
+            ctx.pre_quantised = w_amax is not None
+            if ctx.pre_quantised:
+                sw = Scale(w_amax, E4M3_MAX)
+                w8 = w
+            else:
+                sw = recipe.scale("w", w, fwd_max)
+                w8 = cast(w, sw, recipe.fwd_e5m2())
+            y = gemm(x8, w8, sx, sw, bias, torch.bfloat16)
+            ctx.save_for_backward(x8, w8, sx.amax, sw.amax)
+            ctx.qmax = (sx.qmax, sw.qmax)
+            ctx.recipe, ctx.shape, ctx.has_bias, ctx.slot = recipe, shape, bias is not None, slot
+            return y.view(*shape[:-1], N)
         x8, x8t = cast(x2, sx, recipe.fwd_e5m2(), transpose=True)
         ctx.pre_quantised = w_amax is not None
         if ctx.pre_quantised:
@@ -345,6 +380,8 @@ class _Fp8LinearFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        if ctx.mn:
+            return _Fp8LinearFn._backward_mn(ctx, dy)
         x8t, w8t, ax, aw = ctx.saved_tensors
         if ctx.pre_quantised and ctx.transpose_w:
             w8t = transpose_fp8(w8t)
@@ -364,6 +401,34 @@ class _Fp8LinearFn(torch.autograd.Function):
             slot.engine._fused_slot_done(slot)
             return dx.view(ctx.shape), None, db, None, None, None, None
         dw = gemm(dy8t, x8t, sg, sx, None, torch.bfloat16)
+        return dx.view(ctx.shape), dw, db, None, None, None, None
+
+
+    @staticmethod
+    def _backward_mn(ctx, dy):
+        """dx = (w8ᵀ · dy8ᵀ)ᵀ and dW = (x8ᵀ · dy8)ᵀ on the MN-major asm kernel: dy is cast once, row-major."""
+        x8, w8, ax, aw = ctx.saved_tensors
+        sx, sw = Scale(ax, ctx.qmax[0]), Scale(aw, ctx.qmax[1])
+        recipe = ctx.recipe
+        N, K = w8.shape
+        dy2 = dy.reshape(-1, N).contiguous().to(torch.bfloat16)
+        gmax = E5M2_MAX if recipe.grad_e5m2() else E4M3_MAX
+        sg = recipe.scale("g", dy2, gmax, producer_amax(dy))
+        dy8 = cast(dy2, sg, recipe.grad_e5m2())
+        dx = torch.empty((dy2.shape[0], K), dtype=torch.bfloat16, device=dy2.device)
+        if not gemm_t(w8, dy8, sw, sg, dx):
+            raise RuntimeError(f"fp8 MN-major dgrad GEMM declined shape T={dy2.shape[0]} N={N} K={K}")
+        db = dy2.float().sum(0).to(dy.dtype) if ctx.has_bias else None
+        slot = ctx.slot
+        if slot is not None:
+            dest, acc = slot.engine._fused_slot_dest(slot)
+            if not gemm_t(x8, dy8, sx, sg, dest, b_mn=True, accumulate=acc):
+                raise RuntimeError("fp8 MN-major weight-gradient GEMM declined its shape")
+            slot.engine._fused_slot_done(slot)
+            return dx.view(ctx.shape), None, db, None, None, None, None
+        dw = torch.empty((N, K), dtype=torch.bfloat16, device=dy2.device)
+        if not gemm_t(x8, dy8, sx, sg, dw, b_mn=True):
+            raise RuntimeError("fp8 MN-major weight-gradient GEMM declined its shape")
         return dx.view(ctx.shape), dw, db, None, None, None, None
 
 

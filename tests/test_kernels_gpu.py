@@ -403,6 +403,61 @@ def test_bf16_asm_amn_gemm_matches_fp32_reference(M, N, K):
     assert not ext().bf16_gemm_asm_amn(a[:, : M - 128].contiguous(), b, torch.empty(M - 128, N, device=DEV), False, False)
 
 
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 1024), (2048, 1280, 4096)])
+def test_gemm8_two_waves_per_simd_exact(M, N, K):
+    """The 8-wave (two waves per SIMD) asm GEMM (gemm8_kernel, through bf16_gemm_asm_probe(..., 8)): bit-exact on small
+    integers (pins the 64-row slab fragment map, the 4 + 4 DMA split and the ROWMAP-2 epilogue)."""
+    from accelerate_hpc_test_amd.ops._ext import ext
+
+    torch.manual_seed(0)
+    a = torch.randint(-3, 4, (M, K), device=DEV).to(torch.bfloat16)
+    b = torch.randint(-3, 4, (N, K), device=DEV).to(torch.bfloat16)
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    assert ext().bf16_gemm_asm_probe(a, b, out, 8)
+    ref = (a.float() @ b.float().t()).to(torch.bfloat16)
+    assert torch.equal(out, ref), (out.float() - ref.float()).abs().max()
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 256), (512, 768, 640), (1024, 512, 4096), (768, 1280, 8192)])
+def test_fp8_asm_amn_gemm_matches_reference(M, N, K):
+    """The MN-major fp8 asm GEMM (ext().fp8_gemm_asm_amn, ds_read_b64_tr_b8 from the 1040-B-chunk image): a_t [K, M]
+    M-contiguous with b [N, K] or (b_mn) b [K, N]; out [N, M] = (a_tᵀ·bᵀ)ᵀ · sa · sb · smul. Exact small integers for
+    every e4m3 / e5m2 pairing and both B layouts, then scaled random operands with fp32 / bf16 outputs and accumulate
+    against the fp32 product of the dequantised operands."""
+    from accelerate_hpc_test_amd.ops._ext import ext
+
+    torch.manual_seed(0)
+    ai = torch.randint(-3, 4, (K, M), device=DEV).float()
+    bi = torch.randint(-3, 4, (N, K), device=DEV).float()
+    refi = (ai.t() @ bi.t()).t()  # [N, M]
+    for fa in (torch.float8_e4m3fn, torch.float8_e5m2):
+        for fb in (torch.float8_e4m3fn, torch.float8_e5m2):
+            a8, b8 = ai.to(fa), bi.to(fb)
+            out = torch.empty(N, M, device=DEV)
+            assert ext().fp8_gemm_asm_amn(a8, b8, None, None, 1.0, out, False, False)
+            assert torch.equal(out, refi), (fa, fb, (out - refi).abs().max())
+            out2 = torch.empty(N, M, device=DEV)
+            assert ext().fp8_gemm_asm_amn(a8, b8.t().contiguous(), None, None, 1.0, out2, False, True)
+            assert torch.equal(out2, refi), (fa, fb, "b_mn", (out2 - refi).abs().max())
+    a = (torch.randn(K, M, device=DEV) * 8).to(torch.float8_e4m3fn)
+    b = (torch.randn(N, K, device=DEV) * 8).to(torch.float8_e5m2)
+    sa = torch.tensor([0.5], device=DEV)
+    sb = torch.tensor([0.25], device=DEV)
+    ref = (a.float().t() @ b.float().t()).t() * 0.5 * 0.25 * 3.0
+    tol = 1e-3 * ref.abs().max().item()
+    o32 = torch.empty(N, M, device=DEV)
+    assert ext().fp8_gemm_asm_amn(a, b.t().contiguous(), sa, sb, 3.0, o32, False, True)
+    assert torch.allclose(o32, ref, rtol=1e-4, atol=tol), (o32 - ref).abs().max()
+    base = torch.randn(N, M, device=DEV)
+    acc = base.clone()
+    assert ext().fp8_gemm_asm_amn(a, b, sa, sb, 3.0, acc, True, False)
+    assert torch.allclose(acc, base + ref, rtol=1e-4, atol=tol)
+    o16 = torch.empty(N, M, device=DEV, dtype=torch.bfloat16)
+    assert ext().fp8_gemm_asm_amn(a, b, sa, sb, 3.0, o16, False, False)
+    assert _rel(o16.float(), ref) < 1e-2
+    assert not ext().fp8_gemm_asm_amn(a[:, : M - 128].contiguous(), b, None, None, 1.0, torch.empty(N, M - 128, device=DEV), False, False)
+
+
 @pytest.mark.parametrize("M,N,K", [(256, 256, 256), (512, 768, 1024), (1024, 512, 4096), (768, 1280, 2304)])
 def test_fp8_gemm_v4_and_unscaled_kernels_match_reference(M, N, K, monkeypatch):
     """The 16x16x128-MFMA kernel (v4: two 64 KiB LDS slots, BK 128) with the scaled (variant 6) and the unscaled

@@ -28,7 +28,15 @@ def timeit(fn, iters=20):
 def main():
     from accelerate_hpc_test_amd.ops._ext import ext
 
-    names = {0: "full", 1: "no_dma", 2: "no_reads", 3: "mfma_only"}
+    names = {0: "full", 1: "no_dma", 2: "no_reads", 3: "mfma_only", 4: "regload", 5: "regstage", 6: "spread", 7: "khalf", 8: "eight_waves"}
+    ai = torch.randint(-3, 4, (512, 1024), device="cuda").to(torch.bfloat16)
+    bi = torch.randint(-3, 4, (768, 1024), device="cuda").to(torch.bfloat16)
+    oi = torch.empty(512, 768, device="cuda", dtype=torch.bfloat16)
+    ref = (ai.float() @ bi.float().t()).to(torch.bfloat16)
+    for v in (8, 6, 7):
+        assert ext().bf16_gemm_asm_probe(ai, bi, oi, v)
+        print(json.dumps({"variant": v, "exact": bool(torch.equal(oi, ref)), "max_err": float((oi.float() - ref.float()).abs().max())}),
+              flush=True)
     for (m, n, k) in ((8192, 8192, 8192), (8192, 28672, 4096), (8192, 4096, 14336)):
         a = torch.randn(m, k, device="cuda", dtype=torch.bfloat16)
         b = torch.randn(n, k, device="cuda", dtype=torch.bfloat16)

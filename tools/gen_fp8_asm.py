@@ -135,10 +135,20 @@ def b_frag(f, bmn, mn8=False):
     return ds_frag(B_BASE, f, "%[vb]")
 
 
+PROBE_LOADS = [None]
+SPREAD = [False]  # bf16 body in the spread issue order (BF16ASM_SPREAD_MAIN_LOOP)  # "regload" / "regstage": the DMA slots issue register loads (+ LDS writes) instead (timing probe)
+
+
 def dma(op, n, amn=False, mn8=False):
     """n-th (0..7) DMA instruction of operand op ('A'|'B'); m0 must hold this instruction's destination. `amn`: this
     operand is MN-major; `mn8`: in the fp8 MN image (1040-B chunks)."""
     srd = SRD_A if op == "A" else SRD_B
+    if PROBE_LOADS[0] is not None:
+        so = "0" if n == 0 else f"s{SOFF + n - 1}"
+        out = [f"buffer_load_dwordx4 v[252:255], %[voff], s[{srd}:{srd + 3}], {so} offen"]
+        if PROBE_LOADS[0] == "regstage":
+            out.append(f"ds_write_b128 %[va], v[248:251] offset:{1024 * n}")
+        return out
     step = 4 * MN8_CHUNK if (amn and mn8) else CHUNK_STEP
     if op == "A" and amn:
         so = "0" if n == 0 else f"s{SOFF_A + n - 1}"
@@ -215,6 +225,30 @@ def body(dma_on: bool, wait_next: bool, read_next: bool, bf16: bool = False, amn
             lines.append(mfma(i, j))
             lines += slots[k]
         return lines
+    if SPREAD[0]:
+        # bf16, hipBLASLt-like issue order: per quadrant (16 blocks) the 16 first-half MFMAs, then the 16 second halves
+        # (a block's two MFMAs 16 apart); the quadrant's slot work is cut into single memory / wait / barrier
+        # operations (each with the scalar ops that feed it) and laid out evenly over its 32 MFMA gaps, in order.
+        for q in range(4):
+            ops = []
+            for k in range(16 * q, 16 * q + 16):
+                cur = []
+                for ins in slots[k]:
+                    cur.append(ins)
+                    if not ins.startswith(("s_mov_b32 m0", "s_add_u32 s", "s_addc_u32", "s_xor_b32", "v_xor_b32")):
+                        ops.append(cur)
+                        cur = []
+                if cur:
+                    ops.append(cur)
+            blocks = order[16 * q : 16 * q + 16]
+            mf = [mfma_bf16(i, j, 0) for (i, j) in blocks] + [mfma_bf16(i, j, 1) for (i, j) in blocks]
+            pos = {}
+            for n, op in enumerate(ops):
+                pos.setdefault(min(31, (n * 32) // max(1, len(ops))), []).extend(op)
+            for g in range(32):
+                lines.append(mf[g])
+                lines += pos.get(g, [])
+        return lines
     for c in range(0, 64, 4):
         for k in range(c, c + 4):
             lines.append(mfma_bf16(*order[k], 0))
@@ -222,6 +256,74 @@ def body(dma_on: bool, wait_next: bool, read_next: bool, bf16: bool = False, amn
         for k in range(c, c + 4):
             lines.append(mfma_bf16(*order[k], 1))
     return lines
+
+
+def frag_half(base, f, half, addr):
+    """one ds_read_b128: half `half` (K elements 32 half ..) of fragment f into v[base + 8f + 4 half : +3]"""
+    d = base + 8 * f + 4 * half
+    return f"ds_read_b128 v[{d}:{d + 3}], {addr} offset:{128 * f + 64 * half}"
+
+
+def body_kh(dma_on: bool, wait_next: bool, read_next: bool):
+    """bf16 K-tile in K-half order (the issue order of hipBLASLt's MT256x256x64 kernel): the 64 first-half MFMAs of
+    all 8 x 8 blocks, then the 64 second halves. Stage H0 reads this tile's second halves (16 ds_read_b128 into the
+    registers H1 of the previous tile left), then every wave holds the tile: lgkmcnt(0) + barrier, and the 16 DMAs of
+    tile t+2 into this buffer start, one per 4 MFMAs, running into H1. H1 waits for tile t+1 (vmcnt + barrier) and reads
+    its first halves into the registers H0 just released."""
+    gaps = {g: [] for g in range(128)}
+    reads_h1 = [frag_half(B_BASE, f, 1, "%[vb]") for f in range(8)] + [frag_half(A_BASE, f, 1, "%[va]") for f in range(8)]
+    for n, r in enumerate(reads_h1):
+        gaps[2 * n] += [r]
+    gaps[32] += ["s_waitcnt lgkmcnt(0)"]
+    gaps[33] += ["s_barrier"]  # every wave holds all of tile t: tile t+2 may overwrite its buffer
+    nd = 0
+    if dma_on:
+        gaps[34] += [f"s_mov_b32 m0, s{M0_B}"]
+        g = 35
+        for op in ("B", "A"):
+            for n in range(8):
+                gaps[g] += dma(op, n)
+                g += 4
+                nd += 1
+                if op == "B" and n == 7:
+                    gaps[g - 2] += advance_srd("B") + [f"s_mov_b32 m0, s{M0_A}"]
+        gaps[g - 2] += advance_srd("A") + [f"s_xor_b32 s{M0_A}, s{M0_A}, s{M0_X}", f"s_xor_b32 s{M0_B}, s{M0_B}, s{M0_XB}"]
+    if wait_next:
+        # DMAs of this iteration issued before gap 66: (66 - 35) // 4 + 1 = 8
+        issued = sum(1 for gg in range(35, 66) for x in gaps[gg] if x.startswith("buffer_load"))
+        gaps[66] += [f"s_waitcnt vmcnt({issued})" if dma_on else "s_waitcnt vmcnt(0)"]
+        gaps[67] += ["s_barrier"]  # tile t+1 landed for every wave
+    if read_next:
+        gaps[67] += ["v_xor_b32 %[va], %[vax], %[va]", "v_xor_b32 %[vb], %[vbx], %[vb]"]
+        reads_h0 = [frag_half(B_BASE, f, 0, "%[vb]") for f in range(8)] + [frag_half(A_BASE, f, 0, "%[va]") for f in range(8)]
+        for n, r in enumerate(reads_h0):
+            gaps[68 + 3 * n + (1 if n % 2 else 0)] += [r]
+        gaps[127] += ["s_waitcnt lgkmcnt(0)"]
+    lines = []
+    for h in range(2):
+        for i in range(8):
+            for j in range(8):
+                g = 64 * h + 8 * i + j
+                lines.append(mfma_bf16(i, j, h))
+                lines += gaps[g]
+    return lines
+
+
+def main_loop_kh():
+    L = setup(2)
+    L.append(f"s_mov_b32 s{CNT}, %[cnt]")
+    for a in range(256):
+        L.append(f"v_accvgpr_write_b32 a{a}, 0")
+    L += ["s_waitcnt vmcnt(16)", "s_barrier"]
+    L += [frag_half(B_BASE, f, 0, "%[vb]") for f in range(8)] + [frag_half(A_BASE, f, 0, "%[va]") for f in range(8)]
+    L += ["s_waitcnt lgkmcnt(0)"]
+    L += [f"s_cmp_eq_u32 s{CNT}, 0", "s_cbranch_scc1 2f", "1:"]
+    L += body_kh(True, True, True)
+    L += [f"s_sub_u32 s{CNT}, s{CNT}, 1", f"s_cmp_eq_u32 s{CNT}, 0", "s_cbranch_scc0 1b", "2:"]
+    L += body_kh(False, True, True)
+    L += body_kh(False, False, False)
+    L += ["s_nop 7", "s_nop 7", "s_nop 7", f"s_mov_b32 m0, s{M0_KEEP}"]
+    return L
 
 
 def setup(k_tiles_skipped: int, amn: bool = False, bmn: bool = False, mn8: bool = False):
@@ -301,15 +403,177 @@ def main_loop(bf16: bool = False, amn: bool = False, bmn: bool = False, probe: s
     return L
 
 
+# ---------------------------------------------------------------------------------------------------- 8-wave loop
+# Two waves per SIMD (512-thread workgroup): wave (wm, wn), wm = 0..3, owns a 64 x 128 block = 4 x 8 accumulator
+# blocks (a[0:127]); fragments A0-3 in v[32:63], B0-7 in v[64:127] (256 registers per lane: AGPRs + VGPRs). The K-loop
+# has the 4-wave loop's shape (same LDS image, 3 barriers per K-tile, quadrant order A0-1 x B0-3 | A0-1 x B4-7 |
+# A2-3 x B0-3 | A2-3 x B4-7 with the next fragments read into the dead registers), but each wave issues half the
+# MFMAs and half the LDS-DMA (4 A + 4 B per K-tile): the 4-wave probes (tools/bench_gemm_probe.py) put ~15 % of the
+# loop in DMA issue, which a second wave on the SIMD can cover with its MFMAs.
+# A fragment i of lane (r, g) = slab row 8 (r >> 1) + (r & 1) + 2 i: lanes r, r ^ 1 share a chunk 128 B apart and the
+# 16-lane ds_read_b128 groups land on 16 distinct 16-B bank slots.
+A8_BASE, B8_BASE = 32, 64
+CHUNK8_STEP = 8 * 1056  # m0 advance per DMA instruction (8 waves x one chunk)
+
+
+def w8_a(i):
+    return f"v[{A8_BASE + 8 * i}:{A8_BASE + 8 * i + 7}]"
+
+
+def w8_b(j):
+    return f"v[{B8_BASE + 8 * j}:{B8_BASE + 8 * j + 7}]"
+
+
+def w8_mfma(i, j):
+    return f"v_mfma_f32_16x16x128_f8f6f4 {acc(i, j)}, {w8_a(i)}, {w8_b(j)}, {acc(i, j)} cbsz:%c[fa] blgp:%c[fb]"
+
+
+def w8_mfma_bf16(i, j, half):
+    a0, b0 = A8_BASE + 8 * i + 4 * half, B8_BASE + 8 * j + 4 * half
+    return f"v_mfma_f32_16x16x32_bf16 {acc(i, j)}, v[{a0}:{a0 + 3}], v[{b0}:{b0 + 3}], {acc(i, j)}"
+
+
+def w8_afrag(i):
+    d = A8_BASE + 8 * i
+    return [f"ds_read_b128 v[{d}:{d + 3}], %[va] offset:{256 * i}", f"ds_read_b128 v[{d + 4}:{d + 7}], %[va] offset:{256 * i + 64}"]
+
+
+def w8_bfrag(j):
+    d = B8_BASE + 8 * j
+    return [f"ds_read_b128 v[{d}:{d + 3}], %[vb] offset:{128 * j}", f"ds_read_b128 v[{d + 4}:{d + 7}], %[vb] offset:{128 * j + 64}"]
+
+
+def w8_dma(op, n):
+    srd = SRD_A if op == "A" else SRD_B
+    so = "0" if n == 0 else f"s{SOFF + n - 1}"
+    out = [f"buffer_load_dwordx4 %[voff], s[{srd}:{srd + 3}], {so} offen lds"]
+    if n < 3:
+        out.append(f"s_add_u32 m0, m0, {CHUNK8_STEP}")
+    return out
+
+
+def w8_body(dma_on: bool, wait_next: bool, read_next: bool, bf16: bool):
+    slots = {k: [] for k in range(32)}
+    order = ([(i, j) for i in range(2) for j in range(4)] + [(i, j) for i in range(2) for j in range(4, 8)]
+             + [(i, j) for i in range(2, 4) for j in range(4)] + [(i, j) for i in range(2, 4) for j in range(4, 8)])
+    for f in range(4):  # Q1: B4-7 of t
+        slots[f] += w8_bfrag(4 + f)
+    if dma_on:
+        slots[4] += [f"s_mov_b32 m0, s{M0_B}"]
+    slots[4] += ["s_waitcnt lgkmcnt(0)"]
+    slots[5] += ["s_barrier"]  # every wave holds all of B(t): B(t+2) may overwrite the buffer
+    if dma_on:
+        for n in range(4):
+            slots[6 + n] += w8_dma("B", n)
+    slots[10] += w8_afrag(2)  # Q2: A2-3 of t
+    slots[11] += w8_afrag(3)
+    if dma_on:
+        slots[12] += advance_srd("B")
+    slots[13] += ["s_waitcnt lgkmcnt(0)"]
+    slots[14] += ["s_barrier"]  # every wave holds all of A(t)
+    if dma_on:
+        slots[15] += [f"s_mov_b32 m0, s{M0_A}"]
+        for n in range(4):
+            slots[16 + n] += w8_dma("A", n)
+        slots[20] += advance_srd("A")
+    if wait_next:
+        slots[22] += ["s_waitcnt vmcnt(8)" if dma_on else "s_waitcnt vmcnt(0)"]
+        slots[23] += ["s_barrier"]  # K-tile t+1 landed for every wave
+    if read_next:  # Q4: B0-3 and A0-1 of t+1 from the other buffer
+        slots[24] += ["v_xor_b32 %[va], %[vax], %[va]", "v_xor_b32 %[vb], %[vbx], %[vb]"]
+        for f in range(4):
+            slots[24 + f] += w8_bfrag(f)
+        slots[28] += w8_afrag(0)
+        slots[29] += w8_afrag(1)
+    if dma_on:
+        slots[30] += [f"s_xor_b32 s{M0_A}, s{M0_A}, s{M0_X}", f"s_xor_b32 s{M0_B}, s{M0_B}, s{M0_XB}"]
+    if read_next:
+        slots[31] += ["s_waitcnt lgkmcnt(0)"]
+    lines = []
+    if not bf16:
+        for k, (i, j) in enumerate(order):
+            lines.append(w8_mfma(i, j))
+            lines += slots[k]
+        return lines
+    for c in range(0, 32, 4):
+        for k in range(c, c + 4):
+            lines.append(w8_mfma_bf16(*order[k], 0))
+            lines += slots[k]
+        for k in range(c, c + 4):
+            lines.append(w8_mfma_bf16(*order[k], 1))
+    return lines
+
+
+def w8_setup(k_tiles_skipped: int):
+    L = [f"s_mov_b32 s{M0_KEEP}, m0",
+         f"s_mov_b64 s[{SRD_A}:{SRD_A + 1}], %[pa]", f"s_mov_b32 s{SRD_A + 2}, -1", f"s_mov_b32 s{SRD_A + 3}, 0x20000",
+         f"s_mov_b64 s[{SRD_B}:{SRD_B + 1}], %[pb]", f"s_mov_b32 s{SRD_B + 2}, -1", f"s_mov_b32 s{SRD_B + 3}, 0x20000",
+         f"s_mov_b32 s{SOFF}, %[stride]", f"s_add_u32 s{SOFF + 1}, s{SOFF}, %[stride]", f"s_add_u32 s{SOFF + 2}, s{SOFF + 1}, %[stride]"]
+    for _ in range(k_tiles_skipped):
+        L += advance_srd("A") + advance_srd("B")
+    L += [f"s_mov_b32 s{M0_A}, %[m0a]", f"s_add_u32 s{M0_B}, %[m0a], 33792",
+          f"s_add_u32 s{M0_X}, %[m0a], 67584", f"s_xor_b32 s{M0_X}, s{M0_X}, %[m0a]",
+          f"s_add_u32 s{M0_XB}, s{M0_B}, 67584", f"s_xor_b32 s{M0_XB}, s{M0_XB}, s{M0_B}"]
+    return L
+
+
+def w8_issue():
+    L = w8_setup(0)
+    for tile in range(2):
+        L += [f"s_mov_b32 m0, s{M0_B}", "s_nop 0"]
+        for n in range(4):
+            L += w8_dma("B", n)
+        L += [f"s_mov_b32 m0, s{M0_A}", "s_nop 0"]
+        for n in range(4):
+            L += w8_dma("A", n)
+        if tile == 0:
+            L += advance_srd("A") + advance_srd("B")
+            L += [f"s_xor_b32 s{M0_A}, s{M0_A}, s{M0_X}", f"s_xor_b32 s{M0_B}, s{M0_B}, s{M0_XB}"]
+    L.append(f"s_mov_b32 m0, s{M0_KEEP}")
+    return L
+
+
+def w8_main_loop(bf16: bool):
+    L = w8_setup(2)
+    L.append(f"s_mov_b32 s{CNT}, %[cnt]")
+    for a in range(128):
+        L.append(f"v_accvgpr_write_b32 a{a}, 0")
+    L += ["s_waitcnt vmcnt(8)", "s_barrier"]
+    for f in range(4):
+        L += w8_bfrag(f)
+    L += w8_afrag(0) + w8_afrag(1)
+    L += ["s_waitcnt lgkmcnt(0)"]
+    L += [f"s_cmp_eq_u32 s{CNT}, 0", "s_cbranch_scc1 2f", "1:"]
+    L += w8_body(True, True, True, bf16)
+    L += [f"s_sub_u32 s{CNT}, s{CNT}, 1", f"s_cmp_eq_u32 s{CNT}, 0", "s_cbranch_scc0 1b", "2:"]
+    L += w8_body(False, True, True, bf16)
+    L += w8_body(False, False, False, bf16)
+    L += ["s_nop 7", "s_nop 7", "s_nop 7", f"s_mov_b32 m0, s{M0_KEEP}"]
+    return L
+
+
 def generate() -> str:
     I, L, LB = issue(), main_loop(), main_loop(bf16=True)
     IT, LT = issue(amn=True), main_loop(bf16=True, amn=True)
     IBT, LBT = issue(amn=True, bmn=True), main_loop(bf16=True, amn=True, bmn=True)
     probes = [(f"BF16ASM_PROBE_{k.upper()}_LOOP", main_loop(bf16=True, probe=k)) for k in ("nodma", "noread", "mfma")]
+    for k in ("regload", "regstage"):
+        PROBE_LOADS[0] = k
+        probes.append((f"BF16ASM_PROBE_{k.upper()}_LOOP", main_loop(bf16=True)))
+        PROBE_LOADS[0] = None
+    SPREAD[0] = True
+    probes.append(("BF16ASM_SPREAD_MAIN_LOOP", main_loop(bf16=True)))
+    SPREAD[0] = False
+    probes.append(("BF16ASM_KH_MAIN_LOOP", main_loop_kh()))
+    assert sum(1 for x in probes[-1][1] if x.startswith("v_mfma")) == 3 * 128
+    assert sum(1 for x in probes[-1][1] if x.startswith("v_mfma")) == 3 * 128
     f8mn = [("FP8AMN_ISSUE", issue(amn=True, mn8=True)), ("FP8AMN_MAIN_LOOP", main_loop(amn=True, mn8=True)),
             ("FP8ABMN_ISSUE", issue(amn=True, bmn=True, mn8=True)),
             ("FP8ABMN_MAIN_LOOP", main_loop(amn=True, bmn=True, mn8=True))]
     assert sum(1 for x in f8mn[3][1] if x.startswith("ds_read_b64_tr_b8")) == 2 * (16 + 32 + 32 + 16)
+    w8 = [("W8_ISSUE", w8_issue()), ("W8_BF16_MAIN_LOOP", w8_main_loop(True)), ("W8_FP8_MAIN_LOOP", w8_main_loop(False))]
+    assert sum(1 for x in w8[1][1] if x.startswith("v_mfma")) == 3 * 64
+    assert sum(1 for x in w8[2][1] if x.startswith("v_mfma")) == 3 * 32
     assert sum(1 for x in LBT if x.startswith("ds_read_b64_tr_b16")) == 2 * (16 + 32 + 32 + 16)
     n_mfma = sum(1 for x in L if x.startswith("v_mfma"))
     assert n_mfma == 3 * 64, n_mfma
@@ -323,7 +587,7 @@ def generate() -> str:
            "#pragma once"]
     for name, lines in (("FP8ASM_ISSUE", I), ("FP8ASM_MAIN_LOOP", L), ("BF16ASM_MAIN_LOOP", LB),
                         ("BF16AMN_ISSUE", IT), ("BF16AMN_MAIN_LOOP", LT),
-                        ("BF16ABMN_ISSUE", IBT), ("BF16ABMN_MAIN_LOOP", LBT)) + tuple(probes) + tuple(f8mn):
+                        ("BF16ABMN_ISSUE", IBT), ("BF16ABMN_MAIN_LOOP", LBT)) + tuple(probes) + tuple(f8mn) + tuple(w8):
         out.append(f"#define {name} \\")
         for x in lines:
             out.append(f'  "{x}\\n" \\')
@@ -332,6 +596,8 @@ def generate() -> str:
     out.append(f"#define FP8ASM_SGPR_CLOBBERS " + ", ".join(f'"s{s}"' for s in range(SRD_A, M0_KEEP + 1)))
     out.append(f"#define BF16AMN_SGPR_CLOBBERS " + ", ".join(f'"s{s}"' for s in range(SRD_A, ADV_A + 1)))
     out.append(f"#define BF16ABMN_SGPR_CLOBBERS " + ", ".join(f'"s{s}"' for s in range(SRD_A, ADV_B + 1)))
+    out.append(f"#define W8_VCLOBBERS " + ", ".join(f'"v{v}"' for v in range(A8_BASE, 128)))
+    out.append(f"#define W8_ACLOBBERS " + ", ".join(f'"a{a}"' for a in range(128)))
     out.append("")
     return "\n".join(out)
 

@@ -127,7 +127,12 @@ for step in "$@"; do
     asmdiag) run asmdiag 120 python tools/debug/fp8asm_diag.py ;;
     gemm_grp) run gemm_grp 400 python tools/bench_gemm.py --variants ${GEMM_VARIANTS:-bl,18,18g1,18g2,18g8,18g16} --no-bf16 --no-scaled-mm --rounds 3 ;;
     gprobe) run gprobe 300 python tools/bench_gemm_probe.py ;;
+    g8test) run g8test 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "gemm8" ;;
     trprobe) run trprobe 60 tools/microbench/tr_probe ;;
+    f8mn) run ktest_f8mn 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "fp8_asm_amn" ;;
+    f8tests) run f8tests 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "fp8" ;;
+    bench20_fp8_nomn) ACCELERATE_FP8_MN=0 run bench20_fp8_nomn 600 python bench.py --gpus 1 --steps 20 --warmup 5 --precision fp8 ;;
+    bench20_fp8_b) run bench20_fp8_b 600 python bench.py --gpus 1 --steps 20 --warmup 5 --precision fp8 ;;
     amn) run ktest_amn 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "bf16_asm" && \
          run gemm_amn 400 python tools/bench_gemm_amn.py ;;
     gemm_bf16) run ktest_bf16asm 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "bf16_asm" && \
