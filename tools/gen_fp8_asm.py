@@ -220,6 +220,26 @@ def body(dma_on: bool, wait_next: bool, read_next: bool, bf16: bool = False, amn
     if read_next:
         slots[61] += ["s_waitcnt lgkmcnt(0)"]
     lines = []
+    if not bf16 and SPREAD[0]:
+        # fp8: the same evenly spread single operations over each quadrant's 16 MFMA gaps
+        for q in range(4):
+            ops = []
+            for k in range(16 * q, 16 * q + 16):
+                cur = []
+                for ins in slots[k]:
+                    cur.append(ins)
+                    if not ins.startswith(("s_mov_b32 m0", "s_add_u32 s", "s_addc_u32", "s_xor_b32", "v_xor_b32")):
+                        ops.append(cur)
+                        cur = []
+                if cur:
+                    ops.append(cur)
+            pos = {}
+            for n, op in enumerate(ops):
+                pos.setdefault(min(15, (n * 16) // max(1, len(ops))), []).extend(op)
+            for g, (i, j) in enumerate(order[16 * q : 16 * q + 16]):
+                lines.append(mfma(i, j))
+                lines += pos.get(g, [])
+        return lines
     if not bf16:
         for k, (i, j) in enumerate(order):
             lines.append(mfma(i, j))
@@ -229,6 +249,7 @@ def body(dma_on: bool, wait_next: bool, read_next: bool, bf16: bool = False, amn
         # bf16, hipBLASLt-like issue order: per quadrant (16 blocks) the 16 first-half MFMAs, then the 16 second halves
         # (a block's two MFMAs 16 apart); the quadrant's slot work is cut into single memory / wait / barrier
         # operations (each with the scalar ops that feed it) and laid out evenly over its 32 MFMA gaps, in order.
+        # +2.3-3.6 % over the run-of-four order on the 4-wave kernel (profiles/r6_gemm_diagnostics.md).
         for q in range(4):
             ops = []
             for k in range(16 * q, 16 * q + 16):
@@ -554,8 +575,11 @@ def w8_main_loop(bf16: bool):
 
 def generate() -> str:
     I, L, LB = issue(), main_loop(), main_loop(bf16=True)
+    SPREAD[0] = True  # the MN-major bf16 loops (weight gradients, default) in the spread issue order
     IT, LT = issue(amn=True), main_loop(bf16=True, amn=True)
     IBT, LBT = issue(amn=True, bmn=True), main_loop(bf16=True, amn=True, bmn=True)
+    LS8 = main_loop(bf16=False, probe="")  # fp8 K-major loop, spread order (FP8ASM_SPREAD_MAIN_LOOP)
+    SPREAD[0] = False
     probes = [(f"BF16ASM_PROBE_{k.upper()}_LOOP", main_loop(bf16=True, probe=k)) for k in ("nodma", "noread", "mfma")]
     for k in ("regload", "regstage"):
         PROBE_LOADS[0] = k
@@ -585,7 +609,7 @@ def generate() -> str:
            f"// FP8ASM_ISSUE {len(I)} lines; FP8ASM_MAIN_LOOP {len(L)} lines, {n_mfma} MFMAs (loop body 64);",
            f"// BF16ASM_MAIN_LOOP {len(LB)} lines (loop body 128 MFMAs); BF16AMN_* (MN-major A): {len(IT)} / {len(LT)} lines.",
            "#pragma once"]
-    for name, lines in (("FP8ASM_ISSUE", I), ("FP8ASM_MAIN_LOOP", L), ("BF16ASM_MAIN_LOOP", LB),
+    for name, lines in (("FP8ASM_ISSUE", I), ("FP8ASM_MAIN_LOOP", L), ("FP8ASM_SPREAD_MAIN_LOOP", LS8), ("BF16ASM_MAIN_LOOP", LB),
                         ("BF16AMN_ISSUE", IT), ("BF16AMN_MAIN_LOOP", LT),
                         ("BF16ABMN_ISSUE", IBT), ("BF16ABMN_MAIN_LOOP", LBT)) + tuple(probes) + tuple(f8mn) + tuple(w8):
         out.append(f"#define {name} \\")

@@ -35,6 +35,8 @@ for step in "$@"; do
     bench20_asm) ACCELERATE_ASM_BF16_GEMM=1 run bench20_asm 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench20_abmn) ACCELERATE_ASM_WGRAD_ABMN=1 run bench20_abmn 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench20_abmn_b) ACCELERATE_ASM_WGRAD_ABMN=1 run bench20_abmn_b 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    bench20_dgamn) ACCELERATE_ASM_DGRAD_AMN=1 run bench20_dgamn 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    bench20_dgamn_b) ACCELERATE_ASM_DGRAD_AMN=1 run bench20_dgamn_b 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench20_noamn) ACCELERATE_ASM_WGRAD_AMN=0 run bench20_noamn 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench20_b) run bench20_b 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench20_noamn_b) ACCELERATE_ASM_WGRAD_AMN=0 run bench20_noamn_b 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
@@ -132,6 +134,9 @@ for step in "$@"; do
     f8mn) run ktest_f8mn 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "fp8_asm_amn" ;;
     f8tests) run f8tests 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "fp8" ;;
     bench20_fp8_nomn) ACCELERATE_FP8_MN=0 run bench20_fp8_nomn 600 python bench.py --gpus 1 --steps 20 --warmup 5 --precision fp8 ;;
+    f8tests_spread) ACCELERATE_FP8ASM_SPREAD=1 run f8tests_spread 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "fp8" ;;
+    bench20_fp8_spread) ACCELERATE_FP8ASM_SPREAD=1 run bench20_fp8_spread 600 python bench.py --gpus 1 --steps 20 --warmup 5 --precision fp8 ;;
+    gemm_fp8_spread) ACCELERATE_FP8ASM_SPREAD=1 run gemm_fp8_spread 400 python tools/bench_gemm.py --variants bl,18 --no-bf16 --no-scaled-mm --rounds 3 --check ;;
     bench20_fp8_b) run bench20_fp8_b 600 python bench.py --gpus 1 --steps 20 --warmup 5 --precision fp8 ;;
     amn) run ktest_amn 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "bf16_asm" && \
          run gemm_amn 400 python tools/bench_gemm_amn.py ;;
