@@ -95,6 +95,7 @@ void grouped_gemm(torch::Tensor a, torch::Tensor b, torch::Tensor out, torch::Te
 torch::Tensor batched_transpose(torch::Tensor x);
 void attn_debug_mode(int64_t mode);
 void attn_dkdv_config(int64_t waves, int64_t sched, int64_t dq_waves);
+void attn_fwd_config(int64_t w4);
 void attn_trace(torch::Tensor buf);
 // small_allreduce.hip
 std::tuple<int64_t, pybind11::bytes> sar_create(int64_t rank, int64_t world, int64_t max_bytes);
@@ -163,6 +164,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("batched_transpose", &batched_transpose);
   m.def("attn_debug_mode", &attn_debug_mode);
   m.def("attn_dkdv_config", &attn_dkdv_config);
+  m.def("attn_fwd_config", &attn_fwd_config);
   m.def("attn_trace", &attn_trace);
   m.def("sar_create", &sar_create);
   m.def("sar_open", &sar_open);

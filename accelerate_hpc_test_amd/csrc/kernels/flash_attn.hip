@@ -524,6 +524,276 @@ __global__ __launch_bounds__(256 * NH, 2 / NH) void attn_fwd_kernel(FwdParams p)
   wave_trace(p.trace, t_start, wave_id, (unsigned)qt | ((unsigned)h << 16));
 }
 
+// f(integral_constant<int, 0>) ... f(integral_constant<int, N - 1>): a loop whose index is a compile-time constant in
+// every body (register-array indices and per-step schedules), whatever the unroller decides for a body this large.
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// Forward, one wave per SIMD (ACCELERATE_ATTN_FWD_W4=1; S a multiple of 256). A workgroup is 4 waves x 64 queries of
+// one head; each wave owns the WHOLE register file: its two 32-query halves keep Q (AGPRs, pinned) and O^T (compiler
+// accumulators) for the whole sweep, S^T accumulates in VGPRs through the asm MFMAs (no v_accvgpr_read before the
+// softmax). 64-key K / V tiles arrive by LDS-DMA into two 2-deep rings (layout (a), ImgA reads). Per tile T, 16 steps of
+// 4 MFMAs, both query halves in every step so each K / V fragment read from LDS feeds two MFMAs:
+//   steps 0-7   S(T) = K(T) Q^T, both halves        finish softmax(T-1): last exps, bf16 packs, deferred O rescale
+//   steps 8-15  O^T += V(T-1)^T P(T-1)^T            start softmax(T): mask (causal band), max, rescale decision, exps
+// S is double-buffered by tile parity, so softmax(T) spans 12 MFMA steps beside both products. One barrier per tile
+// (its start: K(T), V(T-1) landed, the slots of K(T-1), V(T-2) free); the tile's LDS-DMA (K(T+1), V(T)) is one piece
+// per step in steps 0-7. The rescale of O waits for the next tile's step 0, after the P.V that used the old max.
+__device__ __forceinline__ float max3_raw(float a, float b, float c) {  // fmaxf on MFMA results adds canonicalising ops
+  float x;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(x) : "v"(a), "v"(b), "v"(c));
+  return x;
+}
+
+template <bool CAUSAL>
+__global__ __launch_bounds__(256, 1) void attn_fwd_w4_kernel(FwdParams p) {
+  constexpr int kKeys = 64, kImg = kKeys * kRow;  // 16 KB per operand image
+  __shared__ __attribute__((aligned(1024))) char k0s[kImg], k1s[kImg], v0s[kImg], v1s[kImg];
+  const long long t_start = wall_clock64();
+  const int nqt = p.S / 256;
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hf = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = xcd_head(blockIdx.x, p.Hq), b = blockIdx.z;
+  const int kh = h / (p.Hq / p.Hkv);
+  const int qt = CAUSAL ? (nqt - 1 - (int)blockIdx.y) : (int)blockIdx.y;
+  const int qw0 = qt * 256 + wave * 64;
+  ACC_CHECK_OR_RETURN(qt * 256 + 256 <= p.S && h < p.Hq && kh < p.Hkv && p.Sk % 128 == 0 &&
+                          (!CAUSAL || (qt + 1) * 256 + p.off <= p.Sk), kChkAttnTile);
+  const bf16_t* qb = p.q + b * p.q_bs + (long)h * kD;
+  const bf16_t* kb_ = p.k + b * p.k_bs + (long)kh * kD;
+  const bf16_t* vb_ = p.v + b * p.v_bs + (long)kh * kD;
+
+  v8bf qf[2][8];  // half c: query qw0 + 32 c + r, columns 16 s + 8 hf .. + 7
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+      qf[c][s] = *reinterpret_cast<const v8bf*>(qb + (long)(qw0 + 32 * c + r) * p.q_ts + 16 * s + 8 * hf);
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int s = 0; s < 8; ++s) asm volatile("" : "+a"(qf[c][s]));  // the asm S MFMAs read Q from AGPRs
+  asm volatile("s_nop 2");
+
+  f32x16 o[2][4];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int d = 0; d < 4; ++d) zero(o[c][d]);
+  // S of the tile being computed / of the tile being finished (parity buffers); "tile -1" is all -inf: its exps are 0
+  f32x16 sc[2][2][2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sc[1][c][kb][i] = -INFINITY;
+  v8bf pb[2][2][2];  // [half][kb][s2]: P(T-1), the B operands of this tile's P.V
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) { pb[c][kb][0] = v8bf{}; pb[c][kb][1] = v8bf{}; }
+  float m[2] = {-INFINITY, -INFINITY}, l[2][2] = {{0.f, 0.f}, {0.f, 0.f}}, neg_m[2] = {0.f, 0.f};
+  float alpha[2] = {1.f, 1.f}, mx[2] = {0.f, 0.f};
+  int resc[2] = {0, 0};  // wave-uniform: O of half c is rescaled by alpha at the next tile's step 0
+  const int off = p.off;
+  const int n_kt = CAUSAL ? (qt * 256 + 256 + off) / kKeys : p.Sk / kKeys;  // even: off, Sk multiples of 128
+  const int n_full = CAUSAL ? n_kt - 4 : n_kt;
+
+  TileDMA<kKeys, 4> dk, dv_;
+  const int kts = (int)(p.k_ts * 2), vts = (int)(p.v_ts * 2);
+  dk.init_a(wave, lane, kts);
+  dv_.init_a(wave, lane, vts);
+  ImgA ia;
+  ia.init(lane);
+  const auto krs = head_rsrc(kb_, p.Sk, p.k_ts), vrs = head_rsrc(vb_, p.Sk, p.v_ts);
+  dk.issue(krs, 0, kts, k0s);
+#pragma unroll
+  for (int i = 0; i < kImg / (256 * 16); ++i)  // V(-1): finite zeros under P(-1) = 0
+    *reinterpret_cast<uint4*>(v1s + 16 * (tid + 256 * i)) = make_uint4(0, 0, 0, 0);
+
+  v8bf ka[2][2], va[2][2];  // K fragments (kb 0 / 1) and V^T fragments (d, d + 1) of this step / the next
+  auto k_read = [&](const char* img, int s, v8bf(&x)[2]) __attribute__((always_inline)) {
+    x[0] = ia.row(img, 0, s);
+    x[1] = ia.row(img, 32, s);
+  };
+  // P.V step j: keys 32 kb + 16 s2 .. + 15 with (kb, s2) = (j >> 2, (j >> 1) & 1), d-blocks 2 (j & 1), + 1
+  auto v_read = [&](const char* img, int j, v8bf(&x)[2]) __attribute__((always_inline)) {
+    const int rb = 16 * (j >> 1), d0 = 2 * (j & 1);
+    x[0] = ia.tr(img, rb, d0);
+    x[1] = ia.tr(img, rb, d0 + 1);
+  };
+  auto s_step = [&](auto par_c, int s, const v8bf(&x)[2]) __attribute__((always_inline)) {
+    constexpr int P = decltype(par_c)::value;
+    if (s == 0) {
+      mfma_vacc<3>(sc[P][0][0], x[0], qf[0][0]);
+      mfma_vacc<3>(sc[P][0][1], x[1], qf[0][0]);
+      mfma_vacc<3>(sc[P][1][0], x[0], qf[1][0]);
+      mfma_vacc<3>(sc[P][1][1], x[1], qf[1][0]);
+    } else {
+      mfma_vacc<0>(sc[P][0][0], x[0], qf[0][s]);
+      mfma_vacc<0>(sc[P][0][1], x[1], qf[0][s]);
+      mfma_vacc<0>(sc[P][1][0], x[0], qf[1][s]);
+      if (s == 7) mfma_vacc<2>(sc[P][1][1], x[1], qf[1][s]);  // the softmax VALU reads all four chains next
+      else mfma_vacc<0>(sc[P][1][1], x[1], qf[1][s]);
+    }
+  };
+  auto pv_step = [&](int j, const v8bf(&x)[2]) __attribute__((always_inline)) {
+    const int kb = j >> 2, s2 = (j >> 1) & 1, d0 = 2 * (j & 1);
+    o[0][d0] = mfma(x[0], pb[0][kb][s2], o[0][d0]);
+    o[1][d0] = mfma(x[0], pb[1][kb][s2], o[1][d0]);
+    o[0][d0 + 1] = mfma(x[1], pb[0][kb][s2], o[0][d0 + 1]);
+    o[1][d0 + 1] = mfma(x[1], pb[1][kb][s2], o[1][d0 + 1]);
+  };
+  // the 64 scores of a tile, element e = 32 c + 16 kb + i; exp slot u = 0..11 takes [16 u / 3, 16 (u + 1) / 3)
+  auto exps = [&](auto par_c, int u) __attribute__((always_inline)) {
+    constexpr int P = decltype(par_c)::value;
+    const int lo = 16 * u / 3, hi = 16 * (u + 1) / 3;
+    static_for<64>([&](auto ec) __attribute__((always_inline)) {
+      constexpr int e = decltype(ec)::value, c = e >> 5, kb = (e >> 4) & 1, i = e & 15;
+      if (e < lo || e >= hi) return;
+      const float pv = fast_exp2(fmaf(sc[P][c][kb][i], p.scale_log2, neg_m[c]));
+      sc[P][c][kb][i] = pv;
+      l[c][i & 1] += pv;
+    });
+  };
+  // bf16 packs of group g (8 elements: half g >> 2, kb (g >> 1) & 1, s2 g & 1) at step pack_step(g) of the next tile
+  auto packs = [&](auto par_c, int t) __attribute__((always_inline)) {
+    constexpr int P = decltype(par_c)::value;
+    static_for<8>([&](auto gc) __attribute__((always_inline)) {
+      constexpr int g = decltype(gc)::value, c = g >> 2, kb = (g >> 1) & 1, s2 = g & 1;
+      constexpr int done_u = (3 * (8 * g + 7)) / 16;  // the exp slot of the group's last element
+      constexpr int step = done_u <= 5 ? g / 2 : done_u - 6 + 1;
+      if (t == step) pb[c][kb][s2] = pack8(sc[P][c][kb], s2);
+    });
+  };
+  auto max_half = [&](auto par_c, int c) __attribute__((always_inline)) {
+    constexpr int P = decltype(par_c)::value;
+    const f32x16 &x0 = sc[P][c][0], &x1 = sc[P][c][1];
+    float a = max3_raw(x0[0], x0[1], x0[2]), bb = max3_raw(x1[0], x1[1], x1[2]);
+#pragma unroll
+    for (int i = 3; i < 15; i += 2) {
+      a = max3_raw(a, x0[i], x0[i + 1]);
+      bb = max3_raw(bb, x1[i], x1[i + 1]);
+    }
+    mx[c] = max3_raw(a, bb, fmaxf(x0[15], x1[15]));
+  };
+
+  // one tile: MODE 0 plain, 1 causal band (masked), 2 the P.V of the last tile only; P = T & 1 (S buffer parity);
+  // kc: K(T), kn: K(T + 1)'s slot, vp: V(T - 1), vc: V(T)'s slot
+  auto tile = [&](auto mode_c, auto par_c, int T, const char* kc, char* kn, const char* vp, char* vc)
+                  __attribute__((always_inline)) {
+    constexpr int MODE = decltype(mode_c)::value, P = decltype(par_c)::value;
+    constexpr auto PREV = std::integral_constant<int, 1 - P>{};
+    static_for<16>([&](auto tc) __attribute__((always_inline)) {
+      constexpr int t = decltype(tc)::value;
+      __builtin_amdgcn_sched_barrier(0);
+      if (t == 0) {
+        wait_dma_and_sync();
+        if (MODE != 2) k_read(kc, 0, ka[0]);
+      }
+      // next step's fragments (K(T) for steps 1-7, V(T-1)^T for steps 8-15; step 0's come after the next barrier)
+      if (t < 7) { if (MODE != 2) k_read(kc, t + 1, ka[(t + 1) & 1]); }
+      else if (t < 15) v_read(vp, t + 1 - 8, va[(t + 1) & 1]);
+      if (MODE != 2 && t < 4 && T + 1 < n_kt) dk.issue_piece(krs, (T + 1) * kKeys, kts, kn, t);
+      if (MODE != 2 && t >= 4 && t < 8) dv_.issue_piece(vrs, T * kKeys, vts, vc, t - 4);
+      if (t < 8) {
+        if (t == 0) {  // the deferred O rescale decided in softmax(T-1), after the P.V that used the old max
+#pragma unroll
+          for (int c = 0; c < 2; ++c)
+            if (resc[c]) {
+#pragma unroll
+              for (int d = 0; d < 4; ++d)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) o[c][d][i] *= alpha[c];
+            }
+        }
+        if (t < 6) exps(PREV, t + 6);
+        packs(PREV, t);
+        if (MODE != 2) s_step(par_c, t, ka[t & 1]);
+      } else {
+        pv_step(t - 8, va[t & 1]);
+        if (MODE != 2) {
+          if (t == 8) {
+            if (MODE == 1) {  // causal band: key 64 T + 32 kb + row visible to query qw0 + 32 c + r iff <= it + off
+#pragma unroll
+              for (int c = 0; c < 2; ++c) {
+                const int lim = qw0 + 32 * c + r + off - T * kKeys;
+#pragma unroll
+                for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                  for (int i = 0; i < 16; ++i)
+                    if (32 * kb + acc_row(i, hf) > lim) sc[P][c][kb][i] = -INFINITY;
+              }
+            }
+            max_half(par_c, 0);
+          }
+          if (t == 9) {
+            max_half(par_c, 1);
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+              const float mm = fmaxf(mx[c], __shfl_xor(mx[c], 32, 64));
+              const float m_cand = mm * p.scale_log2;
+              resc[c] = __any(m_cand > m[c] + kRescaleLog2);
+              if (resc[c]) {
+                const float m_new = fmaxf(m[c], m_cand);
+                alpha[c] = fast_exp2(m[c] - m_new);
+                l[c][0] *= alpha[c];
+                l[c][1] *= alpha[c];
+                m[c] = m_new;
+              }
+              neg_m[c] = -m[c];
+            }
+          }
+          if (t >= 10) exps(par_c, t - 10);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  };
+  using Z = std::integral_constant<int, 0>;
+  using O1 = std::integral_constant<int, 1>;
+  using TW = std::integral_constant<int, 2>;
+  int T = 0;
+  for (; T < n_full; T += 2) {
+    tile(Z{}, Z{}, T, k0s, k1s, v1s, v0s);
+    tile(Z{}, O1{}, T + 1, k1s, k0s, v0s, v1s);
+  }
+  if (CAUSAL) {
+    for (; T < n_kt; T += 2) {
+      tile(O1{}, Z{}, T, k0s, k1s, v1s, v0s);
+      tile(O1{}, O1{}, T + 1, k1s, k0s, v0s, v1s);
+    }
+  }
+  tile(TW{}, Z{}, n_kt, k0s, k1s, v1s, v0s);  // P.V of the last tile (odd index: V in v1s)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    float lc = l[c][0] + l[c][1];
+    lc += __shfl_xor(lc, 32, 64);
+    const float inv = 1.f / lc;
+    const int q = qw0 + 32 * c + r;
+    bf16_t* ob = p.o + b * p.o_bs + (long)h * kD + (long)q * p.o_ts;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 w;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) w.v[t] = f2bf(o[c][d][4 * g + t] * inv);
+        *reinterpret_cast<bf16x4*>(ob + d * 32 + 8 * g + 4 * hf) = w;
+      }
+    if (hf == 0) p.lse[((long)b * p.Hq + h) * p.S + q] = (m[c] + __builtin_amdgcn_logf(lc)) * kLn2;
+  }
+  wave_trace(p.trace, t_start, wave, (unsigned)qt | ((unsigned)h << 16));
+}
+
 // The dK / dV kernel's row constants, both pre-negated so they seed its S and dP accumulators as loaded (no VALU):
 // ndelta[b, h, s] = -sum_d dO * O (fp32) and nlse[b, h, s] = -lse / scale. One wave per (b, s, h). (The dQ kernel
 // writes the same two buffers itself on the normal path; this kernel serves the diagnostic variants.)
@@ -1402,6 +1672,8 @@ void check_qkv(const torch::Tensor& t, const char* name) {
 
 // Explicit instantiations: hipcc emits the host launch stub of only the first instantiation a launch chain names for
 // kernels with function-scope static LDS; naming every variant here makes each stub definite.
+template __global__ void attn_fwd_w4_kernel<true>(FwdParams);
+template __global__ void attn_fwd_w4_kernel<false>(FwdParams);
 template __global__ void attn_fwd_kernel<true, 1>(FwdParams);
 template __global__ void attn_fwd_kernel<false, 1>(FwdParams);
 template __global__ void attn_fwd_kernel<true, 2>(FwdParams);
@@ -1448,6 +1720,9 @@ static int env_int(const char* name, int dflt) { const char* e = std::getenv(nam
 static int g_dkdv_waves = env_int("ACCELERATE_ATTN_DKDV", 4);
 static int g_dkdv_sched = env_int("ACCELERATE_ATTN_DKDV_SCHED", 6);
 static int g_dq_waves = env_int("ACCELERATE_ATTN_DQ_W4", 0) ? 4 : 8;  // dQ: 4 = attn_bwd_dq_w4_kernel, 8 = 8-wave
+// forward kernel choice: 1 = attn_fwd_w4_kernel where S % 256 == 0, 0 = the 8-wave kernel (ACCELERATE_ATTN_FWD_W4)
+static int g_fwd_w4 = env_int("ACCELERATE_ATTN_FWD_W4", 0);
+void attn_fwd_config(int64_t w4) { g_fwd_w4 = (int)w4; }
 void attn_dkdv_config(int64_t waves, int64_t sched, int64_t dq_waves) {
   TORCH_CHECK((waves == 4 && ((sched >= 0 && sched <= 3) || sched == 6)) || waves == 8,
               "attn_dkdv_config: waves 4 (sched 0-3, 6) or 8");
@@ -1500,9 +1775,18 @@ std::vector<torch::Tensor> flash_attn_fwd(torch::Tensor q, torch::Tensor k, torc
   // key-tile width of the two-head kernel (ACCELERATE_ATTN_FWD_KEYS=64: the 64-key tiles; 128-key tiles measured
   // 0.639 vs 0.667 ms causal, 0.989 vs 1.001 ms full at S = 8192, 32 / 8 heads, profiles/r4_attention.md)
   static const int fwd_keys = [] { const char* e = std::getenv("ACCELERATE_ATTN_FWD_KEYS"); return e ? std::atoi(e) : 128; }();
+  // one wave per SIMD, 64 queries per wave (attn_fwd_w4_kernel; ACCELERATE_ATTN_FWD_W4=1 / attn_fwd_config), S a
+  // multiple of 256
+  auto stream = at::hip::getCurrentHIPStream();
+  if (g_fwd_w4 && S % 256 == 0) {
+    dim3 g4(Hq, S / 256, B);
+    p.trace = trace_for(g4);
+    if (causal) hipLaunchKernelGGL((attn_fwd_w4_kernel<true>), g4, dim3(256), 0, stream, p);
+    else hipLaunchKernelGGL((attn_fwd_w4_kernel<false>), g4, dim3(256), 0, stream, p);
+    return {o, lse};
+  }
   dim3 grid(Hq / nh, S / 128, B);
   p.trace = trace_for(grid);
-  auto stream = at::hip::getCurrentHIPStream();
   if (nh == 2 && fwd_keys == 128) {
     if (causal) hipLaunchKernelGGL((attn_fwd_kernel<true, 2, 4>), grid, dim3(512), 0, stream, p);
     else hipLaunchKernelGGL((attn_fwd_kernel<false, 2, 4>), grid, dim3(512), 0, stream, p);

@@ -172,6 +172,34 @@ def test_flash_attention_kv_prefix(causal, Sq, Sk):
         assert _rel(a, b) < 3e-2, (name, _rel(a, b))
 
 
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("B,S,Sk,Hq,Hkv", [(1, 256, 256, 4, 2), (2, 512, 512, 8, 2), (1, 2048, 2048, 32, 8),
+                                            (1, 8192, 8192, 32, 8), (1, 256, 640, 8, 2), (1, 512, 3072, 8, 2)])
+def test_flash_attention_fwd_w4_matches_fp32(causal, B, S, Sk, Hq, Hkv):
+    """The one-wave-per-SIMD forward (attn_fwd_w4_kernel, switched on with attn_fwd_config(1)): O and LSE against the
+    fp32 reference, including more keys than queries (bottom-right causal band) and the headline shape; and O / LSE
+    against the 8-wave kernel on the same inputs."""
+    torch.manual_seed(0)
+    D = 128
+    q = torch.randn(B, S, Hq, D, device=DEV, dtype=torch.bfloat16)
+    k = torch.randn(B, Sk, Hkv, D, device=DEV, dtype=torch.bfloat16)
+    v = torch.randn(B, Sk, Hkv, D, device=DEV, dtype=torch.bfloat16)
+    scale = 1 / math.sqrt(D)
+    e = _ext.ext()
+    try:
+        e.attn_fwd_config(1)
+        o, lse = e.flash_attn_fwd(q, k, v, scale, causal)
+    finally:
+        e.attn_fwd_config(0)
+    o8, lse8 = e.flash_attn_fwd(q, k, v, scale, causal)
+    o2, lse2 = _prefix_attn_ref(q, k, v, causal, scale)
+    assert torch.isfinite(o).all() and torch.isfinite(lse).all()
+    assert _rel(o, o2) < 2e-2, _rel(o, o2)
+    assert torch.allclose(lse, lse2, atol=2e-2, rtol=1e-3)
+    assert _rel(o, o8) < 1e-2 and torch.allclose(lse, lse8, atol=1e-3, rtol=1e-4)
+    torch.cuda.empty_cache()
+
+
 def test_flash_attention_lse():
     torch.manual_seed(0)
     B, S, H, D = 1, 256, 2, 128

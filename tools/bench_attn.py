@@ -21,6 +21,8 @@ p.add_argument("--dbg", action="store_true", help="also time the causal backward
 p.add_argument("--dkdv-variants", default="", help="comma list of dq_waves:dkdv_waves:sched backward kernel choices "
                "(e.g. 8:8:0,4:4:2) timed in interleaved rounds in this process: causal / full backward and the causal "
                "dK/dV and dQ kernels alone")
+p.add_argument("--fwd-variants", default="", help="comma list of forward kernels (0 = 8-wave, 1 = one wave per SIMD, "
+               "attn_fwd_config) timed in interleaved rounds in this process, causal and full")
 p.add_argument("--rounds", type=int, default=3)
 a = p.parse_args()
 e = _ext.ext()
@@ -96,6 +98,26 @@ if a.dkdv_variants:
                 row[name] = round(min(row.get(name, 1e9), t), 4)
     e.attn_dkdv_config(4, 6, 8)
     res["dkdv_variants"] = best
+if a.fwd_variants:
+    fv = {}
+    for _ in range(a.rounds):
+        for w in (int(x) for x in a.fwd_variants.split(",")):
+            e.attn_fwd_config(w)
+            for causal in (True, False):
+                f = 0.5 if causal else 1.0
+                fn = lambda: e.flash_attn_fwd(q, k, v, scale, causal)
+                fn(); torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.iters): fn()
+                e1.record(); e1.synchronize()
+                ms = e0.elapsed_time(e1) / a.iters
+                row = fv.setdefault(f"w4={w}", {})
+                key = "causal_fwd_ms" if causal else "full_fwd_ms"
+                row[key] = round(min(row.get(key, 1e9), ms), 4)
+                row[key.replace("ms", "tflops")] = round(4 * a.B * a.Hq * a.S * a.S * D * f / (row[key] * 1e-3) / 1e12, 1)
+    e.attn_fwd_config(0)
+    res["fwd_variants"] = fv
 if a.isolated:
     # one kernel at a time after an idle gap (clock recovered), timed by events around the single launch: against the
     # back-to-back loop above this separates sustained-power clock effects from the kernels' own cost

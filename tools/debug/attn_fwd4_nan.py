@@ -1,0 +1,37 @@
+"""Where the one-wave-per-SIMD attention forward (attn_fwd_config(1)) differs from the 8-wave kernel: NaN positions and
+the largest |difference| per (head, query block, d), causal and full, at a few shapes."""
+import math
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+from accelerate_hpc_test_amd.ops import _ext  # noqa: E402
+
+e = _ext.ext()
+for (B, S, Sk, Hq, Hkv) in [(1, 256, 256, 4, 2), (1, 512, 512, 4, 2), (1, 256, 640, 8, 2)]:
+    for causal in (True, False):
+        torch.manual_seed(0)
+        q = torch.randn(B, S, Hq, 128, device="cuda", dtype=torch.bfloat16)
+        k = torch.randn(B, Sk, Hkv, 128, device="cuda", dtype=torch.bfloat16)
+        v = torch.randn(B, Sk, Hkv, 128, device="cuda", dtype=torch.bfloat16)
+        sc = 1 / math.sqrt(128)
+        e.attn_fwd_config(1)
+        o4, l4 = e.flash_attn_fwd(q, k, v, sc, causal)
+        e.attn_fwd_config(0)
+        o8, l8 = e.flash_attn_fwd(q, k, v, sc, causal)
+        torch.cuda.synchronize()
+        nan = torch.isnan(o4.float())
+        idx = nan.nonzero()
+        print(f"S={S} Sk={Sk} Hq={Hq} causal={causal}: nan {int(nan.sum())} lse_nan {int(torch.isnan(l4).sum())}", flush=True)
+        if idx.numel():
+            qs = sorted(set(idx[:, 1].tolist()))
+            print("  nan q:", qs[:20], "...", qs[-5:], "h:", sorted(set(idx[:, 2].tolist())), "d:", sorted(set(idx[:, 3].tolist()))[:40], flush=True)
+        d = (o4.float() - o8.float()).abs().nan_to_num(0)
+        print("  max|o4-o8| (finite)", float(d.max()), "lse diff", float((l4 - l8).abs().nan_to_num(0).max()), flush=True)
+        per_q = d.amax(dim=(0, 2, 3))
+        bad = (per_q > 0.05).nonzero().flatten().tolist()
+        print("  queries with |diff|>0.05:", bad[:20], len(bad), flush=True)
+        per_d = d.amax(dim=(0, 1, 2))
+        print("  d with |diff|>0.05:", (per_d > 0.05).nonzero().flatten().tolist()[:40], flush=True)

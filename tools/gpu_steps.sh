@@ -37,6 +37,8 @@ for step in "$@"; do
     bench20_abmn_b) ACCELERATE_ASM_WGRAD_ABMN=1 run bench20_abmn_b 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench20_dgamn) ACCELERATE_ASM_DGRAD_AMN=1 run bench20_dgamn 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench20_dgamn_b) ACCELERATE_ASM_DGRAD_AMN=1 run bench20_dgamn_b 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    bench20_dgbl) ACCELERATE_ASM_DGRAD_AMN=0 run bench20_dgbl 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    bench20_dgbl_b) ACCELERATE_ASM_DGRAD_AMN=0 run bench20_dgbl_b 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench20_noamn) ACCELERATE_ASM_WGRAD_AMN=0 run bench20_noamn 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench20_b) run bench20_b 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench20_noamn_b) ACCELERATE_ASM_WGRAD_AMN=0 run bench20_noamn_b 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
@@ -77,6 +79,10 @@ for step in "$@"; do
     prof_ddp_forced) prof prof_ddp_forced 600 bench.py --parallel ddp --ddp-force --steps 3 --warmup 2 $BENCH_ARGS ;;
     prof_ddp) prof prof_ddp 600 bench.py --parallel ddp --steps 3 --warmup 2 $BENCH_ARGS ;;
     prof_mixtral8l_bf16) prof prof_mixtral8l_bf16 600 bench.py --model mixtral-8x7b-8l --steps 2 --warmup 1 ;;
+    mix8_bf16_grid0) ACCELERATE_FP8ASM_GRID=0 run mix8_bf16_grid0 600 python bench.py --model mixtral-8x7b-8l --steps 5 --warmup 2 --verbose $BENCH_ARGS ;;
+    mix8_fp8_grid0) ACCELERATE_FP8ASM_GRID=0 run mix8_fp8_grid0 600 python bench.py --model mixtral-8x7b-8l --steps 5 --warmup 2 --precision fp8 --verbose $BENCH_ARGS ;;
+    bench20_fp8_grid0) ACCELERATE_FP8ASM_GRID=0 run bench20_fp8_grid0 600 python bench.py --gpus 1 --steps 20 --warmup 5 --precision fp8 ;;
+    prof8b_sharded_grid0) ACCELERATE_FP8ASM_GRID=0 OVERLAP_PATTERN="nccl|rccl|copyBuffer" PROF_EXTRA=--memory-copy-trace prof prof8b_sharded_grid0 600 bench.py --steps 3 --warmup 2 --fsdp-force-sharded $BENCH_ARGS ;;
     mix8_bf16) run mix8_bf16 600 python bench.py --model mixtral-8x7b-8l --steps 5 --warmup 2 --verbose $BENCH_ARGS ;;
     mix8_fp8) run mix8_fp8 600 python bench.py --model mixtral-8x7b-8l --steps 5 --warmup 2 --precision fp8 --verbose $BENCH_ARGS ;;
     mix8_bf16_asmall) ACCELERATE_MOE_ASM_BF16=fwd,wgrad,dgrad run mix8_bf16_asmall 600 python bench.py --model mixtral-8x7b-8l --steps 5 --warmup 2 --verbose $BENCH_ARGS ;;
@@ -97,6 +103,9 @@ for step in "$@"; do
     prof_mixtral_bf16) prof prof_mixtral_bf16 600 bench.py --model mixtral-8x7b-4l --steps 2 --warmup 1 ;;
     moetests) run moetests 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "grouped or moe or transpose" ;;
     attn) run attn 300 python tools/bench_attn.py --no-sdpa ;;
+    attn_fwd4) run ktest_fwd4 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "fwd_w4" && \
+               ACCELERATE_ATTN_FWD_W4=1 run ktest_attn_fwd4 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "flash or attention or context_parallel" && \
+               run attn_fwd4 300 python tools/bench_attn.py --no-sdpa --fwd-variants 0,1 --rounds 3 ;;
     attn_w4) run ktest_attn 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "flash or attention or context_parallel" && \
              run attn_w4 300 python tools/bench_attn.py --no-sdpa && ACCELERATE_ATTN_DKDV=8 run attn_w8 300 python tools/bench_attn.py --no-sdpa && \
              ACCELERATE_ATTN_DKDV_SCHED=1 run attn_w4s1 300 python tools/bench_attn.py --no-sdpa ;;
@@ -114,6 +123,11 @@ for step in "$@"; do
     ktest_dq128) ACCELERATE_ATTN_DQ_KEYS=128 run ktest_dq128 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "flash or attention or context_parallel" ;;
     attn_dq128) ACCELERATE_ATTN_DQ_KEYS=128 run attn_dq128 300 python tools/bench_attn.py --no-sdpa ;;
     bench20_dq128) ACCELERATE_ATTN_DQ_KEYS=128 run bench20_dq128 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    bench20_fwd4) ACCELERATE_ATTN_FWD_W4=1 run bench20_fwd4 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    bench20_fwd4_b) ACCELERATE_ATTN_FWD_W4=1 run bench20_fwd4_b 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    bench20_grid0) ACCELERATE_FP8ASM_GRID=0 run bench20_grid0 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    bench20_sharded_grid0) ACCELERATE_FP8ASM_GRID=0 run bench20_sharded_grid0 600 python bench.py --gpus 1 --steps 20 --warmup 5 --fsdp-force-sharded ;;
+    bench20_sharded_dgbl) ACCELERATE_ASM_DGRAD_AMN=0 run bench20_sharded_dgbl 600 python bench.py --gpus 1 --steps 20 --warmup 5 --fsdp-force-sharded ;;
     bench20_sharded) run bench20_sharded 600 python bench.py --gpus 1 --steps 20 --warmup 5 --fsdp-force-sharded ;;
     bench20_sharded_nors) run bench20_sharded_nors 600 python bench.py --gpus 1 --steps 20 --warmup 5 --fsdp-force-sharded --reshard-after-forward off ;;
     bench20_ovl) run bench20_ovl 600 python bench.py --gpus 1 --steps 20 --warmup 5 --optimizer-overlap on ;;
