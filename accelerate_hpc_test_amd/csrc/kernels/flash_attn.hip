@@ -551,7 +551,9 @@ __device__ __forceinline__ float max3_raw(float a, float b, float c) {  // fmaxf
   return x;
 }
 
-template <bool CAUSAL>
+// DMA: when the tile's 8 LDS-DMA pieces issue (latency budget to the next tile's barrier): 0 = one per step in steps
+// 0-7, 1 = two per step in steps 0-3, 2 = all eight at step 0
+template <bool CAUSAL, int DMA = 0>
 __global__ __launch_bounds__(256, 1) void attn_fwd_w4_kernel(FwdParams p) {
   constexpr int kKeys = 64, kImg = kKeys * kRow;  // 16 KB per operand image
   __shared__ __attribute__((aligned(1024))) char k0s[kImg], k1s[kImg], v0s[kImg], v1s[kImg];
@@ -586,14 +588,16 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_w4_kernel(FwdParams p) {
   for (int c = 0; c < 2; ++c)
 #pragma unroll
     for (int d = 0; d < 4; ++d) zero(o[c][d]);
-  // S of the tile being computed / of the tile being finished (parity buffers); "tile -1" is all -inf: its exps are 0
+  // S of the tile being computed / of the tile being finished (parity buffers). "Tile -1" must pack to P = 0: half 0's
+  // exps belong to a step that never ran (0 as it is), half 1's run in tile 0's steps 0-5 (-inf -> exp2 = 0)
   f32x16 sc[2][2][2];
 #pragma unroll
-  for (int c = 0; c < 2; ++c)
+  for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) sc[1][c][kb][i] = -INFINITY;
+    for (int i = 0; i < 16; ++i) {
+      sc[1][0][kb][i] = 0.f;
+      sc[1][1][kb][i] = -INFINITY;
+    }
   v8bf pb[2][2][2];  // [half][kb][s2]: P(T-1), the B operands of this tile's P.V
 #pragma unroll
   for (int c = 0; c < 2; ++c)
@@ -701,8 +705,15 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_w4_kernel(FwdParams p) {
       // next step's fragments (K(T) for steps 1-7, V(T-1)^T for steps 8-15; step 0's come after the next barrier)
       if (t < 7) { if (MODE != 2) k_read(kc, t + 1, ka[(t + 1) & 1]); }
       else if (t < 15) v_read(vp, t + 1 - 8, va[(t + 1) & 1]);
-      if (MODE != 2 && t < 4 && T + 1 < n_kt) dk.issue_piece(krs, (T + 1) * kKeys, kts, kn, t);
-      if (MODE != 2 && t >= 4 && t < 8) dv_.issue_piece(vrs, T * kKeys, vts, vc, t - 4);
+      if (MODE != 2) {
+        static_for<8>([&](auto pc) __attribute__((always_inline)) {
+          constexpr int q = decltype(pc)::value;  // piece q: K(T + 1) pieces 0-3, V(T) pieces 4-7
+          constexpr int at = DMA == 0 ? q : (DMA == 1 ? q / 2 : 0);
+          if (t != at) return;
+          if (q < 4) { if (T + 1 < n_kt) dk.issue_piece(krs, (T + 1) * kKeys, kts, kn, q); }
+          else dv_.issue_piece(vrs, T * kKeys, vts, vc, q - 4);
+        });
+      }
       if (t < 8) {
         if (t == 0) {  // the deferred O rescale decided in softmax(T-1), after the P.V that used the old max
 #pragma unroll
@@ -1672,8 +1683,12 @@ void check_qkv(const torch::Tensor& t, const char* name) {
 
 // Explicit instantiations: hipcc emits the host launch stub of only the first instantiation a launch chain names for
 // kernels with function-scope static LDS; naming every variant here makes each stub definite.
-template __global__ void attn_fwd_w4_kernel<true>(FwdParams);
-template __global__ void attn_fwd_w4_kernel<false>(FwdParams);
+template __global__ void attn_fwd_w4_kernel<true, 0>(FwdParams);
+template __global__ void attn_fwd_w4_kernel<false, 0>(FwdParams);
+template __global__ void attn_fwd_w4_kernel<true, 1>(FwdParams);
+template __global__ void attn_fwd_w4_kernel<false, 1>(FwdParams);
+template __global__ void attn_fwd_w4_kernel<true, 2>(FwdParams);
+template __global__ void attn_fwd_w4_kernel<false, 2>(FwdParams);
 template __global__ void attn_fwd_kernel<true, 1>(FwdParams);
 template __global__ void attn_fwd_kernel<false, 1>(FwdParams);
 template __global__ void attn_fwd_kernel<true, 2>(FwdParams);
@@ -1720,7 +1735,8 @@ static int env_int(const char* name, int dflt) { const char* e = std::getenv(nam
 static int g_dkdv_waves = env_int("ACCELERATE_ATTN_DKDV", 4);
 static int g_dkdv_sched = env_int("ACCELERATE_ATTN_DKDV_SCHED", 6);
 static int g_dq_waves = env_int("ACCELERATE_ATTN_DQ_W4", 0) ? 4 : 8;  // dQ: 4 = attn_bwd_dq_w4_kernel, 8 = 8-wave
-// forward kernel choice: 1 = attn_fwd_w4_kernel where S % 256 == 0, 0 = the 8-wave kernel (ACCELERATE_ATTN_FWD_W4)
+// forward kernel choice: 1 / 2 / 3 = attn_fwd_w4_kernel (DMA pieces spread over steps 0-7 / 0-3 / at step 0) where
+// S % 256 == 0, 0 = the 8-wave kernel (ACCELERATE_ATTN_FWD_W4)
 static int g_fwd_w4 = env_int("ACCELERATE_ATTN_FWD_W4", 0);
 void attn_fwd_config(int64_t w4) { g_fwd_w4 = (int)w4; }
 void attn_dkdv_config(int64_t waves, int64_t sched, int64_t dq_waves) {
@@ -1781,8 +1797,13 @@ std::vector<torch::Tensor> flash_attn_fwd(torch::Tensor q, torch::Tensor k, torc
   if (g_fwd_w4 && S % 256 == 0) {
     dim3 g4(Hq, S / 256, B);
     p.trace = trace_for(g4);
-    if (causal) hipLaunchKernelGGL((attn_fwd_w4_kernel<true>), g4, dim3(256), 0, stream, p);
-    else hipLaunchKernelGGL((attn_fwd_w4_kernel<false>), g4, dim3(256), 0, stream, p);
+#define FWD4_GO(DM)                                                                         \
+  if (causal) hipLaunchKernelGGL((attn_fwd_w4_kernel<true, DM>), g4, dim3(256), 0, stream, p); \
+  else hipLaunchKernelGGL((attn_fwd_w4_kernel<false, DM>), g4, dim3(256), 0, stream, p)
+    if (g_fwd_w4 == 3) { FWD4_GO(2); }
+    else if (g_fwd_w4 == 2) { FWD4_GO(1); }
+    else { FWD4_GO(0); }
+#undef FWD4_GO
     return {o, lse};
   }
   dim3 grid(Hq / nh, S / 128, B);

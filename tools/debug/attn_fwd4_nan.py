@@ -17,10 +17,17 @@ for (B, S, Sk, Hq, Hkv) in [(1, 256, 256, 4, 2), (1, 512, 512, 4, 2), (1, 256, 6
         k = torch.randn(B, Sk, Hkv, 128, device="cuda", dtype=torch.bfloat16)
         v = torch.randn(B, Sk, Hkv, 128, device="cuda", dtype=torch.bfloat16)
         sc = 1 / math.sqrt(128)
+        e.attn_fwd_config(0)
+        o8, l8 = e.flash_attn_fwd(q, k, v, sc, causal)
+        for var in (2, 3):  # the DMA-timing variants must give the same bits as variant 1
+            e.attn_fwd_config(var)
+            ov, lv = e.flash_attn_fwd(q, k, v, sc, causal)
+            e.attn_fwd_config(1)
+            o4, l4 = e.flash_attn_fwd(q, k, v, sc, causal)
+            assert torch.equal(ov, o4) and torch.equal(lv, l4), f"variant {var} differs"
         e.attn_fwd_config(1)
         o4, l4 = e.flash_attn_fwd(q, k, v, sc, causal)
         e.attn_fwd_config(0)
-        o8, l8 = e.flash_attn_fwd(q, k, v, sc, causal)
         torch.cuda.synchronize()
         nan = torch.isnan(o4.float())
         idx = nan.nonzero()
