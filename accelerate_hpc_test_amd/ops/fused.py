@@ -42,10 +42,24 @@ _ASM_WGRAD_AMN = os.environ.get("ACCELERATE_ASM_WGRAD_AMN", "1") != "0"
 # a token-contiguous copy (no transpose in the forward, 2 GiB less for Llama-3-8B at 8k tokens): 387.4 / 387.8 vs
 # 390.9 / 391.1 ms per step on one box (profiles/r6_gemm_amn.md). ACCELERATE_ASM_WGRAD_ABMN=0: the x^T copy + MN-A mode.
 ASM_WGRAD_ABMN = os.environ.get("ACCELERATE_ASM_WGRAD_ABMN", "1") != "0"
-# dgrad dx = dy . W on the asm kernel's MN-major-A mode with a transposed store (dx^T = W^T . dy^T, W read as stored):
-# no transposed weight copy. 389.5 / 389.4 vs 390.3 / 390.7 ms per step against transpose + hipBLASLt TN on one box
-# (profiles/r6_gemm_amn.md); ACCELERATE_ASM_DGRAD_AMN=0 restores the transposed-weight path.
-_ASM_DGRAD_AMN = os.environ.get("ACCELERATE_ASM_DGRAD_AMN", "1") != "0"
+# dgrad dx = dy . W: on the asm kernel's MN-major-A mode with a transposed store (dx^T = W^T . dy^T, W read as stored,
+# no transposed weight copy) or as transpose(W) + hipBLASLt TN. Interleaved bench20 pairs (profiles/r6_gemm_amn.md):
+# with the GPU to itself the transpose + TN path is 0.6-2.5 ms per step faster; beside a sharded engine's collectives
+# and gradient-shard updates the asm path is 2.6 ms faster (the transpose is one more memory-bound kernel competing with
+# them). ACCELERATE_ASM_DGRAD_AMN=auto (default): the asm path once an engine whose collectives run concurrently with
+# the backward exists (set_dgrad_concurrent: FSDP sharded / HSDP, DDP at W > 1); 1 / 0 force one path.
+_ASM_DGRAD_MODE = os.environ.get("ACCELERATE_ASM_DGRAD_AMN", "auto")
+_DGRAD_CONCURRENT = False
+
+
+def set_dgrad_concurrent(on: bool = True) -> None:
+    """Tell the dgrad path that collectives (all-gather / reduce-scatter / all-reduce) run beside the backward."""
+    global _DGRAD_CONCURRENT
+    _DGRAD_CONCURRENT = bool(on)
+
+
+def asm_dgrad_enabled() -> bool:
+    return _ASM_DGRAD_MODE == "1" or (_ASM_DGRAD_MODE == "auto" and _DGRAD_CONCURRENT)
 
 
 def asm_gemm_bf16(a: torch.Tensor, b: torch.Tensor, bias=None, out=None, accumulate: bool = False, kind: str = "fwd"):
@@ -418,7 +432,7 @@ def linear_dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     tools/bench_transpose.py; 436 MB of weights per Llama-3-8B layer ≈ 0.15 ms) and dx = linear(dy2, Wᵀ) runs in the
     forward's layout: 1.1-1.5 % faster end to end on one MI355X (gpu_steps.sh bench8b vs bench8b_dgradwt, two
     boxes). The copy is transient (freed as soon as the GEMM is enqueued)."""
-    if (_ASM_DGRAD_AMN and dy2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and w.is_contiguous()
+    if (asm_dgrad_enabled() and dy2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and w.is_contiguous()
             and dy2.is_contiguous() and use_native(dy2) and w.shape[1] % 256 == 0 and dy2.shape[0] % 256 == 0
             and w.shape[0] % 64 == 0 and w.shape[0] >= 128):
         out = torch.empty((dy2.shape[0], w.shape[1]), dtype=dy2.dtype, device=dy2.device)

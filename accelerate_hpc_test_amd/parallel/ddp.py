@@ -158,6 +158,7 @@ class DistributedDataParallel(nn.Module):
         self.process_group = process_group
         self.world_size = dist.get_world_size(process_group)
         self.rank = dist.get_rank(process_group)
+        fused_ops.set_dgrad_concurrent(True)  # bucket all-reduces beside the backward (the reducer exists only then)
         self.broadcast_buffers = broadcast_buffers
         self.require_backward_grad_sync = True
         # torch DDP semantics: whether a backward all-reduces is decided by the FORWARD that built its graph (under

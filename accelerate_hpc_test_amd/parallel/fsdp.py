@@ -201,6 +201,8 @@ class FSDPEngine:
         # exactly the multi-GPU code (separate full buffer resized 0 <-> full, RCCL all-gather / reduce-scatter with
         # nranks=1, bf16 flat grads reduced into the fp32 shard, reshard-after-forward and prefetch).
         self.sharded = self.world_size > 1 or (bool(force_sharded) and dist.is_available() and dist.is_initialized())
+        if self.sharded or self.replicate_size > 1:
+            fused_ops.set_dgrad_concurrent(True)  # collectives beside the backward: dgrad without the transpose kernel
         mp = plugin.mixed_precision_policy or MixedPrecisionPolicy()
         self.param_dtype = mp.param_dtype or torch.float32
         self.reduce_dtype = mp.reduce_dtype or self.param_dtype
