@@ -8,6 +8,8 @@
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include "common.h"
+#include <cstdlib>
+#include <type_traits>
 
 using namespace acc;
 
@@ -131,6 +133,44 @@ template <> struct Vec4<bf16_t> {
   static constexpr int kAlign = 8;
 };
 
+// Global-address-space (MODE 1) and global non-temporal (MODE 2) forms of Vec4 for the optimizer, which streams every
+// state tensor exactly once per step (ACCELERATE_ADAM_NT=1 / 2 (default); 0 = Vec4's generic-pointer flat accesses).
+typedef float nt_f4 __attribute__((ext_vector_type(4)));
+typedef unsigned int nt_u2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) nt_f4 g_f4;
+typedef __attribute__((address_space(1))) nt_u2 g_u2;
+template <int MODE, typename T>
+__device__ __forceinline__ void ld4(const T* p, float (&o)[4]) {
+  if constexpr (MODE == 0) {
+    Vec4<T>::load(p, o);
+  } else if constexpr (std::is_same<T, float>::value) {
+    const g_f4* q = (const g_f4*)p;
+    const nt_f4 v = MODE == 2 ? __builtin_nontemporal_load(q) : *q;
+    o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+  } else {
+    const g_u2* q = (const g_u2*)p;
+    const nt_u2 v = MODE == 2 ? __builtin_nontemporal_load(q) : *q;
+    o[0] = bf2f((bf16_t)(v.x & 0xffffu)); o[1] = bf2f((bf16_t)(v.x >> 16));
+    o[2] = bf2f((bf16_t)(v.y & 0xffffu)); o[3] = bf2f((bf16_t)(v.y >> 16));
+  }
+}
+template <int MODE, typename T>
+__device__ __forceinline__ void st4(T* p, const float (&o)[4]) {
+  if constexpr (MODE == 0) {
+    Vec4<T>::store(p, o);
+  } else if constexpr (std::is_same<T, float>::value) {
+    const nt_f4 v = {o[0], o[1], o[2], o[3]};
+    if constexpr (MODE == 2) __builtin_nontemporal_store(v, (g_f4*)p);
+    else *(g_f4*)p = v;
+  } else {
+    nt_u2 v;
+    v.x = (unsigned)f2bf(o[0]) | ((unsigned)f2bf(o[1]) << 16);
+    v.y = (unsigned)f2bf(o[2]) | ((unsigned)f2bf(o[3]) << 16);
+    if constexpr (MODE == 2) __builtin_nontemporal_store(v, (g_u2*)p);
+    else *(g_u2*)p = v;
+  }
+}
+
 struct AdamHyper {
   float lr, beta1, beta2, eps, wd, bc1, bc2_sqrt;
   int adamw;
@@ -146,7 +186,7 @@ __device__ __forceinline__ void adam_elem(float& pf, float gf, float& mf, float&
 
 // Each lane owns 4 consecutive elements per iteration; 16-B (fp32) / 8-B (bf16) vector accesses when every
 // operand of the tensor is aligned (chunk starts are multiples of kChunk elements, so the base decides).
-template <typename P, typename G, typename S>
+template <typename P, typename G, typename S, int NT = 0>
 __global__ __launch_bounds__(kMTThreads) void adam_mt_kernel(const TensorMeta* __restrict__ meta,
                                                              const int64_t* __restrict__ block_prefix, int ntensors,
                                                              AdamHyper h, const float* __restrict__ grad_scale) {
@@ -170,16 +210,16 @@ __global__ __launch_bounds__(kMTThreads) void adam_mt_kernel(const TensorMeta* _
     const int64_t vend = start + ((end - start) & ~int64_t(3));
     for (int64_t i = start + (int64_t)threadIdx.x * 4; i < vend; i += (int64_t)kMTThreads * 4) {
       float pf[4], gf[4], mf[4], vf[4];
-      Vec4<P>::load(p + i, pf);
-      Vec4<G>::load(g + i, gf);
-      Vec4<S>::load(m + i, mf);
-      Vec4<S>::load(v + i, vf);
+      ld4<NT>(p + i, pf);
+      ld4<NT>(g + i, gf);
+      ld4<NT>(m + i, mf);
+      ld4<NT>(v + i, vf);
 #pragma unroll
       for (int j = 0; j < 4; ++j) adam_elem(pf[j], gf[j] * gs, mf[j], vf[j], h);
-      Vec4<P>::store(p + i, pf);
-      Vec4<S>::store(m + i, mf);
-      Vec4<S>::store(v + i, vf);
-      if (sh != nullptr) Vec4<bf16_t>::store(sh + i, pf);
+      st4<NT>(p + i, pf);
+      st4<NT>(m + i, mf);
+      st4<NT>(v + i, vf);
+      if (sh != nullptr) st4<NT == 2 ? 1 : NT>(sh + i, pf);  // the shadow is read again soon (all-gather / forward)
       if (amax != nullptr) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) am = fmaxf(am, fabsf(bf2f(f2bf(pf[j]))));
@@ -347,14 +387,19 @@ void adam_multi_tensor(torch::Tensor meta, torch::Tensor block_prefix, int64_t n
   const int64_t* bp = block_prefix.data_ptr<int64_t>();
   const float* gsp = grad_scale.has_value() ? grad_scale->data_ptr<float>() : nullptr;
   AdamHyper hyper{(float)lr, (float)beta1, (float)beta2, (float)eps, (float)wd, (float)bc1, (float)bc2_sqrt, (int)adamw};
-#define ADAM_LAUNCH(P, G, S)                                                                                   \
-  hipLaunchKernelGGL((adam_mt_kernel<P, G, S>), dim3(nblocks), dim3(kMTThreads), 0, stream, mp, bp, nt, hyper, gsp)
-  if (pdtype == 0 && gdtype == 0 && sdtype == 0) ADAM_LAUNCH(float, float, float);
-  else if (pdtype == 0 && gdtype == 1 && sdtype == 0) ADAM_LAUNCH(float, bf16_t, float);
-  else if (pdtype == 1 && gdtype == 1 && sdtype == 1) ADAM_LAUNCH(bf16_t, bf16_t, bf16_t);
-  else if (pdtype == 1 && gdtype == 1 && sdtype == 0) ADAM_LAUNCH(bf16_t, bf16_t, float);
-  else if (pdtype == 0 && gdtype == 0 && sdtype == 1) ADAM_LAUNCH(float, float, bf16_t);  // fp32 master, bf16 m / v
-  else if (pdtype == 0 && gdtype == 1 && sdtype == 1) ADAM_LAUNCH(float, bf16_t, bf16_t);
+  // default 2 (global non-temporal): tools/bench_adam.py at Llama-3-8B scale, 26.6 ms vs 26.9-27.7 (flat) and 27.4-27.6
+  // (global, temporal) per step, two interleaved rounds on one box
+  static const int adam_nt = [] { const char* e = std::getenv("ACCELERATE_ADAM_NT"); return e != nullptr ? std::atoi(e) : 2; }();
+#define ADAM_LAUNCH(P, G, S)                                                                                            \
+  if (adam_nt == 2) hipLaunchKernelGGL((adam_mt_kernel<P, G, S, 2>), dim3(nblocks), dim3(kMTThreads), 0, stream, mp, bp, nt, hyper, gsp); \
+  else if (adam_nt == 1) hipLaunchKernelGGL((adam_mt_kernel<P, G, S, 1>), dim3(nblocks), dim3(kMTThreads), 0, stream, mp, bp, nt, hyper, gsp); \
+  else hipLaunchKernelGGL((adam_mt_kernel<P, G, S>), dim3(nblocks), dim3(kMTThreads), 0, stream, mp, bp, nt, hyper, gsp)
+  if (pdtype == 0 && gdtype == 0 && sdtype == 0) { ADAM_LAUNCH(float, float, float); }
+  else if (pdtype == 0 && gdtype == 1 && sdtype == 0) { ADAM_LAUNCH(float, bf16_t, float); }
+  else if (pdtype == 1 && gdtype == 1 && sdtype == 1) { ADAM_LAUNCH(bf16_t, bf16_t, bf16_t); }
+  else if (pdtype == 1 && gdtype == 1 && sdtype == 0) { ADAM_LAUNCH(bf16_t, bf16_t, float); }
+  else if (pdtype == 0 && gdtype == 0 && sdtype == 1) { ADAM_LAUNCH(float, float, bf16_t); }  // fp32 master, bf16 m / v
+  else if (pdtype == 0 && gdtype == 1 && sdtype == 1) { ADAM_LAUNCH(float, bf16_t, bf16_t); }
   else TORCH_CHECK(false, "adam_multi_tensor: unsupported dtype combination");
 #undef ADAM_LAUNCH
 }

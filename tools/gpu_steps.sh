@@ -125,6 +125,10 @@ for step in "$@"; do
     bench20_dq128) ACCELERATE_ATTN_DQ_KEYS=128 run bench20_dq128 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench20_fwd4) ACCELERATE_ATTN_FWD_W4=1 run bench20_fwd4 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench20_fwd4_b) ACCELERATE_ATTN_FWD_W4=1 run bench20_fwd4_b 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    bench20_adamg) ACCELERATE_ADAM_NT=1 run bench20_adamg 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    bench20_adamnt) ACCELERATE_ADAM_NT=2 run bench20_adamnt 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    adam_tests) ACCELERATE_ADAM_NT=2 run adam_tests_nt 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "adam" && \
+                ACCELERATE_ADAM_NT=1 run adam_tests_g 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "adam" ;;
     bench20_grid0) ACCELERATE_FP8ASM_GRID=0 run bench20_grid0 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench20_sharded_grid0) ACCELERATE_FP8ASM_GRID=0 run bench20_sharded_grid0 600 python bench.py --gpus 1 --steps 20 --warmup 5 --fsdp-force-sharded ;;
     bench20_sharded_dgbl) ACCELERATE_ASM_DGRAD_AMN=0 run bench20_sharded_dgbl 600 python bench.py --gpus 1 --steps 20 --warmup 5 --fsdp-force-sharded ;;
