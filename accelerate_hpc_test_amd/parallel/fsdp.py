@@ -239,7 +239,9 @@ class FSDPEngine:
         self._d2h_pending = []
         if self.is_cuda:
             self.ag_stream = torch.cuda.Stream(device=device, priority=-1)
-            self.rs_stream = torch.cuda.Stream(device=device, priority=-1)
+            # ACCELERATE_FSDP_RS_PRIORITY: 0 = the reduce-scatter / gradient-shard update stream at normal priority (its
+            # work is needed only at the end of backward), -1 = high like the all-gather stream
+            self.rs_stream = torch.cuda.Stream(device=device, priority=int(os.environ.get("ACCELERATE_FSDP_RS_PRIORITY", "-1")))
         else:
             self.ag_stream = self.rs_stream = None
         # All-gather and reduce-scatter get communicators of their own (same ranks as `group`): ProcessGroupNCCL runs
