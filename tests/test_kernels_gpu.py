@@ -380,6 +380,40 @@ def test_bf16_asm_gemm_matches_fp32_reference(M, N, K):
         or (K - 32) % 64 == 0  # K not a multiple of 64: declined, nothing launched
 
 
+@pytest.mark.parametrize("M,N,K", [(4096, 6144, 1024), (14336, 4096, 512), (1024, 512, 4096)])
+def test_bf16_asm_amn_split_tail_matches_fp32_reference(M, N, K):
+    """Both operands MN-major (the weight-gradient form): the last partial wave of tiles runs as K-halves whose fp32
+    partials amn_tail_reduce_kernel adds into C. Shapes with whole waves before the tail (384 and 896 tiles: the
+    Llama-3-8B q/k/v and down projections) and an all-tail grid; exact small integers, the fp32 oracle, fp32 and bf16
+    outputs, written and accumulated."""
+    from accelerate_hpc_test_amd.ops._ext import ext
+
+    torch.manual_seed(0)
+    xi = torch.randint(-3, 4, (K, M), device=DEV).to(torch.bfloat16)
+    dyi = torch.randint(-3, 4, (K, N), device=DEV).to(torch.bfloat16)
+    refi = (xi.float().t() @ dyi.float()).t().contiguous()  # [N, M]
+    out = torch.empty(N, M, device=DEV)
+    assert ext().bf16_gemm_asm_amn(xi, dyi, out, False, True, True)
+    assert torch.equal(out, refi), (out - refi).abs().max()
+    acc = refi.clone()
+    assert ext().bf16_gemm_asm_amn(xi, dyi, acc, True, True, True)
+    assert torch.equal(acc, 2 * refi), (acc - 2 * refi).abs().max()
+    x = torch.randn(K, M, device=DEV, dtype=torch.bfloat16)
+    dy = torch.randn(K, N, device=DEV, dtype=torch.bfloat16)
+    ref = (x.float().t() @ dy.float()).t().contiguous()
+    tol = 1e-3 * ref.abs().max().item()
+    o32 = torch.empty(N, M, device=DEV)
+    assert ext().bf16_gemm_asm_amn(x, dy, o32, False, True, True)
+    assert torch.allclose(o32, ref, rtol=1e-4, atol=tol), (o32 - ref).abs().max()
+    o16 = torch.empty(N, M, device=DEV, dtype=torch.bfloat16)
+    assert ext().bf16_gemm_asm_amn(x, dy, o16, False, True, True)
+    assert _rel(o16.float(), ref) < 1e-2
+    base16 = torch.randn(N, M, device=DEV, dtype=torch.bfloat16)
+    acc16 = base16.clone()
+    assert ext().bf16_gemm_asm_amn(x, dy, acc16, True, True, True)
+    assert _rel(acc16.float(), base16.float() + ref) < 1e-2
+
+
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 320), (1024, 512, 4096), (768, 1280, 8192)])
 def test_bf16_asm_amn_gemm_matches_fp32_reference(M, N, K):
     """The MN-major-A asm GEMM (ext().bf16_gemm_asm_amn, transposed LDS reads): a_t [K, M] M-contiguous, b [N, K];

@@ -130,6 +130,9 @@ for step in "$@"; do
     adam_tests) ACCELERATE_ADAM_NT=2 run adam_tests_nt 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "adam" && \
                 ACCELERATE_ADAM_NT=1 run adam_tests_g 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "adam" ;;
     bench20_sharded_rsp0) ACCELERATE_FSDP_RS_PRIORITY=0 run bench20_sharded_rsp0 600 python bench.py --gpus 1 --steps 20 --warmup 5 --fsdp-force-sharded ;;
+    split_tests) run split_tests 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "amn" ;;
+    bench20_nosplit) ACCELERATE_ASM_SPLIT_TAIL=0 run bench20_nosplit 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    bench20_nosplit_b) ACCELERATE_ASM_SPLIT_TAIL=0 run bench20_nosplit_b 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench20_grid0) ACCELERATE_FP8ASM_GRID=0 run bench20_grid0 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench20_sharded_grid0) ACCELERATE_FP8ASM_GRID=0 run bench20_sharded_grid0 600 python bench.py --gpus 1 --steps 20 --warmup 5 --fsdp-force-sharded ;;
     bench20_sharded_dgbl) ACCELERATE_ASM_DGRAD_AMN=0 run bench20_sharded_dgbl 600 python bench.py --gpus 1 --steps 20 --warmup 5 --fsdp-force-sharded ;;
