@@ -480,12 +480,13 @@ def test_gemm8_two_waves_per_simd_exact(M, N, K):
     assert torch.equal(out, ref), (out.float() - ref.float()).abs().max()
 
 
-@pytest.mark.parametrize("M,N,K", [(256, 256, 256), (512, 768, 640), (1024, 512, 4096), (768, 1280, 8192)])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 256), (512, 768, 640), (1024, 512, 4096), (768, 1280, 8192), (4096, 6144, 1024)])
 def test_fp8_asm_amn_gemm_matches_reference(M, N, K):
     """The MN-major fp8 asm GEMM (ext().fp8_gemm_asm_amn, ds_read_b64_tr_b8 from the 1040-B-chunk image): a_t [K, M]
     M-contiguous with b [N, K] or (b_mn) b [K, N]; out [N, M] = (a_tᵀ·bᵀ)ᵀ · sa · sb · smul. Exact small integers for
     every e4m3 / e5m2 pairing and both B layouts, then scaled random operands with fp32 / bf16 outputs and accumulate
-    against the fp32 product of the dequantised operands."""
+    against the fp32 product of the dequantised operands. With b_mn the last partial wave of tiles runs as K-halves
+    (split tail): all tiles at 8 / 15 tiles, 128 of 384 at the q/k/v shape."""
     from accelerate_hpc_test_amd.ops._ext import ext
 
     torch.manual_seed(0)
