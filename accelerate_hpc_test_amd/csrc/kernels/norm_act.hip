@@ -442,7 +442,9 @@ std::vector<torch::Tensor> rmsnorm_bwd(torch::Tensor dy, torch::Tensor x, torch:
   const int H = x.size(-1);
   const long T = x.numel() / H;
   auto dx = torch::empty_like(x);
-  const int P = (int)std::min<long>(T > 0 ? T : 1, 512);
+  // workgroups (each walks T / P rows, one row prefetched): ACCELERATE_RMSNORM_BWD_BLOCKS, default 512
+  static const long bwd_blocks = [] { const char* e = std::getenv("ACCELERATE_RMSNORM_BWD_BLOCKS"); return e ? std::atol(e) : 512L; }();
+  const int P = (int)std::min<long>(T > 0 ? T : 1, bwd_blocks);
   auto part = torch::empty({P, H}, x.options().dtype(torch::kFloat32));
   torch::Tensor dw;
   if (dw_out.has_value()) {
