@@ -54,6 +54,11 @@ for step in "$@"; do
     bench8b_nodgradwt) ACCELERATE_DGRAD_WT=0 run bench8b_nodgradwt 600 python bench.py --steps 5 --warmup 2 $BENCH_ARGS ;;
     transpose) run transpose 300 python tools/bench_transpose.py && ACCELERATE_TRANSPOSE128=0 run transpose_old 300 python tools/bench_transpose.py ;;
     ktest) run ktest 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "${KTEST:-transpose}" ;;
+    tune_step1) run tune_step 900 python bench.py --gemm-tuning tune --gemm-table gpurun_out/tunableop_step.csv --steps 1 --warmup 2 && \
+               cp accelerate_hpc_test_amd/ops/tuned/tunableop_gfx950.csv gpurun_out/tunableop_merged.csv && \
+               python tools/tune_gemms.py --merge gpurun_out/tunableop_merged.csv gpurun_out/tunableop_step.csv && \
+               run bench_tuned 600 python bench.py --gpus 1 --steps 20 --warmup 5 --gemm-table gpurun_out/tunableop_merged.csv && \
+               run bench_untuned 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     tune_step) run tune_step 900 python bench.py --gemm-tuning tune --gemm-table gpurun_out/tunableop_step.csv --steps 1 --warmup 2 && \
                run tune_step_sharded 900 python bench.py --gemm-tuning tune --gemm-table gpurun_out/tunableop_step_sharded.csv --steps 1 --warmup 2 --fsdp-force-sharded && \
                cp accelerate_hpc_test_amd/ops/tuned/tunableop_gfx950.csv gpurun_out/tunableop_merged.csv && \
